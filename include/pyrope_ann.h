@@ -1,0 +1,136 @@
+/*
+ * pyrope_ann.h -- C ABI of libpyrope_hip.so, the MI355X (gfx950) engine for
+ * Pyrope's batched ANN distance-scan hot path.
+ *
+ * This is the drop-in boundary.  Each entry point replaces one member of the
+ * reference plugin contract `IVectorIndex` (reference:
+ * src/Pyrope.GarnetServer/Vector/IVectorIndex.cs:14-29) or its factory branch
+ * (Services/VectorIndexRegistry.cs:81-113), and is what a C# P/Invoke shim
+ * (`HipVectorIndex : IVectorIndex, ICentroidsProvider`)
+ * binds.  Plain C: no exceptions cross the ABI, caller-owned buffers, the
+ * library copies every input and keeps no caller pointer after return.
+ *
+ * Ids: the reference keys rows by `string id`; the shim maps each id to a
+ * unique int64 label and back.  Labels < 0 are rejected.
+ *
+ * Threading (reference: one ReaderWriterLockSlim per index, e.g.
+ * BruteForceVectorIndex.cs:23): any number of concurrent pyr_index_search*
+ * calls; add/upsert/remove/build take the index exclusively.
+ *
+ * Scores: "higher is better", with the reference's signs
+ * (L2 -> -sum((q-x)^2), IP -> q.x, Cosine -> q.x/(|q||x|), IVF-PQ -> -ADC for
+ * every metric).  Results per query are sorted by score descending, ties by
+ * storage order (DESIGN.md "Tie rule").  Empty result slots hold
+ * score = -INFINITY and label = -1.
+ */
+#ifndef PYROPE_ANN_H
+#define PYROPE_ANN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct pyr_index pyr_index; /* opaque */
+
+typedef enum {
+  PYR_OK = 0,
+  PYR_E_DIM = 1,       /* -> ArgumentException("Vector dimension mismatch.") => VEC_ERR_DIM (VectorCommandSet.cs:837-847) */
+  PYR_E_ARG = 2,       /* -> ArgumentException / ArgumentOutOfRangeException (e.g. topK <= 0, BruteForceVectorIndex.cs:278) */
+  PYR_E_STATE = 3,     /* -> InvalidOperationException (wrong index kind / not built) */
+  PYR_E_OOM = 4,       /* device or host allocation failed */
+  PYR_E_DEVICE = 5,    /* HIP runtime error, or no gfx950 device */
+  PYR_E_DUPLICATE = 6  /* -> InvalidOperationException("Vector with id ... already exists.") (BruteForceVectorIndex.cs:141-144) */
+} pyr_status;
+
+/* == VectorMetric ordinals (IVectorIndex.cs:5-10) */
+typedef enum { PYR_L2 = 0, PYR_IP = 1, PYR_COS = 2 } pyr_metric;
+
+/* FLAT   = BruteForceVectorIndex (the Delta head; BruteForceVectorIndex.cs)
+ * IVF_FLAT = IvfFlatVectorIndex (IvfFlatVectorIndex.cs)
+ * IVF_PQ = IvfPqVectorIndex + ProductQuantizer (IvfPqVectorIndex.cs, ProductQuantizer.cs) */
+typedef enum { PYR_FLAT = 0, PYR_IVF_FLAT = 1, PYR_IVF_PQ = 2 } pyr_kind;
+
+typedef struct {
+  int32_t kind;           /* pyr_kind */
+  int32_t dim;            /* > 0 (BruteForceVectorIndex.cs:43-46) */
+  int32_t metric;         /* pyr_metric */
+  int32_t nlist;          /* IVF: NList (registry default 100, VectorIndexRegistry.cs:100,106) */
+  int32_t pq_m;           /* IVF_PQ: M, dim % M == 0 (ProductQuantizer.cs:18) */
+  int32_t pq_k;           /* IVF_PQ: K <= 256 (ProductQuantizer.cs:19) */
+  int32_t device;         /* HIP device ordinal (one process per GPU) */
+  int32_t default_nprobe; /* <= 0 -> reference default: 3 IVF_FLAT (IvfFlatVectorIndex.cs:14), 1 IVF_PQ (IvfPqVectorIndex.cs:125) */
+} pyr_index_desc;
+
+/* SearchOptions (SearchOptions.cs:3) */
+typedef struct {
+  int32_t nprobe;    /* < 0 -> index default; 0 -> no list is probed (Math.Min(nProbe, n) <= 0) */
+  int32_t reserved;
+  int64_t max_scans; /* < 0 -> unlimited; 0 -> empty result (BruteForceVectorIndex.cs:288-289). IVF_PQ ignores it. */
+} pyr_search_params;
+
+/* new XxxVectorIndex(...) inside VectorIndexRegistry.IndexState (VectorIndexRegistry.cs:81-113). */
+pyr_status pyr_index_create(const pyr_index_desc *desc, pyr_index **out);
+void pyr_index_destroy(pyr_index *index);
+
+/* IVectorIndex.Add (IVectorIndex.cs:19).  x: n x dim row-major fp32.
+ * FLAT: a label that already exists -> PYR_E_DUPLICATE and nothing is added.
+ * IVF_*: Add == Upsert into the pre-build buffer (IvfFlatVectorIndex.cs:39-59, IvfPqVectorIndex.cs:37-47). */
+pyr_status pyr_index_add(pyr_index *index, const float *x, int64_t n, const int64_t *labels);
+/* IVectorIndex.Upsert (IVectorIndex.cs:20; BruteForceVectorIndex.cs:181-222). */
+pyr_status pyr_index_upsert(pyr_index *index, const float *x, int64_t n, const int64_t *labels);
+/* IVectorIndex.Delete (IVectorIndex.cs:21).  removed[i] = 1 if labels[i] was present (may be NULL). */
+pyr_status pyr_index_remove(pyr_index *index, const int64_t *labels, int64_t n, uint8_t *removed);
+/* IVectorIndex.Build (IVectorIndex.cs:25): reference-identical k-means training
+ * (KMeansUtils.Train semantics, run on the GPU), assignment and PQ encoding.  FLAT: no-op. */
+pyr_status pyr_index_build(pyr_index *index);
+
+/* IVectorIndex.Search (IVectorIndex.cs:22) for a batch of queries.  Host buffers.
+ * q: nq x dim; out_scores/out_labels: nq x k; out_counts: nq (may be NULL).
+ * params may be NULL (= SearchOptions null). */
+pyr_status pyr_index_search(pyr_index *index, const float *q, int64_t nq, int32_t k,
+                            const pyr_search_params *params, float *out_scores, int64_t *out_labels,
+                            int32_t *out_counts);
+/* Same on device-resident buffers (HBM), enqueued on `stream` (hipStream_t, NULL = default).
+ * Does not synchronize the stream. */
+pyr_status pyr_index_search_device(pyr_index *index, const float *d_q, int64_t nq, int32_t k,
+                                   const pyr_search_params *params, float *d_scores, int64_t *d_labels,
+                                   int32_t *d_counts, void *stream);
+
+/* IVectorIndex.GetStats (IVectorIndex.cs:28): Count with the reference's semantics
+ * (IvfFlat counts buffer + list rows, IvfFlatVectorIndex.cs:305; IvfPq reports 0, IvfPqVectorIndex.cs:230). */
+pyr_status pyr_index_stats(const pyr_index *index, int64_t *count, int32_t *dim, int32_t *metric);
+
+/* ICentroidsProvider.GetCentroids (ICentroidsProvider.cs:14; IvfFlatVectorIndex.cs:314-325).
+ * out may be NULL to query *nlist; *nlist = 0 when not built. */
+pyr_status pyr_index_get_centroids(const pyr_index *index, float *out, int32_t *nlist);
+
+/* Introspection of the built IVF layout (list-major storage order, used by the
+ * parity tests and the CPU baseline).  list_off: nlist+1 (row offsets without padding),
+ * labels: total rows (state of removed rows: label -1), live: 1 visible, 0 removed/shadowed.
+ * Any output may be NULL; *total receives the row count. */
+pyr_status pyr_index_ivf_layout(const pyr_index *index, int64_t *list_off, int64_t *labels, uint8_t *live,
+                                int64_t *total);
+/* IVF_PQ trained state: codebooks [M][ksub][dim/M]; codes list-major (total x M).  Any output may be NULL. */
+pyr_status pyr_index_pq_state(const pyr_index *index, float *codebooks, int32_t *ksub, uint8_t *codes);
+
+/* Multi-GPU merge (RCCL allgather of per-GPU partial top-k; DESIGN.md "Multi-GPU"):
+ * d_scores/d_labels: nq x nparts x k partial lists, each sorted (score desc, label asc);
+ * writes the global top-k per query, ties by label asc.  Device buffers, async on stream. */
+pyr_status pyr_merge_topk_device(const float *d_scores, const int64_t *d_labels, int64_t nq, int32_t nparts,
+                                 int32_t k, float *d_out_scores, int64_t *d_out_labels, void *stream);
+
+/* Pyrope.Benchmarks synthetic generator (Program.cs:251-263): v[d] = (float)new Random(seed).NextDouble(),
+ * row by row.  Host buffer count x dim.  Measurement-harness utility. */
+pyr_status pyr_generate_synthetic(int64_t count, int32_t dim, int32_t seed, float *out);
+
+/* thread-local message of the last failing call on this thread */
+const char *pyr_last_error(void);
+/* library / device information string, e.g. "pyrope_hip 0.1 gfx950" */
+const char *pyr_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PYROPE_ANN_H */

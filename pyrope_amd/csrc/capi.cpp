@@ -1,0 +1,230 @@
+// capi.cpp -- the extern "C" boundary of libpyrope_hip.so (include/pyrope_ann.h).
+// No C++ exception crosses it: every entry point catches, records a thread-local
+// message (pyr_last_error) and returns a pyr_status.
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "engine.h"
+
+struct pyr_index {
+  std::unique_ptr<pyr::Index> impl;
+};
+
+namespace {
+thread_local std::string g_err;
+
+pyr_status fail(pyr_status s, const std::string &m) {
+  g_err = m;
+  return s;
+}
+
+template <class F>
+pyr_status guard(F &&f) {
+  try {
+    f();
+    return PYR_OK;
+  } catch (const pyr::Error &e) {
+    return fail(e.status, e.what());
+  } catch (const std::bad_alloc &) {
+    return fail(PYR_E_OOM, "host allocation failed");
+  } catch (const std::exception &e) {
+    return fail(PYR_E_ARG, e.what());
+  }
+}
+
+void check_device(int dev) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) throw pyr::Error(PYR_E_DEVICE, "no HIP device available");
+  if (dev < 0 || dev >= n) throw pyr::Error(PYR_E_DEVICE, "device ordinal out of range");
+  hipDeviceProp_t p;
+  HIPCHK(hipGetDeviceProperties(&p, dev));
+  if (std::strncmp(p.gcnArchName, "gfx950", 6) != 0)
+    throw pyr::Error(PYR_E_DEVICE, std::string("libpyrope_hip is built for gfx950, device is ") + p.gcnArchName);
+}
+
+pyr_search_params defaults(const pyr_search_params *p) {
+  pyr_search_params d{-1, 0, -1};
+  return p ? *p : d;
+}
+}  // namespace
+
+extern "C" {
+
+pyr_status pyr_index_create(const pyr_index_desc *desc, pyr_index **out) {
+  if (!desc || !out) return fail(PYR_E_ARG, "null argument");
+  *out = nullptr;
+  return guard([&] {
+    check_device(desc->device);
+    auto *h = new pyr_index;
+    try {
+      h->impl.reset(pyr::create_index(*desc));
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+
+void pyr_index_destroy(pyr_index *index) {
+  if (!index) return;
+  try {
+    std::unique_lock<std::shared_mutex> g(index->impl->mu);
+    g.unlock();
+    delete index;
+  } catch (...) {
+  }
+}
+
+static pyr_status write_op(pyr_index *index, const float *x, int64_t n, const int64_t *labels, bool upsert) {
+  if (!index || (n > 0 && (!x || !labels)) || n < 0) return fail(PYR_E_ARG, "null argument");
+  for (int64_t i = 0; i < n; i++)
+    if (labels[i] < 0) return fail(PYR_E_ARG, "Id cannot be empty.");  // ValidateId
+  return guard([&] {
+    HIPCHK(hipSetDevice(index->impl->device));
+    std::unique_lock<std::shared_mutex> g(index->impl->mu);
+    if (n > 0) index->impl->add(x, n, labels, upsert);
+  });
+}
+
+pyr_status pyr_index_add(pyr_index *index, const float *x, int64_t n, const int64_t *labels) {
+  return write_op(index, x, n, labels, false);
+}
+
+pyr_status pyr_index_upsert(pyr_index *index, const float *x, int64_t n, const int64_t *labels) {
+  return write_op(index, x, n, labels, true);
+}
+
+pyr_status pyr_index_remove(pyr_index *index, const int64_t *labels, int64_t n, uint8_t *removed) {
+  if (!index || (n > 0 && !labels) || n < 0) return fail(PYR_E_ARG, "null argument");
+  return guard([&] {
+    HIPCHK(hipSetDevice(index->impl->device));
+    std::unique_lock<std::shared_mutex> g(index->impl->mu);
+    index->impl->remove(labels, n, removed);
+  });
+}
+
+pyr_status pyr_index_build(pyr_index *index) {
+  if (!index) return fail(PYR_E_ARG, "null argument");
+  return guard([&] {
+    HIPCHK(hipSetDevice(index->impl->device));
+    std::unique_lock<std::shared_mutex> g(index->impl->mu);
+    index->impl->build();
+  });
+}
+
+pyr_status pyr_index_search(pyr_index *index, const float *q, int64_t nq, int32_t k, const pyr_search_params *params,
+                            float *out_scores, int64_t *out_labels, int32_t *out_counts) {
+  if (!index || nq < 0 || (nq > 0 && !q)) return fail(PYR_E_ARG, "null argument");
+  if (k > pyr::KMAX) return fail(PYR_E_ARG, "topK larger than 256 is not supported");
+  return guard([&] {
+    pyr::Index &ix = *index->impl;
+    HIPCHK(hipSetDevice(ix.device));
+    std::shared_lock<std::shared_mutex> g(ix.mu);
+    auto ws = ix.take_ws();
+    try {
+      const int kk = k > 0 ? k : 0;
+      const size_t qb = sizeof(float) * (size_t)nq * ix.dim;
+      ws->q.ensure(qb);
+      ws->out_s.ensure(sizeof(float) * (size_t)nq * kk);
+      ws->out_l.ensure(sizeof(int64_t) * (size_t)nq * kk);
+      ws->out_c.ensure(sizeof(int32_t) * (size_t)nq);
+      if (nq > 0) HIPCHK(hipMemcpyAsync(ws->q.p, q, qb, hipMemcpyHostToDevice, ws->st));
+      ix.search(ws->q.as<float>(), nq, k, defaults(params), ws->out_s.as<float>(), ws->out_l.as<int64_t>(),
+                ws->out_c.as<int32_t>(), *ws);
+      HIPCHK(hipGetLastError());
+      if (nq > 0 && kk > 0) {
+        if (out_scores)
+          HIPCHK(hipMemcpyAsync(out_scores, ws->out_s.p, sizeof(float) * nq * kk, hipMemcpyDeviceToHost, ws->st));
+        if (out_labels)
+          HIPCHK(hipMemcpyAsync(out_labels, ws->out_l.p, sizeof(int64_t) * nq * kk, hipMemcpyDeviceToHost, ws->st));
+      }
+      if (out_counts && nq > 0)
+        HIPCHK(hipMemcpyAsync(out_counts, ws->out_c.p, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, ws->st));
+      HIPCHK(hipStreamSynchronize(ws->st));
+    } catch (...) {
+      (void)hipStreamSynchronize(ws->st);
+      ix.give_ws(std::move(ws));
+      throw;
+    }
+    ix.give_ws(std::move(ws));
+  });
+}
+
+pyr_status pyr_index_search_device(pyr_index *index, const float *d_q, int64_t nq, int32_t k,
+                                   const pyr_search_params *params, float *d_scores, int64_t *d_labels,
+                                   int32_t *d_counts, void *stream) {
+  if (!index || nq < 0 || (nq > 0 && !d_q)) return fail(PYR_E_ARG, "null argument");
+  if (k > pyr::KMAX) return fail(PYR_E_ARG, "topK larger than 256 is not supported");
+  return guard([&] {
+    pyr::Index &ix = *index->impl;
+    HIPCHK(hipSetDevice(ix.device));
+    std::shared_lock<std::shared_mutex> g(ix.mu);
+    pyr::Workspace &ws = ix.ws_for_stream(reinterpret_cast<hipStream_t>(stream));
+    std::lock_guard<std::mutex> wg(ws.m);
+    ix.search(d_q, nq, k, defaults(params), d_scores, d_labels, d_counts, ws);
+    HIPCHK(hipGetLastError());
+  });
+}
+
+pyr_status pyr_index_stats(const pyr_index *index, int64_t *count, int32_t *dim, int32_t *metric) {
+  if (!index) return fail(PYR_E_ARG, "null argument");
+  return guard([&] {
+    std::shared_lock<std::shared_mutex> g(index->impl->mu);
+    if (count) *count = index->impl->count();
+    if (dim) *dim = index->impl->dim;
+    if (metric) *metric = index->impl->metric;
+  });
+}
+
+pyr_status pyr_index_get_centroids(const pyr_index *index, float *out, int32_t *nlist) {
+  if (!index || !nlist) return fail(PYR_E_ARG, "null argument");
+  return guard([&] {
+    std::shared_lock<std::shared_mutex> g(index->impl->mu);
+    index->impl->centroids(out, nlist);
+  });
+}
+
+pyr_status pyr_index_ivf_layout(const pyr_index *index, int64_t *list_off, int64_t *labels, uint8_t *live,
+                                int64_t *total) {
+  if (!index || !total) return fail(PYR_E_ARG, "null argument");
+  return guard([&] {
+    std::shared_lock<std::shared_mutex> g(index->impl->mu);
+    index->impl->ivf_layout(list_off, labels, live, total);
+  });
+}
+
+pyr_status pyr_index_pq_state(const pyr_index *index, float *codebooks, int32_t *ksub, uint8_t *codes) {
+  if (!index) return fail(PYR_E_ARG, "null argument");
+  return guard([&] {
+    HIPCHK(hipSetDevice(index->impl->device));
+    std::shared_lock<std::shared_mutex> g(index->impl->mu);
+    index->impl->pq_state(codebooks, ksub, codes);
+  });
+}
+
+pyr_status pyr_merge_topk_device(const float *d_scores, const int64_t *d_labels, int64_t nq, int32_t nparts,
+                                 int32_t k, float *d_out_scores, int64_t *d_out_labels, void *stream) {
+  if (nq < 0 || nparts <= 0 || nparts > pyr::MAX_PARTS || k <= 0 || k > pyr::KMAX)
+    return fail(PYR_E_ARG, "bad merge shape");
+  return guard([&] {
+    pyr::launch_merge_labels(d_scores, d_labels, nq, nparts, k, d_out_scores, d_out_labels,
+                             reinterpret_cast<hipStream_t>(stream));
+    HIPCHK(hipGetLastError());
+  });
+}
+
+pyr_status pyr_generate_synthetic(int64_t count, int32_t dim, int32_t seed, float *out) {
+  if (count < 0 || dim <= 0 || (count > 0 && !out)) return fail(PYR_E_ARG, "bad argument");
+  pyr::NetRandom r(seed);  // Program.cs:251-263
+  const int64_t n = count * (int64_t)dim;
+  for (int64_t i = 0; i < n; i++) out[i] = (float)r.next_double();
+  return PYR_OK;
+}
+
+const char *pyr_last_error(void) { return g_err.c_str(); }
+
+const char *pyr_version(void) { return "pyrope_hip 0.1.0 gfx950"; }
+
+}  // extern "C"

@@ -1,0 +1,1016 @@
+// engine.cpp -- device-resident index objects behind include/pyrope_ann.h.
+//
+// Each class restates one reference IVectorIndex implementation's observable
+// semantics (storage order, buffer/list interplay, MaxScans, nprobe defaults,
+// quirks) with the scan itself on the GPU.  Paths are relative to
+// /root/reference/src/Pyrope.GarnetServer/.
+#include "engine.h"
+
+#include <algorithm>
+#include <cstring>
+#include <numeric>
+
+namespace pyr {
+
+// ---------------------------------------------------------------------------
+// memory
+// ---------------------------------------------------------------------------
+void DevMem::ensure(size_t bytes) {
+  if (bytes <= n && p) return;
+  if (p) HIPCHK(hipFree(p));
+  p = nullptr;
+  n = 0;
+  size_t want = std::max<size_t>(bytes, 256);
+  if (hipMalloc(&p, want) != hipSuccess) {
+    p = nullptr;
+    throw Error(PYR_E_OOM, "device allocation of " + std::to_string(want) + " bytes failed");
+  }
+  n = want;
+}
+
+void DevMem::grow_keep(size_t bytes, size_t keep, hipStream_t st) {
+  if (bytes <= n && p) return;
+  void *q = nullptr;
+  size_t want = std::max<size_t>(bytes, 256);
+  if (hipMalloc(&q, want) != hipSuccess) throw Error(PYR_E_OOM, "device allocation of " + std::to_string(want) + " bytes failed");
+  if (p && keep) HIPCHK(hipMemcpyAsync(q, p, std::min(keep, n), hipMemcpyDeviceToDevice, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (p) HIPCHK(hipFree(p));
+  p = q;
+  n = want;
+}
+
+static int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+void RowStore::reserve(int64_t slots, hipStream_t st) {
+  if (slots <= cap) return;
+  int64_t nc = round_up(std::max<int64_t>(slots, std::max<int64_t>(cap * 3 / 2, 64)), 8);
+  rows.grow_keep(sizeof(float) * nc * dim, sizeof(float) * cap * dim, st);
+  live.grow_keep(nc, cap, st);
+  labels.grow_keep(sizeof(int64_t) * nc, sizeof(int64_t) * cap, st);
+  if (cosine) norms.grow_keep(sizeof(float) * nc, sizeof(float) * cap, st);
+  // new tail: not visible, zero rows (padding rows of a group are never scored)
+  HIPCHK(hipMemsetAsync(live.as<uint8_t>() + cap, 0, nc - cap, st));
+  HIPCHK(hipMemsetAsync(rows.as<float>() + cap * dim, 0, sizeof(float) * (nc - cap) * dim, st));
+  if (cosine) HIPCHK(hipMemsetAsync(norms.as<float>() + cap, 0, sizeof(float) * (nc - cap), st));
+  cap = nc;
+}
+
+void RowStore::write(const float *x, const int64_t *slots, const int64_t *labs, int64_t cnt, hipStream_t st,
+                     DevMem &stage_x, DevMem &stage_i) {
+  if (cnt <= 0) return;
+  const size_t xb = sizeof(float) * cnt * dim;
+  stage_x.ensure(xb);
+  stage_i.ensure(sizeof(int64_t) * cnt * 2);
+  int64_t *di = stage_i.as<int64_t>();
+  HIPCHK(hipMemcpyAsync(stage_x.p, x, xb, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(di, slots, sizeof(int64_t) * cnt, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(di + cnt, labs, sizeof(int64_t) * cnt, hipMemcpyHostToDevice, st));
+  launch_scatter_blocked(stage_x.as<float>(), di, cnt, dim, rows.as<float>(), st);
+  launch_scatter_i64(labels.as<int64_t>(), di, di + cnt, cnt, st);
+  launch_scatter_u8(live.as<uint8_t>(), di, 1, cnt, st);
+  if (cosine) launch_norms_slots(rows.as<float>(), di, cnt, dim, norms.as<float>(), st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(st));  // staging buffers are reused by the next call
+}
+
+void RowStore::set_live(const std::vector<int64_t> &slots, uint8_t v, hipStream_t st, DevMem &stage) {
+  if (slots.empty()) return;
+  stage.ensure(sizeof(int64_t) * slots.size());
+  HIPCHK(hipMemcpyAsync(stage.p, slots.data(), sizeof(int64_t) * slots.size(), hipMemcpyHostToDevice, st));
+  launch_scatter_u8(live.as<uint8_t>(), stage.as<int64_t>(), v, (int64_t)slots.size(), st);
+  HIPCHK(hipStreamSynchronize(st));
+  for (int64_t s : slots) hlive[s] = v;
+}
+
+// ---------------------------------------------------------------------------
+// Index base
+// ---------------------------------------------------------------------------
+Index::Index(const pyr_index_desc &d) : desc(d), dim(d.dim), metric(d.metric), device(d.device) {
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(hipStreamCreateWithFlags(&wst, hipStreamNonBlocking));
+}
+
+Index::~Index() {
+  (void)hipSetDevice(device);
+  if (wst) (void)hipStreamSynchronize(wst);
+  free_ws.clear();
+  stream_ws.clear();
+  if (wst) (void)hipStreamDestroy(wst);
+}
+
+std::unique_ptr<Workspace> Index::take_ws() {
+  std::lock_guard<std::mutex> g(ws_mu);
+  if (!free_ws.empty()) {
+    auto w = std::move(free_ws.back());
+    free_ws.pop_back();
+    return w;
+  }
+  auto w = std::make_unique<Workspace>();
+  HIPCHK(hipStreamCreateWithFlags(&w->st, hipStreamNonBlocking));
+  w->own_stream = true;
+  return w;
+}
+
+void Index::give_ws(std::unique_ptr<Workspace> w) {
+  std::lock_guard<std::mutex> g(ws_mu);
+  free_ws.push_back(std::move(w));
+}
+
+Workspace &Index::ws_for_stream(hipStream_t st) {
+  std::lock_guard<std::mutex> g(ws_mu);
+  auto &p = stream_ws[st];
+  if (!p) {
+    p = std::make_unique<Workspace>();
+    p->st = st;
+  }
+  return *p;
+}
+
+void Index::ivf_layout(int64_t *, int64_t *, uint8_t *, int64_t *total) const {
+  (void)total;
+  throw Error(PYR_E_STATE, "index kind has no IVF layout");
+}
+void Index::pq_state(float *, int32_t *, uint8_t *) const { throw Error(PYR_E_STATE, "index kind is not IVF_PQ"); }
+
+void fill_empty_results(float *d_s, int64_t *d_l, int32_t *d_c, int64_t nq, int k, hipStream_t st) {
+  launch_fill_results(d_s, d_l, d_c, nq, k, st);
+}
+
+// ---------------------------------------------------------------------------
+// helpers shared by the scans
+// ---------------------------------------------------------------------------
+struct ScanPlan {
+  int chunk_rows = 0, nchunks = 0, nitems = 0, qchunk = QCHUNK;
+};
+
+static ScanPlan plan_flat(int64_t nrows, int64_t nq, int dim, int k, int max_parts) {
+  ScanPlan p;
+  p.qchunk = fast_path(dim, k) ? QCHUNK : QCHUNK_GENERIC;
+  const int64_t nqc = (nq + p.qchunk - 1) / p.qchunk;
+  int64_t want = std::max<int64_t>(1, (2048 + nqc - 1) / nqc);
+  want = std::min<int64_t>(want, std::max<int64_t>(1, nrows / 1024));
+  want = std::min<int64_t>(want, max_parts);
+  p.chunk_rows = (int)round_up((nrows + want - 1) / want, 8);
+  if (p.chunk_rows <= 0) p.chunk_rows = 8;
+  p.nchunks = (int)((nrows + p.chunk_rows - 1) / p.chunk_rows);
+  p.nitems = (int)(p.nchunks * nqc);
+  return p;
+}
+
+// scan rows [0,nrows) of `rs` for all queries into partial slots q*nparts + part_off + c
+static void flat_scan(const RowStore &rs, int64_t nrows, const ScanPlan &p, const float *d_q, const float *d_qn,
+                      int64_t nq, int k, int V, int met, int nparts, int part_off, uint32_t key_base, Workspace &ws,
+                      float *part_s, uint32_t *part_k, bool second = false) {
+  DevMem &items = second ? ws.items2 : ws.items;
+  DevMem &nitems = second ? ws.nitems2 : ws.nitems;
+  items.ensure(sizeof(ScanItem) * std::max(p.nitems, 1));
+  nitems.ensure(sizeof(int32_t) * 4);
+  make_flat_items(items.as<ScanItem>(), nitems.as<int32_t>(), nrows, p.chunk_rows, nq, part_off, p.qchunk, ws.st);
+  ScanArgs a{};
+  a.rows = rs.rows.as<float>();
+  a.live = rs.live.as<uint8_t>();
+  a.rnorm = rs.cosine ? rs.norms.as<float>() : nullptr;
+  a.queries = d_q;
+  a.qnorm = d_qn;
+  a.items = items.as<ScanItem>();
+  a.n_items = nitems.as<int32_t>();
+  a.qlist = nullptr;
+  a.limits = nullptr;
+  a.nparts = nparts;
+  a.k = k;
+  a.key_base = key_base;
+  a.dim = rs.dim;
+  a.part_s = part_s;
+  a.part_k = part_k;
+  launch_scan(a, met, V, p.nitems, ws.st);
+}
+
+static void query_norms(const float *d_q, int64_t nq, int dim, int met, Workspace &ws) {
+  if (met != COS) return;
+  ws.qn.ensure(sizeof(float) * std::max<int64_t>(nq, 1));
+  launch_norms(d_q, nq, dim, 0, ws.qn.as<float>(), ws.st);
+}
+
+// ---------------------------------------------------------------------------
+// k-means on the GPU (KMeansUtils.cs:10-68)
+// ---------------------------------------------------------------------------
+
+void assign_gpu(const float *d_x, int64_t n, int dim, const float *d_cents, int k, int met, int32_t *d_assign,
+                hipStream_t st) {
+  if (n <= 0) return;
+  // centroid store (blocked) as the scanned rows; data rows as the queries; top-1 with ties -> lowest index
+  RowStore cs;
+  cs.dim = dim;
+  cs.cosine = met == COS;
+  cs.reserve(round_up(k, 8), st);
+  launch_to_blocked(d_cents, nullptr, k, dim, cs.rows.as<float>(), 0, st);
+  fill_u8(cs.live.as<uint8_t>(), 1, k, st);
+  if (cs.cosine) launch_norms(cs.rows.as<float>(), k, dim, 1, cs.norms.as<float>(), st);
+  Workspace ws;
+  ws.st = st;
+  if (met == COS) query_norms(d_x, n, dim, met, ws);
+  ScanPlan p;
+  p.qchunk = fast_path(dim, 1) ? QCHUNK : QCHUNK_GENERIC;
+  p.chunk_rows = (int)round_up(k, 8);
+  p.nchunks = 1;
+  p.nitems = (int)((n + p.qchunk - 1) / p.qchunk);
+  DevMem ps, pk;
+  ps.ensure(sizeof(float) * n);
+  pk.ensure(sizeof(uint32_t) * n);
+  flat_scan(cs, k, p, d_x, met == COS ? ws.qn.as<float>() : nullptr, n, 1, 1, met, 1, 0, 0, ws, ps.as<float>(),
+            pk.as<uint32_t>());
+  launch_keys_to_assign(pk.as<uint32_t>(), n, d_assign, st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(st));
+}
+
+int kmeans_train_gpu(const float *d_x, int64_t n, int dim, int k, int met, int max_iter, int seed, float *d_cents,
+                     hipStream_t st) {
+  if (n == 0) return 0;                      // :12
+  if (k <= 0) k = 1;                         // :13
+  if (k > n) k = (int)n;                     // :14
+  // :20 data.OrderBy(_ => rnd.Next()).Take(k): one Next() per row in row order, stable by (key, row)
+  NetRandom rnd(seed);
+  std::vector<std::pair<int32_t, int32_t>> keys((size_t)n);
+  for (int64_t i = 0; i < n; i++) keys[i] = {rnd.next(), (int32_t)i};
+  std::partial_sort(keys.begin(), keys.begin() + k, keys.end());
+  std::vector<int32_t> init(k);
+  for (int i = 0; i < k; i++) init[i] = keys[i].second;
+  keys.clear();
+  keys.shrink_to_fit();
+  DevMem didx;
+  didx.ensure(sizeof(int32_t) * k);
+  HIPCHK(hipMemcpyAsync(didx.p, init.data(), sizeof(int32_t) * k, hipMemcpyHostToDevice, st));
+  launch_gather_rows(d_x, didx.as<int32_t>(), k, dim, d_cents, st);
+
+  DevMem assign, ktmp, iin, members, counts, coff, temp, tmp, flags, changed;
+  assign.ensure(sizeof(int32_t) * n);
+  ktmp.ensure(sizeof(int32_t) * n);
+  iin.ensure(sizeof(int32_t) * n);
+  members.ensure(sizeof(int32_t) * n);
+  counts.ensure(sizeof(int32_t) * (k + 1));
+  coff.ensure(sizeof(int32_t) * (k + 1));
+  const size_t tb = sort_temp_bytes(n, k);
+  temp.ensure(tb);
+  tmp.ensure(sizeof(float) * k * dim);
+  flags.ensure(sizeof(int32_t) * k);
+  changed.ensure(sizeof(int32_t));
+  for (int it = 0; it < max_iter; it++) {     // :22
+    assign_gpu(d_x, n, dim, d_cents, k, met, assign.as<int32_t>(), st);  // :34-38
+    sort_by_key(assign.as<int32_t>(), n, k, ktmp.as<int32_t>(), iin.as<int32_t>(), members.as<int32_t>(),
+                counts.as<int32_t>(), coff.as<int32_t>(), temp.p, tb, st);  // :40-43 members in data order
+    launch_kmeans_update(d_x, members.as<int32_t>(), coff.as<int32_t>(), k, dim, d_cents, tmp.as<float>(),
+                         flags.as<int32_t>(), changed.as<int32_t>(), st);  // :46-62
+    int32_t ch = 0;
+    HIPCHK(hipMemcpyAsync(&ch, changed.p, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (!ch) break;                            // :64
+  }
+  return k;
+}
+
+// ---------------------------------------------------------------------------
+// FLAT = BruteForceVectorIndex (BruteForceVectorIndex.cs)
+// ---------------------------------------------------------------------------
+struct FlatIndex : Index {
+  RowStore st;
+  std::unordered_map<int64_t, int64_t> slot_of;  // _idMap (:15)
+
+  explicit FlatIndex(const pyr_index_desc &d) : Index(d) {
+    st.dim = dim;
+    st.cosine = metric == COS;  // norm cached at Add (:146)
+  }
+
+  void add(const float *x, int64_t n, const int64_t *labels, bool upsert) override {
+    std::vector<int64_t> slots(n);
+    if (!upsert) {  // :141-144 duplicate id -> InvalidOperationException
+      std::unordered_map<int64_t, int> seen;
+      for (int64_t i = 0; i < n; i++)
+        if (slot_of.count(labels[i]) || seen[labels[i]]++)
+          throw Error(PYR_E_DUPLICATE, "Vector with id '" + std::to_string(labels[i]) + "' already exists.");
+    }
+    int64_t next = st.n;
+    std::unordered_map<int64_t, int64_t> batch;
+    for (int64_t i = 0; i < n; i++) {
+      auto f = slot_of.find(labels[i]);
+      if (f != slot_of.end()) slots[i] = f->second;        // :193-210 update in place
+      else {
+        auto b = batch.find(labels[i]);
+        slots[i] = b != batch.end() ? b->second : next++;  // :151-179 append slot
+        batch[labels[i]] = slots[i];
+      }
+    }
+    st.reserve(next, wst);
+    st.hlabels.resize(next, -1);
+    st.hlive.resize(next, 0);
+    st.write(x, slots.data(), labels, n, wst, stage_x, stage_i);
+    for (int64_t i = 0; i < n; i++) {
+      st.hlabels[slots[i]] = labels[i];
+      st.hlive[slots[i]] = 1;
+      slot_of[labels[i]] = slots[i];
+    }
+    st.n = next;
+  }
+
+  void remove(const int64_t *labels, int64_t n, uint8_t *removed) override {  // :224-248
+    std::vector<int64_t> dead;
+    for (int64_t i = 0; i < n; i++) {
+      auto f = slot_of.find(labels[i]);
+      if (removed) removed[i] = f != slot_of.end();
+      if (f == slot_of.end()) continue;
+      dead.push_back(f->second);
+      slot_of.erase(f);
+    }
+    st.set_live(dead, 0, wst, stage_b);
+  }
+
+  void search(const float *d_q, int64_t nq, int k, const pyr_search_params &prm, float *d_s, int64_t *d_l,
+              int32_t *d_c, Workspace &ws) override {
+    if (k <= 0) throw Error(PYR_E_ARG, "topK must be positive.");  // :278
+    int64_t count = st.n;
+    int64_t cutoff = count;  // :288 scanLimit = min(MaxScans, count), counted over live slots in order
+    if (prm.max_scans >= 0) {
+      if (prm.max_scans == 0) cutoff = 0;
+      else {
+        int64_t seen = 0;
+        cutoff = count;
+        for (int64_t i = 0; i < count; i++)
+          if (st.hlive[i] && ++seen == prm.max_scans) {
+            cutoff = i + 1;
+            break;
+          }
+      }
+    }
+    if (count == 0 || cutoff == 0 || nq == 0) {  // :285, :289
+      fill_empty_results(d_s, d_l, d_c, nq, k, ws.st);
+      return;
+    }
+    query_norms(d_q, nq, dim, metric, ws);
+    ScanPlan p = plan_flat(cutoff, nq, dim, k, MAX_PARTS);
+    const size_t np = (size_t)nq * p.nchunks * k;
+    ws.part_s.ensure(sizeof(float) * np);
+    ws.part_k.ensure(sizeof(uint32_t) * np);
+    flat_scan(st, cutoff, p, d_q, metric == COS ? ws.qn.as<float>() : nullptr, nq, k, 4, metric, p.nchunks, 0, 0, ws,
+              ws.part_s.as<float>(), ws.part_k.as<uint32_t>());
+    launch_merge_keys(ws.part_s.as<float>(), ws.part_k.as<uint32_t>(), nq, p.nchunks, k, st.labels.as<int64_t>(),
+                      nullptr, d_s, d_l, nullptr, d_c, ws.st);
+  }
+
+  int64_t count() const override { return (int64_t)slot_of.size(); }  // :115-126
+};
+
+// ---------------------------------------------------------------------------
+// Pre-build buffer with .NET Dictionary<string, ...> slot semantics:
+// enumeration = slot order; removal frees a slot; insertion reuses the most
+// recently freed slot (LIFO free list).  (IvfFlatVectorIndex.cs:17, IvfPqVectorIndex.cs:19)
+// ---------------------------------------------------------------------------
+struct DictBuffer {
+  RowStore st;
+  std::unordered_map<int64_t, int64_t> slot_of;
+  std::vector<int64_t> free_slots;
+
+  // returns slots for labels (overwrite existing, reuse freed, else append)
+  std::vector<int64_t> place(const int64_t *labels, int64_t n) {
+    std::vector<int64_t> slots(n);
+    for (int64_t i = 0; i < n; i++) {
+      auto f = slot_of.find(labels[i]);
+      if (f != slot_of.end()) {
+        slots[i] = f->second;
+        continue;
+      }
+      int64_t s;
+      if (!free_slots.empty()) {
+        s = free_slots.back();
+        free_slots.pop_back();
+      } else {
+        s = st.n++;
+        st.hlabels.push_back(-1);
+        st.hlive.push_back(0);
+      }
+      slot_of[labels[i]] = s;
+      slots[i] = s;
+    }
+    return slots;
+  }
+  void write(const float *x, const int64_t *labels, int64_t n, hipStream_t wst, DevMem &sx, DevMem &si) {
+    std::vector<int64_t> slots = place(labels, n);
+    st.reserve(st.n, wst);
+    st.write(x, slots.data(), labels, n, wst, sx, si);
+    for (int64_t i = 0; i < n; i++) {
+      st.hlabels[slots[i]] = labels[i];
+      st.hlive[slots[i]] = 1;
+    }
+  }
+  bool erase(int64_t label, std::vector<int64_t> &dead) {
+    auto f = slot_of.find(label);
+    if (f == slot_of.end()) return false;
+    dead.push_back(f->second);
+    free_slots.push_back(f->second);
+    slot_of.erase(f);
+    return true;
+  }
+  int64_t live_count() const { return (int64_t)slot_of.size(); }
+  // slot cutoff after the first `m` live slots (m < 0: all)
+  int64_t cutoff(int64_t m) const {
+    if (m < 0 || m >= live_count()) return st.n;
+    if (m == 0) return 0;
+    int64_t seen = 0;
+    for (int64_t i = 0; i < st.n; i++)
+      if (st.hlive[i] && ++seen == m) return i + 1;
+    return st.n;
+  }
+  void clear(hipStream_t wst) {
+    if (st.n) HIPCHK(hipMemsetAsync(st.live.p, 0, st.n, wst));
+    st.clear();
+    slot_of.clear();
+    free_slots.clear();
+  }
+};
+
+// coarse quantizer shared by IVF_FLAT and IVF_PQ: centroids blocked + row-major
+struct Coarse {
+  int nlist = 0;
+  RowStore cs;
+  DevMem rm;  // row-major centroids
+  std::vector<float> host;
+
+  void set(const float *d_cents_rm, int k, int dim, int met, hipStream_t st) {
+    nlist = k;
+    cs.dim = dim;
+    cs.cosine = met == COS;  // centroid norms cached (IvfFlatVectorIndex.cs:122)
+    cs.clear();
+    cs.reserve(round_up(k, 8), st);
+    HIPCHK(hipMemsetAsync(cs.live.p, 0, cs.cap, st));
+    launch_to_blocked(d_cents_rm, nullptr, k, dim, cs.rows.as<float>(), 0, st);
+    fill_u8(cs.live.as<uint8_t>(), 1, k, st);
+    if (cs.cosine) launch_norms(cs.rows.as<float>(), k, dim, 1, cs.norms.as<float>(), st);
+    rm.ensure(sizeof(float) * k * dim);
+    HIPCHK(hipMemcpyAsync(rm.p, d_cents_rm, sizeof(float) * k * dim, hipMemcpyDeviceToDevice, st));
+    host.resize((size_t)k * dim);
+    HIPCHK(hipMemcpyAsync(host.data(), d_cents_rm, sizeof(float) * k * dim, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    cs.n = k;
+  }
+
+  // score all centroids (ComputeScore, safe VectorMath), rank desc (ties by index), keep nprobe
+  // IvfFlatVectorIndex.cs:186-198, IvfPqVectorIndex.cs:141-150
+  void probe(const float *d_q, const float *d_qn, int64_t nq, int nprobe, int met, Workspace &ws) {
+    const int qchunk = fast_path(cs.dim, nprobe) ? QCHUNK : QCHUNK_GENERIC;
+    const int64_t nqc = (nq + qchunk - 1) / qchunk;
+    int want = (int)std::max<int64_t>(1, std::min<int64_t>(16, (2048 + nqc - 1) / nqc));
+    want = std::min(want, std::max(1, nlist / 32));
+    ScanPlan p;
+    p.qchunk = qchunk;
+    p.chunk_rows = (int)round_up((nlist + want - 1) / want, 8);
+    p.nchunks = (nlist + p.chunk_rows - 1) / p.chunk_rows;
+    p.nitems = (int)(p.nchunks * nqc);
+    const size_t np = (size_t)nq * p.nchunks * nprobe;
+    ws.cpart_s.ensure(sizeof(float) * np);
+    ws.cpart_k.ensure(sizeof(uint32_t) * np);
+    flat_scan(cs, nlist, p, d_q, d_qn, nq, nprobe, 1, met, p.nchunks, 0, 0, ws, ws.cpart_s.as<float>(),
+              ws.cpart_k.as<uint32_t>());
+    ws.probes.ensure(sizeof(int32_t) * nq * nprobe);
+    launch_merge_keys(ws.cpart_s.as<float>(), ws.cpart_k.as<uint32_t>(), nq, p.nchunks, nprobe, nullptr, nullptr,
+                      nullptr, nullptr, ws.probes.as<int32_t>(), nullptr, ws.st);
+  }
+};
+
+// list-major work items from ws.probes
+static int build_ivf_items(Workspace &ws, int64_t nq, int nprobe, int nparts, int nlist, const DevMem &lbeg,
+                           const DevMem &lend, int qchunk) {
+  const int maxi = ivf_max_items(nq, nprobe, nlist, qchunk);
+  ws.ivf_cnt.ensure(sizeof(int32_t) * nlist);
+  ws.ivf_fill.ensure(sizeof(int32_t) * nlist);
+  ws.ivf_qoff.ensure(sizeof(int32_t) * (nlist + 1));
+  ws.ivf_ioff.ensure(sizeof(int32_t) * (nlist + 1));
+  ws.qlist.ensure(sizeof(int32_t) * std::max<int64_t>(nq * nprobe, 1));
+  ws.items.ensure(sizeof(ScanItem) * maxi);
+  ws.nitems.ensure(sizeof(int32_t) * 4);
+  IvfItemWs iw{ws.ivf_cnt.as<int32_t>(), ws.ivf_fill.as<int32_t>(), ws.ivf_qoff.as<int32_t>(),
+               ws.ivf_ioff.as<int32_t>(), ws.qlist.as<int32_t>(), ws.items.as<ScanItem>(), ws.nitems.as<int32_t>()};
+  launch_ivf_items(ws.probes.as<int32_t>(), nq, nprobe, nparts, nlist, lbeg.as<int32_t>(), lend.as<int32_t>(), qchunk,
+                   iw, ws.st);
+  return maxi;
+}
+
+// ---------------------------------------------------------------------------
+// IVF_FLAT = IvfFlatVectorIndex (IvfFlatVectorIndex.cs)
+// ---------------------------------------------------------------------------
+struct IvfFlatIndex : Index {
+  DictBuffer buf;                         // _buffer (:17)
+  RowStore lists;                         // _invertedLists (:22), list-major, lists padded to 8 rows
+  std::vector<uint8_t> lstate;            // 0 removed/pad, 1 visible, 2 shadowed by a buffer id (:210)
+  std::unordered_map<int64_t, int64_t> pos_of;
+  std::vector<int32_t> lb, le, llen, llive;
+  DevMem dlb, dle, dllive;
+  Coarse coarse;
+  bool built = false;                     // _isBuilt (:20)
+  int nprobe_default;
+
+  explicit IvfFlatIndex(const pyr_index_desc &d) : Index(d) {
+    buf.st.dim = lists.dim = dim;
+    buf.st.cosine = lists.cosine = metric == COS;  // CreateEntry norm (:343-349)
+    nprobe_default = d.default_nprobe > 0 ? d.default_nprobe : 3;  // CombineNProbe (:14)
+  }
+
+  void upload_list_meta() {
+    const int nl = coarse.nlist;
+    dlb.ensure(sizeof(int32_t) * std::max(nl, 1));
+    dle.ensure(sizeof(int32_t) * std::max(nl, 1));
+    dllive.ensure(sizeof(int32_t) * std::max(nl, 1));
+    HIPCHK(hipMemcpyAsync(dlb.p, lb.data(), sizeof(int32_t) * nl, hipMemcpyHostToDevice, wst));
+    HIPCHK(hipMemcpyAsync(dle.p, le.data(), sizeof(int32_t) * nl, hipMemcpyHostToDevice, wst));
+    HIPCHK(hipMemcpyAsync(dllive.p, llive.data(), sizeof(int32_t) * nl, hipMemcpyHostToDevice, wst));
+    HIPCHK(hipStreamSynchronize(wst));
+  }
+  int list_of_pos(int64_t pos) const {
+    return (int)(std::upper_bound(lb.begin(), lb.end(), (int32_t)pos) - lb.begin()) - 1;
+  }
+
+  void add(const float *x, int64_t n, const int64_t *labels, bool) override {  // Add == Upsert (:39-59)
+    buf.write(x, labels, n, wst, stage_x, stage_i);
+    if (!built) return;
+    std::vector<int64_t> shadow;
+    for (int64_t i = 0; i < n; i++) {
+      auto f = pos_of.find(labels[i]);
+      if (f != pos_of.end() && lstate[f->second] == 1) {
+        lstate[f->second] = 2;
+        llive[list_of_pos(f->second)]--;
+        shadow.push_back(f->second);
+      }
+    }
+    if (!shadow.empty()) {
+      lists.set_live(shadow, 0, wst, stage_b);
+      upload_list_meta();
+    }
+  }
+
+  void remove(const int64_t *labels, int64_t n, uint8_t *removed) override {  // :61-83
+    std::vector<int64_t> dead_buf, dead_list;
+    for (int64_t i = 0; i < n; i++) {
+      bool r = buf.erase(labels[i], dead_buf);
+      if (built) {
+        auto f = pos_of.find(labels[i]);
+        if (f != pos_of.end()) {
+          if (lstate[f->second] == 1) llive[list_of_pos(f->second)]--;
+          lstate[f->second] = 0;
+          dead_list.push_back(f->second);
+          pos_of.erase(f);
+          r = true;
+        }
+      }
+      if (removed) removed[i] = r;
+    }
+    buf.st.set_live(dead_buf, 0, wst, stage_b);
+    if (!dead_list.empty()) {
+      lists.set_live(dead_list, 0, wst, stage_b);
+      for (int64_t p : dead_list) lists.hlabels[p] = -1;
+      upload_list_meta();
+    }
+  }
+
+  void build() override {  // :85-145
+    // 1. uniqueData: existing list items in list order (buffer value wins), then new buffer ids
+    std::vector<int64_t> src, labs;  // src >= 0: list position; < 0: buffer slot (-s-1)
+    if (built)
+      for (int l = 0; l < coarse.nlist; l++)
+        for (int32_t p = lb[l]; p < lb[l] + llen[l]; p++) {
+          if (lstate[p] == 0) continue;
+          const int64_t lab = lists.hlabels[p];
+          src.push_back(lstate[p] == 2 ? -buf.slot_of.at(lab) - 1 : p);
+          labs.push_back(lab);
+        }
+    for (int64_t s = 0; s < buf.st.n; s++) {
+      if (!buf.st.hlive[s]) continue;
+      const int64_t lab = buf.st.hlabels[s];
+      if (built && pos_of.count(lab)) continue;  // already placed (overwritten in place)
+      src.push_back(-s - 1);
+      labs.push_back(lab);
+    }
+    const int64_t n = (int64_t)src.size();
+    if (n == 0) return;  // :111
+    DevMem X, dsrc;
+    X.ensure(sizeof(float) * n * dim);
+    dsrc.ensure(sizeof(int64_t) * n);
+    HIPCHK(hipMemcpyAsync(dsrc.p, src.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, wst));
+    launch_gather2(built ? lists.rows.as<float>() : buf.st.rows.as<float>(), buf.st.rows.as<float>(),
+                   dsrc.as<int64_t>(), n, dim, X.as<float>(), wst);
+    // 2. train (:116-119)
+    int k = (int)std::min<int64_t>(desc.nlist, n);
+    if (k <= 0) k = 1;
+    DevMem C;
+    C.ensure(sizeof(float) * k * dim);
+    k = kmeans_train_gpu(X.as<float>(), n, dim, k, metric, 10, 42, C.as<float>(), wst);
+    // 3. assign (:128-132)
+    DevMem A;
+    A.ensure(sizeof(int32_t) * n);
+    assign_gpu(X.as<float>(), n, dim, C.as<float>(), k, metric, A.as<int32_t>(), wst);
+    std::vector<int32_t> asg(n);
+    HIPCHK(hipMemcpyAsync(asg.data(), A.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, wst));
+    HIPCHK(hipStreamSynchronize(wst));
+    // stable list-major layout, lists padded to 8 rows
+    std::vector<int32_t> cnt(k, 0);
+    for (int32_t a : asg) cnt[a]++;
+    lb.assign(k, 0);
+    le.assign(k, 0);
+    llen = cnt;
+    llive = cnt;
+    int64_t tot = 0;
+    for (int l = 0; l < k; l++) {
+      lb[l] = (int32_t)tot;
+      le[l] = (int32_t)(tot + cnt[l]);
+      tot += round_up(cnt[l], 8);
+    }
+    if (tot >= (int64_t)KEY_BUF) throw Error(PYR_E_ARG, "IVF index larger than 2^31 rows");
+    std::vector<int64_t> srcrow(tot, -1), newlab(tot, -1);
+    std::vector<int32_t> fillp(lb);
+    for (int64_t i = 0; i < n; i++) {
+      const int32_t p = fillp[asg[i]]++;
+      srcrow[p] = i;
+      newlab[p] = labs[i];
+    }
+    // 4. commit (:135-139)
+    RowStore nl;
+    nl.dim = dim;
+    nl.cosine = metric == COS;
+    nl.reserve(std::max<int64_t>(tot, 8), wst);
+    DevMem dsr;
+    dsr.ensure(sizeof(int64_t) * tot);
+    HIPCHK(hipMemcpyAsync(dsr.p, srcrow.data(), sizeof(int64_t) * tot, hipMemcpyHostToDevice, wst));
+    launch_to_blocked(X.as<float>(), dsr.as<int64_t>(), tot, dim, nl.rows.as<float>(), 0, wst);
+    std::vector<uint8_t> lv(tot);
+    for (int64_t p = 0; p < tot; p++) lv[p] = srcrow[p] >= 0;
+    HIPCHK(hipMemcpyAsync(nl.live.p, lv.data(), tot, hipMemcpyHostToDevice, wst));
+    HIPCHK(hipMemcpyAsync(nl.labels.p, newlab.data(), sizeof(int64_t) * tot, hipMemcpyHostToDevice, wst));
+    if (nl.cosine) launch_norms(nl.rows.as<float>(), tot, dim, 1, nl.norms.as<float>(), wst);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(wst));
+    nl.n = tot;
+    nl.hlabels = newlab;
+    nl.hlive = lv;
+    std::swap(lists.rows.p, nl.rows.p);
+    std::swap(lists.rows.n, nl.rows.n);
+    std::swap(lists.live.p, nl.live.p);
+    std::swap(lists.live.n, nl.live.n);
+    std::swap(lists.labels.p, nl.labels.p);
+    std::swap(lists.labels.n, nl.labels.n);
+    std::swap(lists.norms.p, nl.norms.p);
+    std::swap(lists.norms.n, nl.norms.n);
+    lists.n = tot;
+    lists.cap = nl.cap;
+    lists.hlabels.swap(nl.hlabels);
+    lists.hlive.swap(nl.hlive);
+    lstate = lv;
+    pos_of.clear();
+    for (int64_t p = 0; p < tot; p++)
+      if (newlab[p] >= 0) pos_of[newlab[p]] = p;
+    coarse.set(C.as<float>(), k, dim, metric, wst);
+    upload_list_meta();
+    buf.clear(wst);
+    built = true;
+  }
+
+  void search(const float *d_q, int64_t nq, int k, const pyr_search_params &prm, float *d_s, int64_t *d_l,
+              int32_t *d_c, Workspace &ws) override {  // :147-231
+    if (k <= 0 || nq == 0) {
+      fill_empty_results(d_s, d_l, d_c, nq, std::max(k, 0), ws.st);
+      return;
+    }
+    const int nprobe = prm.nprobe < 0 ? nprobe_default : prm.nprobe;                  // :151-158
+    const int64_t maxs = prm.max_scans < 0 ? (int64_t)INT32_MAX : prm.max_scans;       // :152
+    const int64_t bcut = buf.cutoff(std::min<int64_t>(maxs, buf.live_count()));
+    const int64_t bscanned = std::min<int64_t>(maxs, buf.live_count());
+    const bool index_on = built && coarse.nlist > 0 && bscanned < maxs;                // :183
+    const int probes = index_on ? std::max(0, std::min(nprobe, coarse.nlist)) : 0;    // :198
+    ScanPlan bp;
+    if (bcut > 0) bp = plan_flat(bcut, nq, dim, k, MAX_PARTS - probes);
+    const int nparts = probes + bp.nchunks;
+    if (nparts > MAX_PARTS) throw Error(PYR_E_ARG, "nprobe too large");
+    if (nparts == 0) {
+      fill_empty_results(d_s, d_l, d_c, nq, k, ws.st);
+      return;
+    }
+    query_norms(d_q, nq, dim, metric, ws);
+    const float *qn = metric == COS ? ws.qn.as<float>() : nullptr;
+    const size_t np = (size_t)nq * nparts * k;
+    ws.part_s.ensure(sizeof(float) * np);
+    ws.part_k.ensure(sizeof(uint32_t) * np);
+    if (probes > 0) {
+      coarse.probe(d_q, qn, nq, probes, metric, ws);
+      const int qchunk = fast_path(dim, k) ? QCHUNK : QCHUNK_GENERIC;
+      const int maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qchunk);
+      const uint32_t *lim = nullptr;
+      if (prm.max_scans >= 0) {  // :202-212
+        ws.limits.ensure(sizeof(uint32_t) * nq * nparts);
+        launch_ivf_limits(ws.probes.as<int32_t>(), nq, probes, nparts, maxs - bscanned, dlb.as<int32_t>(),
+                          dle.as<int32_t>(), dllive.as<int32_t>(), lists.live.as<uint8_t>(), ws.limits.as<uint32_t>(),
+                          ws.st);
+        lim = ws.limits.as<uint32_t>();
+      }
+      ScanArgs a{};
+      a.rows = lists.rows.as<float>();
+      a.live = lists.live.as<uint8_t>();
+      a.rnorm = lists.cosine ? lists.norms.as<float>() : nullptr;
+      a.queries = d_q;
+      a.qnorm = qn;
+      a.items = ws.items.as<ScanItem>();
+      a.n_items = ws.nitems.as<int32_t>();
+      a.qlist = ws.qlist.as<int32_t>();
+      a.limits = lim;
+      a.nparts = nparts;
+      a.k = k;
+      a.key_base = 0;
+      a.dim = dim;
+      a.part_s = ws.part_s.as<float>();
+      a.part_k = ws.part_k.as<uint32_t>();
+      launch_scan(a, metric, 1, maxi, ws.st);
+    }
+    if (bcut > 0)  // :170-180 exact buffer scan, keys KEY_BUF | slot
+      flat_scan(buf.st, bcut, bp, d_q, qn, nq, k, 1, metric, nparts, probes, KEY_BUF, ws, ws.part_s.as<float>(),
+                ws.part_k.as<uint32_t>(), true);
+    launch_merge_keys(ws.part_s.as<float>(), ws.part_k.as<uint32_t>(), nq, nparts, k, lists.labels.as<int64_t>(),
+                      buf.st.labels.as<int64_t>(), d_s, d_l, nullptr, d_c, ws.st);
+  }
+
+  int64_t count() const override {  // :305 buffer + all list entries (shadowed ones too)
+    int64_t c = buf.live_count();
+    for (uint8_t s : lstate) c += s != 0;
+    return c;
+  }
+
+  void centroids(float *out, int32_t *nl) const override {  // :314-325
+    *nl = built ? coarse.nlist : 0;
+    if (out && built) std::memcpy(out, coarse.host.data(), sizeof(float) * coarse.host.size());
+  }
+
+  void ivf_layout(int64_t *off, int64_t *labels, uint8_t *live, int64_t *total) const override {
+    int64_t t = 0;
+    for (int l = 0; l < coarse.nlist && built; l++) {
+      if (off) off[l] = t;
+      for (int32_t p = lb[l]; p < lb[l] + llen[l]; p++, t++) {
+        if (labels) labels[t] = lstate[p] ? lists.hlabels[p] : -1;
+        if (live) live[t] = lstate[p] == 1;
+      }
+    }
+    if (off && built) off[coarse.nlist] = t;
+    *total = t;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// IVF_PQ = IvfPqVectorIndex + ProductQuantizer
+// ---------------------------------------------------------------------------
+struct IvfPqIndex : Index {
+  DictBuffer buf;                    // _buffer (:19)
+  int M, K, sub;
+  DevMem codes, clive, clabels;      // blocked codes, per code-row visibility, labels
+  std::vector<int64_t> hlabels;      // per code row (-1 pad)
+  std::vector<uint8_t> hlive;
+  std::unordered_map<int64_t, int64_t> pos_of;
+  std::vector<int32_t> lb, le, llen;
+  DevMem dlb, dle;
+  Coarse coarse;
+  DevMem cb;                         // [M][ksub][sub]
+  int ksub = 0;
+  int64_t ncode_rows = 0;
+  bool built = false;
+  int nprobe_default;
+
+  explicit IvfPqIndex(const pyr_index_desc &d) : Index(d) {
+    M = d.pq_m;
+    K = d.pq_k;
+    if (M <= 0 || dim % M != 0) throw Error(PYR_E_ARG, "Dimension must be divisible by M");  // PQ.cs:18
+    if (K > 256 || K <= 0) throw Error(PYR_E_ARG, "K must be <= 256 for byte encoding");    // PQ.cs:19
+    sub = dim / M;
+    buf.st.dim = dim;
+    buf.st.cosine = metric == COS;
+    nprobe_default = d.default_nprobe > 0 ? d.default_nprobe : 1;  // :125
+  }
+
+  void set_shadow(int64_t label, uint8_t visible, std::vector<int64_t> &on, std::vector<int64_t> &off) {
+    auto f = pos_of.find(label);
+    if (f == pos_of.end()) return;
+    if (hlive[f->second] == visible) return;
+    hlive[f->second] = visible;
+    (visible ? on : off).push_back(f->second);
+  }
+  void push_live(const std::vector<int64_t> &slots, uint8_t v) {
+    if (slots.empty()) return;
+    stage_b.ensure(sizeof(int64_t) * slots.size());
+    HIPCHK(hipMemcpyAsync(stage_b.p, slots.data(), sizeof(int64_t) * slots.size(), hipMemcpyHostToDevice, wst));
+    launch_scatter_u8(clive.as<uint8_t>(), stage_b.as<int64_t>(), v, (int64_t)slots.size(), wst);
+    HIPCHK(hipStreamSynchronize(wst));
+  }
+
+  void add(const float *x, int64_t n, const int64_t *labels, bool) override {  // :37-47
+    buf.write(x, labels, n, wst, stage_x, stage_i);
+    std::vector<int64_t> on, off;
+    for (int64_t i = 0; i < n; i++) set_shadow(labels[i], 0, on, off);  // seen (:134,170)
+    push_live(off, 0);
+  }
+
+  void remove(const int64_t *labels, int64_t n, uint8_t *removed) override {  // :48-53 buffer only
+    std::vector<int64_t> dead, on, off;
+    for (int64_t i = 0; i < n; i++) {
+      const bool r = buf.erase(labels[i], dead);
+      if (removed) removed[i] = r;
+      if (r) set_shadow(labels[i], 1, on, off);  // no longer "seen": list entry visible again
+    }
+    buf.st.set_live(dead, 0, wst, stage_b);
+    push_live(on, 1);
+  }
+
+  void build() override {  // :55-116
+    if (buf.live_count() == 0 && !built) return;      // :60
+    std::vector<int64_t> slots, labs;                 // allVectors = _buffer.Values (:64)
+    for (int64_t s = 0; s < buf.st.n; s++)
+      if (buf.st.hlive[s]) {
+        slots.push_back(s);
+        labs.push_back(buf.st.hlabels[s]);
+      }
+    const int64_t n = (int64_t)slots.size();
+    if (n == 0) return;                               // :65
+    DevMem X, ds;
+    X.ensure(sizeof(float) * n * dim);
+    ds.ensure(sizeof(int64_t) * n);
+    HIPCHK(hipMemcpyAsync(ds.p, slots.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, wst));
+    launch_gather_blocked(buf.st.rows.as<float>(), ds.as<int64_t>(), n, dim, X.as<float>(), wst);
+    int nc = (int)std::min<int64_t>(desc.nlist, n);   // :68
+    if (nc <= 0) nc = 1;
+    DevMem C;
+    C.ensure(sizeof(float) * nc * dim);
+    nc = kmeans_train_gpu(X.as<float>(), n, dim, nc, metric, 10, 123, C.as<float>(), wst);  // :69
+    DevMem A, R, S;
+    A.ensure(sizeof(int32_t) * n);
+    assign_gpu(X.as<float>(), n, dim, C.as<float>(), nc, metric, A.as<int32_t>(), wst);   // :79
+    R.ensure(sizeof(float) * n * dim);
+    launch_residuals(X.as<float>(), A.as<int32_t>(), C.as<float>(), n, dim, R.as<float>(), wst);  // :82-85
+    // PQ train (ProductQuantizer.cs:28-58): per subspace k-means, L2, seed 42+m
+    ksub = (int)std::min<int64_t>(K, n);
+    if (ksub <= 0) ksub = 1;
+    cb.ensure(sizeof(float) * (size_t)M * ksub * sub);
+    S.ensure(sizeof(float) * n * sub);
+    for (int m = 0; m < M; m++) {
+      launch_extract_sub(R.as<float>(), n, dim, m * sub, sub, S.as<float>(), wst);
+      kmeans_train_gpu(S.as<float>(), n, sub, K, L2, 10, 42 + m, cb.as<float>() + (size_t)m * ksub * sub, wst);
+    }
+    // Encode (:99-107)
+    DevMem codes_rm;
+    codes_rm.ensure((size_t)n * M);
+    launch_pq_encode(X.as<float>(), A.as<int32_t>(), C.as<float>(), n, dim, M, ksub, cb.as<float>(),
+                     codes_rm.as<uint8_t>(), wst);
+    std::vector<int32_t> asg(n);
+    HIPCHK(hipMemcpyAsync(asg.data(), A.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, wst));
+    HIPCHK(hipStreamSynchronize(wst));
+    std::vector<int32_t> cnt(nc, 0);
+    for (int32_t a : asg) cnt[a]++;
+    lb.assign(nc, 0);
+    le.assign(nc, 0);
+    llen = cnt;
+    int64_t tot = 0;
+    for (int l = 0; l < nc; l++) {
+      lb[l] = (int32_t)tot;
+      le[l] = (int32_t)(tot + cnt[l]);
+      tot += round_up(cnt[l], 64);
+    }
+    std::vector<int64_t> src(tot, -1);
+    hlabels.assign(tot, -1);
+    std::vector<int32_t> fillp(lb);
+    for (int64_t i = 0; i < n; i++) {
+      const int32_t p = fillp[asg[i]]++;
+      src[p] = i;
+      hlabels[p] = labs[i];
+    }
+    const int nch = (M + 15) / 16;
+    codes.ensure((size_t)std::max<int64_t>(tot, 64) * nch * 16);
+    DevMem dsrc;
+    dsrc.ensure(sizeof(int64_t) * std::max<int64_t>(tot, 1));
+    HIPCHK(hipMemcpyAsync(dsrc.p, src.data(), sizeof(int64_t) * tot, hipMemcpyHostToDevice, wst));
+    launch_pack_codes(codes_rm.as<uint8_t>(), dsrc.as<int64_t>(), tot, M, codes.as<uint8_t>(), wst);
+    hlive.assign(tot, 0);
+    for (int64_t p = 0; p < tot; p++) hlive[p] = src[p] >= 0;
+    clive.ensure(std::max<int64_t>(tot, 1));
+    clabels.ensure(sizeof(int64_t) * std::max<int64_t>(tot, 1));
+    HIPCHK(hipMemcpyAsync(clive.p, hlive.data(), tot, hipMemcpyHostToDevice, wst));
+    HIPCHK(hipMemcpyAsync(clabels.p, hlabels.data(), sizeof(int64_t) * tot, hipMemcpyHostToDevice, wst));
+    ncode_rows = tot;
+    pos_of.clear();
+    for (int64_t p = 0; p < tot; p++)
+      if (hlabels[p] >= 0) pos_of[hlabels[p]] = p;
+    coarse.set(C.as<float>(), nc, dim, metric, wst);
+    dlb.ensure(sizeof(int32_t) * nc);
+    dle.ensure(sizeof(int32_t) * nc);
+    HIPCHK(hipMemcpyAsync(dlb.p, lb.data(), sizeof(int32_t) * nc, hipMemcpyHostToDevice, wst));
+    HIPCHK(hipMemcpyAsync(dle.p, le.data(), sizeof(int32_t) * nc, hipMemcpyHostToDevice, wst));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(wst));
+    buf.clear(wst);                                    // :109
+    built = true;
+  }
+
+  void search(const float *d_q, int64_t nq, int k, const pyr_search_params &prm, float *d_s, int64_t *d_l,
+              int32_t *d_c, Workspace &ws) override {  // :118-212 (MaxScans ignored)
+    if (k <= 0 || nq == 0) {
+      fill_empty_results(d_s, d_l, d_c, nq, std::max(k, 0), ws.st);
+      return;
+    }
+    const int nprobe = prm.nprobe < 0 ? nprobe_default : prm.nprobe;
+    const int probes = (built && coarse.nlist > 0) ? std::max(0, std::min(nprobe, coarse.nlist)) : 0;
+    const int64_t bcut = buf.st.n;
+    ScanPlan bp;
+    if (buf.live_count() > 0) bp = plan_flat(bcut, nq, dim, k, MAX_PARTS - probes);
+    const int nparts = probes + bp.nchunks;
+    if (nparts > MAX_PARTS) throw Error(PYR_E_ARG, "nprobe too large");
+    if (nparts == 0) {
+      fill_empty_results(d_s, d_l, d_c, nq, k, ws.st);
+      return;
+    }
+    query_norms(d_q, nq, dim, metric, ws);
+    const float *qn = metric == COS ? ws.qn.as<float>() : nullptr;
+    const size_t np = (size_t)nq * nparts * k;
+    ws.part_s.ensure(sizeof(float) * np);
+    ws.part_k.ensure(sizeof(uint32_t) * np);
+    if (probes > 0) {
+      coarse.probe(d_q, qn, nq, probes, metric, ws);
+      const int qchunk = 32;
+      const int maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qchunk);
+      PqArgs a{};
+      a.codes = codes.as<uint8_t>();
+      a.live = clive.as<uint8_t>();
+      a.queries = d_q;
+      a.cents = coarse.rm.as<float>();
+      a.codebooks = cb.as<float>();
+      a.probes = ws.probes.as<int32_t>();
+      a.list_begin = dlb.as<int32_t>();
+      a.list_end = dle.as<int32_t>();
+      a.items = ws.items.as<ScanItem>();
+      a.n_items = ws.nitems.as<int32_t>();
+      a.qlist = ws.qlist.as<int32_t>();
+      a.nparts = nparts;
+      a.nprobe = probes;
+      a.k = k;
+      a.dim = dim;
+      a.M = M;
+      a.ksub = ksub;
+      a.part_s = ws.part_s.as<float>();
+      a.part_k = ws.part_k.as<uint32_t>();
+      if (pq_scan_lds_bytes(dim, M, ksub, k) > 160 * 1024) throw Error(PYR_E_ARG, "PQ lookup table exceeds LDS");
+      launch_pq_scan(a, maxi, ws.st);
+    }
+    if (bp.nchunks > 0)  // :130-136 exact buffer scan
+      flat_scan(buf.st, bcut, bp, d_q, qn, nq, k, 1, metric, nparts, probes, KEY_BUF, ws, ws.part_s.as<float>(),
+                ws.part_k.as<uint32_t>(), true);
+    launch_merge_keys(ws.part_s.as<float>(), ws.part_k.as<uint32_t>(), nq, nparts, k, clabels.as<int64_t>(),
+                      buf.st.labels.as<int64_t>(), d_s, d_l, nullptr, d_c, ws.st);
+  }
+
+  int64_t count() const override { return 0; }  // :230 GetStats quirk
+
+  void ivf_layout(int64_t *off, int64_t *labels, uint8_t *live, int64_t *total) const override {
+    int64_t t = 0;
+    for (int l = 0; l < coarse.nlist && built; l++) {
+      if (off) off[l] = t;
+      for (int32_t p = lb[l]; p < lb[l] + llen[l]; p++, t++) {
+        if (labels) labels[t] = hlabels[p];
+        if (live) live[t] = hlive[p];
+      }
+    }
+    if (off && built) off[coarse.nlist] = t;
+    *total = t;
+  }
+
+  void pq_state(float *out_cb, int32_t *out_ksub, uint8_t *out_codes) const override {
+    if (out_ksub) *out_ksub = built ? ksub : 0;
+    if (!built) return;
+    if (out_cb) HIPCHK(hipMemcpy(out_cb, cb.p, sizeof(float) * (size_t)M * ksub * sub, hipMemcpyDeviceToHost));
+    if (out_codes) {
+      const int nch = (M + 15) / 16;
+      std::vector<uint8_t> blk((size_t)ncode_rows * nch * 16);
+      HIPCHK(hipMemcpy(blk.data(), codes.p, blk.size(), hipMemcpyDeviceToHost));
+      int64_t t = 0;
+      for (int l = 0; l < coarse.nlist; l++)
+        for (int32_t p = lb[l]; p < lb[l] + llen[l]; p++, t++)
+          for (int m = 0; m < M; m++)
+            out_codes[t * M + m] = blk[(((size_t)(p >> 6) * nch + (m >> 4)) * 64 + (p & 63)) * 16 + (m & 15)];
+    }
+  }
+
+  void centroids(float *out, int32_t *nl) const override {
+    *nl = built ? coarse.nlist : 0;
+    if (out && built) std::memcpy(out, coarse.host.data(), sizeof(float) * coarse.host.size());
+  }
+};
+
+Index *create_index(const pyr_index_desc &d) {
+  if (d.dim <= 0) throw Error(PYR_E_ARG, "Dimension must be positive.");  // BruteForceVectorIndex.cs:43-46
+  if (d.metric < 0 || d.metric > 2) throw Error(PYR_E_ARG, "unknown metric");
+  switch (d.kind) {
+    case PYR_FLAT: return new FlatIndex(d);
+    case PYR_IVF_FLAT: return new IvfFlatIndex(d);
+    case PYR_IVF_PQ: return new IvfPqIndex(d);
+    default: throw Error(PYR_E_ARG, "unknown index kind");
+  }
+}
+
+}  // namespace pyr

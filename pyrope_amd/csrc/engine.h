@@ -1,0 +1,162 @@
+// engine.h -- host runtime of libpyrope_hip.so: device-resident index objects
+// restating the reference's IVectorIndex implementations
+// (src/Pyrope.GarnetServer/Vector/{BruteForce,IvfFlat,IvfPq}VectorIndex.cs).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <shared_mutex>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/pyrope_ann.h"
+#include "kernels.h"
+
+namespace pyr {
+
+struct Error : std::runtime_error {
+  pyr_status status;
+  Error(pyr_status s, const std::string &m) : std::runtime_error(m), status(s) {}
+};
+
+#define HIPCHK(x)                                                                                   \
+  do {                                                                                              \
+    hipError_t e_ = (x);                                                                            \
+    if (e_ != hipSuccess)                                                                           \
+      throw ::pyr::Error(PYR_E_DEVICE, std::string(#x " failed: ") + hipGetErrorString(e_));        \
+  } while (0)
+
+// device allocation that only grows
+struct DevMem {
+  void *p = nullptr;
+  size_t n = 0;
+  DevMem() = default;
+  DevMem(const DevMem &) = delete;
+  DevMem &operator=(const DevMem &) = delete;
+  ~DevMem() {
+    if (p) (void)hipFree(p);
+  }
+  // make room for `bytes`; content discarded
+  void ensure(size_t bytes);
+  // make room for `bytes`; first `keep` bytes preserved (stream-ordered copy, then sync)
+  void grow_keep(size_t bytes, size_t keep, hipStream_t st);
+  template <class T>
+  T *as() const {
+    return reinterpret_cast<T *>(p);
+  }
+};
+
+// Blocked fp32 row store on device (+ host mirrors of labels and visibility).
+struct RowStore {
+  int dim = 0;
+  bool cosine = false;
+  int64_t n = 0;    // slots in use
+  int64_t cap = 0;  // allocated slots (multiple of 8)
+  DevMem rows, norms, live, labels;
+  std::vector<int64_t> hlabels;
+  std::vector<uint8_t> hlive;
+  void reserve(int64_t slots, hipStream_t st);
+  // write rows (host row-major x, n rows) into slots; updates labels/live/norms
+  void write(const float *x, const int64_t *slots, const int64_t *labs, int64_t cnt, hipStream_t st,
+             DevMem &stage_x, DevMem &stage_i);
+  void set_live(const std::vector<int64_t> &slots, uint8_t v, hipStream_t st, DevMem &stage);
+  void clear() {
+    n = 0;
+    hlabels.clear();
+    hlive.clear();
+  }
+};
+
+struct Workspace {
+  hipStream_t st = nullptr;
+  bool own_stream = false;
+  std::mutex m;
+  DevMem q, qn, items, nitems, items2, nitems2, qlist, part_s, part_k, probes, cpart_s, cpart_k, limits;
+  DevMem ivf_cnt, ivf_fill, ivf_qoff, ivf_ioff;
+  DevMem out_s, out_l, out_c;
+  ~Workspace() {
+    if (own_stream && st) (void)hipStreamDestroy(st);
+  }
+};
+
+struct Index {
+  pyr_index_desc desc{};
+  int dim = 0, metric = 0, device = 0;
+  mutable std::shared_mutex mu;
+  hipStream_t wst = nullptr;  // stream for writes/builds
+  DevMem stage_x, stage_i, stage_b;
+  std::mutex ws_mu;
+  std::vector<std::unique_ptr<Workspace>> free_ws;
+  std::map<hipStream_t, std::unique_ptr<Workspace>> stream_ws;
+
+  explicit Index(const pyr_index_desc &d);
+  virtual ~Index();
+  virtual void add(const float *x, int64_t n, const int64_t *labels, bool upsert) = 0;
+  virtual void remove(const int64_t *labels, int64_t n, uint8_t *removed) = 0;
+  virtual void build() {}
+  // enqueue a batch search of device queries on ws.st; outputs device buffers
+  virtual void search(const float *d_q, int64_t nq, int k, const pyr_search_params &p, float *d_s, int64_t *d_l,
+                      int32_t *d_c, Workspace &ws) = 0;
+  virtual int64_t count() const = 0;
+  virtual void centroids(float *out, int32_t *nlist) const {
+    (void)out;
+    *nlist = 0;
+  }
+  virtual void ivf_layout(int64_t *off, int64_t *labels, uint8_t *live, int64_t *total) const;
+  virtual void pq_state(float *cb, int32_t *ksub, uint8_t *codes) const;
+
+  std::unique_ptr<Workspace> take_ws();
+  void give_ws(std::unique_ptr<Workspace> w);
+  Workspace &ws_for_stream(hipStream_t st);
+};
+
+struct NetRandom {  // System.Random legacy (Net5CompatSeedImpl); SURVEY.md Appendix A
+  int32_t sa[56];
+  int32_t inext = 0, inextp = 21;
+  explicit NetRandom(int32_t seed) {
+    const int32_t MBIG = INT32_MAX;
+    int32_t sub = seed == INT32_MIN ? INT32_MAX : (seed < 0 ? -seed : seed);
+    int32_t mj = 161803398 - sub, mk = 1;
+    sa[55] = mj;
+    for (int i = 1; i < 55; i++) {
+      int ii = (21 * i) % 55;
+      sa[ii] = mk;
+      mk = mj - mk;
+      if (mk < 0) mk += MBIG;
+      mj = sa[ii];
+    }
+    for (int p = 1; p < 5; p++)
+      for (int i = 1; i < 56; i++) {
+        sa[i] -= sa[1 + (i + 30) % 55];
+        if (sa[i] < 0) sa[i] += MBIG;
+      }
+  }
+  int32_t next() {
+    if (++inext >= 56) inext = 1;
+    if (++inextp >= 56) inextp = 1;
+    int32_t r = sa[inext] - sa[inextp];
+    if (r == INT32_MAX) r--;
+    if (r < 0) r += INT32_MAX;
+    sa[inext] = r;
+    return r;
+  }
+  double next_double() { return next() * (1.0 / INT32_MAX); }
+};
+
+Index *create_index(const pyr_index_desc &d);
+
+// shared building blocks
+void fill_empty_results(float *d_s, int64_t *d_l, int32_t *d_c, int64_t nq, int k, hipStream_t st);
+// KMeansUtils.Train on the GPU: reference-identical init and Lloyd iterations.
+int kmeans_train_gpu(const float *d_x, int64_t n, int dim, int k, int metric, int max_iter, int seed,
+                     float *d_cents /* k x dim */, hipStream_t st);
+// KMeansUtils.FindNearestCentroid for every row (ties -> lowest index)
+void assign_gpu(const float *d_x, int64_t n, int dim, const float *d_cents, int k, int metric, int32_t *d_assign,
+                hipStream_t st);
+
+}  // namespace pyr

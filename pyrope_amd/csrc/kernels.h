@@ -1,0 +1,152 @@
+// kernels.h -- host-side launchers for the gfx950 kernels in kernels.hip.
+// Internal to libpyrope_hip.so (the public boundary is include/pyrope_ann.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pyr {
+
+enum Metric { L2 = 0, IP = 1, COS = 2 };
+
+constexpr uint32_t KEY_NONE = 0xFFFFFFFFu;
+constexpr uint32_t KEY_BUF = 0x80000000u;  // buffer rows: KEY_BUF | slot (DESIGN.md "Tie rule")
+constexpr int QCHUNK = 128;                // queries per scan work item (fast kernel)
+constexpr int QCHUNK_GENERIC = 64;         // queries per scan work item (generic kernel)
+constexpr int KMAX_FAST = 64;              // largest k served by the fast kernel
+constexpr int KMAX = 256;                  // largest k served at all
+constexpr int MAX_PARTS = 1024;            // partial lists merged per query
+
+// A scan work item: rows [row_begin, row_end) of a blocked row store against up to
+// QCHUNK queries.  If the launch has a qlist, the queries' partial slots are
+// qlist[qbeg .. qbeg+qcnt); otherwise query = qbeg + i and slot = query * nparts + part.
+struct ScanItem {
+  int32_t row_begin;  // multiple of 8
+  int32_t row_end;
+  int32_t qbeg;
+  int32_t qcnt;
+  int32_t part;
+  int32_t list;  // IVF: list id of the item
+};
+
+struct ScanArgs {
+  const float *rows;      // blocked [row/8][D][8]
+  const uint8_t *live;    // per row, 1 = visible
+  const float *rnorm;     // per row norms (cosine) or null
+  const float *queries;   // row-major nq x D
+  const float *qnorm;     // per query norms (cosine) or null
+  const ScanItem *items;
+  const int32_t *n_items; // device count (items beyond it exit)
+  const int32_t *qlist;   // partial-slot ids or null
+  const uint32_t *limits; // per partial slot exclusive row bound (max_scans), or null
+  int32_t nparts;         // partial slots per query
+  int32_t k;
+  uint32_t key_base;      // OR-ed into row index to form the storage key
+  int32_t dim;
+  float *part_s;          // [slot][k] scores
+  uint32_t *part_k;       // [slot][k] keys
+};
+
+// V = 1: VectorMath safe functions (one Vector accumulator; IVF paths, k-means).
+// V = 4: VectorMath *Unsafe functions (four accumulators; BruteForce head).
+void launch_scan(const ScanArgs &a, int metric, int V, int max_items, hipStream_t st);
+
+// FLAT-style items: rows [0, nrows) in chunks of chunk_rows x queries [0,nq) in QCHUNK blocks.
+// Returns item count (also written to *d_nitems).
+int make_flat_items(ScanItem *d_items, int32_t *d_nitems, int64_t nrows, int32_t chunk_rows, int64_t nq,
+                    int32_t part_off, int32_t qchunk, hipStream_t st);
+
+// Per-row / per-query norms (VectorMath.ComputeNorm).  blocked != 0: rows in blocked layout.
+void launch_norms(const float *x, int64_t n, int32_t dim, int blocked, float *out, hipStream_t st);
+
+// Merge nparts sorted partial lists per query into top-k.
+// keys are uint32 storage keys; labels mapped through row_labels / buf_labels when given.
+void launch_merge_keys(const float *ps, const uint32_t *pk, int64_t nq, int32_t nparts, int32_t k,
+                       const int64_t *row_labels, const int64_t *buf_labels, float *out_s, int64_t *out_l,
+                       int32_t *out_keys, int32_t *out_cnt, hipStream_t st);
+// Merge partial lists that carry int64 labels (multi-GPU), ties by label asc.
+void launch_merge_labels(const float *ps, const int64_t *pl, int64_t nq, int32_t nparts, int32_t k, float *out_s,
+                         int64_t *out_l, hipStream_t st);
+
+// IVF: from probes [nq][nprobe] build list-major work items.
+struct IvfItemWs {
+  int32_t *cnt;       // nlist
+  int32_t *fill;      // nlist
+  int32_t *qoff;      // nlist + 1
+  int32_t *ioff;      // nlist + 1
+  int32_t *qlist;     // nq * nprobe
+  ScanItem *items;    // max_items
+  int32_t *n_items;   // 1
+};
+int ivf_max_items(int64_t nq, int32_t nprobe, int32_t nlist, int32_t qchunk);
+void launch_ivf_items(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t nparts, int32_t nlist,
+                      const int32_t *list_begin, const int32_t *list_end, int32_t qchunk, IvfItemWs &ws,
+                      hipStream_t st);
+// IVF max_scans limits per (query, probe) slot (IvfFlatVectorIndex.cs:200-212)
+void launch_ivf_limits(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t nparts, int64_t remaining,
+                       const int32_t *list_begin, const int32_t *list_end, const int32_t *list_live,
+                       const uint8_t *live, uint32_t *limits, hipStream_t st);
+
+// IVF-PQ ADC scan (IvfPqVectorIndex.cs:152-198).
+struct PqArgs {
+  const uint8_t *codes;    // blocked codes, see kernels.hip
+  const uint8_t *live;
+  const float *queries;    // nq x D
+  const float *cents;      // nlist x D row-major
+  const float *codebooks;  // [M][ksub][sub]
+  const int32_t *probes;   // [nq][nprobe]
+  const int32_t *list_begin, *list_end;
+  const ScanItem *items;
+  const int32_t *n_items;
+  const int32_t *qlist;
+  int32_t nparts, nprobe, k, dim, M, ksub;
+  float *part_s;
+  uint32_t *part_k;
+};
+void launch_pq_scan(const PqArgs &a, int max_items, hipStream_t st);
+size_t pq_scan_lds_bytes(int dim, int M, int ksub, int k);
+// PQ encode (ProductQuantizer.Encode on residuals x - c[assign]) -> codes n x M row-major.
+void launch_pq_encode(const float *x, const int32_t *assign, const float *cents, int64_t n, int32_t dim, int32_t M,
+                      int32_t ksub, const float *codebooks, uint8_t *codes, hipStream_t st);
+// residuals r = x - c[assign] (IvfPqVectorIndex.cs:82-84)
+void launch_residuals(const float *x, const int32_t *assign, const float *cents, int64_t n, int32_t dim, float *out,
+                      hipStream_t st);
+// sub-vector extraction for per-subspace k-means (ProductQuantizer.cs:39-45)
+void launch_extract_sub(const float *x, int64_t n, int32_t dim, int32_t off, int32_t sub, float *out, hipStream_t st);
+// codes (row-major n x M, rows in perm order) -> blocked list storage
+void launch_pack_codes(const uint8_t *codes, const int64_t *src_of_dst, int64_t ndst, int32_t M, uint8_t *out,
+                       hipStream_t st);
+
+// layout helpers
+// dst blocked rows [dst_row0 ...] from row-major src rows (src_idx[i] or i when null)
+void launch_to_blocked(const float *src, const int64_t *src_idx, int64_t n, int32_t dim, float *dst, int64_t dst_row0,
+                       hipStream_t st);
+// scattered writes: row i of src (row-major) -> blocked slot dst_slots[i]
+void launch_scatter_blocked(const float *src, const int64_t *dst_slots, int64_t n, int32_t dim, float *dst,
+                            hipStream_t st);
+// gather blocked rows (src_slot[i]) into row-major out
+void launch_gather_blocked(const float *src, const int64_t *src_slots, int64_t n, int32_t dim, float *out,
+                           hipStream_t st);
+// gather rows from two blocked stores: idx >= 0 -> store A row idx, idx < 0 -> store B row (-idx-1)
+void launch_gather2(const float *A, const float *B, const int64_t *idx, int64_t n, int32_t dim, float *out,
+                    hipStream_t st);
+void launch_gather_rows(const float *src, const int32_t *idx, int64_t n, int32_t dim, float *out, hipStream_t st);
+
+// k-means helpers (KMeansUtils.cs:40-62)
+void launch_keys_to_assign(const uint32_t *keys, int64_t n, int32_t *assign, hipStream_t st);
+void launch_kmeans_update(const float *data, const int32_t *members, const int32_t *coff, int32_t k, int32_t dim,
+                          float *cents, float *tmp, int32_t *flags, int32_t *changed, hipStream_t st);
+// stable counting sort of [0,n) by key in [0,k): members and offsets (hipCUB radix sort)
+size_t sort_temp_bytes(int64_t n, int32_t k);
+void sort_by_key(const int32_t *keys, int64_t n, int32_t k, int32_t *keys_tmp, int32_t *idx_in, int32_t *members,
+                 int32_t *counts, int32_t *coff, void *temp, size_t temp_bytes, hipStream_t st);
+
+void fill_u8(uint8_t *p, uint8_t v, int64_t n, hipStream_t st);
+void launch_scatter_i64(int64_t *dst, const int64_t *idx, const int64_t *vals, int64_t n, hipStream_t st);
+void launch_scatter_u8(uint8_t *dst, const int64_t *idx, uint8_t v, int64_t n, hipStream_t st);
+// norms of blocked rows at the given slots (VectorMath.ComputeNorm)
+void launch_norms_slots(const float *rows, const int64_t *slots, int64_t n, int32_t dim, float *out, hipStream_t st);
+// empty result rows: score -inf, label -1, count 0
+void launch_fill_results(float *s, int64_t *l, int32_t *c, int64_t nq, int32_t k, hipStream_t st);
+bool fast_path(int dim, int k);
+
+}  // namespace pyr

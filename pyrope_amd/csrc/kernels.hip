@@ -1,0 +1,1247 @@
+// kernels.hip -- gfx950 (CDNA4) kernels of the Pyrope ANN scan hot path.
+//
+// Parity contract: every score is computed with the SAME fp32 operation order
+// as the reference C# SIMD engine (src/Pyrope.GarnetServer/Vector/VectorMath.cs),
+// restated for x64 AVX2 RyuJIT: 8 fp32 lanes, mul and add rounded separately
+// (no contraction: this file is compiled with -ffp-contract=off and the pragma
+// below), horizontal sum ((v0+v1)+(v2+v3))+((v4+v5)+(v6+v7)).  Scores are
+// therefore bit-identical to the CPU oracle (oracle/oracle.c), not just close.
+//
+// Row storage is "blocked": groups of 8 rows stored dim-major, element
+// (row r, dim d) at ((r/8)*D + d)*8 + r%8.  One group of D=128 rows is 4 KiB
+// contiguous, read by one wave instruction per 1 KiB.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cfloat>
+#include <cmath>
+
+#include "kernels.h"
+
+namespace pyr {
+namespace {
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+constexpr int SCS = 132;  // score-matrix row stride (floats): conflict-free float4 stores
+
+__device__ __forceinline__ bool better(float s1, uint32_t k1, float s2, uint32_t k2) {
+  return s1 > s2 || (s1 == s2 && k1 < k2);
+}
+__device__ __forceinline__ bool better64(float s1, int64_t k1, float s2, int64_t k2) {
+  return s1 > s2 || (s1 == s2 && k1 < k2);
+}
+
+__device__ __forceinline__ size_t blk_off(int64_t r, int d, int D) {
+  return ((size_t)(r >> 3) * (size_t)D + (size_t)d) * 8 + (size_t)(r & 7);
+}
+
+// ---------------------------------------------------------------------------
+// Exact restatements of VectorMath.cs on accessors (generic dims).
+// ---------------------------------------------------------------------------
+struct Lin {
+  const float *p;
+  __device__ float operator()(int i) const { return p[i]; }
+};
+struct Blk {
+  const float *base;
+  int D;
+  int64_t r;
+  __device__ float operator()(int i) const { return base[blk_off(r, i, D)]; }
+};
+struct Off {  // sub-range accessor
+  const float *p;
+  __device__ float operator()(int i) const { return p[i]; }
+};
+
+__device__ __forceinline__ float hsum8(const float *v) {
+  float lo = (v[0] + v[1]) + (v[2] + v[3]);
+  float hi = (v[4] + v[5]) + (v[6] + v[7]);
+  return lo + hi;
+}
+
+// VectorMath.cs:8-37 DotProduct
+template <class A, class B>
+__device__ float em_dot(A a, B b, int n) {
+  int i = 0;
+  float sum = 0.0f;
+  if (n >= 8) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (; i <= n - 8; i += 8)
+#pragma unroll
+      for (int l = 0; l < 8; l++) acc[l] = acc[l] + a(i + l) * b(i + l);
+    sum = sum + hsum8(acc);
+  }
+  for (; i < n; i++) sum = sum + a(i) * b(i);
+  return sum;
+}
+// VectorMath.cs:39-70 L2Squared
+template <class A, class B>
+__device__ float em_l2sq(A a, B b, int n) {
+  int i = 0;
+  float sum = 0.0f;
+  if (n >= 8) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (; i <= n - 8; i += 8)
+#pragma unroll
+      for (int l = 0; l < 8; l++) {
+        float d = a(i + l) - b(i + l);
+        acc[l] = acc[l] + d * d;
+      }
+    sum = sum + hsum8(acc);
+  }
+  for (; i < n; i++) {
+    float d = a(i) - b(i);
+    sum = sum + d * d;
+  }
+  return sum;
+}
+// VectorMath.cs:72-100 ComputeNorm
+template <class A>
+__device__ float em_norm(A a, int n) {
+  int i = 0;
+  float sum = 0.0f;
+  if (n >= 8) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (; i <= n - 8; i += 8)
+#pragma unroll
+      for (int l = 0; l < 8; l++) acc[l] = acc[l] + a(i + l) * a(i + l);
+    sum = sum + hsum8(acc);
+  }
+  for (; i < n; i++) sum = sum + a(i) * a(i);
+  return sqrtf(sum);
+}
+// VectorMath.cs:128-186 DotProductUnsafe
+template <class A, class B>
+__device__ float em_dot_unsafe(A a, B b, int n) {
+  int i = 0;
+  float sum = 0.0f;
+  if (n >= 32) {
+    float a1[8] = {0}, a2[8] = {0}, a3[8] = {0}, a4[8] = {0}, fin[8];
+    for (; i <= n - 32; i += 32)
+#pragma unroll
+      for (int l = 0; l < 8; l++) {
+        a1[l] = a1[l] + a(i + l) * b(i + l);
+        a2[l] = a2[l] + a(i + 8 + l) * b(i + 8 + l);
+        a3[l] = a3[l] + a(i + 16 + l) * b(i + 16 + l);
+        a4[l] = a4[l] + a(i + 24 + l) * b(i + 24 + l);
+      }
+#pragma unroll
+    for (int l = 0; l < 8; l++) fin[l] = ((a1[l] + a2[l]) + a3[l]) + a4[l];
+    sum = sum + hsum8(fin);
+  }
+  if (i <= n - 8) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (; i <= n - 8; i += 8)
+#pragma unroll
+      for (int l = 0; l < 8; l++) acc[l] = acc[l] + a(i + l) * b(i + l);
+    sum = sum + hsum8(acc);
+  }
+  for (; i < n; i++) sum = sum + a(i) * b(i);
+  return sum;
+}
+// VectorMath.cs:188-253 L2SquaredUnsafe
+template <class A, class B>
+__device__ float em_l2sq_unsafe(A a, B b, int n) {
+  int i = 0;
+  float sum = 0.0f;
+  if (n >= 32) {
+    float a1[8] = {0}, a2[8] = {0}, a3[8] = {0}, a4[8] = {0}, fin[8];
+    for (; i <= n - 32; i += 32)
+#pragma unroll
+      for (int l = 0; l < 8; l++) {
+        float d1 = a(i + l) - b(i + l);
+        float d2 = a(i + 8 + l) - b(i + 8 + l);
+        float d3 = a(i + 16 + l) - b(i + 16 + l);
+        float d4 = a(i + 24 + l) - b(i + 24 + l);
+        a1[l] = a1[l] + d1 * d1;
+        a2[l] = a2[l] + d2 * d2;
+        a3[l] = a3[l] + d3 * d3;
+        a4[l] = a4[l] + d4 * d4;
+      }
+#pragma unroll
+    for (int l = 0; l < 8; l++) fin[l] = ((a1[l] + a2[l]) + a3[l]) + a4[l];
+    sum = sum + hsum8(fin);
+  }
+  if (i <= n - 8) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (; i <= n - 8; i += 8)
+#pragma unroll
+      for (int l = 0; l < 8; l++) {
+        float d = a(i + l) - b(i + l);
+        acc[l] = acc[l] + d * d;
+      }
+    sum = sum + hsum8(acc);
+  }
+  for (; i < n; i++) {
+    float d = a(i) - b(i);
+    sum = sum + d * d;
+  }
+  return sum;
+}
+
+// score of one (query, row) pair with the reference's formula for the path:
+// V=4 -> BruteForceVectorIndex.cs:350-356 (Unsafe), V=1 -> IvfFlatVectorIndex.cs:351-360 (safe)
+template <int V, int MET, class A, class B>
+__device__ float em_score(A q, B x, int n, float qn, float xn) {
+  if (MET == L2) return V == 4 ? -em_l2sq_unsafe(q, x, n) : -em_l2sq(q, x, n);
+  if (MET == IP) return V == 4 ? em_dot_unsafe(q, x, n) : em_dot(q, x, n);
+  if (qn < 1e-6f || xn < 1e-6f) return 0.0f;
+  float d = V == 4 ? em_dot_unsafe(q, x, n) : em_dot(q, x, n);
+  return d / (qn * xn);
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+
+// insertion into a sorted (desc) top-k list: same semantics as oracle topk_push
+__device__ __forceinline__ void list_insert(float *ls, uint32_t *lk, int &cnt, int k, float s, uint32_t key) {
+  int n = cnt;
+  if (n == k) n = k - 1;
+  int j = n;
+  while (j > 0 && better(s, key, ls[j - 1], lk[j - 1])) {
+    ls[j] = ls[j - 1];
+    lk[j] = lk[j - 1];
+    j--;
+  }
+  ls[j] = s;
+  lk[j] = key;
+  cnt = n + 1;
+}
+
+// ---------------------------------------------------------------------------
+// Fast scan: D in {32,64,96,128}, k <= 64.
+// Workgroup = 256 threads = 32 "slots" x 8 lanes.  Slot s owns queries
+// 4s..4s+3 of the item (held in registers); lane l of a slot owns Vector<float>
+// lane l, i.e. dims l, l+8, l+16, ...  Rows stream through LDS one 8-row group
+// at a time (double buffered).  Per group each slot computes 4 x 8 pairs with
+// packed fp32 math (v_pk_add/mul_f32), then the 8 lanes of a slot combine their
+// partial sums with the reference's horizontal tree by a DPP transpose-reduce
+// (quad_perm xor1, quad_perm xor2, row_half_mirror), leaving each lane with the
+// 4 scores of one row.  Scores go to an LDS matrix; one owner thread per query
+// keeps that query's sorted top-k in LDS.
+// ---------------------------------------------------------------------------
+template <int D, int V, int MET>
+__global__ __launch_bounds__(256) void scan_fast(ScanArgs a) {
+  constexpr int T = D / 8;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  if ((int)blockIdx.x >= *a.n_items) return;
+  const ScanItem it = a.items[blockIdx.x];
+  const int k = a.k;
+  float *tile = smem;                  // [2][D*8]
+  float *sc = smem + 2 * D * 8;        // [2][8][SCS]
+  float *tks = sc + 2 * 8 * SCS;       // [QCHUNK][k]
+  uint32_t *tkk = (uint32_t *)(tks + QCHUNK * k);
+
+  const int tid = threadIdx.x;
+  const int l = tid & 7, s = tid >> 3;
+  const int c1 = (l ^ (l >> 2)) & 1, c2 = ((l >> 1) ^ (l >> 2)) & 1, c3 = (l >> 2) & 1;
+  const int myj = c1 | (c2 << 1) | (c3 << 2);
+  const bool wave_active = (tid >> 6) * 32 < it.qcnt;
+
+  float q[4][T];
+  float qn[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = s * 4 + u;
+    qn[u] = 0.0f;
+    if (i < it.qcnt) {
+      const int qi = a.qlist ? a.qlist[it.qbeg + i] / a.nparts : it.qbeg + i;
+      const float *qp = a.queries + (size_t)qi * D + l;
+#pragma unroll
+      for (int t = 0; t < T; ++t) q[u][t] = qp[8 * t];
+      if (MET == COS) qn[u] = a.qnorm[qi];
+    } else {
+#pragma unroll
+      for (int t = 0; t < T; ++t) q[u][t] = 0.0f;
+    }
+  }
+
+  const bool owner = tid < it.qcnt;
+  int oslot = 0;
+  uint32_t lim = 0xFFFFFFFFu;
+  if (owner) {
+    oslot = a.qlist ? a.qlist[it.qbeg + tid] : (it.qbeg + tid) * a.nparts + it.part;
+    if (a.limits) lim = a.limits[oslot];
+  }
+  int cnt = 0;
+  float thr_s = -INFINITY;
+  uint32_t thr_k = KEY_NONE;
+  float *ls = tks + tid * k;
+  uint32_t *lk = tkk + tid * k;
+
+  const int g0 = it.row_begin >> 3;
+  const int ng = ((it.row_end + 7) >> 3) - g0;
+  const float4 *src = reinterpret_cast<const float4 *>(a.rows);
+  constexpr int NV = D * 2;  // float4 per group
+  float4 pf;
+  if (ng > 0) {
+    if (tid < NV) reinterpret_cast<float4 *>(tile)[tid] = src[(size_t)g0 * NV + tid];
+  }
+  __syncthreads();
+
+  for (int n = 0; n < ng; ++n) {
+    const int cur = n & 1;
+    const bool more = n + 1 < ng;
+    if (more && tid < NV) pf = src[(size_t)(g0 + n + 1) * NV + tid];
+
+    if (wave_active) {
+      const float *tp = tile + cur * D * 8 + l * 8;
+      float fin[4][8];
+      if constexpr (V == 1) {
+        f2 acc[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int jp = 0; jp < 4; ++jp) acc[u][jp] = f2{0.0f, 0.0f};
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+          const float4 x0 = *reinterpret_cast<const float4 *>(tp + t * 64);
+          const float4 x1 = *reinterpret_cast<const float4 *>(tp + t * 64 + 4);
+          const f2 xx[4] = {f2{x0.x, x0.y}, f2{x0.z, x0.w}, f2{x1.x, x1.y}, f2{x1.z, x1.w}};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const f2 qq = f2{q[u][t], q[u][t]};
+#pragma unroll
+            for (int jp = 0; jp < 4; ++jp) {
+              if constexpr (MET == L2) {
+                const f2 d = qq - xx[jp];
+                acc[u][jp] = acc[u][jp] + d * d;
+              } else {
+                acc[u][jp] = acc[u][jp] + qq * xx[jp];
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int jp = 0; jp < 4; ++jp) {
+            fin[u][2 * jp] = acc[u][jp].x;
+            fin[u][2 * jp + 1] = acc[u][jp].y;
+          }
+      } else {
+        // four Vector accumulators: acc[v] sums dims 32s + 8v + l (VectorMath.cs:197-221)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          f2 acc[4][4][2];
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc[v][u][0] = acc[v][u][1] = f2{0.0f, 0.0f};
+#pragma unroll
+          for (int t = 0; t < T; ++t) {
+            const int v = t & 3;
+            const float4 x0 = *reinterpret_cast<const float4 *>(tp + t * 64 + 4 * h);
+            const f2 xx[2] = {f2{x0.x, x0.y}, f2{x0.z, x0.w}};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const f2 qq = f2{q[u][t], q[u][t]};
+#pragma unroll
+              for (int jp = 0; jp < 2; ++jp) {
+                if constexpr (MET == L2) {
+                  const f2 d = qq - xx[jp];
+                  acc[v][u][jp] = acc[v][u][jp] + d * d;
+                } else {
+                  acc[v][u][jp] = acc[v][u][jp] + qq * xx[jp];
+                }
+              }
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int jp = 0; jp < 2; ++jp) {
+              const f2 f = ((acc[0][u][jp] + acc[1][u][jp]) + acc[2][u][jp]) + acc[3][u][jp];  // :224
+              fin[u][4 * h + 2 * jp] = f.x;
+              fin[u][4 * h + 2 * jp + 1] = f.y;
+            }
+        }
+      }
+      // transpose-reduce = Vector.Dot(acc, One) tree, one row per lane at the end
+      float r1[4][4], r2[4][2], r3[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int jp = 0; jp < 4; ++jp) {
+          const float x0 = fin[u][2 * jp], x1 = fin[u][2 * jp + 1];
+          const float keep = c1 ? x1 : x0, send = c1 ? x0 : x1;
+          r1[u][jp] = keep + dpp<0xB1>(send);
+        }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int jq = 0; jq < 2; ++jq) {
+          const float x0 = r1[u][2 * jq], x1 = r1[u][2 * jq + 1];
+          const float keep = c2 ? x1 : x0, send = c2 ? x0 : x1;
+          r2[u][jq] = keep + dpp<0x4E>(send);
+        }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float x0 = r2[u][0], x1 = r2[u][1];
+        const float keep = c3 ? x1 : x0, send = c3 ? x0 : x1;
+        r3[u] = keep + dpp<0x141>(send);
+      }
+      float sv[4];
+      float xn = 0.0f;
+      if (MET == COS) xn = a.rnorm[(size_t)(g0 + n) * 8 + myj];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float sum = 0.0f + r3[u];  // `sum += Vector.Dot(...)` with sum = 0f
+        if (MET == L2) sv[u] = -sum;
+        else if (MET == IP) sv[u] = sum;
+        else sv[u] = (qn[u] < 1e-6f || xn < 1e-6f) ? 0.0f : sum / (qn[u] * xn);
+      }
+      *reinterpret_cast<float4 *>(sc + cur * 8 * SCS + myj * SCS + s * 4) = make_float4(sv[0], sv[1], sv[2], sv[3]);
+    }
+    if (more && tid < NV) reinterpret_cast<float4 *>(tile + (cur ^ 1) * D * 8)[tid] = pf;
+    __syncthreads();
+
+    if (owner) {
+      const float *scp = sc + cur * 8 * SCS + tid;
+      const int rb = (g0 + n) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = rb + j;
+        const float v = scp[j * SCS];
+        const uint32_t key = a.key_base | (uint32_t)r;
+        if (r >= it.row_end || r < it.row_begin) continue;
+        if (cnt == k && !better(v, key, thr_s, thr_k)) continue;
+        if ((uint32_t)r >= lim || !a.live[r]) continue;
+        list_insert(ls, lk, cnt, k, v, key);
+        if (cnt == k) {
+          thr_s = ls[k - 1];
+          thr_k = lk[k - 1];
+        }
+      }
+    }
+  }
+  if (owner) {
+    float *ps = a.part_s + (size_t)oslot * k;
+    uint32_t *pk = a.part_k + (size_t)oslot * k;
+    for (int j = 0; j < k; ++j) {
+      ps[j] = j < cnt ? ls[j] : -INFINITY;
+      pk[j] = j < cnt ? lk[j] : KEY_NONE;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Generic scan: any D, k <= KMAX.  One thread per query, exact restatement.
+// ---------------------------------------------------------------------------
+template <int V, int MET>
+__global__ __launch_bounds__(64) void scan_generic(ScanArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  if ((int)blockIdx.x >= *a.n_items) return;
+  const ScanItem it = a.items[blockIdx.x];
+  const int tid = threadIdx.x, k = a.k, D = a.dim;
+  if (tid >= it.qcnt) return;
+  float *ls = smem + tid * k;
+  uint32_t *lk = reinterpret_cast<uint32_t *>(smem + 64 * k) + tid * k;
+  const int qi = a.qlist ? a.qlist[it.qbeg + tid] / a.nparts : it.qbeg + tid;
+  const int slot = a.qlist ? a.qlist[it.qbeg + tid] : qi * a.nparts + it.part;
+  const uint32_t lim = a.limits ? a.limits[slot] : 0xFFFFFFFFu;
+  const Lin qa{a.queries + (size_t)qi * D};
+  const float qn = MET == COS ? a.qnorm[qi] : 0.0f;
+  int cnt = 0;
+  for (int r = it.row_begin; r < it.row_end; ++r) {
+    if ((uint32_t)r >= lim) break;
+    if (!a.live[r]) continue;
+    const Blk xa{a.rows, D, r};
+    const float xn = MET == COS ? a.rnorm[r] : 0.0f;
+    const float v = em_score<V, MET>(qa, xa, D, qn, xn);
+    const uint32_t key = a.key_base | (uint32_t)r;
+    if (cnt == k && !better(v, key, ls[k - 1], lk[k - 1])) continue;
+    list_insert(ls, lk, cnt, k, v, key);
+  }
+  float *ps = a.part_s + (size_t)slot * k;
+  uint32_t *pk = a.part_k + (size_t)slot * k;
+  for (int j = 0; j < k; ++j) {
+    ps[j] = j < cnt ? ls[j] : -INFINITY;
+    pk[j] = j < cnt ? lk[j] : KEY_NONE;
+  }
+}
+
+__global__ void flat_items_kernel(ScanItem *items, int32_t *n_items, int nchunks, int nqc, int chunk_rows,
+                                  int64_t nrows, int64_t nq, int part_off, int qchunk) {
+  const int id = blockIdx.x * blockDim.x + threadIdx.x;
+  if (id == 0) *n_items = nchunks * nqc;
+  if (id >= nchunks * nqc) return;
+  const int c = id / nqc, qc = id % nqc;
+  ScanItem it;
+  it.row_begin = c * chunk_rows;
+  const int64_t e = (int64_t)(c + 1) * chunk_rows;
+  it.row_end = (int)(e < nrows ? e : nrows);
+  it.qbeg = qc * qchunk;
+  const int64_t qe = (int64_t)(qc + 1) * qchunk;
+  it.qcnt = (int)((qe < nq ? qe : nq) - it.qbeg);
+  it.part = part_off + c;
+  it.list = 0;
+  items[id] = it;
+}
+
+__global__ void norms_kernel(const float *x, int64_t n, int dim, int blocked, float *out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = blocked ? em_norm(Blk{x, dim, i}, dim) : em_norm(Lin{x + (size_t)i * dim}, dim);
+}
+
+// ---------------------------------------------------------------------------
+// Merge of sorted partial lists: one wave per query, k rounds of wave argmax.
+// ---------------------------------------------------------------------------
+constexpr int MERGE_U = MAX_PARTS / 64;  // parts per lane
+
+__global__ __launch_bounds__(256) void merge_keys_kernel(const float *ps, const uint32_t *pk, int64_t nq, int nparts,
+                                                         int k, const int64_t *row_labels, const int64_t *buf_labels,
+                                                         float *out_s, int64_t *out_l, int32_t *out_keys,
+                                                         int32_t *out_cnt) {
+  const int lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= nq) return;
+  int h[MERGE_U];
+  float cs[MERGE_U];
+  uint32_t ck[MERGE_U];
+  const size_t base = (size_t)q * nparts * k;
+#pragma unroll
+  for (int u = 0; u < MERGE_U; ++u) {
+    const int p = lane + 64 * u;
+    h[u] = 0;
+    if (p < nparts) {
+      cs[u] = ps[base + (size_t)p * k];
+      ck[u] = pk[base + (size_t)p * k];
+    } else {
+      cs[u] = -INFINITY;
+      ck[u] = KEY_NONE;
+    }
+  }
+  int produced = 0;
+  for (int r = 0; r < k; ++r) {
+    float bs = -INFINITY;
+    uint32_t bk = KEY_NONE;
+#pragma unroll
+    for (int u = 0; u < MERGE_U; ++u)
+      if (ck[u] != KEY_NONE && (bk == KEY_NONE || better(cs[u], ck[u], bs, bk))) {
+        bs = cs[u];
+        bk = ck[u];
+      }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const float os = __shfl_xor(bs, off);
+      const uint32_t ok = __shfl_xor(bk, off);
+      if (ok != KEY_NONE && (bk == KEY_NONE || better(os, ok, bs, bk))) {
+        bs = os;
+        bk = ok;
+      }
+    }
+    if (bk == KEY_NONE) break;
+    if (lane == 0) {
+      const size_t o = (size_t)q * k + r;
+      if (out_s) out_s[o] = bs;
+      if (out_keys) out_keys[o] = (int32_t)bk;
+      if (out_l) {
+        int64_t lab;
+        if (bk & KEY_BUF) lab = buf_labels ? buf_labels[bk & ~KEY_BUF] : (int64_t)(bk & ~KEY_BUF);
+        else lab = row_labels ? row_labels[bk] : (int64_t)bk;
+        out_l[o] = lab;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < MERGE_U; ++u)
+      if (ck[u] == bk) {  // keys are unique: exactly one lane/u advances
+        const int p = lane + 64 * u;
+        h[u]++;
+        if (h[u] < k) {
+          cs[u] = ps[base + (size_t)p * k + h[u]];
+          ck[u] = pk[base + (size_t)p * k + h[u]];
+        } else {
+          cs[u] = -INFINITY;
+          ck[u] = KEY_NONE;
+        }
+      }
+    produced++;
+  }
+  if (lane == 0) {
+    for (int r = produced; r < k; ++r) {
+      const size_t o = (size_t)q * k + r;
+      if (out_s) out_s[o] = -INFINITY;
+      if (out_keys) out_keys[o] = -1;
+      if (out_l) out_l[o] = -1;
+    }
+    if (out_cnt) out_cnt[q] = produced;
+  }
+}
+
+__global__ __launch_bounds__(256) void merge_labels_kernel(const float *ps, const int64_t *pl, int64_t nq, int nparts,
+                                                           int k, float *out_s, int64_t *out_l) {
+  const int lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= nq) return;
+  int h[MERGE_U];
+  float cs[MERGE_U];
+  int64_t cl[MERGE_U];
+  const size_t base = (size_t)q * nparts * k;
+#pragma unroll
+  for (int u = 0; u < MERGE_U; ++u) {
+    const int p = lane + 64 * u;
+    h[u] = 0;
+    cs[u] = p < nparts ? ps[base + (size_t)p * k] : -INFINITY;
+    cl[u] = p < nparts ? pl[base + (size_t)p * k] : -1;
+  }
+  int produced = 0;
+  for (int r = 0; r < k; ++r) {
+    float bs = -INFINITY;
+    int64_t bl = -1;
+#pragma unroll
+    for (int u = 0; u < MERGE_U; ++u)
+      if (cl[u] >= 0 && (bl < 0 || better64(cs[u], cl[u], bs, bl))) {
+        bs = cs[u];
+        bl = cl[u];
+      }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const float os = __shfl_xor(bs, off);
+      const int64_t ol = __shfl_xor(bl, off);
+      if (ol >= 0 && (bl < 0 || better64(os, ol, bs, bl))) {
+        bs = os;
+        bl = ol;
+      }
+    }
+    if (bl < 0) break;
+    if (lane == 0) {
+      out_s[(size_t)q * k + r] = bs;
+      out_l[(size_t)q * k + r] = bl;
+    }
+#pragma unroll
+    for (int u = 0; u < MERGE_U; ++u)
+      if (cl[u] == bl && cs[u] == bs) {
+        const int p = lane + 64 * u;
+        h[u]++;
+        cs[u] = h[u] < k ? ps[base + (size_t)p * k + h[u]] : -INFINITY;
+        cl[u] = h[u] < k ? pl[base + (size_t)p * k + h[u]] : -1;
+      }
+    produced++;
+  }
+  if (lane == 0)
+    for (int r = produced; r < k; ++r) {
+      out_s[(size_t)q * k + r] = -INFINITY;
+      out_l[(size_t)q * k + r] = -1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// IVF list-major work lists
+// ---------------------------------------------------------------------------
+__global__ void ivf_count_kernel(const int32_t *probes, int64_t n, int32_t *cnt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) atomicAdd(&cnt[probes[i]], 1);
+}
+
+// single workgroup: qoff = exclusive scan of cnt, ioff = exclusive scan of ceil(cnt/qchunk)
+__global__ __launch_bounds__(1024) void ivf_scan_kernel(const int32_t *cnt, int nlist, int qchunk, int32_t *qoff,
+                                                        int32_t *ioff, int32_t *n_items) {
+  __shared__ int sq[1024], si[1024];
+  const int tid = threadIdx.x;
+  const int per = (nlist + 1023) / 1024;
+  const int b = tid * per, e = min(nlist, b + per);
+  int lq = 0, li = 0;
+  for (int i = b; i < e; ++i) {
+    lq += cnt[i];
+    li += (cnt[i] + qchunk - 1) / qchunk;
+  }
+  sq[tid] = lq;
+  si[tid] = li;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const int vq = tid >= off ? sq[tid - off] : 0;
+    const int vi = tid >= off ? si[tid - off] : 0;
+    __syncthreads();
+    sq[tid] += vq;
+    si[tid] += vi;
+    __syncthreads();
+  }
+  int rq = sq[tid] - lq, ri = si[tid] - li;
+  for (int i = b; i < e; ++i) {
+    qoff[i] = rq;
+    ioff[i] = ri;
+    rq += cnt[i];
+    ri += (cnt[i] + qchunk - 1) / qchunk;
+  }
+  if (tid == 1023) {
+    qoff[nlist] = sq[1023];
+    ioff[nlist] = si[1023];
+    *n_items = si[1023];
+  }
+}
+
+__global__ void ivf_fill_kernel(const int32_t *probes, int64_t nq, int nprobe, int nparts, const int32_t *qoff,
+                                int32_t *fill, int32_t *qlist) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nq * nprobe) return;
+  const int64_t q = i / nprobe;
+  const int p = (int)(i % nprobe);
+  const int lst = probes[i];
+  const int pos = atomicAdd(&fill[lst], 1);
+  qlist[qoff[lst] + pos] = (int32_t)(q * nparts + p);
+}
+
+__global__ void ivf_items_kernel(const int32_t *cnt, const int32_t *qoff, const int32_t *ioff, int nlist,
+                                 const int32_t *lb, const int32_t *le, int qchunk, ScanItem *items) {
+  const int lst = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lst >= nlist) return;
+  const int c = cnt[lst];
+  int o = ioff[lst];
+  for (int b = 0; b < c; b += qchunk, ++o) {
+    ScanItem it;
+    it.row_begin = lb[lst];
+    it.row_end = le[lst];
+    it.qbeg = qoff[lst] + b;
+    it.qcnt = min(qchunk, c - b);
+    it.part = 0;
+    it.list = lst;
+    items[o] = it;
+  }
+}
+
+__global__ void ivf_limits_kernel(const int32_t *probes, int64_t nq, int nprobe, int nparts, int64_t remaining,
+                                  const int32_t *lb, const int32_t *le, const int32_t *llive, const uint8_t *live,
+                                  uint32_t *limits) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  int64_t rem = remaining;
+  for (int p = 0; p < nprobe; ++p) {
+    const int lst = probes[q * nprobe + p];
+    const size_t slot = (size_t)q * nparts + p;
+    if (rem <= 0) {
+      limits[slot] = (uint32_t)lb[lst];
+      continue;
+    }
+    if (rem >= llive[lst]) {
+      limits[slot] = (uint32_t)le[lst];
+      rem -= llive[lst];
+      continue;
+    }
+    int64_t c = 0;
+    int r = lb[lst];
+    for (; r < le[lst]; ++r)
+      if (live[r]) {
+        if (c == rem) break;
+        ++c;
+      }
+    limits[slot] = (uint32_t)r;
+    rem = 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// IVF-PQ: per (query, probed list) LUT in LDS + ADC scan over blocked codes.
+// Codes: lists padded to 64-row blocks; block b holds [ceil(M/16)][64 rows][16 B].
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ size_t pq_code_off(int64_t r, int chunk, int nch) {
+  return (((size_t)(r >> 6) * nch + chunk) * 64 + (size_t)(r & 63)) * 16;
+}
+
+__global__ __launch_bounds__(256) void pq_scan_kernel(PqArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  if ((int)blockIdx.x >= *a.n_items) return;
+  const ScanItem it = a.items[blockIdx.x];
+  const int D = a.dim, M = a.M, ksub = a.ksub, k = a.k, sub = D / M;
+  const int nch = (M + 15) / 16;
+  const int Dp = (D + 3) & ~3;
+  float *res = smem;
+  float *lut = res + Dp;
+  float *tks = lut + M * ksub;
+  uint32_t *tkk = reinterpret_cast<uint32_t *>(tks + k);
+  float *qs = reinterpret_cast<float *>(tkk + k);
+  uint32_t *qk = reinterpret_cast<uint32_t *>(qs + 256);
+  int *misc = reinterpret_cast<int *>(qk + 256);
+  const int tid = threadIdx.x;
+  const int lst = it.list;
+  const float *cent = a.cents + (size_t)lst * D;
+
+  for (int i = 0; i < it.qcnt; ++i) {
+    const int slot = a.qlist[it.qbeg + i];
+    const int qi = slot / a.nparts;
+    const float *qp = a.queries + (size_t)qi * D;
+    for (int d = tid; d < D; d += 256) res[d] = qp[d] - cent[d];  // IvfPqVectorIndex.cs:163
+    if (tid == 0) {
+      misc[0] = 0;
+      misc[1] = 0;
+    }
+    __syncthreads();
+    for (int e = tid; e < M * ksub; e += 256) {  // ProductQuantizer.cs:112-117
+      const int m = e / ksub, j = e - m * ksub;
+      lut[e] = em_l2sq_unsafe(Off{res + m * sub}, Off{a.codebooks + ((size_t)m * ksub + j) * sub}, sub);
+    }
+    __syncthreads();
+    for (int base = it.row_begin; base < it.row_end; base += 256) {
+      const int r = base + tid;
+      bool valid = r < it.row_end && a.live[r];
+      float score = 0.0f;
+      if (valid) {
+        float dist = 0.0f;  // IvfPqVectorIndex.cs:182-186, m order
+        for (int c = 0; c < nch; ++c) {
+          const uint4 w = *reinterpret_cast<const uint4 *>(a.codes + pq_code_off(r, c, nch));
+          const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+          for (int b = 0; b < 16; ++b) {
+            const int m = c * 16 + b;
+            if (m < M) dist = dist + lut[m * ksub + ((ws[b >> 2] >> (8 * (b & 3))) & 0xFF)];
+          }
+        }
+        score = -dist;  // :194
+      }
+      const int cnt = misc[1];
+      const uint32_t key = (uint32_t)r;
+      if (valid && (cnt < k || better(score, key, tks[k - 1], tkk[k - 1]))) {
+        const int idx = atomicAdd(&misc[0], 1);
+        qs[idx] = score;
+        qk[idx] = key;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        int c2 = misc[1];
+        const int nqd = misc[0];
+        for (int j = 0; j < nqd; ++j) {
+          if (c2 == k && !better(qs[j], qk[j], tks[k - 1], tkk[k - 1])) continue;
+          list_insert(tks, tkk, c2, k, qs[j], qk[j]);
+        }
+        misc[1] = c2;
+        misc[0] = 0;
+      }
+      __syncthreads();
+    }
+    const int cnt = misc[1];
+    for (int j = tid; j < k; j += 256) {
+      a.part_s[(size_t)slot * k + j] = j < cnt ? tks[j] : -INFINITY;
+      a.part_k[(size_t)slot * k + j] = j < cnt ? tkk[j] : KEY_NONE;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void pq_encode_kernel(const float *x, const int32_t *assign, const float *cents, int64_t n, int D, int M,
+                                 int ksub, const float *cb, uint8_t *codes) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * M) return;
+  const int64_t i = e / M;
+  const int m = (int)(e % M);
+  const int sub = D / M;
+  const float *xs = x + (size_t)i * D + (size_t)m * sub;
+  const float *cs = cents + (size_t)assign[i] * D + (size_t)m * sub;
+  struct R {
+    const float *x, *c;
+    __device__ float operator()(int d) const { return x[d] - c[d]; }
+  };
+  float mind = FLT_MAX;
+  int best = 0;
+  for (int j = 0; j < ksub; ++j) {  // ProductQuantizer.cs:124-134
+    const float d = em_l2sq_unsafe(R{xs, cs}, Off{cb + ((size_t)m * ksub + j) * sub}, sub);
+    if (d < mind) {
+      mind = d;
+      best = j;
+    }
+  }
+  codes[i * M + m] = (uint8_t)best;
+}
+
+__global__ void residuals_kernel(const float *x, const int32_t *assign, const float *cents, int64_t n, int D,
+                                 float *out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * D) return;
+  const int64_t i = e / D;
+  const int d = (int)(e % D);
+  out[e] = x[e] - cents[(size_t)assign[i] * D + d];
+}
+
+__global__ void extract_sub_kernel(const float *x, int64_t n, int D, int off, int sub, float *out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * sub) return;
+  const int64_t i = e / sub;
+  const int d = (int)(e % sub);
+  out[e] = x[(size_t)i * D + off + d];
+}
+
+__global__ void pack_codes_kernel(const uint8_t *codes, const int64_t *src, int64_t ndst, int M, uint8_t *out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int nch = (M + 15) / 16;
+  if (e >= ndst * nch * 16) return;
+  const int64_t r = e / (nch * 16);
+  const int m = (int)(e % (nch * 16));
+  const int64_t s = src[r];
+  const uint8_t v = (s >= 0 && m < M) ? codes[(size_t)s * M + m] : 0;
+  out[pq_code_off(r, m >> 4, nch) + (m & 15)] = v;
+}
+
+// ---------------------------------------------------------------------------
+// layout helpers
+// ---------------------------------------------------------------------------
+__global__ void to_blocked_kernel(const float *src, const int64_t *sidx, int64_t n, int D, float *dst, int64_t r0) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * D) return;
+  const int64_t i = e / D;
+  const int d = (int)(e % D);
+  const int64_t s = sidx ? sidx[i] : i;
+  dst[blk_off(r0 + i, d, D)] = s >= 0 ? src[(size_t)s * D + d] : 0.0f;
+}
+__global__ void scatter_blocked_kernel(const float *src, const int64_t *slots, int64_t n, int D, float *dst) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * D) return;
+  const int64_t i = e / D;
+  const int d = (int)(e % D);
+  dst[blk_off(slots[i], d, D)] = src[e];
+}
+__global__ void gather_blocked_kernel(const float *src, const int64_t *slots, int64_t n, int D, float *out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * D) return;
+  const int64_t i = e / D;
+  const int d = (int)(e % D);
+  out[e] = src[blk_off(slots[i], d, D)];
+}
+__global__ void gather2_kernel(const float *A, const float *B, const int64_t *idx, int64_t n, int D, float *out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * D) return;
+  const int64_t i = e / D;
+  const int d = (int)(e % D);
+  const int64_t s = idx[i];
+  out[e] = s >= 0 ? A[blk_off(s, d, D)] : B[blk_off(-s - 1, d, D)];
+}
+__global__ void gather_rows_kernel(const float *src, const int32_t *idx, int64_t n, int D, float *out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * D) return;
+  const int64_t i = e / D;
+  const int d = (int)(e % D);
+  out[e] = src[(size_t)idx[i] * D + d];
+}
+
+// ---------------------------------------------------------------------------
+// k-means (KMeansUtils.cs:40-62)
+// ---------------------------------------------------------------------------
+__global__ void keys_to_assign_kernel(const uint32_t *keys, int64_t n, int32_t *assign) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) assign[i] = (int32_t)keys[i];
+}
+
+// one thread per (cluster, dim): members summed in data order, then / Count.
+__global__ void kmeans_sum_kernel(const float *data, const int32_t *members, const int32_t *coff, int k, int D,
+                                  const float *cents, float *tmp, int32_t *flags) {
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = blockIdx.y;
+  if (d >= D || c >= k) return;
+  const int b = coff[c], e = coff[c + 1];
+  if (b == e) return;  // :48 empty cluster keeps its centroid
+  float s = 0.0f;
+  int i = b;
+  for (; i + 4 <= e; i += 4) {
+    const float v0 = data[(size_t)members[i] * D + d];
+    const float v1 = data[(size_t)members[i + 1] * D + d];
+    const float v2 = data[(size_t)members[i + 2] * D + d];
+    const float v3 = data[(size_t)members[i + 3] * D + d];
+    s = s + v0;
+    s = s + v1;
+    s = s + v2;
+    s = s + v3;
+  }
+  for (; i < e; ++i) s = s + data[(size_t)members[i] * D + d];
+  const float nc = s / (float)(e - b);  // :55 newC[d] /= Count
+  tmp[(size_t)c * D + d] = nc;
+  if ((double)fabsf(cents[(size_t)c * D + d] - nc) > 1e-6) flags[c] = 1;  // ArraysEqual :95-101
+}
+__global__ void kmeans_commit_kernel(float *cents, const float *tmp, const int32_t *flags, int k, int D,
+                                     int32_t *changed) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)k * D) return;
+  const int c = (int)(e / D);
+  if (flags[c]) {
+    cents[e] = tmp[e];
+    if (e % D == 0) atomicOr(changed, 1);
+  }
+}
+
+__global__ void iota_kernel(int32_t *p, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = (int32_t)i;
+}
+__global__ void hist_kernel(const int32_t *keys, int64_t n, int32_t *counts) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) atomicAdd(&counts[keys[i]], 1);
+}
+__global__ void fill_u8_kernel(uint8_t *p, uint8_t v, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+__global__ void scatter_i64_kernel(int64_t *dst, const int64_t *idx, const int64_t *vals, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[idx[i]] = vals[i];
+}
+__global__ void scatter_u8_kernel(uint8_t *dst, const int64_t *idx, uint8_t v, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[idx[i]] = v;
+}
+__global__ void norms_slots_kernel(const float *rows, const int64_t *slots, int64_t n, int dim, float *out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t r = slots[i];
+  out[r] = em_norm(Blk{rows, dim, r}, dim);
+}
+__global__ void fill_results_kernel(float *s, int64_t *l, int32_t *c, int64_t nq, int k) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nq * k) {
+    if (s) s[i] = -INFINITY;
+    if (l) l[i] = -1;
+  }
+  if (c && i < nq) c[i] = 0;
+}
+
+inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
+
+template <int D, int V, int MET>
+void launch_fast_t(const ScanArgs &a, int max_items, hipStream_t st) {
+  const size_t lds = (size_t)(2 * D * 8 + 2 * 8 * SCS + QCHUNK * a.k * 2) * sizeof(float);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&scan_fast<D, V, MET>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL((scan_fast<D, V, MET>), dim3(max_items), dim3(256), lds, st, a);
+}
+
+template <int V, int MET>
+void launch_generic_t(const ScanArgs &a, int max_items, hipStream_t st) {
+  const size_t lds = (size_t)64 * a.k * 8;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&scan_generic<V, MET>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL((scan_generic<V, MET>), dim3(max_items), dim3(64), lds, st, a);
+}
+
+template <int D, int V>
+void launch_fast_m(const ScanArgs &a, int metric, int max_items, hipStream_t st) {
+  if (metric == L2) launch_fast_t<D, V, L2>(a, max_items, st);
+  else if (metric == IP) launch_fast_t<D, V, IP>(a, max_items, st);
+  else launch_fast_t<D, V, COS>(a, max_items, st);
+}
+template <int D>
+void launch_fast_v(const ScanArgs &a, int metric, int V, int max_items, hipStream_t st) {
+  if (V == 4) launch_fast_m<D, 4>(a, metric, max_items, st);
+  else launch_fast_m<D, 1>(a, metric, max_items, st);
+}
+
+}  // namespace
+
+bool fast_path(int dim, int k) { return k <= KMAX_FAST && (dim == 32 || dim == 64 || dim == 96 || dim == 128); }
+
+void launch_scan(const ScanArgs &a, int metric, int V, int max_items, hipStream_t st) {
+  if (max_items <= 0) return;
+  if (fast_path(a.dim, a.k)) {
+    switch (a.dim) {
+      case 32: launch_fast_v<32>(a, metric, V, max_items, st); return;
+      case 64: launch_fast_v<64>(a, metric, V, max_items, st); return;
+      case 96: launch_fast_v<96>(a, metric, V, max_items, st); return;
+      default: launch_fast_v<128>(a, metric, V, max_items, st); return;
+    }
+  }
+  if (V == 4) {
+    if (metric == L2) launch_generic_t<4, L2>(a, max_items, st);
+    else if (metric == IP) launch_generic_t<4, IP>(a, max_items, st);
+    else launch_generic_t<4, COS>(a, max_items, st);
+  } else {
+    if (metric == L2) launch_generic_t<1, L2>(a, max_items, st);
+    else if (metric == IP) launch_generic_t<1, IP>(a, max_items, st);
+    else launch_generic_t<1, COS>(a, max_items, st);
+  }
+}
+
+int make_flat_items(ScanItem *d_items, int32_t *d_nitems, int64_t nrows, int32_t chunk_rows, int64_t nq,
+                    int32_t part_off, int32_t qchunk, hipStream_t st) {
+  const int nchunks = (int)((nrows + chunk_rows - 1) / chunk_rows);
+  const int nqc = (int)((nq + qchunk - 1) / qchunk);
+  const int n = nchunks * nqc;
+  hipLaunchKernelGGL(flat_items_kernel, dim3(nblk(n > 0 ? n : 1, 256)), dim3(256), 0, st, d_items, d_nitems, nchunks,
+                     nqc, chunk_rows, nrows, nq, part_off, qchunk);
+  return n;
+}
+
+void launch_norms(const float *x, int64_t n, int32_t dim, int blocked, float *out, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(norms_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, x, n, dim, blocked, out);
+}
+
+void launch_merge_keys(const float *ps, const uint32_t *pk, int64_t nq, int32_t nparts, int32_t k,
+                       const int64_t *row_labels, const int64_t *buf_labels, float *out_s, int64_t *out_l,
+                       int32_t *out_keys, int32_t *out_cnt, hipStream_t st) {
+  if (nq <= 0) return;
+  hipLaunchKernelGGL(merge_keys_kernel, dim3(nblk(nq, 4)), dim3(256), 0, st, ps, pk, nq, nparts, k, row_labels,
+                     buf_labels, out_s, out_l, out_keys, out_cnt);
+}
+
+void launch_merge_labels(const float *ps, const int64_t *pl, int64_t nq, int32_t nparts, int32_t k, float *out_s,
+                         int64_t *out_l, hipStream_t st) {
+  if (nq <= 0) return;
+  hipLaunchKernelGGL(merge_labels_kernel, dim3(nblk(nq, 4)), dim3(256), 0, st, ps, pl, nq, nparts, k, out_s, out_l);
+}
+
+int ivf_max_items(int64_t nq, int32_t nprobe, int32_t nlist, int32_t qchunk) {
+  return (int)((nq * nprobe + qchunk - 1) / qchunk) + nlist;
+}
+
+void launch_ivf_items(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t nparts, int32_t nlist,
+                      const int32_t *list_begin, const int32_t *list_end, int32_t qchunk, IvfItemWs &ws,
+                      hipStream_t st) {
+  (void)hipMemsetAsync(ws.cnt, 0, sizeof(int32_t) * nlist, st);
+  (void)hipMemsetAsync(ws.fill, 0, sizeof(int32_t) * nlist, st);
+  const int64_t n = nq * nprobe;
+  if (n > 0) hipLaunchKernelGGL(ivf_count_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, probes, n, ws.cnt);
+  hipLaunchKernelGGL(ivf_scan_kernel, dim3(1), dim3(1024), 0, st, ws.cnt, nlist, qchunk, ws.qoff, ws.ioff, ws.n_items);
+  if (n > 0)
+    hipLaunchKernelGGL(ivf_fill_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, probes, nq, nprobe, nparts, ws.qoff,
+                       ws.fill, ws.qlist);
+  hipLaunchKernelGGL(ivf_items_kernel, dim3(nblk(nlist, 256)), dim3(256), 0, st, ws.cnt, ws.qoff, ws.ioff, nlist,
+                     list_begin, list_end, qchunk, ws.items);
+}
+
+void launch_ivf_limits(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t nparts, int64_t remaining,
+                       const int32_t *list_begin, const int32_t *list_end, const int32_t *list_live,
+                       const uint8_t *live, uint32_t *limits, hipStream_t st) {
+  if (nq <= 0) return;
+  hipLaunchKernelGGL(ivf_limits_kernel, dim3(nblk(nq, 64)), dim3(64), 0, st, probes, nq, nprobe, nparts, remaining,
+                     list_begin, list_end, list_live, live, limits);
+}
+
+size_t pq_scan_lds_bytes(int dim, int M, int ksub, int k) {
+  return (size_t)(((dim + 3) & ~3) + M * ksub + 2 * k + 2 * 256 + 4) * 4;
+}
+
+void launch_pq_scan(const PqArgs &a, int max_items, hipStream_t st) {
+  if (max_items <= 0) return;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&pq_scan_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(pq_scan_kernel, dim3(max_items), dim3(256), pq_scan_lds_bytes(a.dim, a.M, a.ksub, a.k), st, a);
+}
+
+void launch_pq_encode(const float *x, const int32_t *assign, const float *cents, int64_t n, int32_t dim, int32_t M,
+                      int32_t ksub, const float *codebooks, uint8_t *codes, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(pq_encode_kernel, dim3(nblk(n * M, 256)), dim3(256), 0, st, x, assign, cents, n, dim, M, ksub,
+                     codebooks, codes);
+}
+void launch_residuals(const float *x, const int32_t *assign, const float *cents, int64_t n, int32_t dim, float *out,
+                      hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(residuals_kernel, dim3(nblk(n * dim, 256)), dim3(256), 0, st, x, assign, cents, n, dim, out);
+}
+void launch_extract_sub(const float *x, int64_t n, int32_t dim, int32_t off, int32_t sub, float *out, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(extract_sub_kernel, dim3(nblk(n * sub, 256)), dim3(256), 0, st, x, n, dim, off, sub, out);
+}
+void launch_pack_codes(const uint8_t *codes, const int64_t *src_of_dst, int64_t ndst, int32_t M, uint8_t *out,
+                       hipStream_t st) {
+  if (ndst <= 0) return;
+  const int nch = (M + 15) / 16;
+  hipLaunchKernelGGL(pack_codes_kernel, dim3(nblk(ndst * nch * 16, 256)), dim3(256), 0, st, codes, src_of_dst, ndst,
+                     M, out);
+}
+
+void launch_to_blocked(const float *src, const int64_t *src_idx, int64_t n, int32_t dim, float *dst, int64_t dst_row0,
+                       hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(to_blocked_kernel, dim3(nblk(n * dim, 256)), dim3(256), 0, st, src, src_idx, n, dim, dst,
+                     dst_row0);
+}
+void launch_scatter_blocked(const float *src, const int64_t *dst_slots, int64_t n, int32_t dim, float *dst,
+                            hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(scatter_blocked_kernel, dim3(nblk(n * dim, 256)), dim3(256), 0, st, src, dst_slots, n, dim, dst);
+}
+void launch_gather_blocked(const float *src, const int64_t *src_slots, int64_t n, int32_t dim, float *out,
+                           hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(gather_blocked_kernel, dim3(nblk(n * dim, 256)), dim3(256), 0, st, src, src_slots, n, dim, out);
+}
+void launch_gather2(const float *A, const float *B, const int64_t *idx, int64_t n, int32_t dim, float *out,
+                    hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(gather2_kernel, dim3(nblk(n * dim, 256)), dim3(256), 0, st, A, B, idx, n, dim, out);
+}
+void launch_gather_rows(const float *src, const int32_t *idx, int64_t n, int32_t dim, float *out, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(nblk(n * dim, 256)), dim3(256), 0, st, src, idx, n, dim, out);
+}
+
+void launch_keys_to_assign(const uint32_t *keys, int64_t n, int32_t *assign, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(keys_to_assign_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, keys, n, assign);
+}
+
+void launch_kmeans_update(const float *data, const int32_t *members, const int32_t *coff, int32_t k, int32_t dim,
+                          float *cents, float *tmp, int32_t *flags, int32_t *changed, hipStream_t st) {
+  (void)hipMemsetAsync(flags, 0, sizeof(int32_t) * k, st);
+  (void)hipMemsetAsync(changed, 0, sizeof(int32_t), st);
+  const int bx = dim < 64 ? dim : 64;
+  hipLaunchKernelGGL(kmeans_sum_kernel, dim3((dim + bx - 1) / bx, k), dim3(bx), 0, st, data, members, coff, k, dim,
+                     cents, tmp, flags);
+  hipLaunchKernelGGL(kmeans_commit_kernel, dim3(nblk((int64_t)k * dim, 256)), dim3(256), 0, st, cents, tmp, flags, k,
+                     dim, changed);
+}
+
+static int key_bits(int32_t k) {
+  int b = 1;
+  while ((1 << b) < k) ++b;
+  return b;
+}
+
+size_t sort_temp_bytes(int64_t n, int32_t k) {
+  size_t a = 0, b = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, a, (const int32_t *)nullptr, (int32_t *)nullptr,
+                                           (const int32_t *)nullptr, (int32_t *)nullptr, (int)n, 0, key_bits(k));
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (const int32_t *)nullptr, (int32_t *)nullptr, k + 1);
+  return (a > b ? a : b) + 256;
+}
+
+void sort_by_key(const int32_t *keys, int64_t n, int32_t k, int32_t *keys_tmp, int32_t *idx_in, int32_t *members,
+                 int32_t *counts, int32_t *coff, void *temp, size_t temp_bytes, hipStream_t st) {
+  hipLaunchKernelGGL(iota_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, idx_in, n);
+  size_t tb = temp_bytes;
+  (void)hipcub::DeviceRadixSort::SortPairs(temp, tb, keys, keys_tmp, idx_in, members, (int)n, 0, key_bits(k), st);
+  (void)hipMemsetAsync(counts, 0, sizeof(int32_t) * (k + 1), st);
+  hipLaunchKernelGGL(hist_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, keys, n, counts);
+  tb = temp_bytes;
+  (void)hipcub::DeviceScan::ExclusiveSum(temp, tb, counts, coff, k + 1, st);
+}
+
+void launch_scatter_i64(int64_t *dst, const int64_t *idx, const int64_t *vals, int64_t n, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(scatter_i64_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, dst, idx, vals, n);
+}
+void launch_scatter_u8(uint8_t *dst, const int64_t *idx, uint8_t v, int64_t n, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(scatter_u8_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, dst, idx, v, n);
+}
+void launch_norms_slots(const float *rows, const int64_t *slots, int64_t n, int32_t dim, float *out, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(norms_slots_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, rows, slots, n, dim, out);
+}
+void launch_fill_results(float *s, int64_t *l, int32_t *c, int64_t nq, int32_t k, hipStream_t st) {
+  const int64_t n = nq * (k > 1 ? k : 1) > nq ? nq * (k > 1 ? k : 1) : nq;
+  if (n <= 0) return;
+  hipLaunchKernelGGL(fill_results_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, s, l, c, nq, k);
+}
+
+void fill_u8(uint8_t *p, uint8_t v, int64_t n, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(fill_u8_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, p, v, n);
+}
+
+}  // namespace pyr

@@ -1,0 +1,418 @@
+"""Host-side mirror of the reference plugin surface for the scan path.
+
+Restates the C# contract `IVectorIndex` (reference
+src/Pyrope.GarnetServer/Vector/IVectorIndex.cs:5-31), `SearchOptions`
+(SearchOptions.cs:3), `ICentroidsProvider` (ICentroidsProvider.cs:14), the
+`DeltaVectorIndex` composite (DeltaVectorIndex.cs) and the registry factory
+branch (Services/VectorIndexRegistry.cs:81-113) over the C ABI of
+libpyrope_hip.so.  This is what the C# P/Invoke shim does:
+string ids <-> int64 labels, argument validation with the reference's
+exception types and messages, one call per batch.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import enum
+from abc import ABC, abstractmethod
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import (ArgumentException, ArgumentNullException, ArgumentOutOfRangeException,
+                   InvalidOperationException, check, ptr)
+
+
+class VectorMetric(enum.IntEnum):  # IVectorIndex.cs:5-10
+    L2 = 0
+    InnerProduct = 1
+    Cosine = 2
+
+
+@dataclass(frozen=True)
+class SearchResult:  # IVectorIndex.cs:12
+    id: str
+    score: float
+
+
+@dataclass(frozen=True)
+class IndexStats:  # IVectorIndex.cs:31
+    count: int
+    dimension: int
+    metric: str
+
+
+@dataclass(frozen=True)
+class SearchOptions:  # SearchOptions.cs:3
+    max_scans: Optional[int] = None
+    nprobe: Optional[int] = None
+    ef_search: Optional[int] = None
+
+
+class IVectorIndex(ABC):  # IVectorIndex.cs:14-29
+    dimension: int
+    metric: VectorMetric
+
+    @abstractmethod
+    def add(self, id: str, vector: Sequence[float]) -> None: ...
+
+    @abstractmethod
+    def upsert(self, id: str, vector: Sequence[float]) -> None: ...
+
+    @abstractmethod
+    def delete(self, id: str) -> bool: ...
+
+    @abstractmethod
+    def search(self, query: Sequence[float], top_k: int,
+               options: Optional[SearchOptions] = None) -> List[SearchResult]: ...
+
+    @abstractmethod
+    def build(self) -> None: ...
+
+    def snapshot(self, path: str) -> None:  # on-disk format is SURVEY.md 8(f)-4 (not this round)
+        raise NotImplementedError("Snapshot is not part of the scan path (SURVEY.md 8f-4)")
+
+    def load(self, path: str) -> None:
+        raise NotImplementedError("Load is not part of the scan path (SURVEY.md 8f-4)")
+
+    @abstractmethod
+    def get_stats(self) -> IndexStats: ...
+
+
+class ICentroidsProvider(ABC):  # ICentroidsProvider.cs:14
+    @abstractmethod
+    def get_centroids(self) -> Optional[List[np.ndarray]]: ...
+
+
+def _validate_id(id: str) -> None:  # BruteForceVectorIndex.cs:386-389
+    if id is None or str(id).strip() == "":
+        raise ArgumentException("Id cannot be empty.")
+
+
+class HipVectorIndex(IVectorIndex):
+    """An IVectorIndex backed by libpyrope_hip.so (the C# shim's behaviour)."""
+
+    KIND = _lib.PYR_FLAT
+
+    def __init__(self, dimension: int, metric: VectorMetric, *, nlist: int = 100, m: int = 4, k: int = 256,
+                 device: int = 0, default_nprobe: int = 0):
+        if dimension <= 0:
+            raise ArgumentOutOfRangeException("Dimension must be positive.")
+        self.dimension = int(dimension)
+        self.metric = VectorMetric(metric)
+        self._L = _lib.load()
+        desc = _lib.IndexDesc(self.KIND, self.dimension, int(self.metric), nlist, m, k, device, default_nprobe)
+        h = C.c_void_p()
+        check(self._L.pyr_index_create(C.byref(desc), C.byref(h)))
+        self._h = h
+        self._label_of: Dict[str, int] = {}
+        self._id_of: Dict[int, str] = {}
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.pyr_index_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- id <-> label (the shim's job) ----
+    def _label(self, id: str) -> int:
+        lab = self._label_of.get(id)
+        if lab is None:
+            lab = len(self._label_of)
+            self._label_of[id] = lab
+            self._id_of[lab] = id
+        return lab
+
+    def _vec(self, vector) -> np.ndarray:
+        if vector is None:
+            raise ArgumentNullException("vector")
+        v = np.ascontiguousarray(vector, dtype=np.float32).reshape(-1)
+        if v.size != self.dimension:
+            raise ArgumentException("Vector dimension mismatch.")
+        return v
+
+    def _write(self, fn, ids: Sequence[str], x: np.ndarray) -> None:
+        labels = np.array([self._label(i) for i in ids], dtype=np.int64)
+        x = np.ascontiguousarray(x, dtype=np.float32).reshape(len(labels), self.dimension)
+        check(fn(self._h, ptr(x, C.c_float), len(labels), ptr(labels, C.c_int64)))
+
+    # ---- IVectorIndex ----
+    def add(self, id: str, vector) -> None:
+        _validate_id(id)
+        self._write(self._L.pyr_index_add, [id], self._vec(vector))
+
+    def upsert(self, id: str, vector) -> None:
+        _validate_id(id)
+        self._write(self._L.pyr_index_upsert, [id], self._vec(vector))
+
+    def add_batch(self, ids: Sequence[str], x: np.ndarray) -> None:
+        self._write(self._L.pyr_index_add, ids, x)
+
+    def add_labels(self, labels: np.ndarray, x: np.ndarray) -> None:
+        """Bulk add with caller-chosen int64 labels (id = str(label))."""
+        labels = np.ascontiguousarray(labels, dtype=np.int64)
+        for lab in labels.tolist():
+            self._label_of[str(lab)] = lab
+            self._id_of[lab] = str(lab)
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        check(self._L.pyr_index_add(self._h, ptr(x, C.c_float), len(labels), ptr(labels, C.c_int64)))
+
+    def delete(self, id: str) -> bool:
+        _validate_id(id)
+        lab = self._label_of.get(id)
+        if lab is None:
+            return False
+        labels = np.array([lab], np.int64)
+        removed = np.zeros(1, np.uint8)
+        check(self._L.pyr_index_remove(self._h, ptr(labels, C.c_int64), 1, ptr(removed, C.c_uint8)))
+        return bool(removed[0])
+
+    def build(self) -> None:
+        check(self._L.pyr_index_build(self._h))
+
+    def _params(self, options: Optional[SearchOptions]) -> _lib.SearchParams:
+        p = _lib.SearchParams(-1, 0, -1)
+        if options is not None:
+            if options.nprobe is not None:
+                p.nprobe = max(int(options.nprobe), 0)
+            if options.max_scans is not None:
+                p.max_scans = max(int(options.max_scans), 0)
+        return p
+
+    def search_batch(self, queries: np.ndarray, top_k: int, options: Optional[SearchOptions] = None):
+        """Batched Search: returns (scores [nq,k] fp32, labels [nq,k] int64, counts [nq])."""
+        q = np.ascontiguousarray(queries, dtype=np.float32).reshape(-1, self.dimension)
+        nq = q.shape[0]
+        kk = max(int(top_k), 0)
+        s = np.empty((nq, kk), np.float32)
+        lab = np.empty((nq, kk), np.int64)
+        cnt = np.empty(nq, np.int32)
+        p = self._params(options)
+        check(self._L.pyr_index_search(self._h, ptr(q, C.c_float), nq, int(top_k), C.byref(p), ptr(s, C.c_float),
+                                       ptr(lab, C.c_int64), ptr(cnt, C.c_int32)))
+        return s, lab, cnt
+
+    def search(self, query, top_k: int, options: Optional[SearchOptions] = None) -> List[SearchResult]:
+        q = self._vec(query)
+        s, lab, cnt = self.search_batch(q[None, :], top_k, options)
+        return [SearchResult(self._id_of[int(lab[0, j])], float(s[0, j])) for j in range(int(cnt[0]))]
+
+    def search_device(self, d_q: int, nq: int, top_k: int, d_scores: int, d_labels: int, d_counts: int = 0,
+                      stream: int = 0, options: Optional[SearchOptions] = None) -> None:
+        """Search on device-resident buffers (raw device pointers, e.g. torch tensor.data_ptr())."""
+        p = self._params(options)
+        check(self._L.pyr_index_search_device(self._h, C.c_void_p(d_q), nq, int(top_k), C.byref(p),
+                                              C.c_void_p(d_scores), C.c_void_p(d_labels),
+                                              C.c_void_p(d_counts or None), C.c_void_p(stream or None)))
+
+    def get_stats(self) -> IndexStats:
+        cnt = C.c_int64()
+        check(self._L.pyr_index_stats(self._h, C.byref(cnt), None, None))
+        return IndexStats(int(cnt.value), self.dimension, self.metric.name)
+
+    # ---- introspection used by parity tests and the CPU baseline ----
+    def ivf_layout(self):
+        total = C.c_int64()
+        nl = C.c_int32()
+        check(self._L.pyr_index_get_centroids(self._h, None, C.byref(nl)))
+        check(self._L.pyr_index_ivf_layout(self._h, None, None, None, C.byref(total)))
+        off = np.zeros(nl.value + 1, np.int64)
+        labels = np.zeros(total.value, np.int64)
+        live = np.zeros(total.value, np.uint8)
+        check(self._L.pyr_index_ivf_layout(self._h, ptr(off, C.c_int64), ptr(labels, C.c_int64),
+                                           ptr(live, C.c_uint8), C.byref(total)))
+        return off, labels, live
+
+    def centroids_array(self) -> Optional[np.ndarray]:
+        nl = C.c_int32()
+        check(self._L.pyr_index_get_centroids(self._h, None, C.byref(nl)))
+        if nl.value == 0:
+            return None
+        out = np.zeros((nl.value, self.dimension), np.float32)
+        check(self._L.pyr_index_get_centroids(self._h, ptr(out, C.c_float), C.byref(nl)))
+        return out
+
+
+class BruteForceVectorIndex(HipVectorIndex):
+    """FLAT (BruteForceVectorIndex.cs) -- the Delta head."""
+    KIND = _lib.PYR_FLAT
+
+    def __init__(self, dimension: int, metric: VectorMetric, **kw):
+        super().__init__(dimension, metric, **kw)
+
+    def search(self, query, top_k: int, options: Optional[SearchOptions] = None) -> List[SearchResult]:
+        self._vec(query)
+        if top_k <= 0:  # :278
+            raise ArgumentOutOfRangeException("topK must be positive.")
+        return super().search(query, top_k, options)
+
+    def scan(self):  # :250-273 (compaction source)
+        raise NotImplementedError("device-side compaction is SURVEY.md 8(f)-2")
+
+
+class IvfFlatVectorIndex(HipVectorIndex, ICentroidsProvider):
+    """IVF_FLAT (IvfFlatVectorIndex.cs)."""
+    KIND = _lib.PYR_IVF_FLAT
+
+    def __init__(self, dimension: int, metric: VectorMetric, n_list: int = 100, **kw):
+        super().__init__(dimension, metric, nlist=n_list, **kw)
+        self.n_list = n_list
+        self.combine_nprobe = 3  # CombineNProbe (:14)
+
+    def _params(self, options):
+        p = super()._params(options)
+        if options is None or options.nprobe is None:
+            p.nprobe = max(int(self.combine_nprobe), 0)
+        return p
+
+    def get_centroids(self):  # :314-325
+        c = self.centroids_array()
+        return None if c is None else [row.copy() for row in c]
+
+
+class IvfPqVectorIndex(HipVectorIndex):
+    """IVF_PQ (IvfPqVectorIndex.cs + ProductQuantizer.cs)."""
+    KIND = _lib.PYR_IVF_PQ
+
+    def __init__(self, dimension: int, metric: VectorMetric, m: int, k: int, n_list: int, **kw):
+        super().__init__(dimension, metric, nlist=n_list, m=m, k=k, **kw)
+        self.m, self.k, self.n_list = m, k, n_list
+
+    def add(self, id: str, vector) -> None:  # IvfPq.Add does not validate (:37-45)
+        self._write(self._L.pyr_index_add, [id], self._vec(vector))
+
+    def upsert(self, id: str, vector) -> None:
+        self.add(id, vector)
+
+    def delete(self, id: str) -> bool:
+        lab = self._label_of.get(id)
+        if lab is None:
+            return False
+        labels = np.array([lab], np.int64)
+        removed = np.zeros(1, np.uint8)
+        check(self._L.pyr_index_remove(self._h, ptr(labels, C.c_int64), 1, ptr(removed, C.c_uint8)))
+        return bool(removed[0])
+
+    def pq_state(self):
+        ks = C.c_int32()
+        check(self._L.pyr_index_pq_state(self._h, None, C.byref(ks), None))
+        off, labels, live = self.ivf_layout()
+        cb = np.zeros((self.m, ks.value, self.dimension // self.m), np.float32)
+        codes = np.zeros((len(labels), self.m), np.uint8)
+        check(self._L.pyr_index_pq_state(self._h, ptr(cb, C.c_float), C.byref(ks), ptr(codes, C.c_uint8)))
+        return cb, codes, off, labels, live
+
+
+class DeltaVectorIndex(IVectorIndex, ICentroidsProvider):
+    """LSM head/tail composite (DeltaVectorIndex.cs) -- host logic, unchanged from the reference."""
+
+    def __init__(self, head: IVectorIndex, tail: IVectorIndex):
+        if head.dimension != tail.dimension:
+            raise ArgumentException("Head and Tail dimensions must match")
+        if head.metric != tail.metric:
+            raise ArgumentException("Head and Tail metrics must match")
+        self.head, self.tail = head, tail
+        self.dimension, self.metric = head.dimension, head.metric
+
+    def add(self, id, vector):  # :29-43 writes go to the head
+        self.head.add(id, vector)
+
+    def upsert(self, id, vector):
+        self.head.upsert(id, vector)
+
+    def delete(self, id) -> bool:  # :58-74
+        h = self.head.delete(id)
+        t = self.tail.delete(id)
+        return h or t
+
+    def search(self, query, top_k, options=None):  # :76-122
+        head_res = self.head.search(query, top_k, options)
+        tail_res = self.tail.search(query, top_k, options)
+        merged: Dict[str, SearchResult] = {}
+        for r in tail_res:
+            merged[r.id] = r
+        for r in head_res:  # head wins on id collision
+            merged[r.id] = r
+        out = sorted(merged.values(), key=lambda r: -r.score)
+        return out[:top_k]
+
+    def build(self):  # :124-158 compaction head -> tail
+        items = self.head.scan_items() if hasattr(self.head, "scan_items") else None
+        if items is not None:
+            for id, vec in items:
+                self.tail.add(id, vec)
+                self.head.delete(id)
+        self.head.build()
+        self.tail.build()
+
+    def get_stats(self) -> IndexStats:  # :209-221
+        h, t = self.head.get_stats(), self.tail.get_stats()
+        return IndexStats(h.count + t.count, h.dimension, h.metric)
+
+    def get_centroids(self):  # :223-233
+        return self.tail.get_centroids() if isinstance(self.tail, ICentroidsProvider) else None
+
+
+class VectorIndexRegistry:
+    """Factory branch of Services/VectorIndexRegistry.cs:81-113 with the GPU-backed tail."""
+
+    def __init__(self, device: int = 0):
+        self._indices: Dict[str, DeltaVectorIndex] = {}
+        self.device = device
+
+    @staticmethod
+    def _int_param(params: Optional[dict], key: str, default: int) -> int:  # :115-126
+        if params and key in params:
+            v = params[key]
+            if isinstance(v, bool):
+                return default
+            if isinstance(v, int):
+                return v
+        return default
+
+    def create(self, dimension: int, metric: VectorMetric, algorithm: Optional[str] = None,
+               parameters: Optional[dict] = None) -> DeltaVectorIndex:
+        algo = (algorithm or "IVF_FLAT").upper()  # :87
+        if algo == "HNSW":
+            raise InvalidOperationException("HNSW is outside the GPU scan path (SURVEY.md 2, row 12)")
+        if algo == "IVF_PQ":  # :96-102
+            tail: IVectorIndex = IvfPqVectorIndex(dimension, metric, m=self._int_param(parameters, "m", 4),
+                                                  k=self._int_param(parameters, "k", 256),
+                                                  n_list=self._int_param(parameters, "nlist", 100),
+                                                  device=self.device)
+        else:  # :103-108 (unknown strings -> IVF_FLAT)
+            tail = IvfFlatVectorIndex(dimension, metric, n_list=self._int_param(parameters, "nlist", 100),
+                                      device=self.device)
+            nprobe = self._int_param(parameters, "nprobe", 0)
+            if nprobe > 0:
+                tail.combine_nprobe = nprobe
+        head = BruteForceVectorIndex(dimension, metric, device=self.device)  # :111
+        return DeltaVectorIndex(head, tail)
+
+    def get_or_create(self, tenant: str, index: str, dimension: int, metric: VectorMetric,
+                      algorithm: Optional[str] = None, parameters: Optional[dict] = None) -> DeltaVectorIndex:
+        key = f"{tenant}:{index}"
+        if key not in self._indices:
+            self._indices[key] = self.create(dimension, metric, algorithm, parameters)
+        idx = self._indices[key]
+        if idx.dimension != dimension:
+            raise ArgumentException("Vector dimension mismatch.")
+        if idx.metric != metric:
+            raise ArgumentException("Vector metric mismatch.")
+        return idx
+
+    def try_get_index(self, tenant: str, index: str) -> Optional[DeltaVectorIndex]:
+        return self._indices.get(f"{tenant}:{index}")
+
+
+def generate_synthetic(count: int, dim: int, seed: int) -> np.ndarray:
+    """Pyrope.Benchmarks GenerateRandomVectors (Program.cs:251-263), via the library."""
+    out = np.empty((count, dim), np.float32)
+    check(_lib.load().pyr_generate_synthetic(count, dim, seed, ptr(out, C.c_float)))
+    return out

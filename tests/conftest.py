@@ -1,0 +1,28 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) device; calls the HIP path through the C ABI")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    import oracle as O
+    O.lib()
+    return O
+
+
+@pytest.fixture(scope="session")
+def hiplib():
+    """The product library; on a GPU box a missing .so or device is a failure, not a skip."""
+    from pyrope_amd import _lib
+    from pyrope_amd.build import build
+    build()
+    return _lib.load()
