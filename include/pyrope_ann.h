@@ -86,6 +86,17 @@ pyr_status pyr_index_remove(pyr_index *index, const int64_t *labels, int64_t n, 
  * (KMeansUtils.Train semantics, run on the GPU), assignment and PQ encoding.  FLAT: no-op. */
 pyr_status pyr_index_build(pyr_index *index);
 
+/* Supply a trained coarse quantizer (nlist x dim, row-major) for the next Build of an IVF index,
+ * which then only assigns (and, for IVF_PQ, trains codebooks).  The C# shim uses it to hand over
+ * KMeansUtils.Train output; the multi-GPU path uses it so every shard shares one quantizer. */
+pyr_status pyr_index_set_centroids(pyr_index *index, const float *centroids, int32_t nlist);
+
+/* KMeansUtils.Train (KMeansUtils.cs:10-68) on the GPU, reference-identical: OrderBy(rnd.Next())
+ * initialisation, <= max_iter Lloyd iterations, member sums in data order, ArraysEqual(1e-6) stop.
+ * data: n x dim host row-major.  out: k x dim (k clamped to [1, n]); *k_out = k used. */
+pyr_status pyr_kmeans_train(int32_t device, const float *data, int64_t n, int32_t dim, int32_t k, int32_t metric,
+                            int32_t max_iter, int32_t seed, float *out, int32_t *k_out);
+
 /* IVectorIndex.Search (IVectorIndex.cs:22) for a batch of queries.  Host buffers.
  * q: nq x dim; out_scores/out_labels: nq x k; out_counts: nq (may be NULL).
  * params may be NULL (= SearchOptions null). */
@@ -124,6 +135,13 @@ pyr_status pyr_merge_topk_device(const float *d_scores, const int64_t *d_labels,
 /* Pyrope.Benchmarks synthetic generator (Program.cs:251-263): v[d] = (float)new Random(seed).NextDouble(),
  * row by row.  Host buffer count x dim.  Measurement-harness utility. */
 pyr_status pyr_generate_synthetic(int64_t count, int32_t dim, int32_t seed, float *out);
+
+/* Kernel-phase profiler (HIP events on the search stream; adds a host sync per search while on).
+ * phase: 0 coarse scan+select, 1 IVF work lists, 2 IVF list scan, 3 buffer scan, 4 final merge,
+ * 5 FLAT scan, 6 IVF-PQ LUT+ADC scan.  *work = (query, row) pairs the phase scored. */
+void pyr_profile_enable(int32_t on);
+void pyr_profile_reset(void);
+pyr_status pyr_profile_get(int32_t phase, double *total_ms, int64_t *calls, int64_t *work);
 
 /* thread-local message of the last failing call on this thread */
 const char *pyr_last_error(void);

@@ -77,6 +77,12 @@ SIGNATURES = {
     "pyr_index_pq_state": (C.c_int, [_vp, _f, _i32, _u8]),
     "pyr_merge_topk_device": (C.c_int, [_vp, _vp, C.c_int64, C.c_int32, C.c_int32, _vp, _vp, _vp]),
     "pyr_generate_synthetic": (C.c_int, [C.c_int64, C.c_int32, C.c_int32, _f]),
+    "pyr_index_set_centroids": (C.c_int, [_vp, _f, C.c_int32]),
+    "pyr_kmeans_train": (C.c_int, [C.c_int32, _f, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                   _f, _i32]),
+    "pyr_profile_enable": (None, [C.c_int32]),
+    "pyr_profile_reset": (None, []),
+    "pyr_profile_get": (C.c_int, [C.c_int32, C.POINTER(C.c_double), _i64, _i64]),
     "pyr_last_error": (C.c_char_p, []),
     "pyr_version": (C.c_char_p, []),
 }

@@ -114,6 +114,60 @@ pyr_status pyr_index_build(pyr_index *index) {
   });
 }
 
+pyr_status pyr_index_set_centroids(pyr_index *index, const float *centroids, int32_t nlist) {
+  if (!index || !centroids) return fail(PYR_E_ARG, "null argument");
+  return guard([&] {
+    std::unique_lock<std::shared_mutex> g(index->impl->mu);
+    index->impl->set_centroids(centroids, nlist);
+  });
+}
+
+pyr_status pyr_kmeans_train(int32_t device, const float *data, int64_t n, int32_t dim, int32_t k, int32_t metric,
+                            int32_t max_iter, int32_t seed, float *out, int32_t *k_out) {
+  if (!data || !out || n < 0 || dim <= 0) return fail(PYR_E_ARG, "bad argument");
+  return guard([&] {
+    check_device(device);
+    HIPCHK(hipSetDevice(device));
+    hipStream_t st;
+    HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    try {
+      pyr::DevMem X, C;
+      X.ensure(sizeof(float) * (size_t)std::max<int64_t>(n, 1) * dim);
+      const int kk = (int)std::max<int64_t>(1, std::min<int64_t>(k <= 0 ? 1 : k, std::max<int64_t>(n, 1)));
+      C.ensure(sizeof(float) * (size_t)kk * dim);
+      HIPCHK(hipMemcpyAsync(X.p, data, sizeof(float) * n * dim, hipMemcpyHostToDevice, st));
+      const int used = pyr::kmeans_train_gpu(X.as<float>(), n, dim, k, metric, max_iter, seed, C.as<float>(), st);
+      if (used > 0) HIPCHK(hipMemcpyAsync(out, C.p, sizeof(float) * (size_t)used * dim, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      if (k_out) *k_out = used;
+    } catch (...) {
+      (void)hipStreamDestroy(st);
+      throw;
+    }
+    (void)hipStreamDestroy(st);
+  });
+}
+
+void pyr_profile_enable(int32_t on) {
+  std::lock_guard<std::mutex> g(pyr::prof().m);
+  pyr::prof().on = on != 0;
+}
+
+void pyr_profile_reset(void) {
+  std::lock_guard<std::mutex> g(pyr::prof().m);
+  pyr::prof().reset();
+}
+
+pyr_status pyr_profile_get(int32_t phase, double *total_ms, int64_t *calls, int64_t *work) {
+  if (phase < 0 || phase >= pyr::PH_N) return fail(PYR_E_ARG, "bad phase");
+  std::lock_guard<std::mutex> g(pyr::prof().m);
+  pyr::prof().drain();
+  if (total_ms) *total_ms = pyr::prof().ms[phase];
+  if (calls) *calls = pyr::prof().calls[phase];
+  if (work) *work = pyr::prof().work[phase];
+  return PYR_OK;
+}
+
 pyr_status pyr_index_search(pyr_index *index, const float *q, int64_t nq, int32_t k, const pyr_search_params *params,
                             float *out_scores, int64_t *out_labels, int32_t *out_counts) {
   if (!index || nq < 0 || (nq > 0 && !q)) return fail(PYR_E_ARG, "null argument");

@@ -72,6 +72,7 @@ void RowStore::write(const float *x, const int64_t *slots, const int64_t *labs, 
   if (cosine) launch_norms_slots(rows.as<float>(), di, cnt, dim, norms.as<float>(), st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(st));  // staging buffers are reused by the next call
+  if (stage_x.n > (size_t(256) << 20)) stage_x.release();  // bulk loads: do not pin GBs of staging
 }
 
 void RowStore::set_live(const std::vector<int64_t> &slots, uint8_t v, hipStream_t st, DevMem &stage) {
@@ -133,6 +134,39 @@ void Index::ivf_layout(int64_t *, int64_t *, uint8_t *, int64_t *total) const {
 }
 void Index::pq_state(float *, int32_t *, uint8_t *) const { throw Error(PYR_E_STATE, "index kind is not IVF_PQ"); }
 
+Profiler &prof() {
+  static Profiler p;
+  return p;
+}
+void Profiler::drain() {
+  for (auto &r : pending) {
+    (void)hipEventSynchronize(r.b);
+    float t = 0;
+    if (hipEventElapsedTime(&t, r.a, r.b) == hipSuccess) ms[r.phase] += t;
+    calls[r.phase]++;
+    work[r.phase] += r.work;
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  pending.clear();
+}
+void Profiler::reset() {
+  drain();
+  for (int i = 0; i < PH_N; i++) ms[i] = 0, calls[i] = 0, work[i] = 0;
+}
+PhaseTimer::PhaseTimer(int ph, hipStream_t s, int64_t w) : phase(ph), st(s), work(w) {
+  if (!prof().on) return;
+  if (hipEventCreate(&a) == hipSuccess) (void)hipEventRecord(a, st);
+}
+PhaseTimer::~PhaseTimer() {
+  if (!a) return;
+  hipEvent_t b;
+  if (hipEventCreate(&b) != hipSuccess) return;
+  (void)hipEventRecord(b, st);
+  std::lock_guard<std::mutex> g(prof().m);
+  prof().pending.push_back({phase, a, b, work});
+}
+
 void fill_empty_results(float *d_s, int64_t *d_l, int32_t *d_c, int64_t nq, int k, hipStream_t st) {
   launch_fill_results(d_s, d_l, d_c, nq, k, st);
 }
@@ -172,6 +206,7 @@ static void flat_scan(const RowStore &rs, int64_t nrows, const ScanPlan &p, cons
   a.live = rs.live.as<uint8_t>();
   a.rnorm = rs.cosine ? rs.norms.as<float>() : nullptr;
   a.queries = d_q;
+  a.queries_t = ws.qt.as<float>();  // filled by prep_queries for the same d_q
   a.qnorm = d_qn;
   a.items = items.as<ScanItem>();
   a.n_items = nitems.as<int32_t>();
@@ -186,10 +221,17 @@ static void flat_scan(const RowStore &rs, int64_t nrows, const ScanPlan &p, cons
   launch_scan(a, met, V, p.nitems, ws.st);
 }
 
-static void query_norms(const float *d_q, int64_t nq, int dim, int met, Workspace &ws) {
-  if (met != COS) return;
-  ws.qn.ensure(sizeof(float) * std::max<int64_t>(nq, 1));
-  launch_norms(d_q, nq, dim, 0, ws.qn.as<float>(), ws.st);
+// per-batch query preparation shared by every scan of one search: cosine norms, and the
+// lane-major copy the fast scan kernel loads its query registers from
+static void prep_queries(const float *d_q, int64_t nq, int dim, int met, Workspace &ws) {
+  if (met == COS) {
+    ws.qn.ensure(sizeof(float) * std::max<int64_t>(nq, 1));
+    launch_norms(d_q, nq, dim, 0, ws.qn.as<float>(), ws.st);
+  }
+  if (fast_path(dim, 1) && nq > 0) {
+    ws.qt.ensure(sizeof(float) * nq * dim);
+    launch_transpose_queries(d_q, nq, dim, ws.qt.as<float>(), ws.st);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -209,7 +251,7 @@ void assign_gpu(const float *d_x, int64_t n, int dim, const float *d_cents, int 
   if (cs.cosine) launch_norms(cs.rows.as<float>(), k, dim, 1, cs.norms.as<float>(), st);
   Workspace ws;
   ws.st = st;
-  if (met == COS) query_norms(d_x, n, dim, met, ws);
+  prep_queries(d_x, n, dim, met, ws);
   ScanPlan p;
   p.qchunk = fast_path(dim, 1) ? QCHUNK : QCHUNK_GENERIC;
   p.chunk_rows = (int)round_up(k, 8);
@@ -346,13 +388,17 @@ struct FlatIndex : Index {
       fill_empty_results(d_s, d_l, d_c, nq, k, ws.st);
       return;
     }
-    query_norms(d_q, nq, dim, metric, ws);
+    prep_queries(d_q, nq, dim, metric, ws);
     ScanPlan p = plan_flat(cutoff, nq, dim, k, MAX_PARTS);
     const size_t np = (size_t)nq * p.nchunks * k;
     ws.part_s.ensure(sizeof(float) * np);
     ws.part_k.ensure(sizeof(uint32_t) * np);
-    flat_scan(st, cutoff, p, d_q, metric == COS ? ws.qn.as<float>() : nullptr, nq, k, 4, metric, p.nchunks, 0, 0, ws,
-              ws.part_s.as<float>(), ws.part_k.as<uint32_t>());
+    {
+      PhaseTimer t(PH_FLAT_SCAN, ws.st, nq * cutoff);
+      flat_scan(st, cutoff, p, d_q, metric == COS ? ws.qn.as<float>() : nullptr, nq, k, 4, metric, p.nchunks, 0, 0,
+                ws, ws.part_s.as<float>(), ws.part_k.as<uint32_t>());
+    }
+    PhaseTimer t(PH_MERGE, ws.st);
     launch_merge_keys(ws.part_s.as<float>(), ws.part_k.as<uint32_t>(), nq, p.nchunks, k, st.labels.as<int64_t>(),
                       nullptr, d_s, d_l, nullptr, d_c, ws.st);
   }
@@ -422,6 +468,14 @@ struct DictBuffer {
   }
   void clear(hipStream_t wst) {
     if (st.n) HIPCHK(hipMemsetAsync(st.live.p, 0, st.n, wst));
+    HIPCHK(hipStreamSynchronize(wst));
+    if (st.cap > 65536) {  // a bulk-loaded buffer was compacted into lists: give the HBM back
+      st.rows.release();
+      st.norms.release();
+      st.live.release();
+      st.labels.release();
+      st.cap = 0;
+    }
     st.clear();
     slot_of.clear();
     free_slots.clear();
@@ -476,6 +530,17 @@ struct Coarse {
   }
 };
 
+// (query, row) pairs a list scan scores: sum of probed list lengths (profiling only; syncs)
+static int64_t probed_rows(Workspace &ws, int64_t nq, int probes, const std::vector<int32_t> &le,
+                           const std::vector<int32_t> &lb) {
+  std::vector<int32_t> pr((size_t)nq * probes);
+  HIPCHK(hipMemcpyAsync(pr.data(), ws.probes.p, sizeof(int32_t) * pr.size(), hipMemcpyDeviceToHost, ws.st));
+  HIPCHK(hipStreamSynchronize(ws.st));
+  int64_t s = 0;
+  for (int32_t l : pr) s += le[l] - lb[l];
+  return s;
+}
+
 // list-major work items from ws.probes
 static int build_ivf_items(Workspace &ws, int64_t nq, int nprobe, int nparts, int nlist, const DevMem &lbeg,
                            const DevMem &lend, int qchunk) {
@@ -507,6 +572,14 @@ struct IvfFlatIndex : Index {
   Coarse coarse;
   bool built = false;                     // _isBuilt (:20)
   int nprobe_default;
+  std::vector<float> given;               // pyr_index_set_centroids
+  int given_k = 0;
+
+  void set_centroids(const float *c, int nl) override {
+    if (nl <= 0) throw Error(PYR_E_ARG, "nlist must be positive");
+    given.assign(c, c + (size_t)nl * dim);
+    given_k = nl;
+  }
 
   explicit IvfFlatIndex(const pyr_index_desc &d) : Index(d) {
     buf.st.dim = lists.dim = dim;
@@ -596,12 +669,18 @@ struct IvfFlatIndex : Index {
     HIPCHK(hipMemcpyAsync(dsrc.p, src.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, wst));
     launch_gather2(built ? lists.rows.as<float>() : buf.st.rows.as<float>(), buf.st.rows.as<float>(),
                    dsrc.as<int64_t>(), n, dim, X.as<float>(), wst);
-    // 2. train (:116-119)
+    // 2. train (:116-119), or take the supplied quantizer
     int k = (int)std::min<int64_t>(desc.nlist, n);
     if (k <= 0) k = 1;
     DevMem C;
-    C.ensure(sizeof(float) * k * dim);
-    k = kmeans_train_gpu(X.as<float>(), n, dim, k, metric, 10, 42, C.as<float>(), wst);
+    if (given_k > 0) {
+      k = given_k;
+      C.ensure(sizeof(float) * k * dim);
+      HIPCHK(hipMemcpyAsync(C.p, given.data(), sizeof(float) * k * dim, hipMemcpyHostToDevice, wst));
+    } else {
+      C.ensure(sizeof(float) * k * dim);
+      k = kmeans_train_gpu(X.as<float>(), n, dim, k, metric, 10, 42, C.as<float>(), wst);
+    }
     // 3. assign (:128-132)
     DevMem A;
     A.ensure(sizeof(int32_t) * n);
@@ -691,15 +770,22 @@ struct IvfFlatIndex : Index {
       fill_empty_results(d_s, d_l, d_c, nq, k, ws.st);
       return;
     }
-    query_norms(d_q, nq, dim, metric, ws);
+    prep_queries(d_q, nq, dim, metric, ws);
     const float *qn = metric == COS ? ws.qn.as<float>() : nullptr;
     const size_t np = (size_t)nq * nparts * k;
     ws.part_s.ensure(sizeof(float) * np);
     ws.part_k.ensure(sizeof(uint32_t) * np);
     if (probes > 0) {
-      coarse.probe(d_q, qn, nq, probes, metric, ws);
+      {
+        PhaseTimer t(PH_COARSE, ws.st, nq * coarse.nlist);
+        coarse.probe(d_q, qn, nq, probes, metric, ws);
+      }
       const int qchunk = fast_path(dim, k) ? QCHUNK : QCHUNK_GENERIC;
-      const int maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qchunk);
+      int maxi;
+      {
+        PhaseTimer t(PH_ITEMS, ws.st);
+        maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qchunk);
+      }
       const uint32_t *lim = nullptr;
       if (prm.max_scans >= 0) {  // :202-212
         ws.limits.ensure(sizeof(uint32_t) * nq * nparts);
@@ -713,6 +799,7 @@ struct IvfFlatIndex : Index {
       a.live = lists.live.as<uint8_t>();
       a.rnorm = lists.cosine ? lists.norms.as<float>() : nullptr;
       a.queries = d_q;
+      a.queries_t = ws.qt.as<float>();
       a.qnorm = qn;
       a.items = ws.items.as<ScanItem>();
       a.n_items = ws.nitems.as<int32_t>();
@@ -724,11 +811,15 @@ struct IvfFlatIndex : Index {
       a.dim = dim;
       a.part_s = ws.part_s.as<float>();
       a.part_k = ws.part_k.as<uint32_t>();
+      PhaseTimer t(PH_LIST_SCAN, ws.st, prof().on ? probed_rows(ws, nq, probes, le, lb) : 0);
       launch_scan(a, metric, 1, maxi, ws.st);
     }
-    if (bcut > 0)  // :170-180 exact buffer scan, keys KEY_BUF | slot
+    if (bcut > 0) {  // :170-180 exact buffer scan, keys KEY_BUF | slot
+      PhaseTimer t(PH_BUF_SCAN, ws.st, nq * bcut);
       flat_scan(buf.st, bcut, bp, d_q, qn, nq, k, 1, metric, nparts, probes, KEY_BUF, ws, ws.part_s.as<float>(),
                 ws.part_k.as<uint32_t>(), true);
+    }
+    PhaseTimer tm(PH_MERGE, ws.st);
     launch_merge_keys(ws.part_s.as<float>(), ws.part_k.as<uint32_t>(), nq, nparts, k, lists.labels.as<int64_t>(),
                       buf.st.labels.as<int64_t>(), d_s, d_l, nullptr, d_c, ws.st);
   }
@@ -776,6 +867,14 @@ struct IvfPqIndex : Index {
   int64_t ncode_rows = 0;
   bool built = false;
   int nprobe_default;
+  std::vector<float> given;
+  int given_k = 0;
+
+  void set_centroids(const float *c, int nl) override {
+    if (nl <= 0) throw Error(PYR_E_ARG, "nlist must be positive");
+    given.assign(c, c + (size_t)nl * dim);
+    given_k = nl;
+  }
 
   explicit IvfPqIndex(const pyr_index_desc &d) : Index(d) {
     M = d.pq_m;
@@ -839,8 +938,14 @@ struct IvfPqIndex : Index {
     int nc = (int)std::min<int64_t>(desc.nlist, n);   // :68
     if (nc <= 0) nc = 1;
     DevMem C;
-    C.ensure(sizeof(float) * nc * dim);
-    nc = kmeans_train_gpu(X.as<float>(), n, dim, nc, metric, 10, 123, C.as<float>(), wst);  // :69
+    if (given_k > 0) {
+      nc = given_k;
+      C.ensure(sizeof(float) * nc * dim);
+      HIPCHK(hipMemcpyAsync(C.p, given.data(), sizeof(float) * nc * dim, hipMemcpyHostToDevice, wst));
+    } else {
+      C.ensure(sizeof(float) * nc * dim);
+      nc = kmeans_train_gpu(X.as<float>(), n, dim, nc, metric, 10, 123, C.as<float>(), wst);  // :69
+    }
     DevMem A, R, S;
     A.ensure(sizeof(int32_t) * n);
     assign_gpu(X.as<float>(), n, dim, C.as<float>(), nc, metric, A.as<int32_t>(), wst);   // :79
@@ -926,13 +1031,16 @@ struct IvfPqIndex : Index {
       fill_empty_results(d_s, d_l, d_c, nq, k, ws.st);
       return;
     }
-    query_norms(d_q, nq, dim, metric, ws);
+    prep_queries(d_q, nq, dim, metric, ws);
     const float *qn = metric == COS ? ws.qn.as<float>() : nullptr;
     const size_t np = (size_t)nq * nparts * k;
     ws.part_s.ensure(sizeof(float) * np);
     ws.part_k.ensure(sizeof(uint32_t) * np);
     if (probes > 0) {
-      coarse.probe(d_q, qn, nq, probes, metric, ws);
+      {
+        PhaseTimer t(PH_COARSE, ws.st, nq * coarse.nlist);
+        coarse.probe(d_q, qn, nq, probes, metric, ws);
+      }
       const int qchunk = 32;
       const int maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qchunk);
       PqArgs a{};
@@ -956,11 +1064,15 @@ struct IvfPqIndex : Index {
       a.part_s = ws.part_s.as<float>();
       a.part_k = ws.part_k.as<uint32_t>();
       if (pq_scan_lds_bytes(dim, M, ksub, k) > 160 * 1024) throw Error(PYR_E_ARG, "PQ lookup table exceeds LDS");
+      PhaseTimer t(PH_PQ_SCAN, ws.st, prof().on ? probed_rows(ws, nq, probes, le, lb) : 0);
       launch_pq_scan(a, maxi, ws.st);
     }
-    if (bp.nchunks > 0)  // :130-136 exact buffer scan
+    if (bp.nchunks > 0) {  // :130-136 exact buffer scan
+      PhaseTimer t(PH_BUF_SCAN, ws.st, nq * bcut);
       flat_scan(buf.st, bcut, bp, d_q, qn, nq, k, 1, metric, nparts, probes, KEY_BUF, ws, ws.part_s.as<float>(),
                 ws.part_k.as<uint32_t>(), true);
+    }
+    PhaseTimer tm(PH_MERGE, ws.st);
     launch_merge_keys(ws.part_s.as<float>(), ws.part_k.as<uint32_t>(), nq, nparts, k, clabels.as<int64_t>(),
                       buf.st.labels.as<int64_t>(), d_s, d_l, nullptr, d_c, ws.st);
   }

@@ -45,6 +45,11 @@ struct DevMem {
   void ensure(size_t bytes);
   // make room for `bytes`; first `keep` bytes preserved (stream-ordered copy, then sync)
   void grow_keep(size_t bytes, size_t keep, hipStream_t st);
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
   template <class T>
   T *as() const {
     return reinterpret_cast<T *>(p);
@@ -76,7 +81,7 @@ struct Workspace {
   hipStream_t st = nullptr;
   bool own_stream = false;
   std::mutex m;
-  DevMem q, qn, items, nitems, items2, nitems2, qlist, part_s, part_k, probes, cpart_s, cpart_k, limits;
+  DevMem q, qn, qt, items, nitems, items2, nitems2, qlist, part_s, part_k, probes, cpart_s, cpart_k, limits;
   DevMem ivf_cnt, ivf_fill, ivf_qoff, ivf_ioff;
   DevMem out_s, out_l, out_c;
   ~Workspace() {
@@ -109,6 +114,11 @@ struct Index {
   }
   virtual void ivf_layout(int64_t *off, int64_t *labels, uint8_t *live, int64_t *total) const;
   virtual void pq_state(float *cb, int32_t *ksub, uint8_t *codes) const;
+  virtual void set_centroids(const float *c, int nlist) {
+    (void)c;
+    (void)nlist;
+    throw Error(PYR_E_STATE, "index kind has no coarse quantizer");
+  }
 
   std::unique_ptr<Workspace> take_ws();
   void give_ws(std::unique_ptr<Workspace> w);
@@ -149,6 +159,33 @@ struct NetRandom {  // System.Random legacy (Net5CompatSeedImpl); SURVEY.md Appe
 };
 
 Index *create_index(const pyr_index_desc &d);
+
+// kernel-phase profiler (pyr_profile_*): HIP events around each phase on the search stream
+enum Phase { PH_COARSE = 0, PH_ITEMS = 1, PH_LIST_SCAN = 2, PH_BUF_SCAN = 3, PH_MERGE = 4, PH_FLAT_SCAN = 5,
+             PH_PQ_SCAN = 6, PH_N = 8 };
+struct Profiler {
+  bool on = false;
+  std::mutex m;
+  double ms[PH_N] = {0};
+  int64_t calls[PH_N] = {0}, work[PH_N] = {0};
+  struct Rec {
+    int phase;
+    hipEvent_t a, b;
+    int64_t work;
+  };
+  std::vector<Rec> pending;
+  void drain();
+  void reset();
+};
+Profiler &prof();
+struct PhaseTimer {
+  int phase;
+  hipStream_t st;
+  hipEvent_t a = nullptr;
+  int64_t work;
+  PhaseTimer(int ph, hipStream_t s, int64_t w = 0);
+  ~PhaseTimer();
+};
 
 // shared building blocks
 void fill_empty_results(float *d_s, int64_t *d_l, int32_t *d_c, int64_t nq, int k, hipStream_t st);

@@ -32,7 +32,8 @@ struct ScanArgs {
   const float *rows;      // blocked [row/8][D][8]
   const uint8_t *live;    // per row, 1 = visible
   const float *rnorm;     // per row norms (cosine) or null
-  const float *queries;   // row-major nq x D
+  const float *queries;   // row-major nq x D (generic kernel)
+  const float *queries_t; // lane-major nq x D (fast kernel; launch_transpose_queries)
   const float *qnorm;     // per query norms (cosine) or null
   const ScanItem *items;
   const int32_t *n_items; // device count (items beyond it exit)
@@ -54,6 +55,9 @@ void launch_scan(const ScanArgs &a, int metric, int V, int max_items, hipStream_
 // Returns item count (also written to *d_nitems).
 int make_flat_items(ScanItem *d_items, int32_t *d_nitems, int64_t nrows, int32_t chunk_rows, int64_t nq,
                     int32_t part_off, int32_t qchunk, hipStream_t st);
+
+// fast-scan query layout: qt[q][l][t] = q[q][8t + l]
+void launch_transpose_queries(const float *q, int64_t nq, int32_t dim, float *qt, hipStream_t st);
 
 // Per-row / per-query norms (VectorMath.ComputeNorm).  blocked != 0: rows in blocked layout.
 void launch_norms(const float *x, int64_t n, int32_t dim, int blocked, float *out, hipStream_t st);

@@ -17,6 +17,7 @@
 
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 
 #include "kernels.h"
 
@@ -216,26 +217,30 @@ __device__ __forceinline__ void list_insert(float *ls, uint32_t *lk, int &cnt, i
 // ---------------------------------------------------------------------------
 // Fast scan: D in {32,64,96,128}, k <= 64.
 // Workgroup = 256 threads = 32 "slots" x 8 lanes.  Slot s owns queries
-// 4s..4s+3 of the item (held in registers); lane l of a slot owns Vector<float>
-// lane l, i.e. dims l, l+8, l+16, ...  Rows stream through LDS one 8-row group
-// at a time (double buffered).  Per group each slot computes 4 x 8 pairs with
-// packed fp32 math (v_pk_add/mul_f32), then the 8 lanes of a slot combine their
-// partial sums with the reference's horizontal tree by a DPP transpose-reduce
-// (quad_perm xor1, quad_perm xor2, row_half_mirror), leaving each lane with the
-// 4 scores of one row.  Scores go to an LDS matrix; one owner thread per query
-// keeps that query's sorted top-k in LDS.
+// 4s..4s+3 of the item (held in registers, dims of two Vector blocks packed in
+// one VGPR pair and broadcast with op_sel); lane l of a slot owns Vector<float>
+// lane l, i.e. dims l, l+8, l+16, ...  Rows stream through LDS in stages of
+// GPS 8-row groups (double buffered, one barrier per stage).  Per group each
+// slot computes 4 x 8 pairs with packed fp32 math (v_pk_add/mul_f32: sub, mul,
+// add per element, phase-ordered so no dependent pair is adjacent), then the 8
+// lanes of a slot combine their partial sums with the reference's horizontal
+// tree by a DPP transpose-reduce (quad_perm xor1, quad_perm xor2,
+// row_half_mirror), leaving each lane with the 4 scores of one row.  Scores go
+// to an LDS matrix; one owner thread per query filters them against its k-th
+// best (branch-free) and keeps that query's sorted top-k in LDS.
 // ---------------------------------------------------------------------------
-template <int D, int V, int MET>
+template <int D, int V, int MET, int GPS>
 __global__ __launch_bounds__(256) void scan_fast(ScanArgs a) {
-  constexpr int T = D / 8;
+  constexpr int T = D / 8;              // Vector<float> blocks per row
+  constexpr int GF = D * 8;             // floats per 8-row group
   extern __shared__ __attribute__((aligned(16))) float smem[];
   if ((int)blockIdx.x >= *a.n_items) return;
   const ScanItem it = a.items[blockIdx.x];
   const int k = a.k;
-  float *tile = smem;                  // [2][D*8]
-  float *sc = smem + 2 * D * 8;        // [2][8][SCS]
-  float *tks = sc + 2 * 8 * SCS;       // [QCHUNK][k]
-  uint32_t *tkk = (uint32_t *)(tks + QCHUNK * k);
+  float *tile = smem;                            // [2][GPS*GF]
+  float *sc = smem + 2 * GPS * GF;               // [2][GPS*8][SCS]
+  float *tks = sc + 2 * GPS * 8 * SCS;           // [QCHUNK][k]
+  uint32_t *tkk = reinterpret_cast<uint32_t *>(tks + QCHUNK * k);
 
   const int tid = threadIdx.x;
   const int l = tid & 7, s = tid >> 3;
@@ -243,6 +248,9 @@ __global__ __launch_bounds__(256) void scan_fast(ScanArgs a) {
   const int myj = c1 | (c2 << 1) | (c3 << 2);
   const bool wave_active = (tid >> 6) * 32 < it.qcnt;
 
+  // queries arrive lane-major (transpose_queries): lane l's dims l, l+8, ... are
+  // contiguous and load as float4; kept as plain scalars (packed FP32 has no extra
+  // rate on gfx950 and its op_sel broadcast would double the register footprint).
   float q[4][T];
   float qn[4];
 #pragma unroll
@@ -251,9 +259,15 @@ __global__ __launch_bounds__(256) void scan_fast(ScanArgs a) {
     qn[u] = 0.0f;
     if (i < it.qcnt) {
       const int qi = a.qlist ? a.qlist[it.qbeg + i] / a.nparts : it.qbeg + i;
-      const float *qp = a.queries + (size_t)qi * D + l;
+      const float4 *qp = reinterpret_cast<const float4 *>(a.queries_t + (size_t)qi * D + l * T);
 #pragma unroll
-      for (int t = 0; t < T; ++t) q[u][t] = qp[8 * t];
+      for (int p = 0; p < T / 4; ++p) {
+        const float4 v = qp[p];
+        q[u][4 * p] = v.x;
+        q[u][4 * p + 1] = v.y;
+        q[u][4 * p + 2] = v.z;
+        q[u][4 * p + 3] = v.w;
+      }
       if (MET == COS) qn[u] = a.qnorm[qi];
     } else {
 #pragma unroll
@@ -269,153 +283,219 @@ __global__ __launch_bounds__(256) void scan_fast(ScanArgs a) {
     if (a.limits) lim = a.limits[oslot];
   }
   int cnt = 0;
-  float thr_s = -INFINITY;
+  float thr_s = -INFINITY;  // (-inf, NONE) lets every real candidate pass until the list is full
   uint32_t thr_k = KEY_NONE;
   float *ls = tks + tid * k;
   uint32_t *lk = tkk + tid * k;
 
   const int g0 = it.row_begin >> 3;
   const int ng = ((it.row_end + 7) >> 3) - g0;
+  const int nst = (ng + GPS - 1) / GPS;
+  // Register staging of the next stage: the loads are issued at the top of stage st
+  // (pinned there by sched_barrier so the scheduler cannot sink them behind the
+  // compute) and written to the other LDS buffer after the compute, so their HBM
+  // latency hides under a whole stage of VALU work.
+  constexpr int NV = GPS * D * 2;  // float4 per stage
+  constexpr int LOADS = (NV + 255) / 256;
   const float4 *src = reinterpret_cast<const float4 *>(a.rows);
-  constexpr int NV = D * 2;  // float4 per group
-  float4 pf;
-  if (ng > 0) {
-    if (tid < NV) reinterpret_cast<float4 *>(tile)[tid] = src[(size_t)g0 * NV + tid];
+  float4 pf[LOADS];
+#define PYR_LOAD_STAGE(STG)                                                                     \
+  _Pragma("unroll") for (int i = 0; i < LOADS; ++i) {                                          \
+    const int v = min(tid + 256 * i, NV - 1);                                                   \
+    const int gg = min((STG) * GPS + v / (2 * D), ng - 1); /* clamp: rows past the end unused */ \
+    pf[i] = src[(size_t)(g0 + gg) * (2 * D) + v % (2 * D)];                                     \
+  }
+#define PYR_STORE_STAGE(BUF)                                                                    \
+  _Pragma("unroll") for (int i = 0; i < LOADS; ++i) {                                          \
+    const int v = tid + 256 * i;                                                                \
+    if (v < NV) reinterpret_cast<float4 *>(tile + (BUF) * GPS * GF)[v] = pf[i];                 \
+  }
+  float xn_next[GPS], xn_cur[GPS];  // cosine row norms, prefetched one stage ahead
+#pragma unroll
+  for (int g = 0; g < GPS; ++g) xn_next[g] = xn_cur[g] = 0.0f;
+  if (nst > 0) {
+    if (MET == COS) {
+#pragma unroll
+      for (int g = 0; g < GPS; ++g) xn_next[g] = a.rnorm[(size_t)(g0 + min(g, ng - 1)) * 8 + myj];
+    }
+    PYR_LOAD_STAGE(0)
+    PYR_STORE_STAGE(0)
   }
   __syncthreads();
 
-  for (int n = 0; n < ng; ++n) {
-    const int cur = n & 1;
-    const bool more = n + 1 < ng;
-    if (more && tid < NV) pf = src[(size_t)(g0 + n + 1) * NV + tid];
+  for (int st = 0; st < nst; ++st) {
+    const int cur = st & 1;
+    const bool more = st + 1 < nst;
+    if (MET == COS) {
+#pragma unroll
+      for (int g = 0; g < GPS; ++g) {
+        xn_cur[g] = xn_next[g];  // retired by the previous barrier
+        xn_next[g] = a.rnorm[(size_t)(g0 + min((st + 1) * GPS + g, ng - 1)) * 8 + myj];
+      }
+    }
+    {
+      const int nxt = more ? st + 1 : st;
+      PYR_LOAD_STAGE(nxt)
+    }
+    __builtin_amdgcn_sched_barrier(0);
 
     if (wave_active) {
-      const float *tp = tile + cur * D * 8 + l * 8;
-      float fin[4][8];
-      if constexpr (V == 1) {
-        f2 acc[4][4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+      for (int g = 0; g < GPS; ++g) {
+        if (st * GPS + g >= ng) break;
+        const float *tp = tile + cur * GPS * GF + g * GF + l * 8;
+        float fin[4][8];
+        if constexpr (V == 1) {
+          // 4 queries x 8 rows per slot, one accumulator per (query, row) for lane l of
+          // the single Vector accumulator (VectorMath.cs:52-58).  LDS reads are
+          // software-pipelined one t-step ahead; sched_barrier pins the order.
+          float acc[4][8];
 #pragma unroll
-          for (int jp = 0; jp < 4; ++jp) acc[u][jp] = f2{0.0f, 0.0f};
+          for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int t = 0; t < T; ++t) {
-          const float4 x0 = *reinterpret_cast<const float4 *>(tp + t * 64);
-          const float4 x1 = *reinterpret_cast<const float4 *>(tp + t * 64 + 4);
-          const f2 xx[4] = {f2{x0.x, x0.y}, f2{x0.z, x0.w}, f2{x1.x, x1.y}, f2{x1.z, x1.w}};
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const f2 qq = f2{q[u][t], q[u][t]};
-#pragma unroll
-            for (int jp = 0; jp < 4; ++jp) {
-              if constexpr (MET == L2) {
-                const f2 d = qq - xx[jp];
-                acc[u][jp] = acc[u][jp] + d * d;
-              } else {
-                acc[u][jp] = acc[u][jp] + qq * xx[jp];
-              }
-            }
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-          for (int jp = 0; jp < 4; ++jp) {
-            fin[u][2 * jp] = acc[u][jp].x;
-            fin[u][2 * jp + 1] = acc[u][jp].y;
-          }
-      } else {
-        // four Vector accumulators: acc[v] sums dims 32s + 8v + l (VectorMath.cs:197-221)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          f2 acc[4][4][2];
-#pragma unroll
-          for (int v = 0; v < 4; ++v)
-#pragma unroll
-            for (int u = 0; u < 4; ++u) acc[v][u][0] = acc[v][u][1] = f2{0.0f, 0.0f};
+            for (int j = 0; j < 8; ++j) acc[u][j] = 0.0f;
+          float4 xa = *reinterpret_cast<const float4 *>(tp);
+          float4 xb = *reinterpret_cast<const float4 *>(tp + 4);
 #pragma unroll
           for (int t = 0; t < T; ++t) {
-            const int v = t & 3;
-            const float4 x0 = *reinterpret_cast<const float4 *>(tp + t * 64 + 4 * h);
-            const f2 xx[2] = {f2{x0.x, x0.y}, f2{x0.z, x0.w}};
+            float4 na = xa, nb = xb;
+            if (t + 1 < T) {
+              na = *reinterpret_cast<const float4 *>(tp + (t + 1) * 64);
+              nb = *reinterpret_cast<const float4 *>(tp + (t + 1) * 64 + 4);
+            }
+            const float xs[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-              const f2 qq = f2{q[u][t], q[u][t]};
+              float d[8];
+              if constexpr (MET == L2) {
 #pragma unroll
-              for (int jp = 0; jp < 2; ++jp) {
-                if constexpr (MET == L2) {
-                  const f2 d = qq - xx[jp];
-                  acc[v][u][jp] = acc[v][u][jp] + d * d;
-                } else {
-                  acc[v][u][jp] = acc[v][u][jp] + qq * xx[jp];
-                }
+                for (int j = 0; j < 8; ++j) d[j] = q[u][t] - xs[j];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) d[j] = d[j] * d[j];
+              } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) d[j] = q[u][t] * xs[j];
               }
+#pragma unroll
+              for (int j = 0; j < 8; ++j) acc[u][j] = acc[u][j] + d[j];
             }
+            xa = na;
+            xb = nb;
           }
 #pragma unroll
           for (int u = 0; u < 4; ++u)
 #pragma unroll
-            for (int jp = 0; jp < 2; ++jp) {
-              const f2 f = ((acc[0][u][jp] + acc[1][u][jp]) + acc[2][u][jp]) + acc[3][u][jp];  // :224
-              fin[u][4 * h + 2 * jp] = f.x;
-              fin[u][4 * h + 2 * jp + 1] = f.y;
+            for (int j = 0; j < 8; ++j) fin[u][j] = acc[u][j];
+        } else {
+          // four Vector accumulators: acc[v] sums dims 32s + 8v + l (VectorMath.cs:197-221),
+          // rows in two halves of 4 to bound the register tile
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            float acc[4][4][4];
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+#pragma unroll
+              for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[v][u][j] = 0.0f;
+            float4 xa = *reinterpret_cast<const float4 *>(tp + 4 * h);
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+              const int v = t & 3;
+              float4 na = xa;
+              if (t + 1 < T) na = *reinterpret_cast<const float4 *>(tp + (t + 1) * 64 + 4 * h);
+              const float xs[4] = {xa.x, xa.y, xa.z, xa.w};
+#pragma unroll
+              for (int u = 0; u < 4; ++u) {
+                float d[4];
+                if constexpr (MET == L2) {
+#pragma unroll
+                  for (int j = 0; j < 4; ++j) d[j] = q[u][t] - xs[j];
+#pragma unroll
+                  for (int j = 0; j < 4; ++j) d[j] = d[j] * d[j];
+                } else {
+#pragma unroll
+                  for (int j = 0; j < 4; ++j) d[j] = q[u][t] * xs[j];
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[v][u][j] = acc[v][u][j] + d[j];
+              }
+              xa = na;
             }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+              for (int j = 0; j < 4; ++j)
+                fin[u][4 * h + j] = ((acc[0][u][j] + acc[1][u][j]) + acc[2][u][j]) + acc[3][u][j];  // :224
+          }
         }
-      }
-      // transpose-reduce = Vector.Dot(acc, One) tree, one row per lane at the end
-      float r1[4][4], r2[4][2], r3[4];
+        // transpose-reduce = Vector.Dot(acc, One) tree, one row per lane at the end
+        float r1[4][4], r2[4][2], r3[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int jp = 0; jp < 4; ++jp) {
-          const float x0 = fin[u][2 * jp], x1 = fin[u][2 * jp + 1];
-          const float keep = c1 ? x1 : x0, send = c1 ? x0 : x1;
-          r1[u][jp] = keep + dpp<0xB1>(send);
+          for (int jp = 0; jp < 4; ++jp) {
+            const float x0 = fin[u][2 * jp], x1 = fin[u][2 * jp + 1];
+            const float keep = c1 ? x1 : x0, send = c1 ? x0 : x1;
+            r1[u][jp] = keep + dpp<0xB1>(send);
+          }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int jq = 0; jq < 2; ++jq) {
+            const float x0 = r1[u][2 * jq], x1 = r1[u][2 * jq + 1];
+            const float keep = c2 ? x1 : x0, send = c2 ? x0 : x1;
+            r2[u][jq] = keep + dpp<0x4E>(send);
+          }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float x0 = r2[u][0], x1 = r2[u][1];
+          const float keep = c3 ? x1 : x0, send = c3 ? x0 : x1;
+          r3[u] = keep + dpp<0x141>(send);
         }
+        float sv[4];
+        const float xn = xn_cur[g];
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int jq = 0; jq < 2; ++jq) {
-          const float x0 = r1[u][2 * jq], x1 = r1[u][2 * jq + 1];
-          const float keep = c2 ? x1 : x0, send = c2 ? x0 : x1;
-          r2[u][jq] = keep + dpp<0x4E>(send);
+        for (int u = 0; u < 4; ++u) {
+          const float sum = 0.0f + r3[u];  // `sum += Vector.Dot(...)` with sum = 0f
+          if (MET == L2) sv[u] = -sum;
+          else if (MET == IP) sv[u] = sum;
+          else sv[u] = (qn[u] < 1e-6f || xn < 1e-6f) ? 0.0f : sum / (qn[u] * xn);
         }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float x0 = r2[u][0], x1 = r2[u][1];
-        const float keep = c3 ? x1 : x0, send = c3 ? x0 : x1;
-        r3[u] = keep + dpp<0x141>(send);
+        *reinterpret_cast<float4 *>(sc + (cur * GPS * 8 + g * 8 + myj) * SCS + s * 4) =
+            make_float4(sv[0], sv[1], sv[2], sv[3]);
       }
-      float sv[4];
-      float xn = 0.0f;
-      if (MET == COS) xn = a.rnorm[(size_t)(g0 + n) * 8 + myj];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float sum = 0.0f + r3[u];  // `sum += Vector.Dot(...)` with sum = 0f
-        if (MET == L2) sv[u] = -sum;
-        else if (MET == IP) sv[u] = sum;
-        else sv[u] = (qn[u] < 1e-6f || xn < 1e-6f) ? 0.0f : sum / (qn[u] * xn);
-      }
-      *reinterpret_cast<float4 *>(sc + cur * 8 * SCS + myj * SCS + s * 4) = make_float4(sv[0], sv[1], sv[2], sv[3]);
     }
-    if (more && tid < NV) reinterpret_cast<float4 *>(tile + (cur ^ 1) * D * 8)[tid] = pf;
+    PYR_STORE_STAGE(cur ^ 1)  // after the last stage this fills an unused buffer
     __syncthreads();
 
     if (owner) {
-      const float *scp = sc + cur * 8 * SCS + tid;
-      const int rb = (g0 + n) * 8;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int r = rb + j;
-        const float v = scp[j * SCS];
-        const uint32_t key = a.key_base | (uint32_t)r;
-        if (r >= it.row_end || r < it.row_begin) continue;
-        if (cnt == k && !better(v, key, thr_s, thr_k)) continue;
-        if ((uint32_t)r >= lim || !a.live[r]) continue;
-        list_insert(ls, lk, cnt, k, v, key);
-        if (cnt == k) {
-          thr_s = ls[k - 1];
-          thr_k = lk[k - 1];
+      for (int g = 0; g < GPS; ++g) {
+        if (st * GPS + g >= ng) break;
+        const float *scp = sc + (cur * GPS * 8 + g * 8) * SCS + tid;
+        const int rb = (g0 + st * GPS + g) * 8;
+        float v[8];
+        unsigned pass = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          v[j] = scp[j * SCS];
+          const int r = rb + j;
+          if (r < it.row_end && better(v[j], a.key_base | (uint32_t)r, thr_s, thr_k)) pass |= 1u << j;
+        }
+        if (pass) {  // rare once the list is full
+          for (int j = 0; j < 8; ++j) {
+            if (!((pass >> j) & 1)) continue;
+            const int r = rb + j;
+            const uint32_t key = a.key_base | (uint32_t)r;
+            const float vj = scp[j * SCS];
+            if (!better(vj, key, thr_s, thr_k) || (uint32_t)r >= lim || !a.live[r]) continue;
+            list_insert(ls, lk, cnt, k, vj, key);
+            if (cnt == k) {
+              thr_s = ls[k - 1];
+              thr_k = lk[k - 1];
+            }
+          }
         }
       }
     }
@@ -428,6 +508,8 @@ __global__ __launch_bounds__(256) void scan_fast(ScanArgs a) {
       pk[j] = j < cnt ? lk[j] : KEY_NONE;
     }
   }
+#undef PYR_LOAD_STAGE
+#undef PYR_STORE_STAGE
 }
 
 // ---------------------------------------------------------------------------
@@ -482,6 +564,16 @@ __global__ void flat_items_kernel(ScanItem *items, int32_t *n_items, int nchunks
   it.part = part_off + c;
   it.list = 0;
   items[id] = it;
+}
+
+// queries row-major -> lane-major: qt[q][l][t] = q[q][8t + l] (fast-scan register layout)
+__global__ void transpose_queries_kernel(const float *q, int64_t nq, int D, float *qt) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nq * D) return;
+  const int64_t i = e / D;
+  const int r = (int)(e % D);
+  const int T = D / 8, l = r / T, t = r % T;
+  qt[e] = q[(size_t)i * D + 8 * t + l];
 }
 
 __global__ void norms_kernel(const float *x, int64_t n, int dim, int blocked, float *out) {
@@ -999,16 +1091,28 @@ __global__ void fill_results_kernel(float *s, int64_t *l, int32_t *c, int64_t nq
 
 inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
-template <int D, int V, int MET>
-void launch_fast_t(const ScanArgs &a, int max_items, hipStream_t st) {
-  const size_t lds = (size_t)(2 * D * 8 + 2 * 8 * SCS + QCHUNK * a.k * 2) * sizeof(float);
+template <int D, int V, int MET, int GPS>
+void launch_fast_g(const ScanArgs &a, int max_items, hipStream_t st) {
+  const size_t lds = (size_t)(2 * GPS * D * 8 + 2 * GPS * 8 * SCS + QCHUNK * a.k * 2) * sizeof(float);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&scan_fast<D, V, MET>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&scan_fast<D, V, MET, GPS>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((scan_fast<D, V, MET>), dim3(max_items), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((scan_fast<D, V, MET, GPS>), dim3(max_items), dim3(256), lds, st, a);
+}
+
+// 8-row groups per LDS stage (default 1; PYR_GPS=2 for A/B measurement)
+int stage_groups() {
+  const char *e = getenv("PYR_GPS");
+  return (e && atoi(e) == 2) ? 2 : 1;
+}
+
+template <int D, int V, int MET>
+void launch_fast_t(const ScanArgs &a, int max_items, hipStream_t st) {
+  if (stage_groups() == 1) launch_fast_g<D, V, MET, 1>(a, max_items, st);
+  else launch_fast_g<D, V, MET, 2>(a, max_items, st);
 }
 
 template <int V, int MET>
@@ -1041,7 +1145,7 @@ bool fast_path(int dim, int k) { return k <= KMAX_FAST && (dim == 32 || dim == 6
 
 void launch_scan(const ScanArgs &a, int metric, int V, int max_items, hipStream_t st) {
   if (max_items <= 0) return;
-  if (fast_path(a.dim, a.k)) {
+  if (fast_path(a.dim, a.k) && a.queries_t) {
     switch (a.dim) {
       case 32: launch_fast_v<32>(a, metric, V, max_items, st); return;
       case 64: launch_fast_v<64>(a, metric, V, max_items, st); return;
@@ -1068,6 +1172,11 @@ int make_flat_items(ScanItem *d_items, int32_t *d_nitems, int64_t nrows, int32_t
   hipLaunchKernelGGL(flat_items_kernel, dim3(nblk(n > 0 ? n : 1, 256)), dim3(256), 0, st, d_items, d_nitems, nchunks,
                      nqc, chunk_rows, nrows, nq, part_off, qchunk);
   return n;
+}
+
+void launch_transpose_queries(const float *q, int64_t nq, int32_t dim, float *qt, hipStream_t st) {
+  if (nq <= 0) return;
+  hipLaunchKernelGGL(transpose_queries_kernel, dim3(nblk(nq * dim, 256)), dim3(256), 0, st, q, nq, dim, qt);
 }
 
 void launch_norms(const float *x, int64_t n, int32_t dim, int blocked, float *out, hipStream_t st) {

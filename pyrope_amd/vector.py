@@ -211,6 +211,11 @@ class HipVectorIndex(IVectorIndex):
                                               C.c_void_p(d_scores), C.c_void_p(d_labels),
                                               C.c_void_p(d_counts or None), C.c_void_p(stream or None)))
 
+    def set_centroids(self, centroids: np.ndarray) -> None:
+        """Supply the coarse quantizer used by the next build() (pyr_index_set_centroids)."""
+        c = np.ascontiguousarray(centroids, dtype=np.float32).reshape(-1, self.dimension)
+        check(self._L.pyr_index_set_centroids(self._h, ptr(c, C.c_float), c.shape[0]))
+
     def get_stats(self) -> IndexStats:
         cnt = C.c_int64()
         check(self._L.pyr_index_stats(self._h, C.byref(cnt), None, None))
@@ -409,6 +414,18 @@ class VectorIndexRegistry:
 
     def try_get_index(self, tenant: str, index: str) -> Optional[DeltaVectorIndex]:
         return self._indices.get(f"{tenant}:{index}")
+
+
+def kmeans_train(data: np.ndarray, k: int, metric: VectorMetric, max_iter: int = 10, seed: int = 42,
+                 device: int = 0) -> np.ndarray:
+    """KMeansUtils.Train (KMeansUtils.cs:10-68) on the GPU (pyr_kmeans_train)."""
+    x = np.ascontiguousarray(data, dtype=np.float32)
+    n, dim = x.shape
+    out = np.zeros((max(1, min(max(k, 1), max(n, 1))), dim), np.float32)
+    used = C.c_int32()
+    check(_lib.load().pyr_kmeans_train(device, ptr(x, C.c_float), n, dim, k, int(metric), max_iter, seed,
+                                       ptr(out, C.c_float), C.byref(used)))
+    return out[: used.value]
 
 
 def generate_synthetic(count: int, dim: int, seed: int) -> np.ndarray:

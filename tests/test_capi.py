@@ -1,0 +1,84 @@
+"""The C-ABI library builds, loads and exports every symbol include/pyrope_ann.h declares.
+
+CPU-only: no compute call reaches a GPU here.  Where no device exists the product
+path must fail loudly (PYR_E_DEVICE), never fall back to the CPU.
+"""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "pyrope_ann.h")
+
+
+def _declared():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(pyr_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_the_boundary():
+    names = _declared()
+    for must in ["pyr_index_create", "pyr_index_add", "pyr_index_upsert", "pyr_index_remove", "pyr_index_build",
+                 "pyr_index_search", "pyr_index_search_device", "pyr_index_stats", "pyr_index_get_centroids",
+                 "pyr_merge_topk_device", "pyr_last_error"]:
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol(hiplib):
+    for name in _declared():
+        assert hasattr(hiplib, name), name
+
+
+def test_binding_covers_every_declared_symbol():
+    from pyrope_amd import _lib
+    assert set(_declared()) == set(_lib.SIGNATURES), set(_declared()) ^ set(_lib.SIGNATURES)
+
+
+def test_version(hiplib):
+    assert b"gfx950" in hiplib.pyr_version()
+
+
+def test_generate_synthetic_matches_oracle(hiplib, oracle):
+    from pyrope_amd import generate_synthetic
+    np.testing.assert_array_equal(generate_synthetic(100, 16, 42), oracle.generate_vectors(100, 16, 42))
+    np.testing.assert_array_equal(generate_synthetic(3, 5, 1337), oracle.generate_vectors(3, 5, 1337))
+
+
+def _has_gpu():
+    try:
+        import torch
+        return torch.cuda.device_count() > 0
+    except Exception:
+        return False
+
+
+@pytest.mark.skipif(_has_gpu(), reason="checks the no-device failure path")
+def test_no_device_fails_loudly(hiplib):
+    from pyrope_amd import BruteForceVectorIndex, DeviceError, VectorMetric, kmeans_train
+    with pytest.raises(DeviceError):
+        BruteForceVectorIndex(4, VectorMetric.L2)
+    with pytest.raises(DeviceError):
+        kmeans_train(np.zeros((4, 4), np.float32), 2, VectorMetric.L2)
+
+
+def test_null_arguments_are_rejected(hiplib):
+    from pyrope_amd import _lib
+    assert hiplib.pyr_index_create(None, None) == _lib.PYR_E_ARG
+    assert b"null" in hiplib.pyr_last_error()
+    assert hiplib.pyr_index_search(None, None, 0, 10, None, None, None, None) == _lib.PYR_E_ARG
+    assert hiplib.pyr_merge_topk_device(None, None, 1, 0, 10, None, None, None) == _lib.PYR_E_ARG
+    assert hiplib.pyr_generate_synthetic(-1, 4, 1, None) == _lib.PYR_E_ARG
+    hiplib.pyr_index_destroy(None)  # no-op
+
+
+def test_status_mapping():
+    from pyrope_amd import _lib
+    for st, exc in [(_lib.PYR_E_DIM, _lib.ArgumentException), (_lib.PYR_E_DUPLICATE, _lib.InvalidOperationException),
+                    (_lib.PYR_E_STATE, _lib.InvalidOperationException), (_lib.PYR_E_DEVICE, _lib.DeviceError)]:
+        with pytest.raises(exc):
+            _lib.check(st)
+    _lib.check(_lib.PYR_OK)
