@@ -48,10 +48,16 @@ void RowStore::reserve(int64_t slots, hipStream_t st) {
   rows.grow_keep(sizeof(float) * nc * dim, sizeof(float) * cap * dim, st);
   live.grow_keep(nc, cap, st);
   labels.grow_keep(sizeof(int64_t) * nc, sizeof(int64_t) * cap, st);
+  rsq.grow_keep(sizeof(float) * nc, sizeof(float) * cap, st);
   if (cosine) norms.grow_keep(sizeof(float) * nc, sizeof(float) * cap, st);
+  if (!rmax.p) {
+    rmax.ensure(sizeof(uint32_t));
+    HIPCHK(hipMemsetAsync(rmax.p, 0, sizeof(uint32_t), st));  // below score_key of any float
+  }
   // new tail: not visible, zero rows (padding rows of a group are never scored)
   HIPCHK(hipMemsetAsync(live.as<uint8_t>() + cap, 0, nc - cap, st));
   HIPCHK(hipMemsetAsync(rows.as<float>() + cap * dim, 0, sizeof(float) * (nc - cap) * dim, st));
+  HIPCHK(hipMemsetAsync(rsq.as<float>() + cap, 0, sizeof(float) * (nc - cap), st));
   if (cosine) HIPCHK(hipMemsetAsync(norms.as<float>() + cap, 0, sizeof(float) * (nc - cap), st));
   cap = nc;
 }
@@ -70,6 +76,7 @@ void RowStore::write(const float *x, const int64_t *slots, const int64_t *labs, 
   launch_scatter_i64(labels.as<int64_t>(), di, di + cnt, cnt, st);
   launch_scatter_u8(live.as<uint8_t>(), di, 1, cnt, st);
   if (cosine) launch_norms_slots(rows.as<float>(), di, cnt, dim, norms.as<float>(), st);
+  launch_sqnorms(rows.as<float>(), di, cnt, dim, rsq.as<float>(), rmax.as<uint32_t>(), st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(st));  // staging buffers are reused by the next call
   if (stage_x.n > (size_t(256) << 20)) stage_x.release();  // bulk loads: do not pin GBs of staging
@@ -195,7 +202,7 @@ static ScanPlan plan_flat(int64_t nrows, int64_t nq, int dim, int k, int max_par
 // scan rows [0,nrows) of `rs` for all queries into partial slots q*nparts + part_off + c
 static void flat_scan(const RowStore &rs, int64_t nrows, const ScanPlan &p, const float *d_q, const float *d_qn,
                       int64_t nq, int k, int V, int met, int nparts, int part_off, uint32_t key_base, Workspace &ws,
-                      float *part_s, uint32_t *part_k, bool second = false) {
+                      float *part_s, uint32_t *part_k, bool second = false, uint32_t *gthr = nullptr) {
   DevMem &items = second ? ws.items2 : ws.items;
   DevMem &nitems = second ? ws.nitems2 : ws.nitems;
   items.ensure(sizeof(ScanItem) * std::max(p.nitems, 1));
@@ -218,7 +225,95 @@ static void flat_scan(const RowStore &rs, int64_t nrows, const ScanPlan &p, cons
   a.dim = rs.dim;
   a.part_s = part_s;
   a.part_k = part_k;
+  a.gthr = gthr;
   launch_scan(a, met, V, p.nitems, ws.st);
+}
+
+// Per-query shared top-k bound of one search (ScanArgs::gthr), reset to -inf.
+// PYR_GTHR=0 disables it (A/B measurement); results are identical either way.
+static bool bounds_enabled() {
+  const char *e = getenv("PYR_GTHR");
+  return !(e && atoi(e) == 0);
+}
+static uint32_t *shared_bounds(Workspace &ws, int64_t nq) {
+  if (!bounds_enabled() || nq <= 0) return nullptr;
+  ws.gthr.ensure(sizeof(uint32_t) * nq);
+  HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ws.gthr.p), (int)score_key(-INFINITY), nq, ws.st));
+  return ws.gthr.as<uint32_t>();
+}
+
+// ---------------------------------------------------------------------------
+// MFMA candidate filter + exact refine (filter.hip).  Same results as the exact scans
+// (certified per query, failures re-run exactly); PYR_FILTER=0 forces the exact scans,
+// PYR_FILTER_MARGIN sets K1 - k (default 8).
+// ---------------------------------------------------------------------------
+static bool filter_enabled() {
+  const char *e = getenv("PYR_FILTER");
+  return !(e && atoi(e) == 0);
+}
+static int filter_k1(int k) {
+  int m = 8;
+  if (const char *e = getenv("PYR_FILTER_MARGIN")) m = std::max(0, atoi(e));
+  return std::min(64, k + m);
+}
+
+// merge the K1-candidate partials, re-score exactly, certify; returns the number of
+// queries whose certificate failed (listed in ws.fail).  Synchronizes ws.st.
+static int64_t filter_finish(Workspace &ws, int64_t nq, int nparts, int k1, int k, int dim, int met, int V,
+                             const float *d_q, const RowStore &rs, const MergeIvf *mi, float *d_s, int64_t *d_l,
+                             int32_t *d_c) {
+  ws.ms.ensure(sizeof(float) * nq * k1);
+  ws.mk.ensure(sizeof(int32_t) * nq * k1);
+  {
+    PhaseTimer t(PH_MERGE, ws.st);
+    launch_merge_keys(ws.part_s.as<float>(), ws.part_k.as<uint32_t>(), nq, nparts, k1, nullptr, nullptr,
+                      ws.ms.as<float>(), nullptr, ws.mk.as<int32_t>(), nullptr, ws.st, mi);
+  }
+  ws.fail.ensure(sizeof(int32_t) * nq);
+  ws.fail_cnt.ensure(sizeof(int32_t));
+  HIPCHK(hipMemsetAsync(ws.fail_cnt.p, 0, sizeof(int32_t), ws.st));
+  RefineArgs r{};
+  r.rows = rs.rows.as<float>();
+  r.row_labels = rs.labels.as<int64_t>();
+  r.queries = d_q;
+  r.ms = ws.ms.as<float>();
+  r.mk = ws.mk.as<int32_t>();
+  r.max_rsq = rs.rmax.as<uint32_t>();
+  r.nq = nq;
+  r.k1 = k1;
+  r.k = k;
+  r.dim = dim;
+  r.c_err = 4.0 * dim + 64.0;
+  r.out_s = d_s;
+  r.out_l = d_l;
+  r.out_c = d_c;
+  r.fail_list = ws.fail.as<int32_t>();
+  r.fail_cnt = ws.fail_cnt.as<int32_t>();
+  {
+    PhaseTimer t(PH_REFINE, ws.st, nq * k1);
+    launch_refine(r, met, V, ws.st);
+  }
+  HIPCHK(hipGetLastError());
+  int32_t nf = 0;
+  HIPCHK(hipMemcpyAsync(&nf, ws.fail_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, ws.st));
+  HIPCHK(hipStreamSynchronize(ws.st));
+  return nf;
+}
+
+// re-run the listed queries through the exact scan and put their rows in place
+template <class F>
+static void filter_fallback(Workspace &ws, int64_t nf, const float *d_q, int dim, int k, float *d_s, int64_t *d_l,
+                            int32_t *d_c, F &&exact) {
+  if (nf <= 0) return;
+  PhaseTimer t(PH_FALLBACK, ws.st, nf);
+  ws.fq.ensure(sizeof(float) * nf * dim);
+  ws.fs.ensure(sizeof(float) * nf * k);
+  ws.fl.ensure(sizeof(int64_t) * nf * k);
+  ws.fc.ensure(sizeof(int32_t) * nf);
+  launch_gather_queries(d_q, ws.fail.as<int32_t>(), nf, dim, ws.fq.as<float>(), ws.st);
+  exact(ws.fq.as<float>(), nf, ws.fs.as<float>(), ws.fl.as<int64_t>(), ws.fc.as<int32_t>());
+  launch_scatter_results(ws.fail.as<int32_t>(), nf, k, ws.fs.as<float>(), ws.fl.as<int64_t>(), ws.fc.as<int32_t>(),
+                         d_s, d_l, d_c, ws.st);
 }
 
 // per-batch query preparation shared by every scan of one search: cosine norms, and the
@@ -388,15 +483,65 @@ struct FlatIndex : Index {
       fill_empty_results(d_s, d_l, d_c, nq, k, ws.st);
       return;
     }
+    const int k1 = filter_k1(k);
+    if (filter_enabled() && k <= KMAX_FAST && filter_supported(dim, metric, k1)) {
+      search_filter(d_q, nq, k, k1, cutoff, d_s, d_l, d_c, ws);
+      return;
+    }
+    search_exact(d_q, nq, k, cutoff, d_s, d_l, d_c, ws);
+  }
+
+  // MFMA candidate filter over slots [0, cutoff), exact refine with the *Unsafe form (V = 4)
+  void search_filter(const float *d_q, int64_t nq, int k, int k1, int64_t cutoff, float *d_s, int64_t *d_l,
+                     int32_t *d_c, Workspace &ws) {
+    ScanPlan p = plan_flat(cutoff, nq, dim, k1, MAX_PARTS);
+    const size_t np = (size_t)nq * p.nchunks * k1;
+    ws.part_s.ensure(sizeof(float) * np);
+    ws.part_k.ensure(sizeof(uint32_t) * np);
+    uint32_t *gthr = shared_bounds(ws, nq);
+    ws.items.ensure(sizeof(ScanItem) * std::max(p.nitems, 1));
+    ws.nitems.ensure(sizeof(int32_t) * 4);
+    make_flat_items(ws.items.as<ScanItem>(), ws.nitems.as<int32_t>(), cutoff, p.chunk_rows, nq, 0, p.qchunk, ws.st);
+    FilterArgs fa{};
+    fa.rows = st.rows.as<float>();
+    fa.live = st.live.as<uint8_t>();
+    fa.rsq = st.rsq.as<float>();
+    fa.queries = d_q;
+    fa.items = ws.items.as<ScanItem>();
+    fa.n_items = ws.nitems.as<int32_t>();
+    fa.qlist = nullptr;
+    fa.nparts = p.nchunks;
+    fa.k1 = k1;
+    fa.dim = dim;
+    fa.key_base = 0;
+    fa.row_limit = (uint32_t)cutoff;
+    fa.part_s = ws.part_s.as<float>();
+    fa.part_k = ws.part_k.as<uint32_t>();
+    fa.gthr = gthr;
+    {
+      PhaseTimer t(PH_FLAT_SCAN, ws.st, nq * cutoff);
+      launch_filter(fa, metric, p.nitems, ws.st);
+    }
+    const int64_t nf = filter_finish(ws, nq, p.nchunks, k1, k, dim, metric, 4, d_q, st, nullptr, d_s, d_l, d_c);
+    filter_fallback(ws, nf, d_q, dim, k, d_s, d_l, d_c,
+                    [&](const float *q2, int64_t n2, float *s2, int64_t *l2, int32_t *c2) {
+                      search_exact(q2, n2, k, cutoff, s2, l2, c2, ws);
+                    });
+  }
+
+  // BruteForceVectorIndex.Search (:275-379) on the VALU, the reference's exact arithmetic
+  void search_exact(const float *d_q, int64_t nq, int k, int64_t cutoff, float *d_s, int64_t *d_l, int32_t *d_c,
+                    Workspace &ws) {
     prep_queries(d_q, nq, dim, metric, ws);
     ScanPlan p = plan_flat(cutoff, nq, dim, k, MAX_PARTS);
     const size_t np = (size_t)nq * p.nchunks * k;
     ws.part_s.ensure(sizeof(float) * np);
     ws.part_k.ensure(sizeof(uint32_t) * np);
+    uint32_t *gthr = shared_bounds(ws, nq);
     {
       PhaseTimer t(PH_FLAT_SCAN, ws.st, nq * cutoff);
       flat_scan(st, cutoff, p, d_q, metric == COS ? ws.qn.as<float>() : nullptr, nq, k, 4, metric, p.nchunks, 0, 0,
-                ws, ws.part_s.as<float>(), ws.part_k.as<uint32_t>());
+                ws, ws.part_s.as<float>(), ws.part_k.as<uint32_t>(), false, gthr);
     }
     PhaseTimer t(PH_MERGE, ws.st);
     launch_merge_keys(ws.part_s.as<float>(), ws.part_k.as<uint32_t>(), nq, p.nchunks, k, st.labels.as<int64_t>(),
@@ -471,6 +616,7 @@ struct DictBuffer {
     HIPCHK(hipStreamSynchronize(wst));
     if (st.cap > 65536) {  // a bulk-loaded buffer was compacted into lists: give the HBM back
       st.rows.release();
+      st.rsq.release();
       st.norms.release();
       st.live.release();
       st.labels.release();
@@ -542,21 +688,56 @@ static int64_t probed_rows(Workspace &ws, int64_t nq, int probes, const std::vec
 }
 
 // list-major work items from ws.probes
+// phase 0 -> ws.items / ws.nitems, phase 1 -> ws.items3 / ws.nitems3 (IvfChunking, kernels.h)
 static int build_ivf_items(Workspace &ws, int64_t nq, int nprobe, int nparts, int nlist, const DevMem &lbeg,
-                           const DevMem &lend, int qchunk) {
-  const int maxi = ivf_max_items(nq, nprobe, nlist, qchunk);
+                           const DevMem &lend, int qchunk, IvfChunking ch, int phase = 0) {
+  const int64_t maxi64 = ivf_max_items(nq, nprobe, nlist, qchunk, ch, phase);
+  if (maxi64 > INT32_MAX) throw Error(PYR_E_ARG, "query batch too large for one launch");
+  const int maxi = (int)maxi64;
+  DevMem &items = phase == 0 ? ws.items : ws.items3;
+  DevMem &nitems = phase == 0 ? ws.nitems : ws.nitems3;
   ws.ivf_cnt.ensure(sizeof(int32_t) * nlist);
   ws.ivf_fill.ensure(sizeof(int32_t) * nlist);
   ws.ivf_qoff.ensure(sizeof(int32_t) * (nlist + 1));
   ws.ivf_ioff.ensure(sizeof(int32_t) * (nlist + 1));
   ws.qlist.ensure(sizeof(int32_t) * std::max<int64_t>(nq * nprobe, 1));
-  ws.items.ensure(sizeof(ScanItem) * maxi);
-  ws.nitems.ensure(sizeof(int32_t) * 4);
+  items.ensure(sizeof(ScanItem) * std::max(maxi, 1));
+  nitems.ensure(sizeof(int32_t) * 4);
   IvfItemWs iw{ws.ivf_cnt.as<int32_t>(), ws.ivf_fill.as<int32_t>(), ws.ivf_qoff.as<int32_t>(),
-               ws.ivf_ioff.as<int32_t>(), ws.qlist.as<int32_t>(), ws.items.as<ScanItem>(), ws.nitems.as<int32_t>()};
+               ws.ivf_ioff.as<int32_t>(), ws.qlist.as<int32_t>(), items.as<ScanItem>(), nitems.as<int32_t>()};
   launch_ivf_items(ws.probes.as<int32_t>(), nq, nprobe, nparts, nlist, lbeg.as<int32_t>(), lend.as<int32_t>(), qchunk,
-                   iw, ws.st);
+                   ch, phase, iw, ws.st);
   return maxi;
+}
+
+// Row chunking of the IVF list scan (IvfChunking, kernels.h): a `warm`-row chunk 0 per
+// list scanned by an earlier launch to seed the shared per-query bounds, then chunks of
+// <= `chunk` rows so that work items are uniform whatever the list-size skew of the
+// trained quantizer.  Each (query, probe, chunk) gets its own partial top-k slot, within
+// the MAX_PARTS budget left after `other_parts` and a cap on the partial buffer.
+// PYR_IVF_CHUNK / PYR_IVF_WARM override the defaults for measurements.
+static IvfChunking ivf_chunking(int64_t max_len, int probes, int other_parts, int64_t nq, int k, bool bounds) {
+  int64_t chunk = 2048, warm = 0;  // warm-up launch: measured neutral at the bench config (profiles/)
+  if (const char *e = getenv("PYR_IVF_CHUNK")) chunk = std::max<int64_t>(8, atoll(e));
+  if (const char *e = getenv("PYR_IVF_WARM")) warm = std::max<int64_t>(0, atoll(e));
+  if (!bounds) warm = 0;  // the warm-up launch only pays with shared bounds
+  chunk = round_up(chunk, 8);
+  warm = round_up(warm, 8);
+  auto chunks = [&](int64_t c) {
+    return (int64_t)ivf_list_chunks((int)max_len, IvfChunking{(int32_t)c, 1, (int32_t)warm});
+  };
+  int64_t cmax = chunks(chunk);
+  int64_t budget = probes > 0 ? (MAX_PARTS - other_parts) / probes : 1;
+  const int64_t buf_cap = (int64_t(4) << 30) / std::max<int64_t>(1, nq * (int64_t)k * 8);  // <= 4 GiB of partials
+  budget = std::min(budget, std::max<int64_t>(1, buf_cap / std::max(probes, 1)));
+  if (budget < 1) throw Error(PYR_E_ARG, "nprobe too large");
+  if (cmax > budget) {
+    if (budget < 2) warm = 0;
+    const int64_t room = std::max<int64_t>(1, budget - (warm > 0 ? 1 : 0));
+    chunk = round_up(std::max<int64_t>(8, (max_len - warm + room - 1) / room), 8);
+    cmax = chunks(chunk);
+  }
+  return IvfChunking{(int32_t)chunk, (int32_t)cmax, (int32_t)warm};
 }
 
 // ---------------------------------------------------------------------------
@@ -568,6 +749,7 @@ struct IvfFlatIndex : Index {
   std::vector<uint8_t> lstate;            // 0 removed/pad, 1 visible, 2 shadowed by a buffer id (:210)
   std::unordered_map<int64_t, int64_t> pos_of;
   std::vector<int32_t> lb, le, llen, llive;
+  int64_t max_len = 0;                    // longest list (rows incl. tombstones): row chunking
   DevMem dlb, dle, dllive;
   Coarse coarse;
   bool built = false;                     // _isBuilt (:20)
@@ -696,10 +878,12 @@ struct IvfFlatIndex : Index {
     llen = cnt;
     llive = cnt;
     int64_t tot = 0;
+    max_len = 0;
     for (int l = 0; l < k; l++) {
       lb[l] = (int32_t)tot;
       le[l] = (int32_t)(tot + cnt[l]);
       tot += round_up(cnt[l], 8);
+      max_len = std::max<int64_t>(max_len, cnt[l]);
     }
     if (tot >= (int64_t)KEY_BUF) throw Error(PYR_E_ARG, "IVF index larger than 2^31 rows");
     std::vector<int64_t> srcrow(tot, -1), newlab(tot, -1);
@@ -723,6 +907,7 @@ struct IvfFlatIndex : Index {
     HIPCHK(hipMemcpyAsync(nl.live.p, lv.data(), tot, hipMemcpyHostToDevice, wst));
     HIPCHK(hipMemcpyAsync(nl.labels.p, newlab.data(), sizeof(int64_t) * tot, hipMemcpyHostToDevice, wst));
     if (nl.cosine) launch_norms(nl.rows.as<float>(), tot, dim, 1, nl.norms.as<float>(), wst);
+    launch_sqnorms(nl.rows.as<float>(), nullptr, tot, dim, nl.rsq.as<float>(), nl.rmax.as<uint32_t>(), wst);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(wst));
     nl.n = tot;
@@ -736,6 +921,10 @@ struct IvfFlatIndex : Index {
     std::swap(lists.labels.n, nl.labels.n);
     std::swap(lists.norms.p, nl.norms.p);
     std::swap(lists.norms.n, nl.norms.n);
+    std::swap(lists.rsq.p, nl.rsq.p);
+    std::swap(lists.rsq.n, nl.rsq.n);
+    std::swap(lists.rmax.p, nl.rmax.p);
+    std::swap(lists.rmax.n, nl.rmax.n);
     lists.n = tot;
     lists.cap = nl.cap;
     lists.hlabels.swap(nl.hlabels);
@@ -756,15 +945,91 @@ struct IvfFlatIndex : Index {
       fill_empty_results(d_s, d_l, d_c, nq, std::max(k, 0), ws.st);
       return;
     }
+    // MFMA filter path: built lists only (empty pre-build buffer), no MaxScans, L2 / IP
+    const int nprobe = prm.nprobe < 0 ? nprobe_default : prm.nprobe;
+    const int probes = (built && coarse.nlist > 0) ? std::max(0, std::min(nprobe, coarse.nlist)) : 0;
+    const int k1 = filter_k1(k);
+    if (filter_enabled() && probes > 0 && buf.live_count() == 0 && prm.max_scans < 0 && k <= KMAX_FAST &&
+        probes < MAX_PARTS && filter_supported(dim, metric, k1)) {
+      search_filter(d_q, nq, k, k1, probes, d_s, d_l, d_c, ws);
+      return;
+    }
+    search_exact(d_q, nq, k, prm, d_s, d_l, d_c, ws);
+  }
+
+  void search_filter(const float *d_q, int64_t nq, int k, int k1, int probes, float *d_s, int64_t *d_l, int32_t *d_c,
+                     Workspace &ws) {
+    prep_queries(d_q, nq, dim, metric, ws);
+    {
+      PhaseTimer t(PH_COARSE, ws.st, nq * coarse.nlist);
+      coarse.probe(d_q, nullptr, nq, probes, metric, ws);  // exact coarse ranking (ComputeScore, :186-198)
+    }
+    const IvfChunking ch = ivf_chunking(max_len, probes, 0, nq, k1, bounds_enabled());
+    const int nparts = probes * ch.cmax;
+    const size_t np = (size_t)nq * nparts * k1;
+    ws.part_s.ensure(sizeof(float) * np);
+    ws.part_k.ensure(sizeof(uint32_t) * np);
+    uint32_t *gthr = shared_bounds(ws, nq);
+    int maxi, maxi_main = 0;
+    {
+      PhaseTimer t(PH_ITEMS, ws.st);
+      maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, QCHUNK, ch, 0);
+      if (ch.warm > 0) maxi_main = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, QCHUNK, ch, 1);
+    }
+    FilterArgs fa{};
+    fa.rows = lists.rows.as<float>();
+    fa.live = lists.live.as<uint8_t>();
+    fa.rsq = lists.rsq.as<float>();
+    fa.queries = d_q;
+    fa.items = ws.items.as<ScanItem>();
+    fa.n_items = ws.nitems.as<int32_t>();
+    fa.qlist = ws.qlist.as<int32_t>();
+    fa.nparts = nparts;
+    fa.k1 = k1;
+    fa.dim = dim;
+    fa.key_base = 0;
+    fa.row_limit = 0xFFFFFFFFu;
+    fa.part_s = ws.part_s.as<float>();
+    fa.part_k = ws.part_k.as<uint32_t>();
+    fa.gthr = gthr;
+    {
+      PhaseTimer t(PH_LIST_SCAN, ws.st, prof().on ? probed_rows(ws, nq, probes, le, lb) : 0);
+      launch_filter(fa, metric, maxi, ws.st);
+      if (ch.warm > 0) {
+        fa.items = ws.items3.as<ScanItem>();
+        fa.n_items = ws.nitems3.as<int32_t>();
+        launch_filter(fa, metric, maxi_main, ws.st);
+      }
+    }
+    MergeIvf mi;
+    mi.probes = ws.probes.as<int32_t>();
+    mi.lb = dlb.as<int32_t>();
+    mi.le = dle.as<int32_t>();
+    mi.nprobe = probes;
+    mi.ch = ch;
+    const int64_t nf = filter_finish(ws, nq, nparts, k1, k, dim, metric, 1, d_q, lists, &mi, d_s, d_l, d_c);
+    pyr_search_params ex{probes, 0, -1};
+    filter_fallback(ws, nf, d_q, dim, k, d_s, d_l, d_c,
+                    [&](const float *q2, int64_t n2, float *s2, int64_t *l2, int32_t *c2) {
+                      search_exact(q2, n2, k, ex, s2, l2, c2, ws);
+                    });
+  }
+
+  // IvfFlatVectorIndex.Search (:147-231) with the list scan on the VALU, the reference's exact arithmetic
+  void search_exact(const float *d_q, int64_t nq, int k, const pyr_search_params &prm, float *d_s, int64_t *d_l,
+                    int32_t *d_c, Workspace &ws) {
     const int nprobe = prm.nprobe < 0 ? nprobe_default : prm.nprobe;                  // :151-158
     const int64_t maxs = prm.max_scans < 0 ? (int64_t)INT32_MAX : prm.max_scans;       // :152
     const int64_t bcut = buf.cutoff(std::min<int64_t>(maxs, buf.live_count()));
     const int64_t bscanned = std::min<int64_t>(maxs, buf.live_count());
     const bool index_on = built && coarse.nlist > 0 && bscanned < maxs;                // :183
     const int probes = index_on ? std::max(0, std::min(nprobe, coarse.nlist)) : 0;    // :198
+    if (probes >= MAX_PARTS) throw Error(PYR_E_ARG, "nprobe too large");
     ScanPlan bp;
-    if (bcut > 0) bp = plan_flat(bcut, nq, dim, k, MAX_PARTS - probes);
-    const int nparts = probes + bp.nchunks;
+    if (bcut > 0) bp = plan_flat(bcut, nq, dim, k, std::max(1, std::min(64, MAX_PARTS - probes)));
+    const IvfChunking ch =
+        probes > 0 ? ivf_chunking(max_len, probes, bp.nchunks, nq, k, bounds_enabled()) : IvfChunking{8, 1, 0};
+    const int nparts = probes * ch.cmax + bp.nchunks;
     if (nparts > MAX_PARTS) throw Error(PYR_E_ARG, "nprobe too large");
     if (nparts == 0) {
       fill_empty_results(d_s, d_l, d_c, nq, k, ws.st);
@@ -775,23 +1040,25 @@ struct IvfFlatIndex : Index {
     const size_t np = (size_t)nq * nparts * k;
     ws.part_s.ensure(sizeof(float) * np);
     ws.part_k.ensure(sizeof(uint32_t) * np);
+    uint32_t *gthr = shared_bounds(ws, nq);
     if (probes > 0) {
       {
         PhaseTimer t(PH_COARSE, ws.st, nq * coarse.nlist);
         coarse.probe(d_q, qn, nq, probes, metric, ws);
       }
       const int qchunk = fast_path(dim, k) ? QCHUNK : QCHUNK_GENERIC;
-      int maxi;
+      int maxi, maxi_main = 0;
       {
         PhaseTimer t(PH_ITEMS, ws.st);
-        maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qchunk);
+        maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qchunk, ch, 0);
+        if (ch.warm > 0) maxi_main = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qchunk, ch, 1);
       }
       const uint32_t *lim = nullptr;
       if (prm.max_scans >= 0) {  // :202-212
         ws.limits.ensure(sizeof(uint32_t) * nq * nparts);
         launch_ivf_limits(ws.probes.as<int32_t>(), nq, probes, nparts, maxs - bscanned, dlb.as<int32_t>(),
-                          dle.as<int32_t>(), dllive.as<int32_t>(), lists.live.as<uint8_t>(), ws.limits.as<uint32_t>(),
-                          ws.st);
+                          dle.as<int32_t>(), dllive.as<int32_t>(), lists.live.as<uint8_t>(), ch,
+                          ws.limits.as<uint32_t>(), ws.st);
         lim = ws.limits.as<uint32_t>();
       }
       ScanArgs a{};
@@ -811,17 +1078,31 @@ struct IvfFlatIndex : Index {
       a.dim = dim;
       a.part_s = ws.part_s.as<float>();
       a.part_k = ws.part_k.as<uint32_t>();
+      a.gthr = gthr;
       PhaseTimer t(PH_LIST_SCAN, ws.st, prof().on ? probed_rows(ws, nq, probes, le, lb) : 0);
-      launch_scan(a, metric, 1, maxi, ws.st);
+      launch_scan(a, metric, 1, maxi, ws.st);  // chunk 0 of every list (all chunks when ch.warm == 0)
+      if (ch.warm > 0) {                       // the rest, behind the bounds the first launch published
+        a.items = ws.items3.as<ScanItem>();
+        a.n_items = ws.nitems3.as<int32_t>();
+        launch_scan(a, metric, 1, maxi_main, ws.st);
+      }
     }
     if (bcut > 0) {  // :170-180 exact buffer scan, keys KEY_BUF | slot
       PhaseTimer t(PH_BUF_SCAN, ws.st, nq * bcut);
-      flat_scan(buf.st, bcut, bp, d_q, qn, nq, k, 1, metric, nparts, probes, KEY_BUF, ws, ws.part_s.as<float>(),
-                ws.part_k.as<uint32_t>(), true);
+      flat_scan(buf.st, bcut, bp, d_q, qn, nq, k, 1, metric, nparts, probes * ch.cmax, KEY_BUF, ws,
+                ws.part_s.as<float>(), ws.part_k.as<uint32_t>(), true, gthr);
     }
     PhaseTimer tm(PH_MERGE, ws.st);
+    MergeIvf mi;
+    if (probes > 0) {
+      mi.probes = ws.probes.as<int32_t>();
+      mi.lb = dlb.as<int32_t>();
+      mi.le = dle.as<int32_t>();
+      mi.nprobe = probes;
+      mi.ch = ch;
+    }
     launch_merge_keys(ws.part_s.as<float>(), ws.part_k.as<uint32_t>(), nq, nparts, k, lists.labels.as<int64_t>(),
-                      buf.st.labels.as<int64_t>(), d_s, d_l, nullptr, d_c, ws.st);
+                      buf.st.labels.as<int64_t>(), d_s, d_l, nullptr, d_c, ws.st, &mi);
   }
 
   int64_t count() const override {  // :305 buffer + all list entries (shadowed ones too)
@@ -1042,7 +1323,7 @@ struct IvfPqIndex : Index {
         coarse.probe(d_q, qn, nq, probes, metric, ws);
       }
       const int qchunk = 32;
-      const int maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qchunk);
+      const int maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qchunk, IvfChunking{1 << 30, 1});
       PqArgs a{};
       a.codes = codes.as<uint8_t>();
       a.live = clive.as<uint8_t>();

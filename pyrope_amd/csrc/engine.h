@@ -63,6 +63,8 @@ struct RowStore {
   int64_t n = 0;    // slots in use
   int64_t cap = 0;  // allocated slots (multiple of 8)
   DevMem rows, norms, live, labels;
+  DevMem rsq;       // per slot |x|^2 (MFMA filter, filter.hip)
+  DevMem rmax;      // score_key of the largest |x|^2 ever stored (device scalar, only grows)
   std::vector<int64_t> hlabels;
   std::vector<uint8_t> hlive;
   void reserve(int64_t slots, hipStream_t st);
@@ -81,9 +83,11 @@ struct Workspace {
   hipStream_t st = nullptr;
   bool own_stream = false;
   std::mutex m;
-  DevMem q, qn, qt, items, nitems, items2, nitems2, qlist, part_s, part_k, probes, cpart_s, cpart_k, limits;
-  DevMem ivf_cnt, ivf_fill, ivf_qoff, ivf_ioff;
+  DevMem q, qn, qt, items, nitems, items2, nitems2, items3, nitems3, qlist, part_s, part_k, probes, cpart_s, cpart_k,
+      limits;
+  DevMem ivf_cnt, ivf_fill, ivf_qoff, ivf_ioff, gthr;
   DevMem out_s, out_l, out_c;
+  DevMem ms, mk, fail, fail_cnt, fq, fs, fl, fc;  // MFMA filter: merged candidates, certificate failures
   ~Workspace() {
     if (own_stream && st) (void)hipStreamDestroy(st);
   }
@@ -162,7 +166,7 @@ Index *create_index(const pyr_index_desc &d);
 
 // kernel-phase profiler (pyr_profile_*): HIP events around each phase on the search stream
 enum Phase { PH_COARSE = 0, PH_ITEMS = 1, PH_LIST_SCAN = 2, PH_BUF_SCAN = 3, PH_MERGE = 4, PH_FLAT_SCAN = 5,
-             PH_PQ_SCAN = 6, PH_N = 8 };
+             PH_PQ_SCAN = 6, PH_REFINE = 7, PH_FALLBACK = 8, PH_N = 10 };
 struct Profiler {
   bool on = false;
   std::mutex m;

@@ -1,0 +1,493 @@
+// filter.hip -- MFMA candidate filter + exact refine for the FLAT / IVF-Flat scans (gfx950).
+//
+// The reference's scores are fixed fp32 operation sequences (VectorMath.cs): sub, mul,
+// add per element, 8-lane Vector accumulators and a horizontal tree.  Those can only be
+// reproduced on the VALU (3 instructions per element, kernels.hip scan_fast).  This file
+// gets the same answers at matrix-core rate:
+//
+//   1. mfma_filter: for every (query, row) pair of a work item an APPROXIMATE score from
+//      fp32 MFMA (v_mfma_f32_32x32x2_f32): L2 -> 2 q.x - |x|^2 (the per-query constant
+//      -|q|^2 is added later), IP -> q.x.  Each (query, slot) keeps its top-K1 (K1 = k +
+//      margin) by approximate score, with the same shared per-query bound machinery as
+//      the exact scan (ScanArgs::gthr).
+//   2. the partial lists are merged (merge_keys_kernel) into each query's top-K1 by
+//      approximate score; s~_K1 = the K1-th approximate score.
+//   3. refine_kernel: exact reference scores of the K1 candidates (the same restatement
+//      as the exact scan and the oracle), top-k by (score desc, key asc), and a
+//      certificate: every row outside the candidate set has approximate score <= s~_K1,
+//      and |approx - reference| <= E(q) for every row (fp32 error bounds, see
+//      refine_kernel), so if the k-th exact candidate score is > s~_K1 + E no excluded
+//      row can be in the top-k and the result equals the exact scan's.  Queries whose
+//      certificate fails are listed and re-run through the exact scan by the engine.
+//
+// So the returned ids and scores stay bit-identical to the CPU restatement; only the
+// work per pair moves from 3 VALU instructions per dimension to fp32 MFMA.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+
+#include "kernels.h"
+
+namespace pyr {
+namespace {
+
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ bool better(float s1, uint32_t k1, float s2, uint32_t k2) {
+  return s1 > s2 || (s1 == s2 && k1 < k2);
+}
+
+__device__ __forceinline__ size_t blk_off(int64_t r, int d, int D) {
+  return ((size_t)(r >> 3) * (size_t)D + (size_t)d) * 8 + (size_t)(r & 7);
+}
+
+__device__ __forceinline__ void list_insert(float *ls, uint32_t *lk, int &cnt, int k, float s, uint32_t key) {
+  int n = cnt;
+  if (n == k) n = k - 1;
+  int j = n;
+  while (j > 0 && better(s, key, ls[j - 1], lk[j - 1])) {
+    ls[j] = ls[j - 1];
+    lk[j] = lk[j - 1];
+    j--;
+  }
+  ls[j] = s;
+  lk[j] = key;
+  cnt = n + 1;
+}
+
+constexpr int FQ = 128;      // queries per work item (4 waves x 32)
+constexpr int RT = 32;       // rows per stage (one 32x32 MFMA tile per wave)
+constexpr int SCR = RT + 4;  // score-transpose row stride (floats)
+
+// LDS layout of mfma_filter
+template <int D>
+struct FilterLds {
+  static constexpr int RSTR = D + 4;      // padded row stride: conflict-free ds_read_b128 / ds_write_b32
+  static constexpr int TILE = RT * RSTR;  // floats per row tile
+  static constexpr size_t bytes(int k1) { return sizeof(float) * (2 * TILE + 4 * 32 * SCR) + (size_t)FQ * k1 * 8; }
+};
+
+// ---------------------------------------------------------------------------
+// mfma_filter: one work item (ScanItem) = up to 128 queries x a row range.  Wave w owns
+// queries 32w..32w+31 of the item; its A operand (the queries) stays in registers for the
+// whole item: lane l holds query (l & 31), dims [(l >> 5) * D/2, (l >> 5) * D/2 + D/2).
+// Rows stream HBM -> registers -> LDS (row-major, padded) 32 at a time, double buffered.
+// Per stage each wave runs D/2 MFMAs of 32x32x2 (C[query][row] += 2 dims per step; the
+// two lane halves split the dimension range), then moves its C tile through a
+// wave-private LDS transpose so that lane i (< 32) sees query i's 32 row scores, filters
+// them against the query's K1-th best / shared bound and inserts survivors into the
+// query's LDS list.
+// ---------------------------------------------------------------------------
+template <int D, int MET, bool IVF>
+__global__ __launch_bounds__(256, 2) void mfma_filter(FilterArgs a) {
+  using L = FilterLds<D>;
+  constexpr int KH = D / 2;  // k-steps: lanes 0-31 take dims [0, KH), lanes 32-63 [KH, D)
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  if ((int)blockIdx.x >= *a.n_items) return;
+  const ScanItem it = a.items[blockIdx.x];
+  const int k1 = a.k1;
+  float *rt = smem;                 // [2][RT][RSTR]
+  float *scw = smem + 2 * L::TILE;  // [4][32][SCR]
+  float *tks = scw + 4 * 32 * SCR;  // [FQ][k1]
+  uint32_t *tkk = reinterpret_cast<uint32_t *>(tks + FQ * k1);
+
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int i32 = lane & 31, h = lane >> 5;
+  float *sc = scw + w * 32 * SCR;
+
+  // A operand: query 32w + i32 of the item, dims h*KH .. h*KH + KH - 1
+  float qa[KH];
+  {
+    const int i = 32 * w + i32;
+    if (i < it.qcnt) {
+      const int qi = IVF ? a.qlist[it.qbeg + i] / a.nparts : it.qbeg + i;
+      const float4 *qp = reinterpret_cast<const float4 *>(a.queries + (size_t)qi * D + h * KH);
+#pragma unroll
+      for (int p = 0; p < KH / 4; ++p) {
+        const float4 v = qp[p];
+        qa[4 * p] = v.x;
+        qa[4 * p + 1] = v.y;
+        qa[4 * p + 2] = v.z;
+        qa[4 * p + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < KH; ++s) qa[s] = 0.0f;
+    }
+  }
+  const bool wave_active = 32 * w < it.qcnt;
+
+  // owners: lane i32 of wave w (lower half) owns query 32w + i32
+  const int oq = 32 * w + i32;
+  const bool owner = h == 0 && oq < it.qcnt;
+  int oslot = 0, qown = 0;
+  float gs = -INFINITY;
+  uint32_t published = 0;
+  if (owner) {
+    oslot = IVF ? a.qlist[it.qbeg + oq] + it.part : (it.qbeg + oq) * a.nparts + it.part;
+    qown = IVF ? a.qlist[it.qbeg + oq] / a.nparts : it.qbeg + oq;
+    if (a.gthr) gs = key_score(__hip_atomic_load(a.gthr + qown, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  }
+  int cnt = 0;
+  float thr_s = -INFINITY;
+  uint32_t thr_k = KEY_NONE;
+  float *ls = tks + oq * k1;
+  uint32_t *lk = tkk + oq * k1;
+
+  // stage staging: RT rows of the blocked store = RT/8 groups of [D][8]; float4 v of a
+  // group holds rows (v&1)*4 .. +3 at dim v>>1 (kernels.hip blk_off)
+  const int r0 = it.row_begin;  // multiple of 8
+  const int nst = (it.row_end - r0 + RT - 1) / RT;
+  constexpr int NV = RT * D / 4;  // float4 per stage
+  constexpr int LOADS = NV / 256;
+  static_assert(NV % 256 == 0, "stage must split evenly over 256 threads");
+  const float4 *src = reinterpret_cast<const float4 *>(a.rows);
+  const int gmax = ((it.row_end + 7) >> 3) - 1;  // last group with rows of this item
+  float4 pf[LOADS];
+  auto load_stage = [&](int stg) {
+#pragma unroll
+    for (int i = 0; i < LOADS; ++i) {
+      const int v = tid + 256 * i;
+      const int g = min((r0 >> 3) + stg * (RT / 8) + v / (2 * D), gmax);  // clamp: rows past the end unused
+      pf[i] = src[(size_t)g * (2 * D) + v % (2 * D)];
+    }
+  };
+  auto store_stage = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < LOADS; ++i) {
+      const int v = tid + 256 * i;
+      const int gl = v / (2 * D), vv = v % (2 * D);
+      float *dst = rt + buf * L::TILE + (gl * 8 + (vv & 1) * 4) * L::RSTR + (vv >> 1);
+      dst[0] = pf[i].x;
+      dst[L::RSTR] = pf[i].y;
+      dst[2 * L::RSTR] = pf[i].z;
+      dst[3 * L::RSTR] = pf[i].w;
+    }
+  };
+
+  if (nst > 0) {
+    load_stage(0);
+    store_stage(0);
+  }
+  __syncthreads();
+
+  for (int st = 0; st < nst; ++st) {
+    const int cur = st & 1;
+    if (st + 1 < nst) load_stage(st + 1);
+    const int row = r0 + st * RT + i32;  // this lane's C column
+    const int rc = min(row, it.row_end - 1);
+    const bool rvalid = row < it.row_end && (uint32_t)row < a.row_limit && a.live[rc];
+    const float xsq = MET == L2 ? a.rsq[rc] : 0.0f;
+    if (wave_active) {
+      f16v acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+      const float *bp = rt + cur * L::TILE + i32 * L::RSTR + h * KH;
+#pragma unroll
+      for (int s4 = 0; s4 < KH / 4; ++s4) {
+        const float4 b = *reinterpret_cast<const float4 *>(bp + 4 * s4);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qa[4 * s4 + 0], b.x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qa[4 * s4 + 1], b.y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qa[4 * s4 + 2], b.z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qa[4 * s4 + 3], b.w, acc, 0, 0, 0);
+      }
+      // C[i][j]: lane column j = i32 (row), register r -> query (r&3) + 8(r>>2) + 4h
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qi = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float s = MET == L2 ? 2.0f * acc[r] - xsq : acc[r];
+        sc[qi * SCR + i32] = rvalid ? s : -INFINITY;
+      }
+    }
+    if (st + 1 < nst) store_stage(cur ^ 1);
+    __syncthreads();  // next tile staged; this wave's score transpose visible
+
+    if (owner) {
+      const float *scp = sc + i32 * SCR;
+      const int rb = r0 + st * RT;
+      uint32_t pass = 0;
+#pragma unroll
+      for (int j = 0; j < RT; ++j) {
+        const float v = scp[j];
+        if (v > -INFINITY && v >= gs && better(v, a.key_base | (uint32_t)(rb + j), thr_s, thr_k)) pass |= 1u << j;
+      }
+      while (pass) {
+        const int j = __builtin_ctz(pass);
+        pass &= pass - 1;
+        const float v = scp[j];
+        const uint32_t key = a.key_base | (uint32_t)(rb + j);
+        if (!better(v, key, thr_s, thr_k)) continue;
+        list_insert(ls, lk, cnt, k1, v, key);
+        if (cnt == k1) {
+          thr_s = ls[k1 - 1];
+          thr_k = lk[k1 - 1];
+        }
+      }
+      if (a.gthr && (st & 7) == 7) {  // every 8 stages: publish this list's K1-th best, refresh the bound
+        if (cnt == k1 && score_key(thr_s) > published) {
+          published = score_key(thr_s);
+          atomicMax(a.gthr + qown, published);
+        }
+        gs = fmaxf(gs, key_score(__hip_atomic_load(a.gthr + qown, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+      }
+    }
+  }
+  if (owner) {
+    if (a.gthr && cnt == k1 && score_key(thr_s) > published) atomicMax(a.gthr + qown, score_key(thr_s));
+    float *ps = a.part_s + (size_t)oslot * k1;
+    uint32_t *pk = a.part_k + (size_t)oslot * k1;
+    for (int j = 0; j < k1; ++j) {
+      ps[j] = j < cnt ? ls[j] : -INFINITY;
+      pk[j] = j < cnt ? lk[j] : KEY_NONE;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Exact restatements (VectorMath.cs) for the refine step -- the operation order of
+// kernels.hip em_* and oracle/oracle.c, on one blocked-store row.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float hsum8(const float *v) {
+  float lo = (v[0] + v[1]) + (v[2] + v[3]);
+  float hi = (v[4] + v[5]) + (v[6] + v[7]);
+  return lo + hi;
+}
+
+// V = 1: L2Squared (VectorMath.cs:39-70) / DotProduct (:8-37);
+// V = 4: L2SquaredUnsafe (:188-253) / DotProductUnsafe (:128-186).  D % 8 == 0.
+template <int V, int MET>
+__device__ float exact_score(const float *q, const float *rows, int64_t r, int D) {
+  float sum = 0.0f;
+  int i = 0;
+  if (V == 4 && D >= 32) {
+    float a1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, a2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    float a3[8] = {0, 0, 0, 0, 0, 0, 0, 0}, a4[8] = {0, 0, 0, 0, 0, 0, 0, 0}, fin[8];
+    for (; i <= D - 32; i += 32)
+#pragma unroll
+      for (int l = 0; l < 8; l++) {
+        float t[4];
+#pragma unroll
+        for (int v = 0; v < 4; v++) {
+          const float x = rows[blk_off(r, i + 8 * v + l, D)];
+          if (MET == L2) {
+            const float d = q[i + 8 * v + l] - x;
+            t[v] = d * d;
+          } else {
+            t[v] = q[i + 8 * v + l] * x;
+          }
+        }
+        a1[l] = a1[l] + t[0];
+        a2[l] = a2[l] + t[1];
+        a3[l] = a3[l] + t[2];
+        a4[l] = a4[l] + t[3];
+      }
+#pragma unroll
+    for (int l = 0; l < 8; l++) fin[l] = ((a1[l] + a2[l]) + a3[l]) + a4[l];
+    sum = sum + hsum8(fin);
+  }
+  if (i <= D - 8) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (; i <= D - 8; i += 8)
+#pragma unroll
+      for (int l = 0; l < 8; l++) {
+        const float x = rows[blk_off(r, i + l, D)];
+        if (MET == L2) {
+          const float d = q[i + l] - x;
+          acc[l] = acc[l] + d * d;
+        } else {
+          acc[l] = acc[l] + q[i + l] * x;
+        }
+      }
+    sum = sum + hsum8(acc);
+  }
+  return MET == L2 ? -sum : sum;
+}
+
+// One wave per query: lane c < K1 re-scores candidate c exactly, ranks it among the
+// candidates by (exact score desc, key asc); lanes with rank < k write the result.
+// Certificate (file header), with s~_K1 the merged K1-th approximate score:
+//   L2: approx = 2 q.x - |x|^2 - |q|^2,  IP: approx = q.x, and for every row
+//   |approx - reference| <= E = c_err * u * (|q| + X)^2   (L2)
+//                              c_err * u * |q| * X       (IP)
+// with X >= every row norm of the index and u = 2^-24: the fp32 MFMA dot is an fmaf
+// chain of D terms (error <= D u sum|q_i x_i| <= D u |q||x|), |x|^2 and |q|^2 are fp32
+// sums (<= D u |.|^2 each), one more rounding combines them, and the reference's own
+// sum is within (D/8 + 5) u (|q| + |x|)^2 of the real value: < (3.2 D + 6) u (|q|+|x|)^2
+// in all, against c_err = 4 D + 64 (engine).  If fewer than K1 candidates exist no row
+// was excluded and the result is exact as it stands.
+template <int V, int MET>
+__global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= a.nq) return;
+  const int D = a.dim, k1 = a.k1, k = a.k;
+  const float *qp = a.queries + (size_t)q * D;
+  float part = 0.0f;  // |q|^2, any order (covered by E)
+  for (int d = lane; d < D; d += 64) part += qp[d] * qp[d];
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) part += __shfl_xor(part, off);
+  const float qsq = part;
+
+  const float *ms = a.ms + (size_t)q * k1;
+  const int32_t *mk = a.mk + (size_t)q * k1;
+  uint32_t key = KEY_NONE;
+  float s = -INFINITY;
+  if (lane < k1 && mk[lane] >= 0) {
+    key = (uint32_t)mk[lane];
+    s = exact_score<V, MET>(qp, a.rows, (int64_t)key, D);
+  }
+  int rank = 0, valid = 0;
+  for (int c = 0; c < k1; ++c) {
+    const float sc = __shfl(s, c);
+    const uint32_t kc = __shfl(key, c);
+    if (kc == KEY_NONE) continue;
+    ++valid;
+    if (key != KEY_NONE && better(sc, kc, s, key)) ++rank;
+  }
+  const int nout = min(valid, k);
+  if (key != KEY_NONE && rank < k) {
+    a.out_s[(size_t)q * k + rank] = s;
+    a.out_l[(size_t)q * k + rank] = a.row_labels ? a.row_labels[key] : (int64_t)key;
+  }
+  if (lane >= nout && lane < k) {
+    a.out_s[(size_t)q * k + lane] = -INFINITY;
+    a.out_l[(size_t)q * k + lane] = -1;
+  }
+  bool ok = true;
+  if (mk[k1 - 1] >= 0) {  // K1 candidates: rows were excluded, check the margin
+    float skth = -INFINITY;
+    for (int c = 0; c < k1; ++c) {
+      const int rc = __shfl(rank, c);
+      const uint32_t kc = __shfl(key, c);
+      const float sc = __shfl(s, c);
+      if (kc != KEY_NONE && rc == k - 1) skth = sc;
+    }
+    const double u = 5.9604644775390625e-8;  // 2^-24
+    const double qn = sqrt((double)qsq) * (1.0 + 1e-5);
+    const double X = sqrt((double)key_score(*a.max_rsq)) * (1.0 + 1e-5);
+    const double e = MET == L2 ? a.c_err * u * (qn + X) * (qn + X) : a.c_err * u * qn * X;
+    const double approx_k1 = MET == L2 ? (double)ms[k1 - 1] - (double)qsq : (double)ms[k1 - 1];
+    ok = nout == k && (double)skth > approx_k1 + e;
+  }
+  if (lane == 0) {
+    if (a.out_c) a.out_c[q] = nout;
+    if (!ok) a.fail_list[atomicAdd(a.fail_cnt, 1)] = (int32_t)q;
+  }
+}
+
+// result rows of the exact re-run (sub-batch order) back to their queries
+__global__ void scatter_results_kernel(const int32_t *qidx, int64_t n, int k, const float *ss, const int64_t *sl,
+                                       const int32_t *sc, float *out_s, int64_t *out_l, int32_t *out_c) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * k) return;
+  const int64_t i = e / k;
+  const int j = (int)(e % k);
+  const int64_t q = qidx[i];
+  out_s[q * k + j] = ss[e];
+  out_l[q * k + j] = sl[e];
+  if (j == 0 && out_c) out_c[q] = sc[i];
+}
+
+__global__ void gather_queries_kernel(const float *q, const int32_t *qidx, int64_t n, int D, float *out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * D) return;
+  const int64_t i = e / D;
+  out[e] = q[(size_t)qidx[i] * D + e % D];
+}
+
+// |x|^2 of blocked rows (slots[i], or i when slots is null) and the running maximum
+// (score_key-encoded, only grows) that the refine certificate bounds row norms with
+__global__ void sqnorms_kernel(const float *rows, const int64_t *slots, int64_t n, int D, float *out,
+                               uint32_t *max_key) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t r = slots ? slots[i] : i;
+  float s = 0.0f;
+  for (int d = 0; d < D; ++d) {
+    const float x = rows[blk_off(r, d, D)];
+    s = s + x * x;
+  }
+  out[r] = s;
+  atomicMax(max_key, score_key(s));
+}
+
+inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
+
+template <int D, int MET, bool IVF>
+void launch_filter_t(const FilterArgs &a, int max_items, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mfma_filter<D, MET, IVF>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL((mfma_filter<D, MET, IVF>), dim3(max_items), dim3(256), FilterLds<D>::bytes(a.k1), st, a);
+}
+
+template <int D>
+void launch_filter_d(const FilterArgs &a, int metric, int max_items, hipStream_t st) {
+  const bool ivf = a.qlist != nullptr;
+  if (metric == L2) {
+    if (ivf) launch_filter_t<D, L2, true>(a, max_items, st);
+    else launch_filter_t<D, L2, false>(a, max_items, st);
+  } else {
+    if (ivf) launch_filter_t<D, IP, true>(a, max_items, st);
+    else launch_filter_t<D, IP, false>(a, max_items, st);
+  }
+}
+
+size_t filter_lds(int dim, int k1) {
+  return dim == 128 ? FilterLds<128>::bytes(k1) : dim == 64 ? FilterLds<64>::bytes(k1) : FilterLds<32>::bytes(k1);
+}
+
+}  // namespace
+
+bool filter_supported(int dim, int metric, int k1) {
+  if (metric != L2 && metric != IP) return false;
+  if (dim != 32 && dim != 64 && dim != 128) return false;
+  return k1 >= 1 && k1 <= 64 && filter_lds(dim, k1) <= 160 * 1024;
+}
+
+void launch_filter(const FilterArgs &a, int metric, int max_items, hipStream_t st) {
+  if (max_items <= 0) return;
+  switch (a.dim) {
+    case 32: launch_filter_d<32>(a, metric, max_items, st); return;
+    case 64: launch_filter_d<64>(a, metric, max_items, st); return;
+    default: launch_filter_d<128>(a, metric, max_items, st); return;
+  }
+}
+
+void launch_refine(const RefineArgs &a, int metric, int V, hipStream_t st) {
+  if (a.nq <= 0) return;
+  const dim3 g(nblk(a.nq, 4)), b(256);
+  if (V == 4) {
+    if (metric == L2) hipLaunchKernelGGL((refine_kernel<4, L2>), g, b, 0, st, a);
+    else hipLaunchKernelGGL((refine_kernel<4, IP>), g, b, 0, st, a);
+  } else {
+    if (metric == L2) hipLaunchKernelGGL((refine_kernel<1, L2>), g, b, 0, st, a);
+    else hipLaunchKernelGGL((refine_kernel<1, IP>), g, b, 0, st, a);
+  }
+}
+
+void launch_gather_queries(const float *q, const int32_t *qidx, int64_t n, int32_t dim, float *out, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(gather_queries_kernel, dim3(nblk(n * dim, 256)), dim3(256), 0, st, q, qidx, n, dim, out);
+}
+
+void launch_scatter_results(const int32_t *qidx, int64_t n, int32_t k, const float *ss, const int64_t *sl,
+                            const int32_t *sc, float *out_s, int64_t *out_l, int32_t *out_c, hipStream_t st) {
+  if (n <= 0 || k <= 0) return;
+  hipLaunchKernelGGL(scatter_results_kernel, dim3(nblk(n * k, 256)), dim3(256), 0, st, qidx, n, k, ss, sl, sc, out_s,
+                     out_l, out_c);
+}
+
+void launch_sqnorms(const float *rows, const int64_t *slots, int64_t n, int32_t dim, float *out, uint32_t *max_key,
+                    hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(sqnorms_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, rows, slots, n, dim, out, max_key);
+}
+
+}  // namespace pyr

@@ -18,7 +18,8 @@ constexpr int MAX_PARTS = 1024;            // partial lists merged per query
 
 // A scan work item: rows [row_begin, row_end) of a blocked row store against up to
 // QCHUNK queries.  If the launch has a qlist, the queries' partial slots are
-// qlist[qbeg .. qbeg+qcnt); otherwise query = qbeg + i and slot = query * nparts + part.
+// qlist[qbeg .. qbeg+qcnt) + part (IVF: part = row chunk of the list); otherwise
+// query = qbeg + i and slot = query * nparts + part.
 struct ScanItem {
   int32_t row_begin;  // multiple of 8
   int32_t row_end;
@@ -27,6 +28,29 @@ struct ScanItem {
   int32_t part;
   int32_t list;  // IVF: list id of the item
 };
+
+// IVF row chunking.  List l is split into chunk 0 = its first `warm` rows (if warm > 0)
+// and then chunks of at most `chunk` rows; (query, probe p, chunk c) owns partial slot
+// q * nparts + p * cmax + c.  The chunk-0 items run as a separate, earlier launch: they
+// publish every query's shared bound (ScanArgs::gthr) before the main launch starts,
+// so the main items skip almost every row without a top-k insertion.  Chunking also
+// keeps work items uniform whatever the list-size skew.  warm, chunk: multiples of 8.
+struct IvfChunking {
+  int32_t chunk;  // rows per main chunk
+  int32_t cmax;   // max chunks of any list (slots reserved per probe)
+  int32_t warm;   // rows of chunk 0 (0 = no warm-up chunk)
+};
+__host__ __device__ inline int ivf_list_chunks(int len, IvfChunking ch) {
+  if (ch.warm > 0) return len <= ch.warm ? 1 : 1 + (len - ch.warm + ch.chunk - 1) / ch.chunk;
+  return len <= 0 ? 1 : (len + ch.chunk - 1) / ch.chunk;  // an empty list still gets one (empty) item
+}
+// rows [*b, *e) (relative to the list start) of chunk c
+__host__ __device__ inline void ivf_chunk_rows(int len, int c, IvfChunking ch, int *b, int *e) {
+  int s = ch.warm > 0 ? (c == 0 ? 0 : ch.warm + (c - 1) * ch.chunk) : c * ch.chunk;
+  int t = ch.warm > 0 && c == 0 ? ch.warm : s + ch.chunk;
+  *b = s < len ? s : len;
+  *e = t < len ? t : len;
+}
 
 struct ScanArgs {
   const float *rows;      // blocked [row/8][D][8]
@@ -45,7 +69,28 @@ struct ScanArgs {
   int32_t dim;
   float *part_s;          // [slot][k] scores
   uint32_t *part_k;       // [slot][k] keys
+  // Per-query running bound shared by every item of one search (null = off): the
+  // order-preserving uint32 encoding (score_key) of a score that some k rows of that
+  // query already reach.  A row strictly below it can never enter the final top-k,
+  // so items skip it; owners raise it with atomicMax as their lists fill.
+  uint32_t *gthr;
 };
+
+// order-preserving float <-> uint32 map (a < b  <=>  score_key(a) < score_key(b))
+__host__ __device__ inline uint32_t score_key(float f) {
+  union {
+    float f;
+    uint32_t u;
+  } v{f};
+  return (v.u & 0x80000000u) ? ~v.u : (v.u | 0x80000000u);
+}
+__host__ __device__ inline float key_score(uint32_t k) {
+  union {
+    uint32_t u;
+    float f;
+  } v{(k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k};
+  return v.f;
+}
 
 // V = 1: VectorMath safe functions (one Vector accumulator; IVF paths, k-means).
 // V = 4: VectorMath *Unsafe functions (four accumulators; BruteForce head).
@@ -64,9 +109,17 @@ void launch_norms(const float *x, int64_t n, int32_t dim, int blocked, float *ou
 
 // Merge nparts sorted partial lists per query into top-k.
 // keys are uint32 storage keys; labels mapped through row_labels / buf_labels when given.
+// With `ivf` set, parts [0, nprobe*cmax) are IVF chunk slots and slot p*cmax + c is read
+// only if list probes[q][p] has more than c chunks (unwritten slots are never read).
+struct MergeIvf {
+  const int32_t *probes = nullptr;  // [nq][nprobe]
+  const int32_t *lb = nullptr, *le = nullptr;
+  int32_t nprobe = 0;
+  IvfChunking ch{8, 1, 0};
+};
 void launch_merge_keys(const float *ps, const uint32_t *pk, int64_t nq, int32_t nparts, int32_t k,
                        const int64_t *row_labels, const int64_t *buf_labels, float *out_s, int64_t *out_l,
-                       int32_t *out_keys, int32_t *out_cnt, hipStream_t st);
+                       int32_t *out_keys, int32_t *out_cnt, hipStream_t st, const MergeIvf *ivf = nullptr);
 // Merge partial lists that carry int64 labels (multi-GPU), ties by label asc.
 void launch_merge_labels(const float *ps, const int64_t *pl, int64_t nq, int32_t nparts, int32_t k, float *out_s,
                          int64_t *out_l, hipStream_t st);
@@ -81,14 +134,17 @@ struct IvfItemWs {
   ScanItem *items;    // max_items
   int32_t *n_items;   // 1
 };
-int ivf_max_items(int64_t nq, int32_t nprobe, int32_t nlist, int32_t qchunk);
+// Item list of one launch phase: phase 0 = chunk 0 of every list (all chunks when
+// ch.warm == 0), phase 1 = chunks >= 1 (only with ch.warm > 0).  Phase 0 also builds
+// the per-list query lists (ws.cnt/qoff/qlist) that phase 1 reuses.
+int64_t ivf_max_items(int64_t nq, int32_t nprobe, int32_t nlist, int32_t qchunk, IvfChunking ch, int phase);
 void launch_ivf_items(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t nparts, int32_t nlist,
-                      const int32_t *list_begin, const int32_t *list_end, int32_t qchunk, IvfItemWs &ws,
-                      hipStream_t st);
-// IVF max_scans limits per (query, probe) slot (IvfFlatVectorIndex.cs:200-212)
+                      const int32_t *list_begin, const int32_t *list_end, int32_t qchunk, IvfChunking ch,
+                      int phase, IvfItemWs &ws, hipStream_t st);
+// IVF max_scans limits per (query, probe, chunk) slot (IvfFlatVectorIndex.cs:200-212)
 void launch_ivf_limits(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t nparts, int64_t remaining,
                        const int32_t *list_begin, const int32_t *list_end, const int32_t *list_live,
-                       const uint8_t *live, uint32_t *limits, hipStream_t st);
+                       const uint8_t *live, IvfChunking ch, uint32_t *limits, hipStream_t st);
 
 // IVF-PQ ADC scan (IvfPqVectorIndex.cs:152-198).
 struct PqArgs {
@@ -119,6 +175,49 @@ void launch_extract_sub(const float *x, int64_t n, int32_t dim, int32_t off, int
 // codes (row-major n x M, rows in perm order) -> blocked list storage
 void launch_pack_codes(const uint8_t *codes, const int64_t *src_of_dst, int64_t ndst, int32_t M, uint8_t *out,
                        hipStream_t st);
+
+// ---- MFMA candidate filter + exact refine (filter.hip) ----
+struct FilterArgs {
+  const float *rows;       // blocked [row/8][D][8]
+  const uint8_t *live;     // per row
+  const float *rsq;        // per row |x|^2 (L2)
+  const float *queries;    // row-major nq x D
+  const ScanItem *items;
+  const int32_t *n_items;
+  const int32_t *qlist;    // IVF partial-slot ids, or null (FLAT items)
+  int32_t nparts, k1, dim;
+  uint32_t key_base;
+  uint32_t row_limit;      // rows >= row_limit are not scanned (FLAT MaxScans cutoff)
+  float *part_s;           // [slot][k1] approximate scores
+  uint32_t *part_k;        // [slot][k1] keys
+  uint32_t *gthr;          // shared per-query bound in approximate-score space, or null
+};
+struct RefineArgs {
+  const float *rows;        // blocked store the keys index
+  const int64_t *row_labels;
+  const float *queries;     // row-major nq x D
+  const float *ms;          // merged approximate scores [nq][k1] (desc)
+  const int32_t *mk;        // merged keys [nq][k1] (-1 = none)
+  const uint32_t *max_rsq;  // score_key(max |x|^2 over the store) (device scalar)
+  int64_t nq;
+  int32_t k1, k, dim;
+  double c_err;             // error-bound constant (refine_kernel)
+  float *out_s;
+  int64_t *out_l;
+  int32_t *out_c;
+  int32_t *fail_list;       // queries whose certificate failed
+  int32_t *fail_cnt;
+};
+bool filter_supported(int dim, int metric, int k1);
+void launch_filter(const FilterArgs &a, int metric, int max_items, hipStream_t st);
+// V: 1 = VectorMath safe form (IVF), 4 = *Unsafe form (FLAT)
+void launch_refine(const RefineArgs &a, int metric, int V, hipStream_t st);
+void launch_gather_queries(const float *q, const int32_t *qidx, int64_t n, int32_t dim, float *out, hipStream_t st);
+void launch_scatter_results(const int32_t *qidx, int64_t n, int32_t k, const float *ss, const int64_t *sl,
+                            const int32_t *sc, float *out_s, int64_t *out_l, int32_t *out_c, hipStream_t st);
+// |x|^2 of blocked rows (at slots, or rows [0,n) when slots is null) + atomic running max
+void launch_sqnorms(const float *rows, const int64_t *slots, int64_t n, int32_t dim, float *out, uint32_t *max_key,
+                    hipStream_t st);
 
 // layout helpers
 // dst blocked rows [dst_row0 ...] from row-major src rows (src_idx[i] or i when null)

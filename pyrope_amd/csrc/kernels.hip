@@ -17,6 +17,7 @@
 
 #include <cfloat>
 #include <cmath>
+#include <algorithm>
 #include <cstdlib>
 
 #include "kernels.h"
@@ -26,7 +27,6 @@ namespace {
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 
-constexpr int SCS = 132;  // score-matrix row stride (floats): conflict-free float4 stores
 
 __device__ __forceinline__ bool better(float s1, uint32_t k1, float s2, uint32_t k2) {
   return s1 > s2 || (s1 == s2 && k1 < k2);
@@ -229,36 +229,48 @@ __device__ __forceinline__ void list_insert(float *ls, uint32_t *lk, int &cnt, i
 // to an LDS matrix; one owner thread per query filters them against its k-th
 // best (branch-free) and keeps that query's sorted top-k in LDS.
 // ---------------------------------------------------------------------------
-template <int D, int V, int MET, int GPS>
-__global__ __launch_bounds__(256) void scan_fast(ScanArgs a) {
+// IVF = the launch has a qlist (list-major IVF items); a separate instantiation so the IVF
+// list scan and the FLAT / k-means scans are distinct kernel symbols in rocprof.
+template <int GPS>
+constexpr int score_stride() {  // floats per query row of the score matrix: conflict-free ds_write_b32
+  return GPS * 8 + 4;
+}
+
+// QS = queries per slot: 2 -> 512 threads (register tile small enough for 5-6 waves per
+// SIMD); 4 -> 256 threads (~140 VGPRs, 3 waves per SIMD: VALU issue ~47%, profiles/).
+template <int D, int V, int MET, int GPS, bool IVF, int QS, int W>
+__global__ __launch_bounds__(8 * QCHUNK / QS, W) void scan_fast(ScanArgs a) {
+  constexpr int NT = 8 * QCHUNK / QS;   // threads
+  constexpr int QPW = 8 * QS;           // queries per wave
   constexpr int T = D / 8;              // Vector<float> blocks per row
   constexpr int GF = D * 8;             // floats per 8-row group
+  constexpr int RS = score_stride<GPS>();
   extern __shared__ __attribute__((aligned(16))) float smem[];
   if ((int)blockIdx.x >= *a.n_items) return;
   const ScanItem it = a.items[blockIdx.x];
   const int k = a.k;
   float *tile = smem;                            // [2][GPS*GF]
-  float *sc = smem + 2 * GPS * GF;               // [2][GPS*8][SCS]
-  float *tks = sc + 2 * GPS * 8 * SCS;           // [QCHUNK][k]
+  float *sc = smem + 2 * GPS * GF;               // [2][QCHUNK][RS]  (query-major scores)
+  float *tks = sc + 2 * QCHUNK * RS;             // [QCHUNK][k]
   uint32_t *tkk = reinterpret_cast<uint32_t *>(tks + QCHUNK * k);
 
   const int tid = threadIdx.x;
   const int l = tid & 7, s = tid >> 3;
   const int c1 = (l ^ (l >> 2)) & 1, c2 = ((l >> 1) ^ (l >> 2)) & 1, c3 = (l >> 2) & 1;
   const int myj = c1 | (c2 << 1) | (c3 << 2);
-  const bool wave_active = (tid >> 6) * 32 < it.qcnt;
+  const bool wave_active = (tid >> 6) * QPW < it.qcnt;
 
   // queries arrive lane-major (transpose_queries): lane l's dims l, l+8, ... are
   // contiguous and load as float4; kept as plain scalars (packed FP32 has no extra
   // rate on gfx950 and its op_sel broadcast would double the register footprint).
-  float q[4][T];
-  float qn[4];
+  float q[QS][T];
+  float qn[QS];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int i = s * 4 + u;
+  for (int u = 0; u < QS; ++u) {
+    const int i = s * QS + u;
     qn[u] = 0.0f;
     if (i < it.qcnt) {
-      const int qi = a.qlist ? a.qlist[it.qbeg + i] / a.nparts : it.qbeg + i;
+      const int qi = IVF ? a.qlist[it.qbeg + i] / a.nparts : it.qbeg + i;
       const float4 *qp = reinterpret_cast<const float4 *>(a.queries_t + (size_t)qi * D + l * T);
 #pragma unroll
       for (int p = 0; p < T / 4; ++p) {
@@ -276,11 +288,15 @@ __global__ __launch_bounds__(256) void scan_fast(ScanArgs a) {
   }
 
   const bool owner = tid < it.qcnt;
-  int oslot = 0;
+  int oslot = 0, qown = 0;
   uint32_t lim = 0xFFFFFFFFu;
+  float gs = -INFINITY;  // shared per-query bound (ScanArgs::gthr): rows strictly below it are skipped
+  uint32_t published = 0;
   if (owner) {
-    oslot = a.qlist ? a.qlist[it.qbeg + tid] : (it.qbeg + tid) * a.nparts + it.part;
+    oslot = IVF ? a.qlist[it.qbeg + tid] + it.part : (it.qbeg + tid) * a.nparts + it.part;
+    qown = IVF ? a.qlist[it.qbeg + tid] / a.nparts : it.qbeg + tid;
     if (a.limits) lim = a.limits[oslot];
+    if (a.gthr) gs = key_score(__hip_atomic_load(a.gthr + qown, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   }
   int cnt = 0;
   float thr_s = -INFINITY;  // (-inf, NONE) lets every real candidate pass until the list is full
@@ -296,18 +312,18 @@ __global__ __launch_bounds__(256) void scan_fast(ScanArgs a) {
   // compute) and written to the other LDS buffer after the compute, so their HBM
   // latency hides under a whole stage of VALU work.
   constexpr int NV = GPS * D * 2;  // float4 per stage
-  constexpr int LOADS = (NV + 255) / 256;
+  constexpr int LOADS = (NV + NT - 1) / NT;
   const float4 *src = reinterpret_cast<const float4 *>(a.rows);
   float4 pf[LOADS];
 #define PYR_LOAD_STAGE(STG)                                                                     \
   _Pragma("unroll") for (int i = 0; i < LOADS; ++i) {                                          \
-    const int v = min(tid + 256 * i, NV - 1);                                                   \
+    const int v = min(tid + NT * i, NV - 1);                                                    \
     const int gg = min((STG) * GPS + v / (2 * D), ng - 1); /* clamp: rows past the end unused */ \
     pf[i] = src[(size_t)(g0 + gg) * (2 * D) + v % (2 * D)];                                     \
   }
 #define PYR_STORE_STAGE(BUF)                                                                    \
   _Pragma("unroll") for (int i = 0; i < LOADS; ++i) {                                          \
-    const int v = tid + 256 * i;                                                                \
+    const int v = tid + NT * i;                                                                 \
     if (v < NV) reinterpret_cast<float4 *>(tile + (BUF) * GPS * GF)[v] = pf[i];                 \
   }
   float xn_next[GPS], xn_cur[GPS];  // cosine row norms, prefetched one stage ahead
@@ -344,14 +360,14 @@ __global__ __launch_bounds__(256) void scan_fast(ScanArgs a) {
       for (int g = 0; g < GPS; ++g) {
         if (st * GPS + g >= ng) break;
         const float *tp = tile + cur * GPS * GF + g * GF + l * 8;
-        float fin[4][8];
+        float fin[QS][8];
         if constexpr (V == 1) {
-          // 4 queries x 8 rows per slot, one accumulator per (query, row) for lane l of
+          // QS queries x 8 rows per slot, one accumulator per (query, row) for lane l of
           // the single Vector accumulator (VectorMath.cs:52-58).  LDS reads are
-          // software-pipelined one t-step ahead; sched_barrier pins the order.
-          float acc[4][8];
+          // software-pipelined one t-step ahead.
+          float acc[QS][8];
 #pragma unroll
-          for (int u = 0; u < 4; ++u)
+          for (int u = 0; u < QS; ++u)
 #pragma unroll
             for (int j = 0; j < 8; ++j) acc[u][j] = 0.0f;
           float4 xa = *reinterpret_cast<const float4 *>(tp);
@@ -365,7 +381,7 @@ __global__ __launch_bounds__(256) void scan_fast(ScanArgs a) {
             }
             const float xs[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < QS; ++u) {
               float d[8];
               if constexpr (MET == L2) {
 #pragma unroll
@@ -383,7 +399,7 @@ __global__ __launch_bounds__(256) void scan_fast(ScanArgs a) {
             xb = nb;
           }
 #pragma unroll
-          for (int u = 0; u < 4; ++u)
+          for (int u = 0; u < QS; ++u)
 #pragma unroll
             for (int j = 0; j < 8; ++j) fin[u][j] = acc[u][j];
         } else {
@@ -391,11 +407,11 @@ __global__ __launch_bounds__(256) void scan_fast(ScanArgs a) {
           // rows in two halves of 4 to bound the register tile
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            float acc[4][4][4];
+            float acc[4][QS][4];
 #pragma unroll
             for (int v = 0; v < 4; ++v)
 #pragma unroll
-              for (int u = 0; u < 4; ++u)
+              for (int u = 0; u < QS; ++u)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) acc[v][u][j] = 0.0f;
             float4 xa = *reinterpret_cast<const float4 *>(tp + 4 * h);
@@ -406,7 +422,7 @@ __global__ __launch_bounds__(256) void scan_fast(ScanArgs a) {
               if (t + 1 < T) na = *reinterpret_cast<const float4 *>(tp + (t + 1) * 64 + 4 * h);
               const float xs[4] = {xa.x, xa.y, xa.z, xa.w};
 #pragma unroll
-              for (int u = 0; u < 4; ++u) {
+              for (int u = 0; u < QS; ++u) {
                 float d[4];
                 if constexpr (MET == L2) {
 #pragma unroll
@@ -423,16 +439,16 @@ __global__ __launch_bounds__(256) void scan_fast(ScanArgs a) {
               xa = na;
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
+            for (int u = 0; u < QS; ++u)
 #pragma unroll
               for (int j = 0; j < 4; ++j)
                 fin[u][4 * h + j] = ((acc[0][u][j] + acc[1][u][j]) + acc[2][u][j]) + acc[3][u][j];  // :224
           }
         }
         // transpose-reduce = Vector.Dot(acc, One) tree, one row per lane at the end
-        float r1[4][4], r2[4][2], r3[4];
+        float r1[QS][4], r2[QS][2], r3[QS];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < QS; ++u)
 #pragma unroll
           for (int jp = 0; jp < 4; ++jp) {
             const float x0 = fin[u][2 * jp], x1 = fin[u][2 * jp + 1];
@@ -440,7 +456,7 @@ __global__ __launch_bounds__(256) void scan_fast(ScanArgs a) {
             r1[u][jp] = keep + dpp<0xB1>(send);
           }
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < QS; ++u)
 #pragma unroll
           for (int jq = 0; jq < 2; ++jq) {
             const float x0 = r1[u][2 * jq], x1 = r1[u][2 * jq + 1];
@@ -448,22 +464,21 @@ __global__ __launch_bounds__(256) void scan_fast(ScanArgs a) {
             r2[u][jq] = keep + dpp<0x4E>(send);
           }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < QS; ++u) {
           const float x0 = r2[u][0], x1 = r2[u][1];
           const float keep = c3 ? x1 : x0, send = c3 ? x0 : x1;
           r3[u] = keep + dpp<0x141>(send);
         }
-        float sv[4];
         const float xn = xn_cur[g];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < QS; ++u) {
           const float sum = 0.0f + r3[u];  // `sum += Vector.Dot(...)` with sum = 0f
-          if (MET == L2) sv[u] = -sum;
-          else if (MET == IP) sv[u] = sum;
-          else sv[u] = (qn[u] < 1e-6f || xn < 1e-6f) ? 0.0f : sum / (qn[u] * xn);
+          float sv;
+          if (MET == L2) sv = -sum;
+          else if (MET == IP) sv = sum;
+          else sv = (qn[u] < 1e-6f || xn < 1e-6f) ? 0.0f : sum / (qn[u] * xn);
+          sc[(cur * QCHUNK + s * QS + u) * RS + g * 8 + myj] = sv;
         }
-        *reinterpret_cast<float4 *>(sc + (cur * GPS * 8 + g * 8 + myj) * SCS + s * 4) =
-            make_float4(sv[0], sv[1], sv[2], sv[3]);
       }
     }
     PYR_STORE_STAGE(cur ^ 1)  // after the last stage this fills an unused buffer
@@ -473,22 +488,23 @@ __global__ __launch_bounds__(256) void scan_fast(ScanArgs a) {
 #pragma unroll
       for (int g = 0; g < GPS; ++g) {
         if (st * GPS + g >= ng) break;
-        const float *scp = sc + (cur * GPS * 8 + g * 8) * SCS + tid;
+        const float *scp = sc + (cur * QCHUNK + tid) * RS + g * 8;
         const int rb = (g0 + st * GPS + g) * 8;
         float v[8];
         unsigned pass = 0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          v[j] = scp[j * SCS];
+          v[j] = scp[j];
           const int r = rb + j;
-          if (r < it.row_end && better(v[j], a.key_base | (uint32_t)r, thr_s, thr_k)) pass |= 1u << j;
+          if (r < it.row_end && v[j] >= gs && better(v[j], a.key_base | (uint32_t)r, thr_s, thr_k))
+            pass |= 1u << j;
         }
         if (pass) {  // rare once the list is full
           for (int j = 0; j < 8; ++j) {
             if (!((pass >> j) & 1)) continue;
             const int r = rb + j;
             const uint32_t key = a.key_base | (uint32_t)r;
-            const float vj = scp[j * SCS];
+            const float vj = scp[j];
             if (!better(vj, key, thr_s, thr_k) || (uint32_t)r >= lim || !a.live[r]) continue;
             list_insert(ls, lk, cnt, k, vj, key);
             if (cnt == k) {
@@ -498,9 +514,17 @@ __global__ __launch_bounds__(256) void scan_fast(ScanArgs a) {
           }
         }
       }
+      if (a.gthr && (st & 7) == 7) {  // every 8 stages: publish this list's k-th best, refresh the bound
+        if (cnt == k && score_key(thr_s) > published) {
+          published = score_key(thr_s);
+          atomicMax(a.gthr + qown, published);
+        }
+        gs = fmaxf(gs, key_score(__hip_atomic_load(a.gthr + qown, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+      }
     }
   }
   if (owner) {
+    if (a.gthr && cnt == k && score_key(thr_s) > published) atomicMax(a.gthr + qown, score_key(thr_s));
     float *ps = a.part_s + (size_t)oslot * k;
     uint32_t *pk = a.part_k + (size_t)oslot * k;
     for (int j = 0; j < k; ++j) {
@@ -525,7 +549,7 @@ __global__ __launch_bounds__(64) void scan_generic(ScanArgs a) {
   float *ls = smem + tid * k;
   uint32_t *lk = reinterpret_cast<uint32_t *>(smem + 64 * k) + tid * k;
   const int qi = a.qlist ? a.qlist[it.qbeg + tid] / a.nparts : it.qbeg + tid;
-  const int slot = a.qlist ? a.qlist[it.qbeg + tid] : qi * a.nparts + it.part;
+  const int slot = a.qlist ? a.qlist[it.qbeg + tid] + it.part : qi * a.nparts + it.part;
   const uint32_t lim = a.limits ? a.limits[slot] : 0xFFFFFFFFu;
   const Lin qa{a.queries + (size_t)qi * D};
   const float qn = MET == COS ? a.qnorm[qi] : 0.0f;
@@ -590,7 +614,7 @@ constexpr int MERGE_U = MAX_PARTS / 64;  // parts per lane
 __global__ __launch_bounds__(256) void merge_keys_kernel(const float *ps, const uint32_t *pk, int64_t nq, int nparts,
                                                          int k, const int64_t *row_labels, const int64_t *buf_labels,
                                                          float *out_s, int64_t *out_l, int32_t *out_keys,
-                                                         int32_t *out_cnt) {
+                                                         int32_t *out_cnt, MergeIvf iv) {
   const int lane = threadIdx.x & 63;
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= nq) return;
@@ -598,11 +622,17 @@ __global__ __launch_bounds__(256) void merge_keys_kernel(const float *ps, const 
   float cs[MERGE_U];
   uint32_t ck[MERGE_U];
   const size_t base = (size_t)q * nparts * k;
+  const int ivf_parts = iv.probes ? iv.nprobe * iv.ch.cmax : 0;
 #pragma unroll
   for (int u = 0; u < MERGE_U; ++u) {
     const int p = lane + 64 * u;
     h[u] = 0;
-    if (p < nparts) {
+    bool valid = p < nparts;
+    if (valid && p < ivf_parts) {  // chunk slot p = probe * cmax + c exists iff c < chunks of that list
+      const int lst = iv.probes[q * iv.nprobe + p / iv.ch.cmax];
+      valid = p % iv.ch.cmax < ivf_list_chunks(iv.le[lst] - iv.lb[lst], iv.ch);
+    }
+    if (valid) {
       cs[u] = ps[base + (size_t)p * k];
       ck[u] = pk[base + (size_t)p * k];
     } else {
@@ -646,7 +676,7 @@ __global__ __launch_bounds__(256) void merge_keys_kernel(const float *ps, const 
       if (ck[u] == bk) {  // keys are unique: exactly one lane/u advances
         const int p = lane + 64 * u;
         h[u]++;
-        if (h[u] < k) {
+        if (h[u] < k) {  // a valid slot's list is KEY_NONE-terminated, so reads stay in written slots
           cs[u] = ps[base + (size_t)p * k + h[u]];
           ck[u] = pk[base + (size_t)p * k + h[u]];
         } else {
@@ -732,8 +762,16 @@ __global__ void ivf_count_kernel(const int32_t *probes, int64_t n, int32_t *cnt)
   if (i < n) atomicAdd(&cnt[probes[i]], 1);
 }
 
-// single workgroup: qoff = exclusive scan of cnt, ioff = exclusive scan of ceil(cnt/qchunk)
-__global__ __launch_bounds__(1024) void ivf_scan_kernel(const int32_t *cnt, int nlist, int qchunk, int32_t *qoff,
+// chunks of list `lst` that launch phase `phase` scans (IvfChunking, kernels.h)
+__device__ __forceinline__ int phase_chunks(const int32_t *lb, const int32_t *le, int lst, IvfChunking ch, int phase) {
+  const int n = ivf_list_chunks(le[lst] - lb[lst], ch);
+  if (ch.warm <= 0) return n;
+  return phase == 0 ? 1 : n - 1;
+}
+
+// single workgroup: qoff = exclusive scan of cnt, ioff = exclusive scan of ceil(cnt/qchunk) * chunks
+__global__ __launch_bounds__(1024) void ivf_scan_kernel(const int32_t *cnt, int nlist, int qchunk, const int32_t *lb,
+                                                        const int32_t *le, IvfChunking chk, int phase, int32_t *qoff,
                                                         int32_t *ioff, int32_t *n_items) {
   __shared__ int sq[1024], si[1024];
   const int tid = threadIdx.x;
@@ -742,7 +780,7 @@ __global__ __launch_bounds__(1024) void ivf_scan_kernel(const int32_t *cnt, int 
   int lq = 0, li = 0;
   for (int i = b; i < e; ++i) {
     lq += cnt[i];
-    li += (cnt[i] + qchunk - 1) / qchunk;
+    li += (cnt[i] + qchunk - 1) / qchunk * phase_chunks(lb, le, i, chk, phase);
   }
   sq[tid] = lq;
   si[tid] = li;
@@ -760,7 +798,7 @@ __global__ __launch_bounds__(1024) void ivf_scan_kernel(const int32_t *cnt, int 
     qoff[i] = rq;
     ioff[i] = ri;
     rq += cnt[i];
-    ri += (cnt[i] + qchunk - 1) / qchunk;
+    ri += (cnt[i] + qchunk - 1) / qchunk * phase_chunks(lb, le, i, chk, phase);
   }
   if (tid == 1023) {
     qoff[nlist] = sq[1023];
@@ -769,62 +807,71 @@ __global__ __launch_bounds__(1024) void ivf_scan_kernel(const int32_t *cnt, int 
   }
 }
 
-__global__ void ivf_fill_kernel(const int32_t *probes, int64_t nq, int nprobe, int nparts, const int32_t *qoff,
-                                int32_t *fill, int32_t *qlist) {
+__global__ void ivf_fill_kernel(const int32_t *probes, int64_t nq, int nprobe, int nparts, int cmax,
+                                const int32_t *qoff, int32_t *fill, int32_t *qlist) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nq * nprobe) return;
   const int64_t q = i / nprobe;
   const int p = (int)(i % nprobe);
   const int lst = probes[i];
   const int pos = atomicAdd(&fill[lst], 1);
-  qlist[qoff[lst] + pos] = (int32_t)(q * nparts + p);
+  qlist[qoff[lst] + pos] = (int32_t)(q * nparts + p * cmax);  // chunk c adds c (ScanItem.part)
 }
 
+// items of list l in launch phase `phase`: for each of its row chunks, for each block of
+// <= qchunk probing queries
 __global__ void ivf_items_kernel(const int32_t *cnt, const int32_t *qoff, const int32_t *ioff, int nlist,
-                                 const int32_t *lb, const int32_t *le, int qchunk, ScanItem *items) {
+                                 const int32_t *lb, const int32_t *le, int qchunk, IvfChunking chk, int phase,
+                                 ScanItem *items) {
   const int lst = blockIdx.x * blockDim.x + threadIdx.x;
   if (lst >= nlist) return;
   const int c = cnt[lst];
+  const int len = le[lst] - lb[lst];
+  const int c0 = (chk.warm > 0 && phase == 1) ? 1 : 0;
+  const int c1 = c0 + phase_chunks(lb, le, lst, chk, phase);
   int o = ioff[lst];
-  for (int b = 0; b < c; b += qchunk, ++o) {
-    ScanItem it;
-    it.row_begin = lb[lst];
-    it.row_end = le[lst];
-    it.qbeg = qoff[lst] + b;
-    it.qcnt = min(qchunk, c - b);
-    it.part = 0;
-    it.list = lst;
-    items[o] = it;
+  for (int ch = c0; ch < c1; ++ch) {
+    int rb, re;
+    ivf_chunk_rows(len, ch, chk, &rb, &re);
+    for (int b = 0; b < c; b += qchunk, ++o) {
+      ScanItem it;
+      it.row_begin = lb[lst] + rb;
+      it.row_end = lb[lst] + re;
+      it.qbeg = qoff[lst] + b;
+      it.qcnt = min(qchunk, c - b);
+      it.part = ch;
+      it.list = lst;
+      items[o] = it;
+    }
   }
 }
 
-__global__ void ivf_limits_kernel(const int32_t *probes, int64_t nq, int nprobe, int nparts, int64_t remaining,
-                                  const int32_t *lb, const int32_t *le, const int32_t *llive, const uint8_t *live,
-                                  uint32_t *limits) {
+__global__ void ivf_limits_kernel(const int32_t *probes, int64_t nq, int nprobe, int nparts, int cmax,
+                                  int64_t remaining, const int32_t *lb, const int32_t *le, const int32_t *llive,
+                                  const uint8_t *live, uint32_t *limits) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= nq) return;
   int64_t rem = remaining;
   for (int p = 0; p < nprobe; ++p) {
     const int lst = probes[q * nprobe + p];
-    const size_t slot = (size_t)q * nparts + p;
+    uint32_t lim;
     if (rem <= 0) {
-      limits[slot] = (uint32_t)lb[lst];
-      continue;
-    }
-    if (rem >= llive[lst]) {
-      limits[slot] = (uint32_t)le[lst];
+      lim = (uint32_t)lb[lst];
+    } else if (rem >= llive[lst]) {
+      lim = (uint32_t)le[lst];
       rem -= llive[lst];
-      continue;
+    } else {
+      int64_t c = 0;
+      int r = lb[lst];
+      for (; r < le[lst]; ++r)
+        if (live[r]) {
+          if (c == rem) break;
+          ++c;
+        }
+      lim = (uint32_t)r;
+      rem = 0;
     }
-    int64_t c = 0;
-    int r = lb[lst];
-    for (; r < le[lst]; ++r)
-      if (live[r]) {
-        if (c == rem) break;
-        ++c;
-      }
-    limits[slot] = (uint32_t)r;
-    rem = 0;
+    for (int c = 0; c < cmax; ++c) limits[(size_t)q * nparts + p * cmax + c] = lim;  // bound is absolute
   }
 }
 
@@ -855,7 +902,7 @@ __global__ __launch_bounds__(256) void pq_scan_kernel(PqArgs a) {
   const float *cent = a.cents + (size_t)lst * D;
 
   for (int i = 0; i < it.qcnt; ++i) {
-    const int slot = a.qlist[it.qbeg + i];
+    const int slot = a.qlist[it.qbeg + i] + it.part;
     const int qi = slot / a.nparts;
     const float *qp = a.queries + (size_t)qi * D;
     for (int d = tid; d < D; d += 256) res[d] = qp[d] - cent[d];  // IvfPqVectorIndex.cs:163
@@ -1091,28 +1138,46 @@ __global__ void fill_results_kernel(float *s, int64_t *l, int32_t *c, int64_t nq
 
 inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
-template <int D, int V, int MET, int GPS>
-void launch_fast_g(const ScanArgs &a, int max_items, hipStream_t st) {
-  const size_t lds = (size_t)(2 * GPS * D * 8 + 2 * GPS * 8 * SCS + QCHUNK * a.k * 2) * sizeof(float);
+template <int D, int V, int MET, int GPS, bool IVF, int QS, int W>
+void launch_fast_i(const ScanArgs &a, int max_items, hipStream_t st) {
+  const size_t lds =
+      (size_t)(2 * GPS * D * 8 + 2 * QCHUNK * score_stride<GPS>() + QCHUNK * a.k * 2) * sizeof(float);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&scan_fast<D, V, MET, GPS>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&scan_fast<D, V, MET, GPS, IVF, QS, W>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((scan_fast<D, V, MET, GPS>), dim3(max_items), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((scan_fast<D, V, MET, GPS, IVF, QS, W>), dim3(max_items), dim3(8 * QCHUNK / QS), lds, st, a);
 }
 
-// 8-row groups per LDS stage (default 1; PYR_GPS=2 for A/B measurement)
-int stage_groups() {
-  const char *e = getenv("PYR_GPS");
-  return (e && atoi(e) == 2) ? 2 : 1;
+// Register-tile variant of the fast scan (PYR_SCANVAR overrides for A/B measurement):
+//   0: QS=4, 256 threads (~140 VGPRs, 3 waves/SIMD)
+//   1: QS=2, 512 threads (~98 VGPRs, 4 waves/SIMD)
+//   2: QS=2, 512 threads, register cap for 6 waves/SIMD (80 VGPRs, small spill)
+int scan_variant(int V) {
+  if (const char *e = getenv("PYR_SCANVAR")) return std::min(2, std::max(0, atoi(e)));
+  return V == 1 ? 2 : 1;
+}
+
+template <int D, int V, int MET, int GPS, bool IVF>
+void launch_fast_var(const ScanArgs &a, int max_items, hipStream_t st) {
+  switch (scan_variant(V)) {
+    case 0: launch_fast_i<D, V, MET, GPS, IVF, 4, 1>(a, max_items, st); return;
+    case 1: launch_fast_i<D, V, MET, GPS, IVF, 2, 1>(a, max_items, st); return;
+    default: launch_fast_i<D, V, MET, GPS, IVF, 2, 6>(a, max_items, st); return;
+  }
 }
 
 template <int D, int V, int MET>
 void launch_fast_t(const ScanArgs &a, int max_items, hipStream_t st) {
-  if (stage_groups() == 1) launch_fast_g<D, V, MET, 1>(a, max_items, st);
-  else launch_fast_g<D, V, MET, 2>(a, max_items, st);
+  if constexpr (V == 1) {  // IVF list scans use the safe (1-accumulator) VectorMath form
+    if (a.qlist) {
+      launch_fast_var<D, V, MET, 1, true>(a, max_items, st);
+      return;
+    }
+  }
+  launch_fast_var<D, V, MET, 1, false>(a, max_items, st);
 }
 
 template <int V, int MET>
@@ -1186,10 +1251,11 @@ void launch_norms(const float *x, int64_t n, int32_t dim, int blocked, float *ou
 
 void launch_merge_keys(const float *ps, const uint32_t *pk, int64_t nq, int32_t nparts, int32_t k,
                        const int64_t *row_labels, const int64_t *buf_labels, float *out_s, int64_t *out_l,
-                       int32_t *out_keys, int32_t *out_cnt, hipStream_t st) {
+                       int32_t *out_keys, int32_t *out_cnt, hipStream_t st, const MergeIvf *ivf) {
   if (nq <= 0) return;
+  const MergeIvf iv = ivf ? *ivf : MergeIvf{};
   hipLaunchKernelGGL(merge_keys_kernel, dim3(nblk(nq, 4)), dim3(256), 0, st, ps, pk, nq, nparts, k, row_labels,
-                     buf_labels, out_s, out_l, out_keys, out_cnt);
+                     buf_labels, out_s, out_l, out_keys, out_cnt, iv);
 }
 
 void launch_merge_labels(const float *ps, const int64_t *pl, int64_t nq, int32_t nparts, int32_t k, float *out_s,
@@ -1198,31 +1264,36 @@ void launch_merge_labels(const float *ps, const int64_t *pl, int64_t nq, int32_t
   hipLaunchKernelGGL(merge_labels_kernel, dim3(nblk(nq, 4)), dim3(256), 0, st, ps, pl, nq, nparts, k, out_s, out_l);
 }
 
-int ivf_max_items(int64_t nq, int32_t nprobe, int32_t nlist, int32_t qchunk) {
-  return (int)((nq * nprobe + qchunk - 1) / qchunk) + nlist;
+int64_t ivf_max_items(int64_t nq, int32_t nprobe, int32_t nlist, int32_t qchunk, IvfChunking ch, int phase) {
+  // sum_l ceil(cnt_l / qchunk) * chunks_l <= chunks_max * (ceil(nq * nprobe / qchunk) + nlist)
+  const int64_t cm = ch.warm > 0 ? (phase == 0 ? 1 : std::max(1, ch.cmax - 1)) : ch.cmax;
+  return cm * ((nq * nprobe + qchunk - 1) / qchunk + nlist);
 }
 
 void launch_ivf_items(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t nparts, int32_t nlist,
-                      const int32_t *list_begin, const int32_t *list_end, int32_t qchunk, IvfItemWs &ws,
-                      hipStream_t st) {
-  (void)hipMemsetAsync(ws.cnt, 0, sizeof(int32_t) * nlist, st);
-  (void)hipMemsetAsync(ws.fill, 0, sizeof(int32_t) * nlist, st);
+                      const int32_t *list_begin, const int32_t *list_end, int32_t qchunk, IvfChunking ch,
+                      int phase, IvfItemWs &ws, hipStream_t st) {
   const int64_t n = nq * nprobe;
-  if (n > 0) hipLaunchKernelGGL(ivf_count_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, probes, n, ws.cnt);
-  hipLaunchKernelGGL(ivf_scan_kernel, dim3(1), dim3(1024), 0, st, ws.cnt, nlist, qchunk, ws.qoff, ws.ioff, ws.n_items);
-  if (n > 0)
-    hipLaunchKernelGGL(ivf_fill_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, probes, nq, nprobe, nparts, ws.qoff,
-                       ws.fill, ws.qlist);
+  if (phase == 0) {
+    (void)hipMemsetAsync(ws.cnt, 0, sizeof(int32_t) * nlist, st);
+    (void)hipMemsetAsync(ws.fill, 0, sizeof(int32_t) * nlist, st);
+    if (n > 0) hipLaunchKernelGGL(ivf_count_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, probes, n, ws.cnt);
+  }
+  hipLaunchKernelGGL(ivf_scan_kernel, dim3(1), dim3(1024), 0, st, ws.cnt, nlist, qchunk, list_begin, list_end, ch,
+                     phase, ws.qoff, ws.ioff, ws.n_items);
+  if (phase == 0 && n > 0)
+    hipLaunchKernelGGL(ivf_fill_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, probes, nq, nprobe, nparts, ch.cmax,
+                       ws.qoff, ws.fill, ws.qlist);
   hipLaunchKernelGGL(ivf_items_kernel, dim3(nblk(nlist, 256)), dim3(256), 0, st, ws.cnt, ws.qoff, ws.ioff, nlist,
-                     list_begin, list_end, qchunk, ws.items);
+                     list_begin, list_end, qchunk, ch, phase, ws.items);
 }
 
 void launch_ivf_limits(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t nparts, int64_t remaining,
                        const int32_t *list_begin, const int32_t *list_end, const int32_t *list_live,
-                       const uint8_t *live, uint32_t *limits, hipStream_t st) {
+                       const uint8_t *live, IvfChunking ch, uint32_t *limits, hipStream_t st) {
   if (nq <= 0) return;
-  hipLaunchKernelGGL(ivf_limits_kernel, dim3(nblk(nq, 64)), dim3(64), 0, st, probes, nq, nprobe, nparts, remaining,
-                     list_begin, list_end, list_live, live, limits);
+  hipLaunchKernelGGL(ivf_limits_kernel, dim3(nblk(nq, 64)), dim3(64), 0, st, probes, nq, nprobe, nparts, ch.cmax,
+                     remaining, list_begin, list_end, list_live, live, limits);
 }
 
 size_t pq_scan_lds_bytes(int dim, int M, int ksub, int k) {

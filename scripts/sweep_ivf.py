@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""Measurement sweep for the IVF-Flat list scan (run on the GPU box): builds the bench index
+once, prints list-size statistics, then times the batched search under each setting of the
+PYR_* knobs given on the command line (env values are read by the library per search).
+
+    python scripts/sweep_ivf.py --n 10000000 PYR_IVF_CHUNK=1024,2048,4096
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=10_000_000)
+    ap.add_argument("--dim", type=int, default=128)
+    ap.add_argument("--nlist", type=int, default=1024)
+    ap.add_argument("--nprobe", type=int, default=32)
+    ap.add_argument("--nq", type=int, default=10_000)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("knobs", nargs="*", help="NAME=v1,v2,...")
+    args = ap.parse_args()
+
+    import torch
+    from pyrope_amd import IvfFlatVectorIndex, VectorMetric, generate_synthetic, kmeans_train, _lib
+    from pyrope_amd.vector import SearchOptions
+    L = _lib.load()
+    dev = torch.device("cuda", 0)
+    x = generate_synthetic(args.n, args.dim, 42)
+    cents = kmeans_train(x, args.nlist, VectorMetric.L2, 10, 42)
+    idx = IvfFlatVectorIndex(args.dim, VectorMetric.L2, n_list=args.nlist)
+    idx.set_centroids(cents)
+    idx.add_labels(np.arange(args.n, dtype=np.int64), x)
+    idx.build()
+    off, _, _ = idx.ivf_layout()
+    ln = np.diff(off)
+    print(f"lists: n={len(ln)} mean={ln.mean():.0f} min={ln.min()} p50={np.median(ln):.0f} "
+          f"p99={np.percentile(ln, 99):.0f} max={ln.max()}", flush=True)
+    q = torch.from_numpy(generate_synthetic(args.nq, args.dim, 1337)).to(dev)
+    s = torch.empty((args.nq, args.k), dtype=torch.float32, device=dev)
+    lab = torch.empty((args.nq, args.k), dtype=torch.int64, device=dev)
+    opts = SearchOptions(nprobe=args.nprobe)
+    st = torch.cuda.current_stream().cuda_stream
+
+    def run():
+        idx.search_device(q.data_ptr(), args.nq, args.k, s.data_ptr(), lab.data_ptr(), 0, st, opts)
+
+    settings = [{}]
+    for kv in args.knobs:
+        name, vals = kv.split("=", 1)
+        settings = [dict(d, **{name: v}) for d in settings for v in vals.split(",")]
+    ref = None
+    for cfg in settings:
+        for kname, v in cfg.items():
+            os.environ[kname] = v
+        run()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(args.steps):
+            run()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t) / args.steps
+        L.pyr_profile_reset()
+        L.pyr_profile_enable(1)
+        run()
+        torch.cuda.synchronize()
+        L.pyr_profile_enable(0)
+        ph = {}
+        for i, name in enumerate(["coarse", "items", "scan", "buf", "merge"]):
+            ms, calls, work = C.c_double(), C.c_int64(), C.c_int64()
+            L.pyr_profile_get(i, C.byref(ms), C.byref(calls), C.byref(work))
+            if calls.value:
+                ph[name] = round(ms.value / calls.value, 3)
+        res = (s.cpu().numpy().copy(), lab.cpu().numpy().copy())
+        same = None
+        if ref is None:
+            ref = res
+        else:
+            same = bool(np.array_equal(ref[0].view(np.uint32), res[0].view(np.uint32)) and
+                        np.array_equal(ref[1], res[1]))
+        print(f"{cfg}: {dt * 1e3:.2f} ms/step  {args.nq / dt:,.0f} QPS  phases {ph}  same_as_first={same}",
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,151 @@
+"""MFMA candidate filter + exact refine (pyrope_amd/csrc/filter.hip) on the GPU.
+
+The filter path is the default for FLAT and built IVF_FLAT indexes (L2 / IP).  Its results
+must be bit-identical to the exact VALU scan (PYR_FILTER=0) and to the CPU oracle, including
+when the certificate fails and queries are re-run exactly (forced here with duplicated rows
+and with a zero candidate margin).  Reference: Vector/BruteForceVectorIndex.cs:275-379,
+Vector/IvfFlatVectorIndex.cs:147-231, VectorMath.cs.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+class _env:
+    def __init__(self, **kv):
+        self.kv = {k: str(v) for k, v in kv.items()}
+
+    def __enter__(self):
+        self.old = {k: os.environ.get(k) for k in self.kv}
+        os.environ.update(self.kv)
+
+    def __exit__(self, *a):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _fallbacks(hiplib, fn):
+    """Run fn() with the phase profiler on; return (result, queries re-run exactly)."""
+    hiplib.pyr_profile_reset()
+    hiplib.pyr_profile_enable(1)
+    try:
+        out = fn()
+    finally:
+        hiplib.pyr_profile_enable(0)
+    ms, calls, work = C.c_double(), C.c_int64(), C.c_int64()
+    hiplib.pyr_profile_get(8, C.byref(ms), C.byref(calls), C.byref(work))
+    return out, work.value
+
+
+def _same(a, b):
+    (s1, l1, c1), (s2, l2, c2) = a, b
+    np.testing.assert_array_equal(c1, c2)
+    np.testing.assert_array_equal(l1, l2)
+    assert np.array_equal(s1.view(np.uint32), s2.view(np.uint32))
+
+
+def _flat(dim, metric, x):
+    from pyrope_amd import BruteForceVectorIndex
+    idx = BruteForceVectorIndex(dim, metric)
+    idx.add_labels(np.arange(len(x), dtype=np.int64), x)
+    return idx
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+@pytest.mark.parametrize("dim", [128, 64, 32])
+def test_flat_filter_equals_exact_and_oracle(hiplib, oracle, metric, dim):
+    from pyrope_amd import generate_synthetic
+    x = generate_synthetic(20000, dim, 42)
+    q = generate_synthetic(300, dim, 1337)
+    idx = _flat(dim, metric, x)
+    got, nfb = _fallbacks(hiplib, lambda: idx.search_batch(q, 10))
+    with _env(PYR_FILTER=0):
+        ref = idx.search_batch(q, 10)
+    _same(got, ref)
+    for i in range(0, len(q), 37):
+        os_, ok = oracle.bf_search(x, None, metric, q[i], 10)
+        np.testing.assert_array_equal(got[1][i], ok)
+        assert np.array_equal(got[0][i].view(np.uint32), os_.view(np.uint32))
+    assert nfb < len(q)  # the certificate holds for (almost) every query of uniform data
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_ivf_filter_equals_exact_and_oracle(hiplib, oracle, metric):
+    from pyrope_amd import IvfFlatVectorIndex, SearchOptions, generate_synthetic
+    x = generate_synthetic(20000, 128, 42)
+    idx = IvfFlatVectorIndex(128, metric, n_list=64)
+    idx.add_labels(np.arange(len(x), dtype=np.int64), x)
+    idx.build()
+    q = generate_synthetic(500, 128, 1337)
+    opts = SearchOptions(nprobe=8)
+    got = idx.search_batch(q, 10, opts)
+    with _env(PYR_FILTER=0):
+        ref = idx.search_batch(q, 10, opts)
+    _same(got, ref)
+    off, labels, live = idx.ivf_layout()
+    rows = x[np.where(labels >= 0, labels, 0)]
+    cents = idx.centroids_array()
+    for i in range(0, len(q), 50):
+        os_, ok = oracle.ivf_search(q[i], 10, cents, rows, off, live, metric=metric, nprobe=8)
+        np.testing.assert_array_equal(got[1][i], labels[ok])
+        assert np.array_equal(got[0][i].view(np.uint32), os_.view(np.uint32))
+
+
+def test_flat_duplicates_force_exact_rerun(hiplib, oracle):
+    """Exact ties at the k-th place cannot be certified: those queries are re-run exactly and
+    the tie rule (score desc, storage slot asc) still holds."""
+    from pyrope_amd import generate_synthetic
+    base = generate_synthetic(200, 128, 7)
+    x = np.repeat(base, 25, axis=0)  # every vector 25 times
+    q = generate_synthetic(64, 128, 8)
+    idx = _flat(128, 0, x)
+    got, nfb = _fallbacks(hiplib, lambda: idx.search_batch(q, 10))
+    assert nfb > 0
+    with _env(PYR_FILTER=0):
+        ref = idx.search_batch(q, 10)
+    _same(got, ref)
+    for i in range(0, len(q), 9):
+        os_, ok = oracle.bf_search(x, None, 0, q[i], 10)
+        np.testing.assert_array_equal(got[1][i], ok)
+
+
+@pytest.mark.parametrize("margin", [0, 2])
+def test_small_margin_reruns_stay_exact(hiplib, margin):
+    from pyrope_amd import IvfFlatVectorIndex, SearchOptions, generate_synthetic
+    x = generate_synthetic(12000, 64, 3)
+    idx = IvfFlatVectorIndex(64, 0, n_list=32)
+    idx.add_labels(np.arange(len(x), dtype=np.int64), x)
+    idx.build()
+    q = generate_synthetic(200, 64, 4)
+    opts = SearchOptions(nprobe=6)
+    with _env(PYR_FILTER_MARGIN=margin):
+        got = idx.search_batch(q, 10, opts)
+    with _env(PYR_FILTER=0):
+        ref = idx.search_batch(q, 10, opts)
+    _same(got, ref)
+
+
+def test_flat_filter_respects_max_scans_and_deletes(hiplib, oracle):
+    from pyrope_amd import SearchOptions, generate_synthetic
+    x = generate_synthetic(5000, 128, 11)
+    q = generate_synthetic(40, 128, 12)
+    idx = _flat(128, 0, x)
+    for d in range(0, 5000, 7):
+        idx.delete(str(d))
+    live = np.ones(5000, np.uint8)
+    live[::7] = 0
+    for ms in [None, 1, 100, 2500]:
+        got = idx.search_batch(q, 10, SearchOptions(max_scans=ms))
+        with _env(PYR_FILTER=0):
+            ref = idx.search_batch(q, 10, SearchOptions(max_scans=ms))
+        _same(got, ref)
+        for i in range(0, len(q), 13):
+            os_, ok = oracle.bf_search(x, live, 0, q[i], 10, max_scans=-1 if ms is None else ms)
+            np.testing.assert_array_equal(got[1][i][: len(ok)], ok)
