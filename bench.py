@@ -140,14 +140,21 @@ def main():
     torch.cuda.synchronize()
     L.pyr_profile_enable(0)
     import ctypes as C
-    names = {0: "coarse", 1: "work_lists", 2: "list_scan", 3: "buffer_scan", 4: "merge"}
+    names = {0: "coarse", 1: "work_lists", 2: "list_scan", 3: "buffer_scan", 4: "merge", 7: "refine",
+             8: "exact_rerun"}
+    fallback_queries = 0
     for ph, name in names.items():
         ms, calls, work = C.c_double(), C.c_int64(), C.c_int64()
         L.pyr_profile_get(ph, C.byref(ms), C.byref(calls), C.byref(work))
         if calls.value:
             phases[name] = {"ms": ms.value / calls.value, "pairs": work.value // calls.value}
+        if ph == 8:
+            fallback_queries = work.value
     scan = phases.get("list_scan", {"ms": float("nan"), "pairs": 0})
-    flops = scan["pairs"] * 3 * D               # 3 flops (sub, mul, add) per element
+    filt = os.environ.get("PYR_FILTER", "1") != "0"
+    # MFMA filter (default): the (query, row) GEMM, 2*D flops per pair; exact VALU scan
+    # (PYR_FILTER=0): sub, mul, add per element, 3*D
+    flops = scan["pairs"] * (2 if filt else 3) * D
     achieved = flops / (scan["ms"] * 1e-3) / 1e12
 
     # ---- recall@10 vs exact FLAT top-10 (rank 0) ----
@@ -214,9 +221,15 @@ def main():
             "recall_at_10": recall,
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None,
-                         "kernel": "scan_fast<128,1,L2> (IVF list scan)",
-                         "note": "FP32 compute bound (FP32 VALU peak == FP32 MFMA peak on gfx950); "
-                                 "algorithmic FLOPs = pairs x 3*D per launch"},
+                         "kernel": ("mfma_filter<128,L2,IVF> (IVF list scan, fp32 MFMA candidate filter)" if filt
+                                    else "scan_fast<128,1,L2,IVF> (IVF list scan, exact VALU)"),
+                         "note": ("dense FP32 MFMA peak; algorithmic FLOPs = probed (query,row) pairs x 2*D per "
+                                  "launch (the q.x GEMM; |x|^2 precomputed), HIP-event time of the launch"
+                                  if filt else
+                                  "FP32 peak; algorithmic FLOPs = probed pairs x 3*D (sub, mul, add) per launch; "
+                                  "non-FMA VALU ops top out at half this peak")},
+            "exact_reruns": {"queries": fallback_queries, "in_profiled_steps": args.profile_steps,
+                             "note": "queries whose MFMA-filter certificate failed and were re-scanned exactly"},
             "hbm_equivalent": {"bytes_per_query": bytes_per_query,
                                "GBps": qps * bytes_per_query / 1e9 / world,
                                "frac_of_8TBps_per_gpu": qps * bytes_per_query / 1e9 / world / HBM_PEAK_GBS},

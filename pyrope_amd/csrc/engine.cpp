@@ -251,10 +251,24 @@ static bool filter_enabled() {
   const char *e = getenv("PYR_FILTER");
   return !(e && atoi(e) == 0);
 }
+static int filter_ablate() {  // measurement only (FilterArgs::ablate)
+  const char *e = getenv("PYR_FILTER_ABLATE");
+  return e ? atoi(e) : 0;
+}
+// K1 = candidates per query: the smallest register-list capacity (16, 32, 64) leaving at
+// least 4 candidates beyond k (PYR_FILTER_MARGIN overrides the 4); 0 = filter unavailable
 static int filter_k1(int k) {
-  int m = 8;
+  int m = 4;
   if (const char *e = getenv("PYR_FILTER_MARGIN")) m = std::max(0, atoi(e));
-  return std::min(64, k + m);
+  for (int c : {16, 32, 64})
+    if (k + m <= c) return c;
+  return 0;
+}
+// error-bound constant of the refine certificate (filter.hip refine_kernel); PYR_FILTER_CERR
+// overrides it for tests (a huge value fails every certificate -> every query re-runs exactly)
+static double filter_cerr(int dim) {
+  if (const char *e = getenv("PYR_FILTER_CERR")) return atof(e);
+  return 4.0 * dim + 64.0;
 }
 
 // merge the K1-candidate partials, re-score exactly, certify; returns the number of
@@ -283,7 +297,7 @@ static int64_t filter_finish(Workspace &ws, int64_t nq, int nparts, int k1, int 
   r.k1 = k1;
   r.k = k;
   r.dim = dim;
-  r.c_err = 4.0 * dim + 64.0;
+  r.c_err = filter_cerr(dim);
   r.out_s = d_s;
   r.out_l = d_l;
   r.out_c = d_c;
@@ -518,6 +532,7 @@ struct FlatIndex : Index {
     fa.part_s = ws.part_s.as<float>();
     fa.part_k = ws.part_k.as<uint32_t>();
     fa.gthr = gthr;
+    fa.ablate = filter_ablate();
     {
       PhaseTimer t(PH_FLAT_SCAN, ws.st, nq * cutoff);
       launch_filter(fa, metric, p.nitems, ws.st);
@@ -992,6 +1007,7 @@ struct IvfFlatIndex : Index {
     fa.part_s = ws.part_s.as<float>();
     fa.part_k = ws.part_k.as<uint32_t>();
     fa.gthr = gthr;
+    fa.ablate = filter_ablate();
     {
       PhaseTimer t(PH_LIST_SCAN, ws.st, prof().on ? probed_rows(ws, nq, probes, le, lb) : 0);
       launch_filter(fa, metric, maxi, ws.st);

@@ -44,21 +44,6 @@ __device__ __forceinline__ size_t blk_off(int64_t r, int d, int D) {
   return ((size_t)(r >> 3) * (size_t)D + (size_t)d) * 8 + (size_t)(r & 7);
 }
 
-__device__ __forceinline__ void list_insert(float *ls, uint32_t *lk, int &cnt, int k, float s, uint32_t key) {
-  int n = cnt;
-  if (n == k) n = k - 1;
-  int j = n;
-  while (j > 0 && better(s, key, ls[j - 1], lk[j - 1])) {
-    ls[j] = ls[j - 1];
-    lk[j] = lk[j - 1];
-    j--;
-  }
-  ls[j] = s;
-  lk[j] = key;
-  cnt = n + 1;
-}
-
-constexpr int FQ = 128;      // queries per work item (4 waves x 32)
 constexpr int RT = 32;       // rows per stage (one 32x32 MFMA tile per wave)
 constexpr int SCR = RT + 4;  // score-transpose row stride (floats)
 
@@ -67,7 +52,7 @@ template <int D>
 struct FilterLds {
   static constexpr int RSTR = D + 4;      // padded row stride: conflict-free ds_read_b128 / ds_write_b32
   static constexpr int TILE = RT * RSTR;  // floats per row tile
-  static constexpr size_t bytes(int k1) { return sizeof(float) * (2 * TILE + 4 * 32 * SCR) + (size_t)FQ * k1 * 8; }
+  static constexpr size_t bytes() { return sizeof(float) * (2 * TILE + 4 * 32 * SCR); }
 };
 
 // ---------------------------------------------------------------------------
@@ -81,18 +66,32 @@ struct FilterLds {
 // them against the query's K1-th best / shared bound and inserts survivors into the
 // query's LDS list.
 // ---------------------------------------------------------------------------
-template <int D, int MET, bool IVF>
+// Insert (v, key) into a register-resident sorted (desc) list of compile-time length KR:
+// a branch-free compare-and-shift network (no LDS round trips; the owner lanes of a wave
+// run it together whenever any of them has a candidate, so it must be cheap).
+template <int KR>
+__device__ __forceinline__ void reg_insert(float (&s)[KR], uint32_t (&kk)[KR], float v, uint32_t key) {
+  bool b[KR];
+#pragma unroll
+  for (int j = 0; j < KR; ++j) b[j] = better(v, key, s[j], kk[j]);  // monotone: false..false true..true
+#pragma unroll
+  for (int j = KR - 1; j >= 1; --j) {
+    s[j] = b[j - 1] ? s[j - 1] : (b[j] ? v : s[j]);
+    kk[j] = b[j - 1] ? kk[j - 1] : (b[j] ? key : kk[j]);
+  }
+  s[0] = b[0] ? v : s[0];
+  kk[0] = b[0] ? key : kk[0];
+}
+
+template <int D, int MET, bool IVF, int KR>
 __global__ __launch_bounds__(256, 2) void mfma_filter(FilterArgs a) {
   using L = FilterLds<D>;
   constexpr int KH = D / 2;  // k-steps: lanes 0-31 take dims [0, KH), lanes 32-63 [KH, D)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   if ((int)blockIdx.x >= *a.n_items) return;
   const ScanItem it = a.items[blockIdx.x];
-  const int k1 = a.k1;
   float *rt = smem;                 // [2][RT][RSTR]
   float *scw = smem + 2 * L::TILE;  // [4][32][SCR]
-  float *tks = scw + 4 * 32 * SCR;  // [FQ][k1]
-  uint32_t *tkk = reinterpret_cast<uint32_t *>(tks + FQ * k1);
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int i32 = lane & 31, h = lane >> 5;
@@ -131,11 +130,13 @@ __global__ __launch_bounds__(256, 2) void mfma_filter(FilterArgs a) {
     qown = IVF ? a.qlist[it.qbeg + oq] / a.nparts : it.qbeg + oq;
     if (a.gthr) gs = key_score(__hip_atomic_load(a.gthr + qown, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   }
-  int cnt = 0;
-  float thr_s = -INFINITY;
-  uint32_t thr_k = KEY_NONE;
-  float *ls = tks + oq * k1;
-  uint32_t *lk = tkk + oq * k1;
+  float ts[KR];  // this owner's top-KR by approximate score, sorted desc; (-inf, NONE) = empty
+  uint32_t tk[KR];
+#pragma unroll
+  for (int j = 0; j < KR; ++j) {
+    ts[j] = -INFINITY;
+    tk[j] = KEY_NONE;
+  }
 
   // stage staging: RT rows of the blocked store = RT/8 groups of [D][8]; float4 v of a
   // group holds rows (v&1)*4 .. +3 at dim v>>1 (kernels.hip blk_off)
@@ -168,7 +169,18 @@ __global__ __launch_bounds__(256, 2) void mfma_filter(FilterArgs a) {
     }
   };
 
+  // this lane's C column (a row) per stage: visibility and |x|^2 are loaded one stage
+  // ahead, with that stage's rows, so the stage that uses them never waits on a load
+  // (vmcnt is in order: a load issued behind the row prefetch would drain it)
+  uint8_t lv_next = 0;
+  float xsq_next = 0.0f;
+  auto load_meta = [&](int stg) {
+    const int rc = min(r0 + stg * RT + i32, it.row_end - 1);
+    lv_next = a.live[rc];
+    if (MET == L2) xsq_next = a.rsq[rc];
+  };
   if (nst > 0) {
+    load_meta(0);
     load_stage(0);
     store_stage(0);
   }
@@ -176,12 +188,14 @@ __global__ __launch_bounds__(256, 2) void mfma_filter(FilterArgs a) {
 
   for (int st = 0; st < nst; ++st) {
     const int cur = st & 1;
-    if (st + 1 < nst) load_stage(st + 1);
-    const int row = r0 + st * RT + i32;  // this lane's C column
-    const int rc = min(row, it.row_end - 1);
-    const bool rvalid = row < it.row_end && (uint32_t)row < a.row_limit && a.live[rc];
-    const float xsq = MET == L2 ? a.rsq[rc] : 0.0f;
-    if (wave_active) {
+    const int row = r0 + st * RT + i32;
+    const bool rvalid = row < it.row_end && (uint32_t)row < a.row_limit && lv_next;
+    const float xsq = xsq_next;
+    if (st + 1 < nst) {
+      load_meta(st + 1);
+      if (!(a.ablate & 4)) load_stage(st + 1);
+    }
+    if (wave_active && !(a.ablate & 8)) {
       f16v acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
@@ -195,40 +209,40 @@ __global__ __launch_bounds__(256, 2) void mfma_filter(FilterArgs a) {
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qa[4 * s4 + 3], b.w, acc, 0, 0, 0);
       }
       // C[i][j]: lane column j = i32 (row), register r -> query (r&3) + 8(r>>2) + 4h
+      if (!(a.ablate & 2)) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int qi = (r & 3) + 8 * (r >> 2) + 4 * h;
-        const float s = MET == L2 ? 2.0f * acc[r] - xsq : acc[r];
-        sc[qi * SCR + i32] = rvalid ? s : -INFINITY;
+        for (int r = 0; r < 16; ++r) {
+          const int qi = (r & 3) + 8 * (r >> 2) + 4 * h;
+          const float s = MET == L2 ? 2.0f * acc[r] - xsq : acc[r];
+          sc[qi * SCR + i32] = rvalid ? s : -INFINITY;
+        }
+      } else if (acc[0] == 12345.0f) {
+        sc[i32] = acc[1];  // keep the MFMAs alive in the ablated build
       }
     }
-    if (st + 1 < nst) store_stage(cur ^ 1);
+    if (st + 1 < nst && !(a.ablate & 4)) store_stage(cur ^ 1);
     __syncthreads();  // next tile staged; this wave's score transpose visible
 
-    if (owner) {
+    if (owner && !(a.ablate & 1)) {
       const float *scp = sc + i32 * SCR;
       const int rb = r0 + st * RT;
       uint32_t pass = 0;
+      const float lo = fmaxf(gs, ts[KR - 1]);  // cheap pre-filter; the full (score, key) test follows
 #pragma unroll
       for (int j = 0; j < RT; ++j) {
         const float v = scp[j];
-        if (v > -INFINITY && v >= gs && better(v, a.key_base | (uint32_t)(rb + j), thr_s, thr_k)) pass |= 1u << j;
+        if (v > -INFINITY && v >= lo) pass |= 1u << j;
       }
       while (pass) {
         const int j = __builtin_ctz(pass);
         pass &= pass - 1;
         const float v = scp[j];
         const uint32_t key = a.key_base | (uint32_t)(rb + j);
-        if (!better(v, key, thr_s, thr_k)) continue;
-        list_insert(ls, lk, cnt, k1, v, key);
-        if (cnt == k1) {
-          thr_s = ls[k1 - 1];
-          thr_k = lk[k1 - 1];
-        }
+        if (better(v, key, ts[KR - 1], tk[KR - 1])) reg_insert<KR>(ts, tk, v, key);
       }
-      if (a.gthr && (st & 7) == 7) {  // every 8 stages: publish this list's K1-th best, refresh the bound
-        if (cnt == k1 && score_key(thr_s) > published) {
-          published = score_key(thr_s);
+      if (a.gthr && (st & 7) == 7) {  // every 8 stages: publish this list's KR-th best, refresh the bound
+        if (tk[KR - 1] != KEY_NONE && score_key(ts[KR - 1]) > published) {
+          published = score_key(ts[KR - 1]);
           atomicMax(a.gthr + qown, published);
         }
         gs = fmaxf(gs, key_score(__hip_atomic_load(a.gthr + qown, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
@@ -236,12 +250,14 @@ __global__ __launch_bounds__(256, 2) void mfma_filter(FilterArgs a) {
     }
   }
   if (owner) {
-    if (a.gthr && cnt == k1 && score_key(thr_s) > published) atomicMax(a.gthr + qown, score_key(thr_s));
-    float *ps = a.part_s + (size_t)oslot * k1;
-    uint32_t *pk = a.part_k + (size_t)oslot * k1;
-    for (int j = 0; j < k1; ++j) {
-      ps[j] = j < cnt ? ls[j] : -INFINITY;
-      pk[j] = j < cnt ? lk[j] : KEY_NONE;
+    if (a.gthr && tk[KR - 1] != KEY_NONE && score_key(ts[KR - 1]) > published)
+      atomicMax(a.gthr + qown, score_key(ts[KR - 1]));
+    float *ps = a.part_s + (size_t)oslot * KR;
+    uint32_t *pk = a.part_k + (size_t)oslot * KR;
+#pragma unroll
+    for (int j = 0; j < KR; ++j) {
+      ps[j] = ts[j];
+      pk[j] = tk[j];
     }
   }
 }
@@ -416,31 +432,34 @@ __global__ void sqnorms_kernel(const float *rows, const int64_t *slots, int64_t 
 
 inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
-template <int D, int MET, bool IVF>
+template <int D, int MET, bool IVF, int KR>
 void launch_filter_t(const FilterArgs &a, int max_items, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mfma_filter<D, MET, IVF>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mfma_filter<D, MET, IVF, KR>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((mfma_filter<D, MET, IVF>), dim3(max_items), dim3(256), FilterLds<D>::bytes(a.k1), st, a);
+  hipLaunchKernelGGL((mfma_filter<D, MET, IVF, KR>), dim3(max_items), dim3(256), FilterLds<D>::bytes(), st, a);
+}
+
+template <int D, int MET, bool IVF>
+void launch_filter_k(const FilterArgs &a, int max_items, hipStream_t st) {
+  if (a.k1 == 16) launch_filter_t<D, MET, IVF, 16>(a, max_items, st);
+  else if (a.k1 == 32) launch_filter_t<D, MET, IVF, 32>(a, max_items, st);
+  else launch_filter_t<D, MET, IVF, 64>(a, max_items, st);
 }
 
 template <int D>
 void launch_filter_d(const FilterArgs &a, int metric, int max_items, hipStream_t st) {
   const bool ivf = a.qlist != nullptr;
   if (metric == L2) {
-    if (ivf) launch_filter_t<D, L2, true>(a, max_items, st);
-    else launch_filter_t<D, L2, false>(a, max_items, st);
+    if (ivf) launch_filter_k<D, L2, true>(a, max_items, st);
+    else launch_filter_k<D, L2, false>(a, max_items, st);
   } else {
-    if (ivf) launch_filter_t<D, IP, true>(a, max_items, st);
-    else launch_filter_t<D, IP, false>(a, max_items, st);
+    if (ivf) launch_filter_k<D, IP, true>(a, max_items, st);
+    else launch_filter_k<D, IP, false>(a, max_items, st);
   }
-}
-
-size_t filter_lds(int dim, int k1) {
-  return dim == 128 ? FilterLds<128>::bytes(k1) : dim == 64 ? FilterLds<64>::bytes(k1) : FilterLds<32>::bytes(k1);
 }
 
 }  // namespace
@@ -448,7 +467,7 @@ size_t filter_lds(int dim, int k1) {
 bool filter_supported(int dim, int metric, int k1) {
   if (metric != L2 && metric != IP) return false;
   if (dim != 32 && dim != 64 && dim != 128) return false;
-  return k1 >= 1 && k1 <= 64 && filter_lds(dim, k1) <= 160 * 1024;
+  return k1 == 16 || k1 == 32 || k1 == 64;  // register list capacities (mfma_filter KR)
 }
 
 void launch_filter(const FilterArgs &a, int metric, int max_items, hipStream_t st) {

@@ -191,6 +191,8 @@ struct FilterArgs {
   float *part_s;           // [slot][k1] approximate scores
   uint32_t *part_k;        // [slot][k1] keys
   uint32_t *gthr;          // shared per-query bound in approximate-score space, or null
+  int32_t ablate;          // measurement only (PYR_FILTER_ABLATE; results are wrong when set):
+                           // 1 skip the owner filter, 2 skip the score transpose, 4 skip row loads, 8 skip MFMA
 };
 struct RefineArgs {
   const float *rows;        // blocked store the keys index

@@ -116,8 +116,10 @@ def test_flat_duplicates_force_exact_rerun(hiplib, oracle):
         np.testing.assert_array_equal(got[1][i], ok)
 
 
-@pytest.mark.parametrize("margin", [0, 2])
-def test_small_margin_reruns_stay_exact(hiplib, margin):
+@pytest.mark.parametrize("k", [10, 16, 40])
+def test_failed_certificates_rerun_exactly(hiplib, k):
+    """An impossible error budget fails every certificate: every query goes through the
+    exact re-run (gather, exact scan, scatter) and the results must not change."""
     from pyrope_amd import IvfFlatVectorIndex, SearchOptions, generate_synthetic
     x = generate_synthetic(12000, 64, 3)
     idx = IvfFlatVectorIndex(64, 0, n_list=32)
@@ -125,11 +127,14 @@ def test_small_margin_reruns_stay_exact(hiplib, margin):
     idx.build()
     q = generate_synthetic(200, 64, 4)
     opts = SearchOptions(nprobe=6)
-    with _env(PYR_FILTER_MARGIN=margin):
-        got = idx.search_batch(q, 10, opts)
+    with _env(PYR_FILTER_CERR=1e15):
+        got, nfb = _fallbacks(hiplib, lambda: idx.search_batch(q, k, opts))
+    assert nfb == len(q)
     with _env(PYR_FILTER=0):
-        ref = idx.search_batch(q, 10, opts)
+        ref = idx.search_batch(q, k, opts)
     _same(got, ref)
+    got2 = idx.search_batch(q, k, opts)  # default budget
+    _same(got2, ref)
 
 
 def test_flat_filter_respects_max_scans_and_deletes(hiplib, oracle):
