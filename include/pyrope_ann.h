@@ -117,6 +117,12 @@ pyr_status pyr_index_stats(const pyr_index *index, int64_t *count, int32_t *dim,
  * out may be NULL to query *nlist; *nlist = 0 when not built. */
 pyr_status pyr_index_get_centroids(const pyr_index *index, float *out, int32_t *nlist);
 
+/* BruteForceVectorIndex.Scan (BruteForceVectorIndex.cs:250-273; the source of DeltaVectorIndex.Build's
+ * head -> tail compaction, DeltaVectorIndex.cs:124-158): the live rows in slot order.
+ * labels: *n entries, x: *n x dim row-major; either may be NULL (call with both NULL to size).
+ * FLAT only (PYR_E_STATE otherwise).  Takes the index exclusively (it uses the write stream). */
+pyr_status pyr_index_scan(pyr_index *index, int64_t *labels, float *x, int64_t *n);
+
 /* Introspection of the built IVF layout (list-major storage order, used by the
  * parity tests and the CPU baseline).  list_off: nlist+1 (row offsets without padding),
  * labels: total rows (state of removed rows: label -1), live: 1 visible, 0 removed/shadowed.
@@ -138,7 +144,9 @@ pyr_status pyr_generate_synthetic(int64_t count, int32_t dim, int32_t seed, floa
 
 /* Kernel-phase profiler (HIP events on the search stream; adds a host sync per search while on).
  * phase: 0 coarse scan+select, 1 IVF work lists, 2 IVF list scan, 3 buffer scan, 4 final merge,
- * 5 FLAT scan, 6 IVF-PQ LUT+ADC scan.  *work = (query, row) pairs the phase scored. */
+ * 5 FLAT scan, 6 IVF-PQ LUT+ADC scan, 7 MFMA-filter refine (exact re-score + certificate),
+ * 8 exact re-run of queries whose certificate failed.  *work = (query, row) pairs the phase
+ * scored (phase 8: queries re-run). */
 void pyr_profile_enable(int32_t on);
 void pyr_profile_reset(void);
 pyr_status pyr_profile_get(int32_t phase, double *total_ms, int64_t *calls, int64_t *work);

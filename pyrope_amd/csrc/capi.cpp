@@ -258,6 +258,15 @@ pyr_status pyr_index_pq_state(const pyr_index *index, float *codebooks, int32_t 
   });
 }
 
+pyr_status pyr_index_scan(pyr_index *index, int64_t *labels, float *x, int64_t *n) {
+  if (!index || !n) return fail(PYR_E_ARG, "null argument");
+  return guard([&] {
+    HIPCHK(hipSetDevice(index->impl->device));
+    std::unique_lock<std::shared_mutex> g(index->impl->mu);
+    index->impl->scan(labels, x, n);
+  });
+}
+
 pyr_status pyr_merge_topk_device(const float *d_scores, const int64_t *d_labels, int64_t nq, int32_t nparts,
                                  int32_t k, float *d_out_scores, int64_t *d_out_labels, void *stream) {
   if (nq < 0 || nparts <= 0 || nparts > pyr::MAX_PARTS || k <= 0 || k > pyr::KMAX)

@@ -245,7 +245,7 @@ static uint32_t *shared_bounds(Workspace &ws, int64_t nq) {
 // ---------------------------------------------------------------------------
 // MFMA candidate filter + exact refine (filter.hip).  Same results as the exact scans
 // (certified per query, failures re-run exactly); PYR_FILTER=0 forces the exact scans,
-// PYR_FILTER_MARGIN sets K1 - k (default 8).
+// PYR_FILTER_MARGIN sets the minimum K1 - k (default 4, see filter_k1).
 // ---------------------------------------------------------------------------
 static bool filter_enabled() {
   const char *e = getenv("PYR_FILTER");
@@ -561,6 +561,24 @@ struct FlatIndex : Index {
     PhaseTimer t(PH_MERGE, ws.st);
     launch_merge_keys(ws.part_s.as<float>(), ws.part_k.as<uint32_t>(), nq, p.nchunks, k, st.labels.as<int64_t>(),
                       nullptr, d_s, d_l, nullptr, d_c, ws.st);
+  }
+
+  void scan(int64_t *labels, float *x, int64_t *n) override {  // :250-273
+    std::vector<int64_t> slots;
+    slots.reserve(slot_of.size());
+    for (int64_t i = 0; i < st.n; i++)
+      if (st.hlive[i]) slots.push_back(i);
+    *n = (int64_t)slots.size();
+    if (labels)
+      for (size_t j = 0; j < slots.size(); j++) labels[j] = st.hlabels[slots[j]];
+    if (!x || slots.empty()) return;
+    const int64_t cnt = (int64_t)slots.size();
+    stage_i.ensure(sizeof(int64_t) * cnt);
+    stage_x.ensure(sizeof(float) * cnt * dim);
+    HIPCHK(hipMemcpyAsync(stage_i.p, slots.data(), sizeof(int64_t) * cnt, hipMemcpyHostToDevice, wst));
+    launch_gather_blocked(st.rows.as<float>(), stage_i.as<int64_t>(), cnt, dim, stage_x.as<float>(), wst);
+    HIPCHK(hipMemcpyAsync(x, stage_x.p, sizeof(float) * cnt * dim, hipMemcpyDeviceToHost, wst));
+    HIPCHK(hipStreamSynchronize(wst));
   }
 
   int64_t count() const override { return (int64_t)slot_of.size(); }  // :115-126

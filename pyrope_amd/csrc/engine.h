@@ -118,6 +118,13 @@ struct Index {
   }
   virtual void ivf_layout(int64_t *off, int64_t *labels, uint8_t *live, int64_t *total) const;
   virtual void pq_state(float *cb, int32_t *ksub, uint8_t *codes) const;
+  // BruteForceVectorIndex.Scan (:250-273): live rows in slot order; labels/x may be null
+  virtual void scan(int64_t *labels, float *x, int64_t *n) {
+    (void)labels;
+    (void)x;
+    (void)n;
+    throw Error(PYR_E_STATE, "index kind has no Scan (BruteForceVectorIndex only)");
+  }
   virtual void set_centroids(const float *c, int nlist) {
     (void)c;
     (void)nlist;

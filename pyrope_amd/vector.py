@@ -13,6 +13,8 @@ from __future__ import annotations
 
 import ctypes as C
 import enum
+import re
+import threading
 from abc import ABC, abstractmethod
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence
@@ -20,7 +22,7 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import (ArgumentException, ArgumentNullException, ArgumentOutOfRangeException,
+from ._lib import (ArgumentException, ArgumentNullException, ArgumentOutOfRangeException, FormatException,
                    InvalidOperationException, check, ptr)
 
 
@@ -257,8 +259,19 @@ class BruteForceVectorIndex(HipVectorIndex):
             raise ArgumentOutOfRangeException("topK must be positive.")
         return super().search(query, top_k, options)
 
-    def scan(self):  # :250-273 (compaction source)
-        raise NotImplementedError("device-side compaction is SURVEY.md 8(f)-2")
+    def scan(self):  # :250-273 (compaction source): live rows in slot order
+        """[(id, vector)] of the live rows in slot order (pyr_index_scan)."""
+        n = C.c_int64()
+        check(self._L.pyr_index_scan(self._h, None, None, C.byref(n)))
+        labels = np.zeros(n.value, np.int64)
+        x = np.zeros((n.value, self.dimension), np.float32)
+        check(self._L.pyr_index_scan(self._h, ptr(labels, C.c_int64), ptr(x, C.c_float), C.byref(n)))
+        return [(self._id_of[int(lab)], x[i]) for i, lab in enumerate(labels.tolist())]
+
+    def delete_many(self, ids: Sequence[str]) -> None:
+        labels = np.array([self._label_of[i] for i in ids if i in self._label_of], np.int64)
+        if len(labels):
+            check(self._L.pyr_index_remove(self._h, ptr(labels, C.c_int64), len(labels), None))
 
 
 class IvfFlatVectorIndex(HipVectorIndex, ICentroidsProvider):
@@ -324,21 +337,26 @@ class DeltaVectorIndex(IVectorIndex, ICentroidsProvider):
             raise ArgumentException("Head and Tail metrics must match")
         self.head, self.tail = head, tail
         self.dimension, self.metric = head.dimension, head.metric
+        self._lock = threading.RLock()  # the reference's ReaderWriterLockSlim (:11); writes and builds exclusive
 
     def add(self, id, vector):  # :29-43 writes go to the head
-        self.head.add(id, vector)
+        with self._lock:
+            self.head.add(id, vector)
 
     def upsert(self, id, vector):
-        self.head.upsert(id, vector)
+        with self._lock:
+            self.head.upsert(id, vector)
 
     def delete(self, id) -> bool:  # :58-74
-        h = self.head.delete(id)
-        t = self.tail.delete(id)
-        return h or t
+        with self._lock:
+            h = self.head.delete(id)
+            t = self.tail.delete(id)
+            return h or t
 
     def search(self, query, top_k, options=None):  # :76-122
-        head_res = self.head.search(query, top_k, options)
-        tail_res = self.tail.search(query, top_k, options)
+        with self._lock:
+            head_res = self.head.search(query, top_k, options)
+            tail_res = self.tail.search(query, top_k, options)
         merged: Dict[str, SearchResult] = {}
         for r in tail_res:
             merged[r.id] = r
@@ -348,13 +366,20 @@ class DeltaVectorIndex(IVectorIndex, ICentroidsProvider):
         return out[:top_k]
 
     def build(self):  # :124-158 compaction head -> tail
-        items = self.head.scan_items() if hasattr(self.head, "scan_items") else None
-        if items is not None:
-            for id, vec in items:
-                self.tail.add(id, vec)
-                self.head.delete(id)
-        self.head.build()
-        self.tail.build()
+        with self._lock:
+            items = self.head.scan() if isinstance(self.head, BruteForceVectorIndex) else None
+            if items:
+                if isinstance(self.tail, (IvfFlatVectorIndex, IvfPqVectorIndex)):
+                    # IVF Add == buffer upsert and cannot fail per item: one batched call, then one
+                    # batched tombstone pass over the head (same end state as the per-item loop)
+                    self.tail.add_batch([i for i, _ in items], np.stack([v for _, v in items]))
+                    self.head.delete_many([i for i, _ in items])
+                else:
+                    for id, vec in items:  # a BruteForce tail throws on a duplicate mid-loop, like the reference
+                        self.tail.add(id, vec)
+                        self.head.delete(id)
+            self.head.build()
+            self.tail.build()
 
     def get_stats(self) -> IndexStats:  # :209-221
         h, t = self.head.get_stats(), self.tail.get_stats()
@@ -369,16 +394,25 @@ class VectorIndexRegistry:
 
     def __init__(self, device: int = 0):
         self._indices: Dict[str, DeltaVectorIndex] = {}
+        self._epochs: Dict[str, int] = {}
         self.device = device
 
     @staticmethod
-    def _int_param(params: Optional[dict], key: str, default: int) -> int:  # :115-126
+    def _int_param(params: Optional[dict], key: str, default: int) -> int:  # GetIntParam :115-126
+        """Parameters come from JSON (JsonElement): a number -> GetInt32 (FormatException unless an
+        integral int32); a string -> int.TryParse (optional sign, surrounding whitespace); anything else -> default."""
         if params and key in params:
             v = params[key]
-            if isinstance(v, bool):
+            if isinstance(v, bool):  # JsonValueKind.True/False is not Number
                 return default
-            if isinstance(v, int):
-                return v
+            if isinstance(v, (int, float)):  # a JSON number: JsonElement.GetInt32 throws unless integral int32
+                if isinstance(v, float) and not v.is_integer() or not -2**31 <= v < 2**31:
+                    raise FormatException(f"The JSON value could not be converted to System.Int32: {v}")
+                return int(v)
+            if isinstance(v, str):
+                m = re.fullmatch(r"\s*([+-]?[0-9]+)\s*", v)
+                if m and -2**31 <= int(m.group(1)) < 2**31:
+                    return int(m.group(1))
         return default
 
     def create(self, dimension: int, metric: VectorMetric, algorithm: Optional[str] = None,
@@ -414,6 +448,20 @@ class VectorIndexRegistry:
 
     def try_get_index(self, tenant: str, index: str) -> Optional[DeltaVectorIndex]:
         return self._indices.get(f"{tenant}:{index}")
+
+    def increment_epoch(self, tenant: str, index: str) -> int:  # :52-59
+        key = f"{tenant}:{index}"
+        if key not in self._indices:
+            return 0
+        self._epochs[key] = self._epochs.get(key, 0) + 1
+        return self._epochs[key]
+
+    def get_epoch(self, tenant: str, index: str) -> int:  # :61-68
+        return self._epochs.get(f"{tenant}:{index}", 0)
+
+    def clear(self) -> None:  # :70-73
+        self._indices.clear()
+        self._epochs.clear()
 
 
 def kmeans_train(data: np.ndarray, k: int, metric: VectorMetric, max_iter: int = 10, seed: int = 42,

@@ -1,0 +1,138 @@
+"""Multi-GPU sharding (pyrope_amd/dist.py; SURVEY.md 8(e) option ii, rows within lists).
+
+Rank r holds base row i iff i % world == r and builds its lists with the shared coarse quantizer,
+so the union of the ranks' probed rows is exactly the unsharded index's probed rows, each scored
+with the same arithmetic.  One all_gather of the per-rank top-k partials + a merge by
+(score desc, label asc) must then give the unsharded result (ties between equal scores in
+different lists aside, which random fp32 data does not produce).
+
+CPU tests run the orchestration with gloo at world size 2 (the per-rank scan is the oracle, as
+the GPU scan is bit-identical to it); the GPU test shards one index two ways on one device and
+merges with pyr_merge_topk_device.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+D, N, NLIST, NPROBE, K, NQ = 32, 3000, 16, 4, 10, 24
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _host_merge(s_parts, l_parts, k):
+    """Reference merge for the CPU test: (score desc, label asc), empties (-1) last."""
+    Q = s_parts.shape[0]
+    out_s = np.full((Q, k), -np.inf, np.float32)
+    out_l = np.full((Q, k), -1, np.int64)
+    for q in range(Q):
+        cand = [(float(s), int(l)) for s, l in zip(s_parts[q].reshape(-1), l_parts[q].reshape(-1)) if l >= 0]
+        cand.sort(key=lambda t: (-t[0], t[1]))
+        for j, (s, l) in enumerate(cand[:k]):
+            out_s[q, j], out_l[q, j] = s, l
+    return out_s, out_l
+
+
+def _shard_search(oracle, data, cents, queries, rank, world):
+    """One rank's IVF search over its rows-within-list shard; returns global labels."""
+    from pyrope_amd.dist import shard_labels
+    labels = shard_labels(len(data), world, rank)
+    rows = data[labels]
+    assign = np.array([oracle.find_nearest_centroid(r, cents, oracle.L2) for r in rows], np.int32)
+    lrows, order, off = oracle.lists_from_assign(rows, assign, len(cents))
+    s, kk, _ = oracle.ivf_search_batch(queries, K, cents, lrows, off, metric=oracle.L2, nprobe=NPROBE)
+    lab = np.where(kk >= 0, labels[order[np.maximum(kk, 0)]], -1)
+    return s, lab
+
+
+def _worker(rank, world, port, data, cents, queries, out):
+    import torch
+    import torch.distributed as dist
+
+    import oracle
+    from pyrope_amd.dist import sharded_search
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        def local(q, k):
+            s, lab = _shard_search(oracle, data, cents, q.numpy(), rank, world)
+            return torch.from_numpy(s), torch.from_numpy(lab)
+
+        def merge(sp, lp, k):
+            return tuple(torch.from_numpy(a) for a in _host_merge(sp.numpy(), lp.numpy(), k))
+
+        s, lab = sharded_search(local, merge, torch.from_numpy(queries), K, world)
+        np.save(os.path.join(out, f"s{rank}.npy"), s.numpy())
+        np.save(os.path.join(out, f"l{rank}.npy"), lab.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_labels_partition():
+    from pyrope_amd.dist import shard_labels
+    parts = [shard_labels(103, 4, r) for r in range(4)]
+    allp = np.sort(np.concatenate(parts))
+    np.testing.assert_array_equal(allp, np.arange(103))
+    for r, p in enumerate(parts):
+        assert np.all(p % 4 == r) and np.all(np.diff(p) > 0)
+
+
+def test_gloo_world2_sharded_equals_unsharded(oracle, tmp_path):
+    import torch.multiprocessing as mp
+
+    data = oracle.generate_vectors(N, D, 42)
+    queries = oracle.generate_vectors(NQ, D, 1337)
+    cents = oracle.kmeans_train(data, NLIST, oracle.L2, 5, 42)
+    # unsharded reference: the whole data set in one index with the same quantizer
+    ref_s, ref_l = _shard_search(oracle, data, cents, queries, 0, 1)
+    port = _free_port()
+    mp.start_processes(_worker, args=(2, port, data, cents, queries, str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    for r in range(2):
+        s = np.load(tmp_path / f"s{r}.npy")
+        lab = np.load(tmp_path / f"l{r}.npy")
+        np.testing.assert_array_equal(lab, ref_l)
+        assert np.array_equal(s.view(np.uint32), ref_s.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_gpu_two_shards_merge_equals_unsharded(hiplib):
+    import torch
+
+    from pyrope_amd import IvfFlatVectorIndex, SearchOptions, generate_synthetic, kmeans_train
+    from pyrope_amd.dist import merge_device, shard_labels
+
+    n, d, nl = 20000, 128, 64
+    data = generate_synthetic(n, d, 42)
+    q = generate_synthetic(300, d, 1337)
+    cents = kmeans_train(data, nl, 0, 10, 42)
+    opts = SearchOptions(nprobe=8)
+    full = IvfFlatVectorIndex(d, 0, n_list=nl)
+    full.set_centroids(cents)
+    full.add_labels(np.arange(n, dtype=np.int64), data)
+    full.build()
+    ref_s, ref_l, _ = full.search_batch(q, K, opts)
+    sp, lp = [], []
+    for r in range(2):
+        idx = IvfFlatVectorIndex(d, 0, n_list=nl)
+        idx.set_centroids(cents)
+        lab = shard_labels(n, 2, r)
+        idx.add_labels(lab, data[lab])
+        idx.build()
+        s, l, _ = idx.search_batch(q, K, opts)
+        sp.append(s)
+        lp.append(l)
+    s_parts = torch.from_numpy(np.stack(sp, 1)).cuda()
+    l_parts = torch.from_numpy(np.stack(lp, 1)).cuda()
+    s_out, l_out = merge_device(s_parts, l_parts, K)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(l_out.cpu().numpy(), ref_l)
+    assert np.array_equal(s_out.cpu().numpy().view(np.uint32), ref_s.view(np.uint32))

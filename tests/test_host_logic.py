@@ -1,0 +1,30 @@
+"""Host-side logic of the plugin mirror that needs no device (pyrope_amd/vector.py)."""
+import pytest
+
+
+def test_get_int_param_semantics():  # VectorIndexRegistry.cs:115-126 GetIntParam
+    from pyrope_amd import VectorIndexRegistry
+    from pyrope_amd._lib import FormatException
+    f = VectorIndexRegistry._int_param
+    assert f(None, "nlist", 100) == 100
+    assert f({}, "nlist", 100) == 100
+    assert f({"nlist": 500}, "nlist", 100) == 500
+    assert f({"nlist": "250"}, "nlist", 100) == 250        # int.TryParse on strings
+    assert f({"nlist": " -7 "}, "nlist", 100) == -7
+    assert f({"nlist": "+12"}, "nlist", 100) == 12
+    assert f({"nlist": "1_000"}, "nlist", 100) == 100      # TryParse rejects separators
+    assert f({"nlist": "abc"}, "nlist", 100) == 100
+    assert f({"nlist": "99999999999"}, "nlist", 100) == 100  # Int32 overflow -> TryParse false
+    assert f({"nlist": True}, "nlist", 100) == 100         # JSON true is not a Number
+    assert f({"nlist": 64.0}, "nlist", 100) == 64
+    assert f({"nlist": None}, "nlist", 100) == 100
+    with pytest.raises(FormatException):
+        f({"nlist": 3.5}, "nlist", 100)                    # GetInt32 on a non-integral number
+    with pytest.raises(FormatException):
+        f({"nlist": 2**40}, "nlist", 100)
+
+
+def test_search_options_defaults():  # SearchOptions.cs:3
+    from pyrope_amd import SearchOptions
+    o = SearchOptions()
+    assert o.max_scans is None and o.nprobe is None and o.ef_search is None
