@@ -242,6 +242,13 @@ static uint32_t *shared_bounds(Workspace &ws, int64_t nq) {
   return ws.gthr.as<uint32_t>();
 }
 
+// IVF-PQ list scan kernel: pq_adc (default) or the first-cut pq_scan (PYR_PQ_ADC=0; A/B only,
+// same results)
+static bool pq_adc_enabled() {
+  const char *e = getenv("PYR_PQ_ADC");
+  return !(e && atoi(e) == 0);
+}
+
 // ---------------------------------------------------------------------------
 // MFMA candidate filter + exact refine (filter.hip).  Same results as the exact scans
 // (certified per query, failures re-run exactly); PYR_FILTER=0 forces the exact scans,
@@ -1378,9 +1385,13 @@ struct IvfPqIndex : Index {
       a.ksub = ksub;
       a.part_s = ws.part_s.as<float>();
       a.part_k = ws.part_k.as<uint32_t>();
-      if (pq_scan_lds_bytes(dim, M, ksub, k) > 160 * 1024) throw Error(PYR_E_ARG, "PQ lookup table exceeds LDS");
+      const bool adc = pq_adc_enabled() && pq_adc_supported(dim, M, ksub, k);
+      a.gthr = adc && bounds_enabled() ? shared_bounds(ws, nq) : nullptr;
+      if (!adc && pq_scan_lds_bytes(dim, M, ksub, k) > 160 * 1024)
+        throw Error(PYR_E_ARG, "PQ lookup table exceeds LDS");
       PhaseTimer t(PH_PQ_SCAN, ws.st, prof().on ? probed_rows(ws, nq, probes, le, lb) : 0);
-      launch_pq_scan(a, maxi, ws.st);
+      if (adc) launch_pq_adc(a, maxi, ws.st);
+      else launch_pq_scan(a, maxi, ws.st);
     }
     if (bp.nchunks > 0) {  // :130-136 exact buffer scan
       PhaseTimer t(PH_BUF_SCAN, ws.st, nq * bcut);

@@ -161,8 +161,12 @@ struct PqArgs {
   int32_t nparts, nprobe, k, dim, M, ksub;
   float *part_s;
   uint32_t *part_k;
+  uint32_t *gthr;          // shared per-query bounds (ScanArgs::gthr) or null; pq_adc only
 };
 void launch_pq_scan(const PqArgs &a, int max_items, hipStream_t st);
+// LDS-rate ADC scan (512-thread blocks, wave-distributed top-k); k <= 64, M <= 128
+bool pq_adc_supported(int dim, int M, int ksub, int k);
+void launch_pq_adc(const PqArgs &a, int max_items, hipStream_t st);
 size_t pq_scan_lds_bytes(int dim, int M, int ksub, int k);
 // PQ encode (ProductQuantizer.Encode on residuals x - c[assign]) -> codes n x M row-major.
 void launch_pq_encode(const float *x, const int32_t *assign, const float *cents, int64_t n, int32_t dim, int32_t M,

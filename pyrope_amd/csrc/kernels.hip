@@ -962,6 +962,143 @@ __global__ __launch_bounds__(256) void pq_scan_kernel(PqArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// pq_adc: the IVF-PQ list scan at LDS rate.  One 512-thread block (8 waves) per work item
+// (list, <= qchunk queries); per query of the item:
+//   1. residual q - c_list and its LUT (ProductQuantizer.cs:107-117, M x ksub fp32) in LDS,
+//      built by all 512 threads;
+//   2. every wave streams 64-row code blocks (one row per lane, codes double-buffered in
+//      registers) and sums LUT entries in m order (IvfPqVectorIndex.cs:182-186) -- the LDS
+//      gathers are the bound (ds_read_b32, random banks);
+//   3. each wave keeps its top-k spread over lanes 0..k-1 (lane j = j-th best): candidates
+//      beating the wave's k-th (and the query's shared bound) are found with one ballot and
+//      inserted with a shuffle, so the common no-candidate case costs two compares;
+//   4. the 8 wave lists are merged by wave 0 into the item's partial top-k and the k-th
+//      best is published to the shared per-query bound.
+// Scores, tie rule and partial slots are those of pq_scan_kernel (bit-identical results).
+// Blocks are mapped XCD-major (block b runs on XCD b % 8): each XCD walks its own
+// contiguous range of the list-major items, so the items of one list run side by side on
+// one XCD and share its L2 copy of the list's codes.
+// ---------------------------------------------------------------------------
+constexpr int PQ_THREADS = 512;
+constexpr int PQ_WAVES = PQ_THREADS / 64;
+
+// wave-wide insertion of the candidates flagged in `cand` into the lane-distributed list
+__device__ __forceinline__ void wave_list_insert(bool cand, float sc, uint32_t key, float &ls, uint32_t &lk, float &kth,
+                                                 uint32_t &kthk, int k, int lane) {
+  uint64_t m = __ballot(cand);
+  while (m) {
+    const int j = __ffsll((unsigned long long)m) - 1;
+    const float s = __shfl(sc, j);
+    const uint32_t kk = __shfl(key, j);
+    const int pos = __popcll(__ballot(lane < k && better(ls, lk, s, kk)));
+    const float us = __shfl_up(ls, 1);
+    const uint32_t uk = __shfl_up(lk, 1);
+    if (lane > pos && lane < k) {
+      ls = us;
+      lk = uk;
+    }
+    if (lane == pos) {
+      ls = s;
+      lk = kk;
+    }
+    kth = __shfl(ls, k - 1);
+    kthk = __shfl(lk, k - 1);
+    m &= m - 1;
+    m &= __ballot(cand && better(sc, key, kth, kthk));
+  }
+}
+
+template <int NCH, bool K256>
+__global__ __launch_bounds__(PQ_THREADS) void pq_adc_kernel(PqArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int nit = *a.n_items;
+  const int per = (nit + 7) >> 3;  // items per XCD (the grid has >= 8 * per blocks)
+  if ((int)(blockIdx.x >> 3) >= per) return;
+  const int item = ((int)blockIdx.x & 7) * per + ((int)blockIdx.x >> 3);
+  if (item >= nit) return;
+  const ScanItem it = a.items[item];
+  const int D = a.dim, M = a.M, ksub = K256 ? 256 : a.ksub, k = a.k, sub = D / M;
+  float *lut = smem;                                           // [M][ksub]
+  float *res = lut + M * ksub;                                 // [D]
+  float *mrs = res + ((D + 3) & ~3);                           // [PQ_WAVES][k] wave lists
+  uint32_t *mrk = reinterpret_cast<uint32_t *>(mrs + PQ_WAVES * k);
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const float *cent = a.cents + (size_t)it.list * D;
+  const int rb = it.row_begin, re = it.row_end;  // rb: multiple of 64 (64-row code blocks)
+  const int ngrp = (re - rb + 63) >> 6;
+  const uint4 *codes = reinterpret_cast<const uint4 *>(a.codes);
+
+  for (int i = 0; i < it.qcnt; ++i) {
+    const int slot = a.qlist[it.qbeg + i] + it.part;
+    const int qi = slot / a.nparts;
+    const float *qp = a.queries + (size_t)qi * D;
+    for (int d = tid; d < D; d += PQ_THREADS) res[d] = qp[d] - cent[d];  // IvfPqVectorIndex.cs:161-163
+    __syncthreads();
+    for (int e = tid; e < M * ksub; e += PQ_THREADS) {  // ProductQuantizer.cs:112-117
+      const int m = e / ksub, j = e - m * ksub;
+      lut[e] = em_l2sq_unsafe(Off{res + m * sub}, Off{a.codebooks + ((size_t)m * ksub + j) * sub}, sub);
+    }
+    __syncthreads();
+
+    float ls = -INFINITY, kth = -INFINITY;  // lane j < k holds the wave's j-th best
+    uint32_t lk = KEY_NONE, kthk = KEY_NONE;
+    float gs = a.gthr ? key_score(__hip_atomic_load(a.gthr + qi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                      : -INFINITY;
+    uint4 cur[NCH], nxt[NCH];
+    auto load = [&](uint4 (&dst)[NCH], int g) {
+      const size_t base = ((size_t)((rb >> 6) + g) * NCH) * 64 + lane;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) dst[c] = codes[base + (size_t)c * 64];
+    };
+    if (w < ngrp) load(cur, w);
+    for (int g = w, it2 = 0; g < ngrp; g += PQ_WAVES, ++it2) {
+      if (g + PQ_WAVES < ngrp) load(nxt, g + PQ_WAVES);
+      const int r = rb + g * 64 + lane;
+      const bool valid = r < re && a.live[r];
+      float dist = 0.0f;  // IvfPqVectorIndex.cs:182-186, m order
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const uint32_t ws[4] = {cur[c].x, cur[c].y, cur[c].z, cur[c].w};
+#pragma unroll
+        for (int b = 0; b < 16; ++b) {
+          const int m = c * 16 + b;
+          if (c < NCH - 1 || m < M) dist = dist + lut[m * ksub + ((ws[b >> 2] >> (8 * (b & 3))) & 0xFF)];
+        }
+      }
+      const float score = -dist;  // :194
+      const uint32_t key = (uint32_t)r;
+      if (a.gthr && (it2 & 3) == 3)
+        gs = fmaxf(gs, key_score(__hip_atomic_load(a.gthr + qi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+      const bool cand = valid && score >= gs && better(score, key, kth, kthk);
+      wave_list_insert(cand, score, key, ls, lk, kth, kthk, k, lane);
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) cur[c] = nxt[c];
+    }
+    if (lane < k) {
+      mrs[w * k + lane] = ls;
+      mrk[w * k + lane] = lk;
+    }
+    __syncthreads();
+    if (w == 0) {
+      for (int e0 = k; e0 < PQ_WAVES * k; e0 += 64) {
+        const int e = e0 + lane;
+        const float s = e < PQ_WAVES * k ? mrs[e] : -INFINITY;
+        const uint32_t kk = e < PQ_WAVES * k ? mrk[e] : KEY_NONE;
+        const bool cand = kk != KEY_NONE && better(s, kk, kth, kthk);
+        wave_list_insert(cand, s, kk, ls, lk, kth, kthk, k, lane);
+      }
+      if (lane < k) {
+        a.part_s[(size_t)slot * k + lane] = ls;
+        a.part_k[(size_t)slot * k + lane] = lk;
+      }
+      if (lane == 0 && a.gthr && kthk != KEY_NONE) atomicMax(a.gthr + qi, score_key(kth));
+    }
+    // the next query rewrites res / lut only after the barrier that follows its res stores;
+    // wave 0 reads mrs / mrk before it reaches that barrier
+  }
+}
+
 __global__ void pq_encode_kernel(const float *x, const int32_t *assign, const float *cents, int64_t n, int D, int M,
                                  int ksub, const float *cb, uint8_t *codes) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1298,6 +1435,49 @@ void launch_ivf_limits(const int32_t *probes, int64_t nq, int32_t nprobe, int32_
 
 size_t pq_scan_lds_bytes(int dim, int M, int ksub, int k) {
   return (size_t)(((dim + 3) & ~3) + M * ksub + 2 * k + 2 * 256 + 4) * 4;
+}
+
+size_t pq_adc_lds_bytes(int dim, int M, int ksub, int k) {
+  return (size_t)(M * ksub + ((dim + 3) & ~3) + 2 * PQ_WAVES * k) * 4;
+}
+bool pq_adc_supported(int dim, int M, int ksub, int k) {
+  return k >= 1 && k <= 64 && (M + 15) / 16 <= 8 && pq_adc_lds_bytes(dim, M, ksub, k) <= 160 * 1024;
+}
+
+template <int NCH, bool K256>
+static void launch_pq_adc_t(const PqArgs &a, int max_items, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&pq_adc_kernel<NCH, K256>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  const int grid = (max_items + 7) / 8 * 8;  // XCD-major item mapping needs a multiple of 8 blocks
+  hipLaunchKernelGGL((pq_adc_kernel<NCH, K256>), dim3(grid), dim3(PQ_THREADS), pq_adc_lds_bytes(a.dim, a.M, a.ksub, a.k),
+                     st, a);
+}
+
+void launch_pq_adc(const PqArgs &a, int max_items, hipStream_t st) {
+  if (max_items <= 0) return;
+  const int nch = (a.M + 15) / 16;
+  const bool k256 = a.ksub == 256;
+#define PQ_CASE(N)                                               \
+  case N:                                                        \
+    if (k256) launch_pq_adc_t<N, true>(a, max_items, st);       \
+    else launch_pq_adc_t<N, false>(a, max_items, st);           \
+    break;
+  switch (nch) {
+    PQ_CASE(1)
+    PQ_CASE(2)
+    PQ_CASE(3)
+    PQ_CASE(4)
+    PQ_CASE(5)
+    PQ_CASE(6)
+    PQ_CASE(7)
+    PQ_CASE(8)
+    default: break;
+  }
+#undef PQ_CASE
 }
 
 void launch_pq_scan(const PqArgs &a, int max_items, hipStream_t st) {

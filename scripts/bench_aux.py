@@ -1,0 +1,142 @@
+#!/usr/bin/env python3
+"""Secondary measurements for DESIGN.md (not the driver's bench line; bench.py is that).
+
+    python scripts/bench_aux.py flat  [--n 1000000 --nq 10000 --metric 0|1]
+    python scripts/bench_aux.py ivfpq [--n 3200000 --dim 768 --nlist 256 --m 96 --nprobe 64 --nq 10000]
+
+flat   BASELINE.json configs[1]: FLAT d=128 N=1M Q=10k (L2 and IP), HBM-resident batch.
+ivfpq  IVF_PQ d=768 m=96 k=256 nprobe=64 with lists of ~12.5k rows -- the per-query work of
+       configs[3] (N=50M, nlist=4096: 64 x 12.2k rows x 96 lookups per query) on a
+       smaller index (N/nlist kept, nlist smaller) so that the box builds it in minutes.
+
+Prints one JSON line per run: QPS, per-phase HIP-event times, the dominant kernel's
+algorithmic rate, and parity of a query sample against the CPU oracle (test infrastructure,
+outside the timed region).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+PH = {0: "coarse", 1: "work_lists", 2: "list_scan", 3: "buffer_scan", 4: "merge", 5: "flat_scan", 6: "pq_scan",
+      7: "refine", 8: "exact_rerun"}
+
+
+def log(*a):
+    print("[aux]", *a, file=sys.stderr, flush=True)
+
+
+def timed(idx, q, Q, k, opts, steps, warmup, L):
+    import torch
+    dev = q.device
+    s = torch.empty((Q, k), dtype=torch.float32, device=dev)
+    lab = torch.empty((Q, k), dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def step():
+        idx.search_device(q.data_ptr(), Q, k, s.data_ptr(), lab.data_ptr(), 0, stream, opts)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    L.pyr_profile_reset()
+    L.pyr_profile_enable(1)
+    step()
+    torch.cuda.synchronize()
+    L.pyr_profile_enable(0)
+    phases = {}
+    for ph, name in PH.items():
+        ms, calls, work = C.c_double(), C.c_int64(), C.c_int64()
+        L.pyr_profile_get(ph, C.byref(ms), C.byref(calls), C.byref(work))
+        if calls.value:
+            phases[name] = {"ms": round(ms.value, 4), "work": work.value}
+    return Q * steps / el, el / steps * 1e3, phases, s.cpu().numpy(), lab.cpu().numpy()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("workload", choices=["flat", "ivfpq"])
+    ap.add_argument("--n", type=int, default=0)
+    ap.add_argument("--dim", type=int, default=0)
+    ap.add_argument("--nq", type=int, default=10000)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--metric", type=int, default=0)
+    ap.add_argument("--nlist", type=int, default=256)
+    ap.add_argument("--m", type=int, default=96)
+    ap.add_argument("--nprobe", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--check", type=int, default=20, help="queries compared with the CPU oracle")
+    a = ap.parse_args()
+
+    import torch
+    from pyrope_amd import (BruteForceVectorIndex, IvfPqVectorIndex, SearchOptions, _lib, generate_synthetic)
+    from pyrope_amd.build import build
+    build()
+    L = _lib.load()
+    torch.cuda.set_device(0)
+    import oracle  # parity check of a sample only
+
+    if a.workload == "flat":
+        n, d = a.n or 1_000_000, a.dim or 128
+        x = generate_synthetic(n, d, 42)
+        qh = generate_synthetic(a.nq, d, 1337)
+        idx = BruteForceVectorIndex(d, a.metric)
+        idx.add_labels(np.arange(n, dtype=np.int64), x)
+        q = torch.from_numpy(qh).cuda()
+        qps, ms, phases, s, lab = timed(idx, q, a.nq, a.k, None, a.steps, a.warmup, L)
+        ok = True
+        for i in np.linspace(0, a.nq - 1, a.check).astype(int):
+            os_, ok_ = oracle.bf_search(x, None, a.metric, qh[i], a.k)
+            ok &= bool(np.array_equal(lab[i], ok_) and np.array_equal(s[i].view(np.uint32), os_.view(np.uint32)))
+        scan = phases.get("flat_scan", {"ms": float("nan"), "work": 0})
+        out = {"workload": f"FLAT d={d} N={n} Q={a.nq} k={a.k} metric={['L2', 'IP', 'COS'][a.metric]}",
+               "qps": qps, "ms_per_step": ms, "phases_ms": {k_: v["ms"] for k_, v in phases.items()},
+               "scan_pairs": scan["work"],
+               "scan_tflops_2d": scan["work"] * 2 * d / (scan["ms"] * 1e-3) / 1e12,
+               "hbm_equiv_GBps": qps * n * d * 4 / 1e9,
+               "parity_sample": {"queries": a.check, "ids_and_bits_equal": ok}}
+    else:
+        n, d = a.n or 3_200_000, a.dim or 768
+        x = generate_synthetic(n, d, 42)
+        qh = generate_synthetic(a.nq, d, 1337)
+        t = time.time()
+        idx = IvfPqVectorIndex(d, a.metric, m=a.m, k=256, n_list=a.nlist)
+        idx.add_labels(np.arange(n, dtype=np.int64), x)
+        idx.build()
+        log(f"built IVF_PQ n={n} d={d} nlist={a.nlist} m={a.m} in {time.time() - t:.1f}s")
+        q = torch.from_numpy(qh).cuda()
+        opts = SearchOptions(nprobe=a.nprobe)
+        qps, ms, phases, s, lab = timed(idx, q, a.nq, a.k, opts, a.steps, a.warmup, L)
+        cb, codes, off, labels, live = idx.pq_state()
+        cents = idx.centroids_array()
+        ok = True
+        for i in np.linspace(0, a.nq - 1, a.check).astype(int):
+            os_, ok_ = oracle.ivfpq_search(qh[i], a.k, cents, codes, off, cb, live, metric=a.metric, nprobe=a.nprobe)
+            ok &= bool(np.array_equal(lab[i], labels[ok_]) and np.array_equal(s[i].view(np.uint32),
+                                                                               os_.view(np.uint32)))
+        scan = phases.get("pq_scan", {"ms": float("nan"), "work": 0})
+        out = {"workload": f"IVF_PQ d={d} N={n} nlist={a.nlist} m={a.m} k=256 nprobe={a.nprobe} Q={a.nq}",
+               "qps": qps, "ms_per_step": ms, "phases_ms": {k_: v["ms"] for k_, v in phases.items()},
+               "scan_rows": scan["work"],
+               "lookups_per_s": scan["work"] * a.m / (scan["ms"] * 1e-3),
+               "parity_sample": {"queries": a.check, "ids_and_bits_equal": ok}}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

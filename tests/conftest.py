@@ -21,7 +21,14 @@ def oracle():
 
 @pytest.fixture(scope="session")
 def hiplib():
-    """The product library; on a GPU box a missing .so or device is a failure, not a skip."""
+    """The product library; on a GPU box a missing .so or device is a failure, not a skip.
+
+    PyTorch-ROCm bundles its own HIP runtime; when the library's (/opt/rocm) runtime opens the
+    device first, torch's later lazy init reports no GPU.  Tests that hand torch tensors to the
+    library therefore need torch's runtime up first (bench.py does the same)."""
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.init()
     from pyrope_amd import _lib
     from pyrope_amd.build import build
     build()

@@ -94,3 +94,76 @@ def test_ivfpq_search_returns_results(hiplib, oracle):
     index.build()
     results = index.search([0.5] * 128, 5)
     assert len(results) == 5
+
+
+class _env:
+    def __init__(self, **kv):
+        self.kv = {k: str(v) for k, v in kv.items()}
+
+    def __enter__(self):
+        import os
+        self.old = {k: os.environ.get(k) for k in self.kv}
+        os.environ.update(self.kv)
+
+    def __exit__(self, *a):
+        import os
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _same(a, b):
+    np.testing.assert_array_equal(a[2], b[2])
+    np.testing.assert_array_equal(a[1], b[1])
+    assert np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32))
+
+
+@pytest.mark.parametrize("dim,m,ksub,k", [(64, 8, 256, 10), (96, 24, 256, 1), (128, 32, 64, 33),
+                                          (48, 48, 16, 64), (64, 16, 256, 65), (768, 96, 256, 10)])
+def test_pq_adc_equals_first_kernel_and_oracle(hiplib, oracle, dim, m, ksub, k):
+    """pq_adc (default) vs the first-cut pq_scan (PYR_PQ_ADC=0) vs the oracle: M not a multiple
+    of 16, ksub < 256, k = 1 / 64 / 65 (65 takes the first-cut kernel)."""
+    from pyrope_amd import SearchOptions, generate_synthetic
+    n = 6000 if dim < 768 else 3000
+    idx, x = _build(dim, 0, n, 12, m, k=ksub)
+    q = generate_synthetic(70, dim, 99)
+    opts = SearchOptions(nprobe=5)
+    got = idx.search_batch(q, k, opts)
+    with _env(PYR_PQ_ADC=0):
+        ref = idx.search_batch(q, k, opts)
+    _same(got, ref)
+    with _env(PYR_GTHR=0):
+        _same(idx.search_batch(q, k, opts), ref)
+    cb, codes, off, labels, live = idx.pq_state()
+    cents = idx.centroids_array()
+    for i in range(0, len(q), 23):
+        os_, ok = oracle.ivfpq_search(q[i], k, cents, codes, off, cb, live, metric=0, nprobe=5)
+        np.testing.assert_array_equal(got[1][i][: len(ok)], labels[ok])
+        assert np.array_equal(got[0][i][: len(ok)].view(np.uint32), os_.view(np.uint32))
+
+
+def test_pq_adc_ties_and_deletes(hiplib, oracle):
+    """Duplicated rows give exact score ties (lowest storage position first); Delete after Build
+    leaves listed rows in place (IvfPqVectorIndex.cs:51 touches only the buffer); listed rows
+    whose id is re-added to the buffer are skipped (:134, :170)."""
+    from pyrope_amd import IvfPqVectorIndex, SearchOptions, generate_synthetic
+    base = generate_synthetic(300, 32, 5)
+    x = np.repeat(base, 12, axis=0)
+    idx = IvfPqVectorIndex(32, 0, m=4, k=32, n_list=6)
+    idx.add_labels(np.arange(len(x), dtype=np.int64), x)
+    idx.build()
+    q = generate_synthetic(40, 32, 6)
+    opts = SearchOptions(nprobe=3)
+    before = idx.search_batch(q, 20, opts)
+    for i in range(0, len(x), 5):
+        idx.delete(str(i))
+    _same(idx.search_batch(q, 20, opts), before)
+    shadow = np.arange(0, len(x), 5)
+    idx.add_labels(shadow, x[shadow] + 100.0)  # far away: the shadowed ids drop out of the top-20
+    got = idx.search_batch(q, 20, opts)
+    with _env(PYR_PQ_ADC=0):
+        ref = idx.search_batch(q, 20, opts)
+    _same(got, ref)
+    assert not np.any(np.isin(got[1], shadow))
