@@ -242,11 +242,11 @@ static uint32_t *shared_bounds(Workspace &ws, int64_t nq) {
   return ws.gthr.as<uint32_t>();
 }
 
-// IVF-PQ list scan kernel: pq_adc (default) or the first-cut pq_scan (PYR_PQ_ADC=0; A/B only,
-// same results)
-static bool pq_adc_enabled() {
+// IVF-PQ list scan kernel: 2 = pq_adc4 (default), 1 = pq_adc, 0 = the first-cut pq_scan
+// (PYR_PQ_ADC; A/B only, same results); unsupported shapes step down
+static int pq_adc_mode() {
   const char *e = getenv("PYR_PQ_ADC");
-  return !(e && atoi(e) == 0);
+  return e ? atoi(e) : 2;
 }
 
 // ---------------------------------------------------------------------------
@@ -1345,9 +1345,24 @@ struct IvfPqIndex : Index {
     const int nprobe = prm.nprobe < 0 ? nprobe_default : prm.nprobe;
     const int probes = (built && coarse.nlist > 0) ? std::max(0, std::min(nprobe, coarse.nlist)) : 0;
     const int64_t bcut = buf.st.n;
+    // list-scan kernel: pq_adc4 (4 queries per LDS gather; lists split into PQ4_ROWS-row chunks),
+    // else pq_adc, else the first-cut pq_scan; PYR_PQ_ADC=1 / 0 force the latter two (A/B only)
+    const int mode = pq_adc_mode();
+    IvfChunking ch{1 << 30, 1, 0};
+    int kern = 0;
+    if (mode >= 2 && pq_adc4_supported(dim, M, ksub, k)) {
+      ch.chunk = pq_adc4_rows();
+      int32_t mx = 0;
+      for (int32_t v : llen) mx = std::max(mx, v);
+      ch.cmax = ivf_list_chunks(mx, ch);
+      if ((int64_t)probes * ch.cmax < MAX_PARTS) kern = 2;
+      else ch = IvfChunking{1 << 30, 1, 0};
+    }
+    if (kern == 0 && mode >= 1 && pq_adc_supported(dim, M, ksub, k)) kern = 1;
+    const int lparts = probes * ch.cmax;
     ScanPlan bp;
-    if (buf.live_count() > 0) bp = plan_flat(bcut, nq, dim, k, MAX_PARTS - probes);
-    const int nparts = probes + bp.nchunks;
+    if (buf.live_count() > 0) bp = plan_flat(bcut, nq, dim, k, MAX_PARTS - lparts);
+    const int nparts = lparts + bp.nchunks;
     if (nparts > MAX_PARTS) throw Error(PYR_E_ARG, "nprobe too large");
     if (nparts == 0) {
       fill_empty_results(d_s, d_l, d_c, nq, k, ws.st);
@@ -1364,7 +1379,7 @@ struct IvfPqIndex : Index {
         coarse.probe(d_q, qn, nq, probes, metric, ws);
       }
       const int qchunk = 32;
-      const int maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qchunk, IvfChunking{1 << 30, 1});
+      const int maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qchunk, ch);
       PqArgs a{};
       a.codes = codes.as<uint8_t>();
       a.live = clive.as<uint8_t>();
@@ -1385,22 +1400,29 @@ struct IvfPqIndex : Index {
       a.ksub = ksub;
       a.part_s = ws.part_s.as<float>();
       a.part_k = ws.part_k.as<uint32_t>();
-      const bool adc = pq_adc_enabled() && pq_adc_supported(dim, M, ksub, k);
-      a.gthr = adc && bounds_enabled() ? shared_bounds(ws, nq) : nullptr;
-      if (!adc && pq_scan_lds_bytes(dim, M, ksub, k) > 160 * 1024)
+      a.gthr = kern > 0 && bounds_enabled() ? shared_bounds(ws, nq) : nullptr;
+      if (const char *e = getenv("PYR_PQ_ABLATE")) a.ablate = atoi(e);  // measurement only
+      if (kern == 0 && pq_scan_lds_bytes(dim, M, ksub, k) > 160 * 1024)
         throw Error(PYR_E_ARG, "PQ lookup table exceeds LDS");
       PhaseTimer t(PH_PQ_SCAN, ws.st, prof().on ? probed_rows(ws, nq, probes, le, lb) : 0);
-      if (adc) launch_pq_adc(a, maxi, ws.st);
+      if (kern == 2) launch_pq_adc4(a, maxi, ws.st);
+      else if (kern == 1) launch_pq_adc(a, maxi, ws.st);
       else launch_pq_scan(a, maxi, ws.st);
     }
     if (bp.nchunks > 0) {  // :130-136 exact buffer scan
       PhaseTimer t(PH_BUF_SCAN, ws.st, nq * bcut);
-      flat_scan(buf.st, bcut, bp, d_q, qn, nq, k, 1, metric, nparts, probes, KEY_BUF, ws, ws.part_s.as<float>(),
+      flat_scan(buf.st, bcut, bp, d_q, qn, nq, k, 1, metric, nparts, lparts, KEY_BUF, ws, ws.part_s.as<float>(),
                 ws.part_k.as<uint32_t>(), true);
     }
     PhaseTimer tm(PH_MERGE, ws.st);
+    MergeIvf mi;  // chunk slots p * cmax + c exist only for the chunks a probed list has
+    mi.probes = ws.probes.as<int32_t>();
+    mi.lb = dlb.as<int32_t>();
+    mi.le = dle.as<int32_t>();
+    mi.nprobe = probes;
+    mi.ch = ch;
     launch_merge_keys(ws.part_s.as<float>(), ws.part_k.as<uint32_t>(), nq, nparts, k, clabels.as<int64_t>(),
-                      buf.st.labels.as<int64_t>(), d_s, d_l, nullptr, d_c, ws.st);
+                      buf.st.labels.as<int64_t>(), d_s, d_l, nullptr, d_c, ws.st, ch.cmax > 1 ? &mi : nullptr);
   }
 
   int64_t count() const override { return 0; }  // :230 GetStats quirk

@@ -162,11 +162,17 @@ struct PqArgs {
   float *part_s;
   uint32_t *part_k;
   uint32_t *gthr;          // shared per-query bounds (ScanArgs::gthr) or null; pq_adc only
+  int32_t ablate;          // measurement only (PYR_PQ_ABLATE): 1 LUT once per item, 2 no top-k
 };
 void launch_pq_scan(const PqArgs &a, int max_items, hipStream_t st);
 // LDS-rate ADC scan (512-thread blocks, wave-distributed top-k); k <= 64, M <= 128
 bool pq_adc_supported(int dim, int M, int ksub, int k);
 void launch_pq_adc(const PqArgs &a, int max_items, hipStream_t st);
+// four queries per LDS gather (float4 LUT entries, 8-subspace double-buffered LUT passes);
+// items of at most pq_adc4_rows() rows (IvfChunking chunk), k <= 64, ksub <= 256
+bool pq_adc4_supported(int dim, int M, int ksub, int k);
+int pq_adc4_rows();
+void launch_pq_adc4(const PqArgs &a, int max_items, hipStream_t st);
 size_t pq_scan_lds_bytes(int dim, int M, int ksub, int k);
 // PQ encode (ProductQuantizer.Encode on residuals x - c[assign]) -> codes n x M row-major.
 void launch_pq_encode(const float *x, const int32_t *assign, const float *cents, int64_t n, int32_t dim, int32_t M,

@@ -980,8 +980,7 @@ __global__ __launch_bounds__(256) void pq_scan_kernel(PqArgs a) {
 // contiguous range of the list-major items, so the items of one list run side by side on
 // one XCD and share its L2 copy of the list's codes.
 // ---------------------------------------------------------------------------
-constexpr int PQ_THREADS = 512;
-constexpr int PQ_WAVES = PQ_THREADS / 64;
+constexpr int PQ_MAX_WAVES = 16;
 
 // wave-wide insertion of the candidates flagged in `cand` into the lane-distributed list
 __device__ __forceinline__ void wave_list_insert(bool cand, float sc, uint32_t key, float &ls, uint32_t &lk, float &kth,
@@ -1009,8 +1008,10 @@ __device__ __forceinline__ void wave_list_insert(bool cand, float sc, uint32_t k
   }
 }
 
-template <int NCH, bool K256>
-__global__ __launch_bounds__(PQ_THREADS) void pq_adc_kernel(PqArgs a) {
+template <int NCH, bool K256, int NT>
+__global__ __launch_bounds__(NT) void pq_adc_kernel(PqArgs a) {
+  constexpr int PQ_THREADS = NT, PQ_WAVES = NT / 64;
+  constexpr bool DB = NT <= 512;  // double-buffered code registers (1024 threads: VGPR cap 128)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int nit = *a.n_items;
   const int per = (nit + 7) >> 3;  // items per XCD (the grid has >= 8 * per blocks)
@@ -1035,10 +1036,11 @@ __global__ __launch_bounds__(PQ_THREADS) void pq_adc_kernel(PqArgs a) {
     const float *qp = a.queries + (size_t)qi * D;
     for (int d = tid; d < D; d += PQ_THREADS) res[d] = qp[d] - cent[d];  // IvfPqVectorIndex.cs:161-163
     __syncthreads();
-    for (int e = tid; e < M * ksub; e += PQ_THREADS) {  // ProductQuantizer.cs:112-117
-      const int m = e / ksub, j = e - m * ksub;
-      lut[e] = em_l2sq_unsafe(Off{res + m * sub}, Off{a.codebooks + ((size_t)m * ksub + j) * sub}, sub);
-    }
+    if (!(a.ablate & 1) || i == 0)
+      for (int e = tid; e < M * ksub; e += PQ_THREADS) {  // ProductQuantizer.cs:112-117
+        const int m = e / ksub, j = e - m * ksub;
+        lut[e] = em_l2sq_unsafe(Off{res + m * sub}, Off{a.codebooks + ((size_t)m * ksub + j) * sub}, sub);
+      }
     __syncthreads();
 
     float ls = -INFINITY, kth = -INFINITY;  // lane j < k holds the wave's j-th best
@@ -1051,9 +1053,10 @@ __global__ __launch_bounds__(PQ_THREADS) void pq_adc_kernel(PqArgs a) {
 #pragma unroll
       for (int c = 0; c < NCH; ++c) dst[c] = codes[base + (size_t)c * 64];
     };
-    if (w < ngrp) load(cur, w);
+    if (DB && w < ngrp) load(cur, w);
     for (int g = w, it2 = 0; g < ngrp; g += PQ_WAVES, ++it2) {
-      if (g + PQ_WAVES < ngrp) load(nxt, g + PQ_WAVES);
+      if (!DB) load(cur, g);
+      else if (g + PQ_WAVES < ngrp) load(nxt, g + PQ_WAVES);
       const int r = rb + g * 64 + lane;
       const bool valid = r < re && a.live[r];
       float dist = 0.0f;  // IvfPqVectorIndex.cs:182-186, m order
@@ -1071,9 +1074,14 @@ __global__ __launch_bounds__(PQ_THREADS) void pq_adc_kernel(PqArgs a) {
       if (a.gthr && (it2 & 3) == 3)
         gs = fmaxf(gs, key_score(__hip_atomic_load(a.gthr + qi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
       const bool cand = valid && score >= gs && better(score, key, kth, kthk);
-      wave_list_insert(cand, score, key, ls, lk, kth, kthk, k, lane);
+      if (a.ablate & 2) {
+        if (score == 12345.0f) ls = score;  // keep the scan alive without the top-k work
+      } else {
+        wave_list_insert(cand, score, key, ls, lk, kth, kthk, k, lane);
+      }
+      if (DB)
 #pragma unroll
-      for (int c = 0; c < NCH; ++c) cur[c] = nxt[c];
+        for (int c = 0; c < NCH; ++c) cur[c] = nxt[c];
     }
     if (lane < k) {
       mrs[w * k + lane] = ls;
@@ -1096,6 +1104,162 @@ __global__ __launch_bounds__(PQ_THREADS) void pq_adc_kernel(PqArgs a) {
     }
     // the next query rewrites res / lut only after the barrier that follows its res stores;
     // wave 0 reads mrs / mrk before it reaches that barrier
+  }
+}
+
+// ---------------------------------------------------------------------------
+// pq_adc4: four queries per pass over the rows.  The LUT entries of the 4 queries for one
+// (subspace, code) form one float4, so a single ds_read_b128 serves a row's lookup for all
+// four: a random-bank LDS gather costs about the same per instruction at 4 B or 16 B per
+// lane (MI355X_MICROARCH.md LDS table: b32 = 2 x 32-lane groups over 32 banks, b128 = 4 x
+// 16-lane groups over 16 slots), so lookups per LDS cycle rise ~2x, and the codes and the
+// codebook are read once per 4 queries.  The LUT is built PQ4_SC subspaces at a time into a
+// double buffer (building pass p+1 overlaps the ADC of pass p; LDS holds 2 x PQ4_SC x ksub
+// x 16 B, not M x ksub x 4 B per query).  Each lane keeps its rows' 4 running sums in
+// registers across the passes, adding subspaces in m order (IvfPqVectorIndex.cs:182-186),
+// so the scores are bit-identical to pq_scan_kernel's.  Rows per item <= PQ4_ROWS (longer
+// lists are split into row chunks with their own partial slots, IvfChunking).
+// ---------------------------------------------------------------------------
+constexpr int PQ4_ROWS = 8192, PQ4_SC = 8, PQ4_MAX_NW = 16;
+
+template <int SUB>
+struct CbRow {  // one codebook centroid held in registers
+  float v[SUB];
+  __device__ float operator()(int i) const { return v[i]; }
+};
+
+template <int SUB, bool K256, int NT>
+__global__ __launch_bounds__(NT) void pq_adc4_kernel(PqArgs a) {
+  constexpr int PQ4_NT = NT, PQ4_NW = NT / 64, PQ4_G = PQ4_ROWS / NT;  // row groups per wave
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int nit = *a.n_items;
+  const int per = (nit + 7) >> 3;  // XCD-major item mapping as in pq_adc_kernel
+  if ((int)(blockIdx.x >> 3) >= per) return;
+  const int item = ((int)blockIdx.x & 7) * per + ((int)blockIdx.x >> 3);
+  if (item >= nit) return;
+  const ScanItem it = a.items[item];
+  const int D = a.dim, M = a.M, ksub = K256 ? 256 : a.ksub, k = a.k;
+  const int sub = SUB > 0 ? SUB : D / M;
+  const int npass = (M + PQ4_SC - 1) / PQ4_SC, nch = (M + 15) / 16;
+  float4 *lut = reinterpret_cast<float4 *>(smem);  // [2][PQ4_SC][ksub] x 4 queries
+  float *res = smem + 2 * PQ4_SC * ksub * 4;       // [4][D] residuals
+  float *mrs = res + 4 * D;                        // [4][PQ4_NW][k] wave lists
+  uint32_t *mrk = reinterpret_cast<uint32_t *>(mrs + 4 * PQ4_NW * k);
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const float *cent = a.cents + (size_t)it.list * D;
+  const int rb = it.row_begin, re = it.row_end;  // rb: multiple of 64
+  const int ngrp = (re - rb + 63) >> 6;          // <= PQ4_NW * PQ4_G
+  const uint2 *codes = reinterpret_cast<const uint2 *>(a.codes);
+
+  // LUT entries of subspaces [p*SC, p*SC + SC) for the 4 residuals (ProductQuantizer.cs:112-117)
+  auto build = [&](int p, int buf) {
+#pragma unroll 1
+    for (int e = tid; e < PQ4_SC * ksub; e += PQ4_NT) {
+      const int j = e / ksub, c = e - j * ksub, m = p * PQ4_SC + j;
+      if (m >= M) continue;
+      const float *cb = a.codebooks + ((size_t)m * ksub + c) * sub;
+      float4 o;
+      if constexpr (SUB > 0) {
+        CbRow<SUB> r;
+#pragma unroll
+        for (int t = 0; t < SUB; ++t) r.v[t] = cb[t];
+        o.x = em_l2sq_unsafe(Off{res + m * SUB}, r, SUB);
+        o.y = em_l2sq_unsafe(Off{res + D + m * SUB}, r, SUB);
+        o.z = em_l2sq_unsafe(Off{res + 2 * D + m * SUB}, r, SUB);
+        o.w = em_l2sq_unsafe(Off{res + 3 * D + m * SUB}, r, SUB);
+      } else {
+        o.x = em_l2sq_unsafe(Off{res + m * sub}, Off{cb}, sub);
+        o.y = em_l2sq_unsafe(Off{res + D + m * sub}, Off{cb}, sub);
+        o.z = em_l2sq_unsafe(Off{res + 2 * D + m * sub}, Off{cb}, sub);
+        o.w = em_l2sq_unsafe(Off{res + 3 * D + m * sub}, Off{cb}, sub);
+      }
+      lut[buf * PQ4_SC * ksub + e] = o;
+    }
+  };
+
+  for (int qb = 0; qb < it.qcnt; qb += 4) {
+    for (int e = tid; e < 4 * D; e += PQ4_NT) {  // IvfPqVectorIndex.cs:161-163
+      const int t = e / D, d = e - t * D, i = qb + t;
+      float v = 0.0f;
+      if (i < it.qcnt) v = a.queries[(size_t)(a.qlist[it.qbeg + i] / a.nparts) * D + d] - cent[d];
+      res[e] = v;
+    }
+    __syncthreads();
+    build(0, 0);
+    __syncthreads();
+    float acc[PQ4_G][4];
+#pragma unroll
+    for (int gi = 0; gi < PQ4_G; ++gi) acc[gi][0] = acc[gi][1] = acc[gi][2] = acc[gi][3] = 0.0f;
+    for (int p = 0; p < npass; ++p) {
+      const float4 *L = lut + (p & 1) * PQ4_SC * ksub;
+      if (p + 1 < npass) build(p + 1, (p + 1) & 1);
+#pragma unroll
+      for (int gi = 0; gi < PQ4_G; ++gi) {
+        const int g = w + gi * PQ4_NW;
+        if (g < ngrp) {
+          const int r = rb + g * 64 + lane;  // rows past `re` read the 64-row block padding
+          const uint2 cw = codes[(((size_t)(r >> 6) * nch + (p >> 1)) * 64 + (r & 63)) * 2 + (p & 1)];
+#pragma unroll
+          for (int j = 0; j < PQ4_SC; ++j) {
+            if (p * PQ4_SC + j < M) {
+              const uint32_t word = j < 4 ? cw.x : cw.y;
+              const float4 e = L[j * ksub + ((word >> (8 * (j & 3))) & 0xFF)];
+              acc[gi][0] = acc[gi][0] + e.x;
+              acc[gi][1] = acc[gi][1] + e.y;
+              acc[gi][2] = acc[gi][2] + e.z;
+              acc[gi][3] = acc[gi][3] + e.w;
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep one group's gathers in flight at a time (VGPRs)
+      }
+      __syncthreads();
+    }
+    // per-wave top-k of each query (lane-distributed lists), then wave t merges query t
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (qb + t >= it.qcnt) break;
+      const int qi = a.qlist[it.qbeg + qb + t] / a.nparts;
+      const float gs = a.gthr ? key_score(__hip_atomic_load(a.gthr + qi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                              : -INFINITY;
+      float ls = -INFINITY, kth = -INFINITY;
+      uint32_t lk = KEY_NONE, kthk = KEY_NONE;
+#pragma unroll
+      for (int gi = 0; gi < PQ4_G; ++gi) {
+        const int g = w + gi * PQ4_NW;
+        if (g < ngrp) {
+          const int r = rb + g * 64 + lane;
+          const bool valid = r < re && a.live[r];
+          const float score = -acc[gi][t];  // :194
+          const bool cand = valid && score >= gs && better(score, (uint32_t)r, kth, kthk);
+          wave_list_insert(cand, score, (uint32_t)r, ls, lk, kth, kthk, k, lane);
+        }
+      }
+      if (lane < k) {
+        mrs[(t * PQ4_NW + w) * k + lane] = ls;
+        mrk[(t * PQ4_NW + w) * k + lane] = lk;
+      }
+    }
+    __syncthreads();
+    if (w < 4 && qb + w < it.qcnt) {
+      const int slot = a.qlist[it.qbeg + qb + w] + it.part;
+      const int qi = slot / a.nparts;
+      float ls = -INFINITY, kth = -INFINITY;
+      uint32_t lk = KEY_NONE, kthk = KEY_NONE;
+      for (int e0 = 0; e0 < PQ4_NW * k; e0 += 64) {
+        const int e = e0 + lane;
+        const float s = e < PQ4_NW * k ? mrs[w * PQ4_NW * k + e] : -INFINITY;
+        const uint32_t kk = e < PQ4_NW * k ? mrk[w * PQ4_NW * k + e] : KEY_NONE;
+        const bool cand = kk != KEY_NONE && better(s, kk, kth, kthk);
+        wave_list_insert(cand, s, kk, ls, lk, kth, kthk, k, lane);
+      }
+      if (lane < k) {
+        a.part_s[(size_t)slot * k + lane] = ls;
+        a.part_k[(size_t)slot * k + lane] = lk;
+      }
+      if (lane == 0 && a.gthr && kthk != KEY_NONE) atomicMax(a.gthr + qi, score_key(kth));
+    }
+    // waves 0-3 finish reading mrs / mrk before the barrier after the next quad's residuals
   }
 }
 
@@ -1437,24 +1601,77 @@ size_t pq_scan_lds_bytes(int dim, int M, int ksub, int k) {
   return (size_t)(((dim + 3) & ~3) + M * ksub + 2 * k + 2 * 256 + 4) * 4;
 }
 
-size_t pq_adc_lds_bytes(int dim, int M, int ksub, int k) {
-  return (size_t)(M * ksub + ((dim + 3) & ~3) + 2 * PQ_WAVES * k) * 4;
+size_t pq_adc_lds_bytes(int dim, int M, int ksub, int k) {  // sized for the largest block
+  return (size_t)(M * ksub + ((dim + 3) & ~3) + 2 * PQ_MAX_WAVES * k) * 4;
+}
+static int pq_adc_threads() {  // PYR_PQ_THREADS=1024: measurement variant
+  const char *e = getenv("PYR_PQ_THREADS");
+  return e && atoi(e) == 1024 ? 1024 : 512;
 }
 bool pq_adc_supported(int dim, int M, int ksub, int k) {
   return k >= 1 && k <= 64 && (M + 15) / 16 <= 8 && pq_adc_lds_bytes(dim, M, ksub, k) <= 160 * 1024;
 }
 
-template <int NCH, bool K256>
-static void launch_pq_adc_t(const PqArgs &a, int max_items, hipStream_t st) {
+size_t pq_adc4_lds_bytes(int dim, int ksub, int k) {  // sized for the largest block
+  return (size_t)(2 * PQ4_SC * ksub * 4 + 4 * dim + 2 * 4 * PQ4_MAX_NW * k) * 4;
+}
+int pq_adc4_rows() { return PQ4_ROWS; }
+bool pq_adc4_supported(int dim, int M, int ksub, int k) {
+  return k >= 1 && k <= 64 && ksub <= 256 && M >= 1 && pq_adc4_lds_bytes(dim, ksub, k) <= 160 * 1024;
+}
+template <int SUB, bool K256, int NT>
+static void launch_pq_adc4_nt(const PqArgs &a, int max_items, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&pq_adc_kernel<NCH, K256>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&pq_adc4_kernel<SUB, K256, NT>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  const int grid = (max_items + 7) / 8 * 8;
+  hipLaunchKernelGGL((pq_adc4_kernel<SUB, K256, NT>), dim3(grid), dim3(NT), pq_adc4_lds_bytes(a.dim, a.ksub, a.k), st,
+                     a);
+}
+template <int SUB, bool K256>
+static void launch_pq_adc4_t(const PqArgs &a, int max_items, hipStream_t st) {
+  const char *e = getenv("PYR_PQ4_THREADS");  // 512: measurement variant (1024 measured 1.5x faster)
+  if (e && atoi(e) == 512) launch_pq_adc4_nt<SUB, K256, 512>(a, max_items, st);
+  else launch_pq_adc4_nt<SUB, K256, 1024>(a, max_items, st);
+}
+void launch_pq_adc4(const PqArgs &a, int max_items, hipStream_t st) {
+  if (max_items <= 0) return;
+  const int sub = a.dim / a.M;
+  const bool k256 = a.ksub == 256;
+  if (sub == 8) {
+    if (k256) launch_pq_adc4_t<8, true>(a, max_items, st);
+    else launch_pq_adc4_t<8, false>(a, max_items, st);
+  } else if (sub == 4) {
+    if (k256) launch_pq_adc4_t<4, true>(a, max_items, st);
+    else launch_pq_adc4_t<4, false>(a, max_items, st);
+  } else if (sub == 16) {
+    if (k256) launch_pq_adc4_t<16, true>(a, max_items, st);
+    else launch_pq_adc4_t<16, false>(a, max_items, st);
+  } else {
+    if (k256) launch_pq_adc4_t<0, true>(a, max_items, st);
+    else launch_pq_adc4_t<0, false>(a, max_items, st);
+  }
+}
+
+template <int NCH, bool K256, int NT>
+static void launch_pq_adc_nt(const PqArgs &a, int max_items, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&pq_adc_kernel<NCH, K256, NT>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
   const int grid = (max_items + 7) / 8 * 8;  // XCD-major item mapping needs a multiple of 8 blocks
-  hipLaunchKernelGGL((pq_adc_kernel<NCH, K256>), dim3(grid), dim3(PQ_THREADS), pq_adc_lds_bytes(a.dim, a.M, a.ksub, a.k),
+  hipLaunchKernelGGL((pq_adc_kernel<NCH, K256, NT>), dim3(grid), dim3(NT), pq_adc_lds_bytes(a.dim, a.M, a.ksub, a.k),
                      st, a);
+}
+template <int NCH, bool K256>
+static void launch_pq_adc_t(const PqArgs &a, int max_items, hipStream_t st) {
+  if (pq_adc_threads() == 1024) launch_pq_adc_nt<NCH, K256, 1024>(a, max_items, st);
+  else launch_pq_adc_nt<NCH, K256, 512>(a, max_items, st);
 }
 
 void launch_pq_adc(const PqArgs &a, int max_items, hipStream_t st) {

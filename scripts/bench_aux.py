@@ -81,6 +81,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--check", type=int, default=20, help="queries compared with the CPU oracle")
+    ap.add_argument("--sweep", default="", help="env settings run one after another on the same index, "
+                                                 "e.g. 'PYR_PQ_THREADS=1024|PYR_PQ_ABLATE=1' (timing only)")
     a = ap.parse_args()
 
     import torch
@@ -122,6 +124,21 @@ def main():
         q = torch.from_numpy(qh).cuda()
         opts = SearchOptions(nprobe=a.nprobe)
         qps, ms, phases, s, lab = timed(idx, q, a.nq, a.k, opts, a.steps, a.warmup, L)
+        for setting in [x for x in a.sweep.split("|") if x]:
+            kv = dict(t.split("=") for t in setting.split(","))
+            old = {k_: os.environ.get(k_) for k_ in kv}
+            os.environ.update(kv)
+            qps2, ms2, ph2, s2, l2 = timed(idx, q, a.nq, a.k, opts, a.steps, a.warmup, L)
+            for k_, v in old.items():
+                if v is None:
+                    os.environ.pop(k_, None)
+                else:
+                    os.environ[k_] = v
+            print(json.dumps({"sweep": setting, "qps": qps2, "ms_per_step": ms2,
+                              "phases_ms": {k_: v["ms"] for k_, v in ph2.items()},
+                              "same_results": bool(np.array_equal(l2, lab) and np.array_equal(s2.view(np.uint32),
+                                                                                             s.view(np.uint32)))}),
+                  flush=True)
         cb, codes, off, labels, live = idx.pq_state()
         cents = idx.centroids_array()
         ok = True
