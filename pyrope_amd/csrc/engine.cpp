@@ -258,6 +258,10 @@ static bool filter_enabled() {
   const char *e = getenv("PYR_FILTER");
   return !(e && atoi(e) == 0);
 }
+static int filter_pub_mask() {  // FilterArgs::pub_mask; PYR_FILTER_PUB overrides (2^n - 1)
+  const char *e = getenv("PYR_FILTER_PUB");
+  return e ? atoi(e) : 7;
+}
 static int filter_ablate() {  // measurement only (FilterArgs::ablate)
   const char *e = getenv("PYR_FILTER_ABLATE");
   return e ? atoi(e) : 0;
@@ -540,6 +544,7 @@ struct FlatIndex : Index {
     fa.part_k = ws.part_k.as<uint32_t>();
     fa.gthr = gthr;
     fa.ablate = filter_ablate();
+    fa.pub_mask = filter_pub_mask();
     {
       PhaseTimer t(PH_FLAT_SCAN, ws.st, nq * cutoff);
       launch_filter(fa, metric, p.nitems, ws.st);
@@ -1033,6 +1038,7 @@ struct IvfFlatIndex : Index {
     fa.part_k = ws.part_k.as<uint32_t>();
     fa.gthr = gthr;
     fa.ablate = filter_ablate();
+    fa.pub_mask = filter_pub_mask();
     {
       PhaseTimer t(PH_LIST_SCAN, ws.st, prof().on ? probed_rows(ws, nq, probes, le, lb) : 0);
       launch_filter(fa, metric, maxi, ws.st);

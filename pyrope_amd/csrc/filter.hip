@@ -233,6 +233,10 @@ __global__ __launch_bounds__(256, 2) void mfma_filter(FilterArgs a) {
         const float v = scp[j];
         if (v > -INFINITY && v >= lo) pass |= 1u << j;
       }
+      if (a.ablate & 16) {  // measurement: filter without inserting
+        if (pass == 0x12345u) ts[0] = lo;
+        pass = 0;
+      }
       while (pass) {
         const int j = __builtin_ctz(pass);
         pass &= pass - 1;
@@ -240,7 +244,7 @@ __global__ __launch_bounds__(256, 2) void mfma_filter(FilterArgs a) {
         const uint32_t key = a.key_base | (uint32_t)(rb + j);
         if (better(v, key, ts[KR - 1], tk[KR - 1])) reg_insert<KR>(ts, tk, v, key);
       }
-      if (a.gthr && (st & 7) == 7) {  // every 8 stages: publish this list's KR-th best, refresh the bound
+      if (a.gthr && (st & a.pub_mask) == a.pub_mask) {  // publish this list's KR-th best, refresh the bound
         if (tk[KR - 1] != KEY_NONE && score_key(ts[KR - 1]) > published) {
           published = score_key(ts[KR - 1]);
           atomicMax(a.gthr + qown, published);

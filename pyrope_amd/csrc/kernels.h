@@ -202,7 +202,9 @@ struct FilterArgs {
   uint32_t *part_k;        // [slot][k1] keys
   uint32_t *gthr;          // shared per-query bound in approximate-score space, or null
   int32_t ablate;          // measurement only (PYR_FILTER_ABLATE; results are wrong when set):
-                           // 1 skip the owner filter, 2 skip the score transpose, 4 skip row loads, 8 skip MFMA
+                           // 1 skip the owner filter, 2 skip the score transpose, 4 skip row loads, 8 skip MFMA,
+                           // 16 filter without inserting
+  int32_t pub_mask;        // publish / refresh the shared bound when (stage & pub_mask) == pub_mask
 };
 struct RefineArgs {
   const float *rows;        // blocked store the keys index
