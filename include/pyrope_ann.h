@@ -123,6 +123,17 @@ pyr_status pyr_index_get_centroids(const pyr_index *index, float *out, int32_t *
  * FLAT only (PYR_E_STATE otherwise).  Takes the index exclusively (it uses the write stream). */
 pyr_status pyr_index_scan(pyr_index *index, int64_t *labels, float *x, int64_t *n);
 
+/* BruteForceVectorIndex.EnableQuantization (BruteForceVectorIndex.cs:25-40), FLAT only:
+ * rows added / upserted while it is on carry ScalarQuantizer codes, and searches run in the
+ * 8-bit mode (:296-336): the query is quantized, scores are -L2Squared8Bit / DotProduct8Bit
+ * (cosine too) as float, rows written while it was off count as scanned but are skipped.
+ * Supported for dim <= 256 and topK <= 64 (PYR_E_ARG otherwise). */
+pyr_status pyr_index_set_quantization(pyr_index *index, int32_t enable);
+
+/* ScalarQuantizer.Quantize (ScalarQuantizer.cs:23-62) of n vectors (n x dim, row-major) on the
+ * GPU: per-vector min/max, codes = clamp(round_half_even((x - min) * (255 / (max - min)))). */
+pyr_status pyr_scalar_quantize(int32_t device, const float *x, int64_t n, int32_t dim, uint8_t *codes);
+
 /* Introspection of the built IVF layout (list-major storage order, used by the
  * parity tests and the CPU baseline).  list_off: nlist+1 (row offsets without padding),
  * labels: total rows (state of removed rows: label -1), live: 1 visible, 0 removed/shadowed.

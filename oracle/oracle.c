@@ -275,6 +275,102 @@ int32_t orc_bf_search(const float *rows, const uint8_t *live, int64_t nslots, in
 }
 
 /* ------------------------------------------------------------------ */
+/* Scalar quantization (ScalarQuantizer.cs) and the 8-bit search mode   */
+/* of BruteForceVectorIndex (EnableQuantization, :25-40, :166-178,      */
+/* :200-211, :296-336).                                                  */
+/* ------------------------------------------------------------------ */
+/* (int)Math.Round(double) as .NET 8 on x64 evaluates it: banker's rounding, and the
+ * cvttsd2si "integer indefinite" (int.MinValue) for NaN and out-of-range values. */
+static int32_t net_round_to_int(float v) {
+  double r = nearbyint((double)v); /* default rounding mode: to nearest, ties to even */
+  if (!(r >= -2147483648.0 && r < 2147483648.0)) return INT32_MIN;
+  return (int32_t)r;
+}
+
+/* ScalarQuantizer.Quantize(ReadOnlySpan<float>, Span<byte>, out min, out max) :23-62 */
+void orc_scalar_quantize(const float *v, int32_t n, uint8_t *out, float *out_min, float *out_max) {
+  if (n == 0) {
+    *out_min = 0.0f;
+    *out_max = 0.0f;
+    return;
+  }
+  float mn = FLT_MAX, mx = -FLT_MAX;
+  for (int32_t i = 0; i < n; i++) {
+    if (v[i] < mn) mn = v[i];
+    if (v[i] > mx) mx = v[i];
+  }
+  *out_min = mn;
+  *out_max = mx;
+  float range = mx - mn;
+  if (range == 0.0f) {
+    memset(out, 0, (size_t)n);
+    return;
+  }
+  float scale = 255.0f / range;
+  for (int32_t i = 0; i < n; i++) {
+    float normalized = (v[i] - mn) * scale;
+    int32_t r = net_round_to_int(normalized);
+    out[i] = (uint8_t)(r < 0 ? 0 : (r > 255 ? 255 : r)); /* Math.Clamp(.., 0, 255) */
+  }
+}
+
+/* VectorMath.L2Squared8Bit / DotProduct8Bit exactly as the x64 SIMD path computes them:
+ * for n >= 32 (Vector<byte>.Count) the first n - n % 32 terms are summed in int32 lanes and
+ * reduced with Vector.Dot in int32 (wrapping modulo 2^32), the scalar tail in long. */
+static int64_t sq8_combine(uint32_t simd, int64_t tail) { return (int64_t)(int32_t)simd + tail; }
+int64_t orc_l2sq_8bit_net(const uint8_t *a, const uint8_t *b, int32_t n) {
+  int32_t sl = n >= 32 ? n - n % 32 : 0;
+  uint32_t s = 0;
+  int64_t t = 0;
+  for (int32_t i = 0; i < n; i++) {
+    int32_t d = (int32_t)a[i] - (int32_t)b[i];
+    if (i < sl) s += (uint32_t)(d * d);
+    else t += d * d;
+  }
+  return sq8_combine(s, t);
+}
+int64_t orc_dot_8bit_net(const uint8_t *a, const uint8_t *b, int32_t n) {
+  int32_t sl = n >= 32 ? n - n % 32 : 0;
+  uint32_t s = 0;
+  int64_t t = 0;
+  for (int32_t i = 0; i < n; i++) {
+    if (i < sl) s += (uint32_t)a[i] * (uint32_t)b[i];
+    else t += (int64_t)a[i] * (int64_t)b[i];
+  }
+  return sq8_combine(s, t);
+}
+
+/* BruteForceVectorIndex.Search with EnableQuantization (:296-336).  has_q[i] = 0 for rows
+ * written while quantization was off (empty quantized data: counted as scanned, skipped). */
+int32_t orc_bf_search_sq8(const float *rows, const uint8_t *live, const uint8_t *has_q, int64_t nslots,
+                          int32_t dim, int32_t metric, const float *q, int32_t k, int64_t max_scans,
+                          float *out_scores, int64_t *out_keys) {
+  if (k <= 0 || nslots == 0) return 0;
+  int64_t scan_limit = (max_scans >= 0 && max_scans < nslots) ? max_scans : nslots;
+  if (scan_limit <= 0) return 0;
+  uint8_t *qq = (uint8_t *)malloc((size_t)dim + 1), *xq = (uint8_t *)malloc((size_t)dim + 1);
+  float mn, mx;
+  orc_scalar_quantize(q, dim, qq, &mn, &mx); /* :304 */
+  cand *h = (cand *)malloc(sizeof(cand) * (size_t)k);
+  int32_t cnt = 0;
+  int64_t scanned = 0;
+  for (int64_t i = 0; i < nslots; i++) {
+    if (!live[i]) continue;           /* :308 */
+    if (scanned >= scan_limit) break; /* :309 */
+    scanned++;
+    if (!has_q[i]) continue;          /* :314 */
+    orc_scalar_quantize(rows + i * (int64_t)dim, dim, xq, &mn, &mx);
+    int64_t v = metric == ORC_L2 ? -orc_l2sq_8bit_net(qq, xq, dim) : orc_dot_8bit_net(qq, xq, dim); /* :325-331 */
+    topk_push(h, &cnt, k, (float)v, i);
+  }
+  int32_t r = topk_emit(h, cnt, out_scores, out_keys);
+  free(h);
+  free(qq);
+  free(xq);
+  return r;
+}
+
+/* ------------------------------------------------------------------ */
 /* KMeansUtils.cs                                                       */
 /* ------------------------------------------------------------------ */
 /* :70-93 FindNearestCentroid: strict '>' from float.MinValue -> lowest index on ties. */

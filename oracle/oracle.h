@@ -98,6 +98,14 @@ int32_t orc_ivfpq_search(const float *buf, const uint8_t *buf_live, int64_t nbuf
                          const float *q, int32_t k, int32_t nprobe,
                          float *out_scores, int64_t *out_keys);
 
+/* ---- scalar quantization and the 8-bit search mode of BruteForceVectorIndex ---- */
+void orc_scalar_quantize(const float *v, int32_t n, uint8_t *out, float *out_min, float *out_max);
+int64_t orc_l2sq_8bit_net(const uint8_t *a, const uint8_t *b, int32_t n);
+int64_t orc_dot_8bit_net(const uint8_t *a, const uint8_t *b, int32_t n);
+int32_t orc_bf_search_sq8(const float *rows, const uint8_t *live, const uint8_t *has_q, int64_t nslots,
+                          int32_t dim, int32_t metric, const float *q, int32_t k, int64_t max_scans,
+                          float *out_scores, int64_t *out_keys);
+
 /* ---- batched drivers for the CPU baseline (one query per worker thread,
  * mirroring the reference's concurrent VEC.SEARCH workers, Program.cs:363-388) ---- */
 void orc_ivf_search_batch(const float *buf, const uint8_t *buf_live, int64_t nbuf_slots,

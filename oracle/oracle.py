@@ -67,6 +67,10 @@ def _declare(L):
         "orc_ivfpq_search": (I32, [_f, _u8, I64, _u8, _u8, _i64, _f, I32, I32, _f, I32, I32, I32, I32, _f, I32, I32, _f, _i64]),
         "orc_ivf_search_batch": (None, [_f, _u8, I64, _f, _u8, _i64, _f, I32, I32, I32, _f, I64, I32, I32, I32, _f, _i64, _i32]),
         "orc_bf_search_batch": (None, [_f, _u8, I64, I32, I32, _f, I64, I32, I32, _f, _i64, _i32]),
+        "orc_scalar_quantize": (None, [_f, I32, _u8, _f, _f]),
+        "orc_l2sq_8bit_net": (I64, [_u8, _u8, I32]),
+        "orc_dot_8bit_net": (I64, [_u8, _u8, I32]),
+        "orc_bf_search_sq8": (I32, [_f, _u8, _u8, I64, I32, I32, _f, I32, I64, _f, _i64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -162,6 +166,40 @@ def bf_search(rows, live, metric, q, k, max_scans=-1):
     kk = np.empty(max(k, 1), np.int64)
     c = lib().orc_bf_search(_p(rows, C.c_float), _p(live, C.c_uint8), n, dim, metric, _p(q, C.c_float), k,
                             max_scans, _p(s, C.c_float), _p(kk, C.c_int64))
+    return s[:c], kk[:c]
+
+
+def scalar_quantize(v):
+    """ScalarQuantizer.Quantize (ScalarQuantizer.cs:23-62) -> (codes uint8, min, max)."""
+    v = _f32(v).reshape(-1)
+    out = np.zeros(max(v.size, 1), np.uint8)
+    mn, mx = C.c_float(), C.c_float()
+    lib().orc_scalar_quantize(_p(v, C.c_float), v.size, _p(out, C.c_uint8), C.byref(mn), C.byref(mx))
+    return out[: v.size], mn.value, mx.value
+
+
+def l2sq_8bit_net(a, b):
+    """VectorMath.L2Squared8Bit with the x64 SIMD path's int32 wrap of the vector part."""
+    a, b = _u8a(a), _u8a(b)
+    return lib().orc_l2sq_8bit_net(_p(a, C.c_uint8), _p(b, C.c_uint8), a.size)
+
+
+def dot_8bit_net(a, b):
+    a, b = _u8a(a), _u8a(b)
+    return lib().orc_dot_8bit_net(_p(a, C.c_uint8), _p(b, C.c_uint8), a.size)
+
+
+def bf_search_sq8(rows, live, has_q, metric, q, k, max_scans=-1):
+    """BruteForceVectorIndex.Search with EnableQuantization (:296-336).  Returns (scores, slots)."""
+    rows = _f32(rows)
+    n, dim = rows.shape
+    live = _u8a(np.ones(n) if live is None else live)
+    has_q = _u8a(np.ones(n) if has_q is None else has_q)
+    q = _f32(q)
+    s = np.empty(max(k, 1), np.float32)
+    kk = np.empty(max(k, 1), np.int64)
+    c = lib().orc_bf_search_sq8(_p(rows, C.c_float), _p(live, C.c_uint8), _p(has_q, C.c_uint8), n, dim, metric,
+                                _p(q, C.c_float), k, max_scans, _p(s, C.c_float), _p(kk, C.c_int64))
     return s[:c], kk[:c]
 
 

@@ -267,6 +267,39 @@ pyr_status pyr_index_scan(pyr_index *index, int64_t *labels, float *x, int64_t *
   });
 }
 
+pyr_status pyr_index_set_quantization(pyr_index *index, int32_t enable) {
+  if (!index) return fail(PYR_E_ARG, "null argument");
+  return guard([&] {
+    std::unique_lock<std::shared_mutex> g(index->impl->mu);
+    index->impl->set_quantization(enable != 0);
+  });
+}
+
+pyr_status pyr_scalar_quantize(int32_t device, const float *x, int64_t n, int32_t dim, uint8_t *codes) {
+  if (!x || !codes || n < 0 || dim <= 0) return fail(PYR_E_ARG, "bad arguments");
+  return guard([&] {
+    if (n == 0) return;
+    HIPCHK(hipSetDevice(device));
+    const int dp = pyr::sq8_dp(dim);
+    float *dx = nullptr;
+    uint8_t *dc = nullptr;
+    int2 *ds = nullptr;
+    HIPCHK(hipMalloc(&dx, sizeof(float) * n * dim));
+    hipError_t e = hipMalloc(&dc, (size_t)dp * n);
+    if (e == hipSuccess) e = hipMalloc(&ds, sizeof(int2) * n);
+    if (e == hipSuccess) e = hipMemcpy(dx, x, sizeof(float) * n * dim, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+      pyr::launch_sq8_quantize(dx, nullptr, 0, n, dim, dp, dc, ds, nullptr, nullptr);
+      e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy2D(codes, dim, dc, dp, dim, n, hipMemcpyDeviceToHost);
+    (void)hipFree(dx);
+    (void)hipFree(dc);
+    (void)hipFree(ds);
+    HIPCHK(e);
+  });
+}
+
 pyr_status pyr_merge_topk_device(const float *d_scores, const int64_t *d_labels, int64_t nq, int32_t nparts,
                                  int32_t k, float *d_out_scores, int64_t *d_out_labels, void *stream) {
   if (nq < 0 || nparts <= 0 || nparts > pyr::MAX_PARTS || k <= 0 || k > pyr::KMAX)

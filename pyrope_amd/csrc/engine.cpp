@@ -438,10 +438,29 @@ int kmeans_train_gpu(const float *d_x, int64_t n, int dim, int k, int met, int m
 struct FlatIndex : Index {
   RowStore st;
   std::unordered_map<int64_t, int64_t> slot_of;  // _idMap (:15)
+  // 8-bit search mode (EnableQuantization, :25-40; _quantizedVectors, :20-21): per slot
+  // ScalarQuantizer codes + sums of squares, and whether the slot has codes at all
+  bool quant = false;
+  DevMem q8, q8s, q8ok;
+  int64_t q8cap = 0;
+  int dp;
 
   explicit FlatIndex(const pyr_index_desc &d) : Index(d) {
     st.dim = dim;
     st.cosine = metric == COS;  // norm cached at Add (:146)
+    dp = sq8_dp(dim);
+  }
+
+  void set_quantization(bool on) override { quant = on; }
+
+  void q8_reserve() {
+    if (q8cap >= st.cap) return;
+    const int64_t nc = st.cap;
+    q8.grow_keep((size_t)dp * nc, (size_t)dp * q8cap, wst);
+    q8s.grow_keep(sizeof(int2) * nc, sizeof(int2) * q8cap, wst);
+    q8ok.grow_keep(nc, q8cap, wst);
+    HIPCHK(hipMemsetAsync(q8ok.as<uint8_t>() + q8cap, 0, nc - q8cap, wst));
+    q8cap = nc;
   }
 
   void add(const float *x, int64_t n, const int64_t *labels, bool upsert) override {
@@ -467,12 +486,67 @@ struct FlatIndex : Index {
     st.hlabels.resize(next, -1);
     st.hlive.resize(next, 0);
     st.write(x, slots.data(), labels, n, wst, stage_x, stage_i);
+    // :166-178 / :200-211: codes when quantization is on, otherwise the slot loses them
+    // (stage_i still holds the device copy of the slots)
+    q8_reserve();
+    if (quant)
+      launch_sq8_quantize(st.rows.as<float>(), stage_i.as<int64_t>(), 1, n, dim, dp, q8.as<uint8_t>(), q8s.as<int2>(),
+                          q8ok.as<uint8_t>(), wst);
+    else
+      launch_scatter_u8(q8ok.as<uint8_t>(), stage_i.as<int64_t>(), 0, n, wst);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(wst));
     for (int64_t i = 0; i < n; i++) {
       st.hlabels[slots[i]] = labels[i];
       st.hlive[slots[i]] = 1;
       slot_of[labels[i]] = slots[i];
     }
     st.n = next;
+  }
+
+  // BruteForceVectorIndex.Search with EnableQuantization (:296-336): quantize the queries,
+  // exact integer scores over slots [0, cutoff) that have codes
+  void search_sq8(const float *d_q, int64_t nq, int k, int64_t cutoff, float *d_s, int64_t *d_l, int32_t *d_c,
+                  Workspace &ws) {
+    if (!sq8_supported(dim, k)) throw Error(PYR_E_ARG, "quantized search supports dim <= 256 and topK <= 64");
+    ws.q8q.ensure((size_t)dp * nq);
+    ws.q8qs.ensure(sizeof(int2) * nq);
+    launch_sq8_quantize(d_q, nullptr, 0, nq, dim, dp, ws.q8q.as<uint8_t>(), ws.q8qs.as<int2>(), nullptr, ws.st);
+    int64_t chunk = 8192;
+    while ((cutoff + chunk - 1) / chunk > MAX_PARTS) chunk *= 2;
+    const int nchunks = (int)((cutoff + chunk - 1) / chunk);
+    const int64_t nqc = (nq + sq8_qgroup() - 1) / sq8_qgroup();
+    if (nqc * nchunks > INT32_MAX) throw Error(PYR_E_ARG, "query batch too large for one launch");
+    const size_t np = (size_t)nq * nchunks * k;
+    ws.part_s.ensure(sizeof(float) * np);
+    ws.part_k.ensure(sizeof(uint32_t) * np);
+    ws.items.ensure(sizeof(ScanItem) * std::max<int64_t>(nqc * nchunks, 1));
+    ws.nitems.ensure(sizeof(int32_t) * 4);
+    const int ni = make_flat_items(ws.items.as<ScanItem>(), ws.nitems.as<int32_t>(), cutoff, (int32_t)chunk, nq, 0,
+                                   sq8_qgroup(), ws.st);
+    Sq8Args a{};
+    a.codes = q8.as<uint8_t>();
+    a.sums = q8s.as<int2>();
+    a.live = st.live.as<uint8_t>();
+    a.ok = q8ok.as<uint8_t>();
+    a.qcodes = ws.q8q.as<uint8_t>();
+    a.qsums = ws.q8qs.as<int2>();
+    a.items = ws.items.as<ScanItem>();
+    a.n_items = ws.nitems.as<int32_t>();
+    a.nparts = nchunks;
+    a.k = k;
+    a.dim = dim;
+    a.dp = dp;
+    a.row_limit = (uint32_t)cutoff;
+    a.part_s = ws.part_s.as<float>();
+    a.part_k = ws.part_k.as<uint32_t>();
+    {
+      PhaseTimer t(PH_FLAT_SCAN, ws.st, nq * cutoff);
+      launch_sq8_scan(a, metric == L2 ? L2 : IP, ni, ws.st);  // Cosine scores with DotProduct8Bit (:329)
+    }
+    PhaseTimer t(PH_MERGE, ws.st);
+    launch_merge_keys(ws.part_s.as<float>(), ws.part_k.as<uint32_t>(), nq, nchunks, k, st.labels.as<int64_t>(),
+                      nullptr, d_s, d_l, nullptr, d_c, ws.st);
   }
 
   void remove(const int64_t *labels, int64_t n, uint8_t *removed) override {  // :224-248
@@ -506,6 +580,10 @@ struct FlatIndex : Index {
     }
     if (count == 0 || cutoff == 0 || nq == 0) {  // :285, :289
       fill_empty_results(d_s, d_l, d_c, nq, k, ws.st);
+      return;
+    }
+    if (quant) {  // :296
+      search_sq8(d_q, nq, k, cutoff, d_s, d_l, d_c, ws);
       return;
     }
     const int k1 = filter_k1(k);

@@ -88,6 +88,7 @@ struct Workspace {
   DevMem ivf_cnt, ivf_fill, ivf_qoff, ivf_ioff, gthr;
   DevMem out_s, out_l, out_c;
   DevMem ms, mk, fail, fail_cnt, fq, fs, fl, fc;  // MFMA filter: merged candidates, certificate failures
+  DevMem q8q, q8qs;                               // 8-bit search mode: quantized queries, their sums
   ~Workspace() {
     if (own_stream && st) (void)hipStreamDestroy(st);
   }
@@ -124,6 +125,11 @@ struct Index {
     (void)x;
     (void)n;
     throw Error(PYR_E_STATE, "index kind has no Scan (BruteForceVectorIndex only)");
+  }
+  // BruteForceVectorIndex.EnableQuantization (BruteForceVectorIndex.cs:25-40)
+  virtual void set_quantization(bool on) {
+    (void)on;
+    throw Error(PYR_E_STATE, "index kind has no quantized search mode (BruteForceVectorIndex only)");
   }
   virtual void set_centroids(const float *c, int nlist) {
     (void)c;

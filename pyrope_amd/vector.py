@@ -259,6 +259,15 @@ class BruteForceVectorIndex(HipVectorIndex):
             raise ArgumentOutOfRangeException("topK must be positive.")
         return super().search(query, top_k, options)
 
+    @property
+    def enable_quantization(self) -> bool:  # EnableQuantization (:25-40)
+        return getattr(self, "_quant", False)
+
+    @enable_quantization.setter
+    def enable_quantization(self, value: bool) -> None:
+        check(self._L.pyr_index_set_quantization(self._h, 1 if value else 0))
+        self._quant = bool(value)
+
     def scan(self):  # :250-273 (compaction source): live rows in slot order
         """[(id, vector)] of the live rows in slot order (pyr_index_scan)."""
         n = C.c_int64()
@@ -474,6 +483,15 @@ def kmeans_train(data: np.ndarray, k: int, metric: VectorMetric, max_iter: int =
     check(_lib.load().pyr_kmeans_train(device, ptr(x, C.c_float), n, dim, k, int(metric), max_iter, seed,
                                        ptr(out, C.c_float), C.byref(used)))
     return out[: used.value]
+
+
+def scalar_quantize(x: np.ndarray, device: int = 0) -> np.ndarray:
+    """ScalarQuantizer.Quantize (ScalarQuantizer.cs:23-62) of each row, on the GPU."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    x2 = x.reshape(-1, x.shape[-1])
+    out = np.zeros(x2.shape, np.uint8)
+    check(_lib.load().pyr_scalar_quantize(device, ptr(x2, C.c_float), x2.shape[0], x2.shape[1], ptr(out, C.c_uint8)))
+    return out.reshape(x.shape)
 
 
 def generate_synthetic(count: int, dim: int, seed: int) -> np.ndarray:

@@ -75,6 +75,7 @@ def main():
     ap.add_argument("--nq", type=int, default=10000)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--metric", type=int, default=0)
+    ap.add_argument("--quant", action="store_true", help="flat: EnableQuantization (8-bit search mode)")
     ap.add_argument("--nlist", type=int, default=256)
     ap.add_argument("--m", type=int, default=96)
     ap.add_argument("--nprobe", type=int, default=64)
@@ -98,15 +99,21 @@ def main():
         x = generate_synthetic(n, d, 42)
         qh = generate_synthetic(a.nq, d, 1337)
         idx = BruteForceVectorIndex(d, a.metric)
+        if a.quant:
+            idx.enable_quantization = True
         idx.add_labels(np.arange(n, dtype=np.int64), x)
         q = torch.from_numpy(qh).cuda()
         qps, ms, phases, s, lab = timed(idx, q, a.nq, a.k, None, a.steps, a.warmup, L)
         ok = True
         for i in np.linspace(0, a.nq - 1, a.check).astype(int):
-            os_, ok_ = oracle.bf_search(x, None, a.metric, qh[i], a.k)
+            if a.quant:
+                os_, ok_ = oracle.bf_search_sq8(x, None, None, a.metric, qh[i], a.k)
+            else:
+                os_, ok_ = oracle.bf_search(x, None, a.metric, qh[i], a.k)
             ok &= bool(np.array_equal(lab[i], ok_) and np.array_equal(s[i].view(np.uint32), os_.view(np.uint32)))
         scan = phases.get("flat_scan", {"ms": float("nan"), "work": 0})
-        out = {"workload": f"FLAT d={d} N={n} Q={a.nq} k={a.k} metric={['L2', 'IP', 'COS'][a.metric]}",
+        out = {"workload": f"FLAT{' SQ8' if a.quant else ''} d={d} N={n} Q={a.nq} k={a.k} "
+                           f"metric={['L2', 'IP', 'COS'][a.metric]}",
                "qps": qps, "ms_per_step": ms, "phases_ms": {k_: v["ms"] for k_, v in phases.items()},
                "scan_pairs": scan["work"],
                "scan_tflops_2d": scan["work"] * 2 * d / (scan["ms"] * 1e-3) / 1e12,

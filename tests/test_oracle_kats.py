@@ -206,3 +206,29 @@ def test_golden_ivf_pq(oracle):
     cents, assign, cb, codes = oracle.ivfpq_build(x, int(g["nlist"]), int(g["m"]), 256, 0)
     np.testing.assert_array_equal(cb.view(np.uint32), g["codebooks"].view(np.uint32))
     np.testing.assert_array_equal(codes, g["codes"])
+
+
+# ---- ScalarQuantizer.cs / VectorMath 8-bit (the BruteForce EnableQuantization mode) ----
+def test_scalar_quantize_known_answers(oracle):
+    c, mn, mx = oracle.scalar_quantize([0.0, 0.5, 1.0, 0.25])  # 127.5 -> 128, 63.75 -> 64
+    assert list(c) == [0, 128, 255, 64] and (mn, mx) == (0.0, 1.0)
+    c, mn, mx = oracle.scalar_quantize([2.0, 2.0, 2.0])        # range 0 -> zeros (:46-50)
+    assert list(c) == [0, 0, 0] and (mn, mx) == (2.0, 2.0)
+    c, _, _ = oracle.scalar_quantize([-1.0, 1.0, 0.0])         # 127.5 -> 128
+    assert list(c) == [0, 255, 128]
+
+
+def test_8bit_simd_wrap_semantics(oracle):
+    """The x64 SIMD path sums the first n - n % 32 terms in wrapping int32 lanes: identical to
+    the exact sum below 33,025 dims, wrapped above (VectorMath.cs:441-564)."""
+    rng = np.random.default_rng(0)
+    a = rng.integers(0, 256, 1000, dtype=np.uint8)
+    b = rng.integers(0, 256, 1000, dtype=np.uint8)
+    assert oracle.l2sq_8bit_net(a, b) == oracle.l2sq_8bit(a, b)
+    assert oracle.dot_8bit_net(a, b) == oracle.dot_8bit(a, b)
+    big = np.full(40000, 255, np.uint8)
+    exact = 40000 * 255 * 255
+    simd = 40000 - 40000 % 32
+    wrapped = ((simd * 65025 + 2**31) % 2**32) - 2**31 + (40000 - simd) * 65025
+    assert oracle.dot_8bit(big, big) == exact
+    assert oracle.dot_8bit_net(big, big) == wrapped
