@@ -289,7 +289,7 @@ pyr_status pyr_scalar_quantize(int32_t device, const float *x, int64_t n, int32_
     if (e == hipSuccess) e = hipMalloc(&ds, sizeof(int2) * n);
     if (e == hipSuccess) e = hipMemcpy(dx, x, sizeof(float) * n * dim, hipMemcpyHostToDevice);
     if (e == hipSuccess) {
-      pyr::launch_sq8_quantize(dx, nullptr, 0, n, dim, dp, dc, ds, nullptr, nullptr);
+      pyr::launch_sq8_quantize(dx, nullptr, 0, n, dim, dp, 0, dc, ds, nullptr, nullptr);
       e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipMemcpy2D(codes, dim, dc, dp, dim, n, hipMemcpyDeviceToHost);

@@ -490,8 +490,8 @@ struct FlatIndex : Index {
     // (stage_i still holds the device copy of the slots)
     q8_reserve();
     if (quant)
-      launch_sq8_quantize(st.rows.as<float>(), stage_i.as<int64_t>(), 1, n, dim, dp, q8.as<uint8_t>(), q8s.as<int2>(),
-                          q8ok.as<uint8_t>(), wst);
+      launch_sq8_quantize(st.rows.as<float>(), stage_i.as<int64_t>(), 1, n, dim, dp, 1, q8.as<uint8_t>(),
+                          q8s.as<int2>(), q8ok.as<uint8_t>(), wst);
     else
       launch_scatter_u8(q8ok.as<uint8_t>(), stage_i.as<int64_t>(), 0, n, wst);
     HIPCHK(hipGetLastError());
@@ -509,9 +509,10 @@ struct FlatIndex : Index {
   void search_sq8(const float *d_q, int64_t nq, int k, int64_t cutoff, float *d_s, int64_t *d_l, int32_t *d_c,
                   Workspace &ws) {
     if (!sq8_supported(dim, k)) throw Error(PYR_E_ARG, "quantized search supports dim <= 256 and topK <= 64");
+    // exact int8 MFMA scores (sq8.hip); items of 128 queries x 8192-row chunks
     ws.q8q.ensure((size_t)dp * nq);
     ws.q8qs.ensure(sizeof(int2) * nq);
-    launch_sq8_quantize(d_q, nullptr, 0, nq, dim, dp, ws.q8q.as<uint8_t>(), ws.q8qs.as<int2>(), nullptr, ws.st);
+    launch_sq8_quantize(d_q, nullptr, 0, nq, dim, dp, 1, ws.q8q.as<uint8_t>(), ws.q8qs.as<int2>(), nullptr, ws.st);
     int64_t chunk = 8192;
     while ((cutoff + chunk - 1) / chunk > MAX_PARTS) chunk *= 2;
     const int nchunks = (int)((cutoff + chunk - 1) / chunk);

@@ -188,26 +188,27 @@ void launch_pack_codes(const uint8_t *codes, const int64_t *src_of_dst, int64_t 
 
 // ---- 8-bit search mode of the FLAT index (sq8.hip; BruteForceVectorIndex EnableQuantization) ----
 struct Sq8Args {
-  const uint8_t *codes;    // [slot][dp] ScalarQuantizer codes (zero padded)
-  const int2 *sums;        // [slot] {sum of squares of the first sl codes (u32 wrap), of the rest}
+  const uint8_t *codes;    // [slot][dp] ScalarQuantizer codes - 128 (int8), zero padded
+  const int2 *sums;        // [slot] {sum of codes, sum of squared codes}
   const uint8_t *live;     // [slot]
   const uint8_t *ok;       // [slot] 1 = has codes (written while quantization was on)
-  const uint8_t *qcodes;   // [q][dp]
+  const uint8_t *qcodes;   // [q][dp], as codes
   const int2 *qsums;       // [q]
   const ScanItem *items;   // make_flat_items, qchunk = sq8_qgroup()
   const int32_t *n_items;
-  int32_t nparts, k, dim, dp, sl;
+  int32_t nparts, k, dim, dp;
   uint32_t row_limit;      // rows >= row_limit are not scanned (MaxScans cutoff)
   float *part_s;           // [q * nparts + part][k]
   uint32_t *part_k;
 };
-int sq8_dp(int dim);       // code row stride (dim rounded up to 16)
+int sq8_dp(int dim);       // code row stride (dim rounded up to 32)
 int sq8_qgroup();          // queries per scan item
 bool sq8_supported(int dim, int k);
 // ScalarQuantizer.Quantize of n vectors: blocked != 0 -> rows of a blocked store at slots[i]
-// (codes written at slot), else row-major src with codes at i.  ok (may be null) set to 1.
+// (codes written at slot), else row-major src with codes at i.  shifted: store code - 128
+// (the scan's int8 operands).  ok (may be null) set to 1.
 void launch_sq8_quantize(const float *src, const int64_t *slots, int blocked, int64_t n, int32_t dim, int32_t dp,
-                         uint8_t *codes, int2 *sums, uint8_t *ok, hipStream_t st);
+                         int shifted, uint8_t *codes, int2 *sums, uint8_t *ok, hipStream_t st);
 void launch_sq8_scan(const Sq8Args &a, int metric, int max_items, hipStream_t st);
 
 // ---- MFMA candidate filter + exact refine (filter.hip) ----

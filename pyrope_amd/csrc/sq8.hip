@@ -7,11 +7,13 @@
 // and converted long -> float.  Rows written while it was off have no codes: they count as
 // scanned (MaxScans) but are skipped (:308-318).
 //
-// Integer arithmetic makes parity exact: the dot product runs on v_dot4_u32_u8 (4 byte MACs
-// per lane op), L2 through sum(a^2) + sum(b^2) - 2 sum(ab) with the per-vector sums of squares
-// precomputed at quantization time.  The reference's x64 SIMD path sums the first
-// n - n % 32 terms in wrapping int32 lanes and the tail in long; both parts are kept apart
-// here (u32 arithmetic for the vector part, int64 for the tail) so even the wrap is the same.
+// The products run on the int8 matrix cores (v_mfma_i32_32x32x32_i8, exact int32 sums).
+// Codes are stored shifted, c' = c - 128 in [-128, 127], and zero padded to a multiple of 32,
+// so with A = sum(a), B = sum(b) over the real dims:
+//     sum(a b)     = sum(a' b') + 128 (A + B) - 16384 n
+//     sum((a-b)^2) = sum(a^2) + sum(b^2) - 2 sum(a b)
+// all exact in 64-bit integers.  (The reference's x64 SIMD path sums in wrapping int32 lanes;
+// no wrap is possible at the supported dims, n <= 256: |sum| <= 256 * 255^2 < 2^31.)
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
@@ -22,6 +24,9 @@
 
 namespace pyr {
 namespace {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ bool better(float s1, uint32_t k1, float s2, uint32_t k2) {
   return s1 > s2 || (s1 == s2 && k1 < k2);
@@ -36,9 +41,10 @@ __device__ __forceinline__ int net_round_to_int(float v) {
 }
 
 // One wave per vector.  src: blocked row store + slot list (FLAT rows) or row-major vectors
-// (queries).  Writes codes [dst][dp] (zero padded), the two sums of squares and has-codes.
+// (queries).  Writes codes [dst][dp] (shifted by -128 when `shifted`, zero padded), the sums
+// {sum c, sum c^2} over the real dims, and has-codes.
 __global__ __launch_bounds__(256) void sq8_quantize_kernel(const float *src, const int64_t *slots, int blocked,
-                                                           int64_t n, int D, int dp, int sl, uint8_t *codes,
+                                                           int64_t n, int D, int dp, int shifted, uint8_t *codes,
                                                            int2 *sums, uint8_t *ok) {
   const int64_t v = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -63,8 +69,7 @@ __global__ __launch_bounds__(256) void sq8_quantize_kernel(const float *src, con
   const float range = mx - mn;
   const float scale = 255.0f / range;
   uint8_t *out = codes + (size_t)slot * dp;
-  uint32_t sv = 0;
-  int st = 0;
+  int s1 = 0, s2 = 0;
   for (int d = lane; d < dp; d += 64) {
     int c = 0;
     if (d < D && range != 0.0f) {  // :46-50 range 0 -> all zeros
@@ -72,185 +77,190 @@ __global__ __launch_bounds__(256) void sq8_quantize_kernel(const float *src, con
       const int r = net_round_to_int(normalized);
       c = r < 0 ? 0 : (r > 255 ? 255 : r);  // Math.Clamp(.., 0, 255)
     }
-    out[d] = (uint8_t)c;
-    if (d < sl) sv += (uint32_t)(c * c);
-    else st += c * c;
+    if (d < D) {
+      s1 += c;
+      s2 += c * c;
+      out[d] = (uint8_t)(shifted ? c - 128 : c);
+    } else {
+      out[d] = 0;  // padding: 0 in the shifted domain contributes nothing to sum(a' b')
+    }
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
-    sv += __shfl_xor(sv, o);
-    st += __shfl_xor(st, o);
+    s1 += __shfl_xor(s1, o);
+    s2 += __shfl_xor(s2, o);
   }
   if (lane == 0) {
-    sums[slot] = make_int2((int)sv, st);
+    sums[slot] = make_int2(s1, s2);
     if (ok) ok[slot] = 1;
   }
 }
 
-// One block (4 waves) per item: rows [row_begin, row_end) x queries [qbeg, qbeg + qcnt),
-// qcnt <= SQ8_QG.  Lane = row; the query codes sit in LDS (read as broadcasts).  Each wave
-// keeps a top-k per query spread over its lanes (lane j = j-th best, ballot-filtered
-// insertion as in kernels.hip pq_adc); the four waves' lists are merged per query at the end
-// into the item's partial slot q * nparts + part.
-constexpr int SQ8_QG = 8;
+// Insert (v, key) into a register-resident sorted (desc) list of length KR (as filter.hip).
+template <int KR>
+__device__ __forceinline__ void reg_insert(float (&s)[KR], uint32_t (&kk)[KR], float v, uint32_t key) {
+  bool b[KR];
+#pragma unroll
+  for (int j = 0; j < KR; ++j) b[j] = better(v, key, s[j], kk[j]);
+#pragma unroll
+  for (int j = KR - 1; j >= 1; --j) {
+    s[j] = b[j - 1] ? s[j - 1] : (b[j] ? v : s[j]);
+    kk[j] = b[j - 1] ? kk[j - 1] : (b[j] ? key : kk[j]);
+  }
+  s[0] = b[0] ? v : s[0];
+  kk[0] = b[0] ? key : kk[0];
+}
 
-__device__ __forceinline__ void lane_list_insert(bool cand, float sc, uint32_t key, float &ls, uint32_t &lk,
-                                                 float &kth, uint32_t &kthk, int k, int lane) {
-  uint64_t m = __ballot(cand);
-  while (m) {
-    const int j = __ffsll((unsigned long long)m) - 1;
-    const float s = __shfl(sc, j);
-    const uint32_t kk = __shfl(key, j);
-    const int pos = __popcll(__ballot(lane < k && better(ls, lk, s, kk)));
-    const float us = __shfl_up(ls, 1);
-    const uint32_t uk = __shfl_up(lk, 1);
-    if (lane > pos && lane < k) {
-      ls = us;
-      lk = uk;
+// One block = 4 independent waves; wave w scores queries qbeg + 32w .. +31 of the item
+// against the item's rows, 32 rows per step:
+//   A operand (queries, registers for the whole item): lane l holds query (l & 31), code
+//     bytes [32s + 16h, 32s + 16h + 16) of k-step s, h = l >> 5;
+//   B operand (rows, straight from HBM/L2, one step ahead): lane l holds row (l & 31) of the
+//     step, the same bytes;
+//   C[query][row] (C/D map: lane = row, register r = query (r&3) + 8(r>>2) + 4h) is turned into
+//     exact scores in place (query sums in registers, row sums loaded with the row), moved
+//     through a wave-private LDS transpose, and lane i < 32 (the query's owner) filters its 32
+//     scores against its list's k-th and inserts survivors (register list, KR >= k).
+constexpr int SQ8_RT = 32;
+constexpr int SQ8_SCR = SQ8_RT + 4;
+
+template <int NS, int MET, int KR>  // NS: 32-byte k-steps per row (dp / 32)
+__global__ __launch_bounds__(256) void sq8_mfma_kernel(Sq8Args a) {
+  __shared__ float scw[4][32][SQ8_SCR];
+  if ((int)blockIdx.x >= *a.n_items) return;
+  const ScanItem it = a.items[blockIdx.x];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, i32 = lane & 31, h = lane >> 5;
+  if (32 * w >= it.qcnt) return;  // no block barrier below: idle waves may leave
+  float(*sc)[SQ8_SCR] = scw[w];
+  const int64_t D = a.dim;
+
+  // A operand and the sums of the 16 queries this lane's C registers hold
+  v4i qa[NS];
+  {
+    const int qi = it.qbeg + 32 * w + i32;
+    const bool qv = 32 * w + i32 < it.qcnt;
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      qa[s] = qv ? *reinterpret_cast<const v4i *>(a.qcodes + (size_t)qi * a.dp + 32 * s + 16 * h) : v4i{0, 0, 0, 0};
+  }
+  int qs1[16], qs2[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int qq = 32 * w + (r & 3) + 8 * (r >> 2) + 4 * h;
+    const int2 v = qq < it.qcnt ? a.qsums[it.qbeg + qq] : make_int2(0, 0);
+    qs1[r] = v.x;
+    qs2[r] = v.y;
+  }
+  const bool owner = h == 0 && 32 * w + i32 < it.qcnt;
+  float ts[KR];
+  uint32_t tk[KR];
+#pragma unroll
+  for (int j = 0; j < KR; ++j) {
+    ts[j] = -INFINITY;
+    tk[j] = KEY_NONE;
+  }
+
+  const int r0 = it.row_begin, re = it.row_end;
+  const int nst = (re - r0 + SQ8_RT - 1) / SQ8_RT;
+  v4i rb[NS];
+  int2 rs = make_int2(0, 0);
+  bool rvalid = false;
+  auto load_row = [&](int stg) {
+    const int r = r0 + stg * SQ8_RT + i32;
+    rvalid = r < re && (uint32_t)r < a.row_limit && a.live[r] && a.ok[r];
+    const int rr = rvalid ? r : r0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) rb[s] = *reinterpret_cast<const v4i *>(a.codes + (size_t)rr * a.dp + 32 * s + 16 * h);
+    rs = a.sums[rr];
+  };
+  if (nst > 0) load_row(0);
+  for (int st = 0; st < nst; ++st) {
+    v16i acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(qa[s], rb[s], acc, 0, 0, 0);
+    const int2 cs = rs;
+    const bool cv = rvalid;
+    if (st + 1 < nst) load_row(st + 1);  // next step's operand while this one is scored
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t dot = (int64_t)acc[r] + 128 * (int64_t)(qs1[r] + cs.x) - 16384 * D;  // sum(a b)
+      const int64_t v = MET == L2 ? -((int64_t)qs2[r] + cs.y - 2 * dot) : dot;
+      sc[(r & 3) + 8 * (r >> 2) + 4 * h][i32] = cv ? (float)v : -INFINITY;  // long -> float (:325-331)
     }
-    if (lane == pos) {
-      ls = s;
-      lk = kk;
+    __builtin_amdgcn_wave_barrier();
+    if (owner) {
+      const float *scp = sc[i32];
+      const float lo = ts[KR - 1];
+      uint32_t pass = 0;
+#pragma unroll
+      for (int j = 0; j < SQ8_RT; ++j) {
+        const float v = scp[j];
+        if (v > -INFINITY && v >= lo) pass |= 1u << j;
+      }
+      const int rbase = r0 + st * SQ8_RT;
+      while (pass) {
+        const int j = __builtin_ctz(pass);
+        pass &= pass - 1;
+        const float v = scp[j];
+        const uint32_t key = (uint32_t)(rbase + j);
+        if (better(v, key, ts[KR - 1], tk[KR - 1])) reg_insert<KR>(ts, tk, v, key);
+      }
     }
-    kth = __shfl(ls, k - 1);
-    kthk = __shfl(lk, k - 1);
-    m &= m - 1;
-    m &= __ballot(cand && better(sc, key, kth, kthk));
+    __builtin_amdgcn_wave_barrier();  // the owners have read sc before the next step rewrites it
+  }
+  if (owner) {
+    const size_t slot = (size_t)(it.qbeg + 32 * w + i32) * a.nparts + it.part;
+#pragma unroll
+    for (int j = 0; j < KR; ++j)
+      if (j < a.k) {
+        a.part_s[slot * a.k + j] = ts[j];
+        a.part_k[slot * a.k + j] = tk[j];
+      }
   }
 }
 
-template <int DW, int MET>  // DW: 32-bit code words per row (dp / 4)
-__global__ __launch_bounds__(256) void sq8_scan_kernel(Sq8Args a) {
-  __shared__ uint32_t qw[SQ8_QG][DW];
-  __shared__ int2 qsum[SQ8_QG];
-  __shared__ float mrs[SQ8_QG][4][64];
-  __shared__ uint32_t mrk[SQ8_QG][4][64];
-  if ((int)blockIdx.x >= *a.n_items) return;
-  const ScanItem it = a.items[blockIdx.x];
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, k = a.k;
-  const int swords = a.sl / 4;  // words of the int32-wrapped vector part
-  for (int e = tid; e < SQ8_QG * DW; e += 256) {
-    const int j = e / DW, d = e - j * DW;
-    qw[j][d] = j < it.qcnt ? reinterpret_cast<const uint32_t *>(a.qcodes + (size_t)(it.qbeg + j) * a.dp)[d] : 0u;
-  }
-  if (tid < SQ8_QG) qsum[tid] = tid < it.qcnt ? a.qsums[it.qbeg + tid] : make_int2(0, 0);
-  __syncthreads();
-
-  float ls[SQ8_QG], kth[SQ8_QG];
-  uint32_t lk[SQ8_QG], kthk[SQ8_QG];
-#pragma unroll
-  for (int j = 0; j < SQ8_QG; ++j) {
-    ls[j] = kth[j] = -INFINITY;
-    lk[j] = kthk[j] = KEY_NONE;
-  }
-  const int rb = it.row_begin, re = it.row_end;
-  for (int r0 = rb + 64 * w; r0 < re; r0 += 256) {
-    // the query words are re-read from LDS (broadcasts) per row group: hoisting all
-    // SQ8_QG x DW of them into registers would cost the occupancy
-    asm volatile("" ::: "memory");
-    const int r = r0 + lane;
-    const bool valid = r < re && (uint32_t)r < a.row_limit && a.live[r] && a.ok[r];
-    uint32_t rw[DW];
-    const uint4 *rp = reinterpret_cast<const uint4 *>(a.codes + (size_t)(valid ? r : rb) * a.dp);
-#pragma unroll
-    for (int c = 0; c < DW / 4; ++c) {
-      const uint4 v = rp[c];
-      rw[4 * c] = v.x;
-      rw[4 * c + 1] = v.y;
-      rw[4 * c + 2] = v.z;
-      rw[4 * c + 3] = v.w;
-    }
-    const int2 rs = a.sums[valid ? r : rb];
-#pragma unroll
-    for (int j = 0; j < SQ8_QG; ++j) {
-      uint32_t dv = 0, dt = 0;  // vector part (wraps like the int32 lanes), tail (exact)
-#pragma unroll
-      for (int d = 0; d < DW; ++d) {
-        if (d < swords) dv = __builtin_amdgcn_udot4(rw[d], qw[j][d], dv, false);
-        else dt = __builtin_amdgcn_udot4(rw[d], qw[j][d], dt, false);
-      }
-      int64_t tot;
-      if (MET == L2) {
-        const uint32_t vpart = (uint32_t)qsum[j].x + (uint32_t)rs.x - 2u * dv;
-        tot = (int64_t)(int32_t)vpart + ((int64_t)qsum[j].y + rs.y - 2 * (int64_t)dt);
-        tot = -tot;
-      } else {
-        tot = (int64_t)(int32_t)dv + (int64_t)dt;
-      }
-      const float score = (float)tot;  // long -> float, round to nearest (BruteForceVectorIndex.cs:325-331)
-      const bool cand = valid && j < it.qcnt && better(score, (uint32_t)r, kth[j], kthk[j]);
-      lane_list_insert(cand, score, (uint32_t)r, ls[j], lk[j], kth[j], kthk[j], k, lane);
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < SQ8_QG; ++j) {
-    if (lane < k) {
-      mrs[j][w][lane] = ls[j];
-      mrk[j][w][lane] = lk[j];
-    }
-  }
-  __syncthreads();
-  for (int j = w; j < it.qcnt; j += 4) {  // wave w merges queries w, w + 4, ...
-    float s = -INFINITY, kt = -INFINITY;
-    uint32_t kk = KEY_NONE, ktk = KEY_NONE;
-    for (int v = 0; v < 4; ++v) {
-      const float cs = lane < k ? mrs[j][v][lane] : -INFINITY;
-      const uint32_t ck = lane < k ? mrk[j][v][lane] : KEY_NONE;
-      const bool cand = ck != KEY_NONE && better(cs, ck, kt, ktk);
-      lane_list_insert(cand, cs, ck, s, kk, kt, ktk, k, lane);
-    }
-    if (lane < k) {
-      const size_t slot = (size_t)(it.qbeg + j) * a.nparts + it.part;
-      a.part_s[slot * k + lane] = s;
-      a.part_k[slot * k + lane] = kk;
-    }
-  }
+template <int NS, int MET>
+void launch_nk(const Sq8Args &a, int max_items, hipStream_t st) {
+  if (a.k <= 16) hipLaunchKernelGGL((sq8_mfma_kernel<NS, MET, 16>), dim3(max_items), dim3(256), 0, st, a);
+  else if (a.k <= 32) hipLaunchKernelGGL((sq8_mfma_kernel<NS, MET, 32>), dim3(max_items), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((sq8_mfma_kernel<NS, MET, 64>), dim3(max_items), dim3(256), 0, st, a);
 }
 
 }  // namespace
 
 void launch_sq8_quantize(const float *src, const int64_t *slots, int blocked, int64_t n, int32_t dim, int32_t dp,
-                         uint8_t *codes, int2 *sums, uint8_t *ok, hipStream_t st) {
+                         int shifted, uint8_t *codes, int2 *sums, uint8_t *ok, hipStream_t st) {
   if (n <= 0) return;
-  const int sl = dim >= 32 ? dim - dim % 32 : 0;
   hipLaunchKernelGGL(sq8_quantize_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, src, slots, blocked, n, dim,
-                     dp, sl, codes, sums, ok);
+                     dp, shifted, codes, sums, ok);
 }
 
-int sq8_dp(int dim) { return (dim + 15) / 16 * 16; }
-int sq8_qgroup() { return SQ8_QG; }
-bool sq8_supported(int dim, int k) { return k >= 1 && k <= 64 && sq8_dp(dim) <= 256; }
+int sq8_dp(int dim) { return (dim + 31) / 32 * 32; }
+int sq8_qgroup() { return 128; }
+bool sq8_supported(int dim, int k) { return k >= 1 && k <= 64 && dim >= 1 && dim <= 256; }
 
 void launch_sq8_scan(const Sq8Args &a, int metric, int max_items, hipStream_t st) {
   if (max_items <= 0) return;
-  const int dw = a.dp / 4;
-  Sq8Args b = a;
-  b.sl = a.dim >= 32 ? a.dim - a.dim % 32 : 0;
-#define SQ8_CASE(W)                                                                                       \
-  case W:                                                                                                 \
-    if (metric == L2) hipLaunchKernelGGL((sq8_scan_kernel<W, L2>), dim3(max_items), dim3(256), 0, st, b); \
-    else hipLaunchKernelGGL((sq8_scan_kernel<W, IP>), dim3(max_items), dim3(256), 0, st, b);              \
+  const bool l2 = metric == L2;
+  switch (a.dp / 32) {
+#define SQ8_CASE(N)                             \
+  case N:                                       \
+    if (l2) launch_nk<N, L2>(a, max_items, st); \
+    else launch_nk<N, IP>(a, max_items, st);    \
     break;
-  switch (dw) {
+    SQ8_CASE(1)
+    SQ8_CASE(2)
+    SQ8_CASE(3)
     SQ8_CASE(4)
+    SQ8_CASE(5)
+    SQ8_CASE(6)
+    SQ8_CASE(7)
     SQ8_CASE(8)
-    SQ8_CASE(12)
-    SQ8_CASE(16)
-    SQ8_CASE(20)
-    SQ8_CASE(24)
-    SQ8_CASE(28)
-    SQ8_CASE(32)
-    SQ8_CASE(36)
-    SQ8_CASE(40)
-    SQ8_CASE(44)
-    SQ8_CASE(48)
-    SQ8_CASE(52)
-    SQ8_CASE(56)
-    SQ8_CASE(60)
-    SQ8_CASE(64)
+#undef SQ8_CASE
     default: break;
   }
-#undef SQ8_CASE
 }
 
 }  // namespace pyr
