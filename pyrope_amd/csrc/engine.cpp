@@ -6,6 +6,8 @@
 // /root/reference/src/Pyrope.GarnetServer/.
 #include "engine.h"
 
+#include <cstdio>
+
 #include <algorithm>
 #include <cstring>
 #include <numeric>
@@ -1118,6 +1120,12 @@ struct IvfFlatIndex : Index {
     fa.gthr = gthr;
     fa.ablate = filter_ablate();
     fa.pub_mask = filter_pub_mask();
+    DevMem dbg;
+    if (getenv("PYR_FILTER_DEBUG")) {  // measurement only: insert statistics to stderr
+      dbg.ensure(16);
+      HIPCHK(hipMemsetAsync(dbg.p, 0, 16, ws.st));
+      fa.dbg = dbg.as<uint32_t>();
+    }
     {
       PhaseTimer t(PH_LIST_SCAN, ws.st, prof().on ? probed_rows(ws, nq, probes, le, lb) : 0);
       launch_filter(fa, metric, maxi, ws.st);
@@ -1126,6 +1134,12 @@ struct IvfFlatIndex : Index {
         fa.n_items = ws.nitems3.as<int32_t>();
         launch_filter(fa, metric, maxi_main, ws.st);
       }
+    }
+    if (fa.dbg) {
+      uint32_t h[4] = {0, 0, 0, 0};
+      HIPCHK(hipMemcpyAsync(h, dbg.p, 12, hipMemcpyDeviceToHost, ws.st));
+      HIPCHK(hipStreamSynchronize(ws.st));
+      fprintf(stderr, "[filter] wave insert-loop iterations %u, candidates %u, owner stages %u\n", h[0], h[1], h[2]);
     }
     MergeIvf mi;
     mi.probes = ws.probes.as<int32_t>();

@@ -237,6 +237,14 @@ __global__ __launch_bounds__(256, 2) void mfma_filter(FilterArgs a) {
         if (pass == 0x12345u) ts[0] = lo;
         pass = 0;
       }
+      if (a.dbg) {  // measurement only
+        const uint32_t np = __popc(pass);
+        atomicAdd(a.dbg + 1, np);
+        atomicAdd(a.dbg + 2, 1u);
+        uint32_t mx = np;
+        for (int o = 16; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 32));
+        if (i32 == 0) atomicAdd(a.dbg, mx);
+      }
       while (pass) {
         const int j = __builtin_ctz(pass);
         pass &= pass - 1;

@@ -230,6 +230,8 @@ struct FilterArgs {
                            // 1 skip the owner filter, 2 skip the score transpose, 4 skip row loads, 8 skip MFMA,
                            // 16 filter without inserting
   int32_t pub_mask;        // publish / refresh the shared bound when (stage & pub_mask) == pub_mask
+  uint32_t *dbg;           // measurement only (PYR_FILTER_DEBUG): [0] insert-loop iterations of
+                           // all waves, [1] candidates inserted, [2] owner stages, or null
 };
 struct RefineArgs {
   const float *rows;        // blocked store the keys index
