@@ -138,9 +138,10 @@ struct IvfItemWs {
 // ch.warm == 0), phase 1 = chunks >= 1 (only with ch.warm > 0).  Phase 0 also builds
 // the per-list query lists (ws.cnt/qoff/qlist) that phase 1 reuses.
 int64_t ivf_max_items(int64_t nq, int32_t nprobe, int32_t nlist, int32_t qchunk, IvfChunking ch, int phase);
+// [pb, pe): the probe ranks taken (pe < 0: all); partial slots keep the absolute rank.
 void launch_ivf_items(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t nparts, int32_t nlist,
                       const int32_t *list_begin, const int32_t *list_end, int32_t qchunk, IvfChunking ch,
-                      int phase, IvfItemWs &ws, hipStream_t st);
+                      int phase, IvfItemWs &ws, hipStream_t st, int32_t pb = 0, int32_t pe = -1);
 // IVF max_scans limits per (query, probe, chunk) slot (IvfFlatVectorIndex.cs:200-212)
 void launch_ivf_limits(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t nparts, int64_t remaining,
                        const int32_t *list_begin, const int32_t *list_end, const int32_t *list_live,

@@ -757,9 +757,11 @@ __global__ __launch_bounds__(256) void merge_labels_kernel(const float *ps, cons
 // ---------------------------------------------------------------------------
 // IVF list-major work lists
 // ---------------------------------------------------------------------------
-__global__ void ivf_count_kernel(const int32_t *probes, int64_t n, int32_t *cnt) {
+// probes [nq][nprobe]; only probe ranks [pb, pe) of every query take part
+__global__ void ivf_count_kernel(const int32_t *probes, int64_t nq, int nprobe, int pb, int pe, int32_t *cnt) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) atomicAdd(&cnt[probes[i]], 1);
+  const int np = pe - pb;
+  if (i < nq * np) atomicAdd(&cnt[probes[(i / np) * nprobe + pb + i % np]], 1);
 }
 
 // chunks of list `lst` that launch phase `phase` scans (IvfChunking, kernels.h)
@@ -807,13 +809,14 @@ __global__ __launch_bounds__(1024) void ivf_scan_kernel(const int32_t *cnt, int 
   }
 }
 
-__global__ void ivf_fill_kernel(const int32_t *probes, int64_t nq, int nprobe, int nparts, int cmax,
+__global__ void ivf_fill_kernel(const int32_t *probes, int64_t nq, int nprobe, int pb, int pe, int nparts, int cmax,
                                 const int32_t *qoff, int32_t *fill, int32_t *qlist) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nq * nprobe) return;
-  const int64_t q = i / nprobe;
-  const int p = (int)(i % nprobe);
-  const int lst = probes[i];
+  const int np = pe - pb;
+  if (i >= nq * np) return;
+  const int64_t q = i / np;
+  const int p = pb + (int)(i % np);
+  const int lst = probes[q * nprobe + p];
   const int pos = atomicAdd(&fill[lst], 1);
   qlist[qoff[lst] + pos] = (int32_t)(q * nparts + p * cmax);  // chunk c adds c (ScanItem.part)
 }
@@ -1573,18 +1576,20 @@ int64_t ivf_max_items(int64_t nq, int32_t nprobe, int32_t nlist, int32_t qchunk,
 
 void launch_ivf_items(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t nparts, int32_t nlist,
                       const int32_t *list_begin, const int32_t *list_end, int32_t qchunk, IvfChunking ch,
-                      int phase, IvfItemWs &ws, hipStream_t st) {
-  const int64_t n = nq * nprobe;
+                      int phase, IvfItemWs &ws, hipStream_t st, int32_t pb, int32_t pe) {
+  if (pe < 0) pe = nprobe;
+  const int64_t n = nq * (pe - pb);
   if (phase == 0) {
     (void)hipMemsetAsync(ws.cnt, 0, sizeof(int32_t) * nlist, st);
     (void)hipMemsetAsync(ws.fill, 0, sizeof(int32_t) * nlist, st);
-    if (n > 0) hipLaunchKernelGGL(ivf_count_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, probes, n, ws.cnt);
+    if (n > 0)
+      hipLaunchKernelGGL(ivf_count_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, probes, nq, nprobe, pb, pe, ws.cnt);
   }
   hipLaunchKernelGGL(ivf_scan_kernel, dim3(1), dim3(1024), 0, st, ws.cnt, nlist, qchunk, list_begin, list_end, ch,
                      phase, ws.qoff, ws.ioff, ws.n_items);
   if (phase == 0 && n > 0)
-    hipLaunchKernelGGL(ivf_fill_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, probes, nq, nprobe, nparts, ch.cmax,
-                       ws.qoff, ws.fill, ws.qlist);
+    hipLaunchKernelGGL(ivf_fill_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, probes, nq, nprobe, pb, pe, nparts,
+                       ch.cmax, ws.qoff, ws.fill, ws.qlist);
   hipLaunchKernelGGL(ivf_items_kernel, dim3(nblk(nlist, 256)), dim3(256), 0, st, ws.cnt, ws.qoff, ws.ioff, nlist,
                      list_begin, list_end, qchunk, ch, phase, ws.items);
 }
