@@ -101,12 +101,25 @@ def main():
     opts = SearchOptions(nprobe=args.nprobe)
     result = [s_loc, l_loc]
 
+    # N > 1: the coarse ranking is split too -- rank r ranks the quantizer for its own nq-query
+    # slice of the batch and one all_gather assembles every query's probe lists -- so per-GPU
+    # work stays fixed as N grows (every rank would otherwise rank the whole N x nq batch)
+    pr_loc = torch.empty((args.nq, args.nprobe), dtype=torch.int32, device=dev)
+    pr_all = torch.empty((Q, args.nprobe), dtype=torch.int32, device=dev)
+
     def step():
         stream = torch.cuda.current_stream().cuda_stream
-        idx.search_device(q.data_ptr(), Q, k, s_loc.data_ptr(), l_loc.data_ptr(), 0, stream, opts)
-        if world > 1:  # RCCL all_gather over xGMI of per-GPU partial top-k, then on-device merge
-            sp, lp = gather_partials(s_loc, l_loc, world)
-            result[:] = merge_device(sp, lp, k, stream)
+        if world == 1:
+            idx.search_device(q.data_ptr(), Q, k, s_loc.data_ptr(), l_loc.data_ptr(), 0, stream, opts)
+            return
+        q_mine = q[rank * args.nq:(rank + 1) * args.nq]
+        width = idx.probe_device(q_mine.data_ptr(), args.nq, pr_loc.data_ptr(), stream, opts)
+        dist.all_gather_into_tensor(pr_all, pr_loc)
+        idx.search_device(q.data_ptr(), Q, k, s_loc.data_ptr(), l_loc.data_ptr(), 0, stream, opts,
+                          d_probes=pr_all.data_ptr(), nprobe=width)
+        # RCCL all_gather over xGMI of per-GPU partial top-k, then on-device merge
+        sp, lp = gather_partials(s_loc, l_loc, world)
+        result[:] = merge_device(sp, lp, k, stream)
 
     def barrier():
         if world > 1:

@@ -109,6 +109,19 @@ pyr_status pyr_index_search_device(pyr_index *index, const float *d_q, int64_t n
                                    const pyr_search_params *params, float *d_scores, int64_t *d_labels,
                                    int32_t *d_counts, void *stream);
 
+/* Multi-GPU split of the coarse step (DESIGN.md "Multi-GPU"): every rank ranks the coarse quantizer
+ * (IvfFlatVectorIndex.cs:186-198) for its slice of the batch, the probe lists are all-gathered, and
+ * every rank searches its shard with the gathered lists.  IVF_FLAT only.
+ * pyr_index_probe_device: d_probes = nq x P device int32 list ids in rank order, P = min(nprobe, nlist)
+ *   (nprobe < 0 -> index default), written to *probes_out (may be NULL).
+ * pyr_index_search_probed_device: pyr_index_search_device with those lists instead of the coarse
+ *   step; nprobe = their width, which must equal what params select. */
+pyr_status pyr_index_probe_device(pyr_index *index, const float *d_q, int64_t nq, int32_t nprobe, int32_t *d_probes,
+                                  int32_t *probes_out, void *stream);
+pyr_status pyr_index_search_probed_device(pyr_index *index, const float *d_q, int64_t nq, int32_t k,
+                                          const pyr_search_params *params, const int32_t *d_probes, int32_t nprobe,
+                                          float *d_scores, int64_t *d_labels, int32_t *d_counts, void *stream);
+
 /* IVectorIndex.GetStats (IVectorIndex.cs:28): Count with the reference's semantics
  * (IvfFlat counts buffer + list rows, IvfFlatVectorIndex.cs:305; IvfPq reports 0, IvfPqVectorIndex.cs:230). */
 pyr_status pyr_index_stats(const pyr_index *index, int64_t *count, int32_t *dim, int32_t *metric);

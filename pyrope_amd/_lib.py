@@ -81,6 +81,9 @@ SIGNATURES = {
     "pyr_index_pq_state": (C.c_int, [_vp, _f, _i32, _u8]),
     "pyr_index_scan": (C.c_int, [_vp, _i64, _f, _i64]),
     "pyr_index_set_quantization": (C.c_int, [_vp, C.c_int32]),
+    "pyr_index_probe_device": (C.c_int, [_vp, _vp, C.c_int64, C.c_int32, _vp, C.POINTER(C.c_int32), _vp]),
+    "pyr_index_search_probed_device": (C.c_int, [_vp, _vp, C.c_int64, C.c_int32, C.POINTER(SearchParams), _vp,
+                                                 C.c_int32, _vp, _vp, _vp, _vp]),
     "pyr_scalar_quantize": (C.c_int, [C.c_int32, _f, C.c_int64, C.c_int32, _u8]),
     "pyr_merge_topk_device": (C.c_int, [_vp, _vp, C.c_int64, C.c_int32, C.c_int32, _vp, _vp, _vp]),
     "pyr_generate_synthetic": (C.c_int, [C.c_int64, C.c_int32, C.c_int32, _f]),

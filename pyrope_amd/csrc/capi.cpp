@@ -222,6 +222,45 @@ pyr_status pyr_index_search_device(pyr_index *index, const float *d_q, int64_t n
   });
 }
 
+pyr_status pyr_index_probe_device(pyr_index *index, const float *d_q, int64_t nq, int32_t nprobe, int32_t *d_probes,
+                                  int32_t *probes_out, void *stream) {
+  if (!index || nq < 0 || (nq > 0 && (!d_q || !d_probes))) return fail(PYR_E_ARG, "null argument");
+  return guard([&] {
+    pyr::Index &ix = *index->impl;
+    HIPCHK(hipSetDevice(ix.device));
+    std::shared_lock<std::shared_mutex> g(ix.mu);
+    pyr::Workspace &ws = ix.ws_for_stream(reinterpret_cast<hipStream_t>(stream));
+    std::lock_guard<std::mutex> wg(ws.m);
+    const int p = ix.probe_only(d_q, nq, nprobe, d_probes, ws);
+    if (probes_out) *probes_out = p;
+    HIPCHK(hipGetLastError());
+  });
+}
+
+pyr_status pyr_index_search_probed_device(pyr_index *index, const float *d_q, int64_t nq, int32_t k,
+                                          const pyr_search_params *params, const int32_t *d_probes, int32_t nprobe,
+                                          float *d_scores, int64_t *d_labels, int32_t *d_counts, void *stream) {
+  if (!index || nq < 0 || (nq > 0 && (!d_q || !d_probes))) return fail(PYR_E_ARG, "null argument");
+  if (k > pyr::KMAX) return fail(PYR_E_ARG, "topK larger than 256 is not supported");
+  return guard([&] {
+    pyr::Index &ix = *index->impl;
+    HIPCHK(hipSetDevice(ix.device));
+    std::shared_lock<std::shared_mutex> g(ix.mu);
+    pyr::Workspace &ws = ix.ws_for_stream(reinterpret_cast<hipStream_t>(stream));
+    std::lock_guard<std::mutex> wg(ws.m);
+    ws.ext_probes = d_probes;
+    ws.ext_nprobe = nprobe;
+    try {
+      ix.search(d_q, nq, k, defaults(params), d_scores, d_labels, d_counts, ws);
+    } catch (...) {
+      ws.ext_probes = nullptr;
+      throw;
+    }
+    ws.ext_probes = nullptr;
+    HIPCHK(hipGetLastError());
+  });
+}
+
 pyr_status pyr_index_stats(const pyr_index *index, int64_t *count, int32_t *dim, int32_t *metric) {
   if (!index) return fail(PYR_E_ARG, "null argument");
   return guard([&] {

@@ -782,6 +782,13 @@ struct Coarse {
   // score all centroids (ComputeScore, safe VectorMath), rank desc (ties by index), keep nprobe
   // IvfFlatVectorIndex.cs:186-198, IvfPqVectorIndex.cs:141-150
   void probe(const float *d_q, const float *d_qn, int64_t nq, int nprobe, int met, Workspace &ws) {
+    if (ws.ext_probes) {  // ranked by the caller (pyr_index_search_probed_device)
+      if (ws.ext_nprobe != nprobe) throw Error(PYR_E_ARG, "probe lists have the wrong width for this nprobe");
+      ws.probes.ensure(sizeof(int32_t) * nq * nprobe);
+      HIPCHK(hipMemcpyAsync(ws.probes.p, ws.ext_probes, sizeof(int32_t) * nq * nprobe, hipMemcpyDeviceToDevice,
+                            ws.st));
+      return;
+    }
     const int qchunk = fast_path(cs.dim, nprobe) ? QCHUNK : QCHUNK_GENERIC;
     const int64_t nqc = (nq + qchunk - 1) / qchunk;
     int want = (int)std::max<int64_t>(1, std::min<int64_t>(16, (2048 + nqc - 1) / nqc));
@@ -1197,6 +1204,16 @@ struct IvfFlatIndex : Index {
                     [&](const float *q2, int64_t n2, float *s2, int64_t *l2, int32_t *c2) {
                       search_exact(q2, n2, k, ex, s2, l2, c2, ws);
                     });
+  }
+
+  int probe_only(const float *d_q, int64_t nq, int nprobe, int32_t *d_out, Workspace &ws) override {
+    if (!built || coarse.nlist <= 0) throw Error(PYR_E_STATE, "index is not built");
+    const int probes = std::max(0, std::min(nprobe < 0 ? nprobe_default : nprobe, coarse.nlist));
+    if (probes == 0 || nq == 0) return probes;
+    prep_queries(d_q, nq, dim, metric, ws);
+    coarse.probe(d_q, metric == COS ? ws.qn.as<float>() : nullptr, nq, probes, metric, ws);
+    HIPCHK(hipMemcpyAsync(d_out, ws.probes.p, sizeof(int32_t) * nq * probes, hipMemcpyDeviceToDevice, ws.st));
+    return probes;
   }
 
   // IvfFlatVectorIndex.Search (:147-231) with the list scan on the VALU, the reference's exact arithmetic

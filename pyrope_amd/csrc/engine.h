@@ -90,6 +90,8 @@ struct Workspace {
   DevMem out_s, out_l, out_c;
   DevMem ms, mk, fail, fail_cnt, fq, fs, fl, fc;  // MFMA filter: merged candidates, certificate failures
   DevMem q8q, q8qs;                               // 8-bit search mode: quantized queries, their sums
+  const int32_t *ext_probes = nullptr;            // caller-ranked probe lists [nq][ext_nprobe] (multi-GPU)
+  int32_t ext_nprobe = 0;
   ~Workspace() {
     if (own_stream && st) (void)hipStreamDestroy(st);
   }
@@ -126,6 +128,15 @@ struct Index {
     (void)x;
     (void)n;
     throw Error(PYR_E_STATE, "index kind has no Scan (BruteForceVectorIndex only)");
+  }
+  // IVF kinds: the coarse ranking alone (probe lists [nq][min(nprobe, nlist)]) into d_out
+  virtual int probe_only(const float *d_q, int64_t nq, int nprobe, int32_t *d_out, Workspace &ws) {
+    (void)d_q;
+    (void)nq;
+    (void)nprobe;
+    (void)d_out;
+    (void)ws;
+    throw Error(PYR_E_STATE, "index kind has no coarse quantizer");
   }
   // BruteForceVectorIndex.EnableQuantization (BruteForceVectorIndex.cs:25-40)
   virtual void set_quantization(bool on) {

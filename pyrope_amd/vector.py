@@ -206,12 +206,29 @@ class HipVectorIndex(IVectorIndex):
         return [SearchResult(self._id_of[int(lab[0, j])], float(s[0, j])) for j in range(int(cnt[0]))]
 
     def search_device(self, d_q: int, nq: int, top_k: int, d_scores: int, d_labels: int, d_counts: int = 0,
-                      stream: int = 0, options: Optional[SearchOptions] = None) -> None:
-        """Search on device-resident buffers (raw device pointers, e.g. torch tensor.data_ptr())."""
+                      stream: int = 0, options: Optional[SearchOptions] = None, d_probes: int = 0,
+                      nprobe: int = 0) -> None:
+        """Search on device-resident buffers (raw device pointers, e.g. torch tensor.data_ptr()).
+        d_probes / nprobe: caller-ranked probe lists (pyr_index_search_probed_device)."""
         p = self._params(options)
+        if d_probes:
+            check(self._L.pyr_index_search_probed_device(self._h, C.c_void_p(d_q), nq, int(top_k), C.byref(p),
+                                                         C.c_void_p(d_probes), int(nprobe), C.c_void_p(d_scores),
+                                                         C.c_void_p(d_labels), C.c_void_p(d_counts or None),
+                                                         C.c_void_p(stream or None)))
+            return
         check(self._L.pyr_index_search_device(self._h, C.c_void_p(d_q), nq, int(top_k), C.byref(p),
                                               C.c_void_p(d_scores), C.c_void_p(d_labels),
                                               C.c_void_p(d_counts or None), C.c_void_p(stream or None)))
+
+    def probe_device(self, d_q: int, nq: int, d_probes: int, stream: int = 0,
+                     options: Optional[SearchOptions] = None) -> int:
+        """Coarse ranking only (pyr_index_probe_device): probe lists [nq][P] at d_probes; returns P."""
+        p = self._params(options)
+        out = C.c_int32()
+        check(self._L.pyr_index_probe_device(self._h, C.c_void_p(d_q), nq, int(p.nprobe), C.c_void_p(d_probes),
+                                             C.byref(out), C.c_void_p(stream or None)))
+        return out.value
 
     def set_centroids(self, centroids: np.ndarray) -> None:
         """Supply the coarse quantizer used by the next build() (pyr_index_set_centroids)."""

@@ -136,3 +136,34 @@ def test_gpu_two_shards_merge_equals_unsharded(hiplib):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(l_out.cpu().numpy(), ref_l)
     assert np.array_equal(s_out.cpu().numpy().view(np.uint32), ref_s.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_gpu_split_coarse_ranking_equals_search(hiplib):
+    """bench.py's N > 1 step: each rank ranks the quantizer for its slice of the batch and the
+    gathered probe lists feed pyr_index_search_probed_device; same results as the plain search."""
+    import torch
+
+    from pyrope_amd import IvfFlatVectorIndex, SearchOptions, generate_synthetic
+
+    n, d, nl, npb = 20000, 128, 64, 8
+    data = generate_synthetic(n, d, 42)
+    qh = generate_synthetic(300, d, 1337)
+    idx = IvfFlatVectorIndex(d, 0, n_list=nl)
+    idx.add_labels(np.arange(n, dtype=np.int64), data)
+    idx.build()
+    opts = SearchOptions(nprobe=npb)
+    ref_s, ref_l, _ = idx.search_batch(qh, K, opts)
+    q = torch.from_numpy(qh).cuda()
+    probes = torch.empty((300, npb), dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    for a, b in [(0, 150), (150, 300)]:  # two "ranks"
+        w = idx.probe_device(q[a:b].data_ptr(), b - a, probes[a:b].data_ptr(), stream, opts)
+        assert w == npb
+    s = torch.empty((300, K), dtype=torch.float32, device="cuda")
+    lab = torch.empty((300, K), dtype=torch.int64, device="cuda")
+    idx.search_device(q.data_ptr(), 300, K, s.data_ptr(), lab.data_ptr(), 0, stream, opts,
+                      d_probes=probes.data_ptr(), nprobe=npb)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(lab.cpu().numpy(), ref_l)
+    assert np.array_equal(s.cpu().numpy().view(np.uint32), ref_s.view(np.uint32))
