@@ -1,0 +1,192 @@
+// coarse.hip -- the IVF coarse step as a dense score matrix + per-query selection (gfx950).
+//
+// IvfFlatVectorIndex.Search (:186-198) and IvfPqVectorIndex.Search (:141-150) score every
+// centroid with ComputeScore (the safe VectorMath forms: one 8-lane accumulator, horizontal
+// tree, then the scalar tail) and keep the first nprobe of the descending sort.  With nlist of
+// ~1k the top-k-insertion scan of kernels.hip spends its time inserting (nprobe of every
+// chunk's few dozen centroids enter the lists), so here the step is split:
+//   coarse_scores_kernel  every (query, centroid) score, exact reference order, 32 x 32 tiles
+//                         from LDS, 2 x 2 pairs per thread (8-lane accumulators each);
+//   coarse_select_kernel  one wave per query: the row in LDS, nprobe rounds of a wave-wide
+//                         argmax by (score desc, centroid asc), i.e. the same ranking.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <algorithm>
+#include <cmath>
+
+#include "kernels.h"
+
+namespace pyr {
+namespace {
+
+constexpr int CT = 32;  // queries / centroids per tile
+
+__device__ __forceinline__ float hsum8(const float *v) {
+  float lo = (v[0] + v[1]) + (v[2] + v[3]);
+  float hi = (v[4] + v[5]) + (v[6] + v[7]);
+  return lo + hi;
+}
+
+// out[q][c] = ComputeScore(query q, centroid c).  Block: CT queries x CT centroids, 256
+// threads, thread (ty, tx) -> queries 2ty, 2ty+1 x centroids 2tx, 2tx+1.  Dimensions stream
+// through LDS KT at a time (KT % 8 == 0), so the 8-lane accumulation order is unchanged.
+constexpr int KT = 128;
+constexpr int KTP = KT + 1;  // odd row stride: the 16 threads of a row read different banks
+
+template <int MET>
+__global__ __launch_bounds__(256) void coarse_scores_kernel(const float *q, const float *c, const float *qn,
+                                                            const float *cn, int64_t nq, int nc, int D, float *out) {
+  __shared__ float qs[CT * KTP], cs[CT * KTP];
+  const int64_t q0 = (int64_t)blockIdx.y * CT;
+  const int c0 = blockIdx.x * CT;
+  const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+  const float *qa = qs + (2 * ty) * KTP, *qb = qa + KTP;
+  const float *ca = cs + (2 * tx) * KTP, *cb = ca + KTP;
+  float acc[4][8];
+#pragma unroll
+  for (int p = 0; p < 4; ++p)
+#pragma unroll
+    for (int l = 0; l < 8; ++l) acc[p][l] = 0.0f;
+  const int D8 = D & ~7;
+  float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (int d0 = 0; d0 < D; d0 += KT) {
+    const int kt = min(KT, D - d0);
+    __syncthreads();  // the previous tile is consumed
+    for (int e = tid; e < CT * kt; e += 256) {
+      const int r = e / kt, d = e - r * kt;
+      qs[r * KTP + d] = q0 + r < nq ? q[(size_t)(q0 + r) * D + d0 + d] : 0.0f;
+      cs[r * KTP + d] = c0 + r < nc ? c[(size_t)(c0 + r) * D + d0 + d] : 0.0f;
+    }
+    __syncthreads();
+    const int g8 = min(kt, D8 - d0);  // full 8-groups of this tile
+    for (int i = 0; i < g8; i += 8) {  // VectorMath.cs:8-70, one Vector accumulator
+#pragma unroll
+      for (int l = 0; l < 8; ++l) {
+        const float x0 = qa[i + l], x1 = qb[i + l], y0 = ca[i + l], y1 = cb[i + l];
+        if (MET == L2) {
+          const float d00 = x0 - y0, d01 = x0 - y1, d10 = x1 - y0, d11 = x1 - y1;
+          acc[0][l] = acc[0][l] + d00 * d00;
+          acc[1][l] = acc[1][l] + d01 * d01;
+          acc[2][l] = acc[2][l] + d10 * d10;
+          acc[3][l] = acc[3][l] + d11 * d11;
+        } else {
+          acc[0][l] = acc[0][l] + x0 * y0;
+          acc[1][l] = acc[1][l] + x0 * y1;
+          acc[2][l] = acc[2][l] + x1 * y0;
+          acc[3][l] = acc[3][l] + x1 * y1;
+        }
+      }
+    }
+    if (d0 + kt >= D) {  // last tile: horizontal sums, then the scalar tail (it lies in this tile)
+#pragma unroll
+      for (int p = 0; p < 4; ++p) s[p] = D8 > 0 ? 0.0f + hsum8(acc[p]) : 0.0f;
+      for (int i = D8 - d0; i < kt; ++i) {
+        const float x0 = qa[i], x1 = qb[i], y0 = ca[i], y1 = cb[i];
+        if (MET == L2) {
+          const float d00 = x0 - y0, d01 = x0 - y1, d10 = x1 - y0, d11 = x1 - y1;
+          s[0] = s[0] + d00 * d00;
+          s[1] = s[1] + d01 * d01;
+          s[2] = s[2] + d10 * d10;
+          s[3] = s[3] + d11 * d11;
+        } else {
+          s[0] = s[0] + x0 * y0;
+          s[1] = s[1] + x0 * y1;
+          s[2] = s[2] + x1 * y0;
+          s[3] = s[3] + x1 * y1;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int64_t qi = q0 + 2 * ty + (p >> 1);
+    const int ci = c0 + 2 * tx + (p & 1);
+    if (qi >= nq || ci >= nc) continue;
+    float v;
+    if (MET == L2) v = -s[p];
+    else if (MET == IP) v = s[p];
+    else {  // Cosine (VectorMath.cs:102-109): 0 when either norm < 1e-6
+      const float a = qn[qi], b = cn[ci];
+      v = (a < 1e-6f || b < 1e-6f) ? 0.0f : s[p] / (a * b);
+    }
+    out[qi * nc + ci] = v;
+  }
+}
+
+// order-preserving 64-bit key: higher = better (score desc, centroid asc)
+__device__ __forceinline__ uint64_t rank_key(float s, int c) {
+  return ((uint64_t)score_key(s) << 32) | (uint32_t)(0x7FFFFFFF - c);
+}
+
+__global__ __launch_bounds__(256) void coarse_select_kernel(const float *scores, int64_t nq, int nc, int nprobe,
+                                                            int wpb, int32_t *probes) {
+  extern __shared__ float sm[];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.x * wpb + w;
+  if (q >= nq) return;  // no block barrier below
+  uint64_t *row = reinterpret_cast<uint64_t *>(sm) + (size_t)w * nc;
+  for (int c = lane; c < nc; c += 64) row[c] = rank_key(scores[q * nc + c], c);
+  __builtin_amdgcn_wave_barrier();
+  for (int p = 0; p < nprobe; ++p) {
+    uint64_t best = 0;
+    int bi = -1;
+    for (int c = lane; c < nc; c += 64) {
+      const uint64_t v = row[c];
+      if (v > best) {
+        best = v;
+        bi = c;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const uint64_t ov = __shfl_xor(best, o);
+      const int oi = __shfl_xor(bi, o);
+      if (ov > best) {
+        best = ov;
+        bi = oi;
+      }
+    }
+    if (lane == 0) {
+      probes[q * nprobe + p] = bi;
+      row[bi] = 0;  // taken (every real key is > 0)
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+}  // namespace
+
+// waves (queries) per selection block: the rows of all of them must fit in LDS
+static int select_wpb(int nlist) {
+  const int64_t row = (int64_t)nlist * sizeof(uint64_t);
+  return (int)std::max<int64_t>(0, std::min<int64_t>(4, (160 * 1024) / row));
+}
+bool coarse_dense_supported(int nlist) { return nlist >= 1 && select_wpb(nlist) >= 1; }
+
+void launch_coarse_dense(const float *q, const float *cents_rm, const float *qn, const float *cn, int64_t nq,
+                         int32_t nlist, int32_t dim, int32_t metric, int32_t nprobe, float *scores, int32_t *probes,
+                         hipStream_t st) {
+  if (nq <= 0 || nlist <= 0 || nprobe <= 0) return;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&coarse_select_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  const dim3 grid((unsigned)((nlist + CT - 1) / CT), (unsigned)((nq + CT - 1) / CT));
+  if (metric == L2)
+    hipLaunchKernelGGL(coarse_scores_kernel<L2>, grid, dim3(256), 0, st, q, cents_rm, qn, cn, nq, nlist, dim, scores);
+  else if (metric == IP)
+    hipLaunchKernelGGL(coarse_scores_kernel<IP>, grid, dim3(256), 0, st, q, cents_rm, qn, cn, nq, nlist, dim, scores);
+  else
+    hipLaunchKernelGGL(coarse_scores_kernel<COS>, grid, dim3(256), 0, st, q, cents_rm, qn, cn, nq, nlist, dim,
+                       scores);
+  const int wpb = select_wpb(nlist);
+  hipLaunchKernelGGL(coarse_select_kernel, dim3((unsigned)((nq + wpb - 1) / wpb)), dim3(64 * wpb),
+                     (size_t)wpb * nlist * sizeof(uint64_t), st, scores, nq, nlist, nprobe, wpb, probes);
+}
+
+}  // namespace pyr

@@ -789,10 +789,25 @@ struct Coarse {
                             ws.st));
       return;
     }
+    const char *ce = getenv("PYR_COARSE_DENSE");  // 0: the top-k scan below (A/B only, same ranking)
+    if (!(ce && atoi(ce) == 0) && coarse_dense_supported(nlist)) {
+      ws.probes.ensure(sizeof(int32_t) * nq * nprobe);
+      // <= 256 MB of scores and <= 2^21 queries (grid.y) per launch
+      const int64_t qb = std::max<int64_t>(1, std::min<int64_t>(int64_t(1) << 21, (int64_t(1) << 26) / nlist));
+      ws.cpart_s.ensure(sizeof(float) * (size_t)std::min<int64_t>(nq, qb) * nlist);
+      for (int64_t a = 0; a < nq; a += qb) {
+        const int64_t n = std::min<int64_t>(qb, nq - a);
+        launch_coarse_dense(d_q + a * cs.dim, rm.as<float>(), d_qn ? d_qn + a : nullptr,
+                            met == COS ? cs.norms.as<float>() : nullptr, n, nlist, cs.dim, met, nprobe,
+                            ws.cpart_s.as<float>(), ws.probes.as<int32_t>() + a * nprobe, ws.st);
+      }
+      return;
+    }
     const int qchunk = fast_path(cs.dim, nprobe) ? QCHUNK : QCHUNK_GENERIC;
     const int64_t nqc = (nq + qchunk - 1) / qchunk;
     int want = (int)std::max<int64_t>(1, std::min<int64_t>(16, (2048 + nqc - 1) / nqc));
     want = std::min(want, std::max(1, nlist / 32));
+    if (const char *e = getenv("PYR_COARSE_CHUNKS")) want = std::max(1, std::min(atoi(e), nlist));  // measurement
     ScanPlan p;
     p.qchunk = qchunk;
     p.chunk_rows = (int)round_up((nlist + want - 1) / want, 8);

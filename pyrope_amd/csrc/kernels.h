@@ -187,6 +187,14 @@ void launch_extract_sub(const float *x, int64_t n, int32_t dim, int32_t off, int
 void launch_pack_codes(const uint8_t *codes, const int64_t *src_of_dst, int64_t ndst, int32_t M, uint8_t *out,
                        hipStream_t st);
 
+// ---- IVF coarse step as dense scores + selection (coarse.hip) ----
+bool coarse_dense_supported(int nlist);
+// probes [nq][nprobe] = the first nprobe centroids by (ComputeScore desc, index asc);
+// scores: nq x nlist scratch.  qn / cn: query / centroid norms (cosine only).
+void launch_coarse_dense(const float *q, const float *cents_rm, const float *qn, const float *cn, int64_t nq,
+                         int32_t nlist, int32_t dim, int32_t metric, int32_t nprobe, float *scores, int32_t *probes,
+                         hipStream_t st);
+
 // ---- 8-bit search mode of the FLAT index (sq8.hip; BruteForceVectorIndex EnableQuantization) ----
 struct Sq8Args {
   const uint8_t *codes;    // [slot][dp] ScalarQuantizer codes - 128 (int8), zero padded
