@@ -140,7 +140,7 @@ pyr_status pyr_index_scan(pyr_index *index, int64_t *labels, float *x, int64_t *
  * rows added / upserted while it is on carry ScalarQuantizer codes, and searches run in the
  * 8-bit mode (:296-336): the query is quantized, scores are -L2Squared8Bit / DotProduct8Bit
  * (cosine too) as float, rows written while it was off count as scanned but are skipped.
- * Scores come from exact int8 MFMA sums; supported for dim <= 256 and topK <= 64 (PYR_E_ARG
+ * Scores come from exact int8 MFMA sums; supported for dim <= 512 and topK <= 64 (PYR_E_ARG
  * otherwise). */
 pyr_status pyr_index_set_quantization(pyr_index *index, int32_t enable);
 

@@ -510,7 +510,7 @@ struct FlatIndex : Index {
   // exact integer scores over slots [0, cutoff) that have codes
   void search_sq8(const float *d_q, int64_t nq, int k, int64_t cutoff, float *d_s, int64_t *d_l, int32_t *d_c,
                   Workspace &ws) {
-    if (!sq8_supported(dim, k)) throw Error(PYR_E_ARG, "quantized search supports dim <= 256 and topK <= 64");
+    if (!sq8_supported(dim, k)) throw Error(PYR_E_ARG, "quantized search supports dim <= 512 and topK <= 64");
     // exact int8 MFMA scores (sq8.hip); items of 128 queries x 8192-row chunks
     ws.q8q.ensure((size_t)dp * nq);
     ws.q8qs.ensure(sizeof(int2) * nq);

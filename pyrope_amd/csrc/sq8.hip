@@ -13,7 +13,7 @@
 //     sum(a b)     = sum(a' b') + 128 (A + B) - 16384 n
 //     sum((a-b)^2) = sum(a^2) + sum(b^2) - 2 sum(a b)
 // all exact in 64-bit integers.  (The reference's x64 SIMD path sums in wrapping int32 lanes;
-// no wrap is possible at the supported dims, n <= 256: |sum| <= 256 * 255^2 < 2^31.)
+// no wrap is possible at the supported dims, n <= 512: |sum| <= 512 * 255^2 < 2^31.)
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
@@ -237,9 +237,14 @@ void launch_sq8_quantize(const float *src, const int64_t *slots, int blocked, in
                      dp, shifted, codes, sums, ok);
 }
 
-int sq8_dp(int dim) { return (dim + 31) / 32 * 32; }
+// code row stride: dim rounded up to 32, then to a k-step count the scan is instantiated for
+int sq8_dp(int dim) {
+  int ns = (dim + 31) / 32;
+  if (ns > 8) ns = ns <= 10 ? 10 : (ns <= 12 ? 12 : 16);
+  return ns * 32;
+}
 int sq8_qgroup() { return 128; }
-bool sq8_supported(int dim, int k) { return k >= 1 && k <= 64 && dim >= 1 && dim <= 256; }
+bool sq8_supported(int dim, int k) { return k >= 1 && k <= 64 && dim >= 1 && dim <= 512; }
 
 void launch_sq8_scan(const Sq8Args &a, int metric, int max_items, hipStream_t st) {
   if (max_items <= 0) return;
@@ -258,6 +263,9 @@ void launch_sq8_scan(const Sq8Args &a, int metric, int max_items, hipStream_t st
     SQ8_CASE(6)
     SQ8_CASE(7)
     SQ8_CASE(8)
+    SQ8_CASE(10)
+    SQ8_CASE(12)
+    SQ8_CASE(16)
 #undef SQ8_CASE
     default: break;
   }

@@ -36,7 +36,7 @@ def _bf(dim, metric, x, quant_from=0):
 
 
 @pytest.mark.parametrize("metric", [0, 1, 2])
-@pytest.mark.parametrize("dim,k", [(128, 10), (37, 1), (200, 64), (16, 33), (3, 5)])
+@pytest.mark.parametrize("dim,k", [(128, 10), (37, 1), (200, 64), (16, 33), (3, 5), (300, 10), (512, 7)])
 def test_quantized_search_matches_oracle(hiplib, oracle, metric, dim, k):
     from pyrope_amd import generate_synthetic
     n = 5000
