@@ -181,3 +181,38 @@ def test_search_with_nprobe_increases_recall(hiplib):
     index.build()
     index.combine_nprobe = 3
     assert len(index.search([0.0, 0.0], 3)) == 3
+
+
+def test_concurrent_searches_match_sequential(hiplib):
+    """The reference serves Search from many session threads at once under a read lock
+    (IvfFlatVectorIndex.cs ReaderWriterLockSlim); the C ABI allows concurrent pyr_index_search
+    calls (a workspace per call).  Results under contention equal the sequential ones."""
+    import threading
+
+    from pyrope_amd import IvfFlatVectorIndex, SearchOptions, generate_synthetic
+    x = generate_synthetic(30000, 64, 21)
+    idx = IvfFlatVectorIndex(64, 0, n_list=32)
+    idx.add_labels(np.arange(len(x), dtype=np.int64), x)
+    idx.build()
+    qs = [generate_synthetic(50, 64, 100 + t) for t in range(8)]
+    opts = SearchOptions(nprobe=6)
+    ref = [idx.search_batch(q, 10, opts) for q in qs]
+    got = [None] * len(qs)
+    errors = []
+
+    def run(t):
+        try:
+            for _ in range(5):
+                got[t] = idx.search_batch(qs[t], 10, opts)
+        except Exception as e:  # surfaced below
+            errors.append(e)
+
+    th = [threading.Thread(target=run, args=(t,)) for t in range(len(qs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors
+    for r, g in zip(ref, got):
+        np.testing.assert_array_equal(r[1], g[1])
+        assert np.array_equal(r[0].view(np.uint32), g[0].view(np.uint32))
