@@ -264,6 +264,11 @@ static int filter_pub_mask() {  // FilterArgs::pub_mask; PYR_FILTER_PUB override
   const char *e = getenv("PYR_FILTER_PUB");
   return e ? atoi(e) : 7;
 }
+// approximate-score arithmetic of the filter: bf16x3 (default) or fp32 (PYR_FILTER_PREC=0)
+static int filter_prec() {
+  const char *e = getenv("PYR_FILTER_PREC");
+  return (e && atoi(e) == 0) ? FILTER_FP32 : FILTER_BF16X3;
+}
 static int filter_ablate() {  // measurement only (FilterArgs::ablate)
   const char *e = getenv("PYR_FILTER_ABLATE");
   return e ? atoi(e) : 0;
@@ -311,6 +316,7 @@ static int64_t filter_finish(Workspace &ws, int64_t nq, int nparts, int k1, int 
   r.k = k;
   r.dim = dim;
   r.c_err = filter_cerr(dim);
+  r.c_bf = filter_prec() == FILTER_BF16X3 ? filter_bf16x3_cerr(dim, met) : 0.0;
   r.out_s = d_s;
   r.out_l = d_l;
   r.out_c = d_c;
@@ -626,6 +632,7 @@ struct FlatIndex : Index {
     fa.gthr = gthr;
     fa.ablate = filter_ablate();
     fa.pub_mask = filter_pub_mask();
+    fa.prec = filter_prec();
     {
       PhaseTimer t(PH_FLAT_SCAN, ws.st, nq * cutoff);
       launch_filter(fa, metric, p.nitems, ws.st);
@@ -1185,6 +1192,7 @@ struct IvfFlatIndex : Index {
     fa.gthr = gthr;
     fa.ablate = filter_ablate();
     fa.pub_mask = filter_pub_mask();
+    fa.prec = filter_prec();
     DevMem dbg;
     if (getenv("PYR_FILTER_DEBUG")) {  // measurement only: insert statistics to stderr
       dbg.ensure(16);

@@ -35,6 +35,7 @@ namespace pyr {
 namespace {
 
 typedef float f16v __attribute__((ext_vector_type(16)));
+typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ bool better(float s1, uint32_t k1, float s2, uint32_t k2) {
   return s1 > s2 || (s1 == s2 && k1 < k2);
@@ -47,12 +48,16 @@ __device__ __forceinline__ size_t blk_off(int64_t r, int d, int D) {
 constexpr int RT = 32;       // rows per stage (one 32x32 MFMA tile per wave)
 constexpr int SCR = RT + 4;  // score-transpose row stride (floats)
 
-// LDS layout of mfma_filter
-template <int D>
+// LDS layout of mfma_filter.  fp32 mode: [2 buffers][RT][RSTR] floats.  bf16x3 mode:
+// [2 buffers][hi, lo][RT][BSTR] bf16 (BSTR = D + 8: the 16-byte row pad makes the
+// ds_read_b128 B fragments conflict-free); the score transpose follows either way.
+template <int D, bool BF>
 struct FilterLds {
   static constexpr int RSTR = D + 4;      // padded row stride: conflict-free ds_read_b128 / ds_write_b32
-  static constexpr int TILE = RT * RSTR;  // floats per row tile
-  static constexpr size_t bytes() { return sizeof(float) * (2 * TILE + 4 * 32 * SCR); }
+  static constexpr int BSTR = D + 8;      // bf16 row stride
+  static constexpr int TILE = BF ? RT * BSTR : RT * RSTR;  // floats per fp32 tile / bf16 per hi or lo tile
+  static constexpr size_t tiles_bytes() { return BF ? sizeof(uint16_t) * 4 * TILE : sizeof(float) * 2 * TILE; }
+  static constexpr size_t bytes() { return tiles_bytes() + sizeof(float) * 4 * 32 * SCR; }
 };
 
 // ---------------------------------------------------------------------------
@@ -83,23 +88,54 @@ __device__ __forceinline__ void reg_insert(float (&s)[KR], uint32_t (&kk)[KR], f
   kk[0] = b[0] ? key : kk[0];
 }
 
-template <int D, int MET, bool IVF, int KR>
+// BF = bf16x3 mode: q.x as qh.xh + qh.xl + ql.xh on v_mfma_f32_32x32x16_bf16, where
+// q = qh + ql (+ |eps| <= 2^-16 |q|) is the two-term bf16 split of each fp32 value (x
+// likewise, split once per block while staging rows into LDS).  Relative error per
+// product <= 3.1 * 2^-16 plus fp32 accumulation over 3D terms; refine_kernel's c_bf term
+// covers it, so the certified results stay exact.  5.3x the fp32 MFMA rate.
+template <int D, int MET, bool IVF, int KR, bool BF>
 __global__ __launch_bounds__(256, 2) void mfma_filter(FilterArgs a) {
-  using L = FilterLds<D>;
-  constexpr int KH = D / 2;  // k-steps: lanes 0-31 take dims [0, KH), lanes 32-63 [KH, D)
+  using L = FilterLds<D, BF>;
+  constexpr int KH = D / 2;  // fp32 k-steps: lanes 0-31 take dims [0, KH), lanes 32-63 [KH, D)
+  constexpr int KS = D / 16;  // bf16 k-steps: lane half h takes dims 16s + 8h .. +7 of step s
   extern __shared__ __attribute__((aligned(16))) float smem[];
   if ((int)blockIdx.x >= *a.n_items) return;
   const ScanItem it = a.items[blockIdx.x];
-  float *rt = smem;                 // [2][RT][RSTR]
-  float *scw = smem + 2 * L::TILE;  // [4][32][SCR]
+  float *rt = smem;                                          // fp32: [2][RT][RSTR]
+  uint16_t *bt = reinterpret_cast<uint16_t *>(smem);         // bf16: [2][hi, lo][RT][BSTR]
+  float *scw = smem + L::tiles_bytes() / sizeof(float);      // [4][32][SCR]
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int i32 = lane & 31, h = lane >> 5;
   float *sc = scw + w * 32 * SCR;
 
-  // A operand: query 32w + i32 of the item, dims h*KH .. h*KH + KH - 1
-  float qa[KH];
-  {
+  // A operand, bf16x3 mode: query 32w + i32, split into hi / lo fragments per k-step
+  bf8v qh[BF ? KS : 1], ql[BF ? KS : 1];
+  if constexpr (BF) {
+    const int i = 32 * w + i32;
+    const int qi = i < it.qcnt ? (IVF ? a.qlist[it.qbeg + i] / a.nparts : it.qbeg + i) : -1;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      float v[8];
+      if (qi >= 0) {
+        const float4 *qp = reinterpret_cast<const float4 *>(a.queries + (size_t)qi * D + 16 * s + 8 * h);
+        const float4 v0 = qp[0], v1 = qp[1];
+        v[0] = v0.x; v[1] = v0.y; v[2] = v0.z; v[3] = v0.w;
+        v[4] = v1.x; v[5] = v1.y; v[6] = v1.z; v[7] = v1.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = 0.0f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        qh[s][j] = (__bf16)v[j];
+        ql[s][j] = (__bf16)(v[j] - (float)qh[s][j]);
+      }
+    }
+  }
+  // A operand, fp32 mode: query 32w + i32 of the item, dims h*KH .. h*KH + KH - 1
+  float qa[BF ? 1 : KH];
+  if constexpr (!BF) {
     const int i = 32 * w + i32;
     if (i < it.qcnt) {
       const int qi = IVF ? a.qlist[it.qbeg + i] / a.nparts : it.qbeg + i;
@@ -143,29 +179,81 @@ __global__ __launch_bounds__(256, 2) void mfma_filter(FilterArgs a) {
   const int r0 = it.row_begin;  // multiple of 8
   const int nst = (it.row_end - r0 + RT - 1) / RT;
   constexpr int NV = RT * D / 4;  // float4 per stage
-  constexpr int LOADS = NV / 256;
-  static_assert(NV % 256 == 0, "stage must split evenly over 256 threads");
+  constexpr int LOADS = BF ? 1 : NV / 256;
+  static_assert(BF || NV % 256 == 0, "stage must split evenly over 256 threads");
+  // bf16x3 staging works on float4 pairs (dims 2p, 2p+1 of the same 4 rows: float4 v and
+  // v + 2 of a group) so each row's two bf16 halves are written as one 32-bit word
+  constexpr int NP = NV / 2;                   // float4 pairs per stage
+  constexpr int PL = BF ? (NP + 255) / 256 : 1;  // pairs per thread
   const float4 *src = reinterpret_cast<const float4 *>(a.rows);
   const int gmax = ((it.row_end + 7) >> 3) - 1;  // last group with rows of this item
   float4 pf[LOADS];
+  float4 pa[PL], pb[PL];
   auto load_stage = [&](int stg) {
+    if constexpr (BF) {
 #pragma unroll
-    for (int i = 0; i < LOADS; ++i) {
-      const int v = tid + 256 * i;
-      const int g = min((r0 >> 3) + stg * (RT / 8) + v / (2 * D), gmax);  // clamp: rows past the end unused
-      pf[i] = src[(size_t)g * (2 * D) + v % (2 * D)];
+      for (int i = 0; i < PL; ++i) {
+        const int pr = tid + 256 * i;
+        if (NP % 256 == 0 || pr < NP) {
+          const int gl = pr / D, pp = pr % D;
+          const int v0 = 4 * (pp >> 1) + (pp & 1);
+          const int g = min((r0 >> 3) + stg * (RT / 8) + gl, gmax);  // clamp: rows past the end unused
+          pa[i] = src[(size_t)g * (2 * D) + v0];
+          pb[i] = src[(size_t)g * (2 * D) + v0 + 2];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < LOADS; ++i) {
+        const int v = tid + 256 * i;
+        const int g = min((r0 >> 3) + stg * (RT / 8) + v / (2 * D), gmax);  // clamp: rows past the end unused
+        pf[i] = src[(size_t)g * (2 * D) + v % (2 * D)];
+      }
     }
   };
+  auto split2 = [](float x0, float x1, uint32_t &hi, uint32_t &lo) {
+    const __bf16 h0 = (__bf16)x0, h1 = (__bf16)x1;
+    const __bf16 l0 = (__bf16)(x0 - (float)h0), l1 = (__bf16)(x1 - (float)h1);
+    hi = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+    lo = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+  };
   auto store_stage = [&](int buf) {
+    if constexpr (BF) {
 #pragma unroll
-    for (int i = 0; i < LOADS; ++i) {
-      const int v = tid + 256 * i;
-      const int gl = v / (2 * D), vv = v % (2 * D);
-      float *dst = rt + buf * L::TILE + (gl * 8 + (vv & 1) * 4) * L::RSTR + (vv >> 1);
-      dst[0] = pf[i].x;
-      dst[L::RSTR] = pf[i].y;
-      dst[2 * L::RSTR] = pf[i].z;
-      dst[3 * L::RSTR] = pf[i].w;
+      for (int i = 0; i < PL; ++i) {
+        const int pr = tid + 256 * i;
+        if (NP % 256 == 0 || pr < NP) {
+          const int gl = pr / D, pp = pr % D;
+          const int row = gl * 8 + (pp & 1) * 4;
+          uint32_t *dh = reinterpret_cast<uint32_t *>(bt + (2 * buf) * L::TILE + row * L::BSTR + 2 * (pp >> 1));
+          uint32_t *dl = dh + L::TILE / 2;
+          constexpr int W = L::BSTR / 2;  // row stride in 32-bit words
+          uint32_t hi, lo;
+          split2(pa[i].x, pb[i].x, hi, lo);
+          dh[0] = hi;
+          dl[0] = lo;
+          split2(pa[i].y, pb[i].y, hi, lo);
+          dh[W] = hi;
+          dl[W] = lo;
+          split2(pa[i].z, pb[i].z, hi, lo);
+          dh[2 * W] = hi;
+          dl[2 * W] = lo;
+          split2(pa[i].w, pb[i].w, hi, lo);
+          dh[3 * W] = hi;
+          dl[3 * W] = lo;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < LOADS; ++i) {
+        const int v = tid + 256 * i;
+        const int gl = v / (2 * D), vv = v % (2 * D);
+        float *dst = rt + buf * L::TILE + (gl * 8 + (vv & 1) * 4) * L::RSTR + (vv >> 1);
+        dst[0] = pf[i].x;
+        dst[L::RSTR] = pf[i].y;
+        dst[2 * L::RSTR] = pf[i].z;
+        dst[3 * L::RSTR] = pf[i].w;
+      }
     }
   };
 
@@ -199,14 +287,27 @@ __global__ __launch_bounds__(256, 2) void mfma_filter(FilterArgs a) {
       f16v acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-      const float *bp = rt + cur * L::TILE + i32 * L::RSTR + h * KH;
+      if constexpr (BF) {
+        const uint16_t *bh = bt + (2 * cur) * L::TILE + i32 * L::BSTR + 8 * h;
+        const uint16_t *bl = bh + L::TILE;
 #pragma unroll
-      for (int s4 = 0; s4 < KH / 4; ++s4) {
-        const float4 b = *reinterpret_cast<const float4 *>(bp + 4 * s4);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qa[4 * s4 + 0], b.x, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qa[4 * s4 + 1], b.y, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qa[4 * s4 + 2], b.z, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qa[4 * s4 + 3], b.w, acc, 0, 0, 0);
+        for (int s = 0; s < KS; ++s) {
+          const bf8v xh = *reinterpret_cast<const bf8v *>(bh + 16 * s);
+          const bf8v xl = *reinterpret_cast<const bf8v *>(bl + 16 * s);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ql[s], xh, acc, 0, 0, 0);  // small terms first
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh[s], xl, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh[s], xh, acc, 0, 0, 0);
+        }
+      } else {
+        const float *bp = rt + cur * L::TILE + i32 * L::RSTR + h * KH;
+#pragma unroll
+        for (int s4 = 0; s4 < KH / 4; ++s4) {
+          const float4 b = *reinterpret_cast<const float4 *>(bp + 4 * s4);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qa[4 * s4 + 0], b.x, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qa[4 * s4 + 1], b.y, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qa[4 * s4 + 2], b.z, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qa[4 * s4 + 3], b.w, acc, 0, 0, 0);
+        }
       }
       // C[i][j]: lane column j = i32 (row), register r -> query (r&3) + 8(r>>2) + 4h
       if (!(a.ablate & 2)) {
@@ -344,7 +445,8 @@ __device__ float exact_score(const float *q, const float *rows, int64_t r, int D
 // chain of D terms (error <= D u sum|q_i x_i| <= D u |q||x|), |x|^2 and |q|^2 are fp32
 // sums (<= D u |.|^2 each), one more rounding combines them, and the reference's own
 // sum is within (D/8 + 5) u (|q| + |x|)^2 of the real value: < (3.2 D + 6) u (|q|+|x|)^2
-// in all, against c_err = 4 D + 64 (engine).  If fewer than K1 candidates exist no row
+// in all, against c_err = 4 D + 64 (engine).  The bf16x3 filter adds c_bf u |q| X
+// (kernels.h filter_bf16x3_cerr) and an absolute term for flushed subnormal halves.  If fewer than K1 candidates exist no row
 // was excluded and the result is exact as it stands.
 template <int V, int MET>
 __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
@@ -396,7 +498,8 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
     const double u = 5.9604644775390625e-8;  // 2^-24
     const double qn = sqrt((double)qsq) * (1.0 + 1e-5);
     const double X = sqrt((double)key_score(*a.max_rsq)) * (1.0 + 1e-5);
-    const double e = MET == L2 ? a.c_err * u * (qn + X) * (qn + X) : a.c_err * u * qn * X;
+    const double e = (MET == L2 ? a.c_err * u * (qn + X) * (qn + X) : a.c_err * u * qn * X) +
+                     a.c_bf * u * qn * X + (a.c_bf > 0.0 ? 1e-30 * (1.0 + qn + X) * D : 0.0);  // bf16 subnormals
     const double approx_k1 = MET == L2 ? (double)ms[k1 - 1] - (double)qsq : (double)ms[k1 - 1];
     ok = nout == k && (double)skth > approx_k1 + e;
   }
@@ -444,15 +547,22 @@ __global__ void sqnorms_kernel(const float *rows, const int64_t *slots, int64_t 
 
 inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
-template <int D, int MET, bool IVF, int KR>
-void launch_filter_t(const FilterArgs &a, int max_items, hipStream_t st) {
+template <int D, int MET, bool IVF, int KR, bool BF>
+void launch_filter_p(const FilterArgs &a, int max_items, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mfma_filter<D, MET, IVF, KR>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mfma_filter<D, MET, IVF, KR, BF>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((mfma_filter<D, MET, IVF, KR>), dim3(max_items), dim3(256), FilterLds<D>::bytes(), st, a);
+  const size_t lds = FilterLds<D, BF>::bytes();
+  hipLaunchKernelGGL((mfma_filter<D, MET, IVF, KR, BF>), dim3(max_items), dim3(256), lds, st, a);
+}
+
+template <int D, int MET, bool IVF, int KR>
+void launch_filter_t(const FilterArgs &a, int max_items, hipStream_t st) {
+  if (a.prec == FILTER_BF16X3) launch_filter_p<D, MET, IVF, KR, true>(a, max_items, st);
+  else launch_filter_p<D, MET, IVF, KR, false>(a, max_items, st);
 }
 
 template <int D, int MET, bool IVF>

@@ -241,7 +241,17 @@ struct FilterArgs {
   int32_t pub_mask;        // publish / refresh the shared bound when (stage & pub_mask) == pub_mask
   uint32_t *dbg;           // measurement only (PYR_FILTER_DEBUG): [0] insert-loop iterations of
                            // all waves, [1] candidates inserted, [2] owner stages, or null
+  int32_t prec;            // FILTER_FP32 or FILTER_BF16X3 (approximate-score arithmetic)
 };
+constexpr int FILTER_FP32 = 0;    // v_mfma_f32_32x32x2_f32
+constexpr int FILTER_BF16X3 = 1;  // hi/lo bf16 split, 3 x v_mfma_f32_32x32x16_bf16
+// refine_kernel error-bound constant of the bf16x3 approximation (per u |q| max|x|)
+inline double filter_bf16x3_cerr(int dim, int metric) {
+  // q.x: <= 3.02 * 2^-16 per product from the splits, <= 2u per addition over 3D terms;
+  // doubled for L2 (approx = 2 q.x - ...)
+  const double c = 6.3 * dim + 800.0;
+  return metric == 0 ? 2.0 * c : c;
+}
 struct RefineArgs {
   const float *rows;        // blocked store the keys index
   const int64_t *row_labels;
@@ -252,6 +262,7 @@ struct RefineArgs {
   int64_t nq;
   int32_t k1, k, dim;
   double c_err;             // error-bound constant (refine_kernel)
+  double c_bf;              // extra constant of the bf16x3 filter (0 for fp32)
   float *out_s;
   int64_t *out_l;
   int32_t *out_c;

@@ -58,14 +58,16 @@ def _flat(dim, metric, x):
     return idx
 
 
+@pytest.mark.parametrize("prec", ["1", "0"])  # PYR_FILTER_PREC: bf16x3 (default), fp32
 @pytest.mark.parametrize("metric", [0, 1])
 @pytest.mark.parametrize("dim", [128, 64, 32])
-def test_flat_filter_equals_exact_and_oracle(hiplib, oracle, metric, dim):
+def test_flat_filter_equals_exact_and_oracle(hiplib, oracle, metric, dim, prec):
     from pyrope_amd import generate_synthetic
     x = generate_synthetic(20000, dim, 42)
     q = generate_synthetic(300, dim, 1337)
     idx = _flat(dim, metric, x)
-    got, nfb = _fallbacks(hiplib, lambda: idx.search_batch(q, 10))
+    with _env(PYR_FILTER_PREC=prec):
+        got, nfb = _fallbacks(hiplib, lambda: idx.search_batch(q, 10))
     with _env(PYR_FILTER=0):
         ref = idx.search_batch(q, 10)
     _same(got, ref)
@@ -76,8 +78,9 @@ def test_flat_filter_equals_exact_and_oracle(hiplib, oracle, metric, dim):
     assert nfb < len(q)  # the certificate holds for (almost) every query of uniform data
 
 
+@pytest.mark.parametrize("prec", ["1", "0"])
 @pytest.mark.parametrize("metric", [0, 1])
-def test_ivf_filter_equals_exact_and_oracle(hiplib, oracle, metric):
+def test_ivf_filter_equals_exact_and_oracle(hiplib, oracle, metric, prec):
     from pyrope_amd import IvfFlatVectorIndex, SearchOptions, generate_synthetic
     x = generate_synthetic(20000, 128, 42)
     idx = IvfFlatVectorIndex(128, metric, n_list=64)
@@ -85,7 +88,8 @@ def test_ivf_filter_equals_exact_and_oracle(hiplib, oracle, metric):
     idx.build()
     q = generate_synthetic(500, 128, 1337)
     opts = SearchOptions(nprobe=8)
-    got = idx.search_batch(q, 10, opts)
+    with _env(PYR_FILTER_PREC=prec):
+        got = idx.search_batch(q, 10, opts)
     with _env(PYR_FILTER=0):
         ref = idx.search_batch(q, 10, opts)
     _same(got, ref)
@@ -154,3 +158,22 @@ def test_flat_filter_respects_max_scans_and_deletes(hiplib, oracle):
         for i in range(0, len(q), 13):
             os_, ok = oracle.bf_search(x, live, 0, q[i], 10, max_scans=-1 if ms is None else ms)
             np.testing.assert_array_equal(got[1][i][: len(ok)], ok)
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+@pytest.mark.parametrize("scale", [1e-3, 1.0, 1e3])
+def test_bf16x3_near_duplicates_and_wide_range(hiplib, metric, scale):
+    """Rows that differ far below one bf16 ulp (clusters of near-duplicates, signed values,
+    magnitudes from 1e-3 to 1e3): the bf16x3 approximation cannot separate them, so its
+    certificate must fail rather than pass a wrong top-k -- results stay bit-identical to
+    the exact scan whatever the certificate decides."""
+    rng = np.random.default_rng(5)
+    base = rng.standard_normal((150, 128)).astype(np.float32)
+    x = (np.repeat(base, 40, axis=0) * (1 + 1e-6 * rng.standard_normal((6000, 128)))).astype(np.float32)
+    x *= np.float32(scale)
+    q = (base[rng.integers(0, 150, 80)] * scale + 1e-3 * scale * rng.standard_normal((80, 128))).astype(np.float32)
+    idx = _flat(128, metric, x)
+    got = idx.search_batch(q, 10)
+    with _env(PYR_FILTER=0):
+        ref = idx.search_batch(q, 10)
+    _same(got, ref)
