@@ -269,6 +269,15 @@ static int filter_prec() {
   const char *e = getenv("PYR_FILTER_PREC");
   return (e && atoi(e) == 0) ? FILTER_FP32 : FILTER_BF16X3;
 }
+// waves per filter block for IVF items (FilterArgs::waves): 4 = 128-query items (default);
+// PYR_FILTER_WAVES=8 -> 256-query items, one block per CU (bf16x3 only): half the row
+// traffic but measured slower, 4.98 -> 7.42 ms at the bench config (profiles/r1_sweeps/sweep23).
+// FLAT items always use 4.
+static int filter_waves_ivf() {
+  const char *e = getenv("PYR_FILTER_WAVES");
+  const int w = e ? atoi(e) : 4;
+  return (w == 8 && filter_prec() == FILTER_BF16X3) ? 8 : 4;
+}
 static int filter_ablate() {  // measurement only (FilterArgs::ablate)
   const char *e = getenv("PYR_FILTER_ABLATE");
   return e ? atoi(e) : 0;
@@ -633,6 +642,7 @@ struct FlatIndex : Index {
     fa.ablate = filter_ablate();
     fa.pub_mask = filter_pub_mask();
     fa.prec = filter_prec();
+    fa.waves = 4;  // items of QCHUNK = 128 queries (plan_flat)
     {
       PhaseTimer t(PH_FLAT_SCAN, ws.st, nq * cutoff);
       launch_filter(fa, metric, p.nitems, ws.st);
@@ -908,7 +918,9 @@ static bool ivf_seed_enabled() {
 // the MAX_PARTS budget left after `other_parts` and a cap on the partial buffer.
 // PYR_IVF_CHUNK / PYR_IVF_WARM override the defaults for measurements.
 static IvfChunking ivf_chunking(int64_t max_len, int probes, int other_parts, int64_t nq, int k, bool bounds) {
-  int64_t chunk = 2048, warm = 0;  // warm-up launch: measured neutral at the bench config (profiles/)
+  // 4096 rows: 5.71 -> 5.27 ms over 2048 at the bench config (profiles/r1_sweeps/sweep21); warm-up
+  // launch measured neutral (profiles/)
+  int64_t chunk = 4096, warm = 0;
   if (const char *e = getenv("PYR_IVF_CHUNK")) chunk = std::max<int64_t>(8, atoll(e));
   if (const char *e = getenv("PYR_IVF_WARM")) warm = std::max<int64_t>(0, atoll(e));
   if (!bounds) warm = 0;  // the warm-up launch only pays with shared bounds
@@ -1163,15 +1175,17 @@ struct IvfFlatIndex : Index {
     ws.part_s.ensure(sizeof(float) * np);
     ws.part_k.ensure(sizeof(uint32_t) * np);
     uint32_t *gthr = shared_bounds(ws, nq);
+    const int waves = filter_waves_ivf();
+    const int qc = filter_qchunk(filter_prec(), waves);
     int maxi, maxi_main = 0;
     {
       PhaseTimer t(PH_ITEMS, ws.st);
       if (seed) {
-        maxi = build_ivf_items_range(ws, 0, nq, probes, 0, 1, nparts, coarse.nlist, dlb, dle, QCHUNK, ch);
-        maxi_main = build_ivf_items_range(ws, 1, nq, probes, 1, probes, nparts, coarse.nlist, dlb, dle, QCHUNK, ch);
+        maxi = build_ivf_items_range(ws, 0, nq, probes, 0, 1, nparts, coarse.nlist, dlb, dle, qc, ch);
+        maxi_main = build_ivf_items_range(ws, 1, nq, probes, 1, probes, nparts, coarse.nlist, dlb, dle, qc, ch);
       } else {
-        maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, QCHUNK, ch, 0);
-        if (ch.warm > 0) maxi_main = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, QCHUNK, ch, 1);
+        maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qc, ch, 0);
+        if (ch.warm > 0) maxi_main = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qc, ch, 1);
       }
     }
     FilterArgs fa{};
@@ -1193,6 +1207,7 @@ struct IvfFlatIndex : Index {
     fa.ablate = filter_ablate();
     fa.pub_mask = filter_pub_mask();
     fa.prec = filter_prec();
+    fa.waves = waves;
     DevMem dbg;
     if (getenv("PYR_FILTER_DEBUG")) {  // measurement only: insert statistics to stderr
       dbg.ensure(16);

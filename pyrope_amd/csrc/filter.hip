@@ -47,17 +47,20 @@ __device__ __forceinline__ size_t blk_off(int64_t r, int d, int D) {
 
 constexpr int RT = 32;       // rows per stage (one 32x32 MFMA tile per wave)
 constexpr int SCR = RT + 4;  // score-transpose row stride (floats)
+constexpr int CB = 16;       // candidate buffer entries per owner
+constexpr int CBS = CB + 1;  // buffer stride (odd: the owners' appends hit distinct banks)
 
 // LDS layout of mfma_filter.  fp32 mode: [2 buffers][RT][RSTR] floats.  bf16x3 mode:
 // [2 buffers][hi, lo][RT][BSTR] bf16 (BSTR = D + 8: the 16-byte row pad makes the
-// ds_read_b128 B fragments conflict-free); the score transpose follows either way.
-template <int D, bool BF>
+// ds_read_b128 B fragments conflict-free); then the score transpose [4][32][SCR] and the
+// owners' candidate buffers (scores [128][CB], keys [128][CB]).
+template <int D, bool BF, int NW = 4>
 struct FilterLds {
   static constexpr int RSTR = D + 4;      // padded row stride: conflict-free ds_read_b128 / ds_write_b32
   static constexpr int BSTR = D + 8;      // bf16 row stride
   static constexpr int TILE = BF ? RT * BSTR : RT * RSTR;  // floats per fp32 tile / bf16 per hi or lo tile
   static constexpr size_t tiles_bytes() { return BF ? sizeof(uint16_t) * 4 * TILE : sizeof(float) * 2 * TILE; }
-  static constexpr size_t bytes() { return tiles_bytes() + sizeof(float) * 4 * 32 * SCR; }
+  static constexpr size_t bytes() { return tiles_bytes() + sizeof(float) * NW * 32 * SCR + 8 * NW * 32 * CBS; }
 };
 
 // ---------------------------------------------------------------------------
@@ -93,9 +96,13 @@ __device__ __forceinline__ void reg_insert(float (&s)[KR], uint32_t (&kk)[KR], f
 // likewise, split once per block while staging rows into LDS).  Relative error per
 // product <= 3.1 * 2^-16 plus fp32 accumulation over 3D terms; refine_kernel's c_bf term
 // covers it, so the certified results stay exact.  5.3x the fp32 MFMA rate.
-template <int D, int MET, bool IVF, int KR, bool BF>
-__global__ __launch_bounds__(256, 2) void mfma_filter(FilterArgs a) {
-  using L = FilterLds<D, BF>;
+// NW = waves per block (32 queries each): 4 (two blocks per CU) or 8 (one block per CU,
+// every staged row tile serves 256 queries: half the HBM / L2 row traffic of NW = 4).
+template <int D, int MET, bool IVF, int KR, bool BF, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void mfma_filter(FilterArgs a) {
+  using L = FilterLds<D, BF, NW>;
+  constexpr int NT = 64 * NW;  // threads per block
+  static_assert(NW == 4 || (BF && NW == 8), "8-wave blocks only in bf16x3 mode");
   constexpr int KH = D / 2;  // fp32 k-steps: lanes 0-31 take dims [0, KH), lanes 32-63 [KH, D)
   constexpr int KS = D / 16;  // bf16 k-steps: lane half h takes dims 16s + 8h .. +7 of step s
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -166,6 +173,10 @@ __global__ __launch_bounds__(256, 2) void mfma_filter(FilterArgs a) {
     qown = IVF ? a.qlist[it.qbeg + oq] / a.nparts : it.qbeg + oq;
     if (a.gthr) gs = key_score(__hip_atomic_load(a.gthr + qown, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   }
+  // this owner's candidate buffer (scores, keys) in LDS, nbuf entries
+  float *bs = scw + NW * 32 * SCR + (w * 32 + i32) * CBS;
+  uint32_t *bk = reinterpret_cast<uint32_t *>(scw + NW * 32 * SCR + NW * 32 * CBS) + (w * 32 + i32) * CBS;
+  int nbuf = 0;
   float ts[KR];  // this owner's top-KR by approximate score, sorted desc; (-inf, NONE) = empty
   uint32_t tk[KR];
 #pragma unroll
@@ -179,12 +190,12 @@ __global__ __launch_bounds__(256, 2) void mfma_filter(FilterArgs a) {
   const int r0 = it.row_begin;  // multiple of 8
   const int nst = (it.row_end - r0 + RT - 1) / RT;
   constexpr int NV = RT * D / 4;  // float4 per stage
-  constexpr int LOADS = BF ? 1 : NV / 256;
-  static_assert(BF || NV % 256 == 0, "stage must split evenly over 256 threads");
+  constexpr int LOADS = BF ? 1 : NV / NT;
+  static_assert(BF || NV % NT == 0, "stage must split evenly over the block");
   // bf16x3 staging works on float4 pairs (dims 2p, 2p+1 of the same 4 rows: float4 v and
   // v + 2 of a group) so each row's two bf16 halves are written as one 32-bit word
   constexpr int NP = NV / 2;                   // float4 pairs per stage
-  constexpr int PL = BF ? (NP + 255) / 256 : 1;  // pairs per thread
+  constexpr int PL = BF ? (NP + NT - 1) / NT : 1;  // pairs per thread
   const float4 *src = reinterpret_cast<const float4 *>(a.rows);
   const int gmax = ((it.row_end + 7) >> 3) - 1;  // last group with rows of this item
   float4 pf[LOADS];
@@ -193,8 +204,8 @@ __global__ __launch_bounds__(256, 2) void mfma_filter(FilterArgs a) {
     if constexpr (BF) {
 #pragma unroll
       for (int i = 0; i < PL; ++i) {
-        const int pr = tid + 256 * i;
-        if (NP % 256 == 0 || pr < NP) {
+        const int pr = tid + NT * i;
+        if (NP % NT == 0 || pr < NP) {
           const int gl = pr / D, pp = pr % D;
           const int v0 = 4 * (pp >> 1) + (pp & 1);
           const int g = min((r0 >> 3) + stg * (RT / 8) + gl, gmax);  // clamp: rows past the end unused
@@ -205,7 +216,7 @@ __global__ __launch_bounds__(256, 2) void mfma_filter(FilterArgs a) {
     } else {
 #pragma unroll
       for (int i = 0; i < LOADS; ++i) {
-        const int v = tid + 256 * i;
+        const int v = tid + NT * i;
         const int g = min((r0 >> 3) + stg * (RT / 8) + v / (2 * D), gmax);  // clamp: rows past the end unused
         pf[i] = src[(size_t)g * (2 * D) + v % (2 * D)];
       }
@@ -221,8 +232,8 @@ __global__ __launch_bounds__(256, 2) void mfma_filter(FilterArgs a) {
     if constexpr (BF) {
 #pragma unroll
       for (int i = 0; i < PL; ++i) {
-        const int pr = tid + 256 * i;
-        if (NP % 256 == 0 || pr < NP) {
+        const int pr = tid + NT * i;
+        if (NP % NT == 0 || pr < NP) {
           const int gl = pr / D, pp = pr % D;
           const int row = gl * 8 + (pp & 1) * 4;
           uint32_t *dh = reinterpret_cast<uint32_t *>(bt + (2 * buf) * L::TILE + row * L::BSTR + 2 * (pp >> 1));
@@ -246,7 +257,7 @@ __global__ __launch_bounds__(256, 2) void mfma_filter(FilterArgs a) {
     } else {
 #pragma unroll
       for (int i = 0; i < LOADS; ++i) {
-        const int v = tid + 256 * i;
+        const int v = tid + NT * i;
         const int gl = v / (2 * D), vv = v % (2 * D);
         float *dst = rt + buf * L::TILE + (gl * 8 + (vv & 1) * 4) * L::RSTR + (vv >> 1);
         dst[0] = pf[i].x;
@@ -324,16 +335,23 @@ __global__ __launch_bounds__(256, 2) void mfma_filter(FilterArgs a) {
     if (st + 1 < nst && !(a.ablate & 4)) store_stage(cur ^ 1);
     __syncthreads();  // next tile staged; this wave's score transpose visible
 
+    // pre-filter against the owner's bound (the full (score, key) test follows): lane half
+    // h tests rows 16h .. 16h + 15 of query i32, the owner joins the two masks
+    const float lo = __shfl(fmaxf(gs, ts[KR - 1]), i32);
+    uint32_t hmask = 0;
+    if (oq < it.qcnt && !(a.ablate & 1)) {
+      const float *sch = sc + i32 * SCR + (RT / 2) * h;
+#pragma unroll
+      for (int j = 0; j < RT / 2; ++j) {
+        const float v = sch[j];
+        if (v > -INFINITY && v >= lo) hmask |= 1u << j;
+      }
+    }
+    const uint32_t upper = __shfl(hmask, i32 + 32);
     if (owner && !(a.ablate & 1)) {
       const float *scp = sc + i32 * SCR;
       const int rb = r0 + st * RT;
-      uint32_t pass = 0;
-      const float lo = fmaxf(gs, ts[KR - 1]);  // cheap pre-filter; the full (score, key) test follows
-#pragma unroll
-      for (int j = 0; j < RT; ++j) {
-        const float v = scp[j];
-        if (v > -INFINITY && v >= lo) pass |= 1u << j;
-      }
+      uint32_t pass = hmask | (upper << (RT / 2));
       if (a.ablate & 16) {  // measurement: filter without inserting
         if (pass == 0x12345u) ts[0] = lo;
         pass = 0;
@@ -346,12 +364,34 @@ __global__ __launch_bounds__(256, 2) void mfma_filter(FilterArgs a) {
         for (int o = 16; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 32));
         if (i32 == 0) atomicAdd(a.dbg, mx);
       }
-      while (pass) {
-        const int j = __builtin_ctz(pass);
-        pass &= pass - 1;
-        const float v = scp[j];
-        const uint32_t key = a.key_base | (uint32_t)(rb + j);
-        if (better(v, key, ts[KR - 1], tk[KR - 1])) reg_insert<KR>(ts, tk, v, key);
+      // Survivors go to the owner's LDS buffer (cheap appends); the register list is
+      // updated only when some owner's buffer would overflow (then every owner of the wave
+      // drains its buffer and inserts this stage directly).  The 32 owners run the insert
+      // network in lockstep, so draining CB buffered candidates at once costs max-over-owners
+      // of the buffered counts instead of a sum over stages of per-stage maxima.
+      const bool direct = (a.ablate & 32) || __any(nbuf + __popc(pass) > CB);
+      if (direct) {
+        for (int i = 0; i < nbuf; ++i) {
+          const float v = bs[i];
+          const uint32_t key = bk[i];
+          if (better(v, key, ts[KR - 1], tk[KR - 1])) reg_insert<KR>(ts, tk, v, key);
+        }
+        nbuf = 0;
+        while (pass) {
+          const int j = __builtin_ctz(pass);
+          pass &= pass - 1;
+          const float v = scp[j];
+          const uint32_t key = a.key_base | (uint32_t)(rb + j);
+          if (better(v, key, ts[KR - 1], tk[KR - 1])) reg_insert<KR>(ts, tk, v, key);
+        }
+      } else {
+        while (pass) {
+          const int j = __builtin_ctz(pass);
+          pass &= pass - 1;
+          bs[nbuf] = scp[j];
+          bk[nbuf] = a.key_base | (uint32_t)(rb + j);
+          ++nbuf;
+        }
       }
       if (a.gthr && (st & a.pub_mask) == a.pub_mask) {  // publish this list's KR-th best, refresh the bound
         if (tk[KR - 1] != KEY_NONE && score_key(ts[KR - 1]) > published) {
@@ -363,6 +403,11 @@ __global__ __launch_bounds__(256, 2) void mfma_filter(FilterArgs a) {
     }
   }
   if (owner) {
+    for (int i = 0; i < nbuf; ++i) {  // drain the candidate buffer
+      const float v = bs[i];
+      const uint32_t key = bk[i];
+      if (better(v, key, ts[KR - 1], tk[KR - 1])) reg_insert<KR>(ts, tk, v, key);
+    }
     if (a.gthr && tk[KR - 1] != KEY_NONE && score_key(ts[KR - 1]) > published)
       atomicMax(a.gthr + qown, score_key(ts[KR - 1]));
     float *ps = a.part_s + (size_t)oslot * KR;
@@ -547,22 +592,26 @@ __global__ void sqnorms_kernel(const float *rows, const int64_t *slots, int64_t 
 
 inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
-template <int D, int MET, bool IVF, int KR, bool BF>
+template <int D, int MET, bool IVF, int KR, bool BF, int NW>
 void launch_filter_p(const FilterArgs &a, int max_items, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mfma_filter<D, MET, IVF, KR, BF>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mfma_filter<D, MET, IVF, KR, BF, NW>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  const size_t lds = FilterLds<D, BF>::bytes();
-  hipLaunchKernelGGL((mfma_filter<D, MET, IVF, KR, BF>), dim3(max_items), dim3(256), lds, st, a);
+  const size_t lds = FilterLds<D, BF, NW>::bytes();
+  hipLaunchKernelGGL((mfma_filter<D, MET, IVF, KR, BF, NW>), dim3(max_items), dim3(64 * NW), lds, st, a);
 }
 
 template <int D, int MET, bool IVF, int KR>
 void launch_filter_t(const FilterArgs &a, int max_items, hipStream_t st) {
-  if (a.prec == FILTER_BF16X3) launch_filter_p<D, MET, IVF, KR, true>(a, max_items, st);
-  else launch_filter_p<D, MET, IVF, KR, false>(a, max_items, st);
+  if (a.prec == FILTER_BF16X3) {
+    if (a.waves == 8) launch_filter_p<D, MET, IVF, KR, true, 8>(a, max_items, st);
+    else launch_filter_p<D, MET, IVF, KR, true, 4>(a, max_items, st);
+  } else {
+    launch_filter_p<D, MET, IVF, KR, false, 4>(a, max_items, st);
+  }
 }
 
 template <int D, int MET, bool IVF>

@@ -237,14 +237,17 @@ struct FilterArgs {
   uint32_t *gthr;          // shared per-query bound in approximate-score space, or null
   int32_t ablate;          // measurement only (PYR_FILTER_ABLATE; results are wrong when set):
                            // 1 skip the owner filter, 2 skip the score transpose, 4 skip row loads, 8 skip MFMA,
-                           // 16 filter without inserting
+                           // 16 filter without inserting, 32 insert directly (no candidate buffer)
   int32_t pub_mask;        // publish / refresh the shared bound when (stage & pub_mask) == pub_mask
   uint32_t *dbg;           // measurement only (PYR_FILTER_DEBUG): [0] insert-loop iterations of
                            // all waves, [1] candidates inserted, [2] owner stages, or null
   int32_t prec;            // FILTER_FP32 or FILTER_BF16X3 (approximate-score arithmetic)
+  int32_t waves;           // waves per block = items' queries / 32: 4, or 8 (bf16x3 only)
 };
 constexpr int FILTER_FP32 = 0;    // v_mfma_f32_32x32x2_f32
 constexpr int FILTER_BF16X3 = 1;  // hi/lo bf16 split, 3 x v_mfma_f32_32x32x16_bf16
+// queries per filter work item (items must be built with this qchunk)
+inline int filter_qchunk(int prec, int waves) { return prec == FILTER_BF16X3 && waves == 8 ? 256 : 128; }
 // refine_kernel error-bound constant of the bf16x3 approximation (per u |q| max|x|)
 inline double filter_bf16x3_cerr(int dim, int metric) {
   // q.x: <= 3.02 * 2^-16 per product from the splits, <= 2u per addition over 3D terms;

@@ -78,9 +78,9 @@ def test_flat_filter_equals_exact_and_oracle(hiplib, oracle, metric, dim, prec):
     assert nfb < len(q)  # the certificate holds for (almost) every query of uniform data
 
 
-@pytest.mark.parametrize("prec", ["1", "0"])
+@pytest.mark.parametrize("prec,waves", [("1", "8"), ("1", "4"), ("0", "4")])  # PYR_FILTER_PREC, _WAVES
 @pytest.mark.parametrize("metric", [0, 1])
-def test_ivf_filter_equals_exact_and_oracle(hiplib, oracle, metric, prec):
+def test_ivf_filter_equals_exact_and_oracle(hiplib, oracle, metric, prec, waves):
     from pyrope_amd import IvfFlatVectorIndex, SearchOptions, generate_synthetic
     x = generate_synthetic(20000, 128, 42)
     idx = IvfFlatVectorIndex(128, metric, n_list=64)
@@ -88,7 +88,7 @@ def test_ivf_filter_equals_exact_and_oracle(hiplib, oracle, metric, prec):
     idx.build()
     q = generate_synthetic(500, 128, 1337)
     opts = SearchOptions(nprobe=8)
-    with _env(PYR_FILTER_PREC=prec):
+    with _env(PYR_FILTER_PREC=prec, PYR_FILTER_WAVES=waves):
         got = idx.search_batch(q, 10, opts)
     with _env(PYR_FILTER=0):
         ref = idx.search_batch(q, 10, opts)
