@@ -14,7 +14,8 @@ all_gather: per-GPU work is fixed as N grows ("weak").
 
 Besides the QPS line the JSON carries:
   roofline      the dominant kernel (IVF list scan) timed with HIP events on its own
-                stream, algorithmic FLOPs = (query,row) pairs x 3*D, against the FP32 peak
+                stream: unique algorithmic bytes (every probed list once + queries) per
+                launch against the HBM peak; "mfma" gives the as-executed MFMA rate
   cpu_baseline  the CPU restatement (oracle/, the reference's algorithm) on the host
                 cores, on a bounded query sample of the same index; its answers are also
                 compared with the GPU's (ids equal, scores bit-identical)
@@ -34,6 +35,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP32_PEAK_TFLOPS = 157.3   # MI355X FP32 vector == FP32 matrix peak (MI355X_MICROARCH.md)
+BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA peak (MI355X_MICROARCH.md, no sparsity)
 HBM_PEAK_GBS = 8000.0      # HBM3E spec peak
 
 
@@ -169,6 +171,20 @@ def main():
     # (PYR_FILTER=0): sub, mul, add per element, 3*D
     flops = scan["pairs"] * (2 if filt else 3) * D
     achieved = flops / (scan["ms"] * 1e-3) / 1e12
+    bf16x3 = filt and os.environ.get("PYR_FILTER_PREC", "1") != "0"
+    # unique algorithmic bytes of one list-scan launch: every list probed by any query of the
+    # batch read once (its live rows x D x 4 B) plus the batch's queries -- the HBM floor of a
+    # batched, list-major scan (SURVEY.md 8(d) "unique-bytes roofline")
+    pr_full = torch.empty((Q, args.nprobe), dtype=torch.int32, device=dev)
+    width = idx.probe_device(q.data_ptr(), Q, pr_full.data_ptr(), 0, opts)
+    torch.cuda.synchronize()
+    off_l, lab_l, live_l = idx.ivf_layout()
+    cs_live = np.concatenate([[0], np.cumsum(live_l.astype(np.int64))])
+    rows_per_list = cs_live[off_l[1:]] - cs_live[off_l[:-1]]
+    probed = np.unique(pr_full[:, :width].cpu().numpy())
+    probed = probed[probed >= 0]
+    unique_bytes = float(rows_per_list[probed].sum()) * D * 4 + Q * D * 4
+    hbm_achieved = unique_bytes / (scan["ms"] * 1e-3) / 1e9
 
     # ---- recall@10 vs exact FLAT top-10 (rank 0) ----
     recall = None
@@ -232,15 +248,22 @@ def main():
                        "shard": "rows-within-list (row i on rank i % n_gpus), shared quantizer",
                        "merge": "RCCL all_gather of partial top-k + on-device merge" if world > 1 else "none"},
             "recall_at_10": recall,
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None,
-                         "kernel": ("mfma_filter<128,L2,IVF> (IVF list scan, fp32 MFMA candidate filter)" if filt
+            "roofline": {"bound": "hbm", "achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": hbm_achieved / HBM_PEAK_GBS, "traffic": None,
+                         "unique_bytes_per_launch": unique_bytes, "lists_probed": int(len(probed)),
+                         "kernel": ("mfma_filter<128,L2,IVF> (IVF list scan, bf16x3 MFMA candidate filter)"
+                                    if bf16x3 else
+                                    "mfma_filter<128,L2,IVF> (IVF list scan, fp32 MFMA candidate filter)" if filt
                                     else "scan_fast<128,1,L2,IVF> (IVF list scan, exact VALU)"),
-                         "note": ("dense FP32 MFMA peak; algorithmic FLOPs = probed (query,row) pairs x 2*D per "
-                                  "launch (the q.x GEMM; |x|^2 precomputed), HIP-event time of the launch"
-                                  if filt else
-                                  "FP32 peak; algorithmic FLOPs = probed pairs x 3*D (sub, mul, add) per launch; "
-                                  "non-FMA VALU ops top out at half this peak")},
+                         "note": ("algorithmic bytes = every probed list read once per launch (live rows x D x "
+                                  "4 B) + queries, over the HIP-event time of the launch; traffic (FETCH_SIZE, "
+                                  "measured in its own rocprofv3 pass) is in profiles/*/summary.md")},
+            "mfma": {"achieved": achieved * (3 if bf16x3 else 1),
+                     "peak": BF16_PEAK_TFLOPS if bf16x3 else FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved * (3 if bf16x3 else 1) / (BF16_PEAK_TFLOPS if bf16x3 else FP32_PEAK_TFLOPS),
+                     "note": ("as-executed bf16 MFMA flops: probed (query,row) pairs x 2*D x 3 (hi.hi, hi.lo, "
+                              "lo.hi) vs the dense bf16 peak" if bf16x3 else
+                              "probed pairs x 2*D (fp32 MFMA) or x 3*D (exact VALU) vs the FP32 peak")},
             "exact_reruns": {"queries": fallback_queries, "in_profiled_steps": args.profile_steps,
                              "note": "queries whose MFMA-filter certificate failed and were re-scanned exactly"},
             "hbm_equivalent": {"bytes_per_query": bytes_per_query,

@@ -278,6 +278,11 @@ static int filter_waves_ivf() {
   const int w = e ? atoi(e) : 4;
   return (w == 8 && filter_prec() == FILTER_BF16X3) ? 8 : 4;
 }
+// XCD-major mapping of IVF filter items (FilterArgs::xcd); PYR_FILTER_XCD=0 disables it
+static int filter_xcd() {
+  const char *e = getenv("PYR_FILTER_XCD");
+  return e ? (atoi(e) != 0) : 1;
+}
 static int filter_ablate() {  // measurement only (FilterArgs::ablate)
   const char *e = getenv("PYR_FILTER_ABLATE");
   return e ? atoi(e) : 0;
@@ -1208,6 +1213,7 @@ struct IvfFlatIndex : Index {
     fa.pub_mask = filter_pub_mask();
     fa.prec = filter_prec();
     fa.waves = waves;
+    fa.xcd = filter_xcd();
     DevMem dbg;
     if (getenv("PYR_FILTER_DEBUG")) {  // measurement only: insert statistics to stderr
       dbg.ensure(16);

@@ -106,8 +106,17 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void mfma_filter(FilterArgs a) {
   constexpr int KH = D / 2;  // fp32 k-steps: lanes 0-31 take dims [0, KH), lanes 32-63 [KH, D)
   constexpr int KS = D / 16;  // bf16 k-steps: lane half h takes dims 16s + 8h .. +7 of step s
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  if ((int)blockIdx.x >= *a.n_items) return;
-  const ScanItem it = a.items[blockIdx.x];
+  // XCD-major item mapping (a.xcd; grid a multiple of 8): block b runs on XCD b % 8, so
+  // giving each XCD a contiguous run of items puts a list chunk's query groups (adjacent
+  // items) on one XCD at about the same time -- the later groups read the rows from its L2
+  int item = blockIdx.x;
+  if (a.xcd) {
+    const int per = (*a.n_items + 7) >> 3;
+    item = ((int)blockIdx.x & 7) * per + ((int)blockIdx.x >> 3);
+    if ((int)(blockIdx.x >> 3) >= per) return;
+  }
+  if (item >= *a.n_items) return;
+  const ScanItem it = a.items[item];
   float *rt = smem;                                          // fp32: [2][RT][RSTR]
   uint16_t *bt = reinterpret_cast<uint16_t *>(smem);         // bf16: [2][hi, lo][RT][BSTR]
   float *scw = smem + L::tiles_bytes() / sizeof(float);      // [4][32][SCR]
@@ -601,7 +610,8 @@ void launch_filter_p(const FilterArgs &a, int max_items, hipStream_t st) {
     attr = true;
   }
   const size_t lds = FilterLds<D, BF, NW>::bytes();
-  hipLaunchKernelGGL((mfma_filter<D, MET, IVF, KR, BF, NW>), dim3(max_items), dim3(64 * NW), lds, st, a);
+  const int grid = a.xcd ? (max_items + 7) / 8 * 8 : max_items;
+  hipLaunchKernelGGL((mfma_filter<D, MET, IVF, KR, BF, NW>), dim3(grid), dim3(64 * NW), lds, st, a);
 }
 
 template <int D, int MET, bool IVF, int KR>

@@ -243,6 +243,7 @@ struct FilterArgs {
                            // all waves, [1] candidates inserted, [2] owner stages, or null
   int32_t prec;            // FILTER_FP32 or FILTER_BF16X3 (approximate-score arithmetic)
   int32_t waves;           // waves per block = items' queries / 32: 4, or 8 (bf16x3 only)
+  int32_t xcd;             // 1: XCD-major item -> block mapping
 };
 constexpr int FILTER_FP32 = 0;    // v_mfma_f32_32x32x2_f32
 constexpr int FILTER_BF16X3 = 1;  // hi/lo bf16 split, 3 x v_mfma_f32_32x32x16_bf16
