@@ -648,6 +648,7 @@ struct FlatIndex : Index {
     fa.pub_mask = filter_pub_mask();
     fa.prec = filter_prec();
     fa.waves = 4;  // items of QCHUNK = 128 queries (plan_flat)
+    fa.xcd = getenv("PYR_FLAT_XCD") ? atoi(getenv("PYR_FLAT_XCD")) != 0 : 0;  // measurement knob
     {
       PhaseTimer t(PH_FLAT_SCAN, ws.st, nq * cutoff);
       launch_filter(fa, metric, p.nitems, ws.st);

@@ -94,6 +94,24 @@ def main():
     torch.cuda.set_device(0)
     import oracle  # parity check of a sample only
 
+    def run_sweep(idx, q, opts, s, lab):
+        """time the same index under each env setting of --sweep (results compared with the default's)"""
+        for setting in [x for x in a.sweep.split("|") if x]:
+            kv = dict(t.split("=") for t in setting.split(","))
+            old = {k_: os.environ.get(k_) for k_ in kv}
+            os.environ.update(kv)
+            qps2, ms2, ph2, s2, l2 = timed(idx, q, a.nq, a.k, opts, a.steps, a.warmup, L)
+            for k_, v in old.items():
+                if v is None:
+                    os.environ.pop(k_, None)
+                else:
+                    os.environ[k_] = v
+            print(json.dumps({"sweep": setting, "qps": qps2, "ms_per_step": ms2,
+                              "phases_ms": {k_: v["ms"] for k_, v in ph2.items()},
+                              "same_results": bool(np.array_equal(l2, lab) and np.array_equal(s2.view(np.uint32),
+                                                                                             s.view(np.uint32)))}),
+                  flush=True)
+
     if a.workload == "flat":
         n, d = a.n or 1_000_000, a.dim or 128
         x = generate_synthetic(n, d, 42)
@@ -104,6 +122,7 @@ def main():
         idx.add_labels(np.arange(n, dtype=np.int64), x)
         q = torch.from_numpy(qh).cuda()
         qps, ms, phases, s, lab = timed(idx, q, a.nq, a.k, None, a.steps, a.warmup, L)
+        run_sweep(idx, q, None, s, lab)
         ok = True
         for i in np.linspace(0, a.nq - 1, a.check).astype(int):
             if a.quant:
@@ -131,21 +150,7 @@ def main():
         q = torch.from_numpy(qh).cuda()
         opts = SearchOptions(nprobe=a.nprobe)
         qps, ms, phases, s, lab = timed(idx, q, a.nq, a.k, opts, a.steps, a.warmup, L)
-        for setting in [x for x in a.sweep.split("|") if x]:
-            kv = dict(t.split("=") for t in setting.split(","))
-            old = {k_: os.environ.get(k_) for k_ in kv}
-            os.environ.update(kv)
-            qps2, ms2, ph2, s2, l2 = timed(idx, q, a.nq, a.k, opts, a.steps, a.warmup, L)
-            for k_, v in old.items():
-                if v is None:
-                    os.environ.pop(k_, None)
-                else:
-                    os.environ[k_] = v
-            print(json.dumps({"sweep": setting, "qps": qps2, "ms_per_step": ms2,
-                              "phases_ms": {k_: v["ms"] for k_, v in ph2.items()},
-                              "same_results": bool(np.array_equal(l2, lab) and np.array_equal(s2.view(np.uint32),
-                                                                                             s.view(np.uint32)))}),
-                  flush=True)
+        run_sweep(idx, q, opts, s, lab)
         cb, codes, off, labels, live = idx.pq_state()
         cents = idx.centroids_array()
         ok = True
