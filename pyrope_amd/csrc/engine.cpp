@@ -1215,6 +1215,7 @@ struct IvfFlatIndex : Index {
     fa.prec = filter_prec();
     fa.waves = waves;
     fa.xcd = filter_xcd();
+    fa.single = getenv("PYR_FILTER_SB") ? atoi(getenv("PYR_FILTER_SB")) != 0 : 0;
     DevMem dbg;
     if (getenv("PYR_FILTER_DEBUG")) {  // measurement only: insert statistics to stderr
       dbg.ensure(16);

@@ -119,7 +119,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void mfma_filter(FilterArgs a) {
   const ScanItem it = a.items[item];
   float *rt = smem;                                          // fp32: [2][RT][RSTR]
   uint16_t *bt = reinterpret_cast<uint16_t *>(smem);         // bf16: [2][hi, lo][RT][BSTR]
-  float *scw = smem + L::tiles_bytes() / sizeof(float);      // [4][32][SCR]
+  // a.single (bf16x3): one row-tile buffer (two barriers per stage) so that three blocks fit a CU
+  const bool single = BF && a.single;
+  float *scw = smem + (single ? L::tiles_bytes() / 2 : L::tiles_bytes()) / sizeof(float);  // [NW][32][SCR]
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int i32 = lane & 31, h = lane >> 5;
@@ -295,7 +297,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void mfma_filter(FilterArgs a) {
   __syncthreads();
 
   for (int st = 0; st < nst; ++st) {
-    const int cur = st & 1;
+    const int cur = single ? 0 : st & 1;
     const int row = r0 + st * RT + i32;
     const bool rvalid = row < it.row_end && (uint32_t)row < a.row_limit && lv_next;
     const float xsq = xsq_next;
@@ -341,8 +343,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void mfma_filter(FilterArgs a) {
         sc[i32] = acc[1];  // keep the MFMAs alive in the ablated build
       }
     }
-    if (st + 1 < nst && !(a.ablate & 4)) store_stage(cur ^ 1);
-    __syncthreads();  // next tile staged; this wave's score transpose visible
+    if (!single && st + 1 < nst && !(a.ablate & 4)) store_stage(cur ^ 1);
+    __syncthreads();  // next tile staged (single: every wave done with this tile); score transpose visible
+    if (single && st + 1 < nst && !(a.ablate & 4)) store_stage(0);
 
     // pre-filter against the owner's bound (the full (score, key) test follows): lane half
     // h tests rows 16h .. 16h + 15 of query i32, the owner joins the two masks
@@ -410,6 +413,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void mfma_filter(FilterArgs a) {
         gs = fmaxf(gs, key_score(__hip_atomic_load(a.gthr + qown, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
       }
     }
+    if (single) __syncthreads();  // the next tile is staged
   }
   if (owner) {
     for (int i = 0; i < nbuf; ++i) {  // drain the candidate buffer
@@ -609,7 +613,7 @@ void launch_filter_p(const FilterArgs &a, int max_items, hipStream_t st) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  const size_t lds = FilterLds<D, BF, NW>::bytes();
+  const size_t lds = FilterLds<D, BF, NW>::bytes() - (BF && a.single ? FilterLds<D, BF, NW>::tiles_bytes() / 2 : 0);
   const int grid = a.xcd ? (max_items + 7) / 8 * 8 : max_items;
   hipLaunchKernelGGL((mfma_filter<D, MET, IVF, KR, BF, NW>), dim3(grid), dim3(64 * NW), lds, st, a);
 }

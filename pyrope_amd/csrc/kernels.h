@@ -244,6 +244,7 @@ struct FilterArgs {
   int32_t prec;            // FILTER_FP32 or FILTER_BF16X3 (approximate-score arithmetic)
   int32_t waves;           // waves per block = items' queries / 32: 4, or 8 (bf16x3 only)
   int32_t xcd;             // 1: XCD-major item -> block mapping
+  int32_t single;          // 1: single-buffered row tiles (bf16x3; smaller LDS, 2 barriers per stage)
 };
 constexpr int FILTER_FP32 = 0;    // v_mfma_f32_32x32x2_f32
 constexpr int FILTER_BF16X3 = 1;  // hi/lo bf16 split, 3 x v_mfma_f32_32x32x16_bf16
