@@ -191,7 +191,10 @@ static ScanPlan plan_flat(int64_t nrows, int64_t nq, int dim, int k, int max_par
   ScanPlan p;
   p.qchunk = fast_path(dim, k) ? QCHUNK : QCHUNK_GENERIC;
   const int64_t nqc = (nq + p.qchunk - 1) / p.qchunk;
-  int64_t want = std::max<int64_t>(1, (2048 + nqc - 1) / nqc);
+  // ~2048 items = 4 full rounds of 512 resident blocks (256 CUs x 2); rounding DOWN keeps the
+  // item count at or below that: rounding up (e.g. 79 query groups x 26 chunks = 2054 items)
+  // left a fifth round of 6 items that cost a whole item duration
+  int64_t want = std::max<int64_t>(1, 2048 / nqc);
   want = std::min<int64_t>(want, std::max<int64_t>(1, nrows / 1024));
   want = std::min<int64_t>(want, max_parts);
   p.chunk_rows = (int)round_up((nrows + want - 1) / want, 8);
