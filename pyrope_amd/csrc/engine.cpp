@@ -927,9 +927,9 @@ static bool ivf_seed_enabled() {
 // the MAX_PARTS budget left after `other_parts` and a cap on the partial buffer.
 // PYR_IVF_CHUNK / PYR_IVF_WARM override the defaults for measurements.
 static IvfChunking ivf_chunking(int64_t max_len, int probes, int other_parts, int64_t nq, int k, bool bounds) {
-  // 4096 rows: 5.71 -> 5.27 ms over 2048 at the bench config (profiles/r1_sweeps/sweep21); warm-up
-  // launch measured neutral (profiles/)
-  int64_t chunk = 4096, warm = 0;
+  // 5120 rows: 2048 -> 4096 -> 5120 gave 5.71 -> 5.27 -> ~5.2 ms at the bench config
+  // (profiles/r1_sweeps/sweep21, sweep28, sweep29); warm-up launch measured neutral (profiles/)
+  int64_t chunk = 5120, warm = 0;
   if (const char *e = getenv("PYR_IVF_CHUNK")) chunk = std::max<int64_t>(8, atoll(e));
   if (const char *e = getenv("PYR_IVF_WARM")) warm = std::max<int64_t>(0, atoll(e));
   if (!bounds) warm = 0;  // the warm-up launch only pays with shared bounds
