@@ -1,31 +1,40 @@
 #!/usr/bin/env python3
 """bench.py -- QPS + recall@10 of the IVF_FLAT scan on MI355X (BASELINE.json metric).
 
-Workload (BASELINE.json configs[2]): IVF_FLAT d=128, N=10M base vectors, nlist=1024,
-nprobe=32, top-10, synthetic uniform [0,1) vectors from the reference benchmark's
-generator (Pyrope.Benchmarks/Program.cs:251-263: base seed 42, query seed 1337).
+Workload (BASELINE.json configs[2], I1): IVF_FLAT d=128, N=10M base vectors, nlist=1024,
+nprobe=32, top-10, synthetic uniform [0,1) vectors from the reference benchmark's generator
+(Pyrope.Benchmarks/Program.cs:251-263) in row blocks of 65,536 rows (block b = Random(42 + b),
+SURVEY.md 8(d)'s large-N deviation; queries = Random(1337)).  `--n 80000000 --nlist 8192`
+is configs[4] (M8).
 
-A step = one batched search of the query batch (10,000 queries per GPU), queries
-and results resident in HBM.  With --gpus N (one process per GPU, RCCL), the
-index is sharded rows-within-list (every rank holds row i iff i % N == rank, all
-ranks share one coarse quantizer), every rank scans its shard for the global
-batch (10,000 x N queries), and partial top-k lists are merged after an RCCL
-all_gather: per-GPU work is fixed as N grows ("weak").
+A step = one batched search of 10,000 queries per GPU, queries and results resident in HBM.
+
+--gpus N: one process per GPU.  Launched by torch.distributed.run (RANK/WORLD_SIZE set) the
+ranks are used as they are; `python bench.py --gpus N` alone starts the N rank processes
+itself (spawn, before anything touches a GPU).  The base set is sharded by generator blocks
+(rank r owns the blocks b % N == r and generates only those), the coarse quantizer is trained
+once on rank 0 and broadcast, and each step runs pyrope_amd.dist.sharded_ivf_step: every rank
+ranks the quantizer for its 10,000-query slice, an RCCL all_gather assembles the probe lists,
+every rank scans its shard for the whole N x 10,000 batch, and an RCCL all_gather of the
+partial top-k plus an on-device merge gives the answer.  Per-GPU work is fixed as N grows
+("weak").
 
 Besides the QPS line the JSON carries:
-  roofline      the dominant kernel (IVF list scan) timed with HIP events on its own
-                stream: unique algorithmic bytes (every probed list once + queries) per
-                launch against the HBM peak; "mfma" gives the as-executed MFMA rate
-  cpu_baseline  the CPU restatement (oracle/, the reference's algorithm) on the host
-                cores, on a bounded query sample of the same index; its answers are also
+  roofline      the dominant kernel (IVF list scan) timed with HIP events on its own stream:
+                unique algorithmic bytes (every probed list once + queries) per launch against
+                the HBM peak; "mfma" gives the as-executed MFMA rate
+  cpu_baseline  the CPU restatement (oracle/, the reference's algorithm) on the host cores, on
+                a bounded query sample of the same index (N = 1 only); its answers are also
                 compared with the GPU's (ids equal, scores bit-identical)
-  recall_at_10  vs exact FLAT top-10 over the full data (GPU FLAT index)
+  recall_at_10  vs the exact FLAT top-10 over the full data (per-rank FLAT shards + merge)
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -43,7 +52,7 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def main():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -54,74 +63,191 @@ def main():
     ap.add_argument("--nprobe", type=int, default=32)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--nq", type=int, default=10_000, help="queries per GPU per step")
+    ap.add_argument("--block-rows", type=int, default=65536, help="generator block (sharding unit)")
+    ap.add_argument("--train-rows", type=int, default=10_000_000,
+                    help="k-means runs on the first min(N, this) rows (all of I1)")
+    ap.add_argument("--add-rows", type=int, default=2_000_000, help="rows per bulk add call")
     ap.add_argument("--recall-queries", type=int, default=1000)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline time (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use")
     ap.add_argument("--profile-steps", type=int, default=3)
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
+
+# ---------------------------------------------------------------------------------------------
+# host CPU description for cpu_baseline ("report the lscpu model, sockets, cores")
+# ---------------------------------------------------------------------------------------------
+def cgroup_cpu_quota():
+    """CPUs granted by a cgroup v2 (cpu.max) or v1 (cfs quota) limit, or None."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return float(q) / float(p)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return q / p
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def host_cpus():
+    info = {"cpu_count": os.cpu_count()}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        info["affinity"] = os.cpu_count()
+    quota = cgroup_cpu_quota()
+    info["cgroup_quota_cpus"] = quota
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k in ("Model name", "Socket(s)", "Core(s) per socket", "Thread(s) per core", "CPU(s)"):
+                info[{"Model name": "model", "Socket(s)": "sockets", "Core(s) per socket": "cores_per_socket",
+                      "Thread(s) per core": "threads_per_core", "CPU(s)": "lscpu_cpus"}[k]] = v
+    except (OSError, subprocess.SubprocessError):
+        pass
+    usable = info["affinity"] or 1
+    if quota:
+        usable = max(1, min(usable, int(quota)))
+    info["usable"] = usable
+    return info
+
+
+# ---------------------------------------------------------------------------------------------
+# rank processes
+# ---------------------------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_entry(rank, world, port, argv):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    run(parse(argv))
+
+
+def spawn_ranks(args, argv):
+    """`--gpus N` without a launcher: N fresh rank processes (this process never touches a GPU)."""
+    import torch.multiprocessing as mp
+    log(f"--gpus {args.gpus} without a launcher: starting {args.gpus} rank processes")
+    mp.start_processes(_rank_entry, args=(args.gpus, _free_port(), argv), nprocs=args.gpus, join=True,
+                       start_method="spawn")
+
+
+# ---------------------------------------------------------------------------------------------
+# the benchmark proper (one rank)
+# ---------------------------------------------------------------------------------------------
+def run(args):
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    from pyrope_amd import IvfFlatVectorIndex, VectorMetric, generate_synthetic, kmeans_train, _lib
+    from pyrope_amd import (BruteForceVectorIndex, IvfFlatVectorIndex, VectorMetric, _lib, generate_synthetic,
+                            generate_synthetic_blocked, kmeans_train)
     from pyrope_amd.build import build
+    from pyrope_amd.dist import gather_partials, merge_device, shard_blocks, sharded_ivf_step
+    from pyrope_amd.vector import SearchOptions
     build()
     L = _lib.load()
 
-    D, N, k = args.dim, args.n, args.k
-    t = time.time()
-    data = generate_synthetic(N, D, 42)  # every rank regenerates the same base set
-    log(f"rank {rank}: generated {N}x{D} in {time.time() - t:.1f}s")
-    t = time.time()
-    cents = kmeans_train(data, args.nlist, VectorMetric.L2, 10, 42, device=local)  # IvfFlat.Build: seed 42
-    log(f"rank {rank}: k-means nlist={len(cents)} in {time.time() - t:.1f}s")
+    D, N, k, B = args.dim, args.n, args.k, args.block_rows
+    blocks = shard_blocks(N, world, rank, B)
+
+    def shard_chunks():
+        """(labels, rows) of this rank's blocks, <= add_rows rows per chunk (regenerated on demand)."""
+        i = 0
+        while i < len(blocks):
+            j, rows = i, 0
+            while j < len(blocks) and (rows == 0 or rows + blocks[j][1] - blocks[j][0] <= args.add_rows):
+                rows += blocks[j][1] - blocks[j][0]
+                j += 1
+            labs = np.concatenate([np.arange(a, b, dtype=np.int64) for a, b in blocks[i:j]])
+            x = np.concatenate([generate_synthetic_blocked(a, b - a, D, 42, B) for a, b in blocks[i:j]])
+            yield labs, x
+            i = j
+
+    # 1) the coarse quantizer: KMeansUtils.Train (IvfFlatVectorIndex.Build, seed 42) over the first
+    #    min(N, train_rows) rows, once, on rank 0; every shard builds with the same centroids
+    T = min(N, args.train_rows)
+    nl = max(1, min(args.nlist, T))
+    ct = torch.empty((nl, D), dtype=torch.float32, device=dev)
+    if rank == 0:
+        t = time.time()
+        train = generate_synthetic_blocked(0, T, D, 42, B)
+        cents = kmeans_train(train, args.nlist, VectorMetric.L2, 10, 42, device=local)
+        del train
+        assert cents.shape == (nl, D)
+        ct.copy_(torch.from_numpy(cents))
+        log(f"k-means nlist={nl} over {T} rows in {time.time() - t:.1f}s")
+    if world > 1:
+        dist.broadcast(ct, 0)
+    cents = ct.cpu().numpy()
+
+    # 2) this rank's shard (IvfFlat Add into the buffer, then Build = assignment with the given quantizer)
     t = time.time()
     idx = IvfFlatVectorIndex(D, VectorMetric.L2, n_list=args.nlist, device=local)
     idx.set_centroids(cents)
-    from pyrope_amd.dist import shard_labels
-    shard = shard_labels(N, world, rank)
-    idx.add_labels(shard, data[rank::world])
+    keep = world == 1 and args.cpu_seconds > 0  # the CPU baseline reads base rows
+    kept = []
+    nrows = 0
+    for labs, x in shard_chunks():
+        idx.add_labels(labs, x, track_ids=False)
+        nrows += len(labs)
+        if keep:
+            kept.append(x)
     idx.build()
-    log(f"rank {rank}: shard of {len(shard)} rows indexed in {time.time() - t:.1f}s")
+    data = np.concatenate(kept) if keep else None  # world == 1: rows in base-row (= label) order
+    del kept
+    log(f"rank {rank}: shard of {nrows} rows ({len(blocks)} blocks) generated + indexed in {time.time() - t:.1f}s")
 
     Q = args.nq * world
     qh = generate_synthetic(Q, D, 1337)
     q = torch.from_numpy(qh).to(dev)
+    opts = SearchOptions(nprobe=args.nprobe)
+    width = max(0, min(args.nprobe, nl))
     s_loc = torch.empty((Q, k), dtype=torch.float32, device=dev)
     l_loc = torch.empty((Q, k), dtype=torch.int64, device=dev)
-    from pyrope_amd.dist import gather_partials, merge_device
-    from pyrope_amd.vector import SearchOptions
-    opts = SearchOptions(nprobe=args.nprobe)
+    pr_loc = torch.empty((args.nq, width), dtype=torch.int32, device=dev)
     result = [s_loc, l_loc]
 
-    # N > 1: the coarse ranking is split too -- rank r ranks the quantizer for its own nq-query
-    # slice of the batch and one all_gather assembles every query's probe lists -- so per-GPU
-    # work stays fixed as N grows (every rank would otherwise rank the whole N x nq batch)
-    pr_loc = torch.empty((args.nq, args.nprobe), dtype=torch.int32, device=dev)
-    pr_all = torch.empty((Q, args.nprobe), dtype=torch.int32, device=dev)
+    def probe(qs):  # this rank's slice of the batch (pyr_index_probe_device)
+        w = idx.probe_device(qs.data_ptr(), qs.shape[0], pr_loc.data_ptr(), torch.cuda.current_stream().cuda_stream,
+                             opts)
+        assert w == width
+        return pr_loc
+
+    def search(qs, probes):  # every query against this rank's shard, the gathered probe lists
+        idx.search_device(qs.data_ptr(), qs.shape[0], k, s_loc.data_ptr(), l_loc.data_ptr(), 0,
+                          torch.cuda.current_stream().cuda_stream, opts, d_probes=probes.data_ptr(), nprobe=width)
+        return s_loc, l_loc
+
+    def merge(sp, lp, kk):  # RCCL all_gather'ed partial top-k -> on-device merge
+        return merge_device(sp, lp, kk, torch.cuda.current_stream().cuda_stream)
 
     def step():
-        stream = torch.cuda.current_stream().cuda_stream
         if world == 1:
-            idx.search_device(q.data_ptr(), Q, k, s_loc.data_ptr(), l_loc.data_ptr(), 0, stream, opts)
+            idx.search_device(q.data_ptr(), Q, k, s_loc.data_ptr(), l_loc.data_ptr(), 0,
+                              torch.cuda.current_stream().cuda_stream, opts)
             return
-        q_mine = q[rank * args.nq:(rank + 1) * args.nq]
-        width = idx.probe_device(q_mine.data_ptr(), args.nq, pr_loc.data_ptr(), stream, opts)
-        dist.all_gather_into_tensor(pr_all, pr_loc)
-        idx.search_device(q.data_ptr(), Q, k, s_loc.data_ptr(), l_loc.data_ptr(), 0, stream, opts,
-                          d_probes=pr_all.data_ptr(), nprobe=width)
-        # RCCL all_gather over xGMI of per-GPU partial top-k, then on-device merge
-        sp, lp = gather_partials(s_loc, l_loc, world)
-        result[:] = merge_device(sp, lp, k, stream)
+        result[:] = sharded_ivf_step(q, args.nq, rank, world, probe, search, merge, k)
 
     def barrier():
         if world > 1:
@@ -172,59 +298,76 @@ def main():
     flops = scan["pairs"] * (2 if filt else 3) * D
     achieved = flops / (scan["ms"] * 1e-3) / 1e12
     bf16x3 = filt and os.environ.get("PYR_FILTER_PREC", "1") != "0"
-    # unique algorithmic bytes of one list-scan launch: every list probed by any query of the
-    # batch read once (its live rows x D x 4 B) plus the batch's queries -- the HBM floor of a
-    # batched, list-major scan (SURVEY.md 8(d) "unique-bytes roofline")
-    pr_full = torch.empty((Q, args.nprobe), dtype=torch.int32, device=dev)
-    width = idx.probe_device(q.data_ptr(), Q, pr_full.data_ptr(), 0, opts)
+    # unique algorithmic bytes of one list-scan launch on this rank: every list probed by any query
+    # of the batch read once (its live rows of this shard x D x 4 B) plus the batch's queries -- the
+    # HBM floor of a batched, list-major scan (SURVEY.md 8(d) "unique-bytes roofline")
+    pr_full = torch.empty((Q, width), dtype=torch.int32, device=dev)
+    idx.probe_device(q.data_ptr(), Q, pr_full.data_ptr(), 0, opts)
     torch.cuda.synchronize()
     off_l, lab_l, live_l = idx.ivf_layout()
     cs_live = np.concatenate([[0], np.cumsum(live_l.astype(np.int64))])
     rows_per_list = cs_live[off_l[1:]] - cs_live[off_l[:-1]]
-    probed = np.unique(pr_full[:, :width].cpu().numpy())
+    probed = np.unique(pr_full.cpu().numpy())
     probed = probed[probed >= 0]
     unique_bytes = float(rows_per_list[probed].sum()) * D * 4 + Q * D * 4
     hbm_achieved = unique_bytes / (scan["ms"] * 1e-3) / 1e9
+    del pr_full
 
-    # ---- recall@10 vs exact FLAT top-10 (rank 0) ----
+    # ---- recall@10 vs the exact FLAT top-10 over all N rows: per-rank FLAT shard + merge ----
     recall = None
     s_fin = result[0].cpu().numpy()
     l_fin = result[1].cpu().numpy()
-    if rank == 0 and args.recall_queries > 0:
-        from pyrope_amd import BruteForceVectorIndex
+    if args.recall_queries > 0:
+        t = time.time()
         R = min(args.recall_queries, Q)
         flat = BruteForceVectorIndex(D, VectorMetric.L2, device=local)
-        flat.add_labels(np.arange(N, dtype=np.int64), data)
-        _, gt, _ = flat.search_batch(qh[:R], k)
+        for labs, x in shard_chunks():
+            flat.add_labels(labs, x, track_ids=False)
+        fs, fl, _ = flat.search_batch(qh[:R], k)
         flat.close()
+        gs, gl = torch.from_numpy(fs).to(dev), torch.from_numpy(fl).to(dev)
+        if world > 1:
+            sp, lp = gather_partials(gs, gl, world)
+            gs, gl = merge_device(sp, lp, k, torch.cuda.current_stream().cuda_stream)
+        gt = gl.cpu().numpy()
         hits = sum(len(set(gt[i].tolist()) & set(l_fin[i].tolist())) for i in range(R))
         recall = hits / (R * k)
-        log(f"recall@10 over {R} queries: {recall:.4f}")
+        log(f"recall@10 over {R} queries: {recall:.4f} ({time.time() - t:.1f}s)")
 
     # ---- CPU baseline: the oracle (CPU restatement of the reference engine) on the same index ----
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         import oracle  # checker / CPU baseline only
-        off, labels, live = idx.ivf_layout()
-        rows = data[labels]
-        cts = idx.centroids_array()
-        threads = max(1, min(16, os.cpu_count() or 1))
+        host = host_cpus()
+        threads = args.cpu_threads or host["usable"]
+        lab_rows = np.where(lab_l >= 0, lab_l, 0)  # list-major position -> base row (labels are row ids)
+        # list-major copy of the rows when it fits (contiguous list scans: the faster CPU baseline), else
+        # the base rows read through the layout's row index
+        lrows = data[lab_rows] if data.nbytes <= (16 << 30) else None
+
+        def cpu_run(S):
+            if lrows is not None:
+                return oracle.ivf_search_batch(qh[:S], k, cents, lrows, off_l, live_l, nprobe=args.nprobe,
+                                               nthreads=threads)
+            return oracle.ivf_search_batch_idx(qh[:S], k, cents, data, lab_rows, off_l, live_l, nprobe=args.nprobe,
+                                               nthreads=threads)
         S = min(Q, 4 * threads)
         t = time.perf_counter()
-        oracle.ivf_search_batch(qh[:S], k, cts, rows, off, live, nprobe=args.nprobe, nthreads=threads)
-        probe = time.perf_counter() - t
-        S = int(min(Q, max(S, S * args.cpu_seconds / max(probe, 1e-3))))
+        cpu_run(S)
+        probe_t = time.perf_counter() - t
+        S = int(min(Q, max(S, S * args.cpu_seconds / max(probe_t, 1e-3))))
         t = time.perf_counter()
-        cs, ck, cc = oracle.ivf_search_batch(qh[:S], k, cts, rows, off, live, nprobe=args.nprobe, nthreads=threads)
-        ct = time.perf_counter() - t
-        ids_equal = bool(np.array_equal(labels[ck], l_fin[:S]))
+        cs, ck, cc = cpu_run(S)
+        ct_ = time.perf_counter() - t
+        ids_equal = bool(np.array_equal(np.where(ck >= 0, lab_l[np.maximum(ck, 0)], -1), l_fin[:S]))
         bits_equal = bool(np.array_equal(cs.view(np.uint32), s_fin[:S].view(np.uint32)))
-        cpu = {"value": S / ct, "unit": "queries/s", "cores": threads, "kind": "port",
-               "sample": f"{S} of the {Q} batch queries, same index (oracle/oracle.c IVF search, "
-                         f"one query per thread, {threads} threads, {ct:.1f}s)",
+        cpu = {"value": S / ct_, "unit": "queries/s", "cores": threads, "kind": "port",
+               "sample": f"{S} of the {Q} batch queries, same index (oracle/oracle.c IVF search, one query per "
+                         f"thread, {threads} threads = every CPU this process may use, {ct_:.1f}s)",
+               "host": host,
                "parity": {"queries": S, "ids_equal": ids_equal, "scores_bit_identical": bits_equal}}
-        log(f"cpu baseline: {S / ct:,.1f} QPS on {threads} threads; parity ids={ids_equal} bits={bits_equal}")
-        del rows
+        log(f"cpu baseline: {S / ct_:,.1f} QPS on {threads} threads ({host.get('model')}); "
+            f"parity ids={ids_equal} bits={bits_equal}")
 
     if rank == 0:
         bytes_per_query = args.nprobe / args.nlist * N * D * 4 + args.nlist * D * 4
@@ -240,13 +383,15 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: Pyrope.Benchmarks generator (.NET Random, base seed 42, query seed 1337), "
-                    "uniform [0,1)",
+            "data": "synthetic: Pyrope.Benchmarks generator (.NET Random), base rows in 65,536-row blocks seeded "
+                    "42 + block, queries seed 1337, uniform [0,1)",
             "config": {"workload": f"IVF_FLAT d={D} N={N} nlist={args.nlist} nprobe={args.nprobe} k={k}",
                        "n": N, "dim": D, "nlist": args.nlist, "nprobe": args.nprobe, "k": k,
-                       "queries_per_step": Q, "queries_per_gpu": args.nq,
-                       "shard": "rows-within-list (row i on rank i % n_gpus), shared quantizer",
-                       "merge": "RCCL all_gather of partial top-k + on-device merge" if world > 1 else "none"},
+                       "queries_per_step": Q, "queries_per_gpu": args.nq, "train_rows": T,
+                       "shard": "rows-within-list: generator blocks b % n_gpus == rank, shared quantizer "
+                                "(trained on rank 0, broadcast)",
+                       "merge": "RCCL all_gather of probe lists and of partial top-k + on-device merge"
+                                if world > 1 else "none"},
             "recall_at_10": recall,
             "roofline": {"bound": "hbm", "achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": hbm_achieved / HBM_PEAK_GBS, "traffic": None,
@@ -256,8 +401,8 @@ def main():
                                     "mfma_filter<128,L2,IVF> (IVF list scan, fp32 MFMA candidate filter)" if filt
                                     else "scan_fast<128,1,L2,IVF> (IVF list scan, exact VALU)"),
                          "note": ("algorithmic bytes = every probed list read once per launch (live rows x D x "
-                                  "4 B) + queries, over the HIP-event time of the launch; traffic (FETCH_SIZE, "
-                                  "measured in its own rocprofv3 pass) is in profiles/*/summary.md")},
+                                  "4 B) + queries, over the HIP-event time of the launch (rank 0); traffic "
+                                  "(FETCH_SIZE, measured in its own rocprofv3 pass) is in profiles/*/summary.md")},
             "mfma": {"achieved": achieved * (3 if bf16x3 else 1),
                      "peak": BF16_PEAK_TFLOPS if bf16x3 else FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved * (3 if bf16x3 else 1) / (BF16_PEAK_TFLOPS if bf16x3 else FP32_PEAK_TFLOPS),
@@ -272,10 +417,20 @@ def main():
             "phases_ms": {k_: round(v["ms"], 4) for k_, v in phases.items()},
             "cpu_baseline": cpu,
         }
-        print(json.dumps(out))
+        print(json.dumps(out), flush=True)
+    idx.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def main():
+    argv = sys.argv[1:]
+    args = parse(argv)
+    if args.gpus > 1 and "RANK" not in os.environ and int(os.environ.get("WORLD_SIZE", "1")) <= 1:
+        spawn_ranks(args, argv)
+        return
+    run(args)
 
 
 if __name__ == "__main__":

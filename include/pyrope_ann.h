@@ -41,7 +41,10 @@ typedef enum {
   PYR_E_STATE = 3,     /* -> InvalidOperationException (wrong index kind / not built) */
   PYR_E_OOM = 4,       /* device or host allocation failed */
   PYR_E_DEVICE = 5,    /* HIP runtime error, or no gfx950 device */
-  PYR_E_DUPLICATE = 6  /* -> InvalidOperationException("Vector with id ... already exists.") (BruteForceVectorIndex.cs:141-144) */
+  PYR_E_DUPLICATE = 6, /* -> InvalidOperationException("Vector with id ... already exists.") (BruteForceVectorIndex.cs:141-144) */
+  PYR_E_NOT_FOUND = 7, /* -> FileNotFoundException("Snapshot file not found.") (BruteForceVectorIndex.cs:87, IvfFlatVectorIndex.cs:259) */
+  PYR_E_FORMAT = 8,    /* -> JsonException: the file is not an index image of this kind / dimension / metric */
+  PYR_E_IO = 9         /* -> IOException: the image could not be written */
 } pyr_status;
 
 /* == VectorMetric ordinals (IVectorIndex.cs:5-10) */
@@ -122,6 +125,21 @@ pyr_status pyr_index_search_probed_device(pyr_index *index, const float *d_q, in
                                           const pyr_search_params *params, const int32_t *d_probes, int32_t nprobe,
                                           float *d_scores, int64_t *d_labels, int32_t *d_counts, void *stream);
 
+/* IVectorIndex.Snapshot (IVectorIndex.cs:26): write a binary image of the index to `path` (UTF-8,
+ * NUL-terminated) through path + ".tmp" and a rename (the temp + move of DeltaVectorIndex.cs:160-191).
+ * The image holds what the reference's snapshot DTOs hold (BruteForceVectorIndex.cs:58-82: live rows
+ * with their labels in slot order; IvfFlatVectorIndex.cs:233-257: IsBuilt, centroids, buffer, inverted
+ * lists in order) as raw arrays that load into HBM with one copy each; IVF_PQ images also hold the
+ * codebooks and codes (the reference's IvfPq Snapshot/Load are no-ops, IvfPqVectorIndex.cs:228-229).
+ * Layout: pyrope_amd/csrc/persist.h.  Takes the index shared (concurrent searches may run). */
+pyr_status pyr_index_snapshot(pyr_index *index, const char *path);
+/* IVectorIndex.Load (IVectorIndex.cs:27): replace the index's state with the image at `path`.
+ * PYR_E_NOT_FOUND if there is no file; PYR_E_FORMAT if it is not an image of an index of this kind
+ * and dimension (the recorded metric is not enforced, as the reference ignores IvfStateDto.Metric).  Sections missing from an image load as empty (IvfFlatVectorIndexTests.cs:
+ * 144-165).  FLAT rows are re-added in slot order (BruteForceVectorIndex.cs:84-106: Clear, then
+ * InternalAdd, so the 8-bit codes follow the loading index's EnableQuantization).  Exclusive. */
+pyr_status pyr_index_load(pyr_index *index, const char *path);
+
 /* IVectorIndex.GetStats (IVectorIndex.cs:28): Count with the reference's semantics
  * (IvfFlat counts buffer + list rows, IvfFlatVectorIndex.cs:305; IvfPq reports 0, IvfPqVectorIndex.cs:230). */
 pyr_status pyr_index_stats(const pyr_index *index, int64_t *count, int32_t *dim, int32_t *metric);
@@ -166,6 +184,12 @@ pyr_status pyr_merge_topk_device(const float *d_scores, const int64_t *d_labels,
 /* Pyrope.Benchmarks synthetic generator (Program.cs:251-263): v[d] = (float)new Random(seed).NextDouble(),
  * row by row.  Host buffer count x dim.  Measurement-harness utility. */
 pyr_status pyr_generate_synthetic(int64_t count, int32_t dim, int32_t seed, float *out);
+/* Row-blocked form for large N (block b of `block_rows` rows is the sequence of
+ * new Random(seed + b)), so a shard of whole blocks is generated without the rows before it.
+ * Writes rows [row0, row0 + count) to out (count x dim); blocks are generated in parallel.
+ * With row0 + count <= block_rows it equals pyr_generate_synthetic. */
+pyr_status pyr_generate_synthetic_blocked(int64_t row0, int64_t count, int32_t dim, int32_t seed, int64_t block_rows,
+                                          float *out);
 
 /* Kernel-phase profiler (HIP events on the search stream; adds a host sync per search while on).
  * phase: 0 coarse scan+select, 1 IVF work lists, 2 IVF list scan, 3 buffer scan, 4 final merge,

@@ -551,6 +551,45 @@ int32_t orc_ivf_search(const float *buf, const uint8_t *buf_live, int64_t nbuf_s
   return r;
 }
 
+/* The coarse ranking alone (:186-198): the first min(nprobe, nlist) list ids in rank order.
+ * The multi-GPU step ranks each query once and hands the lists to every shard. */
+int32_t orc_ivf_probe(const float *q, const float *cents, int32_t nlist, int32_t dim, int32_t metric,
+                      int32_t nprobe, int32_t *out) {
+  if (nprobe < 0) nprobe = 3; /* :14, :151 */
+  int32_t probes = nprobe < nlist ? nprobe : nlist;
+  if (probes <= 0) return 0;
+  float qn = metric == ORC_COS ? orc_norm(q, dim) : 0.0f;
+  cscore *cs = coarse_rank(q, cents, nlist, dim, metric, qn);
+  for (int32_t p = 0; p < probes; p++) out[p] = cs[p].idx;
+  free(cs);
+  return probes;
+}
+
+/* The list scan of Search (:200-218) over caller-ranked lists (built index, empty buffer, no
+ * MaxScans).  Row pos of the list-major store is lrows[row_idx ? row_idx[pos] : pos], so a
+ * caller can pass base rows plus the layout's labels instead of a list-major copy. */
+int32_t orc_ivf_search_probed(const float *lrows, const int64_t *row_idx, const uint8_t *row_live,
+                              const int64_t *list_off, const int32_t *probes, int32_t nprobe, int32_t dim,
+                              int32_t metric, const float *q, int32_t k, float *out_scores, int64_t *out_keys) {
+  if (k <= 0) return 0;
+  cand *h = (cand *)malloc(sizeof(cand) * (size_t)k);
+  int32_t cnt = 0;
+  float qn = metric == ORC_COS ? orc_norm(q, dim) : 0.0f;
+  for (int32_t p = 0; p < nprobe; p++) {
+    int32_t l = probes[p];
+    if (l < 0) continue;
+    for (int64_t pos = list_off[l]; pos < list_off[l + 1]; pos++) {
+      if (row_live && !row_live[pos]) continue;
+      const float *x = lrows + (row_idx ? row_idx[pos] : pos) * dim;
+      float xn = metric == ORC_COS ? orc_norm(x, dim) : 0.0f;
+      topk_push(h, &cnt, k, ivf_score(q, x, dim, metric, qn, xn), pos);
+    }
+  }
+  int32_t r = topk_emit(h, cnt, out_scores, out_keys);
+  free(h);
+  return r;
+}
+
 /* ------------------------------------------------------------------ */
 /* ProductQuantizer.cs                                                  */
 /* ------------------------------------------------------------------ */
@@ -683,13 +722,19 @@ typedef struct {
   int64_t *ok;
   int32_t *oc;
   int32_t tid, nthreads;
+  const int64_t *row_idx; /* kind 2 */
 } batch_arg;
 
 static void *batch_worker(void *p) {
   batch_arg *a = (batch_arg *)p;
+  int32_t *pr = a->kind == 2 ? (int32_t *)malloc(sizeof(int32_t) * (size_t)(a->nprobe > 0 ? a->nprobe : 1)) : NULL;
   for (int64_t i = a->tid; i < a->nq; i += a->nthreads) {
     const float *q = a->qs + i * a->dim;
-    if (a->kind == 0)
+    if (a->kind == 2) { /* Search with rows through row_idx: probe, then the list scan */
+      int32_t np = orc_ivf_probe(q, a->cents, a->nlist, a->dim, a->metric, a->nprobe, pr);
+      a->oc[i] = orc_ivf_search_probed(a->lrows, a->row_idx, a->row_live, a->list_off, pr, np, a->dim, a->metric, q,
+                                       a->k, a->os + i * a->k, a->ok + i * a->k);
+    } else if (a->kind == 0)
       a->oc[i] = orc_ivf_search(a->buf, a->buf_live, a->nbuf, a->lrows, a->row_live, a->list_off, a->cents,
                                 a->nlist, 1, a->dim, a->metric, q, a->k, a->nprobe, -1,
                                 a->os + i * a->k, a->ok + i * a->k);
@@ -697,6 +742,7 @@ static void *batch_worker(void *p) {
       a->oc[i] = orc_bf_search(a->lrows, a->row_live, a->nbuf, a->dim, a->metric, q, a->k, -1,
                                a->os + i * a->k, a->ok + i * a->k);
   }
+  free(pr);
   return NULL;
 }
 
@@ -721,7 +767,18 @@ void orc_ivf_search_batch(const float *buf, const uint8_t *buf_live, int64_t nbu
                           const float *qs, int64_t nq, int32_t k, int32_t nprobe, int32_t nthreads,
                           float *out_scores, int64_t *out_keys, int32_t *out_counts) {
   batch_arg a = {0, buf, buf_live, nbuf_slots, lrows, row_live, list_off, cents, nlist, dim, metric, k, nprobe,
-                 qs, nq, out_scores, out_keys, out_counts, 0, 1};
+                 qs, nq, out_scores, out_keys, out_counts, 0, 1, NULL};
+  run_batch(&a, nthreads);
+}
+
+/* orc_ivf_search_batch over base rows + the layout's row index (rows[row_idx[pos]] is list-major
+ * position pos), built index, empty buffer: one query per worker thread. */
+void orc_ivf_search_batch_idx(const float *rows, const int64_t *row_idx, const uint8_t *row_live,
+                              const int64_t *list_off, const float *cents, int32_t nlist, int32_t dim, int32_t metric,
+                              const float *qs, int64_t nq, int32_t k, int32_t nprobe, int32_t nthreads,
+                              float *out_scores, int64_t *out_keys, int32_t *out_counts) {
+  batch_arg a = {2, NULL, NULL, 0, rows, row_live, list_off, cents, nlist, dim, metric, k, nprobe,
+                 qs, nq, out_scores, out_keys, out_counts, 0, 1, row_idx};
   run_batch(&a, nthreads);
 }
 
@@ -729,6 +786,6 @@ void orc_bf_search_batch(const float *rows, const uint8_t *live, int64_t nslots,
                          int32_t metric, const float *qs, int64_t nq, int32_t k, int32_t nthreads,
                          float *out_scores, int64_t *out_keys, int32_t *out_counts) {
   batch_arg a = {1, NULL, NULL, nslots, rows, live, NULL, NULL, 0, dim, metric, k, 0,
-                 qs, nq, out_scores, out_keys, out_counts, 0, 1};
+                 qs, nq, out_scores, out_keys, out_counts, 0, 1, NULL};
   run_batch(&a, nthreads);
 }

@@ -113,6 +113,15 @@ void orc_ivf_search_batch(const float *buf, const uint8_t *buf_live, int64_t nbu
                           const float *cents, int32_t nlist, int32_t dim, int32_t metric,
                           const float *qs, int64_t nq, int32_t k, int32_t nprobe, int32_t nthreads,
                           float *out_scores, int64_t *out_keys, int32_t *out_counts);
+int32_t orc_ivf_probe(const float *q, const float *cents, int32_t nlist, int32_t dim, int32_t metric,
+                      int32_t nprobe, int32_t *out);
+int32_t orc_ivf_search_probed(const float *lrows, const int64_t *row_idx, const uint8_t *row_live,
+                              const int64_t *list_off, const int32_t *probes, int32_t nprobe, int32_t dim,
+                              int32_t metric, const float *q, int32_t k, float *out_scores, int64_t *out_keys);
+void orc_ivf_search_batch_idx(const float *rows, const int64_t *row_idx, const uint8_t *row_live,
+                              const int64_t *list_off, const float *cents, int32_t nlist, int32_t dim, int32_t metric,
+                              const float *qs, int64_t nq, int32_t k, int32_t nprobe, int32_t nthreads,
+                              float *out_scores, int64_t *out_keys, int32_t *out_counts);
 void orc_bf_search_batch(const float *rows, const uint8_t *live, int64_t nslots, int32_t dim,
                          int32_t metric, const float *qs, int64_t nq, int32_t k, int32_t nthreads,
                          float *out_scores, int64_t *out_keys, int32_t *out_counts);

@@ -67,6 +67,10 @@ def _declare(L):
         "orc_ivfpq_search": (I32, [_f, _u8, I64, _u8, _u8, _i64, _f, I32, I32, _f, I32, I32, I32, I32, _f, I32, I32, _f, _i64]),
         "orc_ivf_search_batch": (None, [_f, _u8, I64, _f, _u8, _i64, _f, I32, I32, I32, _f, I64, I32, I32, I32, _f, _i64, _i32]),
         "orc_bf_search_batch": (None, [_f, _u8, I64, I32, I32, _f, I64, I32, I32, _f, _i64, _i32]),
+        "orc_ivf_probe": (I32, [_f, _f, I32, I32, I32, I32, _i32]),
+        "orc_ivf_search_probed": (I32, [_f, _i64, _u8, _i64, _i32, I32, I32, I32, _f, I32, _f, _i64]),
+        "orc_ivf_search_batch_idx": (None, [_f, _i64, _u8, _i64, _f, I32, I32, I32, _f, I64, I32, I32, I32, _f, _i64,
+                                            _i32]),
         "orc_scalar_quantize": (None, [_f, I32, _u8, _f, _f]),
         "orc_l2sq_8bit_net": (I64, [_u8, _u8, I32]),
         "orc_dot_8bit_net": (I64, [_u8, _u8, I32]),
@@ -355,4 +359,46 @@ def bf_search_batch(qs, k, rows, live=None, metric=L2, nthreads=1):
     cnt = np.zeros(nq, np.int32)
     lib().orc_bf_search_batch(_p(rows, C.c_float), _p(live, C.c_uint8), len(rows), dim, metric, _p(qs, C.c_float),
                               nq, k, nthreads, _p(s, C.c_float), _p(kk, C.c_int64), _p(cnt, C.c_int32))
+    return s, kk, cnt
+
+
+def ivf_probe(q, cents, nprobe, metric=L2):
+    """IvfFlatVectorIndex.cs:186-198: the first min(nprobe, nlist) lists by (score desc, index asc)."""
+    q, cents = _f32(q).reshape(-1), _f32(cents)
+    nlist, dim = cents.shape
+    out = np.zeros(max(nprobe, 1), np.int32)
+    n = lib().orc_ivf_probe(_p(q, C.c_float), _p(cents, C.c_float), nlist, dim, metric, nprobe, _p(out, C.c_int32))
+    return out[:n]
+
+
+def ivf_search_probed(q, k, lrows, list_off, probes, row_live=None, row_idx=None, metric=L2):
+    """IvfFlatVectorIndex.cs:200-218 over caller-ranked lists.  Returns (scores, list-major keys)."""
+    q, lrows = _f32(q).reshape(-1), _f32(lrows)
+    dim = q.size
+    list_off = np.ascontiguousarray(list_off, np.int64)
+    probes = np.ascontiguousarray(probes, np.int32)
+    live = None if row_live is None else _u8a(row_live)
+    ridx = None if row_idx is None else np.ascontiguousarray(row_idx, np.int64)
+    s = np.empty(max(k, 1), np.float32)
+    kk = np.empty(max(k, 1), np.int64)
+    c = lib().orc_ivf_search_probed(_p(lrows, C.c_float), _p(ridx, C.c_int64), _p(live, C.c_uint8),
+                                    _p(list_off, C.c_int64), _p(probes, C.c_int32), len(probes), dim, metric,
+                                    _p(q, C.c_float), k, _p(s, C.c_float), _p(kk, C.c_int64))
+    return s[:c], kk[:c]
+
+
+def ivf_search_batch_idx(qs, k, cents, rows, row_idx, list_off, row_live=None, metric=L2, nprobe=-1, nthreads=1):
+    """CPU baseline over base rows + layout labels (no list-major copy): one query per thread."""
+    qs, rows, cents = _f32(qs), _f32(rows), _f32(cents)
+    nq, dim = qs.shape
+    row_idx = np.ascontiguousarray(row_idx, np.int64)
+    list_off = np.ascontiguousarray(list_off, np.int64)
+    live = None if row_live is None else _u8a(row_live)
+    s = np.full((nq, k), -np.inf, np.float32)
+    kk = np.full((nq, k), -1, np.int64)
+    cnt = np.zeros(nq, np.int32)
+    lib().orc_ivf_search_batch_idx(_p(rows, C.c_float), _p(row_idx, C.c_int64), _p(live, C.c_uint8),
+                                   _p(list_off, C.c_int64), _p(cents, C.c_float), len(cents), dim, metric,
+                                   _p(qs, C.c_float), nq, k, nprobe, nthreads, _p(s, C.c_float), _p(kk, C.c_int64),
+                                   _p(cnt, C.c_int32))
     return s, kk, cnt

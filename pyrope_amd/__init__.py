@@ -6,7 +6,8 @@ mirror of the reference's IVectorIndex plugin surface.
 """
 from .vector import (BruteForceVectorIndex, DeltaVectorIndex, HipVectorIndex, ICentroidsProvider,  # noqa: F401
                      IndexStats, IvfFlatVectorIndex, IvfPqVectorIndex, IVectorIndex, SearchOptions,
-                     SearchResult, VectorIndexRegistry, VectorMetric, generate_synthetic, kmeans_train)
+                     SearchResult, VectorIndexRegistry, VectorMetric, generate_synthetic,
+                     generate_synthetic_blocked, kmeans_train)
 from ._lib import (ArgumentException, ArgumentNullException, ArgumentOutOfRangeException,  # noqa: F401
                    DeviceError, InvalidOperationException)
 

@@ -12,7 +12,8 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libpyrope_hip.so")
 
-PYR_OK, PYR_E_DIM, PYR_E_ARG, PYR_E_STATE, PYR_E_OOM, PYR_E_DEVICE, PYR_E_DUPLICATE = range(7)
+(PYR_OK, PYR_E_DIM, PYR_E_ARG, PYR_E_STATE, PYR_E_OOM, PYR_E_DEVICE, PYR_E_DUPLICATE, PYR_E_NOT_FOUND,
+ PYR_E_FORMAT, PYR_E_IO) = range(10)
 PYR_FLAT, PYR_IVF_FLAT, PYR_IVF_PQ = 0, 1, 2
 
 
@@ -47,6 +48,18 @@ class DeviceError(RuntimeError):
     pass
 
 
+class FileNotFoundException(FileNotFoundError):
+    """System.IO.FileNotFoundException (Load of a missing snapshot)."""
+
+
+class JsonException(ValueError):
+    """System.Text.Json.JsonException (Load of a file that is not a snapshot of this index)."""
+
+
+class IOException(OSError):
+    """System.IO.IOException (a snapshot could not be written)."""
+
+
 class IndexDesc(C.Structure):
     _fields_ = [("kind", C.c_int32), ("dim", C.c_int32), ("metric", C.c_int32), ("nlist", C.c_int32),
                 ("pq_m", C.c_int32), ("pq_k", C.c_int32), ("device", C.c_int32), ("default_nprobe", C.c_int32)]
@@ -76,6 +89,8 @@ SIGNATURES = {
     "pyr_index_search_device": (C.c_int, [_vp, _vp, C.c_int64, C.c_int32, C.POINTER(SearchParams), _vp, _vp, _vp,
                                           _vp]),
     "pyr_index_stats": (C.c_int, [_vp, _i64, _i32, _i32]),
+    "pyr_index_snapshot": (C.c_int, [_vp, C.c_char_p]),
+    "pyr_index_load": (C.c_int, [_vp, C.c_char_p]),
     "pyr_index_get_centroids": (C.c_int, [_vp, _f, _i32]),
     "pyr_index_ivf_layout": (C.c_int, [_vp, _i64, _i64, _u8, _i64]),
     "pyr_index_pq_state": (C.c_int, [_vp, _f, _i32, _u8]),
@@ -87,6 +102,7 @@ SIGNATURES = {
     "pyr_scalar_quantize": (C.c_int, [C.c_int32, _f, C.c_int64, C.c_int32, _u8]),
     "pyr_merge_topk_device": (C.c_int, [_vp, _vp, C.c_int64, C.c_int32, C.c_int32, _vp, _vp, _vp]),
     "pyr_generate_synthetic": (C.c_int, [C.c_int64, C.c_int32, C.c_int32, _f]),
+    "pyr_generate_synthetic_blocked": (C.c_int, [C.c_int64, C.c_int64, C.c_int32, C.c_int32, C.c_int64, _f]),
     "pyr_index_set_centroids": (C.c_int, [_vp, _f, C.c_int32]),
     "pyr_kmeans_train": (C.c_int, [C.c_int32, _f, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                    _f, _i32]),
@@ -131,6 +147,12 @@ def check(status: int, what: str = "") -> None:
         raise InvalidOperationException(msg)
     if status == PYR_E_DEVICE:
         raise DeviceError(msg)
+    if status == PYR_E_NOT_FOUND:
+        raise FileNotFoundException(msg)
+    if status == PYR_E_FORMAT:
+        raise JsonException(msg)
+    if status == PYR_E_IO:
+        raise IOException(msg)
     raise PyrError(status, msg)
 
 

@@ -1,9 +1,13 @@
 // capi.cpp -- the extern "C" boundary of libpyrope_hip.so (include/pyrope_ann.h).
 // No C++ exception crosses it: every entry point catches, records a thread-local
 // message (pyr_last_error) and returns a pyr_status.
+#include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "engine.h"
 
@@ -261,6 +265,27 @@ pyr_status pyr_index_search_probed_device(pyr_index *index, const float *d_q, in
   });
 }
 
+pyr_status pyr_index_snapshot(pyr_index *index, const char *path) {
+  if (!index || !path) return fail(PYR_E_ARG, "null argument");
+  return guard([&] {
+    HIPCHK(hipSetDevice(index->impl->device));
+    // the reference snapshots under its read lock; the image reuses the write stream and
+    // staging buffers, so snapshots serialize among themselves (wmu) but not with searches
+    std::shared_lock<std::shared_mutex> g(index->impl->mu);
+    std::lock_guard<std::mutex> w(index->impl->wmu);
+    index->impl->snapshot(path);
+  });
+}
+
+pyr_status pyr_index_load(pyr_index *index, const char *path) {
+  if (!index || !path) return fail(PYR_E_ARG, "null argument");
+  return guard([&] {
+    HIPCHK(hipSetDevice(index->impl->device));
+    std::unique_lock<std::shared_mutex> g(index->impl->mu);
+    index->impl->load(path);
+  });
+}
+
 pyr_status pyr_index_stats(const pyr_index *index, int64_t *count, int32_t *dim, int32_t *metric) {
   if (!index) return fail(PYR_E_ARG, "null argument");
   return guard([&] {
@@ -355,6 +380,31 @@ pyr_status pyr_generate_synthetic(int64_t count, int32_t dim, int32_t seed, floa
   pyr::NetRandom r(seed);  // Program.cs:251-263
   const int64_t n = count * (int64_t)dim;
   for (int64_t i = 0; i < n; i++) out[i] = (float)r.next_double();
+  return PYR_OK;
+}
+
+pyr_status pyr_generate_synthetic_blocked(int64_t row0, int64_t count, int32_t dim, int32_t seed, int64_t block_rows,
+                                          float *out) {
+  if (row0 < 0 || count < 0 || dim <= 0 || block_rows <= 0 || (count > 0 && !out)) return fail(PYR_E_ARG, "bad argument");
+  if (count == 0) return PYR_OK;
+  // row r belongs to block b = r / block_rows, whose values are the sequence of new Random(seed + b)
+  const int64_t b0 = row0 / block_rows, b1 = (row0 + count - 1) / block_rows;
+  auto gen = [&](int64_t b) {
+    pyr::NetRandom r((int32_t)(seed + b));
+    const int64_t rb = std::max(row0, b * block_rows), re = std::min(row0 + count, (b + 1) * block_rows);
+    for (int64_t i = (b * block_rows) * (int64_t)dim; i < rb * (int64_t)dim; i++) (void)r.next();  // skip to rb
+    float *o = out + (rb - row0) * (int64_t)dim;
+    for (int64_t i = 0; i < (re - rb) * (int64_t)dim; i++) o[i] = (float)r.next_double();
+  };
+  const int64_t nb = b1 - b0 + 1;
+  const int nt = (int)std::min<int64_t>(nb, std::max(1u, std::min(32u, std::thread::hardware_concurrency())));
+  std::atomic<int64_t> nextb{b0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; t++)
+    th.emplace_back([&] {
+      for (int64_t b; (b = nextb.fetch_add(1)) <= b1;) gen(b);
+    });
+  for (auto &t : th) t.join();
   return PYR_OK;
 }
 

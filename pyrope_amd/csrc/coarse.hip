@@ -170,12 +170,8 @@ void launch_coarse_dense(const float *q, const float *cents_rm, const float *qn,
                          int32_t nlist, int32_t dim, int32_t metric, int32_t nprobe, float *scores, int32_t *probes,
                          hipStream_t st) {
   if (nq <= 0 || nlist <= 0 || nprobe <= 0) return;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&coarse_select_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
+  static std::atomic<uint64_t> attr{0};
+  allow_max_lds(reinterpret_cast<const void *>(&coarse_select_kernel), attr);
   const dim3 grid((unsigned)((nlist + CT - 1) / CT), (unsigned)((nq + CT - 1) / CT));
   if (metric == L2)
     hipLaunchKernelGGL(coarse_scores_kernel<L2>, grid, dim3(256), 0, st, q, cents_rm, qn, cn, nq, nlist, dim, scores);

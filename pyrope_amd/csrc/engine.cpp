@@ -5,6 +5,7 @@
 // quirks) with the scan itself on the GPU.  Paths are relative to
 // /root/reference/src/Pyrope.GarnetServer/.
 #include "engine.h"
+#include "persist.h"
 
 #include <cstdio>
 
@@ -91,6 +92,43 @@ void RowStore::set_live(const std::vector<int64_t> &slots, uint8_t v, hipStream_
   launch_scatter_u8(live.as<uint8_t>(), stage.as<int64_t>(), v, (int64_t)slots.size(), st);
   HIPCHK(hipStreamSynchronize(st));
   for (int64_t s : slots) hlive[s] = v;
+}
+
+
+// One batch may repeat a label (an id upserted twice in one call): every occurrence maps to one
+// slot and the reference applies the calls in order, so the LAST vector wins.  Earlier rows of a
+// repeated slot are dropped here (scattered writes of several rows to one slot would race on the
+// device).  The slot of each label stays the one its first occurrence got.  Returns false when
+// nothing repeats (x, labels, n, slots untouched).
+static bool keep_last_writes(const float *&x, const int64_t *&labels, int64_t &n, std::vector<int64_t> &slots,
+                             int dim, int64_t nslots, std::vector<float> &xs, std::vector<int64_t> &ls) {
+  if (n < 2) return false;
+  std::vector<uint8_t> keep((size_t)n, 1);
+  bool drop = false;
+  if (n < 4096) {
+    std::unordered_map<int64_t, int> hit;
+    for (int64_t i = n - 1; i >= 0; i--)
+      if (hit[slots[i]]++) keep[i] = 0, drop = true;
+  } else {
+    std::vector<uint8_t> hit((size_t)nslots, 0);
+    for (int64_t i = n - 1; i >= 0; i--) {
+      if (hit[slots[i]]) keep[i] = 0, drop = true;
+      hit[slots[i]] = 1;
+    }
+  }
+  if (!drop) return false;
+  std::vector<int64_t> ss;
+  for (int64_t i = 0; i < n; i++) {
+    if (!keep[i]) continue;
+    xs.insert(xs.end(), x + i * dim, x + (i + 1) * dim);
+    ls.push_back(labels[i]);
+    ss.push_back(slots[i]);
+  }
+  slots.swap(ss);
+  x = xs.data();
+  labels = ls.data();
+  n = (int64_t)ls.size();
+  return true;
 }
 
 // ---------------------------------------------------------------------------
@@ -310,7 +348,7 @@ static double filter_cerr(int dim) {
 // queries whose certificate failed (listed in ws.fail).  Synchronizes ws.st.
 static int64_t filter_finish(Workspace &ws, int64_t nq, int nparts, int k1, int k, int dim, int met, int V,
                              const float *d_q, const RowStore &rs, const MergeIvf *mi, float *d_s, int64_t *d_l,
-                             int32_t *d_c) {
+                             int32_t *d_c, const uint32_t *list_rmax = nullptr) {
   ws.ms.ensure(sizeof(float) * nq * k1);
   ws.mk.ensure(sizeof(int32_t) * nq * k1);
   {
@@ -328,6 +366,16 @@ static int64_t filter_finish(Workspace &ws, int64_t nq, int nparts, int k1, int 
   r.ms = ws.ms.as<float>();
   r.mk = ws.mk.as<int32_t>();
   r.max_rsq = rs.rmax.as<uint32_t>();
+  // PYR_CERT_GLOBAL=1: bound row norms by the whole store's max only -- no per-list maxima, no
+  // triangle bound (A/B measurement of the refined certificate)
+  const char *cg = getenv("PYR_CERT_GLOBAL");
+  const bool global = cg && atoi(cg) != 0;
+  r.tri = !global;
+  if (list_rmax && mi && !global) {
+    r.list_rmax = list_rmax;
+    r.probes = mi->probes;
+    r.nprobe = mi->nprobe;
+  }
   r.nq = nq;
   r.k1 = k1;
   r.k = k;
@@ -457,6 +505,61 @@ int kmeans_train_gpu(const float *d_x, int64_t n, int dim, int k, int met, int m
   return k;
 }
 
+
+// ---------------------------------------------------------------------------
+// index images (IVectorIndex.Snapshot / Load; persist.h)
+// ---------------------------------------------------------------------------
+static void check_image(const ImageReader &r, int kind, const Index &ix) {
+  if (r.kind != kind) throw Error(PYR_E_FORMAT, "the image holds another index kind");
+  if (r.dim != ix.dim)
+    throw Error(PYR_E_FORMAT, "the image has dimension " + std::to_string(r.dim) + ", the index " + std::to_string(ix.dim));
+  // the metric is recorded but, like the reference's IvfStateDto.Metric (IvfFlatVectorIndex.cs:259-
+  // 298 never reads it), not enforced: rows are re-derived (norms, |x|^2) for the loading index
+  (void)ix.metric;
+}
+
+// rows at `slots` of a blocked store -> row-major device rows in stage_x (slot order)
+static void gather_slots(const RowStore &s, const std::vector<int64_t> &slots, DevMem &stage_x, DevMem &stage_i,
+                         hipStream_t st) {
+  const int64_t n = (int64_t)slots.size();
+  stage_x.ensure(sizeof(float) * std::max<int64_t>(n, 1) * s.dim);
+  if (n == 0) return;
+  stage_i.ensure(sizeof(int64_t) * n);
+  HIPCHK(hipMemcpyAsync(stage_i.p, slots.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, st));
+  launch_gather_blocked(s.rows.as<float>(), stage_i.as<int64_t>(), n, s.dim, stage_x.as<float>(), st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(st));
+}
+
+// the live slots of a store in slot order (BruteForce _vectors / Dictionary enumeration order)
+static std::vector<int64_t> live_slots(const RowStore &s, std::vector<int64_t> &labels) {
+  std::vector<int64_t> slots;
+  for (int64_t i = 0; i < s.n; i++)
+    if (s.hlive[i]) {
+      slots.push_back(i);
+      labels.push_back(s.hlabels[i]);
+    }
+  return slots;
+}
+
+static void write_rows(ImageWriter &w, uint32_t tag_labels, uint32_t tag_rows, const RowStore &s,
+                       const std::vector<int64_t> &slots, const std::vector<int64_t> &labels, DevMem &stage_x,
+                       DevMem &stage_i, hipStream_t st) {
+  w.host(tag_labels, labels.data(), sizeof(int64_t) * labels.size());
+  gather_slots(s, slots, stage_x, stage_i, st);
+  w.device(tag_rows, stage_x.p, sizeof(float) * slots.size() * s.dim, st);
+}
+
+// labels + host rows of a (labels, rows) section pair; absent sections = no rows
+static int64_t read_rows(ImageReader &r, uint32_t tag_labels, uint32_t tag_rows, int dim, std::vector<int64_t> &labels,
+                         std::vector<float> &rows) {
+  labels = r.vec<int64_t>(tag_labels);
+  const int64_t n = (int64_t)labels.size();
+  rows.assign((size_t)n * dim, 0.0f);
+  if (n) r.host(tag_rows, rows.data(), sizeof(float) * rows.size());
+  return n;
+}
+
 // ---------------------------------------------------------------------------
 // FLAT = BruteForceVectorIndex (BruteForceVectorIndex.cs)
 // ---------------------------------------------------------------------------
@@ -507,6 +610,9 @@ struct FlatIndex : Index {
         batch[labels[i]] = slots[i];
       }
     }
+    std::vector<float> xs;
+    std::vector<int64_t> ls;
+    keep_last_writes(x, labels, n, slots, dim, next, xs, ls);
     st.reserve(next, wst);
     st.hlabels.resize(next, -1);
     st.hlive.resize(next, 0);
@@ -701,6 +807,29 @@ struct FlatIndex : Index {
   }
 
   int64_t count() const override { return (int64_t)slot_of.size(); }  // :115-126
+
+  void snapshot(const std::string &path) override {  // :58-82: the live (id, vector) pairs in slot order
+    ImageWriter w(path, PYR_FLAT, dim, metric);
+    std::vector<int64_t> labels;
+    const std::vector<int64_t> slots = live_slots(st, labels);
+    write_rows(w, T_FLABELS, T_FROWS, st, slots, labels, stage_x, stage_i, wst);
+    w.commit();
+  }
+
+  void load(const std::string &path) override {  // :84-106: Clear(), then InternalAdd per entry
+    ImageReader r(path);
+    check_image(r, PYR_FLAT, *this);
+    std::vector<int64_t> labels;
+    std::vector<float> rows;
+    const int64_t n = read_rows(r, T_FLABELS, T_FROWS, dim, labels, rows);
+    if (st.cap) HIPCHK(hipMemsetAsync(st.live.p, 0, st.cap, wst));
+    if (st.rmax.p) HIPCHK(hipMemsetAsync(st.rmax.p, 0, sizeof(uint32_t), wst));
+    if (q8cap) HIPCHK(hipMemsetAsync(q8ok.p, 0, q8cap, wst));
+    HIPCHK(hipStreamSynchronize(wst));
+    st.clear();
+    slot_of.clear();
+    if (n) add(rows.data(), n, labels.data(), false);  // codes iff EnableQuantization now (:166-178)
+  }
 };
 
 // ---------------------------------------------------------------------------
@@ -738,6 +867,9 @@ struct DictBuffer {
   }
   void write(const float *x, const int64_t *labels, int64_t n, hipStream_t wst, DevMem &sx, DevMem &si) {
     std::vector<int64_t> slots = place(labels, n);
+    std::vector<float> xs;
+    std::vector<int64_t> ls;
+    keep_last_writes(x, labels, n, slots, st.dim, st.n, xs, ls);
     st.reserve(st.n, wst);
     st.write(x, slots.data(), labels, n, wst, sx, si);
     for (int64_t i = 0; i < n; i++) {
@@ -963,6 +1095,7 @@ struct IvfFlatIndex : Index {
   std::vector<int32_t> lb, le, llen, llive;
   int64_t max_len = 0;                    // longest list (rows incl. tombstones): row chunking
   DevMem dlb, dle, dllive;
+  DevMem dlmax;                           // per-list max |x|^2 (score_key): refine certificate bound
   Coarse coarse;
   bool built = false;                     // _isBuilt (:20)
   int nprobe_default;
@@ -1082,6 +1215,15 @@ struct IvfFlatIndex : Index {
     std::vector<int32_t> asg(n);
     HIPCHK(hipMemcpyAsync(asg.data(), A.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, wst));
     HIPCHK(hipStreamSynchronize(wst));
+    commit_lists(X.as<float>(), n, asg, labs, C.as<float>(), k);
+    buf.clear(wst);
+    built = true;
+  }
+
+  // 4. commit (:135-139): rows X (device, row-major n x dim; row i has label labs[i]) into the
+  // stable list-major layout by list asg[i] (lists keep X order, padded to 8 rows), quantizer C.
+  void commit_lists(const float *X, int64_t n, const std::vector<int32_t> &asg, const std::vector<int64_t> &labs,
+                    const float *C, int k) {
     // stable list-major layout, lists padded to 8 rows
     std::vector<int32_t> cnt(k, 0);
     for (int32_t a : asg) cnt[a]++;
@@ -1113,7 +1255,7 @@ struct IvfFlatIndex : Index {
     DevMem dsr;
     dsr.ensure(sizeof(int64_t) * tot);
     HIPCHK(hipMemcpyAsync(dsr.p, srcrow.data(), sizeof(int64_t) * tot, hipMemcpyHostToDevice, wst));
-    launch_to_blocked(X.as<float>(), dsr.as<int64_t>(), tot, dim, nl.rows.as<float>(), 0, wst);
+    launch_to_blocked(X, dsr.as<int64_t>(), tot, dim, nl.rows.as<float>(), 0, wst);
     std::vector<uint8_t> lv(tot);
     for (int64_t p = 0; p < tot; p++) lv[p] = srcrow[p] >= 0;
     HIPCHK(hipMemcpyAsync(nl.live.p, lv.data(), tot, hipMemcpyHostToDevice, wst));
@@ -1145,10 +1287,12 @@ struct IvfFlatIndex : Index {
     pos_of.clear();
     for (int64_t p = 0; p < tot; p++)
       if (newlab[p] >= 0) pos_of[newlab[p]] = p;
-    coarse.set(C.as<float>(), k, dim, metric, wst);
+    coarse.set(C, k, dim, metric, wst);
     upload_list_meta();
-    buf.clear(wst);
-    built = true;
+    dlmax.ensure(sizeof(uint32_t) * k);
+    launch_list_rmax(lists.rsq.as<float>(), dlb.as<int32_t>(), dle.as<int32_t>(), k, dlmax.as<uint32_t>(), wst);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(wst));
   }
 
   void search(const float *d_q, int64_t nq, int k, const pyr_search_params &prm, float *d_s, int64_t *d_l,
@@ -1247,11 +1391,31 @@ struct IvfFlatIndex : Index {
     mi.le = dle.as<int32_t>();
     mi.nprobe = probes;
     mi.ch = ch;
-    const int64_t nf = filter_finish(ws, nq, nparts, k1, k, dim, metric, 1, d_q, lists, &mi, d_s, d_l, d_c);
+    const int64_t nf =
+        filter_finish(ws, nq, nparts, k1, k, dim, metric, 1, d_q, lists, &mi, d_s, d_l, d_c, dlmax.as<uint32_t>());
+    // The exact re-run scans the failing queries' OWN probe lists: ws.probes holds the batch's
+    // ranking (computed above or handed in by the caller, pyr_index_search_probed_device), so its
+    // rows are gathered in fail-list order and passed as caller-ranked lists.  (Re-ranking is
+    // only equivalent when this index ranked them itself; caller lists may differ.)
     pyr_search_params ex{probes, 0, -1};
     filter_fallback(ws, nf, d_q, dim, k, d_s, d_l, d_c,
                     [&](const float *q2, int64_t n2, float *s2, int64_t *l2, int32_t *c2) {
-                      search_exact(q2, n2, k, ex, s2, l2, c2, ws);
+                      ws.fprobes.ensure(sizeof(int32_t) * n2 * probes);
+                      launch_gather_rows_i32(ws.probes.as<int32_t>(), ws.fail.as<int32_t>(), n2, probes,
+                                             ws.fprobes.as<int32_t>(), ws.st);
+                      const int32_t *ext = ws.ext_probes;
+                      const int32_t ext_n = ws.ext_nprobe;
+                      ws.ext_probes = ws.fprobes.as<int32_t>();
+                      ws.ext_nprobe = probes;
+                      try {
+                        search_exact(q2, n2, k, ex, s2, l2, c2, ws);
+                      } catch (...) {
+                        ws.ext_probes = ext;
+                        ws.ext_nprobe = ext_n;
+                        throw;
+                      }
+                      ws.ext_probes = ext;
+                      ws.ext_nprobe = ext_n;
                     });
   }
 
@@ -1353,6 +1517,71 @@ struct IvfFlatIndex : Index {
     }
     launch_merge_keys(ws.part_s.as<float>(), ws.part_k.as<uint32_t>(), nq, nparts, k, lists.labels.as<int64_t>(),
                       buf.st.labels.as<int64_t>(), d_s, d_l, nullptr, d_c, ws.st, &mi);
+  }
+
+  void snapshot(const std::string &path) override {  // :233-257 IvfStateDto
+    ImageWriter w(path, PYR_IVF_FLAT, dim, metric);
+    const uint8_t b = built ? 1 : 0;
+    w.host(T_BUILT, &b, 1);
+    if (built) {
+      w.host(T_CENTS, coarse.host.data(), sizeof(float) * coarse.host.size());
+      // _invertedLists in order: visible and buffer-shadowed entries (removed ones are gone, :61-83)
+      std::vector<int32_t> cnt(coarse.nlist, 0);
+      std::vector<int64_t> slots, labels;
+      for (int l = 0; l < coarse.nlist; l++)
+        for (int32_t p = lb[l]; p < lb[l] + llen[l]; p++)
+          if (lstate[p]) {
+            cnt[l]++;
+            slots.push_back(p);
+            labels.push_back(lists.hlabels[p]);
+          }
+      w.host(T_LCOUNT, cnt.data(), sizeof(int32_t) * cnt.size());
+      write_rows(w, T_LLABELS, T_LROWS, lists, slots, labels, stage_x, stage_i, wst);
+    }
+    std::vector<int64_t> blabels;
+    const std::vector<int64_t> bslots = live_slots(buf.st, blabels);
+    write_rows(w, T_BLABELS, T_BROWS, buf.st, bslots, blabels, stage_x, stage_i, wst);
+    w.commit();
+  }
+
+  void load(const std::string &path) override {  // :259-298
+    ImageReader r(path);
+    check_image(r, PYR_IVF_FLAT, *this);
+    buf.clear(wst);
+    built = false;
+    lists.clear();
+    lstate.clear();
+    pos_of.clear();
+    lb.clear();
+    le.clear();
+    llen.clear();
+    llive.clear();
+    max_len = 0;
+    uint8_t b = 0;
+    if (r.has(T_BUILT)) r.host(T_BUILT, &b, 1);
+    const std::vector<float> cents = r.vec<float>(T_CENTS);
+    const int k = (int)(cents.size() / dim);
+    if (b && k > 0) {
+      const std::vector<int32_t> cnt = r.vec<int32_t>(T_LCOUNT);
+      if ((int)cnt.size() != k) ImageReader::throw_format("list counts do not match the centroids");
+      const std::vector<int64_t> labels = r.vec<int64_t>(T_LLABELS);
+      std::vector<int32_t> asg;
+      asg.reserve(labels.size());
+      for (int l = 0; l < k; l++) asg.insert(asg.end(), (size_t)cnt[l], l);
+      if (asg.size() != labels.size()) ImageReader::throw_format("list counts do not match the labels");
+      const int64_t n = (int64_t)labels.size();
+      DevMem X, C;
+      X.ensure(sizeof(float) * std::max<int64_t>(n, 1) * dim);
+      if (n) r.device(T_LROWS, X.p, sizeof(float) * n * dim, wst);
+      C.ensure(sizeof(float) * k * dim);
+      HIPCHK(hipMemcpyAsync(C.p, cents.data(), sizeof(float) * k * dim, hipMemcpyHostToDevice, wst));
+      commit_lists(X.as<float>(), n, asg, labels, C.as<float>(), k);
+      built = true;
+    }
+    std::vector<int64_t> blabels;
+    std::vector<float> brows;
+    const int64_t nb = read_rows(r, T_BLABELS, T_BROWS, dim, blabels, brows);
+    if (nb) add(brows.data(), nb, blabels.data(), true);  // buffer ids shadow their list entries (:210)
   }
 
   int64_t count() const override {  // :305 buffer + all list entries (shadowed ones too)
@@ -1499,6 +1728,15 @@ struct IvfPqIndex : Index {
     std::vector<int32_t> asg(n);
     HIPCHK(hipMemcpyAsync(asg.data(), A.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, wst));
     HIPCHK(hipStreamSynchronize(wst));
+    commit_codes(codes_rm.as<uint8_t>(), n, asg, labs, C.as<float>(), nc);
+    buf.clear(wst);                                    // :109
+    built = true;
+  }
+
+  // codes (device, row-major n x M; row i has label labs[i]) into the list-major blocked layout by
+  // list asg[i] (lists keep code order, padded to 64 rows), with quantizer C (nc x dim, device)
+  void commit_codes(const uint8_t *codes_rm, int64_t n, const std::vector<int32_t> &asg,
+                    const std::vector<int64_t> &labs, const float *C, int nc) {
     std::vector<int32_t> cnt(nc, 0);
     for (int32_t a : asg) cnt[a]++;
     lb.assign(nc, 0);
@@ -1523,7 +1761,7 @@ struct IvfPqIndex : Index {
     DevMem dsrc;
     dsrc.ensure(sizeof(int64_t) * std::max<int64_t>(tot, 1));
     HIPCHK(hipMemcpyAsync(dsrc.p, src.data(), sizeof(int64_t) * tot, hipMemcpyHostToDevice, wst));
-    launch_pack_codes(codes_rm.as<uint8_t>(), dsrc.as<int64_t>(), tot, M, codes.as<uint8_t>(), wst);
+    launch_pack_codes(codes_rm, dsrc.as<int64_t>(), tot, M, codes.as<uint8_t>(), wst);
     hlive.assign(tot, 0);
     for (int64_t p = 0; p < tot; p++) hlive[p] = src[p] >= 0;
     clive.ensure(std::max<int64_t>(tot, 1));
@@ -1534,15 +1772,13 @@ struct IvfPqIndex : Index {
     pos_of.clear();
     for (int64_t p = 0; p < tot; p++)
       if (hlabels[p] >= 0) pos_of[hlabels[p]] = p;
-    coarse.set(C.as<float>(), nc, dim, metric, wst);
+    coarse.set(C, nc, dim, metric, wst);
     dlb.ensure(sizeof(int32_t) * nc);
     dle.ensure(sizeof(int32_t) * nc);
     HIPCHK(hipMemcpyAsync(dlb.p, lb.data(), sizeof(int32_t) * nc, hipMemcpyHostToDevice, wst));
     HIPCHK(hipMemcpyAsync(dle.p, le.data(), sizeof(int32_t) * nc, hipMemcpyHostToDevice, wst));
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(wst));
-    buf.clear(wst);                                    // :109
-    built = true;
   }
 
   void search(const float *d_q, int64_t nq, int k, const pyr_search_params &prm, float *d_s, int64_t *d_l,
@@ -1635,6 +1871,76 @@ struct IvfPqIndex : Index {
   }
 
   int64_t count() const override { return 0; }  // :230 GetStats quirk
+
+  // The reference's IvfPq Snapshot / Load are no-ops (:228-229); the image persists the trained
+  // state (quantizer, codebooks, codes in list order) and the buffer like IVF_FLAT's.
+  void snapshot(const std::string &path) override {
+    ImageWriter w(path, PYR_IVF_PQ, dim, metric);
+    const uint8_t b = built ? 1 : 0;
+    w.host(T_BUILT, &b, 1);
+    if (built) {
+      w.host(T_CENTS, coarse.host.data(), sizeof(float) * coarse.host.size());
+      const int32_t ks = ksub;
+      w.host(T_KSUB, &ks, sizeof(ks));
+      w.device(T_CODEBOOKS, cb.p, sizeof(float) * (size_t)M * ksub * sub, wst);
+      w.host(T_LCOUNT, llen.data(), sizeof(int32_t) * llen.size());
+      std::vector<int64_t> labels;
+      for (int l = 0; l < coarse.nlist; l++)
+        for (int32_t p = lb[l]; p < lb[l] + llen[l]; p++) labels.push_back(hlabels[p]);
+      w.host(T_LLABELS, labels.data(), sizeof(int64_t) * labels.size());
+      std::vector<uint8_t> codes_rm(labels.size() * (size_t)M);
+      pq_state(nullptr, nullptr, codes_rm.data());  // list-major rows of M codes
+      w.host(T_LCODES, codes_rm.data(), codes_rm.size());
+    }
+    std::vector<int64_t> blabels;
+    const std::vector<int64_t> bslots = live_slots(buf.st, blabels);
+    write_rows(w, T_BLABELS, T_BROWS, buf.st, bslots, blabels, stage_x, stage_i, wst);
+    w.commit();
+  }
+
+  void load(const std::string &path) override {
+    ImageReader r(path);
+    check_image(r, PYR_IVF_PQ, *this);
+    buf.clear(wst);
+    built = false;
+    hlabels.clear();
+    hlive.clear();
+    pos_of.clear();
+    lb.clear();
+    le.clear();
+    llen.clear();
+    ncode_rows = 0;
+    uint8_t b = 0;
+    if (r.has(T_BUILT)) r.host(T_BUILT, &b, 1);
+    const std::vector<float> cents = r.vec<float>(T_CENTS);
+    const int k = (int)(cents.size() / dim);
+    if (b && k > 0) {
+      int32_t ks = 0;
+      r.host(T_KSUB, &ks, sizeof(ks));
+      if (ks <= 0 || ks > K) ImageReader::throw_format("codebook size out of range");
+      ksub = ks;
+      cb.ensure(sizeof(float) * (size_t)M * ksub * sub);
+      r.device(T_CODEBOOKS, cb.p, sizeof(float) * (size_t)M * ksub * sub, wst);
+      const std::vector<int32_t> cnt = r.vec<int32_t>(T_LCOUNT);
+      if ((int)cnt.size() != k) ImageReader::throw_format("list counts do not match the centroids");
+      const std::vector<int64_t> labels = r.vec<int64_t>(T_LLABELS);
+      std::vector<int32_t> asg;
+      for (int l = 0; l < k; l++) asg.insert(asg.end(), (size_t)cnt[l], l);
+      if (asg.size() != labels.size()) ImageReader::throw_format("list counts do not match the labels");
+      const int64_t n = (int64_t)labels.size();
+      DevMem codes_rm, C;
+      codes_rm.ensure((size_t)std::max<int64_t>(n, 1) * M);
+      if (n) r.device(T_LCODES, codes_rm.p, (size_t)n * M, wst);
+      C.ensure(sizeof(float) * k * dim);
+      HIPCHK(hipMemcpyAsync(C.p, cents.data(), sizeof(float) * k * dim, hipMemcpyHostToDevice, wst));
+      commit_codes(codes_rm.as<uint8_t>(), n, asg, labels, C.as<float>(), k);
+      built = true;
+    }
+    std::vector<int64_t> blabels;
+    std::vector<float> brows;
+    const int64_t nb = read_rows(r, T_BLABELS, T_BROWS, dim, blabels, brows);
+    if (nb) add(brows.data(), nb, blabels.data(), true);  // buffer ids hide their list entries (:134,170)
+  }
 
   void ivf_layout(int64_t *off, int64_t *labels, uint8_t *live, int64_t *total) const override {
     int64_t t = 0;

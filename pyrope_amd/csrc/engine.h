@@ -89,6 +89,7 @@ struct Workspace {
   DevMem ivf_cnt2, ivf_fill2, ivf_qoff2, ivf_ioff2, qlist2;  // second item set (nearest-list seeding)
   DevMem out_s, out_l, out_c;
   DevMem ms, mk, fail, fail_cnt, fq, fs, fl, fc;  // MFMA filter: merged candidates, certificate failures
+  DevMem fprobes;                                 // probe lists of the failing queries (IVF exact re-run)
   DevMem q8q, q8qs;                               // 8-bit search mode: quantized queries, their sums
   const int32_t *ext_probes = nullptr;            // caller-ranked probe lists [nq][ext_nprobe] (multi-GPU)
   int32_t ext_nprobe = 0;
@@ -101,6 +102,7 @@ struct Index {
   pyr_index_desc desc{};
   int dim = 0, metric = 0, device = 0;
   mutable std::shared_mutex mu;
+  std::mutex wmu;             // snapshot (shared lock on mu) vs the write stream / staging buffers
   hipStream_t wst = nullptr;  // stream for writes/builds
   DevMem stage_x, stage_i, stage_b;
   std::mutex ws_mu;
@@ -142,6 +144,15 @@ struct Index {
   virtual void set_quantization(bool on) {
     (void)on;
     throw Error(PYR_E_STATE, "index kind has no quantized search mode (BruteForceVectorIndex only)");
+  }
+  // IVectorIndex.Snapshot / Load (IVectorIndex.cs:26-27): the binary image of persist.h
+  virtual void snapshot(const std::string &path) {
+    (void)path;
+    throw Error(PYR_E_STATE, "index kind has no snapshot");
+  }
+  virtual void load(const std::string &path) {
+    (void)path;
+    throw Error(PYR_E_STATE, "index kind has no snapshot");
   }
   virtual void set_centroids(const float *c, int nlist) {
     (void)c;

@@ -555,7 +555,26 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
     }
     const double u = 5.9604644775390625e-8;  // 2^-24
     const double qn = sqrt((double)qsq) * (1.0 + 1e-5);
-    const double X = sqrt((double)key_score(*a.max_rsq)) * (1.0 + 1e-5);
+    // X bounds the norm of every row this query's scan could have excluded: the largest |x|^2
+    // of its probed lists (IVF), else of the whole store
+    uint32_t xk = 0;
+    if (a.list_rmax) {
+      for (int p = lane; p < a.nprobe; p += 64) xk = max(xk, a.list_rmax[a.probes[(size_t)q * a.nprobe + p]]);
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) xk = max(xk, (uint32_t)__shfl_xor((int)xk, off));
+    } else {
+      xk = *a.max_rsq;
+    }
+    double X = sqrt((double)key_score(xk)) * (1.0 + 1e-5);
+    if (MET == L2 && a.tri) {
+      // Rows far from the query cannot reach skth whatever the filter saw: the reference's L2 sum
+      // adds non-negative terms, so its value is |q - x|^2 (1 +- 22u) (D <= 128; c_err u is far
+      // above that), and |q - x| >= |x| - |q|.  A row with |x| >= |q| + r, r^2 = -skth (1 + 2 c_err u),
+      // therefore scores below skth; only rows with |x| < |q| + r need the error bound, so X may
+      // be lowered to |q| + r (one large-norm outlier in a probed list then costs nothing).
+      const double r = sqrt(fmax(0.0, -(double)skth) * (1.0 + 2.0 * a.c_err * u) + 1e-30) * (1.0 + 1e-6);
+      X = fmin(X, qn + r);
+    }
     const double e = (MET == L2 ? a.c_err * u * (qn + X) * (qn + X) : a.c_err * u * qn * X) +
                      a.c_bf * u * qn * X + (a.c_bf > 0.0 ? 1e-30 * (1.0 + qn + X) * D : 0.0);  // bf16 subnormals
     const double approx_k1 = MET == L2 ? (double)ms[k1 - 1] - (double)qsq : (double)ms[k1 - 1];
@@ -600,19 +619,36 @@ __global__ void sqnorms_kernel(const float *rows, const int64_t *slots, int64_t 
     s = s + x * x;
   }
   out[r] = s;
-  atomicMax(max_key, score_key(s));
+  // a NaN / inf row cannot be certified against anyway (its approximate score is never a
+  // candidate); leaving it out keeps one bad row from failing every later certificate
+  if (isfinite(s)) atomicMax(max_key, score_key(s));
+}
+
+// per-list max of |x|^2 (score_key, finite rows only) over rows [lb[l], le[l]): the refine
+// certificate of an IVF query bounds row norms over its probed lists only
+__global__ __launch_bounds__(256) void list_rmax_kernel(const float *rsq, const int32_t *lb, const int32_t *le,
+                                                        int nlist, uint32_t *out) {
+  const int l = blockIdx.x;
+  if (l >= nlist) return;
+  uint32_t m = 0;
+  for (int r = lb[l] + (int)threadIdx.x; r < le[l]; r += 256) {
+    const float v = rsq[r];
+    if (isfinite(v)) m = max(m, score_key(v));
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off));
+  __shared__ uint32_t wm[4];
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) out[l] = max(max(wm[0], wm[1]), max(wm[2], wm[3]));
 }
 
 inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
 template <int D, int MET, bool IVF, int KR, bool BF, int NW>
 void launch_filter_p(const FilterArgs &a, int max_items, hipStream_t st) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mfma_filter<D, MET, IVF, KR, BF, NW>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
+  static std::atomic<uint64_t> attr{0};
+  allow_max_lds(reinterpret_cast<const void *>(&mfma_filter<D, MET, IVF, KR, BF, NW>), attr);
   const size_t lds = FilterLds<D, BF, NW>::bytes() - (BF && a.single ? FilterLds<D, BF, NW>::tiles_bytes() / 2 : 0);
   const int grid = a.xcd ? (max_items + 7) / 8 * 8 : max_items;
   hipLaunchKernelGGL((mfma_filter<D, MET, IVF, KR, BF, NW>), dim3(grid), dim3(64 * NW), lds, st, a);
@@ -686,6 +722,12 @@ void launch_scatter_results(const int32_t *qidx, int64_t n, int32_t k, const flo
   if (n <= 0 || k <= 0) return;
   hipLaunchKernelGGL(scatter_results_kernel, dim3(nblk(n * k, 256)), dim3(256), 0, st, qidx, n, k, ss, sl, sc, out_s,
                      out_l, out_c);
+}
+
+void launch_list_rmax(const float *rsq, const int32_t *lb, const int32_t *le, int32_t nlist, uint32_t *out,
+                      hipStream_t st) {
+  if (nlist <= 0) return;
+  hipLaunchKernelGGL(list_rmax_kernel, dim3(nlist), dim3(256), 0, st, rsq, lb, le, nlist, out);
 }
 
 void launch_sqnorms(const float *rows, const int64_t *slots, int64_t n, int32_t dim, float *out, uint32_t *max_key,

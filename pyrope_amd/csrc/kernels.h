@@ -4,7 +4,22 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 namespace pyr {
+
+// Raise a kernel's dynamic-LDS limit to the whole 160 KiB of a CU.  The attribute is per
+// device, so it is set once per (kernel, device ordinal) -- `done` is the kernel's bit mask of
+// devices -- and the bit is published only after the call, so a thread that sees it set (any
+// thread, any index on any device) launches with the attribute in place.
+inline void allow_max_lds(const void *fn, std::atomic<uint64_t> &done) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const uint64_t bit = uint64_t(1) << (dev & 63);
+  if (done.load(std::memory_order_acquire) & bit) return;
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  done.fetch_or(bit, std::memory_order_acq_rel);
+}
 
 enum Metric { L2 = 0, IP = 1, COS = 2 };
 
@@ -264,6 +279,10 @@ struct RefineArgs {
   const float *ms;          // merged approximate scores [nq][k1] (desc)
   const int32_t *mk;        // merged keys [nq][k1] (-1 = none)
   const uint32_t *max_rsq;  // score_key(max |x|^2 over the store) (device scalar)
+  const uint32_t *list_rmax;  // IVF: score_key(max |x|^2) per list, or null (use max_rsq)
+  const int32_t *probes;      // IVF: [nq][nprobe] probed lists (with list_rmax)
+  int32_t nprobe;
+  int32_t tri;                // L2: also bound row norms by |q| + sqrt(-skth) (refine_kernel)
   int64_t nq;
   int32_t k1, k, dim;
   double c_err;             // error-bound constant (refine_kernel)
@@ -282,6 +301,9 @@ void launch_gather_queries(const float *q, const int32_t *qidx, int64_t n, int32
 void launch_scatter_results(const int32_t *qidx, int64_t n, int32_t k, const float *ss, const int64_t *sl,
                             const int32_t *sc, float *out_s, int64_t *out_l, int32_t *out_c, hipStream_t st);
 // |x|^2 of blocked rows (at slots, or rows [0,n) when slots is null) + atomic running max
+// per-list max |x|^2 (score_key; finite rows) of rows [lb[l], le[l]) -> out[nlist]
+void launch_list_rmax(const float *rsq, const int32_t *lb, const int32_t *le, int32_t nlist, uint32_t *out,
+                      hipStream_t st);
 void launch_sqnorms(const float *rows, const int64_t *slots, int64_t n, int32_t dim, float *out, uint32_t *max_key,
                     hipStream_t st);
 
@@ -299,6 +321,9 @@ void launch_gather_blocked(const float *src, const int64_t *src_slots, int64_t n
 void launch_gather2(const float *A, const float *B, const int64_t *idx, int64_t n, int32_t dim, float *out,
                     hipStream_t st);
 void launch_gather_rows(const float *src, const int32_t *idx, int64_t n, int32_t dim, float *out, hipStream_t st);
+// out[i][:] = src[idx[i]][:] for int32 rows of `width` entries (probe lists of a query subset)
+void launch_gather_rows_i32(const int32_t *src, const int32_t *idx, int64_t n, int32_t width, int32_t *out,
+                            hipStream_t st);
 
 // k-means helpers (KMeansUtils.cs:40-62)
 void launch_keys_to_assign(const uint32_t *keys, int64_t n, int32_t *assign, hipStream_t st);

@@ -1352,7 +1352,8 @@ __global__ void gather2_kernel(const float *A, const float *B, const int64_t *id
   const int64_t s = idx[i];
   out[e] = s >= 0 ? A[blk_off(s, d, D)] : B[blk_off(-s - 1, d, D)];
 }
-__global__ void gather_rows_kernel(const float *src, const int32_t *idx, int64_t n, int D, float *out) {
+template <class T>
+__global__ void gather_rows_kernel(const T *src, const int32_t *idx, int64_t n, int D, T *out) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n * D) return;
   const int64_t i = e / D;
@@ -1446,12 +1447,8 @@ template <int D, int V, int MET, int GPS, bool IVF, int QS, int W>
 void launch_fast_i(const ScanArgs &a, int max_items, hipStream_t st) {
   const size_t lds =
       (size_t)(2 * GPS * D * 8 + 2 * QCHUNK * score_stride<GPS>() + QCHUNK * a.k * 2) * sizeof(float);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&scan_fast<D, V, MET, GPS, IVF, QS, W>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
+  static std::atomic<uint64_t> attr{0};
+  allow_max_lds(reinterpret_cast<const void *>(&scan_fast<D, V, MET, GPS, IVF, QS, W>), attr);
   hipLaunchKernelGGL((scan_fast<D, V, MET, GPS, IVF, QS, W>), dim3(max_items), dim3(8 * QCHUNK / QS), lds, st, a);
 }
 
@@ -1487,12 +1484,8 @@ void launch_fast_t(const ScanArgs &a, int max_items, hipStream_t st) {
 template <int V, int MET>
 void launch_generic_t(const ScanArgs &a, int max_items, hipStream_t st) {
   const size_t lds = (size_t)64 * a.k * 8;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&scan_generic<V, MET>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
+  static std::atomic<uint64_t> attr{0};
+  allow_max_lds(reinterpret_cast<const void *>(&scan_generic<V, MET>), attr);
   hipLaunchKernelGGL((scan_generic<V, MET>), dim3(max_items), dim3(64), lds, st, a);
 }
 
@@ -1626,12 +1619,8 @@ bool pq_adc4_supported(int dim, int M, int ksub, int k) {
 }
 template <int SUB, bool K256, int NT>
 static void launch_pq_adc4_nt(const PqArgs &a, int max_items, hipStream_t st) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&pq_adc4_kernel<SUB, K256, NT>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
+  static std::atomic<uint64_t> attr{0};
+  allow_max_lds(reinterpret_cast<const void *>(&pq_adc4_kernel<SUB, K256, NT>), attr);
   const int grid = (max_items + 7) / 8 * 8;
   hipLaunchKernelGGL((pq_adc4_kernel<SUB, K256, NT>), dim3(grid), dim3(NT), pq_adc4_lds_bytes(a.dim, a.ksub, a.k), st,
                      a);
@@ -1663,12 +1652,8 @@ void launch_pq_adc4(const PqArgs &a, int max_items, hipStream_t st) {
 
 template <int NCH, bool K256, int NT>
 static void launch_pq_adc_nt(const PqArgs &a, int max_items, hipStream_t st) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&pq_adc_kernel<NCH, K256, NT>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
+  static std::atomic<uint64_t> attr{0};
+  allow_max_lds(reinterpret_cast<const void *>(&pq_adc_kernel<NCH, K256, NT>), attr);
   const int grid = (max_items + 7) / 8 * 8;  // XCD-major item mapping needs a multiple of 8 blocks
   hipLaunchKernelGGL((pq_adc_kernel<NCH, K256, NT>), dim3(grid), dim3(NT), pq_adc_lds_bytes(a.dim, a.M, a.ksub, a.k),
                      st, a);
@@ -1704,12 +1689,8 @@ void launch_pq_adc(const PqArgs &a, int max_items, hipStream_t st) {
 
 void launch_pq_scan(const PqArgs &a, int max_items, hipStream_t st) {
   if (max_items <= 0) return;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&pq_scan_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
+  static std::atomic<uint64_t> attr{0};
+  allow_max_lds(reinterpret_cast<const void *>(&pq_scan_kernel), attr);
   hipLaunchKernelGGL(pq_scan_kernel, dim3(max_items), dim3(256), pq_scan_lds_bytes(a.dim, a.M, a.ksub, a.k), st, a);
 }
 
@@ -1759,7 +1740,14 @@ void launch_gather2(const float *A, const float *B, const int64_t *idx, int64_t 
 }
 void launch_gather_rows(const float *src, const int32_t *idx, int64_t n, int32_t dim, float *out, hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(gather_rows_kernel, dim3(nblk(n * dim, 256)), dim3(256), 0, st, src, idx, n, dim, out);
+  hipLaunchKernelGGL(gather_rows_kernel<float>, dim3(nblk(n * dim, 256)), dim3(256), 0, st, src, idx, n, dim, out);
+}
+
+void launch_gather_rows_i32(const int32_t *src, const int32_t *idx, int64_t n, int32_t width, int32_t *out,
+                            hipStream_t st) {
+  if (n <= 0 || width <= 0) return;
+  hipLaunchKernelGGL(gather_rows_kernel<int32_t>, dim3(nblk(n * width, 256)), dim3(256), 0, st, src, idx, n, width,
+                     out);
 }
 
 void launch_keys_to_assign(const uint32_t *keys, int64_t n, int32_t *assign, hipStream_t st) {

@@ -13,6 +13,8 @@ from __future__ import annotations
 
 import ctypes as C
 import enum
+import json
+import os
 import re
 import threading
 from abc import ABC, abstractmethod
@@ -72,11 +74,11 @@ class IVectorIndex(ABC):  # IVectorIndex.cs:14-29
     @abstractmethod
     def build(self) -> None: ...
 
-    def snapshot(self, path: str) -> None:  # on-disk format is SURVEY.md 8(f)-4 (not this round)
-        raise NotImplementedError("Snapshot is not part of the scan path (SURVEY.md 8f-4)")
+    @abstractmethod
+    def snapshot(self, path: str) -> None: ...
 
-    def load(self, path: str) -> None:
-        raise NotImplementedError("Load is not part of the scan path (SURVEY.md 8f-4)")
+    @abstractmethod
+    def load(self, path: str) -> None: ...
 
     @abstractmethod
     def get_stats(self) -> IndexStats: ...
@@ -110,6 +112,7 @@ class HipVectorIndex(IVectorIndex):
         self._h = h
         self._label_of: Dict[str, int] = {}
         self._id_of: Dict[int, str] = {}
+        self._next_label = 0  # labels are never reused: above every label handed out so far
 
     def close(self) -> None:
         if getattr(self, "_h", None):
@@ -126,10 +129,19 @@ class HipVectorIndex(IVectorIndex):
     def _label(self, id: str) -> int:
         lab = self._label_of.get(id)
         if lab is None:
-            lab = len(self._label_of)
+            lab = self._next_label
+            self._next_label += 1
             self._label_of[id] = lab
             self._id_of[lab] = id
         return lab
+
+    def _register_labels(self, labels: np.ndarray) -> None:
+        """Caller-chosen labels (id = str(label)); later new ids get labels above all of them."""
+        for lab in labels.tolist():
+            self._label_of[str(lab)] = lab
+            self._id_of[lab] = str(lab)
+        if len(labels):
+            self._next_label = max(self._next_label, int(labels.max()) + 1)
 
     def _vec(self, vector) -> np.ndarray:
         if vector is None:
@@ -156,12 +168,18 @@ class HipVectorIndex(IVectorIndex):
     def add_batch(self, ids: Sequence[str], x: np.ndarray) -> None:
         self._write(self._L.pyr_index_add, ids, x)
 
-    def add_labels(self, labels: np.ndarray, x: np.ndarray) -> None:
-        """Bulk add with caller-chosen int64 labels (id = str(label))."""
+    def upsert_batch(self, ids: Sequence[str], x: np.ndarray) -> None:
+        """Upsert of many rows in one call, applied in order (a repeated id: the last row wins)."""
+        self._write(self._L.pyr_index_upsert, ids, x)
+
+    def add_labels(self, labels: np.ndarray, x: np.ndarray, track_ids: bool = True) -> None:
+        """Bulk add with caller-chosen int64 labels (id = str(label)).  track_ids=False skips the
+        host id map (bulk loads that only ever read labels back, e.g. bench.py at 10^7+ rows)."""
         labels = np.ascontiguousarray(labels, dtype=np.int64)
-        for lab in labels.tolist():
-            self._label_of[str(lab)] = lab
-            self._id_of[lab] = str(lab)
+        if track_ids:
+            self._register_labels(labels)
+        elif len(labels):
+            self._next_label = max(self._next_label, int(labels.max()) + 1)
         x = np.ascontiguousarray(x, dtype=np.float32)
         check(self._L.pyr_index_add(self._h, ptr(x, C.c_float), len(labels), ptr(labels, C.c_int64)))
 
@@ -203,7 +221,8 @@ class HipVectorIndex(IVectorIndex):
     def search(self, query, top_k: int, options: Optional[SearchOptions] = None) -> List[SearchResult]:
         q = self._vec(query)
         s, lab, cnt = self.search_batch(q[None, :], top_k, options)
-        return [SearchResult(self._id_of[int(lab[0, j])], float(s[0, j])) for j in range(int(cnt[0]))]
+        return [SearchResult(self._id_of.get(int(lab[0, j]), str(int(lab[0, j]))), float(s[0, j]))
+                for j in range(int(cnt[0]))]
 
     def search_device(self, d_q: int, nq: int, top_k: int, d_scores: int, d_labels: int, d_counts: int = 0,
                       stream: int = 0, options: Optional[SearchOptions] = None, d_probes: int = 0,
@@ -239,6 +258,35 @@ class HipVectorIndex(IVectorIndex):
         cnt = C.c_int64()
         check(self._L.pyr_index_stats(self._h, C.byref(cnt), None, None))
         return IndexStats(int(cnt.value), self.dimension, self.metric.name)
+
+    # ---- IVectorIndex.Snapshot / Load (IVectorIndex.cs:26-27) ----
+    def snapshot(self, path: str) -> None:
+        """The library's binary image at `path` (pyr_index_snapshot) plus the shim's id <-> label map
+        at path + ".ids" (JSON), each written through a temp file and a rename."""
+        if path is None or str(path).strip() == "":
+            raise ArgumentException("Path cannot be empty.")
+        check(self._L.pyr_index_snapshot(self._h, os.fsencode(str(path))))
+        ids = {"next": self._next_label, "ids": [[i, lab] for i, lab in self._label_of.items()]}
+        tmp = str(path) + ".ids.tmp"
+        with open(tmp, "w") as f:
+            json.dump(ids, f)
+        os.replace(tmp, str(path) + ".ids")
+
+    def load(self, path: str) -> None:
+        if path is None or str(path).strip() == "":
+            raise ArgumentException("Path cannot be empty.")
+        check(self._L.pyr_index_load(self._h, os.fsencode(str(path))))
+        self._label_of, self._id_of = {}, {}
+        self._next_label = 0
+        try:
+            with open(str(path) + ".ids") as f:
+                ids = json.load(f)
+        except FileNotFoundError:
+            return  # an image without the shim's map: ids read back as str(label)
+        for i, lab in ids["ids"]:
+            self._label_of[i] = lab
+            self._id_of[lab] = i
+        self._next_label = int(ids.get("next", 0))
 
     # ---- introspection used by parity tests and the CPU baseline ----
     def ivf_layout(self):
@@ -292,7 +340,7 @@ class BruteForceVectorIndex(HipVectorIndex):
         labels = np.zeros(n.value, np.int64)
         x = np.zeros((n.value, self.dimension), np.float32)
         check(self._L.pyr_index_scan(self._h, ptr(labels, C.c_int64), ptr(x, C.c_float), C.byref(n)))
-        return [(self._id_of[int(lab)], x[i]) for i, lab in enumerate(labels.tolist())]
+        return [(self._id_of.get(int(lab), str(int(lab))), x[i]) for i, lab in enumerate(labels.tolist())]
 
     def delete_many(self, ids: Sequence[str]) -> None:
         labels = np.array([self._label_of[i] for i in ids if i in self._label_of], np.int64)
@@ -411,6 +459,26 @@ class DeltaVectorIndex(IVectorIndex, ICentroidsProvider):
         h, t = self.head.get_stats(), self.tail.get_stats()
         return IndexStats(h.count + t.count, h.dimension, h.metric)
 
+    def snapshot(self, path: str) -> None:  # :160-191
+        with self._lock:
+            head_path, tail_path = path + ".head", path + ".tail"
+            self.head.snapshot(head_path + ".tmp")  # both components to temporary paths
+            self.tail.snapshot(tail_path + ".tmp")
+            for final in (head_path, tail_path):  # then moved into place (with the shim's id maps)
+                os.replace(final + ".tmp", final)
+                os.replace(final + ".tmp.ids", final + ".ids")
+            tmp = path + ".tmp"
+            with open(tmp, "w") as f:
+                f.write('{"Type": "Delta", "Head": ".head", "Tail": ".tail"}')
+            os.replace(tmp, path)  # the manifest last
+
+    def load(self, path: str) -> None:  # :193-212
+        with self._lock:
+            if os.path.exists(path + ".head"):
+                self.head.load(path + ".head")
+            if os.path.exists(path + ".tail"):
+                self.tail.load(path + ".tail")
+
     def get_centroids(self):  # :223-233
         return self.tail.get_centroids() if isinstance(self.tail, ICentroidsProvider) else None
 
@@ -515,4 +583,15 @@ def generate_synthetic(count: int, dim: int, seed: int) -> np.ndarray:
     """Pyrope.Benchmarks GenerateRandomVectors (Program.cs:251-263), via the library."""
     out = np.empty((count, dim), np.float32)
     check(_lib.load().pyr_generate_synthetic(count, dim, seed, ptr(out, C.c_float)))
+    return out
+
+
+BLOCK_ROWS = 65536  # rows per generator block (generate_synthetic_blocked)
+
+
+def generate_synthetic_blocked(row0: int, count: int, dim: int, seed: int, block_rows: int = BLOCK_ROWS) -> np.ndarray:
+    """Rows [row0, row0 + count) of the row-blocked synthetic set: block b (block_rows rows) is the
+    Program.cs:251-263 sequence of Random(seed + b) (SURVEY.md 8(d) large-N deviation)."""
+    out = np.empty((count, dim), np.float32)
+    check(_lib.load().pyr_generate_synthetic_blocked(row0, count, dim, seed, block_rows, ptr(out, C.c_float)))
     return out

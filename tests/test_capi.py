@@ -48,6 +48,18 @@ def test_generate_synthetic_matches_oracle(hiplib, oracle):
     np.testing.assert_array_equal(generate_synthetic(3, 5, 1337), oracle.generate_vectors(3, 5, 1337))
 
 
+def test_generate_synthetic_blocked_matches_oracle(hiplib, oracle):
+    """Row-blocked generator: block b = the Random(seed + b) sequence; any row
+    range, including ranges that start or end inside a block, equals the per-block oracle rows."""
+    from pyrope_amd import generate_synthetic, generate_synthetic_blocked
+    B, D = 37, 6
+    full = np.concatenate([oracle.generate_vectors(B, D, 42 + b) for b in range(5)])
+    for r0, n in [(0, 5 * B), (0, 10), (13, 60), (B, B), (2 * B + 5, 2 * B - 5), (4 * B + 36, 1)]:
+        np.testing.assert_array_equal(generate_synthetic_blocked(r0, n, D, 42, B), full[r0:r0 + n])
+    # within one block it is the plain generator
+    np.testing.assert_array_equal(generate_synthetic_blocked(0, 50, 16, 42), generate_synthetic(50, 16, 42))
+
+
 def _has_gpu():
     try:
         import torch

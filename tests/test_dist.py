@@ -1,8 +1,8 @@
 """Multi-GPU sharding (pyrope_amd/dist.py; SURVEY.md 8(e) option ii, rows within lists).
 
-Rank r holds base row i iff i % world == r and builds its lists with the shared coarse quantizer,
-so the union of the ranks' probed rows is exactly the unsharded index's probed rows, each scored
-with the same arithmetic.  One all_gather of the per-rank top-k partials + a merge by
+Rank r holds the generator blocks b with b % world == r and builds its lists with the shared
+coarse quantizer, so the union of the ranks' probed rows is exactly the unsharded index's probed
+rows, each scored with the same arithmetic.  One all_gather of the per-rank top-k partials + a merge by
 (score desc, label asc) must then give the unsharded result (ties between equal scores in
 different lists aside, which random fp32 data does not produce).
 
@@ -17,6 +17,7 @@ import numpy as np
 import pytest
 
 D, N, NLIST, NPROBE, K, NQ = 32, 3000, 16, 4, 10, 24
+BLK = 256  # generator block rows (the sharding unit) for these small sets
 
 
 def _free_port():
@@ -43,7 +44,7 @@ def _host_merge(s_parts, l_parts, k):
 def _shard_search(oracle, data, cents, queries, rank, world):
     """One rank's IVF search over its rows-within-list shard; returns global labels."""
     from pyrope_amd.dist import shard_labels
-    labels = shard_labels(len(data), world, rank)
+    labels = shard_labels(len(data), world, rank, BLK)
     rows = data[labels]
     assign = np.array([oracle.find_nearest_centroid(r, cents, oracle.L2) for r in rows], np.int32)
     lrows, order, off = oracle.lists_from_assign(rows, assign, len(cents))
@@ -77,12 +78,82 @@ def _worker(rank, world, port, data, cents, queries, out):
 
 
 def test_shard_labels_partition():
-    from pyrope_amd.dist import shard_labels
-    parts = [shard_labels(103, 4, r) for r in range(4)]
+    from pyrope_amd.dist import shard_blocks, shard_labels
+    parts = [shard_labels(103, 4, r, 10) for r in range(4)]
     allp = np.sort(np.concatenate(parts))
     np.testing.assert_array_equal(allp, np.arange(103))
     for r, p in enumerate(parts):
-        assert np.all(p % 4 == r) and np.all(np.diff(p) > 0)
+        assert np.all((p // 10) % 4 == r) and np.all(np.diff(p) > 0)
+    assert shard_blocks(103, 4, 2, 10) == [(20, 30), (60, 70), (100, 103)]
+    assert shard_labels(5, 3, 1, 10).size == 0  # more ranks than blocks: an empty shard
+
+
+def _oracle_shard(oracle, data, cents, rank, world):
+    """One rank's IVF lists over its blocks with the shared quantizer: (labels, lrows, order, off)."""
+    from pyrope_amd.dist import shard_labels
+    labels = shard_labels(len(data), world, rank, BLK)
+    rows = data[labels]
+    assign = np.array([oracle.find_nearest_centroid(r, cents, oracle.L2) for r in rows], np.int32)
+    lrows, order, off = oracle.lists_from_assign(rows, assign, len(cents))
+    return labels, lrows, order, off
+
+
+def _step_worker(rank, world, port, data, cents, queries, out):
+    """bench.py's N > 1 step (pyrope_amd.dist.sharded_ivf_step) with the oracle as the scan."""
+    import torch
+    import torch.distributed as dist
+
+    import oracle
+    from pyrope_amd.dist import sharded_ivf_step
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        labels, lrows, order, off = _oracle_shard(oracle, data, cents, rank, world)
+        seen = {}
+
+        def probe(qs):  # the coarse ranking of this rank's slice (pyr_index_probe_device)
+            return torch.from_numpy(np.stack([oracle.ivf_probe(q, cents, NPROBE) for q in qs.numpy()]))
+
+        def search(qs, probes):  # pyr_index_search_probed_device over this shard
+            seen["probes"] = probes.numpy()
+            S = np.full((len(qs), K), -np.inf, np.float32)
+            Lb = np.full((len(qs), K), -1, np.int64)
+            for i, q in enumerate(qs.numpy()):
+                s, kk = oracle.ivf_search_probed(q, K, lrows, off, probes[i].numpy())
+                S[i, :len(s)] = s
+                Lb[i, :len(s)] = labels[order[kk]]
+            return torch.from_numpy(S), torch.from_numpy(Lb)
+
+        def merge(sp, lp, k):  # pyr_merge_topk_device
+            return tuple(torch.from_numpy(a) for a in _host_merge(sp.numpy(), lp.numpy(), k))
+
+        s, lab = sharded_ivf_step(torch.from_numpy(queries), len(queries) // world, rank, world, probe, search,
+                                  merge, K)
+        np.save(os.path.join(out, f"s{rank}.npy"), s.numpy())
+        np.save(os.path.join(out, f"l{rank}.npy"), lab.numpy())
+        np.save(os.path.join(out, f"p{rank}.npy"), seen["probes"])
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_bench_step_equals_unsharded(oracle, tmp_path):
+    """the exact N > 1 step bench.py times -- split coarse ranking, probe all_gather,
+    per-rank probed search, partial all_gather, merge -- on 2 gloo ranks equals one unsharded search."""
+    import torch.multiprocessing as mp
+
+    data = oracle.generate_vectors(N, D, 42)
+    queries = oracle.generate_vectors(NQ, D, 1337)
+    cents = oracle.kmeans_train(data, NLIST, oracle.L2, 5, 42)
+    ref_s, ref_l = _shard_search(oracle, data, cents, queries, 0, 1)
+    ref_p = np.stack([oracle.ivf_probe(q, cents, NPROBE) for q in queries])
+    port = _free_port()
+    mp.start_processes(_step_worker, args=(2, port, data, cents, queries, str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    for r in range(2):
+        np.testing.assert_array_equal(np.load(tmp_path / f"p{r}.npy"), ref_p)  # every query's lists on every rank
+        np.testing.assert_array_equal(np.load(tmp_path / f"l{r}.npy"), ref_l)
+        assert np.array_equal(np.load(tmp_path / f"s{r}.npy").view(np.uint32), ref_s.view(np.uint32))
 
 
 def test_gloo_world2_sharded_equals_unsharded(oracle, tmp_path):
@@ -124,7 +195,7 @@ def test_gpu_two_shards_merge_equals_unsharded(hiplib):
     for r in range(2):
         idx = IvfFlatVectorIndex(d, 0, n_list=nl)
         idx.set_centroids(cents)
-        lab = shard_labels(n, 2, r)
+        lab = shard_labels(n, 2, r, 4096)
         idx.add_labels(lab, data[lab])
         idx.build()
         s, l, _ = idx.search_batch(q, K, opts)

@@ -28,3 +28,20 @@ def test_search_options_defaults():  # SearchOptions.cs:3
     from pyrope_amd import SearchOptions
     o = SearchOptions()
     assert o.max_scans is None and o.nprobe is None and o.ef_search is None
+
+
+def test_labels_never_collide_after_caller_chosen_labels():
+    """a new id must not get a label already handed out through add_labels
+    (e.g. the sparse shard labels r, r + world, ...)."""
+    import numpy as np
+
+    from pyrope_amd.vector import HipVectorIndex
+    ix = object.__new__(HipVectorIndex)  # host bookkeeping only: no device handle
+    ix._label_of, ix._id_of, ix._next_label = {}, {}, 0
+    ix._register_labels(np.array([1, 3, 5, 7], np.int64))
+    new = [ix._label("a"), ix._label("b"), ix._label("a")]
+    assert new == [8, 9, 8]
+    assert set(new).isdisjoint({1, 3, 5, 7})
+    ix._register_labels(np.array([2], np.int64))  # lower than the counter: the counter keeps going
+    assert ix._label("c") == 10
+    assert ix._id_of[8] == "a" and ix._label_of["7"] == 7
