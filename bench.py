@@ -213,6 +213,8 @@ def run(args):
         nrows += len(labs)
         if keep:
             kept.append(x)
+        if nrows % (5 * args.add_rows) < len(labs):  # progress for long (M8-size) loads
+            log(f"rank {rank}: {nrows} rows added ({time.time() - t:.0f}s)")
     idx.build()
     data = np.concatenate(kept) if keep else None  # world == 1: rows in base-row (= label) order
     del kept

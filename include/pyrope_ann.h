@@ -106,6 +106,13 @@ pyr_status pyr_kmeans_train(int32_t device, const float *data, int64_t n, int32_
 pyr_status pyr_index_search(pyr_index *index, const float *q, int64_t nq, int32_t k,
                             const pyr_search_params *params, float *out_scores, int64_t *out_labels,
                             int32_t *out_counts);
+/* Request coalescing for pyr_index_search (the reference serves one query per VEC.SEARCH call,
+ * Extensions/VectorCommandSet.cs:457-459, from many session threads): with max_wait_us > 0,
+ * concurrent pyr_index_search calls of fewer than max_batch queries and equal (k, params) are merged
+ * into one device search of up to max_batch queries, started when the batch is full or max_wait_us
+ * after its first query arrived; each caller gets exactly its own rows (results are per-query
+ * identical to uncoalesced calls).  max_wait_us <= 0 turns it off (the default). */
+pyr_status pyr_index_set_coalescing(pyr_index *index, int32_t max_batch, int32_t max_wait_us);
 /* Same on device-resident buffers (HBM), enqueued on `stream` (hipStream_t, NULL = default).
  * Does not synchronize the stream. */
 pyr_status pyr_index_search_device(pyr_index *index, const float *d_q, int64_t nq, int32_t k,
@@ -165,6 +172,13 @@ pyr_status pyr_index_set_quantization(pyr_index *index, int32_t enable);
 /* ScalarQuantizer.Quantize (ScalarQuantizer.cs:23-62) of n vectors (n x dim, row-major) on the
  * GPU: per-vector min/max, codes = clamp(round_half_even((x - min) * (255 / (max - min)))). */
 pyr_status pyr_scalar_quantize(int32_t device, const float *x, int64_t n, int32_t dim, uint8_t *codes);
+/* The same with Quantize's `out float min, out float max` per vector (mins / maxs: n entries, may be NULL). */
+pyr_status pyr_scalar_quantize_minmax(int32_t device, const float *x, int64_t n, int32_t dim, uint8_t *codes,
+                                      float *mins, float *maxs);
+/* ScalarQuantizer.Dequantize (ScalarQuantizer.cs:65-84) of n code rows: out = min + q * ((max - min) / 255)
+ * in fp32, or min everywhere when max == min. */
+pyr_status pyr_scalar_dequantize(int32_t device, const uint8_t *codes, int64_t n, int32_t dim, const float *mins,
+                                 const float *maxs, float *out);
 
 /* Introspection of the built IVF layout (list-major storage order, used by the
  * parity tests and the CPU baseline).  list_off: nlist+1 (row offsets without padding),

@@ -15,7 +15,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+#ifndef ORC_LANES
 #define W 8 /* Vector<float>.Count on x64 AVX2 */
+#else
+#define W ORC_LANES /* liboracle_w4.so: Vector<float>.Count on Arm64 NEON (lane-width study only) */
+#endif
 
 /* ------------------------------------------------------------------ */
 /* System.Random legacy generator (BCL Net5CompatSeedImpl) */
@@ -67,11 +71,16 @@ void orc_generate_vectors(int64_t count, int32_t dim, int32_t seed, float *out) 
 /* ------------------------------------------------------------------ */
 /* VectorMath.cs                                                        */
 /* ------------------------------------------------------------------ */
-/* Vector.Dot(v, One): AVX vdpps per 128-bit half, then add halves. */
+/* Vector.Dot(v, One): AVX vdpps per 128-bit half, then add halves (W = 8); the 4-lane NEON
+ * form (faddp pairwise adds) for the lane-width study. */
 static inline float hsum8(const float v[W]) {
+#if W == 8
   float lo = (v[0] + v[1]) + (v[2] + v[3]);
   float hi = (v[4] + v[5]) + (v[6] + v[7]);
   return lo + hi;
+#else
+  return (v[0] + v[1]) + (v[2] + v[3]);
+#endif
 }
 
 /* VectorMath.cs:8-37  DotProduct: one Vector accumulator. */

@@ -24,6 +24,15 @@ def build() -> None:
     subprocess.run(["make", "-s", "-C", _HERE], check=True)
 
 
+def lib_w4():
+    """The 4-lane (Arm64 NEON Vector<float>) build of the same restatement: lane-width study only."""
+    so = os.path.join(_HERE, "liboracle_w4.so")
+    subprocess.run(["make", "-s", "-C", _HERE, "w4"], check=True)
+    L = C.CDLL(so)
+    _declare(L)
+    return L
+
+
 def lib():
     global _lib
     if _lib is None:

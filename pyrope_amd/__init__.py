@@ -5,7 +5,7 @@ this package holds its in-tree build script, the ctypes binding and the host
 mirror of the reference's IVectorIndex plugin surface.
 """
 from .vector import (BruteForceVectorIndex, DeltaVectorIndex, HipVectorIndex, ICentroidsProvider,  # noqa: F401
-                     IndexStats, IvfFlatVectorIndex, IvfPqVectorIndex, IVectorIndex, SearchOptions,
+                     IndexStats, IvfFlatVectorIndex, IvfPqVectorIndex, IVectorIndex, ScalarQuantizer, SearchOptions,
                      SearchResult, VectorIndexRegistry, VectorMetric, generate_synthetic,
                      generate_synthetic_blocked, kmeans_train)
 from ._lib import (ArgumentException, ArgumentNullException, ArgumentOutOfRangeException,  # noqa: F401

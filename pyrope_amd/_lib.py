@@ -90,6 +90,7 @@ SIGNATURES = {
                                           _vp]),
     "pyr_index_stats": (C.c_int, [_vp, _i64, _i32, _i32]),
     "pyr_index_snapshot": (C.c_int, [_vp, C.c_char_p]),
+    "pyr_index_set_coalescing": (C.c_int, [_vp, C.c_int32, C.c_int32]),
     "pyr_index_load": (C.c_int, [_vp, C.c_char_p]),
     "pyr_index_get_centroids": (C.c_int, [_vp, _f, _i32]),
     "pyr_index_ivf_layout": (C.c_int, [_vp, _i64, _i64, _u8, _i64]),
@@ -100,6 +101,8 @@ SIGNATURES = {
     "pyr_index_search_probed_device": (C.c_int, [_vp, _vp, C.c_int64, C.c_int32, C.POINTER(SearchParams), _vp,
                                                  C.c_int32, _vp, _vp, _vp, _vp]),
     "pyr_scalar_quantize": (C.c_int, [C.c_int32, _f, C.c_int64, C.c_int32, _u8]),
+    "pyr_scalar_quantize_minmax": (C.c_int, [C.c_int32, _f, C.c_int64, C.c_int32, _u8, _f, _f]),
+    "pyr_scalar_dequantize": (C.c_int, [C.c_int32, _u8, C.c_int64, C.c_int32, _f, _f, _f]),
     "pyr_merge_topk_device": (C.c_int, [_vp, _vp, C.c_int64, C.c_int32, C.c_int32, _vp, _vp, _vp]),
     "pyr_generate_synthetic": (C.c_int, [C.c_int64, C.c_int32, C.c_int32, _f]),
     "pyr_generate_synthetic_blocked": (C.c_int, [C.c_int64, C.c_int64, C.c_int32, C.c_int32, C.c_int64, _f]),

@@ -3,6 +3,11 @@
 // message (pyr_last_error) and returns a pyr_status.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <map>
+#include <memory>
+#include <tuple>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -11,8 +16,42 @@
 
 #include "engine.h"
 
+namespace {
+// Request coalescer (pyr_index_set_coalescing).  The reference serves one query per VEC.SEARCH
+// call (VectorCommandSet.cs:457-459), one call per Garnet session thread; the scan reaches its
+// throughput only on batches.  Concurrent pyr_index_search calls with the same (k, SearchOptions)
+// join an open batch: the first caller (the leader) waits until the batch holds max_batch queries
+// or max_wait_us has passed since it opened, runs ONE device search for all of them and copies
+// every caller's rows into that caller's buffers; the other callers (followers) block until then.
+// Each query's result is the same as a search of it alone (the engine is per query exact).
+struct Batch {
+  int32_t k = 0;
+  pyr_search_params prm{};
+  std::vector<float> q;  // queries in arrival order
+  struct Part {
+    int64_t off, n;
+    float *s;
+    int64_t *l;
+    int32_t *c;
+  };
+  std::vector<Part> parts;
+  int64_t nq = 0;
+  bool closed = false, done = false;
+  pyr_status status = PYR_OK;
+  std::string err;
+  std::chrono::steady_clock::time_point deadline;
+};
+struct Coalescer {
+  std::mutex m;
+  std::condition_variable cv;
+  int32_t max_batch = 0, max_wait_us = 0;
+  std::map<std::tuple<int32_t, int32_t, int64_t>, std::shared_ptr<Batch>> open;  // (k, nprobe, max_scans)
+};
+}  // namespace
+
 struct pyr_index {
   std::unique_ptr<pyr::Index> impl;
+  Coalescer co;
 };
 
 namespace {
@@ -172,10 +211,8 @@ pyr_status pyr_profile_get(int32_t phase, double *total_ms, int64_t *calls, int6
   return PYR_OK;
 }
 
-pyr_status pyr_index_search(pyr_index *index, const float *q, int64_t nq, int32_t k, const pyr_search_params *params,
-                            float *out_scores, int64_t *out_labels, int32_t *out_counts) {
-  if (!index || nq < 0 || (nq > 0 && !q)) return fail(PYR_E_ARG, "null argument");
-  if (k > pyr::KMAX) return fail(PYR_E_ARG, "topK larger than 256 is not supported");
+static pyr_status search_host(pyr_index *index, const float *q, int64_t nq, int32_t k, const pyr_search_params *params,
+                              float *out_scores, int64_t *out_labels, int32_t *out_counts) {
   return guard([&] {
     pyr::Index &ix = *index->impl;
     HIPCHK(hipSetDevice(ix.device));
@@ -208,6 +245,90 @@ pyr_status pyr_index_search(pyr_index *index, const float *q, int64_t nq, int32_
     }
     ix.give_ws(std::move(ws));
   });
+}
+
+static pyr_status search_coalesced(pyr_index *index, const float *q, int64_t nq, int32_t k,
+                                   const pyr_search_params &prm, float *out_scores, int64_t *out_labels,
+                                   int32_t *out_counts) {
+  Coalescer &co = index->co;
+  const int dim = index->impl->dim;
+  std::unique_lock<std::mutex> lk(co.m);
+  const auto key = std::make_tuple(k, prm.nprobe, prm.max_scans);
+  auto it = co.open.find(key);
+  std::shared_ptr<Batch> b;
+  bool leader = false;
+  if (it == co.open.end() || it->second->closed || it->second->nq + nq > co.max_batch) {
+    b = std::make_shared<Batch>();
+    b->k = k;
+    b->prm = prm;
+    b->deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(co.max_wait_us);
+    co.open[key] = b;
+    leader = true;
+  } else {
+    b = it->second;
+  }
+  b->q.insert(b->q.end(), q, q + nq * dim);
+  b->parts.push_back({b->nq, nq, out_scores, out_labels, out_counts});
+  b->nq += nq;
+  if (b->nq >= co.max_batch) {  // full: the leader runs it now
+    b->closed = true;
+    if (co.open[key] == b) co.open.erase(key);
+    co.cv.notify_all();
+  }
+  if (!leader) {
+    co.cv.wait(lk, [&] { return b->done; });
+    if (b->status != PYR_OK) return fail(b->status, b->err);
+    return PYR_OK;
+  }
+  co.cv.wait_until(lk, b->deadline, [&] { return b->closed; });
+  if (!b->closed) {
+    b->closed = true;
+    auto f = co.open.find(key);
+    if (f != co.open.end() && f->second == b) co.open.erase(f);
+  }
+  lk.unlock();
+  // one device search for the whole batch, then every caller's rows into its own buffers
+  const int kk = k > 0 ? k : 0;
+  std::vector<float> s((size_t)b->nq * kk);
+  std::vector<int64_t> l((size_t)b->nq * kk);
+  std::vector<int32_t> c((size_t)b->nq);
+  const pyr_status st = search_host(index, b->q.data(), b->nq, k, &b->prm, s.data(), l.data(), c.data());
+  if (st == PYR_OK)
+    for (const Batch::Part &p : b->parts) {
+      if (p.s) std::memcpy(p.s, s.data() + p.off * kk, sizeof(float) * p.n * kk);
+      if (p.l) std::memcpy(p.l, l.data() + p.off * kk, sizeof(int64_t) * p.n * kk);
+      if (p.c) std::memcpy(p.c, c.data() + p.off, sizeof(int32_t) * p.n);
+    }
+  lk.lock();
+  b->status = st;
+  if (st != PYR_OK) b->err = pyr_last_error();
+  b->done = true;
+  co.cv.notify_all();
+  return st;
+}
+
+pyr_status pyr_index_search(pyr_index *index, const float *q, int64_t nq, int32_t k, const pyr_search_params *params,
+                            float *out_scores, int64_t *out_labels, int32_t *out_counts) {
+  if (!index || nq < 0 || (nq > 0 && !q)) return fail(PYR_E_ARG, "null argument");
+  if (k > pyr::KMAX) return fail(PYR_E_ARG, "topK larger than 256 is not supported");
+  int32_t mb, mw;
+  {
+    std::lock_guard<std::mutex> g(index->co.m);
+    mb = index->co.max_batch;
+    mw = index->co.max_wait_us;
+  }
+  if (mw > 0 && nq > 0 && k > 0 && nq < mb)
+    return search_coalesced(index, q, nq, k, defaults(params), out_scores, out_labels, out_counts);
+  return search_host(index, q, nq, k, params, out_scores, out_labels, out_counts);
+}
+
+pyr_status pyr_index_set_coalescing(pyr_index *index, int32_t max_batch, int32_t max_wait_us) {
+  if (!index) return fail(PYR_E_ARG, "null argument");
+  if (max_wait_us > 0 && max_batch < 2) return fail(PYR_E_ARG, "max_batch must be at least 2");
+  std::lock_guard<std::mutex> g(index->co.m);
+  index->co.max_batch = max_batch;
+  index->co.max_wait_us = max_wait_us > 0 ? max_wait_us : 0;
+  return PYR_OK;
 }
 
 pyr_status pyr_index_search_device(pyr_index *index, const float *d_q, int64_t nq, int32_t k,
@@ -339,28 +460,57 @@ pyr_status pyr_index_set_quantization(pyr_index *index, int32_t enable) {
   });
 }
 
-pyr_status pyr_scalar_quantize(int32_t device, const float *x, int64_t n, int32_t dim, uint8_t *codes) {
+pyr_status pyr_scalar_quantize_minmax(int32_t device, const float *x, int64_t n, int32_t dim, uint8_t *codes,
+                                      float *mins, float *maxs) {
   if (!x || !codes || n < 0 || dim <= 0) return fail(PYR_E_ARG, "bad arguments");
   return guard([&] {
     if (n == 0) return;
+    check_device(device);
     HIPCHK(hipSetDevice(device));
     const int dp = pyr::sq8_dp(dim);
-    float *dx = nullptr;
-    uint8_t *dc = nullptr;
-    int2 *ds = nullptr;
-    HIPCHK(hipMalloc(&dx, sizeof(float) * n * dim));
-    hipError_t e = hipMalloc(&dc, (size_t)dp * n);
-    if (e == hipSuccess) e = hipMalloc(&ds, sizeof(int2) * n);
-    if (e == hipSuccess) e = hipMemcpy(dx, x, sizeof(float) * n * dim, hipMemcpyHostToDevice);
-    if (e == hipSuccess) {
-      pyr::launch_sq8_quantize(dx, nullptr, 0, n, dim, dp, 0, dc, ds, nullptr, nullptr);
-      e = hipGetLastError();
+    pyr::DevMem dx, dc, ds, dm;
+    dx.ensure(sizeof(float) * n * dim);
+    dc.ensure((size_t)dp * n);
+    ds.ensure(sizeof(int2) * n);
+    dm.ensure(sizeof(float2) * n);
+    HIPCHK(hipMemcpy(dx.p, x, sizeof(float) * n * dim, hipMemcpyHostToDevice));
+    pyr::launch_sq8_quantize(dx.as<float>(), nullptr, 0, n, dim, dp, 0, dc.as<uint8_t>(), ds.as<int2>(), nullptr, nullptr,
+                             dm.as<float2>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpy2D(codes, dim, dc.p, dp, dim, n, hipMemcpyDeviceToHost));
+    if (mins || maxs) {
+      std::vector<float2> mm((size_t)n);
+      HIPCHK(hipMemcpy(mm.data(), dm.p, sizeof(float2) * n, hipMemcpyDeviceToHost));
+      for (int64_t i = 0; i < n; i++) {
+        if (mins) mins[i] = mm[i].x;
+        if (maxs) maxs[i] = mm[i].y;
+      }
     }
-    if (e == hipSuccess) e = hipMemcpy2D(codes, dim, dc, dp, dim, n, hipMemcpyDeviceToHost);
-    (void)hipFree(dx);
-    (void)hipFree(dc);
-    (void)hipFree(ds);
-    HIPCHK(e);
+  });
+}
+
+pyr_status pyr_scalar_quantize(int32_t device, const float *x, int64_t n, int32_t dim, uint8_t *codes) {
+  return pyr_scalar_quantize_minmax(device, x, n, dim, codes, nullptr, nullptr);
+}
+
+pyr_status pyr_scalar_dequantize(int32_t device, const uint8_t *codes, int64_t n, int32_t dim, const float *mins,
+                                 const float *maxs, float *out) {
+  if (!codes || !mins || !maxs || !out || n < 0 || dim < 0) return fail(PYR_E_ARG, "bad arguments");
+  return guard([&] {
+    if (n == 0 || dim == 0) return;
+    check_device(device);
+    HIPCHK(hipSetDevice(device));
+    pyr::DevMem dc, dmn, dmx, dout;
+    dc.ensure((size_t)n * dim);
+    dmn.ensure(sizeof(float) * n);
+    dmx.ensure(sizeof(float) * n);
+    dout.ensure(sizeof(float) * n * dim);
+    HIPCHK(hipMemcpy(dc.p, codes, (size_t)n * dim, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(dmn.p, mins, sizeof(float) * n, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(dmx.p, maxs, sizeof(float) * n, hipMemcpyHostToDevice));
+    pyr::launch_sq8_dequantize(dc.as<uint8_t>(), n, dim, dmn.as<float>(), dmx.as<float>(), dout.as<float>(), nullptr);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpy(out, dout.p, sizeof(float) * n * dim, hipMemcpyDeviceToHost));
   });
 }
 

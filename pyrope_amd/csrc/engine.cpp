@@ -7,6 +7,7 @@
 #include "engine.h"
 #include "persist.h"
 
+#include <cmath>
 #include <cstdio>
 
 #include <algorithm>
@@ -47,7 +48,8 @@ static int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 void RowStore::reserve(int64_t slots, hipStream_t st) {
   if (slots <= cap) return;
-  int64_t nc = round_up(std::max<int64_t>(slots, std::max<int64_t>(cap * 3 / 2, 64)), 8);
+  // whole 32-slot tiles (the fp16 filter's unit; a multiple of the blocked layout's 8)
+  int64_t nc = round_up(std::max<int64_t>(slots, std::max<int64_t>(cap * 3 / 2, 64)), 32);
   rows.grow_keep(sizeof(float) * nc * dim, sizeof(float) * cap * dim, st);
   live.grow_keep(nc, cap, st);
   labels.grow_keep(sizeof(int64_t) * nc, sizeof(int64_t) * cap, st);
@@ -62,7 +64,48 @@ void RowStore::reserve(int64_t slots, hipStream_t st) {
   HIPCHK(hipMemsetAsync(rows.as<float>() + cap * dim, 0, sizeof(float) * (nc - cap) * dim, st));
   HIPCHK(hipMemsetAsync(rsq.as<float>() + cap, 0, sizeof(float) * (nc - cap), st));
   if (cosine) HIPCHK(hipMemsetAsync(norms.as<float>() + cap, 0, sizeof(float) * (nc - cap), st));
+  if (f16) {
+    h16.grow_keep(sizeof(uint16_t) * nc * dim, sizeof(uint16_t) * cap * dim, st);
+    meta.grow_keep(sizeof(float) * nc, sizeof(float) * cap, st);
+    HIPCHK(hipMemsetAsync(static_cast<char *>(h16.p) + sizeof(uint16_t) * cap * dim, 0,
+                          sizeof(uint16_t) * (nc - cap) * dim, st));
+    HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(meta.as<float>() + cap), (int)0xFF800000u, nc - cap,
+                             st));  // -inf: not a row
+    if (!amaxd.p) amaxd.ensure(sizeof(uint32_t));
+  }
   cap = nc;
+}
+
+static float pow2_scale_host(float amax) {  // max |x_i| * sx < 2^14 (filter16.hip pow2_scale)
+  if (!(amax > 0.0f) || !std::isfinite(amax)) return 1.0f;
+  int e;
+  std::frexp(amax, &e);
+  return std::ldexp(1.0f, 14 - e);
+}
+
+void RowStore::encode16(const int64_t *d_slots, int64_t cnt, hipStream_t st) {
+  if (!f16 || cap == 0) return;
+  if (!d_slots) cnt = cap;
+  if (cnt <= 0) return;
+  HIPCHK(hipMemsetAsync(amaxd.p, 0, sizeof(uint32_t), st));
+  launch_absmax(rows.as<float>(), d_slots, cnt, dim, amaxd.as<uint32_t>(), st);
+  uint32_t bits = 0;
+  HIPCHK(hipMemcpyAsync(&bits, amaxd.p, sizeof(bits), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  float am;
+  std::memcpy(&am, &bits, sizeof(am));
+  if (sx == 0.0f || std::max(am, amax) * sx >= 16384.0f) {  // first rows, or a larger row: new scale, all slots
+    amax = std::max(am, amax);
+    sx = pow2_scale_host(amax);
+    launch_encode16(rows.as<float>(), nullptr, cap, dim, sx, h16.p, st);
+    launch_meta16(nullptr, cap, met16, rsq.as<float>(), live.as<uint8_t>(), meta.as<float>(), st);
+  } else {
+    amax = std::max(am, amax);
+    launch_encode16(rows.as<float>(), d_slots, cnt, dim, sx, h16.p, st);
+    launch_meta16(d_slots, cnt, met16, rsq.as<float>(), live.as<uint8_t>(), meta.as<float>(), st);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(st));
 }
 
 void RowStore::write(const float *x, const int64_t *slots, const int64_t *labs, int64_t cnt, hipStream_t st,
@@ -81,6 +124,7 @@ void RowStore::write(const float *x, const int64_t *slots, const int64_t *labs, 
   if (cosine) launch_norms_slots(rows.as<float>(), di, cnt, dim, norms.as<float>(), st);
   launch_sqnorms(rows.as<float>(), di, cnt, dim, rsq.as<float>(), rmax.as<uint32_t>(), st);
   HIPCHK(hipGetLastError());
+  encode16(di, cnt, st);
   HIPCHK(hipStreamSynchronize(st));  // staging buffers are reused by the next call
   if (stage_x.n > (size_t(256) << 20)) stage_x.release();  // bulk loads: do not pin GBs of staging
 }
@@ -90,6 +134,8 @@ void RowStore::set_live(const std::vector<int64_t> &slots, uint8_t v, hipStream_
   stage.ensure(sizeof(int64_t) * slots.size());
   HIPCHK(hipMemcpyAsync(stage.p, slots.data(), sizeof(int64_t) * slots.size(), hipMemcpyHostToDevice, st));
   launch_scatter_u8(live.as<uint8_t>(), stage.as<int64_t>(), v, (int64_t)slots.size(), st);
+  if (f16) launch_meta16(stage.as<int64_t>(), (int64_t)slots.size(), met16, meta_norms(), live.as<uint8_t>(),
+                         meta.as<float>(), st);
   HIPCHK(hipStreamSynchronize(st));
   for (int64_t s : slots) hlive[s] = v;
 }
@@ -235,8 +281,8 @@ static ScanPlan plan_flat(int64_t nrows, int64_t nq, int dim, int k, int max_par
   int64_t want = std::max<int64_t>(1, 2048 / nqc);
   want = std::min<int64_t>(want, std::max<int64_t>(1, nrows / 1024));
   want = std::min<int64_t>(want, max_parts);
-  p.chunk_rows = (int)round_up((nrows + want - 1) / want, 8);
-  if (p.chunk_rows <= 0) p.chunk_rows = 8;
+  p.chunk_rows = (int)round_up((nrows + want - 1) / want, 32);  // whole fp16 tiles (filter16.hip)
+  if (p.chunk_rows <= 0) p.chunk_rows = 32;
   p.nchunks = (int)((nrows + p.chunk_rows - 1) / p.chunk_rows);
   p.nitems = (int)(p.nchunks * nqc);
   return p;
@@ -308,8 +354,13 @@ static int filter_pub_mask() {  // FilterArgs::pub_mask; PYR_FILTER_PUB override
 // approximate-score arithmetic of the filter: bf16x3 (default) or fp32 (PYR_FILTER_PREC=0)
 static int filter_prec() {
   const char *e = getenv("PYR_FILTER_PREC");
-  return (e && atoi(e) == 0) ? FILTER_FP32 : FILTER_BF16X3;
+  if (!e) return FILTER_F16X2;
+  const int v = atoi(e);
+  return (v >= FILTER_FP32 && v <= FILTER_F16X1) ? v : FILTER_F16X2;
 }
+static bool prec16(int prec) { return prec == FILTER_F16X2 || prec == FILTER_F16X1; }
+// the fp16 tile copy is kept for stores the fp16 filter can scan
+static bool store16(int dim, int metric) { return filter16_supported(dim, metric, 16); }
 // waves per filter block for IVF items (FilterArgs::waves): 4 = 128-query items (default);
 // PYR_FILTER_WAVES=8 -> 256-query items, one block per CU (bf16x3 only): half the row
 // traffic but measured slower, 4.98 -> 7.42 ms at the bench config (profiles/r1_sweeps/sweep23).
@@ -337,6 +388,12 @@ static int filter_k1(int k) {
     if (k + m <= c) return c;
   return 0;
 }
+// K1 of the filter re-run of certificate failures: 64 when that widens the margin, else 0 (exact)
+static int filter_k1_next(int k, int k1) {
+  const char *e = getenv("PYR_FILTER_TIER");
+  if (e && atoi(e) == 0) return 0;
+  return (k1 < 64 && k + 4 <= 64) ? 64 : 0;
+}
 // error-bound constant of the refine certificate (filter.hip refine_kernel); PYR_FILTER_CERR
 // overrides it for tests (a huge value fails every certificate -> every query re-runs exactly)
 static double filter_cerr(int dim) {
@@ -348,7 +405,8 @@ static double filter_cerr(int dim) {
 // queries whose certificate failed (listed in ws.fail).  Synchronizes ws.st.
 static int64_t filter_finish(Workspace &ws, int64_t nq, int nparts, int k1, int k, int dim, int met, int V,
                              const float *d_q, const RowStore &rs, const MergeIvf *mi, float *d_s, int64_t *d_l,
-                             int32_t *d_c, const uint32_t *list_rmax = nullptr) {
+                             int32_t *d_c, const uint32_t *list_rmax = nullptr, const float *resid_cents = nullptr,
+                             const uint32_t *list_rmax_r = nullptr) {
   ws.ms.ensure(sizeof(float) * nq * k1);
   ws.mk.ensure(sizeof(int32_t) * nq * k1);
   {
@@ -381,7 +439,22 @@ static int64_t filter_finish(Workspace &ws, int64_t nq, int nparts, int k1, int 
   r.k = k;
   r.dim = dim;
   r.c_err = filter_cerr(dim);
-  r.c_bf = filter_prec() == FILTER_BF16X3 ? filter_bf16x3_cerr(dim, met) : 0.0;
+  const int prec = filter_prec();
+  if (prec16(prec) && rs.f16) {
+    r.c_bf = filter_f16_cerr(dim, met, prec);
+    r.c_abs = filter_f16_abs(dim, met, rs.sx, prec);
+    r.q16 = 1;
+    if (resid_cents && mi && list_rmax) {  // residual tiles: the certificate of filter.hip refine_kernel
+      r.resid = 1;
+      r.cents = resid_cents;
+      r.list_rmax_r = list_rmax_r;
+      r.list_rmax = list_rmax;
+      r.probes = mi->probes;
+      r.nprobe = mi->nprobe;
+    }
+  } else {
+    r.c_bf = prec == FILTER_BF16X3 ? filter_bf16x3_cerr(dim, met) : 0.0;
+  }
   r.out_s = d_s;
   r.out_l = d_l;
   r.out_c = d_c;
@@ -576,6 +649,8 @@ struct FlatIndex : Index {
   explicit FlatIndex(const pyr_index_desc &d) : Index(d) {
     st.dim = dim;
     st.cosine = metric == COS;  // norm cached at Add (:146)
+    st.f16 = store16(dim, metric);
+    st.met16 = metric;
     dp = sq8_dp(dim);
   }
 
@@ -758,14 +833,21 @@ struct FlatIndex : Index {
     fa.prec = filter_prec();
     fa.waves = 4;  // items of QCHUNK = 128 queries (plan_flat)
     fa.xcd = getenv("PYR_FLAT_XCD") ? atoi(getenv("PYR_FLAT_XCD")) != 0 : 0;  // measurement knob
+    fa.h16 = st.h16.p;
+    fa.meta = st.meta.as<float>();
+    fa.sx = st.sx;
     {
       PhaseTimer t(PH_FLAT_SCAN, ws.st, nq * cutoff);
-      launch_filter(fa, metric, p.nitems, ws.st);
+      if (prec16(fa.prec) && st.f16) launch_filter16(fa, metric, p.nitems, ws.st);
+      else launch_filter(fa, metric, p.nitems, ws.st);
     }
     const int64_t nf = filter_finish(ws, nq, p.nchunks, k1, k, dim, metric, 4, d_q, st, nullptr, d_s, d_l, d_c);
+    const int k1_next = filter_k1_next(k, k1);
     filter_fallback(ws, nf, d_q, dim, k, d_s, d_l, d_c,
                     [&](const float *q2, int64_t n2, float *s2, int64_t *l2, int32_t *c2) {
-                      search_exact(q2, n2, k, cutoff, s2, l2, c2, ws);
+                      Workspace &sw = ws.nested();  // K1 = 64 filter first, then the exact scan
+                      if (k1_next > 0) search_filter(q2, n2, k, k1_next, cutoff, s2, l2, c2, sw);
+                      else search_exact(q2, n2, k, cutoff, s2, l2, c2, sw);
                     });
   }
 
@@ -1062,11 +1144,14 @@ static IvfChunking ivf_chunking(int64_t max_len, int probes, int other_parts, in
   // 5120 rows: 2048 -> 4096 -> 5120 gave 5.71 -> 5.27 -> ~5.2 ms at the bench config
   // (profiles/r1_sweeps/sweep21, sweep28, sweep29); warm-up launch measured neutral (profiles/)
   int64_t chunk = 5120, warm = 0;
+  // a small batch (e.g. the re-run of certificate failures) has few (list, query group) items:
+  // shorter chunks give it more of the chip
+  if (nq * probes < 8192) chunk = 1024;
   if (const char *e = getenv("PYR_IVF_CHUNK")) chunk = std::max<int64_t>(8, atoll(e));
   if (const char *e = getenv("PYR_IVF_WARM")) warm = std::max<int64_t>(0, atoll(e));
   if (!bounds) warm = 0;  // the warm-up launch only pays with shared bounds
-  chunk = round_up(chunk, 8);
-  warm = round_up(warm, 8);
+  chunk = round_up(chunk, 32);  // whole fp16 tiles (lists start on a 32-row boundary)
+  warm = round_up(warm, 32);
   auto chunks = [&](int64_t c) {
     return (int64_t)ivf_list_chunks((int)max_len, IvfChunking{(int32_t)c, 1, (int32_t)warm});
   };
@@ -1078,7 +1163,7 @@ static IvfChunking ivf_chunking(int64_t max_len, int probes, int other_parts, in
   if (cmax > budget) {
     if (budget < 2) warm = 0;
     const int64_t room = std::max<int64_t>(1, budget - (warm > 0 ? 1 : 0));
-    chunk = round_up(std::max<int64_t>(8, (max_len - warm + room - 1) / room), 8);
+    chunk = round_up(std::max<int64_t>(32, (max_len - warm + room - 1) / room), 32);
     cmax = chunks(chunk);
   }
   return IvfChunking{(int32_t)chunk, (int32_t)cmax, (int32_t)warm};
@@ -1096,6 +1181,7 @@ struct IvfFlatIndex : Index {
   int64_t max_len = 0;                    // longest list (rows incl. tombstones): row chunking
   DevMem dlb, dle, dllive;
   DevMem dlmax;                           // per-list max |x|^2 (score_key): refine certificate bound
+  DevMem dlmax_r;                         // per-list max |x - c|^2 (residual fp16 tiles)
   Coarse coarse;
   bool built = false;                     // _isBuilt (:20)
   int nprobe_default;
@@ -1236,7 +1322,7 @@ struct IvfFlatIndex : Index {
     for (int l = 0; l < k; l++) {
       lb[l] = (int32_t)tot;
       le[l] = (int32_t)(tot + cnt[l]);
-      tot += round_up(cnt[l], 8);
+      tot += round_up(cnt[l], 32);  // lists start on a 32-row tile boundary
       max_len = std::max<int64_t>(max_len, cnt[l]);
     }
     if (tot >= (int64_t)KEY_BUF) throw Error(PYR_E_ARG, "IVF index larger than 2^31 rows");
@@ -1251,7 +1337,9 @@ struct IvfFlatIndex : Index {
     RowStore nl;
     nl.dim = dim;
     nl.cosine = metric == COS;
-    nl.reserve(std::max<int64_t>(tot, 8), wst);
+    nl.f16 = store16(dim, metric);
+    nl.met16 = metric;
+    nl.reserve(std::max<int64_t>(tot, 32), wst);
     DevMem dsr;
     dsr.ensure(sizeof(int64_t) * tot);
     HIPCHK(hipMemcpyAsync(dsr.p, srcrow.data(), sizeof(int64_t) * tot, hipMemcpyHostToDevice, wst));
@@ -1263,6 +1351,29 @@ struct IvfFlatIndex : Index {
     if (nl.cosine) launch_norms(nl.rows.as<float>(), tot, dim, 1, nl.norms.as<float>(), wst);
     launch_sqnorms(nl.rows.as<float>(), nullptr, tot, dim, nl.rsq.as<float>(), nl.rmax.as<uint32_t>(), wst);
     HIPCHK(hipGetLastError());
+    DevMem dtl;
+    if (nl.f16) {
+      // the fp16 tiles hold residuals x - c[list] (filter16.hip residual mode): lists start on a
+      // 32-row boundary, so every tile belongs to one list
+      std::vector<int32_t> tl((size_t)(nl.cap / 32), 0);
+      for (int l = 0; l < k; l++)
+        for (int64_t t = lb[l] / 32; t < (lb[l] + round_up(cnt[l], 32)) / 32; t++) tl[t] = l;
+      dtl.ensure(sizeof(int32_t) * tl.size());
+      HIPCHK(hipMemcpyAsync(dtl.p, tl.data(), sizeof(int32_t) * tl.size(), hipMemcpyHostToDevice, wst));
+      nl.resid = true;
+      nl.rsq16.ensure(sizeof(float) * nl.cap);
+      launch_resid_sq(nl.rows.as<float>(), nl.cap, dim, C, dtl.as<int32_t>(), nl.rsq16.as<float>(), wst);
+      HIPCHK(hipMemsetAsync(nl.amaxd.p, 0, sizeof(uint32_t), wst));
+      launch_absmax(nl.rows.as<float>(), nullptr, nl.cap, dim, nl.amaxd.as<uint32_t>(), wst, C, dtl.as<int32_t>());
+      uint32_t bits = 0;
+      HIPCHK(hipMemcpyAsync(&bits, nl.amaxd.p, sizeof(bits), hipMemcpyDeviceToHost, wst));
+      HIPCHK(hipStreamSynchronize(wst));
+      std::memcpy(&nl.amax, &bits, sizeof(bits));
+      nl.sx = pow2_scale_host(nl.amax);
+      launch_encode16(nl.rows.as<float>(), nullptr, nl.cap, dim, nl.sx, nl.h16.p, wst, C, dtl.as<int32_t>());
+      launch_meta16(nullptr, nl.cap, metric, nl.rsq16.as<float>(), nl.live.as<uint8_t>(), nl.meta.as<float>(), wst);
+      HIPCHK(hipGetLastError());
+    }
     HIPCHK(hipStreamSynchronize(wst));
     nl.n = tot;
     nl.hlabels = newlab;
@@ -1279,6 +1390,19 @@ struct IvfFlatIndex : Index {
     std::swap(lists.rsq.n, nl.rsq.n);
     std::swap(lists.rmax.p, nl.rmax.p);
     std::swap(lists.rmax.n, nl.rmax.n);
+    std::swap(lists.h16.p, nl.h16.p);
+    std::swap(lists.h16.n, nl.h16.n);
+    std::swap(lists.meta.p, nl.meta.p);
+    std::swap(lists.meta.n, nl.meta.n);
+    std::swap(lists.amaxd.p, nl.amaxd.p);
+    std::swap(lists.amaxd.n, nl.amaxd.n);
+    std::swap(lists.rsq16.p, nl.rsq16.p);
+    std::swap(lists.rsq16.n, nl.rsq16.n);
+    lists.f16 = nl.f16;
+    lists.met16 = nl.met16;
+    lists.sx = nl.sx;
+    lists.amax = nl.amax;
+    lists.resid = nl.resid;
     lists.n = tot;
     lists.cap = nl.cap;
     lists.hlabels.swap(nl.hlabels);
@@ -1291,6 +1415,10 @@ struct IvfFlatIndex : Index {
     upload_list_meta();
     dlmax.ensure(sizeof(uint32_t) * k);
     launch_list_rmax(lists.rsq.as<float>(), dlb.as<int32_t>(), dle.as<int32_t>(), k, dlmax.as<uint32_t>(), wst);
+    if (lists.resid) {
+      dlmax_r.ensure(sizeof(uint32_t) * k);
+      launch_list_rmax(lists.rsq16.as<float>(), dlb.as<int32_t>(), dle.as<int32_t>(), k, dlmax_r.as<uint32_t>(), wst);
+    }
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(wst));
   }
@@ -1363,6 +1491,11 @@ struct IvfFlatIndex : Index {
     fa.waves = waves;
     fa.xcd = filter_xcd();
     fa.single = getenv("PYR_FILTER_SB") ? atoi(getenv("PYR_FILTER_SB")) != 0 : 0;
+    fa.h16 = lists.h16.p;
+    fa.meta = lists.meta.as<float>();
+    fa.sx = lists.sx;
+    fa.cents = lists.resid ? coarse.rm.as<float>() : nullptr;
+    const bool use16 = prec16(fa.prec) && lists.f16;
     DevMem dbg;
     if (getenv("PYR_FILTER_DEBUG")) {  // measurement only: insert statistics to stderr
       dbg.ensure(16);
@@ -1371,19 +1504,23 @@ struct IvfFlatIndex : Index {
     }
     {
       PhaseTimer t(PH_LIST_SCAN, ws.st, prof().on ? probed_rows(ws, nq, probes, le, lb) : 0);
-      launch_filter(fa, metric, maxi, ws.st);
+      if (use16) launch_filter16(fa, metric, maxi, ws.st);
+      else launch_filter(fa, metric, maxi, ws.st);
       if (seed || ch.warm > 0) {
         fa.items = ws.items3.as<ScanItem>();
         fa.n_items = ws.nitems3.as<int32_t>();
         if (seed) fa.qlist = ws.qlist2.as<int32_t>();
-        launch_filter(fa, metric, maxi_main, ws.st);
+        if (use16) launch_filter16(fa, metric, maxi_main, ws.st);
+        else launch_filter(fa, metric, maxi_main, ws.st);
       }
     }
     if (fa.dbg) {
       uint32_t h[4] = {0, 0, 0, 0};
-      HIPCHK(hipMemcpyAsync(h, dbg.p, 12, hipMemcpyDeviceToHost, ws.st));
+      HIPCHK(hipMemcpyAsync(h, dbg.p, 16, hipMemcpyDeviceToHost, ws.st));
       HIPCHK(hipStreamSynchronize(ws.st));
-      fprintf(stderr, "[filter] wave insert-loop iterations %u, candidates %u, owner stages %u\n", h[0], h[1], h[2]);
+      fprintf(stderr, "[filter] %s %u, candidates %u, %s %u\n", use16 ? "survivor wave-tiles" : "wave insert-loop iterations",
+              h[0], h[1], use16 ? "owner drains" : "owner stages", h[2]);
+      if (use16) fprintf(stderr, "[filter] shared-bound refreshes that raised a threshold %u\n", h[3]);
     }
     MergeIvf mi;
     mi.probes = ws.probes.as<int32_t>();
@@ -1391,31 +1528,34 @@ struct IvfFlatIndex : Index {
     mi.le = dle.as<int32_t>();
     mi.nprobe = probes;
     mi.ch = ch;
-    const int64_t nf =
-        filter_finish(ws, nq, nparts, k1, k, dim, metric, 1, d_q, lists, &mi, d_s, d_l, d_c, dlmax.as<uint32_t>());
+    const int64_t nf = filter_finish(ws, nq, nparts, k1, k, dim, metric, 1, d_q, lists, &mi, d_s, d_l, d_c,
+                                     dlmax.as<uint32_t>(), use16 && lists.resid ? coarse.rm.as<float>() : nullptr,
+                                     dlmax_r.as<uint32_t>());
     // The exact re-run scans the failing queries' OWN probe lists: ws.probes holds the batch's
     // ranking (computed above or handed in by the caller, pyr_index_search_probed_device), so its
     // rows are gathered in fail-list order and passed as caller-ranked lists.  (Re-ranking is
     // only equivalent when this index ranked them itself; caller lists may differ.)
+    // Failures are re-run on their own buffers (ws.nested()): first by the filter with K1 = 64
+    // candidates (a 64-deep margin certifies almost every query the K1 = 16 list could not), what
+    // still fails by the exact scan.  PYR_FILTER_TIER=0 sends failures straight to the exact scan.
     pyr_search_params ex{probes, 0, -1};
+    const int k1_next = filter_k1_next(k, k1);
     filter_fallback(ws, nf, d_q, dim, k, d_s, d_l, d_c,
                     [&](const float *q2, int64_t n2, float *s2, int64_t *l2, int32_t *c2) {
-                      ws.fprobes.ensure(sizeof(int32_t) * n2 * probes);
+                      Workspace &sw = ws.nested();
+                      sw.fprobes.ensure(sizeof(int32_t) * n2 * probes);
                       launch_gather_rows_i32(ws.probes.as<int32_t>(), ws.fail.as<int32_t>(), n2, probes,
-                                             ws.fprobes.as<int32_t>(), ws.st);
-                      const int32_t *ext = ws.ext_probes;
-                      const int32_t ext_n = ws.ext_nprobe;
-                      ws.ext_probes = ws.fprobes.as<int32_t>();
-                      ws.ext_nprobe = probes;
+                                             sw.fprobes.as<int32_t>(), ws.st);
+                      sw.ext_probes = sw.fprobes.as<int32_t>();
+                      sw.ext_nprobe = probes;
                       try {
-                        search_exact(q2, n2, k, ex, s2, l2, c2, ws);
+                        if (k1_next > 0) search_filter(q2, n2, k, k1_next, probes, s2, l2, c2, sw);
+                        else search_exact(q2, n2, k, ex, s2, l2, c2, sw);
                       } catch (...) {
-                        ws.ext_probes = ext;
-                        ws.ext_nprobe = ext_n;
+                        sw.ext_probes = nullptr;
                         throw;
                       }
-                      ws.ext_probes = ext;
-                      ws.ext_nprobe = ext_n;
+                      sw.ext_probes = nullptr;
                     });
   }
 

@@ -65,6 +65,18 @@ struct RowStore {
   DevMem rows, norms, live, labels;
   DevMem rsq;       // per slot |x|^2 (MFMA filter, filter.hip)
   DevMem rmax;      // score_key of the largest |x|^2 ever stored (device scalar, only grows)
+  // fp16 tile copy for the fp16 filter (filter16.hip): h16 tiles of 32 slots, per-slot meta
+  // (L2 -|x|^2 / IP 0 / -inf when not live), the power-of-two scale sx with the largest |x_i|
+  // ever stored (amax) below 2^14.  Kept only when f16 is set (FLAT slots, IVF lists).
+  bool f16 = false;
+  int met16 = 0;
+  float sx = 0.0f;
+  float amax = 0.0f;
+  DevMem h16, meta, amaxd;
+  // IVF lists: the tiles hold residuals x - c[list] (resid), with rsq16 = |x - c|^2 per row for meta
+  bool resid = false;
+  DevMem rsq16;
+  const float *meta_norms() const { return resid ? rsq16.as<float>() : rsq.as<float>(); }
   std::vector<int64_t> hlabels;
   std::vector<uint8_t> hlive;
   void reserve(int64_t slots, hipStream_t st);
@@ -72,6 +84,9 @@ struct RowStore {
   void write(const float *x, const int64_t *slots, const int64_t *labs, int64_t cnt, hipStream_t st,
              DevMem &stage_x, DevMem &stage_i);
   void set_live(const std::vector<int64_t> &slots, uint8_t v, hipStream_t st, DevMem &stage);
+  // fp16 copy of slots (device list, or [0, cap) when null) with the current scale; raises the
+  // scale (and re-encodes every slot) when a row exceeds it.  Synchronizes st.
+  void encode16(const int64_t *d_slots, int64_t cnt, hipStream_t st);
   void clear() {
     n = 0;
     hlabels.clear();
@@ -93,6 +108,15 @@ struct Workspace {
   DevMem q8q, q8qs;                               // 8-bit search mode: quantized queries, their sums
   const int32_t *ext_probes = nullptr;            // caller-ranked probe lists [nq][ext_nprobe] (multi-GPU)
   int32_t ext_nprobe = 0;
+  // the re-run of certificate failures searches with its own buffers on the same stream
+  std::unique_ptr<Workspace> sub;
+  Workspace &nested() {
+    if (!sub) {
+      sub = std::make_unique<Workspace>();
+      sub->st = st;
+    }
+    return *sub;
+  }
   ~Workspace() {
     if (own_stream && st) (void)hipStreamDestroy(st);
   }

@@ -518,6 +518,12 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) part += __shfl_xor(part, off);
   const float qsq = part;
+  float qa = 0.0f;  // max |q_i|: the fp16 filter's query scale (filter16.hip pow2_scale)
+  if (a.q16) {
+    for (int d = lane; d < D; d += 64) qa = fmaxf(qa, fabsf(qp[d]));
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) qa = fmaxf(qa, __shfl_xor(qa, off));
+  }
 
   const float *ms = a.ms + (size_t)q * k1;
   const int32_t *mk = a.mk + (size_t)q * k1;
@@ -555,6 +561,64 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
     }
     const double u = 5.9604644775390625e-8;  // 2^-24
     const double qn = sqrt((double)qsq) * (1.0 + 1e-5);
+    if (a.resid) {
+      // IVF fp16 filter over residual tiles (filter16.hip): approx estimates the score itself,
+      //   L2: -|q - x|^2 = 2 (q-c).(x-c) - |x-c|^2 - |q-c|^2,  IP: q.x = q.(x-c) + q.c,
+      // so its error is relative to the residuals: fp16 rows c_bf u Ar Xr (Ar = |q - c| for L2,
+      // |q| for IP; Xr = max |x - c|), fp32 sums / adds (D + 8) u (Ar + Xr)^2, subnormal halves
+      // (c_abs Ar, and the query's, below 2^-36 sqrt(D) Ar Xr), IP's q.c constant (D + 8) u |q||c|.
+      // The reference's own sum: L2 adds non-negative terms, so R = T (1 +- g), g = (D/8 + 8) u;
+      // IP |R - T| <= g |q| max|x|.  Maxima over this query's probed lists.
+      float ar2 = 0.0f, xc2 = 0.0f;
+      uint32_t xrk = 0, xfk = 0;
+      for (int p = lane; p < a.nprobe; p += 64) {
+        const int l = a.probes[(size_t)q * a.nprobe + p];
+        xrk = max(xrk, a.list_rmax_r[l]);
+        xfk = max(xfk, a.list_rmax[l]);
+        const float *c = a.cents + (size_t)l * D;
+        float d2 = 0.0f, c2 = 0.0f;
+        for (int d = 0; d < D; ++d) {
+          const float t = qp[d] - c[d];
+          d2 += t * t;
+          c2 += c[d] * c[d];
+        }
+        ar2 = fmaxf(ar2, d2);
+        xc2 = fmaxf(xc2, c2);
+      }
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) {
+        ar2 = fmaxf(ar2, __shfl_xor(ar2, off));
+        xc2 = fmaxf(xc2, __shfl_xor(xc2, off));
+        xrk = max(xrk, (uint32_t)__shfl_xor((int)xrk, off));
+        xfk = max(xfk, (uint32_t)__shfl_xor((int)xfk, off));
+      }
+      const double Ar = MET == L2 ? sqrt((double)ar2) * (1.0 + 1e-5) + 1e-30 : qn;
+      double Xr = sqrt((double)key_score(xrk)) * (1.0 + 1e-5);
+      const double g = (D / 8.0 + 8.0) * u;
+      if (MET == L2 && a.tri) {
+        // triangle bound on the residuals (the classic branch below, with q - x = (q-c) - (x-c)):
+        // a row with |x - c| >= |q - c| + r, r^2 = -skth (1 + 2 c_err u), scores below skth whatever
+        // the filter saw, so only rows with |x - c| < Ar + r need the error bound
+        const double r = sqrt(fmax(0.0, -(double)skth) * (1.0 + 2.0 * a.c_err * u) + 1e-30) * (1.0 + 1e-6);
+        Xr = fmin(Xr, Ar + r);
+      }
+      // (c_err = 4D + 64 >= D + 8 budgets the fp32 sums; PYR_FILTER_CERR raises it in tests)
+      double e = a.c_bf * u * Ar * Xr + a.c_err * u * (MET == L2 ? (Ar + Xr) * (Ar + Xr) : Ar * Xr) +
+                 a.c_abs * Ar + (MET == L2 ? 2.0 : 1.0) * 1.4551915228366852e-11 * sqrt((double)D) * Ar * Xr;
+      const double ak = (double)ms[k1 - 1];
+      if (MET == L2) {
+        ok = nout == k && (double)skth > (ak + e) + g * fabs(ak + e);
+      } else {
+        e += a.c_err * u * qn * sqrt((double)xc2) * (1.0 + 1e-5) +
+             g * qn * sqrt((double)key_score(xfk)) * (1.0 + 1e-5);
+        ok = nout == k && (double)skth > ak + e;
+      }
+      if (lane == 0) {
+        if (a.out_c) a.out_c[q] = nout;
+        if (!ok) a.fail_list[atomicAdd(a.fail_cnt, 1)] = (int32_t)q;
+      }
+      return;
+    }
     // X bounds the norm of every row this query's scan could have excluded: the largest |x|^2
     // of its probed lists (IVF), else of the whole store
     uint32_t xk = 0;
@@ -575,8 +639,18 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
       const double r = sqrt(fmax(0.0, -(double)skth) * (1.0 + 2.0 * a.c_err * u) + 1e-30) * (1.0 + 1e-6);
       X = fmin(X, qn + r);
     }
-    const double e = (MET == L2 ? a.c_err * u * (qn + X) * (qn + X) : a.c_err * u * qn * X) +
+    double e = (MET == L2 ? a.c_err * u * (qn + X) * (qn + X) : a.c_err * u * qn * X) +
                      a.c_bf * u * qn * X + (a.c_bf > 0.0 ? 1e-30 * (1.0 + qn + X) * D : 0.0);  // bf16 subnormals
+    if (a.q16) {
+      // fp16 filter: the rows' subnormal halves (c_abs |q|) and the query's, 2^-25 sqrt(D) X / sq
+      double sqs = 1.0;
+      if (qa > 0.0f && isfinite(qa)) {
+        int ex;
+        frexp((double)qa, &ex);
+        sqs = ldexp(1.0, 14 - ex);
+      }
+      e += a.c_abs * qn + (MET == L2 ? 2.0 : 1.0) * 2.9802322387695312e-08 * sqrt((double)D) * X / sqs;
+    }
     const double approx_k1 = MET == L2 ? (double)ms[k1 - 1] - (double)qsq : (double)ms[k1 - 1];
     ok = nout == k && (double)skth > approx_k1 + e;
   }

@@ -1,0 +1,527 @@
+// filter16.hip -- fp16 MFMA candidate filter over pre-encoded row tiles (gfx950).
+//
+// Same contract as filter.hip's mfma_filter (approximate scores -> per (query, slot) top-K1
+// candidates -> merge -> exact refine with a certificate, failures re-run exactly), built for the
+// list scan's two costs: bytes and staging.
+//
+//  * Rows are stored a second time, at write / build time, as fp16 in the exact order the MFMA B
+//    operand wants (h16 tiles: 32 rows x D, [k-step s][lane half h][row i][8 halves], 64*D bytes),
+//    scaled by a power of two sx so the store's largest |x| is below 2^14.  The scan reads 2 B per
+//    dimension instead of 4, and a tile goes HBM -> LDS with global_load_lds (no registers, no
+//    VALU split, conflict-free ds_read_b128 fragments since every 1 KiB piece is lane-linear).
+//  * A per-row additive term (meta: -|x|^2 for L2, 0 for IP, -inf for a dead / padding row) travels
+//    with the tile, so the score is one fma per (query, row): approx = f_q * acc + meta, with
+//    f_q = (L2 ? 2 : 1) / (sq * sx) and sq the query's own power-of-two scale.
+//  * Queries are split into two fp16 terms (qh + ql = q * sq to ~2^-22): q.x ~ qh.xh + ql.xh, two
+//    v_mfma_f32_32x32x16_f16 per 16-deep k-step (PYR_FILTER_PREC=3: qh only, one MFMA).  The error
+//    |q.x - approx/f| <= (2^-11 + 2^-22 + 2D u) sum|q_i x_i| + 2^-25 sum|q_i| / sx (x's fp16
+//    rounding, q's split, fp32 accumulation, fp16 subnormals) is what refine_kernel's c_bf / abs
+//    terms certify against (kernels.h filter_f16_cerr).
+//  * The filter runs in the MFMA C layout: lane (i, h) holds row i's scores for 16 queries; each is
+//    compared with that query's threshold (registers, refreshed from LDS after drains), survivors
+//    are appended to the query's LDS buffer, and the query's owner lane inserts them into its
+//    register top-K1 only when the buffer could overflow on the next tile.  No transpose, no
+//    per-tile owner pass.  Block-level sync is one barrier per tile (the LDS ring).
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+#include <type_traits>
+
+#include "kernels.h"
+
+namespace pyr {
+namespace {
+
+typedef float f16v __attribute__((ext_vector_type(16)));
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void gbl_void;
+
+constexpr int RT16 = 32;        // rows per tile (one 32x32 MFMA tile per wave)
+constexpr int NST = 3;          // LDS ring slots (tiles in flight + the one being read)
+constexpr int CB16 = 48;        // candidate buffer entries per query (>= 32 + drain slack)
+
+__device__ __forceinline__ bool better(float s1, uint32_t k1, float s2, uint32_t k2) {
+  return s1 > s2 || (s1 == s2 && k1 < k2);
+}
+
+template <int KR>
+__device__ __forceinline__ void reg_insert(float (&s)[KR], uint32_t (&kk)[KR], float v, uint32_t key) {
+  bool b[KR];
+#pragma unroll
+  for (int j = 0; j < KR; ++j) b[j] = better(v, key, s[j], kk[j]);
+#pragma unroll
+  for (int j = KR - 1; j >= 1; --j) {
+    s[j] = b[j - 1] ? s[j - 1] : (b[j] ? v : s[j]);
+    kk[j] = b[j - 1] ? kk[j - 1] : (b[j] ? key : kk[j]);
+  }
+  s[0] = b[0] ? v : s[0];
+  kk[0] = b[0] ? key : kk[0];
+}
+
+// LDS: two separate objects, so that the compiler can tell the LDS-DMA target (the ring) from
+// the candidate state -- with one array it waits vmcnt(0) (the whole prefetch) before every
+// candidate append.  Ring: NST slots [rows TB][meta: 4 wave copies x 64 floats][dummy 1 KiB when
+// D = 32].  State: thresholds [128], counts [128], candidate scores [128][CB16], keys [128][CB16].
+template <int D>
+struct F16Lds {
+  static constexpr int TB = RT16 * D * 2;               // h16 bytes per tile
+  static constexpr int NCH = TB / 1024;                 // 1 KiB glds pieces per tile
+  static constexpr int NR = NCH >= 4 ? NCH / 4 : 1;     // row pieces per wave per tile
+  static constexpr int META = TB;                       // offset of the meta copies in a slot
+  static constexpr int DUMMY = TB + 1024;               // landing zone of the D = 32 filler pieces
+  static constexpr int SLOT = TB + 1024 + (NCH < 4 ? 1024 : 0);
+  static constexpr int LPT = NR + 1;                    // glds per wave per tile (rows + meta)
+  static constexpr int RING = NST * SLOT;
+  static_assert(NCH <= 4 ? true : NCH % 4 == 0, "row pieces must split evenly over 4 waves");
+};
+struct F16State {
+  float thr[128];
+  int cnt[128];
+  float cs[128 * CB16];
+  uint32_t ck[128 * CB16];
+};
+
+// LDS-DMA of SIZE (16 or 4) bytes per lane: global g (per lane) -> LDS lds + lane * SIZE (lds
+// wave-uniform, in M0).  Written in inline asm on purpose: the compiler does not track these
+// writes, so it does not drain every in-flight tile (vmcnt(0)) before each LDS access it cannot
+// prove disjoint; the kernel's own counted vmcnt waits + barrier order the ring instead.
+template <int SIZE>
+__device__ __forceinline__ void glds(const void *g, uint32_t lds_addr) {
+  int keep;
+  const uint32_t lds = __builtin_amdgcn_readfirstlane(lds_addr);  // wave-uniform: an SGPR for M0
+  if (SIZE == 16)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(lds)
+                 : "memory");
+  else
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(lds)
+                 : "memory");
+}
+
+// query scale: a power of two putting max |q_i| below 2^14 (1 for a zero query)
+__device__ __forceinline__ float pow2_scale(float amax) {
+  if (!(amax > 0.0f) || !isfinite(amax)) return 1.0f;
+  int e;
+  frexpf(amax, &e);  // amax < 2^e
+  return ldexpf(1.0f, 14 - e);
+}
+
+template <int D, int MET, int KR, bool Q2>
+__global__ __launch_bounds__(256, 2) void mfma_filter16(FilterArgs a) {
+  using L = F16Lds<D>;
+  constexpr int KS = D / 16;
+  __shared__ __attribute__((aligned(16))) char ring[L::RING];
+  __shared__ __attribute__((aligned(16))) F16State state16;
+  const uint32_t ring_base = (uint32_t)(size_t)(lds_void *)ring;  // LDS byte address (M0 of the DMA)
+  float *const thr_l = state16.thr;
+  int *const cnt_l = state16.cnt;
+  float *const cs_l = state16.cs;
+  uint32_t *const ck_l = state16.ck;
+
+  int item = blockIdx.x;
+  if (a.xcd) {  // XCD-major mapping (filter.hip): a list chunk's query groups share an XCD's L2
+    const int per = (*a.n_items + 7) >> 3;
+    item = ((int)blockIdx.x & 7) * per + ((int)blockIdx.x >> 3);
+    if ((int)(blockIdx.x >> 3) >= per) return;
+  }
+  if (item >= *a.n_items) return;
+  const ScanItem it = a.items[item];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int i32 = lane & 31, h = lane >> 5;
+
+  // ---- A operand: query 32w + i32, dims 16s + 8h .. +7 of k-step s, scaled and split ----
+  const int qslot = 32 * w + i32;
+  const int qi = qslot < it.qcnt ? (a.qlist ? a.qlist[it.qbeg + qslot] / a.nparts : it.qbeg + qslot) : -1;
+  float qv[KS][8];
+  float amax = 0.0f;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (qi >= 0) {
+      const float4 *qp = reinterpret_cast<const float4 *>(a.queries + (size_t)qi * D + 16 * s + 8 * h);
+      const float4 v0 = qp[0], v1 = qp[1];
+      qv[s][0] = v0.x; qv[s][1] = v0.y; qv[s][2] = v0.z; qv[s][3] = v0.w;
+      qv[s][4] = v1.x; qv[s][5] = v1.y; qv[s][6] = v1.z; qv[s][7] = v1.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qv[s][j] = 0.0f;
+    }
+  }
+  // IVF residual mode (a.cents): the tiles hold x - c of the item's list c, so the A operand is
+  // q - c (L2) or q (IP), and a per (query, list) constant completes the score:
+  //   L2: -|q - x|^2 = 2 (q-c).(x-c) - |x-c|^2 - |q-c|^2,   IP: q.x = q.(x-c) + q.c
+  float cq = 0.0f;
+  if (a.cents) {
+    const float *c = a.cents + (size_t)it.list * D;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float cv = c[16 * s + 8 * h + j];
+        if (MET == L2) {
+          qv[s][j] = qv[s][j] - cv;
+          cq += qv[s][j] * qv[s][j];
+        } else {
+          cq += qv[s][j] * cv;
+        }
+      }
+    cq += __shfl_xor(cq, 32);
+    if (MET == L2) cq = -cq;
+  }
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(qv[s][j]));
+  amax = fmaxf(amax, __shfl_xor(amax, 32));
+  const float sq = pow2_scale(amax);
+  h8v qh[KS], ql[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = qv[s][j] * sq;  // exact (power of two)
+      qh[s][j] = (_Float16)v;
+      ql[s][j] = (_Float16)(v - (float)qh[s][j]);
+    }
+  // C layout: register r of lane (i32, h) is query (r & 3) + 8 (r >> 2) + 4h of the wave
+  const float myf = (MET == L2 ? 2.0f : 1.0f) / (sq * a.sx);
+  float f[16], cqr[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    f[r] = __shfl(myf, (r & 3) + 8 * (r >> 2) + 4 * h);
+    cqr[r] = __shfl(cq, (r & 3) + 8 * (r >> 2) + 4 * h);
+  }
+
+  // ---- owners (lane i32 < 32 of each wave): query 32w + i32, its top-KR and partial slot ----
+  const bool owner = h == 0 && qslot < it.qcnt;
+  int oslot = 0, qown = 0;
+  float gs = -INFINITY;
+  if (owner) {
+    oslot = a.qlist ? a.qlist[it.qbeg + qslot] + it.part : (it.qbeg + qslot) * a.nparts + it.part;
+    qown = qi;
+    if (a.gthr) gs = key_score(__hip_atomic_load(a.gthr + qown, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  }
+  float ts[KR];
+  uint32_t tk[KR];
+#pragma unroll
+  for (int j = 0; j < KR; ++j) {
+    ts[j] = -INFINITY;
+    tk[j] = KEY_NONE;
+  }
+  uint32_t published = 0;
+  if (h == 0) {
+    // an unused query slot of an active wave scores zero queries: +inf keeps its rows out of the
+    // buffers (with -inf every row would survive for it and force a drain every tile)
+    thr_l[qslot] = qslot < it.qcnt ? gs : INFINITY;
+    cnt_l[qslot] = 0;
+  }
+
+  // ---- tile loads: rows as NR lane-linear 1 KiB pieces per wave, meta as one 128-B piece per wave ----
+  const int r0 = it.row_begin;  // multiple of 32
+  const int nt = (it.row_end - r0 + RT16 - 1) / RT16;
+  const char *hsrc = reinterpret_cast<const char *>(a.h16);
+  // tile t -> ring slot t % NST (LDS-DMA; issued in inline asm, see glds())
+  auto issue = [&](int t) {
+    const size_t tile = (size_t)(r0 / RT16 + t);
+    const uint32_t base = ring_base + (uint32_t)((t % NST) * L::SLOT);
+#pragma unroll
+    for (int p = 0; p < L::NR; ++p) {
+      const int c = L::NCH >= 4 ? w * L::NR + p : (w & (L::NCH - 1));
+      const uint32_t dst = (L::NCH >= 4 || w < L::NCH) ? base + c * 1024 : base + L::DUMMY;
+      glds<16>(hsrc + tile * L::TB + (size_t)c * 1024 + lane * 16, dst);
+    }
+    // meta: the tile's 32 floats, 4 B per lane, into this wave's 256-B copy (lanes 32-63 repeat them)
+    glds<4>(a.meta + tile * RT16 + (lane & 31), base + L::META + w * 256);
+  };
+  __syncthreads();  // thresholds / counts initialised (the first barrier of the loop orders the rest)
+#pragma unroll
+  for (int t = 0; t < NST - 1; ++t)
+    if (t < nt) issue(t);
+
+  float thr[16];
+  auto load_thr = [&]() {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float4 t4 = *reinterpret_cast<const float4 *>(thr_l + 32 * w + 8 * j + 4 * h);
+      thr[4 * j] = t4.x;
+      thr[4 * j + 1] = t4.y;
+      thr[4 * j + 2] = t4.z;
+      thr[4 * j + 3] = t4.w;
+    }
+  };
+  load_thr();
+  const bool wave_active = 32 * w < it.qcnt;
+  int cnt[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) cnt[r] = 0;
+  // register counts -> LDS for the owners (lane 0 of each half writes its 16 queries'); DS ops of
+  // one wave complete in order, so the owners' reads after the wave barrier see them
+  auto publish_counts = [&]() {
+    if (i32 == 0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) cnt_l[32 * w + (r & 3) + 8 * (r >> 2) + 4 * h] = cnt[r];
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
+
+  for (int st = 0; st < nt; ++st) {
+    // tile st has landed for this wave once at most the younger tiles' loads are outstanding
+    // (the compiler does not see the LDS-DMA, so these waits are the only ones ordering it)
+    if (st + 1 < nt)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L::LPT * (NST - 2)) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's pieces of tile st landed; tile st-1 fully read
+    if (a.gthr && (st & a.pub_mask) == a.pub_mask && wave_active) {
+      // every pub_mask + 1 tiles: publish this list's K1-th best and take the query's shared bound
+      // (other items' progress) back.  Done before this iteration's prefetch is issued, so the wait
+      // for the returned value only drains tile st + 1's pieces.
+      if (owner) {
+        const uint32_t mine = tk[KR - 1] != KEY_NONE ? score_key(ts[KR - 1]) : 0u;
+        const uint32_t old = atomicMax(a.gthr + qown, max(mine, published));
+        published = max(mine, published);
+        const float g = key_score(max(old, published));
+        if (g > gs) {
+          gs = g;
+          thr_l[qslot] = fmaxf(thr_l[qslot], gs);
+          if (a.dbg) atomicAdd(a.dbg + 3, 1u);  // measurement only: refreshes that raised the bound
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      load_thr();
+    }
+    if (st + NST - 1 < nt) issue(st + NST - 1);  // into the slot tile st-1 used
+    if (!wave_active) continue;
+    const char *slot = ring + (st % NST) * L::SLOT;
+    f16v acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const h8v xh = *reinterpret_cast<const h8v *>(slot + ((s * 2 + h) * 32 + i32) * 16);
+      if (Q2) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ql[s], xh, acc, 0, 0, 0);  // small term first
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qh[s], xh, acc, 0, 0, 0);
+    }
+    const int row = r0 + st * RT16 + i32;
+    float m = reinterpret_cast<const float *>(slot + L::META + w * 256)[i32];
+    if (row >= it.row_end || (uint32_t)row >= a.row_limit) m = -INFINITY;
+    float sv[16];
+    bool any = false;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      sv[r] = fmaf(f[r], acc[r], m) + cqr[r];
+      any |= sv[r] >= thr[r] && sv[r] > -INFINITY;
+    }
+    if (!__any(any)) continue;
+    // survivors -> the queries' LDS buffers (at most 32 per query per tile: one per row).  The wave
+    // owns its 32 queries' buffers, so the fill counts live in registers (cnt[r]: query q(r, h),
+    // uniform over the half-wave) and a survivor's slot is its rank among the half's survivors.
+    const uint32_t key = a.key_base | (uint32_t)row;
+    if (a.dbg) {  // measurement only: survivors, survivor tiles
+      int ns = 0;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ns += sv[r] >= thr[r] && sv[r] > -INFINITY;
+      atomicAdd(a.dbg + 1, (uint32_t)ns);
+      if (lane == 0) atomicAdd(a.dbg, 1u);
+    }
+    const uint32_t below = (1u << i32) - 1u;
+    int cmax = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const bool s = sv[r] >= thr[r] && sv[r] > -INFINITY;
+      const uint64_t b = __ballot(s);
+      if (b == 0) continue;
+      const uint32_t bh = h ? (uint32_t)(b >> 32) : (uint32_t)b;
+      if (s) {
+        const int q = 32 * w + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int idx = cnt[r] + __builtin_popcount(bh & below);
+        cs_l[q * CB16 + idx] = sv[r];
+        ck_l[q * CB16 + idx] = key;
+      }
+      cnt[r] += __builtin_popcount(bh);
+      cmax = max(cmax, cnt[r]);
+    }
+    // the owners drain every buffer of the wave when one could overflow on the next tile
+    if (!__any(cmax > CB16 - RT16)) continue;
+    publish_counts();
+    int c = 0;
+    if (h == 0) c = cnt_l[qslot];
+    if (owner) {
+      for (int i = 0; i < c; ++i) {
+        const float v = cs_l[qslot * CB16 + i];
+        const uint32_t k2 = ck_l[qslot * CB16 + i];
+        if (better(v, k2, ts[KR - 1], tk[KR - 1])) reg_insert<KR>(ts, tk, v, k2);
+      }
+      if (a.gthr) {
+        // publish this list's K1-th best and take the query's shared bound back (other items'
+        // progress); waiting for the returned value drains this wave's loads once per drain
+        const uint32_t mine = tk[KR - 1] != KEY_NONE ? score_key(ts[KR - 1]) : 0u;
+        const uint32_t old = atomicMax(a.gthr + qown, max(mine, published));
+        published = max(mine, published);
+        gs = fmaxf(gs, key_score(max(old, published)));
+      }
+      float t = gs;
+      if (tk[KR - 1] != KEY_NONE) t = fmaxf(t, ts[KR - 1]);
+      if (a.dbg) atomicAdd(a.dbg + 2, 1u);  // measurement only: drains
+      thr_l[qslot] = t;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) cnt[r] = 0;
+    __builtin_amdgcn_wave_barrier();
+    load_thr();
+  }
+  publish_counts();
+  if (owner) {
+    const int c = cnt_l[qslot];
+    for (int i = 0; i < c; ++i) {
+      const float v = cs_l[qslot * CB16 + i];
+      const uint32_t k2 = ck_l[qslot * CB16 + i];
+      if (better(v, k2, ts[KR - 1], tk[KR - 1])) reg_insert<KR>(ts, tk, v, k2);
+    }
+    if (a.gthr && tk[KR - 1] != KEY_NONE && score_key(ts[KR - 1]) > published)
+      atomicMax(a.gthr + qown, score_key(ts[KR - 1]));
+    float *ps = a.part_s + (size_t)oslot * KR;
+    uint32_t *pk = a.part_k + (size_t)oslot * KR;
+#pragma unroll
+    for (int j = 0; j < KR; ++j) {
+      ps[j] = ts[j];
+      pk[j] = tk[j];
+    }
+  }
+}
+
+inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
+
+template <int D, int MET, int KR, bool Q2>
+void launch16_p(const FilterArgs &a, int max_items, hipStream_t st) {
+  // all LDS is static (77 KiB at D = 128): no dynamic-LDS attribute (a 160 KiB dynamic limit on top
+  // of the static size makes the launch invalid)
+  const int grid = a.xcd ? (max_items + 7) / 8 * 8 : max_items;
+  hipLaunchKernelGGL((mfma_filter16<D, MET, KR, Q2>), dim3(grid), dim3(256), 0, st, a);
+}
+
+template <int D, int MET>
+void launch16_k(const FilterArgs &a, int max_items, hipStream_t st) {
+  const bool q2 = a.prec != FILTER_F16X1;
+  if (a.k1 == 16) q2 ? launch16_p<D, MET, 16, true>(a, max_items, st) : launch16_p<D, MET, 16, false>(a, max_items, st);
+  else if (a.k1 == 32) q2 ? launch16_p<D, MET, 32, true>(a, max_items, st) : launch16_p<D, MET, 32, false>(a, max_items, st);
+  else q2 ? launch16_p<D, MET, 64, true>(a, max_items, st) : launch16_p<D, MET, 64, false>(a, max_items, st);
+}
+
+template <int D>
+void launch16_d(const FilterArgs &a, int metric, int max_items, hipStream_t st) {
+  if (metric == L2) launch16_k<D, L2>(a, max_items, st);
+  else launch16_k<D, IP>(a, max_items, st);
+}
+
+// ---- write / build side: fp16 tiles, per-row meta, the store's |x| maximum ----
+
+// h16 tile element of (row r, dim d): tile r/32, k-step d/16, half (d/8)&1, row r%32, d%8
+// residual mode: cents (row-major) and tile_list (list id of each 32-row tile) -> x - c[list]
+__device__ __forceinline__ float resid_val(const float *rows, const float *cents, const int32_t *tile_list, int64_t r,
+                                           int d, int D) {
+  const float x = rows[((size_t)(r >> 3) * D + d) * 8 + (r & 7)];
+  return cents ? x - cents[(size_t)tile_list[r >> 5] * D + d] : x;
+}
+
+__global__ void encode16_kernel(const float *rows, const int64_t *slots, int64_t n, int D, float sx,
+                                const float *cents, const int32_t *tile_list, _Float16 *h16) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (row, 8-dim group)
+  const int G = D / 8;
+  if (e >= n * G) return;
+  const int64_t i = e / G;
+  const int g = (int)(e % G);
+  const int64_t r = slots ? slots[i] : i;
+  h8v v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (_Float16)(resid_val(rows, cents, tile_list, r, 8 * g + j, D) * sx);
+  const size_t off = (((size_t)(r >> 5) * (D / 16) + (g >> 1)) * 2 + (g & 1)) * 32 + (r & 31);
+  *reinterpret_cast<h8v *>(h16 + off * 8) = v;
+}
+
+// meta[r] = live ? (L2 ? -|x|^2 : 0) : -inf
+__global__ void meta16_kernel(const int64_t *slots, int64_t n, int met, const float *rsq, const uint8_t *live,
+                              float *meta) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t r = slots ? slots[i] : i;
+  meta[r] = live[r] ? (met == L2 ? -rsq[r] : 0.0f) : -INFINITY;
+}
+
+// max |x_i| over the given rows (finite values; non-negative floats order as their bits)
+__global__ void absmax_kernel(const float *rows, const int64_t *slots, int64_t n, int D, const float *cents,
+                              const int32_t *tile_list, uint32_t *out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t r = slots ? slots[i] : i;
+  float m = 0.0f;
+  for (int d = 0; d < D; ++d) {
+    const float v = fabsf(resid_val(rows, cents, tile_list, r, d, D));
+    if (isfinite(v)) m = fmaxf(m, v);
+  }
+  atomicMax(out, __float_as_uint(m));
+}
+
+// |x - c[list]|^2 per row (fp32, any order: the certificate budgets its rounding)
+__global__ void resid_sq_kernel(const float *rows, int64_t n, int D, const float *cents, const int32_t *tile_list,
+                                float *out) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  float s = 0.0f;
+  for (int d = 0; d < D; ++d) {
+    const float v = resid_val(rows, cents, tile_list, r, d, D);
+    s += v * v;
+  }
+  out[r] = s;
+}
+
+}  // namespace
+
+bool filter16_supported(int dim, int metric, int k1) {
+  if (metric != L2 && metric != IP) return false;
+  if (dim != 32 && dim != 64 && dim != 128) return false;
+  return k1 == 16 || k1 == 32 || k1 == 64;
+}
+
+void launch_filter16(const FilterArgs &a, int metric, int max_items, hipStream_t st) {
+  if (max_items <= 0) return;
+  switch (a.dim) {
+    case 32: launch16_d<32>(a, metric, max_items, st); return;
+    case 64: launch16_d<64>(a, metric, max_items, st); return;
+    default: launch16_d<128>(a, metric, max_items, st); return;
+  }
+}
+
+void launch_encode16(const float *rows, const int64_t *slots, int64_t n, int32_t dim, float sx, void *h16,
+                     hipStream_t st, const float *cents, const int32_t *tile_list) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(encode16_kernel, dim3(nblk(n * (dim / 8), 256)), dim3(256), 0, st, rows, slots, n, dim, sx, cents,
+                     tile_list, reinterpret_cast<_Float16 *>(h16));
+}
+
+void launch_resid_sq(const float *rows, int64_t n, int32_t dim, const float *cents, const int32_t *tile_list,
+                     float *out, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(resid_sq_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, rows, n, dim, cents, tile_list, out);
+}
+
+void launch_meta16(const int64_t *slots, int64_t n, int32_t metric, const float *rsq, const uint8_t *live, float *meta,
+                   hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(meta16_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, slots, n, metric, rsq, live, meta);
+}
+
+void launch_absmax(const float *rows, const int64_t *slots, int64_t n, int32_t dim, uint32_t *out, hipStream_t st,
+                   const float *cents, const int32_t *tile_list) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(absmax_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, rows, slots, n, dim, cents, tile_list, out);
+}
+
+}  // namespace pyr

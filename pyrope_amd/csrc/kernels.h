@@ -232,7 +232,11 @@ bool sq8_supported(int dim, int k);
 // (codes written at slot), else row-major src with codes at i.  shifted: store code - 128
 // (the scan's int8 operands).  ok (may be null) set to 1.
 void launch_sq8_quantize(const float *src, const int64_t *slots, int blocked, int64_t n, int32_t dim, int32_t dp,
-                         int shifted, uint8_t *codes, int2 *sums, uint8_t *ok, hipStream_t st);
+                         int shifted, uint8_t *codes, int2 *sums, uint8_t *ok, hipStream_t st,
+                         float2 *minmax = nullptr);  // minmax[i]: Quantize's out min / max (may be null)
+// ScalarQuantizer.Dequantize (ScalarQuantizer.cs:65-84) of n code rows (n x dim) -> out (n x dim)
+void launch_sq8_dequantize(const uint8_t *codes, int64_t n, int32_t dim, const float *mins, const float *maxs,
+                           float *out, hipStream_t st);
 void launch_sq8_scan(const Sq8Args &a, int metric, int max_items, hipStream_t st);
 
 // ---- MFMA candidate filter + exact refine (filter.hip) ----
@@ -260,9 +264,16 @@ struct FilterArgs {
   int32_t waves;           // waves per block = items' queries / 32: 4, or 8 (bf16x3 only)
   int32_t xcd;             // 1: XCD-major item -> block mapping
   int32_t single;          // 1: single-buffered row tiles (bf16x3; smaller LDS, 2 barriers per stage)
+  // fp16 tile filter (filter16.hip, prec FILTER_F16X2 / FILTER_F16X1)
+  const void *h16;         // fp16 row tiles of the store (RowStore::h16)
+  const float *meta;       // per row: L2 -|x|^2, IP 0, -inf dead / padding (RowStore::meta)
+  float sx;                // the store's power-of-two fp16 scale
+  const float *cents;      // IVF residual tiles: list centroids (row-major), item.list selects; null = raw rows
 };
 constexpr int FILTER_FP32 = 0;    // v_mfma_f32_32x32x2_f32
 constexpr int FILTER_BF16X3 = 1;  // hi/lo bf16 split, 3 x v_mfma_f32_32x32x16_bf16
+constexpr int FILTER_F16X2 = 2;   // fp16 row tiles x two-term fp16 queries, 2 x v_mfma_f32_32x32x16_f16
+constexpr int FILTER_F16X1 = 3;   // fp16 row tiles x one-term fp16 queries, 1 MFMA per k-step
 // queries per filter work item (items must be built with this qchunk)
 inline int filter_qchunk(int prec, int waves) { return prec == FILTER_BF16X3 && waves == 8 ? 256 : 128; }
 // refine_kernel error-bound constant of the bf16x3 approximation (per u |q| max|x|)
@@ -271,6 +282,21 @@ inline double filter_bf16x3_cerr(int dim, int metric) {
   // doubled for L2 (approx = 2 q.x - ...)
   const double c = 6.3 * dim + 800.0;
   return metric == 0 ? 2.0 * c : c;
+}
+// refine_kernel constants of the fp16 tile filter: relative c_bf (per u |q| max|x|) and the absolute
+// term (per |q|) from fp16 subnormals of the rows, 2^-25 sqrt(D) / sx; doubled for L2.  x's fp16
+// rounding is 2^-11 = 8192 u relative; the two-term query split 2^-22 = 4 u; fp32 accumulation of
+// 2D exact products <= 2D u; one-term queries add q's own 2^-11.
+inline double filter_f16_cerr(int dim, int metric, int prec) {
+  const double c = 8192.0 + 4.0 + 2.0 * dim + 64.0 + (prec == FILTER_F16X1 ? 8192.0 + 64.0 : 0.0);
+  return metric == 0 ? 2.0 * c : c;
+}
+inline double filter_f16_abs(int dim, int metric, float sx, int prec) {
+  const double a = 2.9802322387695312e-08 * __builtin_sqrt((double)dim) / (double)sx;  // 2^-25 sqrt(D) / sx
+  // one-term queries: q's own subnormal halves (|q_i| sq < 2^-14) add 2^-25 / sq per |x_i|, bounded
+  // through |x| <= X in refine (q_abs there)
+  (void)prec;
+  return metric == 0 ? 2.0 * a : a;
 }
 struct RefineArgs {
   const float *rows;        // blocked store the keys index
@@ -286,7 +312,14 @@ struct RefineArgs {
   int64_t nq;
   int32_t k1, k, dim;
   double c_err;             // error-bound constant (refine_kernel)
-  double c_bf;              // extra constant of the bf16x3 filter (0 for fp32)
+  double c_bf;              // extra constant of the bf16x3 / fp16 filter (0 for fp32)
+  double c_abs;             // fp16 filter: absolute error per |q| (filter_f16_abs), else 0
+  int32_t q16;              // fp16 filter: add the queries' own fp16 subnormal term (per X, / sq)
+  // IVF residual fp16 filter (approx = estimate of the score itself): centroids, per-list max
+  // |x - c|^2 (score_key), and the query's probed lists (probes / nprobe above)
+  const float *cents;
+  const uint32_t *list_rmax_r;
+  int32_t resid;
   float *out_s;
   int64_t *out_l;
   int32_t *out_c;
@@ -294,6 +327,21 @@ struct RefineArgs {
   int32_t *fail_cnt;
 };
 bool filter_supported(int dim, int metric, int k1);
+bool filter16_supported(int dim, int metric, int k1);
+void launch_filter16(const FilterArgs &a, int metric, int max_items, hipStream_t st);
+// fp16 tiles of blocked fp32 rows (slots[i], or rows [0, n)), scaled by sx; with cents (row-major)
+// and tile_list (list of each 32-row tile) the residuals x - c[list] (IVF lists)
+void launch_encode16(const float *rows, const int64_t *slots, int64_t n, int32_t dim, float sx, void *h16,
+                     hipStream_t st, const float *cents = nullptr, const int32_t *tile_list = nullptr);
+// |x - c[list]|^2 of rows [0, n)
+void launch_resid_sq(const float *rows, int64_t n, int32_t dim, const float *cents, const int32_t *tile_list,
+                     float *out, hipStream_t st);
+// meta[r] = live ? (L2 ? -rsq : 0) : -inf for slots[i] (or rows [0, n))
+void launch_meta16(const int64_t *slots, int64_t n, int32_t metric, const float *rsq, const uint8_t *live, float *meta,
+                   hipStream_t st);
+// atomicMax of the float bits of max |x_i| (finite) over the rows into *out
+void launch_absmax(const float *rows, const int64_t *slots, int64_t n, int32_t dim, uint32_t *out, hipStream_t st,
+                   const float *cents = nullptr, const int32_t *tile_list = nullptr);
 void launch_filter(const FilterArgs &a, int metric, int max_items, hipStream_t st);
 // V: 1 = VectorMath safe form (IVF), 4 = *Unsafe form (FLAT)
 void launch_refine(const RefineArgs &a, int metric, int V, hipStream_t st);

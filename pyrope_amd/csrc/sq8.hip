@@ -45,7 +45,7 @@ __device__ __forceinline__ int net_round_to_int(float v) {
 // {sum c, sum c^2} over the real dims, and has-codes.
 __global__ __launch_bounds__(256) void sq8_quantize_kernel(const float *src, const int64_t *slots, int blocked,
                                                            int64_t n, int D, int dp, int shifted, uint8_t *codes,
-                                                           int2 *sums, uint8_t *ok) {
+                                                           int2 *sums, uint8_t *ok, float2 *minmax) {
   const int64_t v = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (v >= n) return;
@@ -66,6 +66,7 @@ __global__ __launch_bounds__(256) void sq8_quantize_kernel(const float *src, con
     if (a < mn) mn = a;
     if (b > mx) mx = b;
   }
+  if (minmax && lane == 0) minmax[v] = make_float2(mn, mx);  // the out min / out max of Quantize
   const float range = mx - mn;
   const float scale = 255.0f / range;
   uint8_t *out = codes + (size_t)slot * dp;
@@ -231,10 +232,34 @@ void launch_nk(const Sq8Args &a, int max_items, hipStream_t st) {
 }  // namespace
 
 void launch_sq8_quantize(const float *src, const int64_t *slots, int blocked, int64_t n, int32_t dim, int32_t dp,
-                         int shifted, uint8_t *codes, int2 *sums, uint8_t *ok, hipStream_t st) {
+                         int shifted, uint8_t *codes, int2 *sums, uint8_t *ok, hipStream_t st, float2 *minmax) {
   if (n <= 0) return;
   hipLaunchKernelGGL(sq8_quantize_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, src, slots, blocked, n, dim,
-                     dp, shifted, codes, sums, ok);
+                     dp, shifted, codes, sums, ok, minmax);
+}
+
+// ScalarQuantizer.Dequantize (ScalarQuantizer.cs:65-84): range 0 -> min everywhere, else
+// min + q * (range / 255) in fp32 (no contraction: the file is compiled with fp-contract off)
+__global__ void sq8_dequantize_kernel(const uint8_t *codes, int64_t n, int D, const float *mins, const float *maxs,
+                                      float *out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * D) return;
+  const int64_t v = e / D;
+  const float mn = mins[v], range = maxs[v] - mn;
+  if (range == 0.0f) {
+    out[e] = mn;
+    return;
+  }
+  const float scale = range / 255.0f;
+  const float t = (float)codes[e] * scale;
+  out[e] = mn + t;
+}
+
+void launch_sq8_dequantize(const uint8_t *codes, int64_t n, int32_t dim, const float *mins, const float *maxs,
+                           float *out, hipStream_t st) {
+  if (n <= 0 || dim <= 0) return;
+  hipLaunchKernelGGL(sq8_dequantize_kernel, dim3((unsigned)((n * dim + 255) / 256)), dim3(256), 0, st, codes, n, dim,
+                     mins, maxs, out);
 }
 
 // code row stride: dim rounded up to 32, then to a k-step count the scan is instantiated for

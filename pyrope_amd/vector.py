@@ -224,6 +224,10 @@ class HipVectorIndex(IVectorIndex):
         return [SearchResult(self._id_of.get(int(lab[0, j]), str(int(lab[0, j]))), float(s[0, j]))
                 for j in range(int(cnt[0]))]
 
+    def set_coalescing(self, max_batch: int, max_wait_us: int) -> None:
+        """Merge concurrent searches into device batches (pyr_index_set_coalescing); 0 turns it off."""
+        check(self._L.pyr_index_set_coalescing(self._h, int(max_batch), int(max_wait_us)))
+
     def search_device(self, d_q: int, nq: int, top_k: int, d_scores: int, d_labels: int, d_counts: int = 0,
                       stream: int = 0, options: Optional[SearchOptions] = None, d_probes: int = 0,
                       nprobe: int = 0) -> None:
@@ -595,3 +599,44 @@ def generate_synthetic_blocked(row0: int, count: int, dim: int, seed: int, block
     out = np.empty((count, dim), np.float32)
     check(_lib.load().pyr_generate_synthetic_blocked(row0, count, dim, seed, block_rows, ptr(out, C.c_float)))
     return out
+
+
+class ScalarQuantizer:
+    """Vector/ScalarQuantizer.cs (static class): per-vector min/max 8-bit quantization, on the GPU."""
+
+    @staticmethod
+    def quantize(vector, device: int = 0):
+        """Quantize(float[] vector, out min, out max) (:8-20) -> (codes, min, max); empty -> ([], 0, 0)."""
+        if vector is None or len(vector) == 0:
+            return np.zeros(0, np.uint8), 0.0, 0.0
+        v = np.ascontiguousarray(vector, dtype=np.float32).reshape(1, -1)
+        codes = np.zeros(v.shape, np.uint8)
+        mn, mx = np.zeros(1, np.float32), np.zeros(1, np.float32)
+        check(_lib.load().pyr_scalar_quantize_minmax(device, ptr(v, C.c_float), 1, v.shape[1], ptr(codes, C.c_uint8),
+                                                     ptr(mn, C.c_float), ptr(mx, C.c_float)))
+        return codes[0], float(mn[0]), float(mx[0])
+
+    @staticmethod
+    def quantize_into(vector, destination: np.ndarray, device: int = 0):
+        """Quantize(ReadOnlySpan<float>, Span<byte>, out min, out max) (:22-62) -> (min, max)."""
+        if len(vector) != len(destination):
+            raise ArgumentException("Vector and destination lengths must match.")
+        if len(vector) == 0:
+            return 0.0, 0.0
+        codes, mn, mx = ScalarQuantizer.quantize(vector, device)
+        destination[:] = codes
+        return mn, mx
+
+    @staticmethod
+    def dequantize(codes, vmin: float, vmax: float, device: int = 0) -> np.ndarray:
+        """Dequantize(byte[], min, max) (:64-84)."""
+        if codes is None:
+            return np.zeros(0, np.float32)
+        c = np.ascontiguousarray(codes, dtype=np.uint8).reshape(1, -1)
+        out = np.zeros(c.shape, np.float32)
+        if c.shape[1] == 0:
+            return out[0]
+        mn, mx = np.array([vmin], np.float32), np.array([vmax], np.float32)
+        check(_lib.load().pyr_scalar_dequantize(device, ptr(c, C.c_uint8), 1, c.shape[1], ptr(mn, C.c_float),
+                                                ptr(mx, C.c_float), ptr(out, C.c_float)))
+        return out[0]

@@ -82,6 +82,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--check", type=int, default=20, help="queries compared with the CPU oracle")
+    ap.add_argument("--cpu-seconds", type=float, default=0.0,
+                    help="flat: also time the CPU restatement (oracle, one query per thread, every usable CPU)")
     ap.add_argument("--sweep", default="", help="env settings run one after another on the same index, "
                                                  "e.g. 'PYR_PQ_THREADS=1024|PYR_PQ_ABLATE=1' (timing only)")
     a = ap.parse_args()
@@ -130,6 +132,23 @@ def main():
             else:
                 os_, ok_ = oracle.bf_search(x, None, a.metric, qh[i], a.k)
             ok &= bool(np.array_equal(lab[i], ok_) and np.array_equal(s[i].view(np.uint32), os_.view(np.uint32)))
+        cpu = None
+        if a.cpu_seconds > 0 and not a.quant:  # CPU baseline leg (BruteForceVectorIndex.Search per query)
+            from bench import host_cpus
+            host = host_cpus()
+            th = host["usable"]
+            S = min(a.nq, 4 * th)
+            t = time.perf_counter()
+            oracle.bf_search_batch(qh[:S], a.k, x, metric=a.metric, nthreads=th)
+            S = int(min(a.nq, max(S, S * a.cpu_seconds / max(time.perf_counter() - t, 1e-3))))
+            t = time.perf_counter()
+            cs, ck, _ = oracle.bf_search_batch(qh[:S], a.k, x, metric=a.metric, nthreads=th)
+            ct = time.perf_counter() - t
+            cpu = {"value": S / ct, "unit": "queries/s", "cores": th, "kind": "port", "host": host,
+                   "sample": f"{S} of the {a.nq} queries (oracle/oracle.c BruteForce search, one query per thread)",
+                   "parity": {"queries": S, "ids_equal": bool(np.array_equal(ck, lab[:S])),
+                              "scores_bit_identical": bool(np.array_equal(cs.view(np.uint32), s[:S].view(np.uint32)))}}
+            log(f"cpu baseline {S / ct:,.1f} QPS on {th} threads")
         scan = phases.get("flat_scan", {"ms": float("nan"), "work": 0})
         out = {"workload": f"FLAT{' SQ8' if a.quant else ''} d={d} N={n} Q={a.nq} k={a.k} "
                            f"metric={['L2', 'IP', 'COS'][a.metric]}",
@@ -137,7 +156,7 @@ def main():
                "scan_pairs": scan["work"],
                "scan_tflops_2d": scan["work"] * 2 * d / (scan["ms"] * 1e-3) / 1e12,
                "hbm_equiv_GBps": qps * n * d * 4 / 1e9,
-               "parity_sample": {"queries": a.check, "ids_and_bits_equal": ok}}
+               "parity_sample": {"queries": a.check, "ids_and_bits_equal": ok}, "cpu_baseline": cpu}
     else:
         n, d = a.n or 3_200_000, a.dim or 768
         x = generate_synthetic(n, d, 42)

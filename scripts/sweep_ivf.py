@@ -32,15 +32,16 @@ def main():
     args = ap.parse_args()
 
     import torch
-    from pyrope_amd import IvfFlatVectorIndex, VectorMetric, generate_synthetic, kmeans_train, _lib
+    from pyrope_amd import (IvfFlatVectorIndex, VectorMetric, generate_synthetic, generate_synthetic_blocked,
+                            kmeans_train, _lib)
     from pyrope_amd.vector import SearchOptions
     L = _lib.load()
     dev = torch.device("cuda", 0)
-    x = generate_synthetic(args.n, args.dim, 42)
+    x = generate_synthetic_blocked(0, args.n, args.dim, 42)  # bench.py's row-blocked base set
     cents = kmeans_train(x, args.nlist, VectorMetric.L2, 10, 42)
     idx = IvfFlatVectorIndex(args.dim, VectorMetric.L2, n_list=args.nlist)
     idx.set_centroids(cents)
-    idx.add_labels(np.arange(args.n, dtype=np.int64), x)
+    idx.add_labels(np.arange(args.n, dtype=np.int64), x, track_ids=False)
     idx.build()
     off, _, _ = idx.ivf_layout()
     ln = np.diff(off)
@@ -76,11 +77,13 @@ def main():
         torch.cuda.synchronize()
         L.pyr_profile_enable(0)
         ph = {}
-        for i, name in enumerate(["coarse", "items", "scan", "buf", "merge"]):
+        for i, name in {0: "coarse", 1: "items", 2: "scan", 3: "buf", 4: "merge", 7: "refine", 8: "rerun"}.items():
             ms, calls, work = C.c_double(), C.c_int64(), C.c_int64()
             L.pyr_profile_get(i, C.byref(ms), C.byref(calls), C.byref(work))
             if calls.value:
-                ph[name] = round(ms.value / calls.value, 3)
+                ph[name] = round(ms.value, 3)
+            if i == 8 and calls.value:
+                ph["reran_queries"] = work.value
         res = (s.cpu().numpy().copy(), lab.cpu().numpy().copy())
         same = None
         if ref is None:

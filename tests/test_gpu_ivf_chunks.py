@@ -145,7 +145,7 @@ def test_caller_ranked_probes_with_failed_certificates(hiplib, chunk):
         (_, nfb) = _fallbacks(hiplib, lambda: (idx.search_device(q.data_ptr(), nq, 10, s.data_ptr(), lab.data_ptr(),
                                                                   0, stream, opts, d_probes=probes.data_ptr(),
                                                                   nprobe=npb), torch.cuda.synchronize()))
-    assert nfb == nq
+    assert nfb >= nq  # every query re-run (filter tier, then exact)
     np.testing.assert_array_equal(lab.cpu().numpy(), ref[1])
     assert np.array_equal(s.cpu().numpy().view(np.uint32), ref[0].view(np.uint32))
 
@@ -174,15 +174,22 @@ def test_per_list_certificate_on_skewed_data(hiplib, metric):
     idx.add_labels(np.arange(len(x), dtype=np.int64), x)
     idx.build()
     opts = SearchOptions(nprobe=8)
-    got, nfb_list = _fallbacks(hiplib, lambda: idx.search_batch(q, 10, opts))
-    with _env(PYR_CERT_GLOBAL=1):
-        got_g, nfb_global = _fallbacks(hiplib, lambda: idx.search_batch(q, 10, opts))
     with _env(PYR_FILTER=0):
         ref = idx.search_batch(q, 10, opts)
+    # the bf16x3 filter's certificate (|q| |x|-relative error): per-list maxima + triangle bound
+    # against the index-wide maximum alone
+    with _env(PYR_FILTER_PREC=1, PYR_FILTER_TIER=0):
+        got, nfb_list = _fallbacks(hiplib, lambda: idx.search_batch(q, 10, opts))
+        with _env(PYR_CERT_GLOBAL=1):
+            got_g, nfb_global = _fallbacks(hiplib, lambda: idx.search_batch(q, 10, opts))
     _same(got, ref)
     _same(got_g, ref)
-    print(f"\n[cert] metric={metric}: exact re-runs per-list bound {nfb_list}/{len(q)}, "
-          f"index-wide bound {nfb_global}/{len(q)}")
+    # the default fp16 residual-tile filter: hub lists far from the query make its residual error
+    # bound large, so more queries go to the re-run tiers -- results stay exact
+    got16, nfb16 = _fallbacks(hiplib, lambda: idx.search_batch(q, 10, opts))
+    _same(got16, ref)
+    print(f"\n[cert] metric={metric}: bf16x3 exact re-runs per-list bound {nfb_list}/{len(q)}, "
+          f"index-wide bound {nfb_global}/{len(q)}; fp16 tiles re-runs (all tiers) {nfb16}")
     assert nfb_list <= nfb_global
     if metric == 0:
         assert nfb_list < len(q) // 10

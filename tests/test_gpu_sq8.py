@@ -90,3 +90,34 @@ def test_quantization_off_uses_float_path(hiplib, oracle):
     for i in range(len(q)):
         os_, ok = oracle.bf_search(x, None, 0, q[i], 10)
         np.testing.assert_array_equal(lab[i], ok)
+
+
+# ---- ScalarQuantizerTests.cs:10-68, restated as written ----
+def test_sq_quantize_and_dequantize_round_trip(hiplib):  # :10-30
+    from pyrope_amd import ScalarQuantizer
+    original = np.array([0.0, 0.5, 1.0, -1.0], np.float32)
+    quantized, vmin, vmax = ScalarQuantizer.quantize(original)
+    assert len(quantized) == len(original)
+    assert vmin == -1.0 and vmax == 1.0
+    reconstructed = ScalarQuantizer.dequantize(quantized, vmin, vmax)
+    for i in range(len(original)):
+        assert abs(original[i] - reconstructed[i]) <= 0.02
+
+
+def test_sq_quantize_handles_flat_vector(hiplib):  # :32-45
+    from pyrope_amd import ScalarQuantizer
+    original = np.array([0.5, 0.5, 0.5], np.float32)
+    quantized, vmin, vmax = ScalarQuantizer.quantize(original)
+    assert vmin == 0.5 and vmax == 0.5
+    assert all(b == 0 for b in quantized)
+    reconstructed = ScalarQuantizer.dequantize(quantized, vmin, vmax)
+    assert all(f == 0.5 for f in reconstructed)
+
+
+def test_sq_quantize_span_overload_works(hiplib):  # :47-60
+    from pyrope_amd import ScalarQuantizer
+    original = np.array([0.0, 1.0], np.float32)
+    dest = np.zeros(2, np.uint8)
+    vmin, vmax = ScalarQuantizer.quantize_into(original, dest)
+    assert vmin == 0.0 and vmax == 1.0
+    assert dest[0] == 0 and dest[1] == 255

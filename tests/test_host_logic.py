@@ -45,3 +45,14 @@ def test_labels_never_collide_after_caller_chosen_labels():
     ix._register_labels(np.array([2], np.int64))  # lower than the counter: the counter keeps going
     assert ix._label("c") == 10
     assert ix._id_of[8] == "a" and ix._label_of["7"] == 7
+
+
+
+def test_sq_span_overload_throws_on_length_mismatch():  # ScalarQuantizerTests.cs:62-68
+    import numpy as np
+    import pytest
+
+    from pyrope_amd import ArgumentException, ScalarQuantizer
+    with pytest.raises(ArgumentException, match="lengths must match"):
+        ScalarQuantizer.quantize_into(np.zeros(2, np.float32), np.zeros(3, np.uint8))
+    assert ScalarQuantizer.quantize([]) [1:] == (0.0, 0.0)  # empty vector: min = max = 0, no device call
