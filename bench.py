@@ -299,7 +299,16 @@ def run(args):
     # (PYR_FILTER=0): sub, mul, add per element, 3*D
     flops = scan["pairs"] * (2 if filt else 3) * D
     achieved = flops / (scan["ms"] * 1e-3) / 1e12
-    bf16x3 = filt and os.environ.get("PYR_FILTER_PREC", "1") != "0"
+    # the list-scan arithmetic (engine.cpp filter_prec): 2 = fp16 residual tiles, hi/lo query split
+    # (2 fp16 MFMAs per k-step, filter16.hip, default); 3 = one fp16 MFMA; 1 = bf16x3; 0 = fp32 MFMA
+    prec = int(os.environ.get("PYR_FILTER_PREC", "2")) if filt else -1
+    mfma_mult, mfma_peak = {2: (2, BF16_PEAK_TFLOPS), 3: (1, BF16_PEAK_TFLOPS), 1: (3, BF16_PEAK_TFLOPS),
+                            0: (1, FP32_PEAK_TFLOPS)}.get(prec, (1, FP32_PEAK_TFLOPS))
+    kernel_name = {2: "mfma_filter16<128,L2,16,f16x2> (IVF list scan, fp16 residual tiles, 2 fp16 MFMAs per k-step)",
+                   3: "mfma_filter16<128,L2,16,f16x1> (IVF list scan, fp16 residual tiles, 1 fp16 MFMA per k-step)",
+                   1: "mfma_filter<128,L2,IVF> (IVF list scan, bf16x3 MFMA candidate filter)",
+                   0: "mfma_filter<128,L2,IVF> (IVF list scan, fp32 MFMA candidate filter)"}.get(
+                       prec, "scan_fast<128,1,L2,IVF> (IVF list scan, exact VALU)")
     # unique algorithmic bytes of one list-scan launch on this rank: every list probed by any query
     # of the batch read once (its live rows of this shard x D x 4 B) plus the batch's queries -- the
     # HBM floor of a batched, list-major scan (SURVEY.md 8(d) "unique-bytes roofline")
@@ -312,6 +321,9 @@ def run(args):
     probed = np.unique(pr_full.cpu().numpy())
     probed = probed[probed >= 0]
     unique_bytes = float(rows_per_list[probed].sum()) * D * 4 + Q * D * 4
+    # what the fp16 tile kernel streams for the same rows: D x 2 B + a 4-B row term, padded lists
+    padded = np.diff(off_l).astype(np.int64)
+    stored_bytes = float(padded[probed].sum()) * (D * 2 + 4) + Q * D * 4 if prec in (2, 3) else unique_bytes
     hbm_achieved = unique_bytes / (scan["ms"] * 1e-3) / 1e9
     del pr_full
 
@@ -384,7 +396,7 @@ def run(args):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32",  # results and the certified refine are fp32; the filter streams fp16 tiles
             "data": "synthetic: Pyrope.Benchmarks generator (.NET Random), base rows in 65,536-row blocks seeded "
                     "42 + block, queries seed 1337, uniform [0,1)",
             "config": {"workload": f"IVF_FLAT d={D} N={N} nlist={args.nlist} nprobe={args.nprobe} k={k}",
@@ -398,18 +410,18 @@ def run(args):
             "roofline": {"bound": "hbm", "achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": hbm_achieved / HBM_PEAK_GBS, "traffic": None,
                          "unique_bytes_per_launch": unique_bytes, "lists_probed": int(len(probed)),
-                         "kernel": ("mfma_filter<128,L2,IVF> (IVF list scan, bf16x3 MFMA candidate filter)"
-                                    if bf16x3 else
-                                    "mfma_filter<128,L2,IVF> (IVF list scan, fp32 MFMA candidate filter)" if filt
-                                    else "scan_fast<128,1,L2,IVF> (IVF list scan, exact VALU)"),
+                         "kernel": kernel_name,
+                         "stored_bytes_per_launch": stored_bytes,
+                         "stored_GBps": stored_bytes / (scan["ms"] * 1e-3) / 1e9,
                          "note": ("algorithmic bytes = every probed list read once per launch (live rows x D x "
-                                  "4 B) + queries, over the HIP-event time of the launch (rank 0); traffic "
-                                  "(FETCH_SIZE, measured in its own rocprofv3 pass) is in profiles/*/summary.md")},
-            "mfma": {"achieved": achieved * (3 if bf16x3 else 1),
-                     "peak": BF16_PEAK_TFLOPS if bf16x3 else FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved * (3 if bf16x3 else 1) / (BF16_PEAK_TFLOPS if bf16x3 else FP32_PEAK_TFLOPS),
-                     "note": ("as-executed bf16 MFMA flops: probed (query,row) pairs x 2*D x 3 (hi.hi, hi.lo, "
-                              "lo.hi) vs the dense bf16 peak" if bf16x3 else
+                                  "4 B, the reference's fp32 rows) + queries, over the HIP-event time of the launch "
+                                  "(rank 0); stored_bytes = what the fp16 tile kernel actually streams for them "
+                                  "(D x 2 + 4 B per padded row); traffic (FETCH_SIZE x 2, its own rocprofv3 pass) is "
+                                  "in profiles/*/summary.md")},
+            "mfma": {"achieved": achieved * mfma_mult, "peak": mfma_peak, "unit": "TFLOP/s",
+                     "frac": achieved * mfma_mult / mfma_peak,
+                     "note": (f"as-executed MFMA flops: probed (query,row) pairs x 2*D x {mfma_mult} (MFMAs per "
+                              f"k-step) vs the dense fp16/bf16 peak" if prec in (1, 2, 3) else
                               "probed pairs x 2*D (fp32 MFMA) or x 3*D (exact VALU) vs the FP32 peak")},
             "exact_reruns": {"queries": fallback_queries, "in_profiled_steps": args.profile_steps,
                              "note": "queries whose MFMA-filter certificate failed and were re-scanned exactly"},

@@ -361,6 +361,12 @@ static int filter_prec() {
 static bool prec16(int prec) { return prec == FILTER_F16X2 || prec == FILTER_F16X1; }
 // the fp16 tile copy is kept for stores the fp16 filter can scan
 static bool store16(int dim, int metric) { return filter16_supported(dim, metric, 16); }
+// the arithmetic a filter launch really runs: the fp16 tile filter needs the store's fp16 tiles and
+// items of at most filter16_max_rows() rows; otherwise an fp16 request runs as bf16x3
+static int filter_prec_for(int prec, bool f16_store, int64_t max_item_rows) {
+  if (!prec16(prec)) return prec;
+  return f16_store && max_item_rows <= filter16_max_rows() ? prec : FILTER_BF16X3;
+}
 // waves per filter block for IVF items (FilterArgs::waves): 4 = 128-query items (default);
 // PYR_FILTER_WAVES=8 -> 256-query items, one block per CU (bf16x3 only): half the row
 // traffic but measured slower, 4.98 -> 7.42 ms at the bench config (profiles/r1_sweeps/sweep23).
@@ -406,7 +412,7 @@ static double filter_cerr(int dim) {
 static int64_t filter_finish(Workspace &ws, int64_t nq, int nparts, int k1, int k, int dim, int met, int V,
                              const float *d_q, const RowStore &rs, const MergeIvf *mi, float *d_s, int64_t *d_l,
                              int32_t *d_c, const uint32_t *list_rmax = nullptr, const float *resid_cents = nullptr,
-                             const uint32_t *list_rmax_r = nullptr) {
+                             const uint32_t *list_rmax_r = nullptr, int prec = -1) {
   ws.ms.ensure(sizeof(float) * nq * k1);
   ws.mk.ensure(sizeof(int32_t) * nq * k1);
   {
@@ -439,7 +445,7 @@ static int64_t filter_finish(Workspace &ws, int64_t nq, int nparts, int k1, int 
   r.k = k;
   r.dim = dim;
   r.c_err = filter_cerr(dim);
-  const int prec = filter_prec();
+  if (prec < 0) prec = filter_prec();
   if (prec16(prec) && rs.f16) {
     r.c_bf = filter_f16_cerr(dim, met, prec);
     r.c_abs = filter_f16_abs(dim, met, rs.sx, prec);
@@ -830,7 +836,7 @@ struct FlatIndex : Index {
     fa.gthr = gthr;
     fa.ablate = filter_ablate();
     fa.pub_mask = filter_pub_mask();
-    fa.prec = filter_prec();
+    fa.prec = filter_prec_for(filter_prec(), st.f16, p.chunk_rows);
     fa.waves = 4;  // items of QCHUNK = 128 queries (plan_flat)
     fa.xcd = getenv("PYR_FLAT_XCD") ? atoi(getenv("PYR_FLAT_XCD")) != 0 : 0;  // measurement knob
     fa.h16 = st.h16.p;
@@ -838,10 +844,12 @@ struct FlatIndex : Index {
     fa.sx = st.sx;
     {
       PhaseTimer t(PH_FLAT_SCAN, ws.st, nq * cutoff);
-      if (prec16(fa.prec) && st.f16) launch_filter16(fa, metric, p.nitems, ws.st);
+      if (prec16(fa.prec)) launch_filter16(fa, metric, p.nitems, ws.st);
       else launch_filter(fa, metric, p.nitems, ws.st);
     }
-    const int64_t nf = filter_finish(ws, nq, p.nchunks, k1, k, dim, metric, 4, d_q, st, nullptr, d_s, d_l, d_c);
+    const int64_t nf =
+        filter_finish(ws, nq, p.nchunks, k1, k, dim, metric, 4, d_q, st, nullptr, d_s, d_l, d_c, nullptr, nullptr,
+                      nullptr, fa.prec);
     const int k1_next = filter_k1_next(k, k1);
     filter_fallback(ws, nf, d_q, dim, k, d_s, d_l, d_c,
                     [&](const float *q2, int64_t n2, float *s2, int64_t *l2, int32_t *c2) {
@@ -1487,7 +1495,7 @@ struct IvfFlatIndex : Index {
     fa.gthr = gthr;
     fa.ablate = filter_ablate();
     fa.pub_mask = filter_pub_mask();
-    fa.prec = filter_prec();
+    fa.prec = filter_prec_for(filter_prec(), lists.f16, std::max(ch.chunk, ch.warm));
     fa.waves = waves;
     fa.xcd = filter_xcd();
     fa.single = getenv("PYR_FILTER_SB") ? atoi(getenv("PYR_FILTER_SB")) != 0 : 0;
@@ -1495,12 +1503,14 @@ struct IvfFlatIndex : Index {
     fa.meta = lists.meta.as<float>();
     fa.sx = lists.sx;
     fa.cents = lists.resid ? coarse.rm.as<float>() : nullptr;
-    const bool use16 = prec16(fa.prec) && lists.f16;
+    const bool use16 = prec16(fa.prec);
     DevMem dbg;
-    if (getenv("PYR_FILTER_DEBUG")) {  // measurement only: insert statistics to stderr
-      dbg.ensure(16);
-      HIPCHK(hipMemsetAsync(dbg.p, 0, 16, ws.st));
-      fa.dbg = dbg.as<uint32_t>();
+    const int dbg_mode = getenv("PYR_FILTER_DEBUG") ? atoi(getenv("PYR_FILTER_DEBUG")) : 0;
+    if (dbg_mode) {  // measurement only: 1 insert statistics, 2 filter16 cycle buckets, to stderr
+      dbg.ensure(128);
+      HIPCHK(hipMemsetAsync(dbg.p, 0, 128, ws.st));
+      if (dbg_mode == 2) fa.tdbg = reinterpret_cast<unsigned long long *>(dbg.p) + 8;
+      else fa.dbg = dbg.as<uint32_t>();
     }
     {
       PhaseTimer t(PH_LIST_SCAN, ws.st, prof().on ? probed_rows(ws, nq, probes, le, lb) : 0);
@@ -1522,6 +1532,17 @@ struct IvfFlatIndex : Index {
               h[0], h[1], use16 ? "owner drains" : "owner stages", h[2]);
       if (use16) fprintf(stderr, "[filter] shared-bound refreshes that raised a threshold %u\n", h[3]);
     }
+    if (fa.tdbg) {
+      unsigned long long c[8];
+      HIPCHK(hipMemcpyAsync(c, fa.tdbg, sizeof(c), hipMemcpyDeviceToHost, ws.st));
+      HIPCHK(hipStreamSynchronize(ws.st));
+      const double tot = (double)c[5];
+      fprintf(stderr,
+              "[filter16 cycles] total %.3g (wave-cycles), wait %.1f%%, refresh %.1f%%, compute %.1f%%, append %.1f%%, "
+              "drain %.1f%%, prologue %.1f%%; active wave-tiles %llu, compute cycles per wave-tile %.0f\n",
+              tot, 100 * c[0] / tot, 100 * c[1] / tot, 100 * c[2] / tot, 100 * c[3] / tot, 100 * c[4] / tot,
+              100 * c[6] / tot, c[7], c[7] ? (double)c[2] / c[7] : 0.0);
+    }
     MergeIvf mi;
     mi.probes = ws.probes.as<int32_t>();
     mi.lb = dlb.as<int32_t>();
@@ -1530,7 +1551,7 @@ struct IvfFlatIndex : Index {
     mi.ch = ch;
     const int64_t nf = filter_finish(ws, nq, nparts, k1, k, dim, metric, 1, d_q, lists, &mi, d_s, d_l, d_c,
                                      dlmax.as<uint32_t>(), use16 && lists.resid ? coarse.rm.as<float>() : nullptr,
-                                     dlmax_r.as<uint32_t>());
+                                     dlmax_r.as<uint32_t>(), fa.prec);
     // The exact re-run scans the failing queries' OWN probe lists: ws.probes holds the batch's
     // ranking (computed above or handed in by the caller, pyr_index_search_probed_device), so its
     // rows are gathered in fail-list order and passed as caller-ranked lists.  (Re-ranking is

@@ -41,7 +41,6 @@ typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void gbl_void;
 
 constexpr int RT16 = 32;        // rows per tile (one 32x32 MFMA tile per wave)
-constexpr int NST = 3;          // LDS ring slots (tiles in flight + the one being read)
 constexpr int CB16 = 48;        // candidate buffer entries per query (>= 32 + drain slack)
 
 __device__ __forceinline__ bool better(float s1, uint32_t k1, float s2, uint32_t k2) {
@@ -62,33 +61,44 @@ __device__ __forceinline__ void reg_insert(float (&s)[KR], uint32_t (&kk)[KR], f
   kk[0] = b[0] ? key : kk[0];
 }
 
-// LDS: two separate objects, so that the compiler can tell the LDS-DMA target (the ring) from
-// the candidate state -- with one array it waits vmcnt(0) (the whole prefetch) before every
-// candidate append.  Ring: NST slots [rows TB][meta: 4 wave copies x 64 floats][dummy 1 KiB when
-// D = 32].  State: thresholds [128], counts [128], candidate scores [128][CB16], keys [128][CB16].
-template <int D>
-struct F16Lds {
-  static constexpr int TB = RT16 * D * 2;               // h16 bytes per tile
-  static constexpr int NCH = TB / 1024;                 // 1 KiB glds pieces per tile
-  static constexpr int NR = NCH >= 4 ? NCH / 4 : 1;     // row pieces per wave per tile
-  static constexpr int META = TB;                       // offset of the meta copies in a slot
-  static constexpr int DUMMY = TB + 1024;               // landing zone of the D = 32 filler pieces
-  static constexpr int SLOT = TB + 1024 + (NCH < 4 ? 1024 : 0);
-  static constexpr int LPT = NR + 1;                    // glds per wave per tile (rows + meta)
-  static constexpr int RING = NST * SLOT;
-  static_assert(NCH <= 4 ? true : NCH % 4 == 0, "row pieces must split evenly over 4 waves");
-};
+// LDS: two separate objects, so that the compiler can tell the LDS-DMA targets (ring, shared
+// bounds) from the candidate state -- with one array it waits vmcnt(0) (the whole prefetch) before
+// every candidate append.  Ring: NST slots [rows TB][meta: 64 floats, rows 0-31 twice].  State:
+// thresholds [128], counts [128], candidate scores [128][CB16], keys [128][CB16] as row offsets in
+// the item (u16: items span at most 65536 rows, filter16_max_rows()), the shared bounds [4][64].
+// NST is as deep as two blocks per CU allow (80 KiB each): 5 at D = 128, 8 below.
 struct F16State {
   float thr[128];
   int cnt[128];
   float cs[128 * CB16];
-  uint32_t ck[128 * CB16];
+  uint16_t ck[128 * CB16];
+};
+template <int D, int NSTC = 0>  // NSTC: ring depth (0 = as deep as the LDS budget allows, capped at 8)
+struct F16Lds {
+  static constexpr int TB = RT16 * D * 2;               // h16 bytes per tile
+  static constexpr int NCH = TB / 1024;                 // 1 KiB glds pieces per tile
+  static constexpr int NR = NCH >= 4 ? NCH / 4 : 1;     // row pieces per loading wave per tile
+  static constexpr int META = TB;                       // offset of the meta piece in a slot
+  static constexpr int SLOT = TB + 256;
+  static constexpr int BOUNDS = 4 * 256;                // shared-bound landing zone (one piece per wave)
+  static constexpr int BUDGET = 80 * 1024 - (int)sizeof(F16State) - BOUNDS;
+  static constexpr int NST_MAX = BUDGET / SLOT > 8 ? 8 : BUDGET / SLOT;
+  static constexpr int NST = NSTC > 0 && NSTC < NST_MAX ? NSTC : NST_MAX;  // ring slots
+  static constexpr int RING = NST * SLOT;
+  static_assert(NST >= 3, "LDS ring too shallow");
+  static_assert(NCH <= 4 ? true : NCH % 4 == 0, "row pieces must split evenly over 4 waves");
+  // glds issued by wave w per tile: its row pieces, + the meta piece for wave 0
+  static __device__ __forceinline__ int lpt(int w) {
+    return (NCH >= 4 ? NR : (w < NCH ? 1 : 0)) + (w == 0 ? 1 : 0);
+  }
 };
 
 // LDS-DMA of SIZE (16 or 4) bytes per lane: global g (per lane) -> LDS lds + lane * SIZE (lds
 // wave-uniform, in M0).  Written in inline asm on purpose: the compiler does not track these
 // writes, so it does not drain every in-flight tile (vmcnt(0)) before each LDS access it cannot
 // prove disjoint; the kernel's own counted vmcnt waits + barrier order the ring instead.
+// SIZE 16: row pieces; 4: meta; 5: a 4-byte agent-coherent read (sc1, the shared bounds, as
+// __hip_atomic_load with agent scope compiles to).
 template <int SIZE>
 __device__ __forceinline__ void glds(const void *g, uint32_t lds_addr) {
   int keep;
@@ -98,11 +108,30 @@ __device__ __forceinline__ void glds(const void *g, uint32_t lds_addr) {
                  : "=&s"(keep)
                  : "v"(g), "s"(lds)
                  : "memory");
-  else
+  else if (SIZE == 4)
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
                  : "v"(g), "s"(lds)
                  : "memory");
+  else
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off sc1\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(lds)
+                 : "memory");
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform n in [0, 3 * (NST - 2)] (immediate operand)
+template <int N>
+__device__ __forceinline__ void wait_vm_le(int n) {
+  if constexpr (N > 0) {
+    if (n >= N) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+      return;
+    }
+    wait_vm_le<N - 1>(n);
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
 }
 
 // query scale: a power of two putting max |q_i| below 2^14 (1 for a zero query)
@@ -113,17 +142,42 @@ __device__ __forceinline__ float pow2_scale(float amax) {
   return ldexpf(1.0f, 14 - e);
 }
 
-template <int D, int MET, int KR, bool Q2>
+// measurement only (a.tdbg): wave-uniform cycle buckets of the scan loop
+struct CycleBuckets {
+  unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long t0 = 0, prev = 0;
+  bool on = false;
+  __device__ void start(bool enable) {
+    on = enable;
+    if (on) t0 = prev = __builtin_amdgcn_s_memtime();
+  }
+  __device__ void mark(int b) {
+    if (!on) return;
+    const unsigned long long now = __builtin_amdgcn_s_memtime();
+    acc[b] += now - prev;
+    prev = now;
+  }
+  __device__ void flush(unsigned long long *out, int lane) {
+    if (!on) return;
+    acc[5] = __builtin_amdgcn_s_memtime() - t0;
+    if (lane == 0)
+      for (int b = 0; b < 8; ++b) atomicAdd(out + b, acc[b]);
+  }
+};
+
+template <int D, int MET, int KR, bool Q2, int NSTC>
 __global__ __launch_bounds__(256, 2) void mfma_filter16(FilterArgs a) {
-  using L = F16Lds<D>;
+  using L = F16Lds<D, NSTC>;
   constexpr int KS = D / 16;
+  constexpr int NST = L::NST;
   __shared__ __attribute__((aligned(16))) char ring[L::RING];
+  __shared__ __attribute__((aligned(16))) uint32_t bounds_l[L::BOUNDS / 4];
   __shared__ __attribute__((aligned(16))) F16State state16;
   const uint32_t ring_base = (uint32_t)(size_t)(lds_void *)ring;  // LDS byte address (M0 of the DMA)
   float *const thr_l = state16.thr;
   int *const cnt_l = state16.cnt;
   float *const cs_l = state16.cs;
-  uint32_t *const ck_l = state16.ck;
+  uint16_t *const ck_l = state16.ck;
 
   int item = blockIdx.x;
   if (a.xcd) {  // XCD-major mapping (filter.hip): a list chunk's query groups share an XCD's L2
@@ -135,6 +189,8 @@ __global__ __launch_bounds__(256, 2) void mfma_filter16(FilterArgs a) {
   const ScanItem it = a.items[item];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int i32 = lane & 31, h = lane >> 5;
+  CycleBuckets cb;
+  cb.start(a.tdbg != nullptr);
 
   // ---- A operand: query 32w + i32, dims 16s + 8h .. +7 of k-step s, scaled and split ----
   const int qslot = 32 * w + i32;
@@ -215,6 +271,8 @@ __global__ __launch_bounds__(256, 2) void mfma_filter16(FilterArgs a) {
     tk[j] = KEY_NONE;
   }
   uint32_t published = 0;
+  float sink = 0.0f;  // measurement only (ablations): keeps the ablated work live
+  int bst = -1;  // tile at which the shared bounds were last read into bounds_l (-1: never)
   if (h == 0) {
     // an unused query slot of an active wave scores zero queries: +inf keeps its rows out of the
     // buffers (with -inf every row would survive for it and force a drain every tile)
@@ -222,37 +280,47 @@ __global__ __launch_bounds__(256, 2) void mfma_filter16(FilterArgs a) {
     cnt_l[qslot] = 0;
   }
 
-  // ---- tile loads: rows as NR lane-linear 1 KiB pieces per wave, meta as one 128-B piece per wave ----
+  // ---- tile loads: rows as lane-linear 1 KiB pieces spread over the waves, meta (one 256-B piece,
+  // lanes 32-63 repeating rows 0-31) by wave 0 ----
   const int r0 = it.row_begin;  // multiple of 32
   const int nt = (it.row_end - r0 + RT16 - 1) / RT16;
   const char *hsrc = reinterpret_cast<const char *>(a.h16);
+  const int lpt = L::lpt(w);  // this wave's loads per tile (its counted waits)
   // tile t -> ring slot t % NST (LDS-DMA; issued in inline asm, see glds())
   auto issue = [&](int t) {
     const size_t tile = (size_t)(r0 / RT16 + t);
     const uint32_t base = ring_base + (uint32_t)((t % NST) * L::SLOT);
+    if (L::NCH >= 4 || w < L::NCH) {
 #pragma unroll
-    for (int p = 0; p < L::NR; ++p) {
-      const int c = L::NCH >= 4 ? w * L::NR + p : (w & (L::NCH - 1));
-      const uint32_t dst = (L::NCH >= 4 || w < L::NCH) ? base + c * 1024 : base + L::DUMMY;
-      glds<16>(hsrc + tile * L::TB + (size_t)c * 1024 + lane * 16, dst);
+      for (int p = 0; p < L::NR; ++p) {
+        const int c = L::NCH >= 4 ? w * L::NR + p : w;
+        glds<16>(hsrc + tile * L::TB + (size_t)c * 1024 + lane * 16, base + c * 1024);
+      }
     }
-    // meta: the tile's 32 floats, 4 B per lane, into this wave's 256-B copy (lanes 32-63 repeat them)
-    glds<4>(a.meta + tile * RT16 + (lane & 31), base + L::META + w * 256);
+    if (w == 0) glds<4>(a.meta + tile * RT16 + (lane & 31), base + L::META);
   };
   __syncthreads();  // thresholds / counts initialised (the first barrier of the loop orders the rest)
 #pragma unroll
   for (int t = 0; t < NST - 1; ++t)
     if (t < nt) issue(t);
 
+  // thr[r]: query q(r, h)'s threshold moved to the pre-constant score y = f * acc + meta (the
+  // score is y + cq): t - cq lowered by a margin that covers both roundings (y + cq rounded >= t
+  // implies y >= t - cq - ulp terms), so every row with score >= t passes (a few below it may too;
+  // the owners' insertion compares the exact buffered scores).  A -inf threshold becomes -FLT_MAX
+  // (dead / padding rows, y = -inf, never pass), +inf (unused query slot) stays +inf.
   float thr[16];
   auto load_thr = [&]() {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float4 t4 = *reinterpret_cast<const float4 *>(thr_l + 32 * w + 8 * j + 4 * h);
-      thr[4 * j] = t4.x;
-      thr[4 * j + 1] = t4.y;
-      thr[4 * j + 2] = t4.z;
-      thr[4 * j + 3] = t4.w;
+      const float tv[4] = {t4.x, t4.y, t4.z, t4.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float t = tv[e], c = cqr[4 * j + e];
+        const float lowered = (t - c) - 0x1p-20f * (fabsf(t) + fabsf(c));
+        thr[4 * j + e] = isinf(t) ? (t > 0.0f ? t : -FLT_MAX) : fmaxf(lowered, -FLT_MAX);
+      }
     }
   };
   load_thr();
@@ -270,36 +338,54 @@ __global__ __launch_bounds__(256, 2) void mfma_filter16(FilterArgs a) {
     __builtin_amdgcn_wave_barrier();
   };
 
+  cb.mark(6);
   for (int st = 0; st < nt; ++st) {
     // tile st has landed for this wave once at most the younger tiles' loads are outstanding
     // (the compiler does not see the LDS-DMA, so these waits are the only ones ordering it)
-    if (st + 1 < nt)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L::LPT * (NST - 2)) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // (extra loads issued after tile st -- the shared bounds, publishes -- only make it stricter)
+    wait_vm_le<3 * (NST - 2)>(st + 1 < nt ? lpt * min(NST - 2, nt - 1 - st) : 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave's pieces of tile st landed; tile st-1 fully read
+    cb.mark(0);
     if (a.gthr && (st & a.pub_mask) == a.pub_mask && wave_active) {
-      // every pub_mask + 1 tiles: publish this list's K1-th best and take the query's shared bound
-      // (other items' progress) back.  Done before this iteration's prefetch is issued, so the wait
-      // for the returned value only drains tile st + 1's pieces.
+      // every pub_mask + 1 tiles: take the query's shared bound (other items' progress) read by the
+      // previous refresh -- an LDS-DMA issued pub_mask + 1 (>= NST - 1) tiles ago, so this tile's
+      // counted wait covered it -- publish this list's K1-th best (an atomic nothing waits for) and
+      // read the bound again for the next refresh.  No wait on a returning atomic in the loop.
+      // the previous read is consumed only once NST - 2 younger tiles' loads have been issued after
+      // it (then the counted wait at the top of this iteration covered it)
+      const bool landed = bst >= 0 && st - bst >= NST - 2;
       if (owner) {
-        const uint32_t mine = tk[KR - 1] != KEY_NONE ? score_key(ts[KR - 1]) : 0u;
-        const uint32_t old = atomicMax(a.gthr + qown, max(mine, published));
-        published = max(mine, published);
-        const float g = key_score(max(old, published));
-        if (g > gs) {
-          gs = g;
-          thr_l[qslot] = fmaxf(thr_l[qslot], gs);
-          if (a.dbg) atomicAdd(a.dbg + 3, 1u);  // measurement only: refreshes that raised the bound
+        if (landed) {
+          const float g = key_score(bounds_l[64 * w + i32]);
+          if (g > gs) {
+            gs = g;
+            thr_l[qslot] = fmaxf(thr_l[qslot], gs);
+            if (a.dbg) atomicAdd(a.dbg + 3, 1u);  // measurement only: refreshes that raised the bound
+          }
         }
+        if (tk[KR - 1] != KEY_NONE && score_key(ts[KR - 1]) > published) {
+          published = score_key(ts[KR - 1]);
+          atomicMax(a.gthr + qown, published);
+        }
+      }
+      if (landed || bst < 0) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the read above before the DMA rewrites it
+        glds<5>(a.gthr + (qi >= 0 ? qi : 0), (uint32_t)(size_t)(lds_void *)bounds_l + 256 * w);
+        bst = st;
       }
       __builtin_amdgcn_wave_barrier();
       load_thr();
     }
     if (st + NST - 1 < nt) issue(st + NST - 1);  // into the slot tile st-1 used
+    cb.mark(1);
     if (!wave_active) continue;
+    cb.acc[7] += 1;
     const char *slot = ring + (st % NST) * L::SLOT;
+    if (a.ablate & 128) {  // measurement only: the tile stream alone
+      sink += reinterpret_cast<const float *>(slot + L::META)[i32];
+      continue;
+    }
     f16v acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
@@ -310,45 +396,55 @@ __global__ __launch_bounds__(256, 2) void mfma_filter16(FilterArgs a) {
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qh[s], xh, acc, 0, 0, 0);
     }
     const int row = r0 + st * RT16 + i32;
-    float m = reinterpret_cast<const float *>(slot + L::META + w * 256)[i32];
+    float m = reinterpret_cast<const float *>(slot + L::META)[i32];
     if (row >= it.row_end || (uint32_t)row >= a.row_limit) m = -INFINITY;
-    float sv[16];
-    bool any = false;
+    float y[16];
+    uint64_t bm[16];  // wave-uniform survivor masks per register
+    uint64_t anyb = 0;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      sv[r] = fmaf(f[r], acc[r], m) + cqr[r];
-      any |= sv[r] >= thr[r] && sv[r] > -INFINITY;
+      y[r] = fmaf(f[r], acc[r], m);
+      bm[r] = __ballot(y[r] >= thr[r]);
+      anyb |= bm[r];
     }
-    if (!__any(any)) continue;
+    cb.mark(2);
+    if (a.ablate & 64) {  // measurement only: stream + MFMA + scores, no candidates
+      sink += anyb ? y[0] : 0.0f;
+      continue;
+    }
+    if (anyb == 0) continue;
     // survivors -> the queries' LDS buffers (at most 32 per query per tile: one per row).  The wave
     // owns its 32 queries' buffers, so the fill counts live in registers (cnt[r]: query q(r, h),
     // uniform over the half-wave) and a survivor's slot is its rank among the half's survivors.
-    const uint32_t key = a.key_base | (uint32_t)row;
+    const uint16_t off = (uint16_t)(row - r0);
     if (a.dbg) {  // measurement only: survivors, survivor tiles
       int ns = 0;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) ns += sv[r] >= thr[r] && sv[r] > -INFINITY;
-      atomicAdd(a.dbg + 1, (uint32_t)ns);
-      if (lane == 0) atomicAdd(a.dbg, 1u);
+      for (int r = 0; r < 16; ++r) ns += __builtin_popcountll(bm[r]);
+      if (lane == 0) {
+        atomicAdd(a.dbg + 1, (uint32_t)ns);
+        atomicAdd(a.dbg, 1u);
+      }
     }
-    const uint32_t below = (1u << i32) - 1u;
     int cmax = 0;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const bool s = sv[r] >= thr[r] && sv[r] > -INFINITY;
-      const uint64_t b = __ballot(s);
-      if (b == 0) continue;
-      const uint32_t bh = h ? (uint32_t)(b >> 32) : (uint32_t)b;
-      if (s) {
+      if (bm[r] == 0) continue;
+      const uint32_t lo = (uint32_t)bm[r], hi = (uint32_t)(bm[r] >> 32);
+      const int plo = __builtin_popcount(lo), phi = __builtin_popcount(hi);
+      // rank among the half's survivors: mbcnt counts the mask's bits below the lane over all 64
+      const int rank = (int)__builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u)) - (h ? plo : 0);
+      if (y[r] >= thr[r]) {
         const int q = 32 * w + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int idx = cnt[r] + __builtin_popcount(bh & below);
-        cs_l[q * CB16 + idx] = sv[r];
-        ck_l[q * CB16 + idx] = key;
+        const int idx = cnt[r] + rank;
+        cs_l[q * CB16 + idx] = y[r] + cqr[r];
+        ck_l[q * CB16 + idx] = off;
       }
-      cnt[r] += __builtin_popcount(bh);
+      cnt[r] += h ? phi : plo;
       cmax = max(cmax, cnt[r]);
     }
     // the owners drain every buffer of the wave when one could overflow on the next tile
+    cb.mark(3);
     if (!__any(cmax > CB16 - RT16)) continue;
     publish_counts();
     int c = 0;
@@ -356,16 +452,14 @@ __global__ __launch_bounds__(256, 2) void mfma_filter16(FilterArgs a) {
     if (owner) {
       for (int i = 0; i < c; ++i) {
         const float v = cs_l[qslot * CB16 + i];
-        const uint32_t k2 = ck_l[qslot * CB16 + i];
+        const uint32_t k2 = a.key_base | (uint32_t)(r0 + ck_l[qslot * CB16 + i]);
         if (better(v, k2, ts[KR - 1], tk[KR - 1])) reg_insert<KR>(ts, tk, v, k2);
       }
-      if (a.gthr) {
-        // publish this list's K1-th best and take the query's shared bound back (other items'
-        // progress); waiting for the returned value drains this wave's loads once per drain
-        const uint32_t mine = tk[KR - 1] != KEY_NONE ? score_key(ts[KR - 1]) : 0u;
-        const uint32_t old = atomicMax(a.gthr + qown, max(mine, published));
-        published = max(mine, published);
-        gs = fmaxf(gs, key_score(max(old, published)));
+      if (a.gthr && tk[KR - 1] != KEY_NONE && score_key(ts[KR - 1]) > published) {
+        // publish this list's K1-th best (no return value: nothing waits for it; the shared bound
+        // comes back through the periodic refresh)
+        published = score_key(ts[KR - 1]);
+        atomicMax(a.gthr + qown, published);
       }
       float t = gs;
       if (tk[KR - 1] != KEY_NONE) t = fmaxf(t, ts[KR - 1]);
@@ -376,13 +470,14 @@ __global__ __launch_bounds__(256, 2) void mfma_filter16(FilterArgs a) {
     for (int r = 0; r < 16; ++r) cnt[r] = 0;
     __builtin_amdgcn_wave_barrier();
     load_thr();
+    cb.mark(4);
   }
   publish_counts();
   if (owner) {
     const int c = cnt_l[qslot];
     for (int i = 0; i < c; ++i) {
       const float v = cs_l[qslot * CB16 + i];
-      const uint32_t k2 = ck_l[qslot * CB16 + i];
+      const uint32_t k2 = a.key_base | (uint32_t)(r0 + ck_l[qslot * CB16 + i]);
       if (better(v, k2, ts[KR - 1], tk[KR - 1])) reg_insert<KR>(ts, tk, v, k2);
     }
     if (a.gthr && tk[KR - 1] != KEY_NONE && score_key(ts[KR - 1]) > published)
@@ -394,17 +489,35 @@ __global__ __launch_bounds__(256, 2) void mfma_filter16(FilterArgs a) {
       ps[j] = ts[j];
       pk[j] = tk[j];
     }
+    if (a.ablate & (64 | 128)) ps[0] = sink;
   }
+  cb.flush(a.tdbg, lane);
 }
 
 inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
+// ring depth of the D = 128, K1 = 16 kernels (PYR_F16_NST, measurement knob: 3, 4 or 0 = deepest)
+static int f16_nst() {
+  static const int v = getenv("PYR_F16_NST") ? atoi(getenv("PYR_F16_NST")) : 3;
+  return v;
+}
+
 template <int D, int MET, int KR, bool Q2>
 void launch16_p(const FilterArgs &a, int max_items, hipStream_t st) {
-  // all LDS is static (77 KiB at D = 128): no dynamic-LDS attribute (a 160 KiB dynamic limit on top
+  // all LDS is static (79 KiB at D = 128): no dynamic-LDS attribute (a 160 KiB dynamic limit on top
   // of the static size makes the launch invalid)
   const int grid = a.xcd ? (max_items + 7) / 8 * 8 : max_items;
-  hipLaunchKernelGGL((mfma_filter16<D, MET, KR, Q2>), dim3(grid), dim3(256), 0, st, a);
+  if constexpr (D == 128 && KR == 16) {
+    if (f16_nst() == 3) {
+      hipLaunchKernelGGL((mfma_filter16<D, MET, KR, Q2, 3>), dim3(grid), dim3(256), 0, st, a);
+      return;
+    }
+    if (f16_nst() == 4) {
+      hipLaunchKernelGGL((mfma_filter16<D, MET, KR, Q2, 4>), dim3(grid), dim3(256), 0, st, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((mfma_filter16<D, MET, KR, Q2, 0>), dim3(grid), dim3(256), 0, st, a);
 }
 
 template <int D, int MET>
@@ -483,6 +596,8 @@ __global__ void resid_sq_kernel(const float *rows, int64_t n, int D, const float
 }
 
 }  // namespace
+
+int filter16_max_rows() { return 65536; }  // candidate keys are u16 row offsets within an item
 
 bool filter16_supported(int dim, int metric, int k1) {
   if (metric != L2 && metric != IP) return false;

@@ -269,6 +269,8 @@ struct FilterArgs {
   const float *meta;       // per row: L2 -|x|^2, IP 0, -inf dead / padding (RowStore::meta)
   float sx;                // the store's power-of-two fp16 scale
   const float *cents;      // IVF residual tiles: list centroids (row-major), item.list selects; null = raw rows
+  unsigned long long *tdbg;  // measurement only (PYR_FILTER_DEBUG=2, filter16): per-wave cycle buckets
+                             // [wait, refresh, compute, append, drain, total, prologue, wave-tiles]
 };
 constexpr int FILTER_FP32 = 0;    // v_mfma_f32_32x32x2_f32
 constexpr int FILTER_BF16X3 = 1;  // hi/lo bf16 split, 3 x v_mfma_f32_32x32x16_bf16
@@ -327,6 +329,7 @@ struct RefineArgs {
   int32_t *fail_cnt;
 };
 bool filter_supported(int dim, int metric, int k1);
+int filter16_max_rows();  // rows per scan item the fp16 filter accepts
 bool filter16_supported(int dim, int metric, int k1);
 void launch_filter16(const FilterArgs &a, int metric, int max_items, hipStream_t st);
 // fp16 tiles of blocked fp32 rows (slots[i], or rows [0, n)), scaled by sx; with cents (row-major)
