@@ -65,6 +65,7 @@ void RowStore::reserve(int64_t slots, hipStream_t st) {
   HIPCHK(hipMemsetAsync(rsq.as<float>() + cap, 0, sizeof(float) * (nc - cap), st));
   if (cosine) HIPCHK(hipMemsetAsync(norms.as<float>() + cap, 0, sizeof(float) * (nc - cap), st));
   if (f16) {
+    if (center16) rsq16.grow_keep(sizeof(float) * nc, sizeof(float) * cap, st);
     h16.grow_keep(sizeof(uint16_t) * nc * dim, sizeof(uint16_t) * cap * dim, st);
     meta.grow_keep(sizeof(float) * nc, sizeof(float) * cap, st);
     HIPCHK(hipMemsetAsync(static_cast<char *>(h16.p) + sizeof(uint16_t) * cap * dim, 0,
@@ -87,8 +88,12 @@ void RowStore::encode16(const int64_t *d_slots, int64_t cnt, hipStream_t st) {
   if (!f16 || cap == 0) return;
   if (!d_slots) cnt = cap;
   if (cnt <= 0) return;
+  // FLAT L2 centering: tiles hold x - center (one "list"), meta -|x - center|^2
+  const float *ctr = center16 && resid ? center.as<float>() : nullptr;
+  if (ctr) launch_resid_sq(rows.as<float>(), cnt, dim, ctr, nullptr, rsq16.as<float>(), st, d_slots,
+                           rmax_r.as<uint32_t>());
   HIPCHK(hipMemsetAsync(amaxd.p, 0, sizeof(uint32_t), st));
-  launch_absmax(rows.as<float>(), d_slots, cnt, dim, amaxd.as<uint32_t>(), st);
+  launch_absmax(rows.as<float>(), d_slots, cnt, dim, amaxd.as<uint32_t>(), st, ctr, nullptr);
   uint32_t bits = 0;
   HIPCHK(hipMemcpyAsync(&bits, amaxd.p, sizeof(bits), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
@@ -97,12 +102,14 @@ void RowStore::encode16(const int64_t *d_slots, int64_t cnt, hipStream_t st) {
   if (sx == 0.0f || std::max(am, amax) * sx >= 16384.0f) {  // first rows, or a larger row: new scale, all slots
     amax = std::max(am, amax);
     sx = pow2_scale_host(amax);
-    launch_encode16(rows.as<float>(), nullptr, cap, dim, sx, h16.p, st);
-    launch_meta16(nullptr, cap, met16, rsq.as<float>(), live.as<uint8_t>(), meta.as<float>(), st);
+    if (ctr && d_slots)  // every slot is re-encoded: their residual norms too
+      launch_resid_sq(rows.as<float>(), cap, dim, ctr, nullptr, rsq16.as<float>(), st, nullptr, rmax_r.as<uint32_t>());
+    launch_encode16(rows.as<float>(), nullptr, cap, dim, sx, h16.p, st, ctr, nullptr);
+    launch_meta16(nullptr, cap, met16, meta_norms(), live.as<uint8_t>(), meta.as<float>(), st);
   } else {
     amax = std::max(am, amax);
-    launch_encode16(rows.as<float>(), d_slots, cnt, dim, sx, h16.p, st);
-    launch_meta16(d_slots, cnt, met16, rsq.as<float>(), live.as<uint8_t>(), meta.as<float>(), st);
+    launch_encode16(rows.as<float>(), d_slots, cnt, dim, sx, h16.p, st, ctr, nullptr);
+    launch_meta16(d_slots, cnt, met16, meta_norms(), live.as<uint8_t>(), meta.as<float>(), st);
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(st));
@@ -124,6 +131,29 @@ void RowStore::write(const float *x, const int64_t *slots, const int64_t *labs, 
   if (cosine) launch_norms_slots(rows.as<float>(), di, cnt, dim, norms.as<float>(), st);
   launch_sqnorms(rows.as<float>(), di, cnt, dim, rsq.as<float>(), rmax.as<uint32_t>(), st);
   HIPCHK(hipGetLastError());
+  if (f16 && center16 && !resid) {
+    // the first rows written fix the center: their mean (finite values), computed on the host
+    std::vector<double> acc(dim, 0.0);
+    std::vector<int64_t> num(dim, 0);
+    for (int64_t i = 0; i < cnt; i++)
+      for (int d = 0; d < dim; d++) {
+        const float v = x[(size_t)i * dim + d];
+        if (std::isfinite(v)) {
+          acc[d] += v;
+          num[d]++;
+        }
+      }
+    std::vector<float> c(dim);
+    for (int d = 0; d < dim; d++) c[d] = num[d] ? (float)(acc[d] / (double)num[d]) : 0.0f;
+    center.ensure(sizeof(float) * dim);
+    rmax_r.ensure(sizeof(uint32_t));
+    HIPCHK(hipMemcpyAsync(center.p, c.data(), sizeof(float) * dim, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(rmax_r.p, 0, sizeof(uint32_t), st));
+    rsq16.grow_keep(sizeof(float) * cap, 0, st);
+    resid = true;
+    sx = 0.0f;  // encode every slot with the center (first write: the scale is set from these rows)
+    amax = 0.0f;
+  }
   encode16(di, cnt, st);
   HIPCHK(hipStreamSynchronize(st));  // staging buffers are reused by the next call
   if (stage_x.n > (size_t(256) << 20)) stage_x.release();  // bulk loads: do not pin GBs of staging
@@ -450,13 +480,13 @@ static int64_t filter_finish(Workspace &ws, int64_t nq, int nparts, int k1, int 
     r.c_bf = filter_f16_cerr(dim, met, prec);
     r.c_abs = filter_f16_abs(dim, met, rs.sx, prec);
     r.q16 = 1;
-    if (resid_cents && mi && list_rmax) {  // residual tiles: the certificate of filter.hip refine_kernel
+    if (resid_cents && list_rmax && list_rmax_r) {  // residual tiles: the certificate of refine_kernel
       r.resid = 1;
       r.cents = resid_cents;
       r.list_rmax_r = list_rmax_r;
       r.list_rmax = list_rmax;
-      r.probes = mi->probes;
-      r.nprobe = mi->nprobe;
+      r.probes = mi ? mi->probes : nullptr;  // FLAT: one center (list 0)
+      r.nprobe = mi ? mi->nprobe : 1;
     }
   } else {
     r.c_bf = prec == FILTER_BF16X3 ? filter_bf16x3_cerr(dim, met) : 0.0;
@@ -656,6 +686,7 @@ struct FlatIndex : Index {
     st.dim = dim;
     st.cosine = metric == COS;  // norm cached at Add (:146)
     st.f16 = store16(dim, metric);
+    st.center16 = st.f16 && metric == L2;  // fp16 tiles of x - mean (engine.h RowStore)
     st.met16 = metric;
     dp = sq8_dp(dim);
   }
@@ -842,14 +873,17 @@ struct FlatIndex : Index {
     fa.h16 = st.h16.p;
     fa.meta = st.meta.as<float>();
     fa.sx = st.sx;
+    const bool centered = prec16(fa.prec) && st.resid;
+    fa.cents = centered ? st.center.as<float>() : nullptr;
     {
       PhaseTimer t(PH_FLAT_SCAN, ws.st, nq * cutoff);
       if (prec16(fa.prec)) launch_filter16(fa, metric, p.nitems, ws.st);
       else launch_filter(fa, metric, p.nitems, ws.st);
     }
     const int64_t nf =
-        filter_finish(ws, nq, p.nchunks, k1, k, dim, metric, 4, d_q, st, nullptr, d_s, d_l, d_c, nullptr, nullptr,
-                      nullptr, fa.prec);
+        filter_finish(ws, nq, p.nchunks, k1, k, dim, metric, 4, d_q, st, nullptr, d_s, d_l, d_c,
+                      centered ? st.rmax.as<uint32_t>() : nullptr, centered ? st.center.as<float>() : nullptr,
+                      centered ? st.rmax_r.as<uint32_t>() : nullptr, fa.prec);
     const int k1_next = filter_k1_next(k, k1);
     filter_fallback(ws, nf, d_q, dim, k, d_s, d_l, d_c,
                     [&](const float *q2, int64_t n2, float *s2, int64_t *l2, int32_t *c2) {

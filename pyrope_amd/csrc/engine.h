@@ -73,9 +73,12 @@ struct RowStore {
   float sx = 0.0f;
   float amax = 0.0f;
   DevMem h16, meta, amaxd;
-  // IVF lists: the tiles hold residuals x - c[list] (resid), with rsq16 = |x - c|^2 per row for meta
+  // IVF lists: the tiles hold residuals x - c[list] (resid), with rsq16 = |x - c|^2 per row for meta.
+  // FLAT L2 (center16): one center, the mean of the first rows written, fixed from then on; rmax_r =
+  // score_key of the largest |x - center|^2 (the certificate's residual norm bound).
   bool resid = false;
-  DevMem rsq16;
+  bool center16 = false;
+  DevMem rsq16, center, rmax_r;
   const float *meta_norms() const { return resid ? rsq16.as<float>() : rsq.as<float>(); }
   std::vector<int64_t> hlabels;
   std::vector<uint8_t> hlive;

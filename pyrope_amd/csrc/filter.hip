@@ -571,8 +571,10 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
       // IP |R - T| <= g |q| max|x|.  Maxima over this query's probed lists.
       float ar2 = 0.0f, xc2 = 0.0f;
       uint32_t xrk = 0, xfk = 0;
-      for (int p = lane; p < a.nprobe; p += 64) {
-        const int l = a.probes[(size_t)q * a.nprobe + p];
+      // FLAT (no probes): one center, list 0
+      const int np = a.probes ? a.nprobe : 1;
+      for (int p = lane; p < np; p += 64) {
+        const int l = a.probes ? a.probes[(size_t)q * a.nprobe + p] : 0;
         xrk = max(xrk, a.list_rmax_r[l]);
         xfk = max(xfk, a.list_rmax[l]);
         const float *c = a.cents + (size_t)l * D;

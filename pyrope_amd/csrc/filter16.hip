@@ -537,11 +537,12 @@ void launch16_d(const FilterArgs &a, int metric, int max_items, hipStream_t st) 
 // ---- write / build side: fp16 tiles, per-row meta, the store's |x| maximum ----
 
 // h16 tile element of (row r, dim d): tile r/32, k-step d/16, half (d/8)&1, row r%32, d%8
-// residual mode: cents (row-major) and tile_list (list id of each 32-row tile) -> x - c[list]
+// residual mode: cents (row-major) and tile_list (list id of each 32-row tile; null = every tile
+// list 0, the FLAT store's single center) -> x - c[list]
 __device__ __forceinline__ float resid_val(const float *rows, const float *cents, const int32_t *tile_list, int64_t r,
                                            int d, int D) {
   const float x = rows[((size_t)(r >> 3) * D + d) * 8 + (r & 7)];
-  return cents ? x - cents[(size_t)tile_list[r >> 5] * D + d] : x;
+  return cents ? x - cents[(size_t)(tile_list ? tile_list[r >> 5] : 0) * D + d] : x;
 }
 
 __global__ void encode16_kernel(const float *rows, const int64_t *slots, int64_t n, int D, float sx,
@@ -582,17 +583,20 @@ __global__ void absmax_kernel(const float *rows, const int64_t *slots, int64_t n
   atomicMax(out, __float_as_uint(m));
 }
 
-// |x - c[list]|^2 per row (fp32, any order: the certificate budgets its rounding)
-__global__ void resid_sq_kernel(const float *rows, int64_t n, int D, const float *cents, const int32_t *tile_list,
-                                float *out) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n) return;
+// |x - c[list]|^2 per row (fp32, any order: the certificate budgets its rounding) of rows [0, n) or
+// of the n rows at slots; out_max (may be null): atomic max of the finite values' score keys
+__global__ void resid_sq_kernel(const float *rows, const int64_t *slots, int64_t n, int D, const float *cents,
+                                const int32_t *tile_list, float *out, uint32_t *out_max) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t r = slots ? slots[i] : i;
   float s = 0.0f;
   for (int d = 0; d < D; ++d) {
     const float v = resid_val(rows, cents, tile_list, r, d, D);
     s += v * v;
   }
   out[r] = s;
+  if (out_max && isfinite(s)) atomicMax(out_max, score_key(s));
 }
 
 }  // namespace
@@ -622,9 +626,10 @@ void launch_encode16(const float *rows, const int64_t *slots, int64_t n, int32_t
 }
 
 void launch_resid_sq(const float *rows, int64_t n, int32_t dim, const float *cents, const int32_t *tile_list,
-                     float *out, hipStream_t st) {
+                     float *out, hipStream_t st, const int64_t *slots, uint32_t *out_max) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(resid_sq_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, rows, n, dim, cents, tile_list, out);
+  hipLaunchKernelGGL(resid_sq_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, rows, slots, n, dim, cents, tile_list,
+                     out, out_max);
 }
 
 void launch_meta16(const int64_t *slots, int64_t n, int32_t metric, const float *rsq, const uint8_t *live, float *meta,

@@ -338,7 +338,7 @@ void launch_encode16(const float *rows, const int64_t *slots, int64_t n, int32_t
                      hipStream_t st, const float *cents = nullptr, const int32_t *tile_list = nullptr);
 // |x - c[list]|^2 of rows [0, n)
 void launch_resid_sq(const float *rows, int64_t n, int32_t dim, const float *cents, const int32_t *tile_list,
-                     float *out, hipStream_t st);
+                     float *out, hipStream_t st, const int64_t *slots = nullptr, uint32_t *out_max = nullptr);
 // meta[r] = live ? (L2 ? -rsq : 0) : -inf for slots[i] (or rows [0, n))
 void launch_meta16(const int64_t *slots, int64_t n, int32_t metric, const float *rsq, const uint8_t *live, float *meta,
                    hipStream_t st);

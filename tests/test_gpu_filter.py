@@ -78,6 +78,34 @@ def test_flat_filter_equals_exact_and_oracle(hiplib, oracle, metric, dim, prec):
     assert nfb < len(q)  # the certificate holds for (almost) every query of uniform data
 
 
+def test_flat_l2_centered_tiles_offset_data(hiplib, oracle):
+    """FLAT L2 fp16 tiles hold x - center (the first batch's mean; engine.h RowStore::center16): data
+    sitting far from the origin keeps its fp16 error (and the certificate) at the spread's scale, so
+    almost no query re-runs; rows added later with another distribution and deletes stay exact."""
+    from pyrope_amd import generate_synthetic
+    d = 128
+    x = (100.0 + generate_synthetic(20000, d, 42)).astype(np.float32)
+    q = (100.0 + generate_synthetic(200, d, 1337)).astype(np.float32)
+    idx = _flat(d, 0, x)
+    got, nfb = _fallbacks(hiplib, lambda: idx.search_batch(q, 10))
+    with _env(PYR_FILTER=0):
+        ref = idx.search_batch(q, 10)
+    _same(got, ref)
+    for i in range(0, len(q), 29):
+        os_, ok = oracle.bf_search(x, None, 0, q[i], 10)
+        np.testing.assert_array_equal(got[1][i], ok)
+        assert np.array_equal(got[0][i].view(np.uint32), os_.view(np.uint32))
+    assert nfb <= len(q) // 20, nfb
+    # later rows off the first batch's center, and deletes: still bit-identical to the exact scan
+    x2 = (103.0 + 2.0 * generate_synthetic(5000, d, 7)).astype(np.float32)
+    idx.add_labels(np.arange(20000, 25000, dtype=np.int64), x2)
+    idx.delete_many([str(i) for i in range(0, 25000, 11)])
+    got = idx.search_batch(q, 10)
+    with _env(PYR_FILTER=0):
+        ref = idx.search_batch(q, 10)
+    _same(got, ref)
+
+
 @pytest.mark.parametrize("prec,waves", [("2", "4"), ("3", "4"), ("1", "8"), ("1", "4"), ("0", "4")])  # PREC, WAVES
 @pytest.mark.parametrize("metric", [0, 1])
 def test_ivf_filter_equals_exact_and_oracle(hiplib, oracle, metric, prec, waves):
