@@ -94,6 +94,17 @@ pyr_status pyr_index_build(pyr_index *index);
  * KMeansUtils.Train output; the multi-GPU path uses it so every shard shares one quantizer. */
 pyr_status pyr_index_set_centroids(pyr_index *index, const float *centroids, int32_t nlist);
 
+/* IVF_PQ: supply trained ProductQuantizer codebooks (m x ksub x dim/m, ProductQuantizer._centroids,
+ * ProductQuantizer.cs:7-8) together with pyr_index_set_centroids; the next Build then only assigns
+ * and encodes (Encode, :60-80), streaming the buffer in chunks -- what a 50M x 768 build needs
+ * (training on every row is the reference's behaviour when no quantizer is supplied). */
+pyr_status pyr_index_set_codebooks(pyr_index *index, const float *codebooks, int32_t m, int32_t ksub);
+
+/* Capacity hint: room for `rows` more rows (FLAT slots / IVF buffer) without re-allocation.  The
+ * .NET collections the reference fills grow by copying; a device store of 10^8 rows cannot hold the
+ * old and the new copy at once, so bulk loaders reserve first.  No effect on results. */
+pyr_status pyr_index_reserve(pyr_index *index, int64_t rows);
+
 /* KMeansUtils.Train (KMeansUtils.cs:10-68) on the GPU, reference-identical: OrderBy(rnd.Next())
  * initialisation, <= max_iter Lloyd iterations, member sums in data order, ArraysEqual(1e-6) stop.
  * data: n x dim host row-major.  out: k x dim (k clamped to [1, n]); *k_out = k used. */

@@ -107,6 +107,8 @@ SIGNATURES = {
     "pyr_generate_synthetic": (C.c_int, [C.c_int64, C.c_int32, C.c_int32, _f]),
     "pyr_generate_synthetic_blocked": (C.c_int, [C.c_int64, C.c_int64, C.c_int32, C.c_int32, C.c_int64, _f]),
     "pyr_index_set_centroids": (C.c_int, [_vp, _f, C.c_int32]),
+    "pyr_index_set_codebooks": (C.c_int, [_vp, _f, C.c_int32, C.c_int32]),
+    "pyr_index_reserve": (C.c_int, [_vp, C.c_int64]),
     "pyr_kmeans_train": (C.c_int, [C.c_int32, _f, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                    _f, _i32]),
     "pyr_profile_enable": (None, [C.c_int32]),

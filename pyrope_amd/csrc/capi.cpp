@@ -165,6 +165,23 @@ pyr_status pyr_index_set_centroids(pyr_index *index, const float *centroids, int
   });
 }
 
+pyr_status pyr_index_set_codebooks(pyr_index *index, const float *codebooks, int32_t m, int32_t ksub) {
+  if (!index || !codebooks) return fail(PYR_E_ARG, "null argument");
+  return guard([&] {
+    std::unique_lock<std::shared_mutex> g(index->impl->mu);
+    index->impl->set_codebooks(codebooks, m, ksub);
+  });
+}
+
+pyr_status pyr_index_reserve(pyr_index *index, int64_t rows) {
+  if (!index || rows < 0) return fail(PYR_E_ARG, "bad argument");
+  return guard([&] {
+    HIPCHK(hipSetDevice(index->impl->device));
+    std::unique_lock<std::shared_mutex> g(index->impl->mu);
+    index->impl->reserve(rows);
+  });
+}
+
 pyr_status pyr_kmeans_train(int32_t device, const float *data, int64_t n, int32_t dim, int32_t k, int32_t metric,
                             int32_t max_iter, int32_t seed, float *out, int32_t *k_out) {
   if (!data || !out || n < 0 || dim <= 0) return fail(PYR_E_ARG, "bad argument");

@@ -11,6 +11,7 @@
 #include <cstdio>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <numeric>
 
@@ -692,6 +693,10 @@ struct FlatIndex : Index {
   }
 
   void set_quantization(bool on) override { quant = on; }
+  void reserve(int64_t rows) override {
+    st.reserve(st.n + rows, wst);
+    slot_of.reserve(slot_of.size() + (size_t)rows);
+  }
 
   void q8_reserve() {
     if (q8cap >= st.cap) return;
@@ -1010,6 +1015,12 @@ struct DictBuffer {
     return true;
   }
   int64_t live_count() const { return (int64_t)slot_of.size(); }
+  void reserve(int64_t rows, hipStream_t wst) {
+    st.reserve(st.n + rows, wst);
+    slot_of.reserve(slot_of.size() + (size_t)rows);
+    st.hlabels.reserve(st.n + rows);
+    st.hlive.reserve(st.n + rows);
+  }
   // slot cutoff after the first `m` live slots (m < 0: all)
   int64_t cutoff(int64_t m) const {
     if (m < 0 || m >= live_count()) return st.n;
@@ -1224,6 +1235,7 @@ struct IvfFlatIndex : Index {
   DevMem dlb, dle, dllive;
   DevMem dlmax;                           // per-list max |x|^2 (score_key): refine certificate bound
   DevMem dlmax_r;                         // per-list max |x - c|^2 (residual fp16 tiles)
+  void reserve(int64_t rows) override { buf.reserve(rows, wst); }
   Coarse coarse;
   bool built = false;                     // _isBuilt (:20)
   int nprobe_default;
@@ -1830,6 +1842,15 @@ struct IvfPqIndex : Index {
     given.assign(c, c + (size_t)nl * dim);
     given_k = nl;
   }
+  std::vector<float> given_cb;  // pyr_index_set_codebooks: [M][ksub][sub]
+  int given_ksub = 0;
+  void set_codebooks(const float *c, int m, int ks) override {
+    if (m != M) throw Error(PYR_E_ARG, "codebooks have " + std::to_string(m) + " subspaces, the index " + std::to_string(M));
+    if (ks <= 0 || ks > 256) throw Error(PYR_E_ARG, "K must be <= 256 for byte encoding");
+    given_cb.assign(c, c + (size_t)m * ks * sub);
+    given_ksub = ks;
+  }
+  void reserve(int64_t rows) override { buf.reserve(rows, wst); }
 
   explicit IvfPqIndex(const pyr_index_desc &d) : Index(d) {
     M = d.pq_m;
@@ -1885,6 +1906,10 @@ struct IvfPqIndex : Index {
       }
     const int64_t n = (int64_t)slots.size();
     if (n == 0) return;                               // :65
+    if (given_k > 0 && given_ksub > 0) {
+      build_given(slots, labs);
+      return;
+    }
     DevMem X, ds;
     X.ensure(sizeof(float) * n * dim);
     ds.ensure(sizeof(int64_t) * n);
@@ -1925,6 +1950,52 @@ struct IvfPqIndex : Index {
     HIPCHK(hipStreamSynchronize(wst));
     commit_codes(codes_rm.as<uint8_t>(), n, asg, labs, C.as<float>(), nc);
     buf.clear(wst);                                    // :109
+    built = true;
+  }
+
+  // Build with a supplied quantizer and codebooks (pyr_index_set_centroids + set_codebooks): the
+  // assignment (:79, FindNearestCentroid) and Encode (:99-107) of every buffer row, in chunks of
+  // ~1 GiB of gathered rows, so a buffer of 10^8 rows needs no second full copy (nor residuals).
+  void build_given(const std::vector<int64_t> &slots, const std::vector<int64_t> &labs) {
+    const int64_t n = (int64_t)slots.size();
+    const int nc = given_k;
+    DevMem C;
+    C.ensure(sizeof(float) * nc * dim);
+    HIPCHK(hipMemcpyAsync(C.p, given.data(), sizeof(float) * nc * dim, hipMemcpyHostToDevice, wst));
+    ksub = given_ksub;
+    cb.ensure(sizeof(float) * (size_t)M * ksub * sub);
+    HIPCHK(hipMemcpyAsync(cb.p, given_cb.data(), sizeof(float) * given_cb.size(), hipMemcpyHostToDevice, wst));
+    DevMem codes_rm, A, X, ds;
+    codes_rm.ensure((size_t)n * M);
+    A.ensure(sizeof(int32_t) * n);
+    int64_t chunk = std::max<int64_t>(1024, (int64_t(1) << 30) / ((int64_t)dim * 4));
+    if (const char *e = getenv("PYR_PQ_BUILD_CHUNK")) chunk = std::max<int64_t>(1, atoll(e));  // tests
+    X.ensure(sizeof(float) * std::min(chunk, n) * dim);
+    ds.ensure(sizeof(int64_t) * std::min(chunk, n));
+    const bool progress = getenv("PYR_PROGRESS") && atoi(getenv("PYR_PROGRESS")) != 0;  // long bulk builds
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int64_t off = 0; off < n; off += chunk) {
+      if (progress && (off / chunk) % 8 == 0) {
+        const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        fprintf(stderr, "[pyrope] IVF_PQ build: %lld / %lld rows assigned + encoded (%.1fs)\n", (long long)off,
+                (long long)n, s);
+        fflush(stderr);
+      }
+      const int64_t cn = std::min(chunk, n - off);
+      HIPCHK(hipMemcpyAsync(ds.p, slots.data() + off, sizeof(int64_t) * cn, hipMemcpyHostToDevice, wst));
+      launch_gather_blocked(buf.st.rows.as<float>(), ds.as<int64_t>(), cn, dim, X.as<float>(), wst);
+      assign_gpu(X.as<float>(), cn, dim, C.as<float>(), nc, metric, A.as<int32_t>() + off, wst);
+      launch_pq_encode(X.as<float>(), A.as<int32_t>() + off, C.as<float>(), cn, dim, M, ksub, cb.as<float>(),
+                       codes_rm.as<uint8_t>() + (size_t)off * M, wst);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipStreamSynchronize(wst));
+    }
+    X.release();
+    std::vector<int32_t> asg(n);
+    HIPCHK(hipMemcpyAsync(asg.data(), A.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, wst));
+    HIPCHK(hipStreamSynchronize(wst));
+    commit_codes(codes_rm.as<uint8_t>(), n, asg, labs, C.as<float>(), nc);
+    buf.clear(wst);
     built = true;
   }
 

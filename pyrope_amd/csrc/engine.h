@@ -186,6 +186,15 @@ struct Index {
     (void)nlist;
     throw Error(PYR_E_STATE, "index kind has no coarse quantizer");
   }
+  virtual void set_codebooks(const float *cb, int m, int ksub) {
+    (void)cb;
+    (void)m;
+    (void)ksub;
+    throw Error(PYR_E_STATE, "index kind has no product quantizer");
+  }
+  // capacity hint: room for `rows` more rows without re-allocation (bulk loads of 10^7-10^8 rows,
+  // where a grow-by-copy would need the old and the new store at once)
+  virtual void reserve(int64_t rows) { (void)rows; }
 
   std::unique_ptr<Workspace> take_ws();
   void give_ws(std::unique_ptr<Workspace> w);

@@ -258,6 +258,10 @@ class HipVectorIndex(IVectorIndex):
         c = np.ascontiguousarray(centroids, dtype=np.float32).reshape(-1, self.dimension)
         check(self._L.pyr_index_set_centroids(self._h, ptr(c, C.c_float), c.shape[0]))
 
+    def reserve(self, rows: int) -> None:
+        """Capacity hint for a bulk load of `rows` more rows (pyr_index_reserve); results unchanged."""
+        check(self._L.pyr_index_reserve(self._h, int(rows)))
+
     def get_stats(self) -> IndexStats:
         cnt = C.c_int64()
         check(self._L.pyr_index_stats(self._h, C.byref(cnt), None, None))
@@ -403,6 +407,14 @@ class IvfPqVectorIndex(HipVectorIndex):
         codes = np.zeros((len(labels), self.m), np.uint8)
         check(self._L.pyr_index_pq_state(self._h, ptr(cb, C.c_float), C.byref(ks), ptr(codes, C.c_uint8)))
         return cb, codes, off, labels, live
+
+    def set_codebooks(self, codebooks: np.ndarray) -> None:
+        """Supply trained ProductQuantizer codebooks (m x ksub x dim/m) with set_centroids(); the next
+        build() then assigns and encodes only, streaming the buffer (pyr_index_set_codebooks)."""
+        cb = np.ascontiguousarray(codebooks, dtype=np.float32)
+        if cb.ndim != 3 or cb.shape[0] != self.m or cb.shape[2] != self.dimension // self.m:
+            raise ArgumentException("codebooks must be m x ksub x dimension/m")
+        check(self._L.pyr_index_set_codebooks(self._h, ptr(cb, C.c_float), cb.shape[0], cb.shape[1]))
 
 
 class DeltaVectorIndex(IVectorIndex, ICentroidsProvider):

@@ -82,6 +82,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--check", type=int, default=20, help="queries compared with the CPU oracle")
+    ap.add_argument("--train-rows", type=int, default=0,
+                    help="ivfpq: train the quantizers on the first N rows and stream the rest (0 = all rows)")
     ap.add_argument("--cpu-seconds", type=float, default=0.0,
                     help="flat: also time the CPU restatement (oracle, one query per thread, every usable CPU)")
     ap.add_argument("--sweep", default="", help="env settings run one after another on the same index, "
@@ -159,11 +161,38 @@ def main():
                "parity_sample": {"queries": a.check, "ids_and_bits_equal": ok}, "cpu_baseline": cpu}
     else:
         n, d = a.n or 3_200_000, a.dim or 768
-        x = generate_synthetic(n, d, 42)
+        from pyrope_amd import generate_synthetic_blocked
         qh = generate_synthetic(a.nq, d, 1337)
         t = time.time()
-        idx = IvfPqVectorIndex(d, a.metric, m=a.m, k=256, n_list=a.nlist)
-        idx.add_labels(np.arange(n, dtype=np.int64), x)
+        if a.train_rows > 0 and a.train_rows < n:
+            # P1 at full size: train the coarse quantizer and the codebooks on the first train_rows rows
+            # (reference-identical training on that sample), then stream every row into an index that
+            # only assigns and encodes (set_centroids + set_codebooks, IvfPqIndex::build_given)
+            xs = generate_synthetic_blocked(0, a.train_rows, d, 42)
+            tr = IvfPqVectorIndex(d, a.metric, m=a.m, k=256, n_list=a.nlist)
+            tr.add_labels(np.arange(a.train_rows, dtype=np.int64), xs, track_ids=False)
+            tr.build()
+            cents = tr.centroids_array()
+            cb0 = tr.pq_state()[0]
+            tr.close()
+            del xs
+            log(f"trained quantizers on {a.train_rows} rows in {time.time() - t:.1f}s")
+            idx = IvfPqVectorIndex(d, a.metric, m=a.m, k=256, n_list=a.nlist)
+            idx.set_centroids(cents)
+            idx.set_codebooks(cb0)
+            idx.reserve(n)
+            step_rows = 1 << 20
+            for r0 in range(0, n, step_rows):
+                cn = min(step_rows, n - r0)
+                idx.add_labels(np.arange(r0, r0 + cn, dtype=np.int64), generate_synthetic_blocked(r0, cn, d, 42),
+                               track_ids=False)
+                if (r0 // step_rows) % 8 == 0:
+                    log(f"added {r0 + cn} rows ({time.time() - t:.1f}s)")
+            x = None
+        else:
+            x = generate_synthetic(n, d, 42)
+            idx = IvfPqVectorIndex(d, a.metric, m=a.m, k=256, n_list=a.nlist)
+            idx.add_labels(np.arange(n, dtype=np.int64), x)
         idx.build()
         log(f"built IVF_PQ n={n} d={d} nlist={a.nlist} m={a.m} in {time.time() - t:.1f}s")
         q = torch.from_numpy(qh).cuda()
@@ -177,12 +206,38 @@ def main():
             os_, ok_ = oracle.ivfpq_search(qh[i], a.k, cents, codes, off, cb, live, metric=a.metric, nprobe=a.nprobe)
             ok &= bool(np.array_equal(lab[i], labels[ok_]) and np.array_equal(s[i].view(np.uint32),
                                                                                os_.view(np.uint32)))
+        cpu = None
+        if a.cpu_seconds > 0:  # CPU baseline leg: the oracle's IvfPq search, one query per thread
+            from concurrent.futures import ThreadPoolExecutor
+            from bench import host_cpus
+            host = host_cpus()
+            th = host["usable"]
+
+            def one(i):
+                return oracle.ivfpq_search(qh[i], a.k, cents, codes, off, cb, live, metric=a.metric, nprobe=a.nprobe)
+            S = th
+            with ThreadPoolExecutor(th) as ex:
+                t1 = time.perf_counter()
+                list(ex.map(one, range(S)))
+                S = int(min(a.nq, max(S, S * a.cpu_seconds / max(time.perf_counter() - t1, 1e-3))))
+                t1 = time.perf_counter()
+                res = list(ex.map(one, range(S)))
+                ct = time.perf_counter() - t1
+            ids_eq = all(np.array_equal(lab[i], labels[r[1]]) for i, r in enumerate(res))
+            bits_eq = all(np.array_equal(s[i].view(np.uint32), r[0].view(np.uint32)) for i, r in enumerate(res))
+            cpu = {"value": S / ct, "unit": "queries/s", "cores": th, "kind": "port", "host": host,
+                   "sample": f"{S} of the {a.nq} queries (oracle/oracle.c IvfPq search, one query per thread)",
+                   "parity": {"queries": S, "ids_equal": bool(ids_eq), "scores_bit_identical": bool(bits_eq)}}
+            log(f"cpu baseline {S / ct:,.1f} QPS on {th} threads")
         scan = phases.get("pq_scan", {"ms": float("nan"), "work": 0})
         out = {"workload": f"IVF_PQ d={d} N={n} nlist={a.nlist} m={a.m} k=256 nprobe={a.nprobe} Q={a.nq}",
+               "training": (f"coarse k-means + codebooks trained (reference-identical) on the first {a.train_rows} "
+                            f"rows, every row assigned + encoded" if 0 < a.train_rows < n else "all rows"),
                "qps": qps, "ms_per_step": ms, "phases_ms": {k_: v["ms"] for k_, v in phases.items()},
                "scan_rows": scan["work"],
                "lookups_per_s": scan["work"] * a.m / (scan["ms"] * 1e-3),
-               "parity_sample": {"queries": a.check, "ids_and_bits_equal": ok}}
+               "code_bytes_GBps": scan["work"] * a.m / (scan["ms"] * 1e-3) / 1e9,
+               "parity_sample": {"queries": a.check, "ids_and_bits_equal": ok}, "cpu_baseline": cpu}
     print(json.dumps(out), flush=True)
 
 

@@ -167,3 +167,39 @@ def test_pq_adc_ties_and_deletes(hiplib, oracle):
         ref = idx.search_batch(q, 20, opts)
     _same(got, ref)
     assert not np.any(np.isin(got[1], shadow))
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_pq_build_with_given_quantizers_streams_identically(hiplib, oracle, metric):
+    """set_centroids + set_codebooks (the P1 bulk path, engine.cpp IvfPqIndex::build_given): the
+    build only assigns and encodes, in chunks (forced to 700 rows here), and must give the same lists,
+    codes and search results as the reference build that trained those quantizers."""
+    import os
+    from pyrope_amd import IvfPqVectorIndex, SearchOptions, generate_synthetic
+    ref, x = _build(64, metric, 4096, 32, 8)
+    cents = ref.centroids_array()
+    cb, codes, off, labels, live = ref.pq_state()
+    idx = IvfPqVectorIndex(64, metric, m=8, k=256, n_list=32)
+    idx.set_centroids(cents)
+    idx.set_codebooks(cb)
+    idx.reserve(len(x))
+    for a in range(0, len(x), 1000):  # bulk load in several calls
+        idx.add_labels(np.arange(a, min(a + 1000, len(x)), dtype=np.int64), x[a:a + 1000])
+    os.environ["PYR_PQ_BUILD_CHUNK"] = "700"
+    try:
+        idx.build()
+    finally:
+        os.environ.pop("PYR_PQ_BUILD_CHUNK", None)
+    gcb, gcodes, goff, glabels, glive = idx.pq_state()
+    assert np.array_equal(gcb.view(np.uint32), cb.view(np.uint32))
+    np.testing.assert_array_equal(goff, off)
+    np.testing.assert_array_equal(glabels, labels)
+    np.testing.assert_array_equal(gcodes, codes)
+    q = generate_synthetic(32, 64, 1337)
+    opts = SearchOptions(nprobe=4)
+    s1, l1, c1 = ref.search_batch(q, 10, opts)
+    s2, l2, c2 = idx.search_batch(q, 10, opts)
+    np.testing.assert_array_equal(l1, l2)
+    assert np.array_equal(s1.view(np.uint32), s2.view(np.uint32))
+    with pytest.raises(Exception):
+        idx.set_codebooks(cb[:4])  # wrong subspace count
