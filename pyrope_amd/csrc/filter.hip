@@ -676,10 +676,11 @@ __global__ void scatter_results_kernel(const int32_t *qidx, int64_t n, int k, co
 }
 
 __global__ void gather_queries_kernel(const float *q, const int32_t *qidx, int64_t n, int D, float *out) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n * D) return;
-  const int64_t i = e / D;
-  out[e] = q[(size_t)qidx[i] * D + e % D];
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * D;
+       e += (int64_t)gridDim.x * blockDim.x) {  // grid-stride: grids stay below 2^32 work-items
+    const int64_t i = e / D;
+    out[e] = q[(size_t)qidx[i] * D + e % D];
+  }
 }
 
 // |x|^2 of blocked rows (slots[i], or i when slots is null) and the running maximum
@@ -790,7 +791,7 @@ void launch_refine(const RefineArgs &a, int metric, int V, hipStream_t st) {
 
 void launch_gather_queries(const float *q, const int32_t *qidx, int64_t n, int32_t dim, float *out, hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(gather_queries_kernel, dim3(nblk(n * dim, 256)), dim3(256), 0, st, q, qidx, n, dim, out);
+  hipLaunchKernelGGL(gather_queries_kernel, dim3(gblk(n * dim)), dim3(256), 0, st, q, qidx, n, dim, out);
 }
 
 void launch_scatter_results(const int32_t *qidx, int64_t n, int32_t k, const float *ss, const int64_t *sl,

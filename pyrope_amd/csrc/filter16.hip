@@ -547,17 +547,18 @@ __device__ __forceinline__ float resid_val(const float *rows, const float *cents
 
 __global__ void encode16_kernel(const float *rows, const int64_t *slots, int64_t n, int D, float sx,
                                 const float *cents, const int32_t *tile_list, _Float16 *h16) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (row, 8-dim group)
   const int G = D / 8;
-  if (e >= n * G) return;
-  const int64_t i = e / G;
-  const int g = (int)(e % G);
-  const int64_t r = slots ? slots[i] : i;
-  h8v v;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = (_Float16)(resid_val(rows, cents, tile_list, r, 8 * g + j, D) * sx);
-  const size_t off = (((size_t)(r >> 5) * (D / 16) + (g >> 1)) * 2 + (g & 1)) * 32 + (r & 31);
-  *reinterpret_cast<h8v *>(h16 + off * 8) = v;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * G;
+       e += (int64_t)gridDim.x * blockDim.x) {  // grid-stride: grids stay below 2^32 work-items
+    const int64_t i = e / G;
+    const int g = (int)(e % G);
+    const int64_t r = slots ? slots[i] : i;
+    h8v v;
+  #pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (_Float16)(resid_val(rows, cents, tile_list, r, 8 * g + j, D) * sx);
+    const size_t off = (((size_t)(r >> 5) * (D / 16) + (g >> 1)) * 2 + (g & 1)) * 32 + (r & 31);
+    *reinterpret_cast<h8v *>(h16 + off * 8) = v;
+  }
 }
 
 // meta[r] = live ? (L2 ? -|x|^2 : 0) : -inf
@@ -621,7 +622,7 @@ void launch_filter16(const FilterArgs &a, int metric, int max_items, hipStream_t
 void launch_encode16(const float *rows, const int64_t *slots, int64_t n, int32_t dim, float sx, void *h16,
                      hipStream_t st, const float *cents, const int32_t *tile_list) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(encode16_kernel, dim3(nblk(n * (dim / 8), 256)), dim3(256), 0, st, rows, slots, n, dim, sx, cents,
+  hipLaunchKernelGGL(encode16_kernel, dim3(gblk(n * (dim / 8))), dim3(256), 0, st, rows, slots, n, dim, sx, cents,
                      tile_list, reinterpret_cast<_Float16 *>(h16));
 }
 

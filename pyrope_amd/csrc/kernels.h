@@ -35,6 +35,13 @@ constexpr int MAX_PARTS = 1024;            // partial lists merged per query
 // QCHUNK queries.  If the launch has a qlist, the queries' partial slots are
 // qlist[qbeg .. qbeg+qcnt) + part (IVF: part = row chunk of the list); otherwise
 // query = qbeg + i and slot = query * nparts + part.
+// blocks of 256 threads for a grid-stride element loop over n items: capped at 2^22 blocks, since a
+// dispatch's grid is a 32-bit work-item count (n x dim of 10^8 rows is far past it)
+inline unsigned gblk(int64_t n) {
+  const int64_t b = (n + 255) / 256;
+  return (unsigned)(b < (int64_t(1) << 22) ? b : (int64_t(1) << 22));
+}
+
 struct ScanItem {
   int32_t row_begin;  // multiple of 8
   int32_t row_end;

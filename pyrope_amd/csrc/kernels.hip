@@ -592,12 +592,13 @@ __global__ void flat_items_kernel(ScanItem *items, int32_t *n_items, int nchunks
 
 // queries row-major -> lane-major: qt[q][l][t] = q[q][8t + l] (fast-scan register layout)
 __global__ void transpose_queries_kernel(const float *q, int64_t nq, int D, float *qt) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= nq * D) return;
-  const int64_t i = e / D;
-  const int r = (int)(e % D);
-  const int T = D / 8, l = r / T, t = r % T;
-  qt[e] = q[(size_t)i * D + 8 * t + l];
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nq * D;
+       e += (int64_t)gridDim.x * blockDim.x) {  // grid-stride: grids stay below 2^32 work-items
+    const int64_t i = e / D;
+    const int r = (int)(e % D);
+    const int T = D / 8, l = r / T, t = r % T;
+    qt[e] = q[(size_t)i * D + 8 * t + l];
+  }
 }
 
 __global__ void norms_kernel(const float *x, int64_t n, int dim, int blocked, float *out) {
@@ -1268,97 +1269,106 @@ __global__ __launch_bounds__(NT) void pq_adc4_kernel(PqArgs a) {
 
 __global__ void pq_encode_kernel(const float *x, const int32_t *assign, const float *cents, int64_t n, int D, int M,
                                  int ksub, const float *cb, uint8_t *codes) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n * M) return;
-  const int64_t i = e / M;
-  const int m = (int)(e % M);
-  const int sub = D / M;
-  const float *xs = x + (size_t)i * D + (size_t)m * sub;
-  const float *cs = cents + (size_t)assign[i] * D + (size_t)m * sub;
-  struct R {
-    const float *x, *c;
-    __device__ float operator()(int d) const { return x[d] - c[d]; }
-  };
-  float mind = FLT_MAX;
-  int best = 0;
-  for (int j = 0; j < ksub; ++j) {  // ProductQuantizer.cs:124-134
-    const float d = em_l2sq_unsafe(R{xs, cs}, Off{cb + ((size_t)m * ksub + j) * sub}, sub);
-    if (d < mind) {
-      mind = d;
-      best = j;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * M;
+       e += (int64_t)gridDim.x * blockDim.x) {  // grid-stride: grids stay below 2^32 work-items
+    const int64_t i = e / M;
+    const int m = (int)(e % M);
+    const int sub = D / M;
+    const float *xs = x + (size_t)i * D + (size_t)m * sub;
+    const float *cs = cents + (size_t)assign[i] * D + (size_t)m * sub;
+    struct R {
+      const float *x, *c;
+      __device__ float operator()(int d) const { return x[d] - c[d]; }
+    };
+    float mind = FLT_MAX;
+    int best = 0;
+    for (int j = 0; j < ksub; ++j) {  // ProductQuantizer.cs:124-134
+      const float d = em_l2sq_unsafe(R{xs, cs}, Off{cb + ((size_t)m * ksub + j) * sub}, sub);
+      if (d < mind) {
+        mind = d;
+        best = j;
+      }
     }
+    codes[i * M + m] = (uint8_t)best;
   }
-  codes[i * M + m] = (uint8_t)best;
 }
 
 __global__ void residuals_kernel(const float *x, const int32_t *assign, const float *cents, int64_t n, int D,
                                  float *out) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n * D) return;
-  const int64_t i = e / D;
-  const int d = (int)(e % D);
-  out[e] = x[e] - cents[(size_t)assign[i] * D + d];
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * D;
+       e += (int64_t)gridDim.x * blockDim.x) {  // grid-stride: grids stay below 2^32 work-items
+    const int64_t i = e / D;
+    const int d = (int)(e % D);
+    out[e] = x[e] - cents[(size_t)assign[i] * D + d];
+  }
 }
 
 __global__ void extract_sub_kernel(const float *x, int64_t n, int D, int off, int sub, float *out) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n * sub) return;
-  const int64_t i = e / sub;
-  const int d = (int)(e % sub);
-  out[e] = x[(size_t)i * D + off + d];
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * sub;
+       e += (int64_t)gridDim.x * blockDim.x) {  // grid-stride: grids stay below 2^32 work-items
+    const int64_t i = e / sub;
+    const int d = (int)(e % sub);
+    out[e] = x[(size_t)i * D + off + d];
+  }
 }
 
 __global__ void pack_codes_kernel(const uint8_t *codes, const int64_t *src, int64_t ndst, int M, uint8_t *out) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int nch = (M + 15) / 16;
-  if (e >= ndst * nch * 16) return;
-  const int64_t r = e / (nch * 16);
-  const int m = (int)(e % (nch * 16));
-  const int64_t s = src[r];
-  const uint8_t v = (s >= 0 && m < M) ? codes[(size_t)s * M + m] : 0;
-  out[pq_code_off(r, m >> 4, nch) + (m & 15)] = v;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < ndst * nch * 16;
+       e += (int64_t)gridDim.x * blockDim.x) {  // grid-stride: grids stay below 2^32 work-items
+    const int64_t r = e / (nch * 16);
+    const int m = (int)(e % (nch * 16));
+    const int64_t s = src[r];
+    const uint8_t v = (s >= 0 && m < M) ? codes[(size_t)s * M + m] : 0;
+    out[pq_code_off(r, m >> 4, nch) + (m & 15)] = v;
+  }
 }
 
 // ---------------------------------------------------------------------------
 // layout helpers
 // ---------------------------------------------------------------------------
 __global__ void to_blocked_kernel(const float *src, const int64_t *sidx, int64_t n, int D, float *dst, int64_t r0) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n * D) return;
-  const int64_t i = e / D;
-  const int d = (int)(e % D);
-  const int64_t s = sidx ? sidx[i] : i;
-  dst[blk_off(r0 + i, d, D)] = s >= 0 ? src[(size_t)s * D + d] : 0.0f;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * D;
+       e += (int64_t)gridDim.x * blockDim.x) {  // grid-stride: grids stay below 2^32 work-items
+    const int64_t i = e / D;
+    const int d = (int)(e % D);
+    const int64_t s = sidx ? sidx[i] : i;
+    dst[blk_off(r0 + i, d, D)] = s >= 0 ? src[(size_t)s * D + d] : 0.0f;
+  }
 }
 __global__ void scatter_blocked_kernel(const float *src, const int64_t *slots, int64_t n, int D, float *dst) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n * D) return;
-  const int64_t i = e / D;
-  const int d = (int)(e % D);
-  dst[blk_off(slots[i], d, D)] = src[e];
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * D;
+       e += (int64_t)gridDim.x * blockDim.x) {  // grid-stride: grids stay below 2^32 work-items
+    const int64_t i = e / D;
+    const int d = (int)(e % D);
+    dst[blk_off(slots[i], d, D)] = src[e];
+  }
 }
 __global__ void gather_blocked_kernel(const float *src, const int64_t *slots, int64_t n, int D, float *out) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n * D) return;
-  const int64_t i = e / D;
-  const int d = (int)(e % D);
-  out[e] = src[blk_off(slots[i], d, D)];
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * D;
+       e += (int64_t)gridDim.x * blockDim.x) {  // grid-stride: grids stay below 2^32 work-items
+    const int64_t i = e / D;
+    const int d = (int)(e % D);
+    out[e] = src[blk_off(slots[i], d, D)];
+  }
 }
 __global__ void gather2_kernel(const float *A, const float *B, const int64_t *idx, int64_t n, int D, float *out) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n * D) return;
-  const int64_t i = e / D;
-  const int d = (int)(e % D);
-  const int64_t s = idx[i];
-  out[e] = s >= 0 ? A[blk_off(s, d, D)] : B[blk_off(-s - 1, d, D)];
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * D;
+       e += (int64_t)gridDim.x * blockDim.x) {  // grid-stride: grids stay below 2^32 work-items
+    const int64_t i = e / D;
+    const int d = (int)(e % D);
+    const int64_t s = idx[i];
+    out[e] = s >= 0 ? A[blk_off(s, d, D)] : B[blk_off(-s - 1, d, D)];
+  }
 }
 template <class T>
 __global__ void gather_rows_kernel(const T *src, const int32_t *idx, int64_t n, int D, T *out) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n * D) return;
-  const int64_t i = e / D;
-  const int d = (int)(e % D);
-  out[e] = src[(size_t)idx[i] * D + d];
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * D;
+       e += (int64_t)gridDim.x * blockDim.x) {  // grid-stride: grids stay below 2^32 work-items
+    const int64_t i = e / D;
+    const int d = (int)(e % D);
+    out[e] = src[(size_t)idx[i] * D + d];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1538,7 +1548,7 @@ int make_flat_items(ScanItem *d_items, int32_t *d_nitems, int64_t nrows, int32_t
 
 void launch_transpose_queries(const float *q, int64_t nq, int32_t dim, float *qt, hipStream_t st) {
   if (nq <= 0) return;
-  hipLaunchKernelGGL(transpose_queries_kernel, dim3(nblk(nq * dim, 256)), dim3(256), 0, st, q, nq, dim, qt);
+  hipLaunchKernelGGL(transpose_queries_kernel, dim3(gblk(nq * dim)), dim3(256), 0, st, q, nq, dim, qt);
 }
 
 void launch_norms(const float *x, int64_t n, int32_t dim, int blocked, float *out, hipStream_t st) {
@@ -1697,56 +1707,56 @@ void launch_pq_scan(const PqArgs &a, int max_items, hipStream_t st) {
 void launch_pq_encode(const float *x, const int32_t *assign, const float *cents, int64_t n, int32_t dim, int32_t M,
                       int32_t ksub, const float *codebooks, uint8_t *codes, hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(pq_encode_kernel, dim3(nblk(n * M, 256)), dim3(256), 0, st, x, assign, cents, n, dim, M, ksub,
+  hipLaunchKernelGGL(pq_encode_kernel, dim3(gblk(n * M)), dim3(256), 0, st, x, assign, cents, n, dim, M, ksub,
                      codebooks, codes);
 }
 void launch_residuals(const float *x, const int32_t *assign, const float *cents, int64_t n, int32_t dim, float *out,
                       hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(residuals_kernel, dim3(nblk(n * dim, 256)), dim3(256), 0, st, x, assign, cents, n, dim, out);
+  hipLaunchKernelGGL(residuals_kernel, dim3(gblk(n * dim)), dim3(256), 0, st, x, assign, cents, n, dim, out);
 }
 void launch_extract_sub(const float *x, int64_t n, int32_t dim, int32_t off, int32_t sub, float *out, hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(extract_sub_kernel, dim3(nblk(n * sub, 256)), dim3(256), 0, st, x, n, dim, off, sub, out);
+  hipLaunchKernelGGL(extract_sub_kernel, dim3(gblk(n * sub)), dim3(256), 0, st, x, n, dim, off, sub, out);
 }
 void launch_pack_codes(const uint8_t *codes, const int64_t *src_of_dst, int64_t ndst, int32_t M, uint8_t *out,
                        hipStream_t st) {
   if (ndst <= 0) return;
   const int nch = (M + 15) / 16;
-  hipLaunchKernelGGL(pack_codes_kernel, dim3(nblk(ndst * nch * 16, 256)), dim3(256), 0, st, codes, src_of_dst, ndst,
+  hipLaunchKernelGGL(pack_codes_kernel, dim3(gblk(ndst * nch * 16)), dim3(256), 0, st, codes, src_of_dst, ndst,
                      M, out);
 }
 
 void launch_to_blocked(const float *src, const int64_t *src_idx, int64_t n, int32_t dim, float *dst, int64_t dst_row0,
                        hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(to_blocked_kernel, dim3(nblk(n * dim, 256)), dim3(256), 0, st, src, src_idx, n, dim, dst,
+  hipLaunchKernelGGL(to_blocked_kernel, dim3(gblk(n * dim)), dim3(256), 0, st, src, src_idx, n, dim, dst,
                      dst_row0);
 }
 void launch_scatter_blocked(const float *src, const int64_t *dst_slots, int64_t n, int32_t dim, float *dst,
                             hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(scatter_blocked_kernel, dim3(nblk(n * dim, 256)), dim3(256), 0, st, src, dst_slots, n, dim, dst);
+  hipLaunchKernelGGL(scatter_blocked_kernel, dim3(gblk(n * dim)), dim3(256), 0, st, src, dst_slots, n, dim, dst);
 }
 void launch_gather_blocked(const float *src, const int64_t *src_slots, int64_t n, int32_t dim, float *out,
                            hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(gather_blocked_kernel, dim3(nblk(n * dim, 256)), dim3(256), 0, st, src, src_slots, n, dim, out);
+  hipLaunchKernelGGL(gather_blocked_kernel, dim3(gblk(n * dim)), dim3(256), 0, st, src, src_slots, n, dim, out);
 }
 void launch_gather2(const float *A, const float *B, const int64_t *idx, int64_t n, int32_t dim, float *out,
                     hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(gather2_kernel, dim3(nblk(n * dim, 256)), dim3(256), 0, st, A, B, idx, n, dim, out);
+  hipLaunchKernelGGL(gather2_kernel, dim3(gblk(n * dim)), dim3(256), 0, st, A, B, idx, n, dim, out);
 }
 void launch_gather_rows(const float *src, const int32_t *idx, int64_t n, int32_t dim, float *out, hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(gather_rows_kernel<float>, dim3(nblk(n * dim, 256)), dim3(256), 0, st, src, idx, n, dim, out);
+  hipLaunchKernelGGL(gather_rows_kernel<float>, dim3(gblk(n * dim)), dim3(256), 0, st, src, idx, n, dim, out);
 }
 
 void launch_gather_rows_i32(const int32_t *src, const int32_t *idx, int64_t n, int32_t width, int32_t *out,
                             hipStream_t st) {
   if (n <= 0 || width <= 0) return;
-  hipLaunchKernelGGL(gather_rows_kernel<int32_t>, dim3(nblk(n * width, 256)), dim3(256), 0, st, src, idx, n, width,
+  hipLaunchKernelGGL(gather_rows_kernel<int32_t>, dim3(gblk(n * width)), dim3(256), 0, st, src, idx, n, width,
                      out);
 }
 

@@ -16,6 +16,8 @@
 // no wrap is possible at the supported dims, n <= 512: |sum| <= 512 * 255^2 < 2^31.)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <cfloat>
 #include <climits>
 #include <cmath>
@@ -234,8 +236,18 @@ void launch_nk(const Sq8Args &a, int max_items, hipStream_t st) {
 void launch_sq8_quantize(const float *src, const int64_t *slots, int blocked, int64_t n, int32_t dim, int32_t dp,
                          int shifted, uint8_t *codes, int2 *sums, uint8_t *ok, hipStream_t st, float2 *minmax) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(sq8_quantize_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, src, slots, blocked, n, dim,
-                     dp, shifted, codes, sums, ok, minmax);
+  // 64 threads per row: launched in pieces of 2^24 rows so a grid stays below 2^32 work-items (a
+  // piece offset is a multiple of 8, so a blocked source moves by whole 8-row groups)
+  constexpr int64_t PIECE = int64_t(1) << 24;
+  for (int64_t off = 0; off < n; off += PIECE) {
+    const int64_t m = n - off < PIECE ? n - off : PIECE;
+    const bool rm = slots == nullptr;  // row i of the call -> code row i (else -> code row slots[i])
+    // the source row: a blocked store is read at the slot; a row-major source at the call's row
+    hipLaunchKernelGGL(sq8_quantize_kernel, dim3((unsigned)((m + 3) / 4)), dim3(256), 0, st,
+                       src + (blocked && !rm ? 0 : off * dim), slots ? slots + off : nullptr, blocked, m, dim, dp, shifted,
+                       codes + (rm ? off * dp : 0), sums + (rm ? off : 0), ok ? ok + (rm ? off : 0) : nullptr,
+                       minmax ? minmax + off : nullptr);
+  }
 }
 
 // ScalarQuantizer.Dequantize (ScalarQuantizer.cs:65-84): range 0 -> min everywhere, else
@@ -258,8 +270,12 @@ __global__ void sq8_dequantize_kernel(const uint8_t *codes, int64_t n, int D, co
 void launch_sq8_dequantize(const uint8_t *codes, int64_t n, int32_t dim, const float *mins, const float *maxs,
                            float *out, hipStream_t st) {
   if (n <= 0 || dim <= 0) return;
-  hipLaunchKernelGGL(sq8_dequantize_kernel, dim3((unsigned)((n * dim + 255) / 256)), dim3(256), 0, st, codes, n, dim,
-                     mins, maxs, out);
+  const int64_t piece = std::max<int64_t>(1, (int64_t(1) << 30) / dim);  // rows per launch: < 2^32 work-items
+  for (int64_t off = 0; off < n; off += piece) {
+    const int64_t m = std::min(piece, n - off);
+    hipLaunchKernelGGL(sq8_dequantize_kernel, dim3((unsigned)((m * dim + 255) / 256)), dim3(256), 0, st,
+                       codes + off * dim, m, dim, mins + off, maxs + off, out + off * dim);
+  }
 }
 
 // code row stride: dim rounded up to 32, then to a k-step count the scan is instantiated for
