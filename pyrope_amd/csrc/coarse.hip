@@ -16,6 +16,7 @@
 #include <cfloat>
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "kernels.h"
 
@@ -157,6 +158,58 @@ __global__ __launch_bounds__(256) void coarse_select_kernel(const float *scores,
   }
 }
 
+// One pass instead of nprobe: each lane keeps the P best keys of its share of the row (every 64th
+// centroid) sorted in registers, then P rounds pop the wave's best head -- the same ranking, O(nlist)
+// reads instead of O(nprobe x nlist).  P (>= nprobe) is a compile-time list length.
+template <int P>
+__device__ __forceinline__ void key_insert(uint64_t (&l)[P], uint64_t v) {
+  bool b[P];
+#pragma unroll
+  for (int j = 0; j < P; ++j) b[j] = v > l[j];
+#pragma unroll
+  for (int j = P - 1; j >= 1; --j) l[j] = b[j - 1] ? l[j - 1] : (b[j] ? v : l[j]);
+  l[0] = b[0] ? v : l[0];
+}
+
+template <int P>
+__global__ __launch_bounds__(256) void coarse_select_reg_kernel(const float *scores, int64_t nq, int nc, int nprobe,
+                                                                int32_t *probes) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.x * 4 + w;
+  if (q >= nq) return;  // no block barrier below
+  uint64_t l[P];
+#pragma unroll
+  for (int j = 0; j < P; ++j) l[j] = 0;  // below every real key
+  const float *row = scores + q * nc;
+  constexpr int U = 8;  // independent loads in flight per lane before the (branchy) insertions
+  for (int c0 = lane; c0 < nc; c0 += 64 * U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = c0 + 64 * u < nc ? row[c0 + 64 * u] : 0.0f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (c0 + 64 * u >= nc) break;
+      const uint64_t kv = rank_key(v[u], c0 + 64 * u);
+      if (kv > l[P - 1]) key_insert<P>(l, kv);
+    }
+  }
+  for (int p = 0; p < nprobe; ++p) {
+    uint64_t best = l[0];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const uint64_t ov = __shfl_xor(best, o);
+      best = ov > best ? ov : best;
+    }
+    if (l[0] == best) {  // keys are unique (centroid index in the low half): one lane pops its head
+#pragma unroll
+      for (int j = 0; j < P - 1; ++j) l[j] = l[j + 1];
+      l[P - 1] = 0;
+      if (best != 0) probes[q * nprobe + p] = 0x7FFFFFFF - (int)(uint32_t)best;
+    }
+    if (best == 0 && lane == 0) probes[q * nprobe + p] = -1;  // fewer centroids than nprobe (as the LDS kernel)
+  }
+}
+
 }  // namespace
 
 // waves (queries) per selection block: the rows of all of them must fit in LDS
@@ -180,9 +233,20 @@ void launch_coarse_dense(const float *q, const float *cents_rm, const float *qn,
   else
     hipLaunchKernelGGL(coarse_scores_kernel<COS>, grid, dim3(256), 0, st, q, cents_rm, qn, cn, nq, nlist, dim,
                        scores);
-  const int wpb = select_wpb(nlist);
-  hipLaunchKernelGGL(coarse_select_kernel, dim3((unsigned)((nq + wpb - 1) / wpb)), dim3(64 * wpb),
-                     (size_t)wpb * nlist * sizeof(uint64_t), st, scores, nq, nlist, nprobe, wpb, probes);
+  // register lists for nprobe <= 64 (PYR_COARSE_SELECT=0: the LDS argmax rounds, measurement knob)
+  const bool reg = !getenv("PYR_COARSE_SELECT") || atoi(getenv("PYR_COARSE_SELECT")) != 0;
+  const dim3 g4((unsigned)((nq + 3) / 4));
+  if (reg && nprobe <= 16) {
+    hipLaunchKernelGGL(coarse_select_reg_kernel<16>, g4, dim3(256), 0, st, scores, nq, nlist, nprobe, probes);
+  } else if (reg && nprobe <= 32) {
+    hipLaunchKernelGGL(coarse_select_reg_kernel<32>, g4, dim3(256), 0, st, scores, nq, nlist, nprobe, probes);
+  } else if (reg && nprobe <= 64) {
+    hipLaunchKernelGGL(coarse_select_reg_kernel<64>, g4, dim3(256), 0, st, scores, nq, nlist, nprobe, probes);
+  } else {
+    const int wpb = select_wpb(nlist);
+    hipLaunchKernelGGL(coarse_select_kernel, dim3((unsigned)((nq + wpb - 1) / wpb)), dim3(64 * wpb),
+                       (size_t)wpb * nlist * sizeof(uint64_t), st, scores, nq, nlist, nprobe, wpb, probes);
+  }
 }
 
 }  // namespace pyr
