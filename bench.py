@@ -383,6 +383,18 @@ def run(args):
         log(f"cpu baseline: {S / ct_:,.1f} QPS on {threads} threads ({host.get('model')}); "
             f"parity ids={ids_equal} bits={bits_equal}")
 
+    # roofline traffic: HBM bytes per list-scan launch from the committed FETCH_SIZE counter pass
+    # (traffic.json; counters need their own rocprofv3 run), used only for the configuration and the
+    # list-scan arithmetic it was measured on
+    traffic, traffic_src = None, None
+    tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "traffic.json")
+    if os.path.exists(tpath) and world == 1 and prec == 2:
+        tj = json.load(open(tpath))
+        tc = tj.get("config", {})
+        if (tc.get("n"), tc.get("dim"), tc.get("nlist"), tc.get("nprobe"), tc.get("k"), tc.get("nq")) == \
+                (N, D, args.nlist, args.nprobe, k, args.nq):
+            traffic, traffic_src = tj["hbm_read_bytes_per_launch"], tj["source"]
+
     if rank == 0:
         bytes_per_query = args.nprobe / args.nlist * N * D * 4 + args.nlist * D * 4
         out = {
@@ -408,7 +420,8 @@ def run(args):
                                 if world > 1 else "none"},
             "recall_at_10": recall,
             "roofline": {"bound": "hbm", "achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": hbm_achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": hbm_achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "unique_bytes_per_launch": unique_bytes, "lists_probed": int(len(probed)),
                          "kernel": kernel_name,
                          "stored_bytes_per_launch": stored_bytes,
