@@ -105,11 +105,11 @@ void RowStore::encode16(const int64_t *d_slots, int64_t cnt, hipStream_t st) {
     sx = pow2_scale_host(amax);
     if (ctr && d_slots)  // every slot is re-encoded: their residual norms too
       launch_resid_sq(rows.as<float>(), cap, dim, ctr, nullptr, rsq16.as<float>(), st, nullptr, rmax_r.as<uint32_t>());
-    launch_encode16(rows.as<float>(), nullptr, cap, dim, sx, h16.p, st, ctr, nullptr);
+    launch_encode16(rows.as<float>(), nullptr, cap, dim, sx, h16.p, st, ctr, nullptr, meta_norms());
     launch_meta16(nullptr, cap, met16, meta_norms(), live.as<uint8_t>(), meta.as<float>(), st);
   } else {
     amax = std::max(am, amax);
-    launch_encode16(rows.as<float>(), d_slots, cnt, dim, sx, h16.p, st, ctr, nullptr);
+    launch_encode16(rows.as<float>(), d_slots, cnt, dim, sx, h16.p, st, ctr, nullptr, meta_norms());
     launch_meta16(d_slots, cnt, met16, meta_norms(), live.as<uint8_t>(), meta.as<float>(), st);
   }
   HIPCHK(hipGetLastError());
@@ -1424,7 +1424,8 @@ struct IvfFlatIndex : Index {
       HIPCHK(hipStreamSynchronize(wst));
       std::memcpy(&nl.amax, &bits, sizeof(bits));
       nl.sx = pow2_scale_host(nl.amax);
-      launch_encode16(nl.rows.as<float>(), nullptr, nl.cap, dim, nl.sx, nl.h16.p, wst, C, dtl.as<int32_t>());
+      launch_encode16(nl.rows.as<float>(), nullptr, nl.cap, dim, nl.sx, nl.h16.p, wst, C, dtl.as<int32_t>(),
+                      nl.rsq16.as<float>());
       launch_meta16(nullptr, nl.cap, metric, nl.rsq16.as<float>(), nl.live.as<uint8_t>(), nl.meta.as<float>(), wst);
       HIPCHK(hipGetLastError());
     }

@@ -165,9 +165,14 @@ struct CycleBuckets {
   }
 };
 
-template <int D, int MET, int KR, bool Q2, int NSTC>
+// STEP: tiles per block barrier.  STEP = 2 waits for and releases two tiles at a time (ring of
+// 4 = the two being read + the next two in flight), halving the barriers and letting per-wave work
+// (appends, drains) even out over two tiles; the drain checks stay per tile.
+template <int D, int MET, int KR, bool Q2, int NSTC, int STEP>
 __global__ __launch_bounds__(256, 2) void mfma_filter16(FilterArgs a) {
   using L = F16Lds<D, NSTC>;
+  static_assert(STEP == 1 || STEP == 2, "tiles per barrier");
+  static_assert(L::NST >= 2 * STEP + (STEP == 1 ? 1 : 0), "ring too shallow for the step");
   constexpr int KS = D / 16;
   constexpr int NST = L::NST;
   __shared__ __attribute__((aligned(16))) char ring[L::RING];
@@ -301,7 +306,7 @@ __global__ __launch_bounds__(256, 2) void mfma_filter16(FilterArgs a) {
   };
   __syncthreads();  // thresholds / counts initialised (the first barrier of the loop orders the rest)
 #pragma unroll
-  for (int t = 0; t < NST - 1; ++t)
+  for (int t = 0; t < NST - STEP; ++t)
     if (t < nt) issue(t);
 
   // thr[r]: query q(r, h)'s threshold moved to the pre-constant score y = f * acc + meta (the
@@ -339,15 +344,20 @@ __global__ __launch_bounds__(256, 2) void mfma_filter16(FilterArgs a) {
   };
 
   cb.mark(6);
+  // refresh the shared bounds every pub_mask + 1 tiles, i.e. every (pub_mask + 1) / STEP steps
+  const int rmask = max(1, (a.pub_mask + 1) / STEP) - 1;
   for (int st = 0; st < nt; ++st) {
-    // tile st has landed for this wave once at most the younger tiles' loads are outstanding
-    // (the compiler does not see the LDS-DMA, so these waits are the only ones ordering it)
-    // (extra loads issued after tile st -- the shared bounds, publishes -- only make it stricter)
-    wait_vm_le<3 * (NST - 2)>(st + 1 < nt ? lpt * min(NST - 2, nt - 1 - st) : 0);
+    if (STEP == 2 && (st & 1)) goto compute;  // the odd tile of a step landed with the even one
+    {
+    // tiles st .. st+STEP-1 have landed for this wave once at most the younger tiles' loads are
+    // outstanding (the compiler does not see the LDS-DMA, so these waits are the only ones ordering
+    // it; extra loads issued after them -- the shared bounds, publishes -- only make it stricter)
+    const int last = min(st + STEP, nt) - 1;
+    wait_vm_le<3 * (NST - 2)>(lpt * max(0, min(NST - 2 * STEP, nt - 1 - last)));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave's pieces of tile st landed; tile st-1 fully read
+    __builtin_amdgcn_s_barrier();  // every wave's pieces of this step landed; the previous step fully read
     cb.mark(0);
-    if (a.gthr && (st & a.pub_mask) == a.pub_mask && wave_active) {
+    if (a.gthr && ((st / STEP) & rmask) == rmask && wave_active) {
       // every pub_mask + 1 tiles: take the query's shared bound (other items' progress) read by the
       // previous refresh -- an LDS-DMA issued pub_mask + 1 (>= NST - 1) tiles ago, so this tile's
       // counted wait covered it -- publish this list's K1-th best (an atomic nothing waits for) and
@@ -377,8 +387,12 @@ __global__ __launch_bounds__(256, 2) void mfma_filter16(FilterArgs a) {
       __builtin_amdgcn_wave_barrier();
       load_thr();
     }
-    if (st + NST - 1 < nt) issue(st + NST - 1);  // into the slot tile st-1 used
+#pragma unroll
+    for (int u = 0; u < STEP; ++u)  // into the slots the previous step used
+      if (st + NST - STEP + u < nt) issue(st + NST - STEP + u);
     cb.mark(1);
+    }
+  compute:
     if (!wave_active) continue;
     cb.acc[7] += 1;
     const char *slot = ring + (st % NST) * L::SLOT;
@@ -498,8 +512,14 @@ inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
 // ring depth of the D = 128, K1 = 16 kernels (PYR_F16_NST, measurement knob: 3, 4 or 0 = deepest)
 static int f16_nst() {
-  static const int v = getenv("PYR_F16_NST") ? atoi(getenv("PYR_F16_NST")) : 3;
-  return v;
+  const char *e = getenv("PYR_F16_NST");
+  return e ? atoi(e) : 3;
+}
+// tiles per block barrier of the K1 = 16 kernels (PYR_F16_STEP, measurement knob: 2 = default, 1 =
+// one tile per barrier: 3.81 -> 3.45 ms list scan at I1, profiles/r2_sweeps/r2st_sweep.log)
+static int f16_step() {
+  const char *e = getenv("PYR_F16_STEP");
+  return e ? atoi(e) : 2;
 }
 
 template <int D, int MET, int KR, bool Q2>
@@ -507,17 +527,23 @@ void launch16_p(const FilterArgs &a, int max_items, hipStream_t st) {
   // all LDS is static (79 KiB at D = 128): no dynamic-LDS attribute (a 160 KiB dynamic limit on top
   // of the static size makes the launch invalid)
   const int grid = a.xcd ? (max_items + 7) / 8 * 8 : max_items;
-  if constexpr (D == 128 && KR == 16) {
-    if (f16_nst() == 3) {
-      hipLaunchKernelGGL((mfma_filter16<D, MET, KR, Q2, 3>), dim3(grid), dim3(256), 0, st, a);
-      return;
-    }
-    if (f16_nst() == 4) {
-      hipLaunchKernelGGL((mfma_filter16<D, MET, KR, Q2, 4>), dim3(grid), dim3(256), 0, st, a);
+  if constexpr (KR == 16) {  // the K1 = 16 list scans: two tiles per barrier (default)
+    if (f16_step() == 2) {
+      hipLaunchKernelGGL((mfma_filter16<D, MET, KR, Q2, 4, 2>), dim3(grid), dim3(256), 0, st, a);
       return;
     }
   }
-  hipLaunchKernelGGL((mfma_filter16<D, MET, KR, Q2, 0>), dim3(grid), dim3(256), 0, st, a);
+  if constexpr (D == 128 && KR == 16) {
+    if (f16_nst() == 3) {
+      hipLaunchKernelGGL((mfma_filter16<D, MET, KR, Q2, 3, 1>), dim3(grid), dim3(256), 0, st, a);
+      return;
+    }
+    if (f16_nst() == 4) {
+      hipLaunchKernelGGL((mfma_filter16<D, MET, KR, Q2, 4, 1>), dim3(grid), dim3(256), 0, st, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((mfma_filter16<D, MET, KR, Q2, 0, 1>), dim3(grid), dim3(256), 0, st, a);
 }
 
 template <int D, int MET>
@@ -545,8 +571,11 @@ __device__ __forceinline__ float resid_val(const float *rows, const float *cents
   return cents ? x - cents[(size_t)(tile_list ? tile_list[r >> 5] : 0) * D + d] : x;
 }
 
+// A row whose norm (rn: |x|^2 or |x - c|^2) is not finite holds an Inf or a NaN: its tile entries are
+// zero (an Inf times a zero or opposite-signed query half would make the whole score NaN), and
+// meta16_kernel makes it always (Inf) or never (NaN) a candidate.
 __global__ void encode16_kernel(const float *rows, const int64_t *slots, int64_t n, int D, float sx,
-                                const float *cents, const int32_t *tile_list, _Float16 *h16) {
+                                const float *cents, const int32_t *tile_list, const float *rn, _Float16 *h16) {
   const int G = D / 8;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * G;
        e += (int64_t)gridDim.x * blockDim.x) {  // grid-stride: grids stay below 2^32 work-items
@@ -554,20 +583,26 @@ __global__ void encode16_kernel(const float *rows, const int64_t *slots, int64_t
     const int g = (int)(e % G);
     const int64_t r = slots ? slots[i] : i;
     h8v v;
-  #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (_Float16)(resid_val(rows, cents, tile_list, r, 8 * g + j, D) * sx);
+    const bool special = rn && !isfinite(rn[r]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      v[j] = special ? (_Float16)0.0f : (_Float16)(resid_val(rows, cents, tile_list, r, 8 * g + j, D) * sx);
     const size_t off = (((size_t)(r >> 5) * (D / 16) + (g >> 1)) * 2 + (g & 1)) * 32 + (r & 31);
     *reinterpret_cast<h8v *>(h16 + off * 8) = v;
   }
 }
 
-// meta[r] = live ? (L2 ? -|x|^2 : 0) : -inf
+// meta[r] = live ? (L2 ? -|x|^2 : 0) : -inf; a live row with a non-finite norm: +inf when it holds an
+// Inf (approx = +inf: always a candidate; the exact refine gives its real +-inf / NaN score, and the
+// certificate's K1-th approximate score still bounds every row left out), -inf when it holds a NaN
+// (never a candidate: the reference heap keeps a NaN score only among the first k rows it scans)
 __global__ void meta16_kernel(const int64_t *slots, int64_t n, int met, const float *rsq, const uint8_t *live,
                               float *meta) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t r = slots ? slots[i] : i;
-  meta[r] = live[r] ? (met == L2 ? -rsq[r] : 0.0f) : -INFINITY;
+  const float n2 = rsq[r];
+  meta[r] = !live[r] || isnan(n2) ? -INFINITY : isinf(n2) ? INFINITY : (met == L2 ? -n2 : 0.0f);
 }
 
 // max |x_i| over the given rows (finite values; non-negative floats order as their bits)
@@ -620,10 +655,10 @@ void launch_filter16(const FilterArgs &a, int metric, int max_items, hipStream_t
 }
 
 void launch_encode16(const float *rows, const int64_t *slots, int64_t n, int32_t dim, float sx, void *h16,
-                     hipStream_t st, const float *cents, const int32_t *tile_list) {
+                     hipStream_t st, const float *cents, const int32_t *tile_list, const float *rn) {
   if (n <= 0) return;
   hipLaunchKernelGGL(encode16_kernel, dim3(gblk(n * (dim / 8))), dim3(256), 0, st, rows, slots, n, dim, sx, cents,
-                     tile_list, reinterpret_cast<_Float16 *>(h16));
+                     tile_list, rn, reinterpret_cast<_Float16 *>(h16));
 }
 
 void launch_resid_sq(const float *rows, int64_t n, int32_t dim, const float *cents, const int32_t *tile_list,

@@ -341,8 +341,10 @@ bool filter16_supported(int dim, int metric, int k1);
 void launch_filter16(const FilterArgs &a, int metric, int max_items, hipStream_t st);
 // fp16 tiles of blocked fp32 rows (slots[i], or rows [0, n)), scaled by sx; with cents (row-major)
 // and tile_list (list of each 32-row tile) the residuals x - c[list] (IVF lists)
+// rn (may be null): the rows' meta norms; a non-finite one zeroes the row's tile (encode16_kernel)
 void launch_encode16(const float *rows, const int64_t *slots, int64_t n, int32_t dim, float sx, void *h16,
-                     hipStream_t st, const float *cents = nullptr, const int32_t *tile_list = nullptr);
+                     hipStream_t st, const float *cents = nullptr, const int32_t *tile_list = nullptr,
+                     const float *rn = nullptr);
 // |x - c[list]|^2 of rows [0, n)
 void launch_resid_sq(const float *rows, int64_t n, int32_t dim, const float *cents, const int32_t *tile_list,
                      float *out, hipStream_t st, const int64_t *slots = nullptr, uint32_t *out_max = nullptr);

@@ -205,3 +205,24 @@ def test_bf16x3_near_duplicates_and_wide_range(hiplib, metric, scale):
     with _env(PYR_FILTER=0):
         ref = idx.search_batch(q, 10)
     _same(got, ref)
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_non_finite_rows_do_not_poison_the_certificate(hiplib, metric):
+    """a NaN / Inf row must not enter the certificate's norm bound (rmax only grows), or
+    every later query would fail its certificate and re-run exactly.  The rows sit past the first
+    k slots, where the reference's heap never admits a NaN score (NaN > x is false), so the filter
+    path and the exact scan agree."""
+    from pyrope_amd import generate_synthetic
+    d = 128
+    x = generate_synthetic(20000, d, 42)
+    x[5000] = np.nan
+    x[7000, 3] = np.inf
+    q = generate_synthetic(200, d, 1337)
+    idx = _flat(d, metric, x)
+    got, nfb = _fallbacks(hiplib, lambda: idx.search_batch(q, 10))
+    with _env(PYR_FILTER=0):
+        ref = idx.search_batch(q, 10)
+    _same(got, ref)
+    assert 5000 not in got[1]  # NaN scores never rank (the Inf row does rank first for IP: +inf)
+    assert nfb <= len(q) // 20, nfb
