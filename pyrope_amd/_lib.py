@@ -10,7 +10,8 @@ import os
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpyrope_hip.so")
+# PYR_LIB: another build of the library (measurement only: A/B runs of two builds on one box)
+LIB_PATH = os.environ.get("PYR_LIB") or os.path.join(HERE, "libpyrope_hip.so")
 
 (PYR_OK, PYR_E_DIM, PYR_E_ARG, PYR_E_STATE, PYR_E_OOM, PYR_E_DEVICE, PYR_E_DUPLICATE, PYR_E_NOT_FOUND,
  PYR_E_FORMAT, PYR_E_IO) = range(10)

@@ -445,50 +445,54 @@ __device__ __forceinline__ float hsum8(const float *v) {
 
 // V = 1: L2Squared (VectorMath.cs:39-70) / DotProduct (:8-37);
 // V = 4: L2SquaredUnsafe (:188-253) / DotProductUnsafe (:128-186).  D % 8 == 0.
+// (kernels.hip em_* hold the one-lane form; the refine spreads it over 8 lanes, below.)
+
+// hsum8 over the 8 lanes of an aligned lane group, lane l holding v[l]: the same three levels of
+// pairwise adds (fp32 adds commute, so every lane of the group ends with the identical value)
+__device__ __forceinline__ float hsum8_lanes(float v) {
+  v = v + __shfl_xor(v, 1);  // (v0 + v1), (v2 + v3), ...
+  v = v + __shfl_xor(v, 2);  // lo = (v0 + v1) + (v2 + v3), hi
+  return v + __shfl_xor(v, 4);  // lo + hi
+}
+
+// exact_score with its 8 accumulator lanes spread over an 8-lane group: lane l (0..7) runs the
+// chains of accumulator l (a1..a4[l] for V = 4, acc[l] for the 8-wide loop), in the same order, and
+// the group reduces them as hsum8 does.  Every lane of the group returns the score.
 template <int V, int MET>
-__device__ float exact_score(const float *q, const float *rows, int64_t r, int D) {
+__device__ float exact_score_l8(const float *q, const float *rows, int64_t r, int D, int l) {
   float sum = 0.0f;
   int i = 0;
   if (V == 4 && D >= 32) {
-    float a1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, a2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    float a3[8] = {0, 0, 0, 0, 0, 0, 0, 0}, a4[8] = {0, 0, 0, 0, 0, 0, 0, 0}, fin[8];
+    float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     for (; i <= D - 32; i += 32)
 #pragma unroll
-      for (int l = 0; l < 8; l++) {
-        float t[4];
-#pragma unroll
-        for (int v = 0; v < 4; v++) {
-          const float x = rows[blk_off(r, i + 8 * v + l, D)];
-          if (MET == L2) {
-            const float d = q[i + 8 * v + l] - x;
-            t[v] = d * d;
-          } else {
-            t[v] = q[i + 8 * v + l] * x;
-          }
+      for (int v = 0; v < 4; v++) {
+        const float x = rows[blk_off(r, i + 8 * v + l, D)];
+        float t;
+        if (MET == L2) {
+          const float d = q[i + 8 * v + l] - x;
+          t = d * d;
+        } else {
+          t = q[i + 8 * v + l] * x;
         }
-        a1[l] = a1[l] + t[0];
-        a2[l] = a2[l] + t[1];
-        a3[l] = a3[l] + t[2];
-        a4[l] = a4[l] + t[3];
+        a[v] = a[v] + t;
       }
-#pragma unroll
-    for (int l = 0; l < 8; l++) fin[l] = ((a1[l] + a2[l]) + a3[l]) + a4[l];
-    sum = sum + hsum8(fin);
+    const float fin = ((a[0] + a[1]) + a[2]) + a[3];
+    sum = sum + hsum8_lanes(fin);
   }
   if (i <= D - 8) {
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (; i <= D - 8; i += 8)
-#pragma unroll
-      for (int l = 0; l < 8; l++) {
-        const float x = rows[blk_off(r, i + l, D)];
-        if (MET == L2) {
-          const float d = q[i + l] - x;
-          acc[l] = acc[l] + d * d;
-        } else {
-          acc[l] = acc[l] + q[i + l] * x;
-        }
+    float acc = 0.0f;
+#pragma unroll 4
+    for (; i <= D - 8; i += 8) {
+      const float x = rows[blk_off(r, i + l, D)];
+      if (MET == L2) {
+        const float d = q[i + l] - x;
+        acc = acc + d * d;
+      } else {
+        acc = acc + q[i + l] * x;
       }
-    sum = sum + hsum8(acc);
+    }
+    sum = sum + hsum8_lanes(acc);
   }
   return MET == L2 ? -sum : sum;
 }
@@ -529,9 +533,15 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
   const int32_t *mk = a.mk + (size_t)q * k1;
   uint32_t key = KEY_NONE;
   float s = -INFINITY;
-  if (lane < k1 && mk[lane] >= 0) {
-    key = (uint32_t)mk[lane];
-    s = exact_score<V, MET>(qp, a.rows, (int64_t)key, D);
+  if (lane < k1 && mk[lane] >= 0) key = (uint32_t)mk[lane];
+  // exact scores, 8 candidates per pass (an 8-lane group per candidate), then candidate c's score
+  // moves to lane c
+  for (int p = 0; 8 * p < k1; ++p) {
+    const int c = 8 * p + (lane >> 3);
+    const int32_t kc = c < k1 ? mk[c] : -1;
+    const float sc = exact_score_l8<V, MET>(qp, a.rows, kc >= 0 ? (int64_t)kc : 0, D, lane & 7);
+    const float t = __shfl(sc, 8 * (lane & 7));
+    if ((lane >> 3) == p && key != KEY_NONE) s = t;
   }
   int rank = 0, valid = 0;
   for (int c = 0; c < k1; ++c) {
@@ -572,17 +582,26 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
       float ar2 = 0.0f, xc2 = 0.0f;
       uint32_t xrk = 0, xfk = 0;
       // FLAT (no probes): one center, list 0
+      // 8 probes per pass, an 8-lane group per probe, lane j of it summing dims j, j + 8, ...
       const int np = a.probes ? a.nprobe : 1;
-      for (int p = lane; p < np; p += 64) {
-        const int l = a.probes ? a.probes[(size_t)q * a.nprobe + p] : 0;
-        xrk = max(xrk, a.list_rmax_r[l]);
-        xfk = max(xfk, a.list_rmax[l]);
-        const float *c = a.cents + (size_t)l * D;
+      for (int p0 = 0; p0 < np; p0 += 8) {
+        const int p = p0 + (lane >> 3), j = lane & 7;
         float d2 = 0.0f, c2 = 0.0f;
-        for (int d = 0; d < D; ++d) {
-          const float t = qp[d] - c[d];
-          d2 += t * t;
-          c2 += c[d] * c[d];
+        if (p < np) {
+          const int l = a.probes ? a.probes[(size_t)q * a.nprobe + p] : 0;
+          xrk = max(xrk, a.list_rmax_r[l]);
+          xfk = max(xfk, a.list_rmax[l]);
+          const float *c = a.cents + (size_t)l * D;
+          for (int d = j; d < D; d += 8) {
+            const float t = qp[d] - c[d];
+            d2 += t * t;
+            c2 += c[d] * c[d];
+          }
+        }
+#pragma unroll
+        for (int off = 1; off <= 4; off <<= 1) {
+          d2 += __shfl_xor(d2, off);
+          c2 += __shfl_xor(c2, off);
         }
         ar2 = fmaxf(ar2, d2);
         xc2 = fmaxf(xc2, c2);

@@ -36,6 +36,7 @@ namespace pyr {
 namespace {
 
 typedef float f16v __attribute__((ext_vector_type(16)));
+typedef float f4v __attribute__((ext_vector_type(4)));
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void gbl_void;
@@ -508,6 +509,373 @@ __global__ __launch_bounds__(256, 2) void mfma_filter16(FilterArgs a) {
   cb.flush(a.tdbg, lane);
 }
 
+// ---------------------------------------------------------------------------------------------
+// mfma_filter16w: the same filter with 8 waves x 16 queries per 128-query item, on
+// v_mfma_f32_16x16x32_f16.  A wave's per-query state shrinks to a quarter of the 32-query form
+// (4 scores per lane per 16-row half tile, 4 thresholds, 4 counts) and each query's register
+// top-K1 is spread over the query's 4 lanes (K1 / 4 entries each), so a wave fits 128 VGPRs:
+// two 512-thread blocks per CU, 4 waves per SIMD (the 32-query kernel: 2).  Tiles, meta, partial
+// lists and the certificate are unchanged; the h16 tile order serves the 16x16x32 B operand too
+// (lane (c, g) of k-step s, rows 16b..16b+15: piece (4s + g), row 16b + c -- 256 contiguous bytes
+// per lane group, conflict-free ds_read_b128).
+//
+// C layout (16x16x32): register i of lane (c = lane & 15, g = lane >> 4) is query 4g + i of the
+// wave, data row c of the 16-row half b.  A operand: lane (c, g) holds query c, dims 32s + 8g .. +7.
+template <int D, int MET, int KR, bool Q2, int NSTC, int STEP>
+__global__ __launch_bounds__(512, 4) void mfma_filter16w(FilterArgs a) {
+  constexpr int NW = 8;
+  constexpr int TB = RT16 * D * 2;                    // h16 bytes per tile
+  constexpr int NCH = TB / 1024;                      // 1 KiB pieces per tile (2, 4 or 8)
+  constexpr int SLOT = TB + 256;                      // tile + meta
+  constexpr int STATE = (int)sizeof(F16State);
+  constexpr int BOUNDS = NW * 256;
+  constexpr int NST_MAX0 = (80 * 1024 - STATE - BOUNDS) / SLOT;
+  constexpr int NST_MAX = NST_MAX0 > 8 ? 8 : NST_MAX0;
+  constexpr int NST = NSTC > 0 && NSTC < NST_MAX ? NSTC : NST_MAX;
+  static_assert(STEP == 1 || STEP == 2, "tiles per barrier");
+  static_assert(NST >= 2 * STEP + (STEP == 1 ? 1 : 0), "ring too shallow for the step");
+  static_assert(NCH <= NW, "one piece per wave at most");
+  static_assert(KR % 4 == 0, "top-K1 spread over 4 lanes");
+  constexpr int KS = D / 32;  // 16x16x32 k-steps
+  constexpr int R = KR / 4;   // top-K1 entries per lane
+  constexpr int CB = CB16;
+  __shared__ __attribute__((aligned(16))) char ring[NST * SLOT];
+  __shared__ __attribute__((aligned(16))) uint32_t bounds_l[BOUNDS / 4];
+  __shared__ __attribute__((aligned(16))) F16State state16;
+  const uint32_t ring_base = (uint32_t)(size_t)(lds_void *)ring;
+  float *const thr_l = state16.thr;
+  int *const cnt_l = state16.cnt;
+  float *const cs_l = state16.cs;
+  uint16_t *const ck_l = state16.ck;
+
+  int item = blockIdx.x;
+  if (a.xcd) {
+    const int per = (*a.n_items + 7) >> 3;
+    item = ((int)blockIdx.x & 7) * per + ((int)blockIdx.x >> 3);
+    if ((int)(blockIdx.x >> 3) >= per) return;
+  }
+  if (item >= *a.n_items) return;
+  const ScanItem it = a.items[item];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int c16 = lane & 15, g = lane >> 4;
+  CycleBuckets cb;
+  cb.start(a.tdbg != nullptr);
+
+  // ---- A operand: query 16w + c16, dims 32s + 8g .. +7 of k-step s, scaled and split ----
+  const int qslot = 16 * w + c16;
+  const int qi = qslot < it.qcnt ? (a.qlist ? a.qlist[it.qbeg + qslot] / a.nparts : it.qbeg + qslot) : -1;
+  float qv[KS][8];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (qi >= 0) {
+      const float4 *qp = reinterpret_cast<const float4 *>(a.queries + (size_t)qi * D + 32 * s + 8 * g);
+      const float4 v0 = qp[0], v1 = qp[1];
+      qv[s][0] = v0.x; qv[s][1] = v0.y; qv[s][2] = v0.z; qv[s][3] = v0.w;
+      qv[s][4] = v1.x; qv[s][5] = v1.y; qv[s][6] = v1.z; qv[s][7] = v1.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qv[s][j] = 0.0f;
+    }
+  }
+  // IVF residual mode: A = q - c (L2) or q (IP), cq the per (query, list) constant (filter16)
+  float cq = 0.0f;
+  if (a.cents) {
+    const float *c = a.cents + (size_t)it.list * D;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float cv = c[32 * s + 8 * g + j];
+        if (MET == L2) {
+          qv[s][j] = qv[s][j] - cv;
+          cq += qv[s][j] * qv[s][j];
+        } else {
+          cq += qv[s][j] * cv;
+        }
+      }
+    cq += __shfl_xor(cq, 16);
+    cq += __shfl_xor(cq, 32);
+    if (MET == L2) cq = -cq;
+  }
+  float amax = 0.0f;
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(qv[s][j]));
+  amax = fmaxf(amax, __shfl_xor(amax, 16));
+  amax = fmaxf(amax, __shfl_xor(amax, 32));
+  const float sq = pow2_scale(amax);
+  h8v qh[KS], ql[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = qv[s][j] * sq;  // exact (power of two)
+      qh[s][j] = (_Float16)v;
+      ql[s][j] = (_Float16)(v - (float)qh[s][j]);
+    }
+  const float myf = (MET == L2 ? 2.0f : 1.0f) / (sq * a.sx);
+  float f[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) f[i] = __shfl(myf, 4 * g + i);
+
+  // ---- owners: lanes (c16, g = 0); query 16w + c16's top-KR is spread over its 4 lanes: lane
+  // (c16, g) holds entries R g .. R g + R - 1 (descending) ----
+  const bool qvalid = qslot < it.qcnt;
+  const bool owner = g == 0 && qvalid;
+  int oslot = 0;
+  float gs = -INFINITY;
+  if (qvalid) {
+    oslot = a.qlist ? a.qlist[it.qbeg + qslot] + it.part : (it.qbeg + qslot) * a.nparts + it.part;
+    if (a.gthr) gs = key_score(__hip_atomic_load(a.gthr + qi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  }
+  float ts[R];
+  uint32_t tk[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    ts[j] = -INFINITY;
+    tk[j] = KEY_NONE;
+  }
+  // the query's K1-th entry (lane (c16, 3), entry R - 1), on all 4 of its lanes
+  auto last_s = [&]() { return __shfl(ts[R - 1], 48 + c16); };
+  auto last_k = [&]() { return (uint32_t)__shfl((int)tk[R - 1], 48 + c16); };
+  uint32_t published = 0;
+  float sink = 0.0f;
+  int bst = -1;
+  if (g == 0) {
+    thr_l[qslot] = qvalid ? gs : INFINITY;
+    cnt_l[qslot] = 0;
+  }
+
+  const int r0 = it.row_begin;
+  const int nt = (it.row_end - r0 + RT16 - 1) / RT16;
+  const char *hsrc = reinterpret_cast<const char *>(a.h16);
+  const int lpt = (w < NCH ? 1 : 0) + (w == NW - 1 ? 1 : 0);  // pieces per tile; meta by the last wave
+  auto issue = [&](int t) {
+    const size_t tile = (size_t)(r0 / RT16 + t);
+    const uint32_t base = ring_base + (uint32_t)((t % NST) * SLOT);
+    if (w < NCH) glds<16>(hsrc + tile * TB + (size_t)w * 1024 + lane * 16, base + w * 1024);
+    if (w == NW - 1) glds<4>(a.meta + tile * RT16 + (lane & 31), base + TB);
+  };
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < NST - STEP; ++t)
+    if (t < nt) issue(t);
+
+  // thresholds of queries 4g + i moved to the pre-constant score y (filter16 load_thr)
+  float thr[4];
+  auto load_thr = [&]() {
+    const float4 t4 = *reinterpret_cast<const float4 *>(thr_l + 16 * w + 4 * g);
+    const float tv[4] = {t4.x, t4.y, t4.z, t4.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float t = tv[i], c = __shfl(cq, 4 * g + i);
+      const float lowered = (t - c) - 0x1p-20f * (fabsf(t) + fabsf(c));
+      thr[i] = isinf(t) ? (t > 0.0f ? t : -FLT_MAX) : fmaxf(lowered, -FLT_MAX);
+    }
+  };
+  load_thr();
+  const bool wave_active = 16 * w < it.qcnt;
+  int cnt[4] = {0, 0, 0, 0};
+  auto publish_counts = [&]() {
+    if (c16 == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) cnt_l[16 * w + 4 * g + i] = cnt[i];
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
+  // distributed insert of (v, key) into the query's 4-lane list (all 4 lanes of the query call it)
+  auto dist_insert = [&](float v, uint32_t key) {
+    bool b[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) b[j] = better(v, key, ts[j], tk[j]);
+    const float ps = __shfl(ts[R - 1], lane - 16);
+    const uint32_t pk = (uint32_t)__shfl((int)tk[R - 1], lane - 16);
+    // (every lane of the query takes part in the shuffles: a bpermute reads 0 from a disabled lane)
+    const int pbi = __shfl((int)b[R - 1], lane - 16);
+    const bool pb = g > 0 && pbi != 0;
+#pragma unroll
+    for (int j = R - 1; j >= 1; --j) {
+      ts[j] = b[j - 1] ? ts[j - 1] : (b[j] ? v : ts[j]);
+      tk[j] = b[j - 1] ? tk[j - 1] : (b[j] ? key : tk[j]);
+    }
+    ts[0] = pb ? ps : (b[0] ? v : ts[0]);
+    tk[0] = pb ? pk : (b[0] ? key : tk[0]);
+  };
+  // the query's buffered candidates -> its list (cq added here: the buffer holds y)
+  auto insert_buffer = [&](int n) {
+    for (int i = 0; i < n; ++i) {
+      const float v = cs_l[qslot * CB + i] + cq;
+      const uint32_t k2 = a.key_base | (uint32_t)(r0 + ck_l[qslot * CB + i]);
+      if (better(v, k2, last_s(), last_k())) dist_insert(v, k2);
+    }
+  };
+  auto drain = [&]() {
+    publish_counts();
+    const int n = qvalid ? cnt_l[qslot] : 0;
+    insert_buffer(n);
+    const float ls = last_s();
+    const uint32_t lk = last_k();
+    if (owner) {
+      if (a.gthr && lk != KEY_NONE && score_key(ls) > published) {
+        published = score_key(ls);
+        atomicMax(a.gthr + qi, published);
+      }
+      float t = gs;
+      if (lk != KEY_NONE) t = fmaxf(t, ls);
+      if (a.dbg) atomicAdd(a.dbg + 2, 1u);  // measurement only: drains
+      thr_l[qslot] = t;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cnt[i] = 0;
+    __builtin_amdgcn_wave_barrier();
+    load_thr();
+  };
+
+  cb.mark(6);
+  const int rmask = max(1, (a.pub_mask + 1) / STEP) - 1;
+  for (int st = 0; st < nt; ++st) {
+    if (STEP == 2 && (st & 1)) goto compute;
+    {
+    const int last = min(st + STEP, nt) - 1;
+    wait_vm_le<3 * (NST - 2)>(lpt * max(0, min(NST - 2 * STEP, nt - 1 - last)));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    cb.mark(0);
+    if (a.gthr && ((st / STEP) & rmask) == rmask && wave_active) {
+      // shared-bound refresh (filter16): take the bound read by the previous refresh, publish the
+      // list's K1-th best, read the bound again
+      const bool landed = bst >= 0 && st - bst >= NST - 2;
+      const float ls = last_s();
+      const uint32_t lk = last_k();
+      if (owner) {
+        if (landed) {
+          const float gv = key_score(bounds_l[64 * w + c16]);
+          if (gv > gs) {
+            gs = gv;
+            thr_l[qslot] = fmaxf(thr_l[qslot], gs);
+            if (a.dbg) atomicAdd(a.dbg + 3, 1u);
+          }
+        }
+        if (lk != KEY_NONE && score_key(ls) > published) {
+          published = score_key(ls);
+          atomicMax(a.gthr + qi, published);
+        }
+      }
+      if (landed || bst < 0) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        glds<5>(a.gthr + (qi >= 0 ? qi : 0), (uint32_t)(size_t)(lds_void *)bounds_l + 256 * w);
+        bst = st;
+      }
+      __builtin_amdgcn_wave_barrier();
+      load_thr();
+    }
+#pragma unroll
+    for (int u = 0; u < STEP; ++u)
+      if (st + NST - STEP + u < nt) issue(st + NST - STEP + u);
+    cb.mark(1);
+    }
+  compute:
+    if (!wave_active) continue;
+    cb.acc[7] += 1;
+    const char *slot = ring + (st % NST) * SLOT;
+    if (a.ablate & 128) {
+      sink += reinterpret_cast<const float *>(slot + TB)[lane & 31];
+      continue;
+    }
+    f4v acc[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[b][i] = 0.0f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const h8v xh = *reinterpret_cast<const h8v *>(slot + ((4 * s + g) * 32 + 16 * b + c16) * 16);
+        if (Q2) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ql[s], xh, acc[b], 0, 0, 0);  // small term first
+        acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qh[s], xh, acc[b], 0, 0, 0);
+      }
+    const float *mrow = reinterpret_cast<const float *>(slot + TB);
+    float y[2][4];
+    uint64_t bm[2][4];
+    uint64_t anyb = 0;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int row = r0 + st * RT16 + 16 * b + c16;
+      float m = mrow[16 * b + c16];
+      if (row >= it.row_end || (uint32_t)row >= a.row_limit) m = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        y[b][i] = fmaf(f[i], acc[b][i], m);
+        bm[b][i] = __ballot(y[b][i] >= thr[i]);
+        anyb |= bm[b][i];
+      }
+    }
+    cb.mark(2);
+    if (a.ablate & 64) {
+      sink += anyb ? y[0][0] : 0.0f;
+      continue;
+    }
+    if (anyb == 0) continue;
+    if (a.dbg) {
+      int ns = 0;
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ns += __builtin_popcountll(bm[b][i]);
+      if (lane == 0) {
+        atomicAdd(a.dbg + 1, (uint32_t)ns);
+        atomicAdd(a.dbg, 1u);
+      }
+    }
+    // survivors -> the queries' LDS buffers: query 4g + i's survivors of half b are the bits of
+    // bm[b][i] in lane group g; a survivor's slot is its rank among them
+    const uint64_t below = (1ull << (16 * g)) - 1ull;  // lanes of the lower groups
+    int cmax = 0;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const uint16_t off = (uint16_t)(st * RT16 + 16 * b + c16);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint64_t mk = bm[b][i];
+        if (mk == 0) continue;
+        const int grp = __builtin_popcountll((mk >> (16 * g)) & 0xFFFFull);
+        const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u)) -
+                         __builtin_popcountll(mk & below);
+        if ((mk >> lane) & 1) {
+          const int q = 16 * w + 4 * g + i;
+          const int idx = cnt[i] + rank;
+          cs_l[q * CB + idx] = y[b][i];
+          ck_l[q * CB + idx] = off;
+        }
+        cnt[i] += grp;
+        cmax = max(cmax, cnt[i]);
+      }
+    }
+    cb.mark(3);
+    if (!__any(cmax > CB - RT16)) continue;
+    drain();
+    cb.mark(4);
+  }
+  publish_counts();
+  insert_buffer(qvalid ? cnt_l[qslot] : 0);
+  if (qvalid) {
+    const float ls = last_s();
+    const uint32_t lk = last_k();
+    if (owner && a.gthr && lk != KEY_NONE && score_key(ls) > published) atomicMax(a.gthr + qi, score_key(ls));
+    float *ps = a.part_s + (size_t)oslot * KR + R * g;
+    uint32_t *pk = a.part_k + (size_t)oslot * KR + R * g;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      ps[j] = ts[j];
+      pk[j] = tk[j];
+    }
+    if ((a.ablate & (64 | 128)) && g == 0) ps[0] = sink;
+  }
+  cb.flush(a.tdbg, lane);
+}
+
 inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
 // ring depth of the D = 128, K1 = 16 kernels (PYR_F16_NST, measurement knob: 3, 4 or 0 = deepest)
@@ -522,11 +890,23 @@ static int f16_step() {
   return e ? atoi(e) : 2;
 }
 
+// 8 waves x 16 queries (mfma_filter16w) for K1 = 16 (PYR_F16_WIDE: 1 = on, 0 = the 4 x 32 kernel)
+static int f16_wide() {
+  const char *e = getenv("PYR_F16_WIDE");
+  return e ? atoi(e) : 1;
+}
+
 template <int D, int MET, int KR, bool Q2>
 void launch16_p(const FilterArgs &a, int max_items, hipStream_t st) {
   // all LDS is static (79 KiB at D = 128): no dynamic-LDS attribute (a 160 KiB dynamic limit on top
   // of the static size makes the launch invalid)
   const int grid = a.xcd ? (max_items + 7) / 8 * 8 : max_items;
+  if constexpr (KR == 16) {  // (K1 = 32 needs more than the 128 VGPRs of four waves per SIMD)
+    if (f16_wide()) {
+      hipLaunchKernelGGL((mfma_filter16w<D, MET, KR, Q2, 4, 2>), dim3(grid), dim3(512), 0, st, a);
+      return;
+    }
+  }
   if constexpr (KR == 16) {  // the K1 = 16 list scans: two tiles per barrier (default)
     if (f16_step() == 2) {
       hipLaunchKernelGGL((mfma_filter16<D, MET, KR, Q2, 4, 2>), dim3(grid), dim3(256), 0, st, a);
