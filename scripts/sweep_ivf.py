@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("knobs", nargs="*", help="NAME=v1,v2,...")
+    ap.add_argument("--cfg", action="append", default=[],
+                    help="one setting 'NAME=v,NAME2=v2' (repeatable; run after the knob grid)")
     args = ap.parse_args()
 
     import torch
@@ -60,10 +62,16 @@ def main():
     for kv in args.knobs:
         name, vals = kv.split("=", 1)
         settings = [dict(d, **{name: v}) for d in settings for v in vals.split(",")]
+    for c in args.cfg:
+        settings.append(dict(kv.split("=", 1) for kv in c.split(",") if kv))
     ref = None
+    touched = set()
     for cfg in settings:
+        for kname in touched - set(cfg):
+            os.environ.pop(kname, None)
         for kname, v in cfg.items():
             os.environ[kname] = v
+            touched.add(kname)
         run()
         torch.cuda.synchronize()
         t = time.perf_counter()
