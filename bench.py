@@ -304,7 +304,10 @@ def run(args):
     prec = int(os.environ.get("PYR_FILTER_PREC", "2")) if filt else -1
     mfma_mult, mfma_peak = {2: (2, BF16_PEAK_TFLOPS), 3: (1, BF16_PEAK_TFLOPS), 1: (3, BF16_PEAK_TFLOPS),
                             0: (1, FP32_PEAK_TFLOPS)}.get(prec, (1, FP32_PEAK_TFLOPS))
-    kernel_name = {2: "mfma_filter16<128,L2,16,f16x2> (IVF list scan, fp16 residual tiles, 2 fp16 MFMAs per k-step)",
+    wide = os.environ.get("PYR_F16_WIDE", "1") != "0"
+    kernel_name = {2: ("mfma_filter16w<128,L2,16,f16x2> (IVF list scan, fp16 residual tiles, 8 waves x 16 queries, "
+                       "2 v_mfma_f32_16x16x32_f16 per k-step)") if wide else
+                      "mfma_filter16<128,L2,16,f16x2> (IVF list scan, fp16 residual tiles, 2 fp16 MFMAs per k-step)",
                    3: "mfma_filter16<128,L2,16,f16x1> (IVF list scan, fp16 residual tiles, 1 fp16 MFMA per k-step)",
                    1: "mfma_filter<128,L2,IVF> (IVF list scan, bf16x3 MFMA candidate filter)",
                    0: "mfma_filter<128,L2,IVF> (IVF list scan, fp32 MFMA candidate filter)"}.get(
@@ -391,8 +394,9 @@ def run(args):
     if os.path.exists(tpath) and world == 1 and prec == 2:
         tj = json.load(open(tpath))
         tc = tj.get("config", {})
-        if (tc.get("n"), tc.get("dim"), tc.get("nlist"), tc.get("nprobe"), tc.get("k"), tc.get("nq")) == \
-                (N, D, args.nlist, args.nprobe, k, args.nq):
+        same_kernel = ("filter16w" in tj.get("kernel", "")) == wide
+        if same_kernel and (tc.get("n"), tc.get("dim"), tc.get("nlist"), tc.get("nprobe"), tc.get("k"),
+                            tc.get("nq")) == (N, D, args.nlist, args.nprobe, k, args.nq):
             traffic, traffic_src = tj["hbm_read_bytes_per_launch"], tj["source"]
 
     if rank == 0:

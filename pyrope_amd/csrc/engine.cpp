@@ -380,7 +380,7 @@ static bool filter_enabled() {
 }
 static int filter_pub_mask() {  // FilterArgs::pub_mask; PYR_FILTER_PUB overrides (2^n - 1)
   const char *e = getenv("PYR_FILTER_PUB");
-  return e ? atoi(e) : 7;
+  return e ? atoi(e) : 15;  // 15 vs 7: I1 list scan 2.88 -> 2.81 ms (profiles/r2_wide/sweep_knobs_ablations.log)
 }
 // approximate-score arithmetic of the filter: bf16x3 (default) or fp32 (PYR_FILTER_PREC=0)
 static int filter_prec() {
@@ -1546,6 +1546,7 @@ struct IvfFlatIndex : Index {
     fa.waves = waves;
     fa.xcd = filter_xcd();
     fa.single = getenv("PYR_FILTER_SB") ? atoi(getenv("PYR_FILTER_SB")) != 0 : 0;
+    fa.prio = getenv("PYR_F16_PRIO") ? atoi(getenv("PYR_F16_PRIO")) : 0;
     fa.h16 = lists.h16.p;
     fa.meta = lists.meta.as<float>();
     fa.sx = lists.sx;

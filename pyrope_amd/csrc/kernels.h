@@ -276,6 +276,7 @@ struct FilterArgs {
   const float *meta;       // per row: L2 -|x|^2, IP 0, -inf dead / padding (RowStore::meta)
   float sx;                // the store's power-of-two fp16 scale
   const float *cents;      // IVF residual tiles: list centroids (row-major), item.list selects; null = raw rows
+  int32_t prio;              // filter16w: 1 = s_setprio 1 for waves 4-7 (PYR_F16_PRIO, measurement knob)
   unsigned long long *tdbg;  // measurement only (PYR_FILTER_DEBUG=2, filter16): per-wave cycle buckets
                              // [wait, refresh, compute, append, drain, total, prologue, wave-tiles]
 };

@@ -610,8 +610,9 @@ __global__ void norms_kernel(const float *x, int64_t n, int dim, int blocked, fl
 // ---------------------------------------------------------------------------
 // Merge of sorted partial lists: one wave per query, k rounds of wave argmax.
 // ---------------------------------------------------------------------------
-constexpr int MERGE_U = MAX_PARTS / 64;  // parts per lane
-
+// MERGE_U: parts per lane, a compile-time bound (1..16) chosen from nparts at launch, so that
+// the per-round scan over a lane's heads touches only the slots that can exist
+template <int MERGE_U>
 __global__ __launch_bounds__(256) void merge_keys_kernel(const float *ps, const uint32_t *pk, int64_t nq, int nparts,
                                                          int k, const int64_t *row_labels, const int64_t *buf_labels,
                                                          float *out_s, int64_t *out_l, int32_t *out_keys,
@@ -698,17 +699,19 @@ __global__ __launch_bounds__(256) void merge_keys_kernel(const float *ps, const 
   }
 }
 
+constexpr int MERGE_LU = MAX_PARTS / 64;  // parts per lane (merge_labels_kernel)
+
 __global__ __launch_bounds__(256) void merge_labels_kernel(const float *ps, const int64_t *pl, int64_t nq, int nparts,
                                                            int k, float *out_s, int64_t *out_l) {
   const int lane = threadIdx.x & 63;
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= nq) return;
-  int h[MERGE_U];
-  float cs[MERGE_U];
-  int64_t cl[MERGE_U];
+  int h[MERGE_LU];
+  float cs[MERGE_LU];
+  int64_t cl[MERGE_LU];
   const size_t base = (size_t)q * nparts * k;
 #pragma unroll
-  for (int u = 0; u < MERGE_U; ++u) {
+  for (int u = 0; u < MERGE_LU; ++u) {
     const int p = lane + 64 * u;
     h[u] = 0;
     cs[u] = p < nparts ? ps[base + (size_t)p * k] : -INFINITY;
@@ -719,7 +722,7 @@ __global__ __launch_bounds__(256) void merge_labels_kernel(const float *ps, cons
     float bs = -INFINITY;
     int64_t bl = -1;
 #pragma unroll
-    for (int u = 0; u < MERGE_U; ++u)
+    for (int u = 0; u < MERGE_LU; ++u)
       if (cl[u] >= 0 && (bl < 0 || better64(cs[u], cl[u], bs, bl))) {
         bs = cs[u];
         bl = cl[u];
@@ -739,7 +742,7 @@ __global__ __launch_bounds__(256) void merge_labels_kernel(const float *ps, cons
       out_l[(size_t)q * k + r] = bl;
     }
 #pragma unroll
-    for (int u = 0; u < MERGE_U; ++u)
+    for (int u = 0; u < MERGE_LU; ++u)
       if (cl[u] == bl && cs[u] == bs) {
         const int p = lane + 64 * u;
         h[u]++;
@@ -763,6 +766,59 @@ __global__ void ivf_count_kernel(const int32_t *probes, int64_t nq, int nprobe, 
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int np = pe - pb;
   if (i < nq * np) atomicAdd(&cnt[probes[(i / np) * nprobe + pb + i % np]], 1);
+}
+
+// The same two passes with block-local LDS histograms (nlist <= IVF_LDS_BINS): a block takes
+// IVF_EPB consecutive (query, probe) entries, counts them per list in LDS and adds each non-empty
+// bin to the global count once; the fill pass reserves one range per (block, list) with one global
+// atomic and places entries by their LDS rank.  320k entries into 1,024 lists: ~80k global atomics
+// instead of 320k on 1,024 addresses.  (Entry order inside a list differs from the one-atomic-per-
+// entry pass; it is arbitrary in both, and results do not depend on it.)
+constexpr int IVF_LDS_BINS = 16384, IVF_EPT = 16, IVF_EPB = 256 * IVF_EPT;
+
+__global__ __launch_bounds__(256) void ivf_count_lds_kernel(const int32_t *probes, int64_t nq, int nprobe, int pb,
+                                                            int pe, int nlist, int32_t *cnt) {
+  extern __shared__ int hist[];
+  const int np = pe - pb;
+  const int64_t n = nq * np, e0 = (int64_t)blockIdx.x * IVF_EPB;
+  for (int i = threadIdx.x; i < nlist; i += 256) hist[i] = 0;
+  __syncthreads();
+  for (int j = 0; j < IVF_EPT; ++j) {
+    const int64_t i = e0 + j * 256 + threadIdx.x;
+    if (i < n) atomicAdd(&hist[probes[(i / np) * nprobe + pb + i % np]], 1);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nlist; i += 256)
+    if (hist[i]) atomicAdd(&cnt[i], hist[i]);
+}
+
+__global__ __launch_bounds__(256) void ivf_fill_lds_kernel(const int32_t *probes, int64_t nq, int nprobe, int pb,
+                                                           int pe, int nparts, int cmax, int nlist,
+                                                           const int32_t *qoff, int32_t *fill, int32_t *qlist) {
+  extern __shared__ int hist[];
+  const int np = pe - pb;
+  const int64_t n = nq * np, e0 = (int64_t)blockIdx.x * IVF_EPB;
+  for (int i = threadIdx.x; i < nlist; i += 256) hist[i] = 0;
+  __syncthreads();
+  int lst[IVF_EPT], rank[IVF_EPT];
+#pragma unroll
+  for (int j = 0; j < IVF_EPT; ++j) {
+    const int64_t i = e0 + j * 256 + threadIdx.x;
+    lst[j] = i < n ? probes[(i / np) * nprobe + pb + i % np] : -1;
+    rank[j] = lst[j] >= 0 ? atomicAdd(&hist[lst[j]], 1) : 0;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nlist; i += 256)  // the block's range of each list
+    if (hist[i]) hist[i] = qoff[i] + atomicAdd(&fill[i], hist[i]);
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < IVF_EPT; ++j) {
+    if (lst[j] < 0) continue;
+    const int64_t i = e0 + j * 256 + threadIdx.x;
+    const int64_t q = i / np;
+    const int p = pb + (int)(i % np);
+    qlist[hist[lst[j]] + rank[j]] = (int32_t)(q * nparts + p * cmax);  // chunk c adds c (ScanItem.part)
+  }
 }
 
 // chunks of list `lst` that launch phase `phase` scans (IvfChunking, kernels.h)
@@ -1561,8 +1617,19 @@ void launch_merge_keys(const float *ps, const uint32_t *pk, int64_t nq, int32_t 
                        int32_t *out_keys, int32_t *out_cnt, hipStream_t st, const MergeIvf *ivf) {
   if (nq <= 0) return;
   const MergeIvf iv = ivf ? *ivf : MergeIvf{};
-  hipLaunchKernelGGL(merge_keys_kernel, dim3(nblk(nq, 4)), dim3(256), 0, st, ps, pk, nq, nparts, k, row_labels,
-                     buf_labels, out_s, out_l, out_keys, out_cnt, iv);
+  const dim3 g(nblk(nq, 4)), b(256);
+  if (nparts <= 64)
+    hipLaunchKernelGGL(merge_keys_kernel<1>, g, b, 0, st, ps, pk, nq, nparts, k, row_labels, buf_labels, out_s, out_l,
+                       out_keys, out_cnt, iv);
+  else if (nparts <= 128)
+    hipLaunchKernelGGL(merge_keys_kernel<2>, g, b, 0, st, ps, pk, nq, nparts, k, row_labels, buf_labels, out_s, out_l,
+                       out_keys, out_cnt, iv);
+  else if (nparts <= 256)
+    hipLaunchKernelGGL(merge_keys_kernel<4>, g, b, 0, st, ps, pk, nq, nparts, k, row_labels, buf_labels, out_s, out_l,
+                       out_keys, out_cnt, iv);
+  else
+    hipLaunchKernelGGL(merge_keys_kernel<MAX_PARTS / 64>, g, b, 0, st, ps, pk, nq, nparts, k, row_labels, buf_labels,
+                       out_s, out_l, out_keys, out_cnt, iv);
 }
 
 void launch_merge_labels(const float *ps, const int64_t *pl, int64_t nq, int32_t nparts, int32_t k, float *out_s,
@@ -1582,15 +1649,23 @@ void launch_ivf_items(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t
                       int phase, IvfItemWs &ws, hipStream_t st, int32_t pb, int32_t pe) {
   if (pe < 0) pe = nprobe;
   const int64_t n = nq * (pe - pb);
+  const bool lds = nlist <= IVF_LDS_BINS && !getenv("PYR_IVF_GLOBAL_HIST");  // (knob: measurement only)
+  const size_t hb = sizeof(int) * (size_t)nlist;
   if (phase == 0) {
     (void)hipMemsetAsync(ws.cnt, 0, sizeof(int32_t) * nlist, st);
     (void)hipMemsetAsync(ws.fill, 0, sizeof(int32_t) * nlist, st);
-    if (n > 0)
+    if (n > 0 && lds)
+      hipLaunchKernelGGL(ivf_count_lds_kernel, dim3(nblk(n, IVF_EPB)), dim3(256), hb, st, probes, nq, nprobe, pb, pe,
+                         nlist, ws.cnt);
+    else if (n > 0)
       hipLaunchKernelGGL(ivf_count_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, probes, nq, nprobe, pb, pe, ws.cnt);
   }
   hipLaunchKernelGGL(ivf_scan_kernel, dim3(1), dim3(1024), 0, st, ws.cnt, nlist, qchunk, list_begin, list_end, ch,
                      phase, ws.qoff, ws.ioff, ws.n_items);
-  if (phase == 0 && n > 0)
+  if (phase == 0 && n > 0 && lds)
+    hipLaunchKernelGGL(ivf_fill_lds_kernel, dim3(nblk(n, IVF_EPB)), dim3(256), hb, st, probes, nq, nprobe, pb, pe,
+                       nparts, ch.cmax, nlist, ws.qoff, ws.fill, ws.qlist);
+  else if (phase == 0 && n > 0)
     hipLaunchKernelGGL(ivf_fill_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, probes, nq, nprobe, pb, pe, nparts,
                        ch.cmax, ws.qoff, ws.fill, ws.qlist);
   hipLaunchKernelGGL(ivf_items_kernel, dim3(nblk(nlist, 256)), dim3(256), 0, st, ws.cnt, ws.qoff, ws.ioff, nlist,
