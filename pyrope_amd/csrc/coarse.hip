@@ -236,9 +236,14 @@ void launch_coarse_dense(const float *q, const float *cents_rm, const float *qn,
   // register lists for nprobe <= 64 (PYR_COARSE_SELECT=0: the LDS argmax rounds, measurement knob)
   const bool reg = !getenv("PYR_COARSE_SELECT") || atoi(getenv("PYR_COARSE_SELECT")) != 0;
   const dim3 g4((unsigned)((nq + 3) / 4));
-  if (reg && nprobe <= 16) {
+  // a lane sees every 64th centroid, so its list never needs more than ceil(nlist / 64) entries: the
+  // wave's P pops then still find every key (nlist = 1,024: 16-entry lists for nprobe = 32)
+  const int per_lane = (nlist + 63) / 64;
+  if (reg && nprobe <= 64 && per_lane <= 8) {
+    hipLaunchKernelGGL(coarse_select_reg_kernel<8>, g4, dim3(256), 0, st, scores, nq, nlist, nprobe, probes);
+  } else if (reg && (nprobe <= 16 || (nprobe <= 64 && per_lane <= 16))) {
     hipLaunchKernelGGL(coarse_select_reg_kernel<16>, g4, dim3(256), 0, st, scores, nq, nlist, nprobe, probes);
-  } else if (reg && nprobe <= 32) {
+  } else if (reg && (nprobe <= 32 || (nprobe <= 64 && per_lane <= 32))) {
     hipLaunchKernelGGL(coarse_select_reg_kernel<32>, g4, dim3(256), 0, st, scores, nq, nlist, nprobe, probes);
   } else if (reg && nprobe <= 64) {
     hipLaunchKernelGGL(coarse_select_reg_kernel<64>, g4, dim3(256), 0, st, scores, nq, nlist, nprobe, probes);
