@@ -68,12 +68,14 @@ __device__ __forceinline__ void reg_insert(float (&s)[KR], uint32_t (&kk)[KR], f
 // thresholds [128], counts [128], candidate scores [128][CB16], keys [128][CB16] as row offsets in
 // the item (u16: items span at most 65536 rows, filter16_max_rows()), the shared bounds [4][64].
 // NST is as deep as two blocks per CU allow (80 KiB each): 5 at D = 128, 8 below.
-struct F16State {
+template <int CB>
+struct F16StateT {
   float thr[128];
   int cnt[128];
-  float cs[128 * CB16];
-  uint16_t ck[128 * CB16];
+  float cs[128 * CB];
+  uint16_t ck[128 * CB];
 };
+using F16State = F16StateT<CB16>;
 template <int D, int NSTC = 0>  // NSTC: ring depth (0 = as deep as the LDS budget allows, capped at 8)
 struct F16Lds {
   static constexpr int TB = RT16 * D * 2;               // h16 bytes per tile
@@ -521,13 +523,17 @@ __global__ __launch_bounds__(256, 2) void mfma_filter16(FilterArgs a) {
 //
 // C layout (16x16x32): register i of lane (c = lane & 15, g = lane >> 4) is query 4g + i of the
 // wave, data row c of the 16-row half b.  A operand: lane (c, g) holds query c, dims 32s + 8g .. +7.
-template <int D, int MET, int KR, bool Q2, int NSTC, int STEP>
+// CB: candidate buffer entries per query (>= 32 + the drain threshold CB - 32).  Measured and not
+// kept: CB = 40 with a 5-slot ring (3.04 vs 2.75 ms), CB = 32 with pre-drains and a 6-slot ring
+// (3.31 vs 3.08 ms) -- more tiles in flight do not shorten the scan (profiles/r2_wide/).
+template <int D, int MET, int KR, bool Q2, int NSTC, int STEP, int CB = CB16>
 __global__ __launch_bounds__(512, 4) void mfma_filter16w(FilterArgs a) {
   constexpr int NW = 8;
   constexpr int TB = RT16 * D * 2;                    // h16 bytes per tile
   constexpr int NCH = TB / 1024;                      // 1 KiB pieces per tile (2, 4 or 8)
   constexpr int SLOT = TB + 256;                      // tile + meta
-  constexpr int STATE = (int)sizeof(F16State);
+  constexpr int STATE = (int)sizeof(F16StateT<CB>);
+  static_assert(CB > RT16, "a tile may add 32 survivors per query");
   constexpr int BOUNDS = NW * 256;
   constexpr int NST_MAX0 = (80 * 1024 - STATE - BOUNDS) / SLOT;
   constexpr int NST_MAX = NST_MAX0 > 8 ? 8 : NST_MAX0;
@@ -538,10 +544,9 @@ __global__ __launch_bounds__(512, 4) void mfma_filter16w(FilterArgs a) {
   static_assert(KR % 4 == 0, "top-K1 spread over 4 lanes");
   constexpr int KS = D / 32;  // 16x16x32 k-steps
   constexpr int R = KR / 4;   // top-K1 entries per lane
-  constexpr int CB = CB16;
   __shared__ __attribute__((aligned(16))) char ring[NST * SLOT];
   __shared__ __attribute__((aligned(16))) uint32_t bounds_l[BOUNDS / 4];
-  __shared__ __attribute__((aligned(16))) F16State state16;
+  __shared__ __attribute__((aligned(16))) F16StateT<CB> state16;
   const uint32_t ring_base = (uint32_t)(size_t)(lds_void *)ring;
   float *const thr_l = state16.thr;
   int *const cnt_l = state16.cnt;
