@@ -1546,7 +1546,8 @@ struct IvfFlatIndex : Index {
     fa.waves = waves;
     fa.xcd = filter_xcd();
     fa.single = getenv("PYR_FILTER_SB") ? atoi(getenv("PYR_FILTER_SB")) != 0 : 0;
-    fa.prio = getenv("PYR_F16_PRIO") ? atoi(getenv("PYR_F16_PRIO")) : 0;
+    // 2: a wave with survivors appends at raised priority (I1 list scan -1.5 %, profiles/r2_wide/)
+    fa.prio = getenv("PYR_F16_PRIO") ? atoi(getenv("PYR_F16_PRIO")) : 2;
     fa.h16 = lists.h16.p;
     fa.meta = lists.meta.as<float>();
     fa.sx = lists.sx;

@@ -826,6 +826,9 @@ __global__ __launch_bounds__(512, 4) void mfma_filter16w(FilterArgs a) {
       continue;
     }
     if (anyb == 0) continue;
+    // PYR_F16_PRIO=2 (default): a wave with survivors to append runs at raised priority, so the
+    // block's slowest wave reaches the next barrier sooner
+    if (a.prio == 2) __builtin_amdgcn_s_setprio(2);
     if (a.dbg) {
       int ns = 0;
 #pragma unroll
@@ -862,8 +865,8 @@ __global__ __launch_bounds__(512, 4) void mfma_filter16w(FilterArgs a) {
       }
     }
     cb.mark(3);
-    if (!__any(cmax > CB - RT16)) continue;
-    drain();
+    if (__any(cmax > CB - RT16)) drain();
+    if (a.prio == 2) __builtin_amdgcn_s_setprio(0);
     cb.mark(4);
   }
   publish_counts();
