@@ -402,10 +402,13 @@ static int filter_prec_for(int prec, bool f16_store, int64_t max_item_rows) {
 // PYR_FILTER_WAVES=8 -> 256-query items, one block per CU (bf16x3 only): half the row
 // traffic but measured slower, 4.98 -> 7.42 ms at the bench config (profiles/r1_sweeps/sweep23).
 // FLAT items always use 4.
-static int filter_waves_ivf() {
+// waves per IVF filter block: 8 (bf16x3, 256-query items), 16 (fp16 tiles, K1 = 16 only: 256-query
+// items on the 16-wave mfma_filter16w), else 4 (128-query items)
+static int filter_waves_ivf(int k1, int prec) {
   const char *e = getenv("PYR_FILTER_WAVES");
   const int w = e ? atoi(e) : 4;
-  return (w == 8 && filter_prec() == FILTER_BF16X3) ? 8 : 4;
+  if (w == 16 && prec16(prec) && k1 == 16) return 16;
+  return (w == 8 && prec == FILTER_BF16X3) ? 8 : 4;
 }
 // XCD-major mapping of IVF filter items (FilterArgs::xcd); PYR_FILTER_XCD=0 disables it
 static int filter_xcd() {
@@ -1511,8 +1514,9 @@ struct IvfFlatIndex : Index {
     ws.part_s.ensure(sizeof(float) * np);
     ws.part_k.ensure(sizeof(uint32_t) * np);
     uint32_t *gthr = shared_bounds(ws, nq);
-    const int waves = filter_waves_ivf();
-    const int qc = filter_qchunk(filter_prec(), waves);
+    const int prec_used = filter_prec_for(filter_prec(), lists.f16, std::max(ch.chunk, ch.warm));
+    const int waves = filter_waves_ivf(k1, prec_used);
+    const int qc = filter_qchunk(prec_used, waves);
     int maxi, maxi_main = 0;
     {
       PhaseTimer t(PH_ITEMS, ws.st);
@@ -1542,7 +1546,7 @@ struct IvfFlatIndex : Index {
     fa.gthr = gthr;
     fa.ablate = filter_ablate();
     fa.pub_mask = filter_pub_mask();
-    fa.prec = filter_prec_for(filter_prec(), lists.f16, std::max(ch.chunk, ch.warm));
+    fa.prec = prec_used;
     fa.waves = waves;
     fa.xcd = filter_xcd();
     fa.single = getenv("PYR_FILTER_SB") ? atoi(getenv("PYR_FILTER_SB")) != 0 : 0;

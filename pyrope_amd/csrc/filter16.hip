@@ -68,12 +68,12 @@ __device__ __forceinline__ void reg_insert(float (&s)[KR], uint32_t (&kk)[KR], f
 // thresholds [128], counts [128], candidate scores [128][CB16], keys [128][CB16] as row offsets in
 // the item (u16: items span at most 65536 rows, filter16_max_rows()), the shared bounds [4][64].
 // NST is as deep as two blocks per CU allow (80 KiB each): 5 at D = 128, 8 below.
-template <int CB>
+template <int CB, int NQ = 128>
 struct F16StateT {
-  float thr[128];
-  int cnt[128];
-  float cs[128 * CB];
-  uint16_t ck[128 * CB];
+  float thr[NQ];
+  int cnt[NQ];
+  float cs[NQ * CB];
+  uint16_t ck[NQ * CB];
 };
 using F16State = F16StateT<CB16>;
 template <int D, int NSTC = 0>  // NSTC: ring depth (0 = as deep as the LDS budget allows, capped at 8)
@@ -526,16 +526,17 @@ __global__ __launch_bounds__(256, 2) void mfma_filter16(FilterArgs a) {
 // CB: candidate buffer entries per query (>= 32 + the drain threshold CB - 32).  Measured and not
 // kept: CB = 40 with a 5-slot ring (3.04 vs 2.75 ms), CB = 32 with pre-drains and a 6-slot ring
 // (3.31 vs 3.08 ms) -- more tiles in flight do not shorten the scan (profiles/r2_wide/).
-template <int D, int MET, int KR, bool Q2, int NSTC, int STEP, int CB = CB16>
-__global__ __launch_bounds__(512, 4) void mfma_filter16w(FilterArgs a) {
-  constexpr int NW = 8;
+// NW: waves per block, 8 (128-query items, two blocks per CU) or 16 (256-query items, one block per
+// CU: each streamed tile serves twice the queries; PYR_FILTER_WAVES=16, measurement).
+template <int D, int MET, int KR, bool Q2, int NSTC, int STEP, int CB = CB16, int NW = 8>
+__global__ __launch_bounds__(64 * NW, 4) void mfma_filter16w(FilterArgs a) {
   constexpr int TB = RT16 * D * 2;                    // h16 bytes per tile
   constexpr int NCH = TB / 1024;                      // 1 KiB pieces per tile (2, 4 or 8)
   constexpr int SLOT = TB + 256;                      // tile + meta
-  constexpr int STATE = (int)sizeof(F16StateT<CB>);
+  constexpr int STATE = (int)sizeof(F16StateT<CB, 16 * NW>);
   static_assert(CB > RT16, "a tile may add 32 survivors per query");
   constexpr int BOUNDS = NW * 256;
-  constexpr int NST_MAX0 = (80 * 1024 - STATE - BOUNDS) / SLOT;
+  constexpr int NST_MAX0 = ((NW == 8 ? 80 : 160) * 1024 - STATE - BOUNDS) / SLOT;
   constexpr int NST_MAX = NST_MAX0 > 8 ? 8 : NST_MAX0;
   constexpr int NST = NSTC > 0 && NSTC < NST_MAX ? NSTC : NST_MAX;
   static_assert(STEP == 1 || STEP == 2, "tiles per barrier");
@@ -546,7 +547,7 @@ __global__ __launch_bounds__(512, 4) void mfma_filter16w(FilterArgs a) {
   constexpr int R = KR / 4;   // top-K1 entries per lane
   __shared__ __attribute__((aligned(16))) char ring[NST * SLOT];
   __shared__ __attribute__((aligned(16))) uint32_t bounds_l[BOUNDS / 4];
-  __shared__ __attribute__((aligned(16))) F16StateT<CB> state16;
+  __shared__ __attribute__((aligned(16))) F16StateT<CB, 16 * NW> state16;
   const uint32_t ring_base = (uint32_t)(size_t)(lds_void *)ring;
   float *const thr_l = state16.thr;
   int *const cnt_l = state16.cnt;
@@ -913,6 +914,10 @@ void launch16_p(const FilterArgs &a, int max_items, hipStream_t st) {
   // of the static size makes the launch invalid)
   const int grid = a.xcd ? (max_items + 7) / 8 * 8 : max_items;
   if constexpr (KR == 16) {  // (K1 = 32 needs more than the 128 VGPRs of four waves per SIMD)
+    if (a.waves == 16) {  // 256-query items (engine filter_qchunk)
+      hipLaunchKernelGGL((mfma_filter16w<D, MET, KR, Q2, 4, 2, CB16, 16>), dim3(grid), dim3(1024), 0, st, a);
+      return;
+    }
     if (f16_wide()) {
       hipLaunchKernelGGL((mfma_filter16w<D, MET, KR, Q2, 4, 2>), dim3(grid), dim3(512), 0, st, a);
       return;

@@ -285,7 +285,11 @@ constexpr int FILTER_BF16X3 = 1;  // hi/lo bf16 split, 3 x v_mfma_f32_32x32x16_b
 constexpr int FILTER_F16X2 = 2;   // fp16 row tiles x two-term fp16 queries, 2 x v_mfma_f32_32x32x16_f16
 constexpr int FILTER_F16X1 = 3;   // fp16 row tiles x one-term fp16 queries, 1 MFMA per k-step
 // queries per filter work item (items must be built with this qchunk)
-inline int filter_qchunk(int prec, int waves) { return prec == FILTER_BF16X3 && waves == 8 ? 256 : 128; }
+inline int filter_qchunk(int prec, int waves) {
+  return (prec == FILTER_BF16X3 && waves == 8) || ((prec == FILTER_F16X2 || prec == FILTER_F16X1) && waves == 16)
+             ? 256
+             : 128;
+}
 // refine_kernel error-bound constant of the bf16x3 approximation (per u |q| max|x|)
 inline double filter_bf16x3_cerr(int dim, int metric) {
   // q.x: <= 3.02 * 2^-16 per product from the splits, <= 2u per addition over 3D terms;
