@@ -685,6 +685,9 @@ struct FlatIndex : Index {
   DevMem q8, q8s, q8ok;
   int64_t q8cap = 0;
   int dp;
+  // VectorMath form of the exact scores: 4 = the *Unsafe forms of BruteForceVectorIndex; 1 = the safe
+  // forms (ComputeScore of the IVF coarse step, when this store holds an index's centroids)
+  int exact_v = 4;
 
   explicit FlatIndex(const pyr_index_desc &d) : Index(d) {
     st.dim = dim;
@@ -889,7 +892,7 @@ struct FlatIndex : Index {
       else launch_filter(fa, metric, p.nitems, ws.st);
     }
     const int64_t nf =
-        filter_finish(ws, nq, p.nchunks, k1, k, dim, metric, 4, d_q, st, nullptr, d_s, d_l, d_c,
+        filter_finish(ws, nq, p.nchunks, k1, k, dim, metric, exact_v, d_q, st, nullptr, d_s, d_l, d_c,
                       centered ? st.rmax.as<uint32_t>() : nullptr, centered ? st.center.as<float>() : nullptr,
                       centered ? st.rmax_r.as<uint32_t>() : nullptr, fa.prec);
     const int k1_next = filter_k1_next(k, k1);
@@ -912,8 +915,8 @@ struct FlatIndex : Index {
     uint32_t *gthr = shared_bounds(ws, nq);
     {
       PhaseTimer t(PH_FLAT_SCAN, ws.st, nq * cutoff);
-      flat_scan(st, cutoff, p, d_q, metric == COS ? ws.qn.as<float>() : nullptr, nq, k, 4, metric, p.nchunks, 0, 0,
-                ws, ws.part_s.as<float>(), ws.part_k.as<uint32_t>(), false, gthr);
+      flat_scan(st, cutoff, p, d_q, metric == COS ? ws.qn.as<float>() : nullptr, nq, k, exact_v, metric, p.nchunks, 0,
+                0, ws, ws.part_s.as<float>(), ws.part_k.as<uint32_t>(), false, gthr);
     }
     PhaseTimer t(PH_MERGE, ws.st);
     launch_merge_keys(ws.part_s.as<float>(), ws.part_k.as<uint32_t>(), nq, p.nchunks, k, st.labels.as<int64_t>(),
@@ -1056,6 +1059,11 @@ struct Coarse {
   RowStore cs;
   DevMem rm;  // row-major centroids
   std::vector<float> host;
+  // optionally (PYR_COARSE_FILTER=1) the centroids once more as a FLAT store (fp16 tiles): the coarse
+  // ranking as a FLAT search with k = nprobe -- MFMA filter, then the exact safe-form scores
+  // (ComputeScore) of K1 candidates and the certificate, failures re-run exactly; ids and order
+  // equal the dense exact ranking
+  std::unique_ptr<FlatIndex> flat;
 
   void set(const float *d_cents_rm, int k, int dim, int met, hipStream_t st) {
     nlist = k;
@@ -1073,6 +1081,28 @@ struct Coarse {
     HIPCHK(hipMemcpyAsync(host.data(), d_cents_rm, sizeof(float) * k * dim, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     cs.n = k;
+    flat.reset();
+    if (filter_on() && met != COS && store16(dim, met)) {
+      pyr_index_desc d{};
+      d.kind = PYR_FLAT;
+      d.dim = dim;
+      d.metric = met;
+      HIPCHK(hipGetDevice(&d.device));
+      flat.reset(new FlatIndex(d));
+      flat->exact_v = 1;
+      std::vector<int64_t> ids((size_t)k);
+      for (int i = 0; i < k; ++i) ids[i] = i;
+      flat->add(host.data(), k, ids.data(), false);
+    }
+  }
+
+  // PYR_COARSE_FILTER=1 (read when the centroids are set): rank through the FLAT filter.  Same probes,
+  // but slower on the bench data (I1 coarse 2.4 vs 0.21 ms, M8 3.5 vs 1.65 ms: the coarse scores of
+  // uniform data are packed too tightly for the certificate at K1 = 64, so most queries re-run the
+  // exact scan); off by default (profiles/r2_wide/sweep_coarse_filter.log)
+  static bool filter_on() {
+    const char *e = getenv("PYR_COARSE_FILTER");
+    return e && atoi(e) != 0;
   }
 
   // score all centroids (ComputeScore, safe VectorMath), rank desc (ties by index), keep nprobe
@@ -1083,6 +1113,19 @@ struct Coarse {
       ws.probes.ensure(sizeof(int32_t) * nq * nprobe);
       HIPCHK(hipMemcpyAsync(ws.probes.p, ws.ext_probes, sizeof(int32_t) * nq * nprobe, hipMemcpyDeviceToDevice,
                             ws.st));
+      return;
+    }
+    const int k1 = filter_k1(nprobe);
+    if (flat && filter_enabled() && k1 > 0 && nprobe <= KMAX_FAST && nprobe <= nlist &&
+        filter_supported(cs.dim, met, k1)) {
+      // on the nested workspace (same stream): the caller may already hold partials and shared bounds
+      // in ws (the exact IVF search sets them up before ranking)
+      Workspace &cw = ws.nested();
+      cw.cpr_s.ensure(sizeof(float) * nq * nprobe);
+      cw.cpr_l.ensure(sizeof(int64_t) * nq * nprobe);
+      flat->search_filter(d_q, nq, nprobe, k1, nlist, cw.cpr_s.as<float>(), cw.cpr_l.as<int64_t>(), nullptr, cw);
+      ws.probes.ensure(sizeof(int32_t) * nq * nprobe);
+      launch_labels_to_i32(cw.cpr_l.as<int64_t>(), nq * nprobe, ws.probes.as<int32_t>(), ws.st);
       return;
     }
     const char *ce = getenv("PYR_COARSE_DENSE");  // 0: the top-k scan below (A/B only, same ranking)

@@ -114,6 +114,9 @@ __host__ __device__ inline float key_score(uint32_t k) {
   return v.f;
 }
 
+// int64 labels (centroid ids, -1 = none) -> int32 probe ids
+void launch_labels_to_i32(const int64_t *in, int64_t n, int32_t *out, hipStream_t st);
+
 // V = 1: VectorMath safe functions (one Vector accumulator; IVF paths, k-means).
 // V = 4: VectorMath *Unsafe functions (four accumulators; BruteForce head).
 void launch_scan(const ScanArgs &a, int metric, int V, int max_items, hipStream_t st);

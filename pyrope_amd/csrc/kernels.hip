@@ -1498,6 +1498,11 @@ __global__ void norms_slots_kernel(const float *rows, const int64_t *slots, int6
   const int64_t r = slots[i];
   out[r] = em_norm(Blk{rows, dim, r}, dim);
 }
+__global__ void labels_to_i32_kernel(const int64_t *in, int64_t n, int32_t *out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (int32_t)in[i];
+}
+
 __global__ void fill_results_kernel(float *s, int64_t *l, int32_t *c, int64_t nq, int k) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < nq * k) {
@@ -1630,6 +1635,11 @@ void launch_merge_keys(const float *ps, const uint32_t *pk, int64_t nq, int32_t 
   else
     hipLaunchKernelGGL(merge_keys_kernel<MAX_PARTS / 64>, g, b, 0, st, ps, pk, nq, nparts, k, row_labels, buf_labels,
                        out_s, out_l, out_keys, out_cnt, iv);
+}
+
+void launch_labels_to_i32(const int64_t *in, int64_t n, int32_t *out, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(labels_to_i32_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, in, n, out);
 }
 
 void launch_merge_labels(const float *ps, const int64_t *pl, int64_t nq, int32_t nparts, int32_t k, float *out_s,
