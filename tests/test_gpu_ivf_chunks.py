@@ -215,3 +215,22 @@ def test_both_list_scan_kernels(hiplib, oracle, metric, wide, prio, waves):
         ref = idx.search_batch(q, 10, opts)
     _same(got, ref)
     _check_oracle(oracle, idx, x, q, got, 10, metric, 16, 100)
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_coarse_ranking_through_flat_filter(hiplib, metric):
+    """PYR_COARSE_FILTER=1 (read when the centroids are set): the coarse step runs as a FLAT filter
+    search over the centroids (fp16 tiles, K1 = 64, exact safe-form refine = ComputeScore,
+    IvfFlatVectorIndex.cs:186-198).  The probes, hence the answers, equal the dense exact ranking."""
+    from pyrope_amd import IvfFlatVectorIndex, SearchOptions, generate_synthetic
+    x = generate_synthetic(40_000, 128, 42)
+    q = generate_synthetic(500, 128, 1337)
+    opts = SearchOptions(nprobe=32)
+    with _env(PYR_COARSE_FILTER=1):
+        idx = IvfFlatVectorIndex(128, metric, n_list=256)
+        idx.add_labels(np.arange(len(x), dtype=np.int64), x)
+        idx.build()
+        got = idx.search_batch(q, 10, opts)
+    with _env(PYR_FILTER=0):  # exact list scan and the dense exact coarse ranking
+        ref = idx.search_batch(q, 10, opts)
+    _same(got, ref)
