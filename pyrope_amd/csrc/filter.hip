@@ -538,7 +538,7 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
   // moves to lane c
   for (int p = 0; 8 * p < k1; ++p) {
     const int c = 8 * p + (lane >> 3);
-    const int32_t kc = c < k1 ? mk[c] : -1;
+    const int32_t kc = __shfl((int)key, c);  // (k1 <= 64: every candidate's key sits on lane c)
     const float sc = exact_score_l8<V, MET>(qp, a.rows, kc >= 0 ? (int64_t)kc : 0, D, lane & 7);
     const float t = __shfl(sc, 8 * (lane & 7));
     if ((lane >> 3) == p && key != KEY_NONE) s = t;
@@ -584,11 +584,17 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
       // FLAT (no probes): one center, list 0
       // 8 probes per pass, an 8-lane group per probe, lane j of it summing dims j, j + 8, ...
       const int np = a.probes ? a.nprobe : 1;
+      // probe ids of 64 probes at a time, one per lane, handed to the 8-lane groups by shuffle (no
+      // dependent id load inside the passes)
+      int pid = 0;
       for (int p0 = 0; p0 < np; p0 += 8) {
+        if ((p0 & 63) == 0)
+          pid = a.probes && p0 + lane < np ? a.probes[(size_t)q * a.nprobe + p0 + lane] : 0;
         const int p = p0 + (lane >> 3), j = lane & 7;
+        const int lp = __shfl(pid, (p0 & 63) + (lane >> 3));
         float d2 = 0.0f, c2 = 0.0f;
         if (p < np) {
-          const int l = a.probes ? a.probes[(size_t)q * a.nprobe + p] : 0;
+          const int l = lp;
           xrk = max(xrk, a.list_rmax_r[l]);
           xfk = max(xfk, a.list_rmax[l]);
           const float *c = a.cents + (size_t)l * D;
