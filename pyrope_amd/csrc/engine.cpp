@@ -302,14 +302,15 @@ struct ScanPlan {
   int chunk_rows = 0, nchunks = 0, nitems = 0, qchunk = QCHUNK;
 };
 
-static ScanPlan plan_flat(int64_t nrows, int64_t nq, int dim, int k, int max_parts) {
+static ScanPlan plan_flat(int64_t nrows, int64_t nq, int dim, int k, int max_parts, int qchunk = 0) {
   ScanPlan p;
-  p.qchunk = fast_path(dim, k) ? QCHUNK : QCHUNK_GENERIC;
+  p.qchunk = qchunk > 0 ? qchunk : fast_path(dim, k) ? QCHUNK : QCHUNK_GENERIC;
   const int64_t nqc = (nq + p.qchunk - 1) / p.qchunk;
   // ~2048 items = 4 full rounds of 512 resident blocks (256 CUs x 2); rounding DOWN keeps the
   // item count at or below that: rounding up (e.g. 79 query groups x 26 chunks = 2054 items)
-  // left a fifth round of 6 items that cost a whole item duration
-  int64_t want = std::max<int64_t>(1, 2048 / nqc);
+  // left a fifth round of 6 items that cost a whole item duration.  256-query items run one block
+  // per CU: 1024 items = 4 rounds.
+  int64_t want = std::max<int64_t>(1, (p.qchunk > QCHUNK ? 1024 : 2048) / nqc);
   want = std::min<int64_t>(want, std::max<int64_t>(1, nrows / 1024));
   want = std::min<int64_t>(want, max_parts);
   p.chunk_rows = (int)round_up((nrows + want - 1) / want, 32);  // whole fp16 tiles (filter16.hip)
@@ -852,7 +853,18 @@ struct FlatIndex : Index {
   // MFMA candidate filter over slots [0, cutoff), exact refine with the *Unsafe form (V = 4)
   void search_filter(const float *d_q, int64_t nq, int k, int k1, int64_t cutoff, float *d_s, int64_t *d_l,
                      int32_t *d_c, Workspace &ws) {
+    // 256-query items on 16-wave blocks (fp16 tiles, K1 = 16): each streamed tile serves twice the
+    // queries (PYR_FLAT_WAVES=16)
+    const char *fw = getenv("PYR_FLAT_WAVES");
+    int waves = 4;
     ScanPlan p = plan_flat(cutoff, nq, dim, k1, MAX_PARTS);
+    if (fw && atoi(fw) == 16 && k1 == 16 && nq > 128) {
+      const ScanPlan p16 = plan_flat(cutoff, nq, dim, k1, MAX_PARTS, 256);
+      if (prec16(filter_prec_for(filter_prec(), st.f16, p16.chunk_rows))) {
+        p = p16;
+        waves = 16;
+      }
+    }
     const size_t np = (size_t)nq * p.nchunks * k1;
     ws.part_s.ensure(sizeof(float) * np);
     ws.part_k.ensure(sizeof(uint32_t) * np);
@@ -879,7 +891,8 @@ struct FlatIndex : Index {
     fa.ablate = filter_ablate();
     fa.pub_mask = filter_pub_mask();
     fa.prec = filter_prec_for(filter_prec(), st.f16, p.chunk_rows);
-    fa.waves = 4;  // items of QCHUNK = 128 queries (plan_flat)
+    fa.waves = prec16(fa.prec) ? waves : 4;  // items of p.qchunk queries (plan_flat)
+    if (fa.waves == 16 && p.qchunk != 256) throw Error(PYR_E_STATE, "filter items / block size mismatch");
     fa.xcd = getenv("PYR_FLAT_XCD") ? atoi(getenv("PYR_FLAT_XCD")) != 0 : 0;  // measurement knob
     fa.h16 = st.h16.p;
     fa.meta = st.meta.as<float>();

@@ -564,8 +564,6 @@ __global__ __launch_bounds__(64 * NW, 4) void mfma_filter16w(FilterArgs a) {
   const ScanItem it = a.items[item];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int c16 = lane & 15, g = lane >> 4;
-  CycleBuckets cb;
-  cb.start(a.tdbg != nullptr);
 
   // ---- A operand: query 16w + c16, dims 32s + 8g .. +7 of k-step s, scaled and split ----
   const int qslot = 16 * w + c16;
@@ -737,8 +735,6 @@ __global__ __launch_bounds__(64 * NW, 4) void mfma_filter16w(FilterArgs a) {
     __builtin_amdgcn_wave_barrier();
     load_thr();
   };
-
-  cb.mark(6);
   // PYR_F16_PRIO=1: static priority for the younger half of the block (waves 4-7), the arbitration
   // loser of a SIMD's two waves of one block (MI355X_MICROARCH.md, two waves per SIMD, item 4)
   if (a.prio && w >= 4) __builtin_amdgcn_s_setprio(1);
@@ -750,7 +746,6 @@ __global__ __launch_bounds__(64 * NW, 4) void mfma_filter16w(FilterArgs a) {
     wait_vm_le<3 * (NST - 2)>(lpt * max(0, min(NST - 2 * STEP, nt - 1 - last)));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    cb.mark(0);
     if (a.gthr && ((st / STEP) & rmask) == rmask && wave_active) {
       // shared-bound refresh (filter16): take the bound read by the previous refresh, publish the
       // list's K1-th best, read the bound again
@@ -782,11 +777,9 @@ __global__ __launch_bounds__(64 * NW, 4) void mfma_filter16w(FilterArgs a) {
 #pragma unroll
     for (int u = 0; u < STEP; ++u)
       if (st + NST - STEP + u < nt) issue(st + NST - STEP + u);
-    cb.mark(1);
     }
   compute:
     if (!wave_active) continue;
-    cb.acc[7] += 1;
     const char *slot = ring + (st % NST) * SLOT;
     if (a.ablate & 128) {
       sink += reinterpret_cast<const float *>(slot + TB)[lane & 31];
@@ -797,14 +790,34 @@ __global__ __launch_bounds__(64 * NW, 4) void mfma_filter16w(FilterArgs a) {
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc[b][i] = 0.0f;
+    // the two halves' accumulation chains interleaved (each MFMA's result is not the next one's
+    // input); every fragment read is issued up front and the scheduler is told to run them one
+    // k-step ahead of the MFMAs (sched_group_barrier: 4 reads, then per k-step 4 MFMAs + the next
+    // 2 reads), so the waves a block barrier releases together do not all wait on LDS per k-step
+    const char *frag = slot + (g * 32 + c16) * 16;
+    h8v xf[KS][2];
 #pragma unroll
-    for (int s = 0; s < KS; ++s)
+    for (int s = 0; s < KS; ++s) {
+      xf[s][0] = *reinterpret_cast<const h8v *>(frag + s * 2048);
+      xf[s][1] = *reinterpret_cast<const h8v *>(frag + s * 2048 + 256);
+    }
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const h8v xh = *reinterpret_cast<const h8v *>(slot + ((4 * s + g) * 32 + 16 * b + c16) * 16);
-        if (Q2) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ql[s], xh, acc[b], 0, 0, 0);  // small term first
-        acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qh[s], xh, acc[b], 0, 0, 0);
+    for (int s = 0; s < KS; ++s) {
+      if (Q2) {  // small term first
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ql[s], xf[s][0], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ql[s], xf[s][1], acc[1], 0, 0, 0);
       }
+      acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qh[s], xf[s][0], acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qh[s], xf[s][1], acc[1], 0, 0, 0);
+    }
+    if constexpr (KS >= 2) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);  // DS reads of k-steps 0, 1
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        __builtin_amdgcn_sched_group_barrier(0x008, Q2 ? 4 : 2, 0);  // k-step s's MFMAs
+        if (s + 2 < KS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // k-step s + 2's reads
+      }
+    }
     const float *mrow = reinterpret_cast<const float *>(slot + TB);
     float y[2][4];
     uint64_t bm[2][4];
@@ -821,7 +834,6 @@ __global__ __launch_bounds__(64 * NW, 4) void mfma_filter16w(FilterArgs a) {
         anyb |= bm[b][i];
       }
     }
-    cb.mark(2);
     if (a.ablate & 64) {
       sink += anyb ? y[0][0] : 0.0f;
       continue;
@@ -865,10 +877,8 @@ __global__ __launch_bounds__(64 * NW, 4) void mfma_filter16w(FilterArgs a) {
         cmax = max(cmax, cnt[i]);
       }
     }
-    cb.mark(3);
     if (__any(cmax > CB - RT16)) drain();
     if (a.prio == 2) __builtin_amdgcn_s_setprio(0);
-    cb.mark(4);
   }
   publish_counts();
   insert_buffer(qvalid ? cnt_l[qslot] : 0);
@@ -885,7 +895,6 @@ __global__ __launch_bounds__(64 * NW, 4) void mfma_filter16w(FilterArgs a) {
     }
     if ((a.ablate & (64 | 128)) && g == 0) ps[0] = sink;
   }
-  cb.flush(a.tdbg, lane);
 }
 
 inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
