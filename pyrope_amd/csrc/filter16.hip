@@ -42,6 +42,9 @@ typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void gbl_void;
 
 constexpr int RT16 = 32;        // rows per tile (one 32x32 MFMA tile per wave)
+#ifndef F16_AHEAD
+#define F16_AHEAD 2  // filter16w: k-steps of B-fragment reads in flight (3: 5 VGPRs spilled, 2.56-2.62 vs 2.49-2.52 ms)
+#endif
 constexpr int CB16 = 48;        // candidate buffer entries per query (>= 32 + drain slack)
 
 __device__ __forceinline__ bool better(float s1, uint32_t k1, float s2, uint32_t k2) {
@@ -811,11 +814,12 @@ __global__ __launch_bounds__(64 * NW, 4) void mfma_filter16w(FilterArgs a) {
       acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(qh[s], xf[s][1], acc[1], 0, 0, 0);
     }
     if constexpr (KS >= 2) {
-      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);  // DS reads of k-steps 0, 1
+      constexpr int AH = F16_AHEAD < KS ? F16_AHEAD : KS;  // k-steps of reads in flight
+      __builtin_amdgcn_sched_group_barrier(0x100, 2 * AH, 0);  // DS reads of k-steps 0 .. AH - 1
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         __builtin_amdgcn_sched_group_barrier(0x008, Q2 ? 4 : 2, 0);  // k-step s's MFMAs
-        if (s + 2 < KS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // k-step s + 2's reads
+        if (s + AH < KS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // k-step s + AH's reads
       }
     }
     const float *mrow = reinterpret_cast<const float *>(slot + TB);
