@@ -915,7 +915,7 @@ static int f16_step() {
   return e ? atoi(e) : 2;
 }
 
-// 8 waves x 16 queries (mfma_filter16w) for K1 = 16 (PYR_F16_WIDE: 1 = on, 0 = the 4 x 32 kernel)
+// 8 waves x 16 queries (mfma_filter16w) for K1 = 16 and 32 (PYR_F16_WIDE: 1 = on, 0 = the 4 x 32 kernel)
 static int f16_wide() {
   const char *e = getenv("PYR_F16_WIDE");
   return e ? atoi(e) : 1;
@@ -926,7 +926,14 @@ void launch16_p(const FilterArgs &a, int max_items, hipStream_t st) {
   // all LDS is static (79 KiB at D = 128): no dynamic-LDS attribute (a 160 KiB dynamic limit on top
   // of the static size makes the launch invalid)
   const int grid = a.xcd ? (max_items + 7) / 8 * 8 : max_items;
-  if constexpr (KR == 16) {  // (K1 = 32 needs more than the 128 VGPRs of four waves per SIMD)
+  if constexpr (KR == 32) {  // K1 = 32 on 8 waves spills ~10 VGPRs at 128 and still wins: k = 20 list scan
+                             // 6.90 -> 3.94 ms (profiles/r2_final/sweep_k20_wide.log)
+    if (f16_wide()) {
+      hipLaunchKernelGGL((mfma_filter16w<D, MET, KR, Q2, 4, 2>), dim3(grid), dim3(512), 0, st, a);
+      return;
+    }
+  }
+  if constexpr (KR == 16) {
     if (a.waves == 16) {  // 256-query items (engine filter_qchunk)
       hipLaunchKernelGGL((mfma_filter16w<D, MET, KR, Q2, 4, 2, CB16, 16>), dim3(grid), dim3(1024), 0, st, a);
       return;

@@ -196,11 +196,12 @@ def test_per_list_certificate_on_skewed_data(hiplib, metric):
 
 
 @pytest.mark.parametrize("metric", [0, 1])
-@pytest.mark.parametrize("wide,prio,waves", [("1", "2", "4"), ("1", "0", "4"), ("1", "1", "4"), ("0", "0", "4"),
-                                             ("1", "2", "16")])
-def test_both_list_scan_kernels(hiplib, oracle, metric, wide, prio, waves):
-    """The K1 = 16 list scan runs on the 8-wave x 16-query kernel (mfma_filter16w: top-K1 spread
-    over a query's 4 lanes, 16x16x32 MFMA) by default and on the 4-wave x 32-query kernel with
+@pytest.mark.parametrize("wide,prio,waves,k", [("1", "2", "4", 10), ("1", "0", "4", 10), ("1", "1", "4", 10),
+                                               ("0", "0", "4", 10), ("1", "2", "16", 10), ("1", "2", "4", 20),
+                                               ("0", "0", "4", 20)])
+def test_both_list_scan_kernels(hiplib, oracle, metric, wide, prio, waves, k):
+    """The K1 = 16 / 32 list scan (k = 10 / 20) runs on the 8-wave x 16-query kernel (mfma_filter16w:
+    top-K1 spread over a query's 4 lanes, 16x16x32 MFMA) by default and on the 4-wave x 32-query kernel with
     PYR_F16_WIDE=0; PYR_FILTER_WAVES=16 runs 256-query items on 16-wave blocks; the priority
     modes only reorder the waves.  Every setting must give the
     exact scan's answers bit for bit, on multi-chunk lists (small forced chunks) and a full
@@ -210,11 +211,11 @@ def test_both_list_scan_kernels(hiplib, oracle, metric, wide, prio, waves):
     q = generate_synthetic(700, 128, 4242)
     opts = SearchOptions(nprobe=16)
     with _env(PYR_F16_WIDE=wide, PYR_F16_PRIO=prio, PYR_FILTER_WAVES=waves, PYR_IVF_CHUNK=520):
-        got = idx.search_batch(q, 10, opts)
+        got = idx.search_batch(q, k, opts)
     with _env(PYR_FILTER=0):
-        ref = idx.search_batch(q, 10, opts)
+        ref = idx.search_batch(q, k, opts)
     _same(got, ref)
-    _check_oracle(oracle, idx, x, q, got, 10, metric, 16, 100)
+    _check_oracle(oracle, idx, x, q, got, k, metric, 16, 100)
 
 
 @pytest.mark.parametrize("metric", [0, 1])
