@@ -138,8 +138,11 @@ def _rank_entry(rank, world, port, argv):
 
 
 def spawn_ranks(args, argv):
-    """`--gpus N` without a launcher: N fresh rank processes (this process never touches a GPU)."""
+    """`--gpus N` without a launcher: N fresh rank processes (this process never touches a GPU).
+    The library is built here first (hipcc needs no GPU), so the ranks find it current."""
     import torch.multiprocessing as mp
+    from pyrope_amd.build import build
+    build()
     log(f"--gpus {args.gpus} without a launcher: starting {args.gpus} rank processes")
     mp.start_processes(_rank_entry, args=(args.gpus, _free_port(), argv), nprocs=args.gpus, join=True,
                        start_method="spawn")

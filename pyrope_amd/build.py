@@ -11,7 +11,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libpyrope_hip.so")
-SOURCES = ["kernels.hip", "filter.hip", "filter16.hip", "sq8.hip", "coarse.hip", "engine.cpp", "persist.cpp", "capi.cpp"]
+SOURCES = ["kernels.hip", "filter.hip", "filter16.hip", "filter16r.hip", "sq8.hip", "coarse.hip", "engine.cpp", "persist.cpp", "capi.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 # -ffp-contract=off: the parity contract (bit-identical scores) forbids FMA contraction.
@@ -28,12 +28,29 @@ def _stale() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile (if stale or forced) and link the library.  Safe against concurrent callers (e.g. the
+    rank processes of a multi-GPU bench): an exclusive lock file serializes builds, the staleness
+    check is repeated under the lock, objects carry the builder's pid and the .so is linked to a
+    temporary name and renamed into place, so no process ever loads a half-written library."""
     if not force and not _stale():
         return OUT
+    import fcntl
+    with open(OUT + ".lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            if not force and not _stale():
+                return OUT  # another process built it while this one waited
+            return _build_locked(verbose)
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
+
+
+def _build_locked(verbose: bool) -> str:
     objs = []
     jobs = []
+    tag = f".{os.getpid()}"
     for src in SOURCES:
-        obj = os.path.join(CSRC, src.rsplit(".", 1)[0] + ".o")
+        obj = os.path.join(CSRC, src.rsplit(".", 1)[0] + tag + ".o")
         cmd = [HIPCC] + COMMON + ["-c", os.path.join(CSRC, src), "-o", obj]
         if src.endswith(".hip"):
             # no SLP: packed FP32 has no extra rate on gfx950 and its op_sel broadcasts double VGPRs
@@ -52,10 +69,15 @@ def build(force: bool = False, verbose: bool = False) -> str:
             sys.stderr.write(out)
     if failed:
         raise RuntimeError("libpyrope_hip build failed")
-    link = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT] + objs
-    subprocess.run(link, check=True)
-    for o in objs:
-        os.remove(o)
+    tmp = OUT + tag + ".tmp"
+    link = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp] + objs
+    try:
+        subprocess.run(link, check=True)
+        os.replace(tmp, OUT)  # atomic: a concurrent loader sees the old or the new library
+    finally:
+        for o in objs + [tmp]:
+            if os.path.exists(o):
+                os.remove(o)
     return OUT
 
 

@@ -411,6 +411,14 @@ static int filter_waves_ivf(int k1, int prec) {
   if (w == 16 && prec16(prec) && k1 == 16) return 16;
   return (w == 8 && prec == FILTER_BF16X3) ? 8 : 4;
 }
+// rows-as-A list scan (filter16r.hip, 384 / 512-query items) for the fp16 IVF filter at K1 = 16 / 32;
+// PYR_F16_RK=1 selects it (A/B measurement while it is tuned; results identical), default the
+// round-2 mfma_filter16w
+static bool use_rk(int dim, int metric, int k1, int prec) {
+  const char *e = getenv("PYR_F16_RK");
+  if (!(e && atoi(e) != 0)) return false;
+  return prec16(prec) && filter16r_supported(dim, metric, k1);
+}
 // XCD-major mapping of IVF filter items (FilterArgs::xcd); PYR_FILTER_XCD=0 disables it
 static int filter_xcd() {
   const char *e = getenv("PYR_FILTER_XCD");
@@ -1190,7 +1198,7 @@ static int64_t probed_rows(Workspace &ws, int64_t nq, int probes, const std::vec
 // list-major work items from ws.probes
 // phase 0 -> ws.items / ws.nitems, phase 1 -> ws.items3 / ws.nitems3 (IvfChunking, kernels.h)
 static int build_ivf_items(Workspace &ws, int64_t nq, int nprobe, int nparts, int nlist, const DevMem &lbeg,
-                           const DevMem &lend, int qchunk, IvfChunking ch, int phase = 0) {
+                           const DevMem &lend, int qchunk, IvfChunking ch, int phase = 0, bool balance = false) {
   const int64_t maxi64 = ivf_max_items(nq, nprobe, nlist, qchunk, ch, phase);
   if (maxi64 > INT32_MAX) throw Error(PYR_E_ARG, "query batch too large for one launch");
   const int maxi = (int)maxi64;
@@ -1206,14 +1214,15 @@ static int build_ivf_items(Workspace &ws, int64_t nq, int nprobe, int nparts, in
   IvfItemWs iw{ws.ivf_cnt.as<int32_t>(), ws.ivf_fill.as<int32_t>(), ws.ivf_qoff.as<int32_t>(),
                ws.ivf_ioff.as<int32_t>(), ws.qlist.as<int32_t>(), items.as<ScanItem>(), nitems.as<int32_t>()};
   launch_ivf_items(ws.probes.as<int32_t>(), nq, nprobe, nparts, nlist, lbeg.as<int32_t>(), lend.as<int32_t>(), qchunk,
-                   ch, phase, iw, ws.st);
+                   ch, phase, iw, ws.st, 0, -1, balance);
   return maxi;
 }
 
 // Items of probe ranks [pb, pe) only, into item set 0 (ws.items, ws.qlist, ...) or 1 (ws.items3,
 // ws.qlist2, ...).  Partial slots keep the absolute probe rank.
 static int build_ivf_items_range(Workspace &ws, int set, int64_t nq, int nprobe, int pb, int pe, int nparts,
-                                 int nlist, const DevMem &lbeg, const DevMem &lend, int qchunk, IvfChunking ch) {
+                                 int nlist, const DevMem &lbeg, const DevMem &lend, int qchunk, IvfChunking ch,
+                                 bool balance = false) {
   const int64_t maxi64 = ivf_max_items(nq, pe - pb, nlist, qchunk, ch, 0);
   if (maxi64 > INT32_MAX) throw Error(PYR_E_ARG, "query batch too large for one launch");
   const int maxi = (int)maxi64;
@@ -1232,7 +1241,7 @@ static int build_ivf_items_range(Workspace &ws, int set, int64_t nq, int nprobe,
   IvfItemWs iw{cnt.as<int32_t>(), fill.as<int32_t>(), qoff.as<int32_t>(), ioff.as<int32_t>(), qlist.as<int32_t>(),
                items.as<ScanItem>(), nitems.as<int32_t>()};
   launch_ivf_items(ws.probes.as<int32_t>(), nq, nprobe, nparts, nlist, lbeg.as<int32_t>(), lend.as<int32_t>(), qchunk,
-                   ch, 0, iw, ws.st, pb, pe);
+                   ch, 0, iw, ws.st, pb, pe, balance);
   return maxi;
 }
 
@@ -1572,16 +1581,17 @@ struct IvfFlatIndex : Index {
     uint32_t *gthr = shared_bounds(ws, nq);
     const int prec_used = filter_prec_for(filter_prec(), lists.f16, std::max(ch.chunk, ch.warm));
     const int waves = filter_waves_ivf(k1, prec_used);
-    const int qc = filter_qchunk(prec_used, waves);
+    const bool rk = use_rk(dim, metric, k1, prec_used);
+    const int qc = filter_qchunk(prec_used, waves, rk);
     int maxi, maxi_main = 0;
     {
       PhaseTimer t(PH_ITEMS, ws.st);
       if (seed) {
-        maxi = build_ivf_items_range(ws, 0, nq, probes, 0, 1, nparts, coarse.nlist, dlb, dle, qc, ch);
-        maxi_main = build_ivf_items_range(ws, 1, nq, probes, 1, probes, nparts, coarse.nlist, dlb, dle, qc, ch);
+        maxi = build_ivf_items_range(ws, 0, nq, probes, 0, 1, nparts, coarse.nlist, dlb, dle, qc, ch, rk);
+        maxi_main = build_ivf_items_range(ws, 1, nq, probes, 1, probes, nparts, coarse.nlist, dlb, dle, qc, ch, rk);
       } else {
-        maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qc, ch, 0);
-        if (ch.warm > 0) maxi_main = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qc, ch, 1);
+        maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qc, ch, 0, rk);
+        if (ch.warm > 0) maxi_main = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qc, ch, 1, rk);
       }
     }
     FilterArgs fa{};
@@ -1604,6 +1614,7 @@ struct IvfFlatIndex : Index {
     fa.pub_mask = filter_pub_mask();
     fa.prec = prec_used;
     fa.waves = waves;
+    fa.rk = rk ? 1 : 0;
     fa.xcd = filter_xcd();
     fa.single = getenv("PYR_FILTER_SB") ? atoi(getenv("PYR_FILTER_SB")) != 0 : 0;
     // 2: a wave with survivors appends at raised priority (I1 list scan -1.5 %, profiles/r2_wide/)
@@ -1623,25 +1634,40 @@ struct IvfFlatIndex : Index {
     }
     {
       PhaseTimer t(PH_LIST_SCAN, ws.st, prof().on ? probed_rows(ws, nq, probes, le, lb) : 0);
-      if (use16) launch_filter16(fa, metric, maxi, ws.st);
-      else launch_filter(fa, metric, maxi, ws.st);
+      auto launch = [&](int mi) {
+        if (rk) launch_filter16r(fa, metric, mi, ws.st);
+        else if (use16) launch_filter16(fa, metric, mi, ws.st);
+        else launch_filter(fa, metric, mi, ws.st);
+      };
+      launch(maxi);
       if (seed || ch.warm > 0) {
         fa.items = ws.items3.as<ScanItem>();
         fa.n_items = ws.nitems3.as<int32_t>();
         if (seed) fa.qlist = ws.qlist2.as<int32_t>();
-        if (use16) launch_filter16(fa, metric, maxi_main, ws.st);
-        else launch_filter(fa, metric, maxi_main, ws.st);
+        launch(maxi_main);
       }
     }
     if (fa.dbg) {
       uint32_t h[4] = {0, 0, 0, 0};
       HIPCHK(hipMemcpyAsync(h, dbg.p, 16, hipMemcpyDeviceToHost, ws.st));
       HIPCHK(hipStreamSynchronize(ws.st));
-      fprintf(stderr, "[filter] %s %u, candidates %u, %s %u\n", use16 ? "survivor wave-tiles" : "wave insert-loop iterations",
+      if (rk) fprintf(stderr, "[filter16r] wave insert passes %u\n", h[0]);
+      else fprintf(stderr, "[filter] %s %u, candidates %u, %s %u\n", use16 ? "survivor wave-tiles" : "wave insert-loop iterations",
               h[0], h[1], use16 ? "owner drains" : "owner stages", h[2]);
       if (use16) fprintf(stderr, "[filter] shared-bound refreshes that raised a threshold %u\n", h[3]);
     }
-    if (fa.tdbg) {
+    if (fa.tdbg && rk) {
+      unsigned long long c[8];
+      HIPCHK(hipMemcpyAsync(c, fa.tdbg, sizeof(c), hipMemcpyDeviceToHost, ws.st));
+      HIPCHK(hipStreamSynchronize(ws.st));
+      const double tot = (double)c[5];
+      fprintf(stderr,
+              "[filter16r cycles] total %.4g wave-cycles: prologue %.1f%%, wait+barrier %.1f%%, refresh+issue %.1f%%, "
+              "compute %.1f%%, epilogue %.1f%%; items %llu, wave-tiles %llu, cycles per wave-tile %.0f, "
+              "per item-wave %.0f\n",
+              tot, 100 * c[0] / tot, 100 * c[1] / tot, 100 * c[2] / tot, 100 * c[3] / tot, 100 * c[4] / tot, c[6],
+              c[7], c[7] ? tot / c[7] : 0.0, c[6] ? tot / c[6] / 8 : 0.0);
+    } else if (fa.tdbg) {
       unsigned long long c[8];
       HIPCHK(hipMemcpyAsync(c, fa.tdbg, sizeof(c), hipMemcpyDeviceToHost, ws.st));
       HIPCHK(hipStreamSynchronize(ws.st));

@@ -561,7 +561,9 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
     a.out_l[(size_t)q * k + lane] = -1;
   }
   bool ok = true;
-  if (mk[k1 - 1] >= 0) {  // K1 candidates: rows were excluded, check the margin
+  // K1 candidates (rows, or a part's floor placeholder KEY_FLOOR = -2 that stands for rows the scan
+  // dropped at or below its score): rows were excluded, check the margin against the K1-th score
+  if (mk[k1 - 1] != -1) {
     float skth = -INFINITY;
     for (int c = 0; c < k1; ++c) {
       const int rc = __shfl(rank, c);

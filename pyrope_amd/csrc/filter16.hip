@@ -35,21 +35,13 @@
 namespace pyr {
 namespace {
 
-typedef float f16v __attribute__((ext_vector_type(16)));
-typedef float f4v __attribute__((ext_vector_type(4)));
-typedef _Float16 h8v __attribute__((ext_vector_type(8)));
-typedef __attribute__((address_space(3))) void lds_void;
-typedef __attribute__((address_space(1))) void gbl_void;
+#include "f16util.h"
 
 constexpr int RT16 = 32;        // rows per tile (one 32x32 MFMA tile per wave)
 #ifndef F16_AHEAD
 #define F16_AHEAD 2  // filter16w: k-steps of B-fragment reads in flight (3: 5 VGPRs spilled, 2.56-2.62 vs 2.49-2.52 ms)
 #endif
 constexpr int CB16 = 48;        // candidate buffer entries per query (>= 32 + drain slack)
-
-__device__ __forceinline__ bool better(float s1, uint32_t k1, float s2, uint32_t k2) {
-  return s1 > s2 || (s1 == s2 && k1 < k2);
-}
 
 template <int KR>
 __device__ __forceinline__ void reg_insert(float (&s)[KR], uint32_t (&kk)[KR], float v, uint32_t key) {
@@ -98,55 +90,6 @@ struct F16Lds {
     return (NCH >= 4 ? NR : (w < NCH ? 1 : 0)) + (w == 0 ? 1 : 0);
   }
 };
-
-// LDS-DMA of SIZE (16 or 4) bytes per lane: global g (per lane) -> LDS lds + lane * SIZE (lds
-// wave-uniform, in M0).  Written in inline asm on purpose: the compiler does not track these
-// writes, so it does not drain every in-flight tile (vmcnt(0)) before each LDS access it cannot
-// prove disjoint; the kernel's own counted vmcnt waits + barrier order the ring instead.
-// SIZE 16: row pieces; 4: meta; 5: a 4-byte agent-coherent read (sc1, the shared bounds, as
-// __hip_atomic_load with agent scope compiles to).
-template <int SIZE>
-__device__ __forceinline__ void glds(const void *g, uint32_t lds_addr) {
-  int keep;
-  const uint32_t lds = __builtin_amdgcn_readfirstlane(lds_addr);  // wave-uniform: an SGPR for M0
-  if (SIZE == 16)
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(g), "s"(lds)
-                 : "memory");
-  else if (SIZE == 4)
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(g), "s"(lds)
-                 : "memory");
-  else
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off sc1\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(g), "s"(lds)
-                 : "memory");
-}
-
-// s_waitcnt vmcnt(n) for a wave-uniform n in [0, 3 * (NST - 2)] (immediate operand)
-template <int N>
-__device__ __forceinline__ void wait_vm_le(int n) {
-  if constexpr (N > 0) {
-    if (n >= N) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-      return;
-    }
-    wait_vm_le<N - 1>(n);
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-}
-
-// query scale: a power of two putting max |q_i| below 2^14 (1 for a zero query)
-__device__ __forceinline__ float pow2_scale(float amax) {
-  if (!(amax > 0.0f) || !isfinite(amax)) return 1.0f;
-  int e;
-  frexpf(amax, &e);  // amax < 2^e
-  return ldexpf(1.0f, 14 - e);
-}
 
 // measurement only (a.tdbg): wave-uniform cycle buckets of the scan loop
 struct CycleBuckets {

@@ -668,7 +668,8 @@ __global__ __launch_bounds__(256) void merge_keys_kernel(const float *ps, const 
       if (out_keys) out_keys[o] = (int32_t)bk;
       if (out_l) {
         int64_t lab;
-        if (bk & KEY_BUF) lab = buf_labels ? buf_labels[bk & ~KEY_BUF] : (int64_t)(bk & ~KEY_BUF);
+        if (bk == KEY_FLOOR) lab = -1;  // a part's floor placeholder (filter16r.hip): no row
+        else if (bk & KEY_BUF) lab = buf_labels ? buf_labels[bk & ~KEY_BUF] : (int64_t)(bk & ~KEY_BUF);
         else lab = row_labels ? row_labels[bk] : (int64_t)bk;
         out_l[o] = lab;
       }
@@ -882,7 +883,7 @@ __global__ void ivf_fill_kernel(const int32_t *probes, int64_t nq, int nprobe, i
 // <= qchunk probing queries
 __global__ void ivf_items_kernel(const int32_t *cnt, const int32_t *qoff, const int32_t *ioff, int nlist,
                                  const int32_t *lb, const int32_t *le, int qchunk, IvfChunking chk, int phase,
-                                 ScanItem *items) {
+                                 int balance, ScanItem *items) {
   const int lst = blockIdx.x * blockDim.x + threadIdx.x;
   if (lst >= nlist) return;
   const int c = cnt[lst];
@@ -890,15 +891,20 @@ __global__ void ivf_items_kernel(const int32_t *cnt, const int32_t *qoff, const 
   const int c0 = (chk.warm > 0 && phase == 1) ? 1 : 0;
   const int c1 = c0 + phase_chunks(lb, le, lst, chk, phase);
   int o = ioff[lst];
+  // balance: the list's ceil(c / qchunk) groups get equal shares rounded up to 16 queries (whole
+  // 16-query MFMA groups) instead of full groups plus a remainder
+  const int ng = (c + qchunk - 1) / qchunk;
+  const int sz = balance && ng > 0 ? ((c + ng - 1) / ng + 15) / 16 * 16 : qchunk;
   for (int ch = c0; ch < c1; ++ch) {
     int rb, re;
     ivf_chunk_rows(len, ch, chk, &rb, &re);
-    for (int b = 0; b < c; b += qchunk, ++o) {
+    for (int gi = 0; gi < ng; ++gi, ++o) {
+      const int b = gi * sz;
       ScanItem it;
       it.row_begin = lb[lst] + rb;
       it.row_end = lb[lst] + re;
-      it.qbeg = qoff[lst] + b;
-      it.qcnt = min(qchunk, c - b);
+      it.qbeg = qoff[lst] + min(b, c);
+      it.qcnt = max(0, min(sz, c - b));
       it.part = ch;
       it.list = lst;
       items[o] = it;
@@ -1656,7 +1662,7 @@ int64_t ivf_max_items(int64_t nq, int32_t nprobe, int32_t nlist, int32_t qchunk,
 
 void launch_ivf_items(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t nparts, int32_t nlist,
                       const int32_t *list_begin, const int32_t *list_end, int32_t qchunk, IvfChunking ch,
-                      int phase, IvfItemWs &ws, hipStream_t st, int32_t pb, int32_t pe) {
+                      int phase, IvfItemWs &ws, hipStream_t st, int32_t pb, int32_t pe, bool balance) {
   if (pe < 0) pe = nprobe;
   const int64_t n = nq * (pe - pb);
   const bool lds = nlist <= IVF_LDS_BINS && !getenv("PYR_IVF_GLOBAL_HIST");  // (knob: measurement only)
@@ -1679,7 +1685,7 @@ void launch_ivf_items(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t
     hipLaunchKernelGGL(ivf_fill_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, probes, nq, nprobe, pb, pe, nparts,
                        ch.cmax, ws.qoff, ws.fill, ws.qlist);
   hipLaunchKernelGGL(ivf_items_kernel, dim3(nblk(nlist, 256)), dim3(256), 0, st, ws.cnt, ws.qoff, ws.ioff, nlist,
-                     list_begin, list_end, qchunk, ch, phase, ws.items);
+                     list_begin, list_end, qchunk, ch, phase, balance ? 1 : 0, ws.items);
 }
 
 void launch_ivf_limits(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t nparts, int64_t remaining,

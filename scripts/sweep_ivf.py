@@ -4,6 +4,11 @@ once, prints list-size statistics, then times the batched search under each sett
 PYR_* knobs given on the command line (env values are read by the library per search).
 
     python scripts/sweep_ivf.py --n 10000000 PYR_IVF_CHUNK=1024,2048,4096
+
+--data mixture: a Gaussian mixture instead of the uniform bench rows -- `--clusters`
+centres ~ N(0, 1)^d, rows = centre + N(0, sigma^2)^d, a fraction `--outliers` of the rows scaled
+by `--outlier-scale`, queries drawn from the same mixture (no outliers) -- to measure how often the
+default fp16 certificate re-runs queries on data that clusters.  --metric ip uses DotProduct.
 """
 from __future__ import annotations
 
@@ -19,6 +24,22 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def mixture(args):
+    """Gaussian-mixture rows and queries (float32), generated in 1M-row blocks."""
+    rng = np.random.default_rng(7)
+    cen = rng.standard_normal((args.clusters, args.dim)).astype(np.float32)
+    x = np.empty((args.n, args.dim), dtype=np.float32)
+    for b in range(0, args.n, 1 << 20):
+        e = min(args.n, b + (1 << 20))
+        lab = rng.integers(0, args.clusters, e - b)
+        x[b:e] = cen[lab] + args.sigma * rng.standard_normal((e - b, args.dim), dtype=np.float32)
+    far = rng.choice(args.n, max(1, int(args.n * args.outliers)), replace=False)
+    x[far] *= args.outlier_scale
+    q = cen[rng.integers(0, args.clusters, args.nq)] + args.sigma * rng.standard_normal((args.nq, args.dim),
+                                                                                         dtype=np.float32)
+    return x, q.astype(np.float32)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=10_000_000)
@@ -28,6 +49,13 @@ def main():
     ap.add_argument("--nq", type=int, default=10_000)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--data", choices=["uniform", "mixture"], default="uniform")
+    ap.add_argument("--train-rows", type=int, default=10_000_000, help="k-means rows (bench.py: all of I1)")
+    ap.add_argument("--metric", choices=["l2", "ip"], default="l2")
+    ap.add_argument("--clusters", type=int, default=1000)
+    ap.add_argument("--sigma", type=float, default=0.5)
+    ap.add_argument("--outliers", type=float, default=1e-4)
+    ap.add_argument("--outlier-scale", type=float, default=30.0)
     ap.add_argument("knobs", nargs="*", help="NAME=v1,v2,...")
     ap.add_argument("--cfg", action="append", default=[],
                     help="one setting 'NAME=v,NAME2=v2' (repeatable; run after the knob grid)")
@@ -39,9 +67,14 @@ def main():
     from pyrope_amd.vector import SearchOptions
     L = _lib.load()
     dev = torch.device("cuda", 0)
-    x = generate_synthetic_blocked(0, args.n, args.dim, 42)  # bench.py's row-blocked base set
-    cents = kmeans_train(x, args.nlist, VectorMetric.L2, 10, 42)
-    idx = IvfFlatVectorIndex(args.dim, VectorMetric.L2, n_list=args.nlist)
+    met = VectorMetric.L2 if args.metric == "l2" else VectorMetric.InnerProduct
+    if args.data == "uniform":
+        x = generate_synthetic_blocked(0, args.n, args.dim, 42)  # bench.py's row-blocked base set
+        qh = generate_synthetic(args.nq, args.dim, 1337)
+    else:
+        x, qh = mixture(args)
+    cents = kmeans_train(x[: min(args.n, args.train_rows)], args.nlist, met, 10, 42)
+    idx = IvfFlatVectorIndex(args.dim, met, n_list=args.nlist)
     idx.set_centroids(cents)
     idx.add_labels(np.arange(args.n, dtype=np.int64), x, track_ids=False)
     idx.build()
@@ -49,7 +82,7 @@ def main():
     ln = np.diff(off)
     print(f"lists: n={len(ln)} mean={ln.mean():.0f} min={ln.min()} p50={np.median(ln):.0f} "
           f"p99={np.percentile(ln, 99):.0f} max={ln.max()}", flush=True)
-    q = torch.from_numpy(generate_synthetic(args.nq, args.dim, 1337)).to(dev)
+    q = torch.from_numpy(qh).to(dev)
     s = torch.empty((args.nq, args.k), dtype=torch.float32, device=dev)
     lab = torch.empty((args.nq, args.k), dtype=torch.int64, device=dev)
     opts = SearchOptions(nprobe=args.nprobe)
