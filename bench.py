@@ -286,7 +286,7 @@ def run(args):
     torch.cuda.synchronize()
     L.pyr_profile_enable(0)
     import ctypes as C
-    names = {0: "coarse", 1: "work_lists", 2: "list_scan", 3: "buffer_scan", 4: "merge", 7: "refine",
+    names = {0: "coarse", 1: "work_lists", 9: "sample", 2: "list_scan", 3: "buffer_scan", 4: "merge", 7: "refine",
              8: "exact_rerun"}
     fallback_queries = 0
     for ph, name in names.items():

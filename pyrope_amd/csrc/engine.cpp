@@ -419,6 +419,26 @@ static bool use_rk(int dim, int metric, int k1, int prec) {
   if (!(e && atoi(e) != 0)) return false;
   return prec16(prec) && filter16r_supported(dim, metric, k1);
 }
+// stream-and-emit list scan (stream16.hip) for the fp16 IVF filter: PYR_IVF_STREAM=0 -> the round-2
+// list scans (filter16.hip / filter16r.hip)
+static bool stream_enabled() {
+  const char *e = getenv("PYR_IVF_STREAM");
+  return !(e && atoi(e) == 0);
+}
+// query terms of the stream scan: 3 = one fp16 term (default), 2 = the hi/lo split (2 MFMAs per k-step)
+static int stream_prec() {
+  const char *e = getenv("PYR_STREAM_PREC");
+  return e && atoi(e) == 2 ? FILTER_F16X2 : FILTER_F16X1;
+}
+// candidate region per (query, part) (PYR_STREAM_CAP) and rows per list chunk (PYR_STREAM_CHUNK)
+static int stream_cap() {
+  const char *e = getenv("PYR_STREAM_CAP");
+  return e ? std::max(8, atoi(e)) : 128;
+}
+static int64_t stream_chunk() {
+  const char *e = getenv("PYR_STREAM_CHUNK");
+  return round_up(e ? std::max<int64_t>(32, atoll(e)) : 5120, 32);
+}
 // XCD-major mapping of IVF filter items (FilterArgs::xcd); PYR_FILTER_XCD=0 disables it
 static int filter_xcd() {
   const char *e = getenv("PYR_FILTER_XCD");
@@ -1566,6 +1586,10 @@ struct IvfFlatIndex : Index {
 
   void search_filter(const float *d_q, int64_t nq, int k, int k1, int probes, float *d_s, int64_t *d_l, int32_t *d_c,
                      Workspace &ws) {
+    if (stream_enabled() && prec16(filter_prec()) && lists.f16 && lists.resid && stream16_supported(dim, metric, k1)) {
+      search_stream(d_q, nq, k, k1, probes, d_s, d_l, d_c, ws);
+      return;
+    }
     prep_queries(d_q, nq, dim, metric, ws);
     {
       PhaseTimer t(PH_COARSE, ws.st, nq * coarse.nlist);
@@ -1707,6 +1731,246 @@ struct IvfFlatIndex : Index {
                       try {
                         if (k1_next > 0) search_filter(q2, n2, k, k1_next, probes, s2, l2, c2, sw);
                         else search_exact(q2, n2, k, ex, s2, l2, c2, sw);
+                      } catch (...) {
+                        sw.ext_probes = nullptr;
+                        throw;
+                      }
+                      sw.ext_probes = nullptr;
+                    });
+  }
+
+  // IvfFlatVectorIndex.Search (:147-231) as stream-and-emit (stream16.hip): the coarse ranking, then per
+  // (list chunk, <= 512 queries) item every row whose approximate score reaches the query's sampled
+  // threshold T_q is emitted; the best 64 per query are re-scored exactly and certified (depth K1, then
+  // depth 64 for the failures); what still fails is re-run by the exact scan.  Query batches are
+  // sliced so that the candidate regions stay within 2 GiB.
+  void search_stream(const float *d_q, int64_t nq, int k, int k1, int probes, float *d_s, int64_t *d_l, int32_t *d_c,
+                     Workspace &ws) {
+    const bool q2 = stream_prec() == FILTER_F16X2;
+    const int cap = stream_cap();
+    int64_t chunk = stream_chunk();
+    IvfChunking ch{(int32_t)chunk, 1, 0};
+    ch.cmax = ivf_list_chunks((int)max_len, ch);
+    if ((int64_t)probes * ch.cmax > MAX_PARTS) {  // fewer, longer chunks
+      const int64_t room = std::max<int64_t>(1, MAX_PARTS / std::max(probes, 1));
+      chunk = round_up(std::max<int64_t>(32, (max_len + room - 1) / room), 32);
+      ch.chunk = (int32_t)chunk;
+      ch.cmax = ivf_list_chunks((int)max_len, ch);
+    }
+    const int nparts = probes * ch.cmax;
+    if (nparts > MAX_PARTS) throw Error(PYR_E_ARG, "nprobe too large");
+    const int64_t per_q = (int64_t)nparts * cap * 8;
+    const int64_t qs = std::max<int64_t>(1, std::min<int64_t>(nq, (int64_t(2) << 30) / per_q));
+    for (int64_t a0 = 0; a0 < nq; a0 += qs) {
+      const int64_t n = std::min(qs, nq - a0);
+      const int32_t *ext = ws.ext_probes;
+      if (ext) ws.ext_probes = ext + a0 * ws.ext_nprobe;
+      try {
+        stream_slice(d_q + a0 * dim, n, k, k1, probes, ch, nparts, cap, q2, d_s + a0 * k, d_l + a0 * k,
+                     d_c ? d_c + a0 : nullptr, ws);
+      } catch (...) {
+        ws.ext_probes = ext;
+        throw;
+      }
+      ws.ext_probes = ext;
+    }
+  }
+
+  // measurement only (PYR_STREAM_DEBUG): candidate pool and certificate statistics of one slice, to stderr
+  void stream_debug(int64_t nq, int k, int k1, int nparts, int cap, int32_t nf, const float *d_s, Workspace &ws) {
+    const size_t nslot = (size_t)nq * nparts;
+    std::vector<float> ms((size_t)nq * STREAM_KO), thr(nq), res((size_t)nq * k);
+    std::vector<int32_t> mk((size_t)nq * STREAM_KO), cn(nslot), f1(nq);
+    std::vector<uint32_t> cf(nslot);
+    int32_t n1 = 0;
+    HIPCHK(hipMemcpyAsync(ms.data(), ws.ms.p, sizeof(float) * ms.size(), hipMemcpyDeviceToHost, ws.st));
+    HIPCHK(hipMemcpyAsync(mk.data(), ws.mk.p, sizeof(int32_t) * mk.size(), hipMemcpyDeviceToHost, ws.st));
+    HIPCHK(hipMemcpyAsync(thr.data(), ws.sthr.p, sizeof(float) * nq, hipMemcpyDeviceToHost, ws.st));
+    HIPCHK(hipMemcpyAsync(res.data(), d_s, sizeof(float) * res.size(), hipMemcpyDeviceToHost, ws.st));
+    HIPCHK(hipMemcpyAsync(cn.data(), ws.scn.p, sizeof(int32_t) * nslot, hipMemcpyDeviceToHost, ws.st));
+    HIPCHK(hipMemcpyAsync(cf.data(), ws.scf.p, sizeof(uint32_t) * nslot, hipMemcpyDeviceToHost, ws.st));
+    HIPCHK(hipMemcpyAsync(&n1, ws.fail_cnt2.p, sizeof(int32_t), hipMemcpyDeviceToHost, ws.st));
+    HIPCHK(hipMemcpyAsync(f1.data(), ws.fail.p, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, ws.st));
+    HIPCHK(hipStreamSynchronize(ws.st));
+    int64_t emitted = 0, full = 0, shallow = 0;
+    for (size_t i = 0; i < nslot; ++i) {
+      emitted += cn[i];
+      full += cf[i] != 0u;
+    }
+    for (int64_t q = 0; q < nq; ++q) {
+      int real = 0;
+      for (int i = 0; i < STREAM_KO; ++i) real += mk[q * STREAM_KO + i] >= 0;
+      shallow += real < STREAM_KO;
+    }
+    fprintf(stderr, "[stream] nq %lld: emitted %lld (%.1f per query), full regions %lld, queries with < %d real "
+            "candidates %lld; certificate failures: depth %d %d, depth %d %d\n", (long long)nq, (long long)emitted,
+            (double)emitted / std::max<int64_t>(nq, 1), (long long)full, STREAM_KO, (long long)shallow, k1, n1,
+            STREAM_KO, nf);
+    for (int i = 0; i < std::min(nf, 6); ++i) {
+      const int64_t q = f1[i];
+      int real = 0, floors = 0;
+      for (int j = 0; j < STREAM_KO; ++j) {
+        real += mk[q * STREAM_KO + j] >= 0;
+        floors += mk[q * STREAM_KO + j] == -2;
+      }
+      fprintf(stderr, "[stream]   failed q %lld: T %.6g, k-th exact %.6g, approx K1-th %.6g, 64th %.6g, real %d, "
+              "floors %d\n", (long long)q, thr[q], res[q * k + k - 1], ms[q * STREAM_KO + k1 - 1],
+              ms[q * STREAM_KO + STREAM_KO - 1], real, floors);
+    }
+  }
+
+  void stream_slice(const float *d_q, int64_t nq, int k, int k1, int probes, IvfChunking ch, int nparts, int cap,
+                    bool q2, float *d_s, int64_t *d_l, int32_t *d_c, Workspace &ws) {
+    {
+      PhaseTimer t(PH_COARSE, ws.st, nq * coarse.nlist);
+      coarse.probe(d_q, nullptr, nq, probes, metric, ws);  // exact coarse ranking (ComputeScore, :186-198)
+    }
+    const int qmax = stream16_qmax(q2);
+    int maxi;
+    {
+      PhaseTimer t(PH_ITEMS, ws.st);
+      maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qmax, ch, 0, true);
+    }
+    const int64_t npos = nq * probes;
+    const int sv = stream16_sample_values();
+    const size_t nslot = (size_t)nq * nparts;
+    ws.sbq.ensure(sizeof(uint16_t) * std::max<int64_t>(npos, 1) * dim);
+    if (q2) ws.sbql.ensure(sizeof(uint16_t) * std::max<int64_t>(npos, 1) * dim);
+    ws.sqsc.ensure(sizeof(float2) * std::max<int64_t>(npos, 1));
+    ws.ssamp.ensure(sizeof(float) * std::max<int64_t>(npos, 1) * sv);
+    ws.sthr.ensure(sizeof(float) * nq);
+    ws.scs.ensure(sizeof(float) * nslot * cap);
+    ws.sck.ensure(sizeof(uint32_t) * nslot * cap);
+    ws.scn.ensure(sizeof(int32_t) * nslot);
+    ws.scf.ensure(sizeof(uint32_t) * nslot);
+    ws.swork.ensure(sizeof(int32_t) * 2);
+    HIPCHK(hipMemsetAsync(ws.scn.p, 0, sizeof(int32_t) * nslot, ws.st));
+    HIPCHK(hipMemsetAsync(ws.scf.p, 0, sizeof(uint32_t) * nslot, ws.st));
+    HIPCHK(hipMemsetAsync(ws.swork.p, 0, sizeof(int32_t) * 2, ws.st));
+    StreamArgs sa{};
+    sa.h16 = lists.h16.p;
+    sa.meta = lists.meta.as<float>();
+    sa.queries = d_q;
+    sa.cents = coarse.rm.as<float>();
+    sa.sx = lists.sx;
+    sa.items = ws.items.as<ScanItem>();
+    sa.n_items = ws.nitems.as<int32_t>();
+    sa.qlist = ws.qlist.as<int32_t>();
+    sa.nparts = nparts;
+    sa.nprobe = probes;
+    sa.cmax = ch.cmax;
+    sa.dim = dim;
+    sa.bq = ws.sbq.as<_Float16>();
+    sa.bql = q2 ? ws.sbql.as<_Float16>() : nullptr;
+    sa.qsc = ws.sqsc.as<float2>();
+    sa.samp = ws.ssamp.as<float>();
+    sa.thr = ws.sthr.as<float>();
+    sa.cand_s = ws.scs.as<float>();
+    sa.cand_k = ws.sck.as<uint32_t>();
+    sa.cand_n = ws.scn.as<int32_t>();
+    sa.cand_f = ws.scf.as<uint32_t>();
+    sa.cap = cap;
+    sa.work = ws.swork.as<int32_t>();
+    sa.key_base = 0;
+    sa.row_limit = 0xFFFFFFFFu;
+    sa.ablate = filter_ablate();
+    {
+      PhaseTimer t(PH_SAMPLE, ws.st);
+      launch_stream_prep(sa, metric, maxi, ws.st);
+      launch_stream_scan(sa, metric, maxi, true, ws.st);
+      launch_stream_select(ws.ssamp.as<float>(), nq, probes * sv, k1, ws.sthr.as<float>(), ws.st);
+    }
+    sa.work = ws.swork.as<int32_t>() + 1;
+    {
+      PhaseTimer t(PH_LIST_SCAN, ws.st, prof().on ? probed_rows(ws, nq, probes, le, lb) : 0);
+      launch_stream_scan(sa, metric, maxi, false, ws.st);
+    }
+    HIPCHK(hipGetLastError());
+    ws.ms.ensure(sizeof(float) * nq * STREAM_KO);
+    ws.mk.ensure(sizeof(int32_t) * nq * STREAM_KO);
+    {
+      PhaseTimer t(PH_MERGE, ws.st);
+      CandMergeArgs m{};
+      m.cand_s = ws.scs.as<float>();
+      m.cand_k = ws.sck.as<uint32_t>();
+      m.cand_n = ws.scn.as<int32_t>();
+      m.cand_f = ws.scf.as<uint32_t>();
+      m.thr = ws.sthr.as<float>();
+      m.nq = nq;
+      m.nparts = nparts;
+      m.cap = cap;
+      m.out_s = ws.ms.as<float>();
+      m.out_k = ws.mk.as<int32_t>();
+      launch_cand_merge(m, ws.st);
+    }
+    // certificate at depth K1, then the failures at depth 64 from the same candidates
+    ws.fail.ensure(sizeof(int32_t) * nq);
+    ws.fail2.ensure(sizeof(int32_t) * nq);
+    ws.fail_cnt.ensure(sizeof(int32_t));
+    ws.fail_cnt2.ensure(sizeof(int32_t));
+    HIPCHK(hipMemsetAsync(ws.fail_cnt.p, 0, sizeof(int32_t), ws.st));
+    HIPCHK(hipMemsetAsync(ws.fail_cnt2.p, 0, sizeof(int32_t), ws.st));
+    RefineArgs r{};
+    r.rows = lists.rows.as<float>();
+    r.row_labels = lists.labels.as<int64_t>();
+    r.queries = d_q;
+    r.ms = ws.ms.as<float>();
+    r.mk = ws.mk.as<int32_t>();
+    r.ld = STREAM_KO;
+    r.max_rsq = lists.rmax.as<uint32_t>();
+    r.tri = 1;
+    r.list_rmax = dlmax.as<uint32_t>();
+    r.probes = ws.probes.as<int32_t>();
+    r.nprobe = probes;
+    r.nq = nq;
+    r.k = k;
+    r.dim = dim;
+    r.c_err = filter_cerr(dim);
+    const int prec = q2 ? FILTER_F16X2 : FILTER_F16X1;
+    r.c_bf = filter_f16_cerr(dim, metric, prec);
+    r.c_abs = filter_f16_abs(dim, metric, lists.sx, prec);
+    r.q16 = 1;
+    r.resid = 1;
+    r.cents = coarse.rm.as<float>();
+    r.list_rmax_r = dlmax_r.as<uint32_t>();
+    r.out_s = d_s;
+    r.out_l = d_l;
+    r.out_c = d_c;
+    int32_t nf = 0;
+    {
+      PhaseTimer t(PH_REFINE, ws.st, nq * k1);
+      r.k1 = k1;
+      r.fail_list = ws.fail2.as<int32_t>();
+      r.fail_cnt = ws.fail_cnt2.as<int32_t>();
+      launch_refine(r, metric, 1, ws.st);
+      if (k1 < STREAM_KO && k + 4 <= STREAM_KO) {
+        r.k1 = STREAM_KO;
+        r.qsel = ws.fail2.as<int32_t>();
+        r.nsel = ws.fail_cnt2.as<int32_t>();
+        r.fail_list = ws.fail.as<int32_t>();
+        r.fail_cnt = ws.fail_cnt.as<int32_t>();
+        launch_refine(r, metric, 1, ws.st);
+      } else {
+        HIPCHK(hipMemcpyAsync(ws.fail.p, ws.fail2.p, sizeof(int32_t) * nq, hipMemcpyDeviceToDevice, ws.st));
+        HIPCHK(hipMemcpyAsync(ws.fail_cnt.p, ws.fail_cnt2.p, sizeof(int32_t), hipMemcpyDeviceToDevice, ws.st));
+      }
+      HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipMemcpyAsync(&nf, ws.fail_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, ws.st));
+    HIPCHK(hipStreamSynchronize(ws.st));
+    if (getenv("PYR_STREAM_DEBUG")) stream_debug(nq, k, k1, nparts, cap, nf, d_s, ws);
+    // what neither certificate covers: the exact scan over the failing queries' own probe lists
+    pyr_search_params ex{probes, 0, -1};
+    filter_fallback(ws, nf, d_q, dim, k, d_s, d_l, d_c,
+                    [&](const float *q2p, int64_t n2, float *s2, int64_t *l2, int32_t *c2) {
+                      Workspace &sw = ws.nested();
+                      sw.fprobes.ensure(sizeof(int32_t) * n2 * probes);
+                      launch_gather_rows_i32(ws.probes.as<int32_t>(), ws.fail.as<int32_t>(), n2, probes,
+                                             sw.fprobes.as<int32_t>(), ws.st);
+                      sw.ext_probes = sw.fprobes.as<int32_t>();
+                      sw.ext_nprobe = probes;
+                      try {
+                        search_exact(q2p, n2, k, ex, s2, l2, c2, sw);
                       } catch (...) {
                         sw.ext_probes = nullptr;
                         throw;

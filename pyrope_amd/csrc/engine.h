@@ -110,6 +110,8 @@ struct Workspace {
   DevMem ms, mk, fail, fail_cnt, fq, fs, fl, fc;  // MFMA filter: merged candidates, certificate failures
   DevMem fprobes;                                 // probe lists of the failing queries (IVF exact re-run)
   DevMem q8q, q8qs;                               // 8-bit search mode: quantized queries, their sums
+  // stream-and-emit list scan (stream16.hip): query operands, samples, thresholds, candidate regions
+  DevMem sbq, sbql, sqsc, ssamp, sthr, scs, sck, scn, scf, swork, fail2, fail_cnt2;
   const int32_t *ext_probes = nullptr;            // caller-ranked probe lists [nq][ext_nprobe] (multi-GPU)
   int32_t ext_nprobe = 0;
   // the re-run of certificate failures searches with its own buffers on the same stream
@@ -239,7 +241,7 @@ Index *create_index(const pyr_index_desc &d);
 
 // kernel-phase profiler (pyr_profile_*): HIP events around each phase on the search stream
 enum Phase { PH_COARSE = 0, PH_ITEMS = 1, PH_LIST_SCAN = 2, PH_BUF_SCAN = 3, PH_MERGE = 4, PH_FLAT_SCAN = 5,
-             PH_PQ_SCAN = 6, PH_REFINE = 7, PH_FALLBACK = 8, PH_N = 10 };
+             PH_PQ_SCAN = 6, PH_REFINE = 7, PH_FALLBACK = 8, PH_SAMPLE = 9, PH_N = 10 };
 struct Profiler {
   bool on = false;
   std::mutex m;

@@ -513,9 +513,14 @@ __device__ float exact_score_l8(const float *q, const float *rows, int64_t r, in
 template <int V, int MET>
 __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
   const int lane = threadIdx.x & 63;
-  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= a.nq) return;
+  if (a.qsel) {  // a device-sized subset (the failures of an earlier certificate): no host round trip
+    if (q >= *a.nsel) return;
+    q = a.qsel[q];
+  }
   const int D = a.dim, k1 = a.k1, k = a.k;
+  const int ld = a.ld > 0 ? a.ld : k1;
   const float *qp = a.queries + (size_t)q * D;
   float part = 0.0f;  // |q|^2, any order (covered by E)
   for (int d = lane; d < D; d += 64) part += qp[d] * qp[d];
@@ -529,8 +534,8 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
     for (int off = 32; off >= 1; off >>= 1) qa = fmaxf(qa, __shfl_xor(qa, off));
   }
 
-  const float *ms = a.ms + (size_t)q * k1;
-  const int32_t *mk = a.mk + (size_t)q * k1;
+  const float *ms = a.ms + (size_t)q * ld;
+  const int32_t *mk = a.mk + (size_t)q * ld;
   uint32_t key = KEY_NONE;
   float s = -INFINITY;
   if (lane < k1 && mk[lane] >= 0) key = (uint32_t)mk[lane];
@@ -574,15 +579,19 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
     const double u = 5.9604644775390625e-8;  // 2^-24
     const double qn = sqrt((double)qsq) * (1.0 + 1e-5);
     if (a.resid) {
-      // IVF fp16 filter over residual tiles (filter16.hip): approx estimates the score itself,
-      //   L2: -|q - x|^2 = 2 (q-c).(x-c) - |x-c|^2 - |q-c|^2,  IP: q.x = q.(x-c) + q.c,
-      // so its error is relative to the residuals: fp16 rows c_bf u Ar Xr (Ar = |q - c| for L2,
-      // |q| for IP; Xr = max |x - c|), fp32 sums / adds (D + 8) u (Ar + Xr)^2, subnormal halves
-      // (c_abs Ar, and the query's, below 2^-36 sqrt(D) Ar Xr), IP's q.c constant (D + 8) u |q||c|.
-      // The reference's own sum: L2 adds non-negative terms, so R = T (1 +- g), g = (D/8 + 8) u;
-      // IP |R - T| <= g |q| max|x|.  Maxima over this query's probed lists.
-      float ar2 = 0.0f, xc2 = 0.0f;
-      uint32_t xrk = 0, xfk = 0;
+      // IVF fp16 filter over residual tiles (filter16.hip, stream16.hip): approx estimates the score
+      // itself,  L2: -|q - x|^2 = 2 (q-c).(x-c) - |x-c|^2 - |q-c|^2,  IP: q.x = q.(x-c) + q.c,
+      // so for a row of list l its error is relative to the residuals: fp16 rows and queries
+      // c_bf u A_l X_l (A_l = |q - c_l| for L2, |q| for IP; X_l = max |x - c_l| over the list), fp32
+      // sums / adds (D + 8) u (A_l + X_l)^2, subnormal halves (c_abs A_l, and the query's, below
+      // 2^-36 sqrt(D) A_l X_l), IP's q.c constant (D + 8) u |q||c_l|.  The reference's own sum: L2
+      // adds non-negative terms, so R = T (1 +- g), g = (D/8 + 8) u; IP |R - T| <= g |q| max|x|.
+      // Per list: a probed list none of whose rows can reach skth whatever the filter
+      // saw -- L2: |q - c_l| - X_l >= r with r^2 = -skth (1 + 2 c_err u); IP: q.c_l + |q| X_l plus its
+      // roundings below skth -- adds no error term; E is the largest term of the other lists.
+      const double g = (D / 8.0 + 8.0) * u;
+      const double r = sqrt(fmax(0.0, -(double)skth) * (1.0 + 2.0 * a.c_err * u) + 1e-30) * (1.0 + 1e-6);
+      double emax = 0.0;
       // FLAT (no probes): one center, list 0
       // 8 probes per pass, an 8-lane group per probe, lane j of it summing dims j, j + 8, ...
       const int np = a.probes ? a.nprobe : 1;
@@ -594,54 +603,52 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
           pid = a.probes && p0 + lane < np ? a.probes[(size_t)q * a.nprobe + p0 + lane] : 0;
         const int p = p0 + (lane >> 3), j = lane & 7;
         const int lp = __shfl(pid, (p0 & 63) + (lane >> 3));
-        float d2 = 0.0f, c2 = 0.0f;
+        float d2 = 0.0f, c2 = 0.0f, qc = 0.0f;
         if (p < np) {
-          const int l = lp;
-          xrk = max(xrk, a.list_rmax_r[l]);
-          xfk = max(xfk, a.list_rmax[l]);
-          const float *c = a.cents + (size_t)l * D;
+          const float *c = a.cents + (size_t)lp * D;
           for (int d = j; d < D; d += 8) {
             const float t = qp[d] - c[d];
             d2 += t * t;
             c2 += c[d] * c[d];
+            qc += qp[d] * c[d];
           }
         }
 #pragma unroll
         for (int off = 1; off <= 4; off <<= 1) {
           d2 += __shfl_xor(d2, off);
           c2 += __shfl_xor(c2, off);
+          qc += __shfl_xor(qc, off);
         }
-        ar2 = fmaxf(ar2, d2);
-        xc2 = fmaxf(xc2, c2);
+        if (p < np) {
+          const double Xr = sqrt((double)key_score(a.list_rmax_r[lp])) * (1.0 + 1e-5);
+          const double cn = sqrt((double)c2) * (1.0 + 1e-5);
+          double el = 0.0;
+          if (MET == L2) {
+            const double Al = sqrt((double)d2) * (1.0 + 1e-5) + 1e-30;
+            const double Alo = sqrt((double)d2) * (1.0 - 1e-5);
+            // (fp32 |q - c|^2: relative error <= (D + 8) u, far inside the 1e-5 margins)
+            if (!a.tri || Alo - Xr < r) {
+              const double X = a.tri ? fmin(Xr, Al + r) : Xr;
+              el = a.c_bf * u * Al * X + a.c_err * u * (Al + X) * (Al + X) + a.c_abs * Al +
+                   2.0 * 1.4551915228366852e-11 * sqrt((double)D) * Al * X;
+            }
+          } else {
+            const double Xf = sqrt((double)key_score(a.list_rmax ? a.list_rmax[lp] : *a.max_rsq)) * (1.0 + 1e-5);
+            // every row x of l: q.x <= q.c + |q| X_l; fp32 q.c is within (D + 8) u |q||c| of the real
+            // value, the reference's sum within g |q||x|
+            const double hi = (double)qc + qn * Xr + (g + a.c_err * u) * qn * (cn + Xr + Xf);
+            if (!a.tri || hi >= (double)skth)
+              el = a.c_bf * u * qn * Xr + a.c_err * u * qn * Xr + a.c_abs * qn +
+                   1.4551915228366852e-11 * sqrt((double)D) * qn * Xr + a.c_err * u * qn * cn + g * qn * Xf;
+          }
+          emax = fmax(emax, el);
+        }
       }
 #pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) {
-        ar2 = fmaxf(ar2, __shfl_xor(ar2, off));
-        xc2 = fmaxf(xc2, __shfl_xor(xc2, off));
-        xrk = max(xrk, (uint32_t)__shfl_xor((int)xrk, off));
-        xfk = max(xfk, (uint32_t)__shfl_xor((int)xfk, off));
-      }
-      const double Ar = MET == L2 ? sqrt((double)ar2) * (1.0 + 1e-5) + 1e-30 : qn;
-      double Xr = sqrt((double)key_score(xrk)) * (1.0 + 1e-5);
-      const double g = (D / 8.0 + 8.0) * u;
-      if (MET == L2 && a.tri) {
-        // triangle bound on the residuals (the classic branch below, with q - x = (q-c) - (x-c)):
-        // a row with |x - c| >= |q - c| + r, r^2 = -skth (1 + 2 c_err u), scores below skth whatever
-        // the filter saw, so only rows with |x - c| < Ar + r need the error bound
-        const double r = sqrt(fmax(0.0, -(double)skth) * (1.0 + 2.0 * a.c_err * u) + 1e-30) * (1.0 + 1e-6);
-        Xr = fmin(Xr, Ar + r);
-      }
-      // (c_err = 4D + 64 >= D + 8 budgets the fp32 sums; PYR_FILTER_CERR raises it in tests)
-      double e = a.c_bf * u * Ar * Xr + a.c_err * u * (MET == L2 ? (Ar + Xr) * (Ar + Xr) : Ar * Xr) +
-                 a.c_abs * Ar + (MET == L2 ? 2.0 : 1.0) * 1.4551915228366852e-11 * sqrt((double)D) * Ar * Xr;
+      for (int off = 32; off >= 1; off >>= 1) emax = fmax(emax, __shfl_xor(emax, off));
       const double ak = (double)ms[k1 - 1];
-      if (MET == L2) {
-        ok = nout == k && (double)skth > (ak + e) + g * fabs(ak + e);
-      } else {
-        e += a.c_err * u * qn * sqrt((double)xc2) * (1.0 + 1e-5) +
-             g * qn * sqrt((double)key_score(xfk)) * (1.0 + 1e-5);
-        ok = nout == k && (double)skth > ak + e;
-      }
+      if (MET == L2) ok = nout == k && (double)skth > (ak + emax) + g * fabs(ak + emax);
+      else ok = nout == k && (double)skth > ak + emax;
       if (lane == 0) {
         if (a.out_c) a.out_c[q] = nout;
         if (!ok) a.fail_list[atomicAdd(a.fail_cnt, 1)] = (int32_t)q;

@@ -322,12 +322,59 @@ inline double filter_f16_abs(int dim, int metric, float sx, int prec) {
   (void)prec;
   return metric == 0 ? 2.0 * a : a;
 }
+// ---- IVF list scan as stream-and-emit (stream16.hip) ----
+constexpr int STREAM_KO = 64;  // merged candidates per query (the deep certificate's K1)
+struct StreamArgs {
+  const void *h16;            // fp16 residual tiles of the lists (RowStore::h16)
+  const float *meta;          // per row: L2 -|x - c|^2, IP 0, -inf dead / padding
+  const float *queries;       // row-major nq x D
+  const float *cents;         // row-major centroids
+  float sx;                   // the store's power-of-two fp16 scale
+  const ScanItem *items;
+  const int32_t *n_items;
+  const int32_t *qlist;       // per (list, query) position: q * nparts + probe * cmax
+  int32_t nparts, nprobe, cmax, dim;
+  _Float16 *bq, *bql;         // [pos][D] scaled query residuals: one fp16 term (+ the low term, or null)
+  float2 *qsc;                // [pos] {f, cq}
+  float *samp;                // [q * nprobe + probe][stream16_sample_values()] sampled scores
+  const float *thr;           // [q] T_q (score space), or null
+  float *cand_s;              // [q * nparts + part][cap] emitted scores
+  uint32_t *cand_k;           // keys
+  int32_t *cand_n;            // [q * nparts + part] rows kept (<= cap)
+  uint32_t *cand_f;           // score_key of the best dropped row (0: none)
+  int32_t cap;
+  int32_t *work;              // persistent-block item counter (zeroed before each launch)
+  uint32_t key_base, row_limit;
+  int32_t ablate;             // measurement only (PYR_FILTER_ABLATE=64: no emission)
+};
+struct CandMergeArgs {
+  const float *cand_s;
+  const uint32_t *cand_k;
+  const int32_t *cand_n;
+  const uint32_t *cand_f;
+  const float *thr;
+  int64_t nq;
+  int32_t nparts, cap;
+  float *out_s;               // [nq][STREAM_KO] desc; floor placeholders key -2, none -1
+  int32_t *out_k;
+};
+bool stream16_supported(int dim, int metric, int k1);
+int stream16_qmax(bool q2);          // queries per work item
+int stream16_sample_values();        // sample values per (query, probe)
+void launch_stream_prep(const StreamArgs &a, int metric, int max_items, hipStream_t st);
+void launch_stream_scan(const StreamArgs &a, int metric, int max_items, bool sample, hipStream_t st);
+void launch_stream_select(const float *samp, int64_t nq, int n, int k1, float *thr, hipStream_t st);
+void launch_cand_merge(const CandMergeArgs &m, hipStream_t st);
+
 struct RefineArgs {
   const float *rows;        // blocked store the keys index
   const int64_t *row_labels;
   const float *queries;     // row-major nq x D
-  const float *ms;          // merged approximate scores [nq][k1] (desc)
-  const int32_t *mk;        // merged keys [nq][k1] (-1 = none)
+  const float *ms;          // merged approximate scores [nq][ld] (desc)
+  const int32_t *mk;        // merged keys [nq][ld] (-1 = none, -2 = a floor placeholder)
+  int32_t ld;               // row stride of ms / mk (0: k1)
+  const int32_t *qsel;      // refine only queries qsel[0 .. *nsel) (null: all nq)
+  const int32_t *nsel;
   const uint32_t *max_rsq;  // score_key(max |x|^2 over the store) (device scalar)
   const uint32_t *list_rmax;  // IVF: score_key(max |x|^2) per list, or null (use max_rsq)
   const int32_t *probes;      // IVF: [nq][nprobe] probed lists (with list_rmax)

@@ -118,7 +118,7 @@ def main():
         torch.cuda.synchronize()
         L.pyr_profile_enable(0)
         ph = {}
-        for i, name in {0: "coarse", 1: "items", 2: "scan", 3: "buf", 4: "merge", 7: "refine", 8: "rerun"}.items():
+        for i, name in {0: "coarse", 1: "items", 9: "sample", 2: "scan", 3: "buf", 4: "merge", 7: "refine", 8: "rerun"}.items():
             ms, calls, work = C.c_double(), C.c_int64(), C.c_int64()
             L.pyr_profile_get(i, C.byref(ms), C.byref(calls), C.byref(work))
             if calls.value:
