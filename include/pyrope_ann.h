@@ -120,9 +120,11 @@ pyr_status pyr_index_search(pyr_index *index, const float *q, int64_t nq, int32_
 /* Request coalescing for pyr_index_search (the reference serves one query per VEC.SEARCH call,
  * Extensions/VectorCommandSet.cs:457-459, from many session threads): with max_wait_us > 0,
  * concurrent pyr_index_search calls of fewer than max_batch queries and equal (k, params) are merged
- * into one device search of up to max_batch queries, started when the batch is full or max_wait_us
- * after its first query arrived; each caller gets exactly its own rows (results are per-query
- * identical to uncoalesced calls).  max_wait_us <= 0 turns it off (the default). */
+ * into one device search of up to max_batch queries.  A batch starts at once when no coalesced
+ * search of the index is running (an idle device adds no wait), else when the running one finishes,
+ * when it is full, or at the latest max_wait_us after its first query arrived; each caller gets
+ * exactly its own rows (results are per-query identical to uncoalesced calls).  max_wait_us <= 0
+ * turns it off (the default). */
 pyr_status pyr_index_set_coalescing(pyr_index *index, int32_t max_batch, int32_t max_wait_us);
 /* Same on device-resident buffers (HBM), enqueued on `stream` (hipStream_t, NULL = default).
  * Does not synchronize the stream. */
@@ -171,6 +173,13 @@ pyr_status pyr_index_get_centroids(const pyr_index *index, float *out, int32_t *
  * labels: *n entries, x: *n x dim row-major; either may be NULL (call with both NULL to size).
  * FLAT only (PYR_E_STATE otherwise).  Takes the index exclusively (it uses the write stream). */
 pyr_status pyr_index_scan(pyr_index *index, int64_t *labels, float *x, int64_t *n);
+
+/* The labels of every row the index holds (FLAT slots; IVF buffer and list entries; a label may
+ * repeat when a buffer row shadows a list entry).  labels may be NULL to size (*n = count); else *n
+ * is its capacity on entry (PYR_E_ARG if too small) and the count on return.  The shim rebuilds its
+ * id <-> label map from it after pyr_index_load of an image written without one (the reference's
+ * snapshot DTOs carry the ids themselves, BruteForceVectorIndex.cs:58-82, IvfFlatVectorIndex.cs:233-257). */
+pyr_status pyr_index_labels(const pyr_index *index, int64_t *labels, int64_t *n);
 
 /* BruteForceVectorIndex.EnableQuantization (BruteForceVectorIndex.cs:25-40), FLAT only:
  * rows added / upserted while it is on carry ScalarQuantizer codes, and searches run in the

@@ -97,6 +97,7 @@ SIGNATURES = {
     "pyr_index_ivf_layout": (C.c_int, [_vp, _i64, _i64, _u8, _i64]),
     "pyr_index_pq_state": (C.c_int, [_vp, _f, _i32, _u8]),
     "pyr_index_scan": (C.c_int, [_vp, _i64, _f, _i64]),
+    "pyr_index_labels": (C.c_int, [_vp, _i64, _i64]),
     "pyr_index_set_quantization": (C.c_int, [_vp, C.c_int32]),
     "pyr_index_probe_device": (C.c_int, [_vp, _vp, C.c_int64, C.c_int32, _vp, C.POINTER(C.c_int32), _vp]),
     "pyr_index_search_probed_device": (C.c_int, [_vp, _vp, C.c_int64, C.c_int32, C.POINTER(SearchParams), _vp,

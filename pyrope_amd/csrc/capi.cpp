@@ -20,10 +20,12 @@ namespace {
 // Request coalescer (pyr_index_set_coalescing).  The reference serves one query per VEC.SEARCH
 // call (VectorCommandSet.cs:457-459), one call per Garnet session thread; the scan reaches its
 // throughput only on batches.  Concurrent pyr_index_search calls with the same (k, SearchOptions)
-// join an open batch: the first caller (the leader) waits until the batch holds max_batch queries
-// or max_wait_us has passed since it opened, runs ONE device search for all of them and copies
-// every caller's rows into that caller's buffers; the other callers (followers) block until then.
-// Each query's result is the same as a search of it alone (the engine is per query exact).
+// join an open batch.  The first caller (the leader) dispatches it as soon as the device has no
+// coalesced search of this index in flight (an idle device never waits: a lone caller pays no
+// added latency), else when the running search finishes, when the batch holds max_batch queries,
+// or at the latest max_wait_us after it opened; it runs ONE device search for all of them and
+// copies every caller's rows into that caller's buffers.  The other callers (followers) block until
+// then.  Each query's result is the same as a search of it alone (the engine is per query exact).
 struct Batch {
   int32_t k = 0;
   pyr_search_params prm{};
@@ -45,6 +47,7 @@ struct Coalescer {
   std::mutex m;
   std::condition_variable cv;
   int32_t max_batch = 0, max_wait_us = 0;
+  int32_t inflight = 0;  // coalesced device searches running
   std::map<std::tuple<int32_t, int32_t, int64_t>, std::shared_ptr<Batch>> open;  // (k, nprobe, max_scans)
 };
 }  // namespace
@@ -271,21 +274,29 @@ static pyr_status search_coalesced(pyr_index *index, const float *q, int64_t nq,
   const int dim = index->impl->dim;
   std::unique_lock<std::mutex> lk(co.m);
   const auto key = std::make_tuple(k, prm.nprobe, prm.max_scans);
-  auto it = co.open.find(key);
   std::shared_ptr<Batch> b;
   bool leader = false;
-  if (it == co.open.end() || it->second->closed || it->second->nq + nq > co.max_batch) {
-    b = std::make_shared<Batch>();
-    b->k = k;
-    b->prm = prm;
-    b->deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(co.max_wait_us);
-    co.open[key] = b;
-    leader = true;
-  } else {
-    b = it->second;
+  try {  // no allocation failure may cross the C ABI or leave followers waiting
+    auto it = co.open.find(key);
+    if (it == co.open.end() || it->second->closed || it->second->nq + nq > co.max_batch) {
+      b = std::make_shared<Batch>();
+      b->k = k;
+      b->prm = prm;
+      b->deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(co.max_wait_us);
+      co.open[key] = b;
+      leader = true;
+    } else {
+      b = it->second;
+    }
+    b->q.insert(b->q.end(), q, q + nq * dim);
+    b->parts.push_back({b->nq, nq, out_scores, out_labels, out_counts});
+  } catch (...) {
+    if (leader) {  // nobody else joined yet (the lock is held): withdraw the batch
+      auto f = co.open.find(key);
+      if (f != co.open.end() && f->second == b) co.open.erase(f);
+    }
+    return fail(PYR_E_OOM, "coalescer: host allocation failed");
   }
-  b->q.insert(b->q.end(), q, q + nq * dim);
-  b->parts.push_back({b->nq, nq, out_scores, out_labels, out_counts});
   b->nq += nq;
   if (b->nq >= co.max_batch) {  // full: the leader runs it now
     b->closed = true;
@@ -297,31 +308,45 @@ static pyr_status search_coalesced(pyr_index *index, const float *q, int64_t nq,
     if (b->status != PYR_OK) return fail(b->status, b->err);
     return PYR_OK;
   }
-  co.cv.wait_until(lk, b->deadline, [&] { return b->closed; });
+  // dispatch when full, when no coalesced search is running (an idle device starts at once; a busy
+  // one gathers every caller that arrives while it works), or at the deadline
+  co.cv.wait_until(lk, b->deadline, [&] { return b->closed || co.inflight == 0; });
   if (!b->closed) {
     b->closed = true;
     auto f = co.open.find(key);
     if (f != co.open.end() && f->second == b) co.open.erase(f);
   }
+  ++co.inflight;
   lk.unlock();
   // one device search for the whole batch, then every caller's rows into its own buffers
-  const int kk = k > 0 ? k : 0;
-  std::vector<float> s((size_t)b->nq * kk);
-  std::vector<int64_t> l((size_t)b->nq * kk);
-  std::vector<int32_t> c((size_t)b->nq);
-  const pyr_status st = search_host(index, b->q.data(), b->nq, k, &b->prm, s.data(), l.data(), c.data());
-  if (st == PYR_OK)
-    for (const Batch::Part &p : b->parts) {
-      if (p.s) std::memcpy(p.s, s.data() + p.off * kk, sizeof(float) * p.n * kk);
-      if (p.l) std::memcpy(p.l, l.data() + p.off * kk, sizeof(int64_t) * p.n * kk);
-      if (p.c) std::memcpy(p.c, c.data() + p.off, sizeof(int32_t) * p.n);
-    }
+  pyr_status st = PYR_OK;
+  std::string err;
+  try {
+    const int kk = k > 0 ? k : 0;
+    std::vector<float> s((size_t)b->nq * kk);
+    std::vector<int64_t> l((size_t)b->nq * kk);
+    std::vector<int32_t> c((size_t)b->nq);
+    st = search_host(index, b->q.data(), b->nq, k, &b->prm, s.data(), l.data(), c.data());
+    if (st == PYR_OK)
+      for (const Batch::Part &p : b->parts) {
+        if (p.s) std::memcpy(p.s, s.data() + p.off * kk, sizeof(float) * p.n * kk);
+        if (p.l) std::memcpy(p.l, l.data() + p.off * kk, sizeof(int64_t) * p.n * kk);
+        if (p.c) std::memcpy(p.c, c.data() + p.off, sizeof(int32_t) * p.n);
+      }
+    else
+      err = pyr_last_error();
+  } catch (...) {
+    st = PYR_E_OOM;
+    err = "coalescer: host allocation failed";
+  }
   lk.lock();
+  --co.inflight;
   b->status = st;
-  if (st != PYR_OK) b->err = pyr_last_error();
+  b->err = err;
   b->done = true;
   co.cv.notify_all();
-  return st;
+  lk.unlock();
+  return st == PYR_OK ? PYR_OK : fail(st, err);
 }
 
 pyr_status pyr_index_search(pyr_index *index, const float *q, int64_t nq, int32_t k, const pyr_search_params *params,
@@ -457,6 +482,20 @@ pyr_status pyr_index_pq_state(const pyr_index *index, float *codebooks, int32_t 
     HIPCHK(hipSetDevice(index->impl->device));
     std::shared_lock<std::shared_mutex> g(index->impl->mu);
     index->impl->pq_state(codebooks, ksub, codes);
+  });
+}
+
+pyr_status pyr_index_labels(const pyr_index *index, int64_t *labels, int64_t *n) {
+  if (!index || !n) return fail(PYR_E_ARG, "null argument");
+  return guard([&] {
+    std::shared_lock<std::shared_mutex> g(index->impl->mu);
+    std::vector<int64_t> all;
+    index->impl->all_labels(all);
+    if (labels) {
+      if (*n < (int64_t)all.size()) throw pyr::Error(PYR_E_ARG, "labels buffer too small");
+      std::copy(all.begin(), all.end(), labels);
+    }
+    *n = (int64_t)all.size();
   });
 }
 

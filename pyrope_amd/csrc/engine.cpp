@@ -57,8 +57,10 @@ void RowStore::reserve(int64_t slots, hipStream_t st) {
   rsq.grow_keep(sizeof(float) * nc, sizeof(float) * cap, st);
   if (cosine) norms.grow_keep(sizeof(float) * nc, sizeof(float) * cap, st);
   if (!rmax.p) {
-    rmax.ensure(sizeof(uint32_t));
-    HIPCHK(hipMemsetAsync(rmax.p, 0, sizeof(uint32_t), st));  // below score_key of any float
+    // [0] score_key of the largest finite |x|^2 (0: below any float), [1] nonzero once a row with a
+    // non-finite |x|^2 was stored (the bf16x3 / fp32 filters cannot certify against such a row)
+    rmax.ensure(2 * sizeof(uint32_t));
+    HIPCHK(hipMemsetAsync(rmax.p, 0, 2 * sizeof(uint32_t), st));
   }
   // new tail: not visible, zero rows (padding rows of a group are never scored)
   HIPCHK(hipMemsetAsync(live.as<uint8_t>() + cap, 0, nc - cap, st));
@@ -983,6 +985,7 @@ struct FlatIndex : Index {
   }
 
   int64_t count() const override { return (int64_t)slot_of.size(); }  // :115-126
+  void all_labels(std::vector<int64_t> &out) const override { (void)live_slots(st, out); }
 
   void snapshot(const std::string &path) override {  // :58-82: the live (id, vector) pairs in slot order
     ImageWriter w(path, PYR_FLAT, dim, metric);
@@ -999,7 +1002,7 @@ struct FlatIndex : Index {
     std::vector<float> rows;
     const int64_t n = read_rows(r, T_FLABELS, T_FROWS, dim, labels, rows);
     if (st.cap) HIPCHK(hipMemsetAsync(st.live.p, 0, st.cap, wst));
-    if (st.rmax.p) HIPCHK(hipMemsetAsync(st.rmax.p, 0, sizeof(uint32_t), wst));
+    if (st.rmax.p) HIPCHK(hipMemsetAsync(st.rmax.p, 0, 2 * sizeof(uint32_t), wst));
     if (q8cap) HIPCHK(hipMemsetAsync(q8ok.p, 0, q8cap, wst));
     HIPCHK(hipStreamSynchronize(wst));
     st.clear();
@@ -1017,6 +1020,9 @@ struct DictBuffer {
   RowStore st;
   std::unordered_map<int64_t, int64_t> slot_of;
   std::vector<int64_t> free_slots;
+  void all_labels(std::vector<int64_t> &out) const {
+    for (const auto &e : slot_of) out.push_back(e.first);
+  }
 
   // returns slots for labels (overwrite existing, reuse freed, else append)
   std::vector<int64_t> place(const int64_t *labels, int64_t n) {
@@ -2120,6 +2126,7 @@ struct IvfFlatIndex : Index {
     uint8_t b = 0;
     if (r.has(T_BUILT)) r.host(T_BUILT, &b, 1);
     const std::vector<float> cents = r.vec<float>(T_CENTS);
+    if (cents.size() % (size_t)dim != 0) ImageReader::throw_format("centroids are not whole rows");
     const int k = (int)(cents.size() / dim);
     if (b && k > 0) {
       const std::vector<int32_t> cnt = r.vec<int32_t>(T_LCOUNT);
@@ -2148,6 +2155,11 @@ struct IvfFlatIndex : Index {
     int64_t c = buf.live_count();
     for (uint8_t s : lstate) c += s != 0;
     return c;
+  }
+  void all_labels(std::vector<int64_t> &out) const override {
+    buf.all_labels(out);
+    for (size_t p = 0; p < lstate.size(); p++)
+      if (lstate[p] != 0) out.push_back(lists.hlabels[p]);
   }
 
   void centroids(float *out, int32_t *nl) const override {  // :314-325
@@ -2490,6 +2502,11 @@ struct IvfPqIndex : Index {
   }
 
   int64_t count() const override { return 0; }  // :230 GetStats quirk
+  void all_labels(std::vector<int64_t> &out) const override {
+    buf.all_labels(out);
+    for (int64_t lab : hlabels)
+      if (lab >= 0) out.push_back(lab);
+  }
 
   // The reference's IvfPq Snapshot / Load are no-ops (:228-229); the image persists the trained
   // state (quantizer, codebooks, codes in list order) and the buffer like IVF_FLAT's.
@@ -2532,6 +2549,7 @@ struct IvfPqIndex : Index {
     uint8_t b = 0;
     if (r.has(T_BUILT)) r.host(T_BUILT, &b, 1);
     const std::vector<float> cents = r.vec<float>(T_CENTS);
+    if (cents.size() % (size_t)dim != 0) ImageReader::throw_format("centroids are not whole rows");
     const int k = (int)(cents.size() / dim);
     if (b && k > 0) {
       int32_t ks = 0;

@@ -154,6 +154,9 @@ struct Index {
   }
   virtual void ivf_layout(int64_t *off, int64_t *labels, uint8_t *live, int64_t *total) const;
   virtual void pq_state(float *cb, int32_t *ksub, uint8_t *codes) const;
+  // the labels of every row the index holds (buffer and lists; a label may repeat when a buffer row
+  // shadows a list entry): the shim's id map of an image loaded without one (pyr_index_labels)
+  virtual void all_labels(std::vector<int64_t> &out) const = 0;
   // BruteForceVectorIndex.Scan (:250-273): live rows in slot order; labels/x may be null
   virtual void scan(int64_t *labels, float *x, int64_t *n) {
     (void)labels;

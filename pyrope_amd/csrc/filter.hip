@@ -689,6 +689,7 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
     }
     const double approx_k1 = MET == L2 ? (double)ms[k1 - 1] - (double)qsq : (double)ms[k1 - 1];
     ok = nout == k && (double)skth > approx_k1 + e;
+    if (!a.q16 && a.max_rsq && a.max_rsq[1] != 0u) ok = false;  // a non-finite row the filter cannot score
   }
   if (lane == 0) {
     if (a.out_c) a.out_c[q] = nout;
@@ -730,9 +731,12 @@ __global__ void sqnorms_kernel(const float *rows, const int64_t *slots, int64_t 
     s = s + x * x;
   }
   out[r] = s;
-  // a NaN / inf row cannot be certified against anyway (its approximate score is never a
-  // candidate); leaving it out keeps one bad row from failing every later certificate
+  // a NaN / inf row is left out of the norm bound (one bad row would fail every later certificate);
+  // the fp16 tile filters carry it in meta (+inf: always a candidate), the bf16x3 / fp32 filters
+  // cannot score it (hi = inf, lo = inf - inf = NaN), so max_key[1] marks the store and their
+  // certificate fails
   if (isfinite(s)) atomicMax(max_key, score_key(s));
+  else max_key[1] = 1u;
 }
 
 // per-list max of |x|^2 (score_key, finite rows only) over rows [lb[l], le[l]): the refine

@@ -93,18 +93,23 @@ ImageReader::ImageReader(const std::string &path) {
   kind = h[1];
   dim = h[2];
   metric = h[3];
+  if (std::fseek(f, 0, SEEK_END) != 0) throw_format("unreadable");
+  const long fend = std::ftell(f);
+  if (fend < 0) throw_format("unreadable");
+  const uint64_t fsize = (uint64_t)fend;
   uint64_t off = 8 + 16 + 4;
+  if (std::fseek(f, (long)off, SEEK_SET) != 0) throw_format("short header");
   for (uint32_t i = 0; i < n; i++) {
     uint32_t t[2];
     uint64_t nb;
     if (std::fread(t, 1, 8, f) != 8 || std::fread(&nb, 1, 8, f) != 8) throw_format("short section header");
     off += 16;
+    // every section lies inside the file (untrusted sizes: no wrap-around of off)
+    if (off > fsize || nb > fsize - off) throw_format("section " + std::to_string(t[0]) + " runs past the end");
     sec[t[0]] = {off, nb};
     off += nb + (8 - nb % 8) % 8;
-    if (std::fseek(f, (long)off, SEEK_SET) != 0) throw_format("short section");
+    if (std::fseek(f, (long)std::min(off, fsize), SEEK_SET) != 0) throw_format("short section");
   }
-  // the last section must be complete
-  if (std::fseek(f, 0, SEEK_END) != 0 || (uint64_t)std::ftell(f) < off - 7) throw_format("truncated");
 }
 
 ImageReader::~ImageReader() {

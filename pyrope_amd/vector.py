@@ -270,14 +270,21 @@ class HipVectorIndex(IVectorIndex):
     # ---- IVectorIndex.Snapshot / Load (IVectorIndex.cs:26-27) ----
     def snapshot(self, path: str) -> None:
         """The library's binary image at `path` (pyr_index_snapshot) plus the shim's id <-> label map
-        at path + ".ids" (JSON), each written through a temp file and a rename."""
+        at path + ".ids" (JSON), each written through a temp file and a rename.  The map records the
+        image it belongs to (size and mtime of the renamed image), so a crash between the two renames
+        cannot pair a new image with the previous snapshot's map: load() then ignores
+        the stale map and falls back to str(label) ids."""
         if path is None or str(path).strip() == "":
             raise ArgumentException("Path cannot be empty.")
         check(self._L.pyr_index_snapshot(self._h, os.fsencode(str(path))))
-        ids = {"next": self._next_label, "ids": [[i, lab] for i, lab in self._label_of.items()]}
+        st = os.stat(str(path))
+        ids = {"next": self._next_label, "image": [st.st_size, st.st_mtime_ns],
+               "ids": [[i, lab] for i, lab in self._label_of.items()]}
         tmp = str(path) + ".ids.tmp"
         with open(tmp, "w") as f:
             json.dump(ids, f)
+            f.flush()
+            os.fsync(f.fileno())
         os.replace(tmp, str(path) + ".ids")
 
     def load(self, path: str) -> None:
@@ -286,15 +293,34 @@ class HipVectorIndex(IVectorIndex):
         check(self._L.pyr_index_load(self._h, os.fsencode(str(path))))
         self._label_of, self._id_of = {}, {}
         self._next_label = 0
+        ids = None
         try:
             with open(str(path) + ".ids") as f:
                 ids = json.load(f)
         except FileNotFoundError:
-            return  # an image without the shim's map: ids read back as str(label)
+            pass
+        if ids is not None and "image" in ids:
+            st = os.stat(str(path))
+            if list(ids["image"]) != [st.st_size, st.st_mtime_ns]:
+                ids = None  # the map of another image
+        if ids is None:
+            # an image without (its own) shim map, e.g. written by pyr_index_snapshot directly or by
+            # another client: every loaded row's id is str(label), new ids get labels above them all
+            self._register_labels(self.loaded_labels())
+            return
         for i, lab in ids["ids"]:
             self._label_of[i] = lab
             self._id_of[lab] = i
         self._next_label = int(ids.get("next", 0))
+
+    def loaded_labels(self) -> np.ndarray:
+        """Labels of every row the index holds (pyr_index_labels)."""
+        n = C.c_int64(0)
+        check(self._L.pyr_index_labels(self._h, None, C.byref(n)))
+        out = np.zeros(max(n.value, 1), np.int64)
+        n2 = C.c_int64(len(out))
+        check(self._L.pyr_index_labels(self._h, ptr(out, C.c_int64), C.byref(n2)))
+        return np.unique(out[: n2.value])
 
     # ---- introspection used by parity tests and the CPU baseline ----
     def ivf_layout(self):

@@ -226,3 +226,27 @@ def test_non_finite_rows_do_not_poison_the_certificate(hiplib, metric):
     _same(got, ref)
     assert 5000 not in got[1]  # NaN scores never rank (the Inf row does rank first for IP: +inf)
     assert nfb <= len(q) // 20, nfb
+
+
+@pytest.mark.parametrize("prec", ["1", "0"])  # bf16x3 (also FLAT items above 65,536 rows), fp32 MFMA
+@pytest.mark.parametrize("metric", [0, 1])
+def test_non_finite_rows_bf16x3_and_fp32_filters(hiplib, metric, prec):
+    """the bf16x3 / fp32 filters cannot score a row holding Inf (bf16x3: hi = inf,
+    lo = inf - inf = NaN), so such a row is never their candidate.  The store marks that it holds
+    one (RowStore::rmax[1]) and their certificate fails, so the exact scan answers: an IP row with an
+    +Inf component ranks first with score +Inf, exactly as the reference's heap keeps it."""
+    from pyrope_amd import generate_synthetic
+    d = 128
+    x = generate_synthetic(20000, d, 42)
+    x[5000] = np.nan
+    x[7000, 3] = np.inf
+    q = generate_synthetic(100, d, 1337)
+    idx = _flat(d, metric, x)
+    with _env(PYR_FILTER_PREC=prec):
+        got = idx.search_batch(q, 10)
+    with _env(PYR_FILTER=0):
+        ref = idx.search_batch(q, 10)
+    _same(got, ref)
+    assert 5000 not in got[1]
+    if metric == 1:
+        assert (got[1][:, 0] == 7000).all() and np.isposinf(got[0][:, 0]).all()

@@ -173,3 +173,71 @@ def test_delta_manifest_round_trip(hiplib, tmp_path):  # DeltaVectorIndex.cs:160
     assert e.get_stats().count == d.get_stats().count
     for i in range(0, 300, 7):
         assert [r.id for r in e.search(x[i], 5)] == [r.id for r in d.search(x[i], 5)]
+
+
+@pytest.mark.parametrize("kind", ["flat", "ivf"])
+def test_load_without_id_map_keeps_labels_unique(hiplib, tmp_path, kind):
+    """an image loaded without the shim's .ids map (written by pyr_index_snapshot directly
+    or by another client) exposes its rows as str(label) ids; a new id must get a label above every
+    loaded one (no collision with row '0'), and deleting a loaded id must work."""
+    from pyrope_amd import BruteForceVectorIndex, IvfFlatVectorIndex, VectorMetric, generate_synthetic
+    mk = (lambda: BruteForceVectorIndex(16, VectorMetric.L2)) if kind == "flat" else \
+        (lambda: IvfFlatVectorIndex(16, VectorMetric.L2, n_list=4))
+    x = generate_synthetic(300, 16, 3)
+    idx = mk()
+    idx.add_labels(np.arange(300, dtype=np.int64), x)
+    if kind == "ivf":
+        idx.build()
+        idx.add_labels(np.array([300, 301], np.int64), x[:2] + 1.0)  # buffer rows after the build
+    path = str(tmp_path / "img")
+    idx.snapshot(path)
+    os.remove(path + ".ids")
+    loaded = mk()
+    loaded.load(path)
+    n_rows = 300 if kind == "flat" else 302
+    assert loaded._next_label == n_rows
+    loaded.add("fresh", np.full(16, 7.0, np.float32))  # FLAT would raise on a reused label 0
+    res = loaded.search(np.full(16, 7.0, np.float32), 1)
+    assert res[0].id == "fresh"
+    assert loaded.delete("0")
+    assert "0" not in [r.id for r in loaded.search(x[0], 5)]
+
+
+def test_stale_id_map_is_ignored(hiplib, tmp_path):
+    """the .ids map records the image it belongs to; an image replaced without its map
+    (a crash between the two renames) loads with str(label) ids instead of another image's ids."""
+    from pyrope_amd import BruteForceVectorIndex, VectorMetric
+    a = BruteForceVectorIndex(4, VectorMetric.L2)
+    a.add("alpha", [1, 0, 0, 0])
+    a.add("beta", [0, 1, 0, 0])
+    path = str(tmp_path / "img")
+    a.snapshot(path)
+    ids_a = open(path + ".ids").read()
+    b = BruteForceVectorIndex(4, VectorMetric.L2)
+    b.add("gamma", [0, 0, 1, 0])
+    b.add("delta", [0, 0, 0, 1])
+    b.add("eps", [1, 1, 0, 0])
+    b.snapshot(path)
+    open(path + ".ids", "w").write(ids_a)  # the previous snapshot's map next to the new image
+    c = BruteForceVectorIndex(4, VectorMetric.L2)
+    c.load(path)
+    assert c.search([0, 0, 1, 0], 1)[0].id == "0"
+    assert c._next_label == 3
+
+
+def test_corrupt_images_raise_format_errors(hiplib, tmp_path):
+    """centroids that are not whole rows, and section sizes running past the end of the
+    file (including sizes that would wrap the offset), are rejected as malformed images."""
+    from pyrope_amd import IvfFlatVectorIndex
+    from pyrope_amd._lib import JsonException
+    p1 = str(tmp_path / "cents")
+    _image(p1, 1, 4, 0, [(1, b"\1"), (2, np.zeros(6, np.float32).tobytes())])  # T_CENTS: 1.5 rows
+    with pytest.raises(JsonException):
+        IvfFlatVectorIndex(4, 0).load(p1)
+    p2 = str(tmp_path / "wrap")
+    with open(p2, "wb") as f:
+        f.write(b"PYRIDX01" + struct.pack("<iiiiI", 1, 1, 4, 0, 2))
+        f.write(struct.pack("<IIQ", 6, 0, 2 ** 64 - 8))  # wraps off back to the start
+        f.write(struct.pack("<IIQ", 1, 0, 1) + b"\1" + b"\0" * 7)
+    with pytest.raises(JsonException):
+        IvfFlatVectorIndex(4, 0).load(p2)
