@@ -302,19 +302,31 @@ def run(args):
     # (PYR_FILTER=0): sub, mul, add per element, 3*D
     flops = scan["pairs"] * (2 if filt else 3) * D
     achieved = flops / (scan["ms"] * 1e-3) / 1e12
-    # the list-scan arithmetic (engine.cpp filter_prec): 2 = fp16 residual tiles, hi/lo query split
-    # (2 fp16 MFMAs per k-step, filter16.hip, default); 3 = one fp16 MFMA; 1 = bf16x3; 0 = fp32 MFMA
+    # the list-scan kernel and arithmetic (engine.cpp search_filter / search_stream): by default the
+    # stream-and-emit scan (stream16.hip) with one fp16 MFMA per k-step (PYR_STREAM_PREC=2: the hi/lo
+    # query split, 2); PYR_IVF_STREAM=0 -> the round-2 filter kernels (PYR_FILTER_PREC: 2 = fp16 tiles
+    # with the hi/lo split, 3 = one fp16 MFMA, 1 = bf16x3, 0 = fp32 MFMA)
     prec = int(os.environ.get("PYR_FILTER_PREC", "2")) if filt else -1
-    mfma_mult, mfma_peak = {2: (2, BF16_PEAK_TFLOPS), 3: (1, BF16_PEAK_TFLOPS), 1: (3, BF16_PEAK_TFLOPS),
-                            0: (1, FP32_PEAK_TFLOPS)}.get(prec, (1, FP32_PEAK_TFLOPS))
+    stream = filt and prec in (2, 3) and os.environ.get("PYR_IVF_STREAM", "1") != "0" and D in (32, 64, 128)
     wide = os.environ.get("PYR_F16_WIDE", "1") != "0"
-    kernel_name = {2: ("mfma_filter16w<128,L2,16,f16x2> (IVF list scan, fp16 residual tiles, 8 waves x 16 queries, "
-                       "2 v_mfma_f32_16x16x32_f16 per k-step)") if wide else
-                      "mfma_filter16<128,L2,16,f16x2> (IVF list scan, fp16 residual tiles, 2 fp16 MFMAs per k-step)",
-                   3: "mfma_filter16<128,L2,16,f16x1> (IVF list scan, fp16 residual tiles, 1 fp16 MFMA per k-step)",
-                   1: "mfma_filter<128,L2,IVF> (IVF list scan, bf16x3 MFMA candidate filter)",
-                   0: "mfma_filter<128,L2,IVF> (IVF list scan, fp32 MFMA candidate filter)"}.get(
-                       prec, "scan_fast<128,1,L2,IVF> (IVF list scan, exact VALU)")
+    if stream:
+        q2 = os.environ.get("PYR_STREAM_PREC", "3") == "2"
+        kernel_tag = "stream16"
+        mfma_mult, mfma_peak = (2 if q2 else 1), BF16_PEAK_TFLOPS
+        kernel_name = (f"stream16_kernel<{D},L2,{'f16x2' if q2 else 'f16x1'},MAIN> (IVF list scan, stream-and-emit over "
+                       f"fp16 residual tiles: persistent 8-wave blocks, tiles straight from HBM into registers, rows "
+                       f"as the A operand of v_mfma_f32_16x16x32_f16, {2 if q2 else 1} MFMA per k-step)")
+    else:
+        kernel_tag = {2: "filter16w" if wide else "filter16", 3: "filter16"}.get(prec, "filter")
+        mfma_mult, mfma_peak = {2: (2, BF16_PEAK_TFLOPS), 3: (1, BF16_PEAK_TFLOPS), 1: (3, BF16_PEAK_TFLOPS),
+                                0: (1, FP32_PEAK_TFLOPS)}.get(prec, (1, FP32_PEAK_TFLOPS))
+        kernel_name = {2: ("mfma_filter16w<128,L2,16,f16x2> (IVF list scan, fp16 residual tiles, 8 waves x 16 queries, "
+                           "2 v_mfma_f32_16x16x32_f16 per k-step)") if wide else
+                          "mfma_filter16<128,L2,16,f16x2> (IVF list scan, fp16 residual tiles, 2 fp16 MFMAs per k-step)",
+                       3: "mfma_filter16<128,L2,16,f16x1> (IVF list scan, fp16 residual tiles, 1 fp16 MFMA per k-step)",
+                       1: "mfma_filter<128,L2,IVF> (IVF list scan, bf16x3 MFMA candidate filter)",
+                       0: "mfma_filter<128,L2,IVF> (IVF list scan, fp32 MFMA candidate filter)"}.get(
+                           prec, "scan_fast<128,1,L2,IVF> (IVF list scan, exact VALU)")
     # unique algorithmic bytes of one list-scan launch on this rank: every list probed by any query
     # of the batch read once (its live rows of this shard x D x 4 B) plus the batch's queries -- the
     # HBM floor of a batched, list-major scan (SURVEY.md 8(d) "unique-bytes roofline")
@@ -394,10 +406,10 @@ def run(args):
     # list-scan arithmetic it was measured on
     traffic, traffic_src = None, None
     tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "traffic.json")
-    if os.path.exists(tpath) and world == 1 and prec == 2:
+    if os.path.exists(tpath) and world == 1:
         tj = json.load(open(tpath))
         tc = tj.get("config", {})
-        same_kernel = ("filter16w" in tj.get("kernel", "")) == wide
+        same_kernel = tj.get("kernel_tag") == kernel_tag
         if same_kernel and (tc.get("n"), tc.get("dim"), tc.get("nlist"), tc.get("nprobe"), tc.get("k"),
                             tc.get("nq")) == (N, D, args.nlist, args.nprobe, k, args.nq):
             traffic, traffic_src = tj["hbm_read_bytes_per_launch"], tj["source"]
@@ -409,6 +421,8 @@ def run(args):
             "value": qps,
             "unit": "queries/s",
             "n_gpus": world,
+            "ranks_seen": dist.get_world_size() if world > 1 else 1,
+            "backend": dist.get_backend() + " (RCCL)" if world > 1 else None,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
@@ -433,11 +447,12 @@ def run(args):
                          "kernel": kernel_name,
                          "stored_bytes_per_launch": stored_bytes,
                          "stored_GBps": stored_bytes / (scan["ms"] * 1e-3) / 1e9,
+                         "stored_frac": stored_bytes / (scan["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
                          "note": ("algorithmic bytes = every probed list read once per launch (live rows x D x "
                                   "4 B, the reference's fp32 rows) + queries, over the HIP-event time of the launch "
                                   "(rank 0); stored_bytes = what the fp16 tile kernel actually streams for them "
-                                  "(D x 2 + 4 B per padded row); traffic (FETCH_SIZE x 2, its own rocprofv3 pass) is "
-                                  "in profiles/*/summary.md")},
+                                  "(D x 2 + 4 B per padded row), stored_frac = their rate vs the peak; traffic (FETCH_SIZE x 2, its "
+                                  "own rocprofv3 pass, per launch) is in profiles/*/summary.md")},
             "mfma": {"achieved": achieved * mfma_mult, "peak": mfma_peak, "unit": "TFLOP/s",
                      "frac": achieved * mfma_mult / mfma_peak,
                      "note": (f"as-executed MFMA flops: probed (query,row) pairs x 2*D x {mfma_mult} (MFMAs per "
@@ -445,9 +460,9 @@ def run(args):
                               "probed pairs x 2*D (fp32 MFMA) or x 3*D (exact VALU) vs the FP32 peak")},
             "exact_reruns": {"queries": fallback_queries, "in_profiled_steps": args.profile_steps,
                              "note": "queries whose MFMA-filter certificate failed and were re-scanned exactly"},
-            "hbm_equivalent": {"bytes_per_query": bytes_per_query,
-                               "GBps": qps * bytes_per_query / 1e9 / world,
-                               "frac_of_8TBps_per_gpu": qps * bytes_per_query / 1e9 / world / HBM_PEAK_GBS},
+            "per_query_bytes": {"bytes_per_query": bytes_per_query,
+                                "note": "SURVEY.md 8(d): nprobe/nlist x N x D x 4 + nlist x D x 4 per query (no "
+                                        "batching reuse); not a roofline"},
             "phases_ms": {k_: round(v["ms"], 4) for k_, v in phases.items()},
             "cpu_baseline": cpu,
         }

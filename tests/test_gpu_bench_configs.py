@@ -1,0 +1,130 @@
+"""The coarse / probe configurations the benches run, under the oracle.
+
+I1 ranks nlist = 1024 centroids with nprobe = 32, M8 8192 with nprobe = 32 (and 64 here), P1 4096
+with nprobe = 64 on d = 768 / M = 96 codes.  The coarse selection kernel is instantiated by list count
+and nprobe (coarse.hip coarse_select_reg_kernel<16> at 1024 centroids, <32> at nprobe = 32 and <64>
+at nprobe = 64 over 4096 / 8192), so these sizes reach code the small-nlist tests never run.  N stays small (a few to a few tens of rows
+per list), and the quantizers are supplied (pyr_index_set_centroids / set_codebooks: sampled rows),
+so every case takes seconds.  Reference: Vector/IvfFlatVectorIndex.cs:186-198 (ranking) and
+:200-218 (list scan), Vector/IvfPqVectorIndex.cs:141-198, ProductQuantizer.cs:98-120.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+class _env:
+    def __init__(self, **kv):
+        self.kv = {k: str(v) for k, v in kv.items()}
+
+    def __enter__(self):
+        self.old = {k: os.environ.get(k) for k in self.kv}
+        os.environ.update(self.kv)
+
+    def __exit__(self, *a):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _same(a, b):
+    (s1, l1, c1), (s2, l2, c2) = a, b
+    np.testing.assert_array_equal(c1, c2)
+    np.testing.assert_array_equal(l1, l2)
+    assert np.array_equal(s1.view(np.uint32), s2.view(np.uint32))
+
+
+_CACHE = {}
+
+
+def _ivf(nlist, per_list, metric, dim=128):
+    from pyrope_amd import IvfFlatVectorIndex, generate_synthetic
+    key = (nlist, per_list, metric, dim)
+    if key not in _CACHE:
+        n = nlist * per_list
+        x = generate_synthetic(n, dim, 42)
+        rng = np.random.default_rng(nlist)
+        cents = x[rng.choice(n, nlist, replace=False)].copy()
+        idx = IvfFlatVectorIndex(dim, metric, n_list=nlist)
+        idx.set_centroids(cents)
+        idx.add_labels(np.arange(n, dtype=np.int64), x)
+        idx.build()
+        _CACHE[key] = (idx, x)
+    return _CACHE[key]
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+@pytest.mark.parametrize("nlist,nprobe,per_list", [(1024, 32, 40), (4096, 64, 12), (8192, 32, 12), (8192, 64, 12)])
+def test_ivf_flat_bench_coarse_configs(hiplib, oracle, metric, nlist, nprobe, per_list):
+    """I1 / M8-shaped coarse ranking + list scan vs the exact VALU path and the oracle."""
+    from pyrope_amd import SearchOptions, generate_synthetic
+    idx, x = _ivf(nlist, per_list, metric)
+    q = generate_synthetic(600, 128, 1337)
+    opts = SearchOptions(nprobe=nprobe)
+    got = idx.search_batch(q, 10, opts)
+    with _env(PYR_FILTER=0):
+        ref = idx.search_batch(q, 10, opts)
+    _same(got, ref)
+    off, labels, live = idx.ivf_layout()
+    rows = x[np.where(labels >= 0, labels, 0)]
+    cents = idx.centroids_array()
+    for i in range(0, len(q), 47):
+        os_, ok = oracle.ivf_search(q[i], 10, cents, rows, off, live, metric=metric, nprobe=nprobe)
+        np.testing.assert_array_equal(got[1][i][: len(ok)], labels[ok])
+        assert np.array_equal(got[0][i][: len(ok)].view(np.uint32), os_.view(np.uint32))
+
+
+@pytest.mark.parametrize("nlist", [1024, 8192])
+def test_probe_lists_equal_oracle_ranking(hiplib, oracle, nlist):
+    """pyr_index_probe_device (the multi-GPU step's coarse split) at the bench list counts: the
+    probe SET of every query equals the oracle's top-nprobe ranking (ComputeScore, ties -> lower
+    centroid index)."""
+    import torch
+
+    from pyrope_amd import SearchOptions, generate_synthetic
+    idx, _ = _ivf(nlist, 12 if nlist > 1024 else 40, 0)
+    nq, npb = 200, 32
+    qh = generate_synthetic(nq, 128, 7)
+    q = torch.from_numpy(qh).cuda()
+    pr = torch.empty((nq, npb), dtype=torch.int32, device="cuda")
+    assert idx.probe_device(q.data_ptr(), nq, pr.data_ptr(), 0, SearchOptions(nprobe=npb)) == npb
+    torch.cuda.synchronize()
+    got = pr.cpu().numpy()
+    cents = idx.centroids_array()
+    for i in range(0, nq, 19):
+        exp = np.asarray(oracle.ivf_probe(qh[i], cents, npb, metric=0))
+        assert sorted(got[i].tolist()) == sorted(exp.tolist())
+
+
+@pytest.mark.parametrize("nlist,nprobe", [(256, 64), (4096, 64)])
+def test_ivf_pq_p1_geometry(hiplib, oracle, nlist, nprobe):
+    """P1 geometry: d = 768, M = 96 (8-dim subspaces), K = 256, nprobe = 64, with supplied quantizers
+    (the P1 bulk path) -- LUT, ADC and ranking bit-identical to the oracle."""
+    from pyrope_amd import IvfPqVectorIndex, SearchOptions, generate_synthetic
+    d, m, ksub = 768, 96, 256
+    n = nlist * 6
+    x = generate_synthetic(n, d, 42)
+    rng = np.random.default_rng(5)
+    cents = x[rng.choice(n, nlist, replace=False)].copy()
+    sub = x[rng.choice(n, ksub, replace=False)].reshape(ksub, m, d // m)
+    cb = np.ascontiguousarray(sub.transpose(1, 0, 2))  # [M][ksub][d / M]
+    idx = IvfPqVectorIndex(d, 0, m=m, k=ksub, n_list=nlist)
+    idx.set_centroids(cents)
+    idx.set_codebooks(cb)
+    idx.add_labels(np.arange(n, dtype=np.int64), x)
+    idx.build()
+    gcb, codes, off, labels, live = idx.pq_state()
+    assert np.array_equal(gcb.view(np.uint32), cb.view(np.uint32))
+    q = generate_synthetic(64, d, 1337)
+    s, l, c = idx.search_batch(q, 10, SearchOptions(nprobe=nprobe))
+    gc = idx.centroids_array()
+    for i in range(0, len(q), 9):
+        os_, ok = oracle.ivfpq_search(q[i], 10, gc, codes, off, gcb, live, metric=0, nprobe=nprobe)
+        assert int(c[i]) == len(os_)
+        np.testing.assert_array_equal(l[i][: len(ok)], labels[ok])
+        assert np.array_equal(s[i][: len(os_)].view(np.uint32), os_.view(np.uint32))
