@@ -1880,6 +1880,7 @@ struct IvfFlatIndex : Index {
     sa.key_base = 0;
     sa.row_limit = 0xFFFFFFFFu;
     sa.ablate = filter_ablate();
+    sa.thr_bias = getenv("PYR_STREAM_THR_BIAS") ? (float)atof(getenv("PYR_STREAM_THR_BIAS")) : 0.0f;
     {
       PhaseTimer t(PH_SAMPLE, ws.st);
       launch_stream_prep(sa, metric, maxi, ws.st);

@@ -346,6 +346,7 @@ struct StreamArgs {
   int32_t *work;              // persistent-block item counter (zeroed before each launch)
   uint32_t key_base, row_limit;
   int32_t ablate;             // measurement only (PYR_FILTER_ABLATE=64: no emission)
+  float thr_bias;             // measurement only (PYR_STREAM_THR_BIAS: added to T_q; results then differ)
 };
 struct CandMergeArgs {
   const float *cand_s;

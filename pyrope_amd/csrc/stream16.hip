@@ -111,9 +111,8 @@ __global__ __launch_bounds__(64 * SNW, 1) void stream16_kernel(StreamArgs a) {
   constexpr int QMAX = Q2 ? 256 : 512;  // queries per item
   constexpr int PIECES = QMAX / 16 * KS;
   __shared__ __attribute__((aligned(16))) char bl[(Q2 ? 2 : 1) * PIECES * 1024];
-  __shared__ float2 ft[QMAX];     // {f, threshold in y = f acc + meta space}
-  __shared__ float cqs[QMAX];     // score = y + cq
-  __shared__ int osl[QMAX];       // region (MAIN) / sample row (SAMPLE) of the query
+  __shared__ float4 qr[QMAX];     // per query slot: {f, threshold in y = f acc + meta space, cq (score = y + cq),
+                                  //  region (MAIN) / sample row (SAMPLE) as int bits}
   __shared__ int cnt_l[QMAX];     // rows emitted
   __shared__ uint32_t flr_l[QMAX];  // score_key of the best row a full region dropped (0: none)
   __shared__ int item_sh;
@@ -151,14 +150,12 @@ __global__ __launch_bounds__(64 * SNW, 1) void stream16_kernel(StreamArgs a) {
           const int slot = a.qlist[pos];
           const float2 fc = a.qsc[pos];
           const int q = slot / a.nparts;
-          const float T = (!SAMPLE && a.thr) ? a.thr[q] : -INFINITY;
+          const float T = (!SAMPLE && a.thr) ? a.thr[q] + a.thr_bias : -INFINITY;
           v = make_float2(fc.x, lower_thr(T, fc.y));
           cqv = fc.y;
           o = SAMPLE ? q * a.nprobe + (slot % a.nparts) / a.cmax : slot + it.part;
         }
-        ft[i] = v;
-        cqs[i] = cqv;
-        osl[i] = o;
+        qr[i] = make_float4(v.x, v.y, cqv, __int_as_float(o));
         cnt_l[i] = 0;
         flr_l[i] = 0u;
       }
@@ -240,7 +237,8 @@ __global__ __launch_bounds__(64 * SNW, 1) void stream16_kernel(StreamArgs a) {
       if (h1) row_terms(M1, w + SNW, mr1);
       for (int j = 0; j < ng; ++j) {
         const int qi = 16 * j + c;
-        const float f = ft[qi].x;
+        const float4 rq = qr[qi];
+        const float f = rq.x;
         float mx = -INFINITY;
         if (h0) {
           float y[8];
@@ -252,90 +250,111 @@ __global__ __launch_bounds__(64 * SNW, 1) void stream16_kernel(StreamArgs a) {
           scores(A1, mr1, j, f, y);
           mx = fmaxf(mx, max3f(max3f(y[0], y[1], y[2]), max3f(y[3], y[4], y[5]), fmaxf(y[6], y[7])));
         }
-        if (qi < qcnt) a.samp[(size_t)osl[qi] * SV + w * 4 + g] = mx + cqs[qi];
+        if (qi < qcnt) a.samp[(size_t)__float_as_int(rq.w) * SV + w * 4 + g] = mx + rq.z;
       }
     } else {
-      // rows whose score can reach T_q -> the query's region of the part
-      auto emit = [&](int j, const float (&y)[8], float tl, int rt) {
-        const int qi = 16 * j + c;
-        const float cqv = cqs[qi];
-        const size_t rb = (size_t)osl[qi] * a.cap;
+      const bool ABL = (a.ablate & 64) != 0;
+      // rows whose score can reach T_q -> the query's region of the part: the lane counts its passing
+      // rows, reserves that many slots with ONE returning LDS atomic, then stores them (a region that
+      // is full keeps the best score it had to drop as its floor)
+      auto emit = [&](const float (&y)[8], const float4 rq, int qi, int rt) {
+        uint32_t m = 0u;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m |= (y[e] >= rq.y ? 1u : 0u) << e;
+        if (m == 0u) return;
+        int slot = atomicAdd(&cnt_l[qi], __builtin_popcount(m));
+        const size_t rb = (size_t)__float_as_int(rq.w) * a.cap;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const bool p = y[e] >= tl;
-          if (!__builtin_amdgcn_ballot_w64(p)) continue;
-          if (p) {
-            const float s = y[e] + cqv;
-            const uint32_t key = a.key_base | (uint32_t)(rt + 16 * (e >> 2) + 4 * g + (e & 3));
-            const int slot = atomicAdd(&cnt_l[qi], 1);
+          if (m & (1u << e)) {
+            const float s = y[e] + rq.z;
             if (slot < a.cap) {
               a.cand_s[rb + slot] = s;
-              a.cand_k[rb + slot] = key;
+              a.cand_k[rb + slot] = a.key_base | (uint32_t)(rt + 16 * (e >> 2) + 4 * g + (e & 3));
             } else {
               atomicMax(&flr_l[qi], score_key(s));
             }
+            ++slot;
           }
         }
       };
-      // group j's scores from its accumulators; the emit branch when a row can reach T_q
-      auto epi = [&](const f4v (&acc)[2], const float (&mr)[8], int j, int rt) {
-        const float2 fs = ft[16 * j + c];
+      // group j's scores from its accumulators (rq: the group's query record, read one group ahead);
+      // the emit branch when a row of the wave can reach its query's T_q
+      auto epi = [&](const f4v (&acc)[2], const float (&mr)[8], int j, const float4 rq, int rt) {
         float y[8];
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) y[4 * b + i] = fmaf(fs.x, acc[b][i], mr[4 * b + i]);
+          for (int i = 0; i < 4; ++i) y[4 * b + i] = fmaf(rq.x, acc[b][i], mr[4 * b + i]);
         const float mx = max3f(max3f(y[0], y[1], y[2]), max3f(y[3], y[4], y[5]), fmaxf(y[6], y[7]));
-        if (a.ablate & 64) {
+        if (ABL) {
           if (mx == 12345.0f) cnt_l[0] = 1;  // measurement only: keep the scores live
           return;
         }
-        if (__builtin_amdgcn_ballot_w64(mx >= fs.y)) emit(j, y, fs.y, rt);
+        if (__builtin_amdgcn_ballot_w64(mx >= rq.y)) emit(y, rq, 16 * j + c, rt);
       };
-      // one tile against every group, software-pipelined over pairs of groups: group j + 1's operands
-      // are read while group j's MFMAs run, and group j - 1's epilogue runs behind group j's MFMAs
+      // one tile against every group, software-pipelined over pairs of groups: group j + 1's record and
+      // operands are read while group j's MFMAs run (the record first, so waiting for it never waits for
+      // operand reads issued after it), and group j - 1's epilogue runs behind group j's MFMAs
       auto tile = [&](const h8v (&A)[KS][2], const f4v (&M)[2], int t) {
         float mr[8];
         row_terms(M, t, mr);
         const int rt = r0 + 32 * t;
         h8v b0[KS], b1[KS], o0[KS], o1[KS];
         f4v a0[2], a1[2];
+        // (the reads ahead are unconditional, clamped to the last group: a conditional read would make
+        // the compiler's lgkmcnt accounting wait for every outstanding LDS read at the join)
+        float4 r0q = qr[c], r1q = r0q, r0n = r0q, r1p = r0q;
         read_b(0, b0, o0);
         for (int j = 0;;) {
-          if (j + 1 < ng) read_b(j + 1, b1, o1);
+          {
+            const int jn = min(j + 1, ng - 1);
+            r1q = qr[16 * jn + c];
+            read_b(jn, b1, o1);
+          }
           mma(A, b0, o0, a0);
-          if (j > 0) epi(a1, mr, j - 1, rt);
+          if (j > 0) epi(a1, mr, j - 1, r1p, rt);
           if (j + 1 >= ng) {
-            epi(a0, mr, j, rt);
+            epi(a0, mr, j, r0q, rt);
             break;
           }
-          if (j + 2 < ng) read_b(j + 2, b0, o0);
+          {
+            const int jn = min(j + 2, ng - 1);
+            r0n = qr[16 * jn + c];
+            read_b(jn, b0, o0);
+          }
           mma(A, b1, o1, a1);
-          epi(a0, mr, j, rt);
+          epi(a0, mr, j, r0q, rt);
+          r0q = r0n;
+          r1p = r1q;
           j += 2;
           if (j >= ng) {
-            epi(a1, mr, j - 1, rt);
+            epi(a1, mr, j - 1, r1p, rt);
             break;
           }
         }
       };
+      // double-buffered tiles; the prefetch of tile t + 8 is unconditional (the last tile is re-read when
+      // there is none): a conditional load makes the compiler's vmcnt accounting wait for the
+      // prefetch itself before the current tile, which serialised every tile behind an HBM round trip
       h8v A0[KS][2], A1[KS][2];
       f4v M0[2], M1[2];
       int t = w;
       if (t < nt) load(t, A0, M0);
       while (t < nt) {
-        if (t + SNW < nt) load(t + SNW, A1, M1);
+        load(min(t + SNW, nt - 1), A1, M1);
         tile(A0, M0, t);
         t += SNW;
         if (t >= nt) break;
-        if (t + SNW < nt) load(t + SNW, A0, M0);
+        load(min(t + SNW, nt - 1), A0, M0);
         tile(A1, M1, t);
         t += SNW;
       }
       __syncthreads();
       for (int i = tid; i < qcnt; i += 64 * SNW) {
-        a.cand_n[osl[i]] = min(cnt_l[i], a.cap);
-        a.cand_f[osl[i]] = flr_l[i];
+        const int o = __float_as_int(qr[i].w);
+        a.cand_n[o] = min(cnt_l[i], a.cap);
+        a.cand_f[o] = flr_l[i];
       }
     }
   }
