@@ -432,6 +432,16 @@ static int stream_prec() {
   const char *e = getenv("PYR_STREAM_PREC");
   return e && atoi(e) == 2 ? FILTER_F16X2 : FILTER_F16X1;
 }
+// T_q = the R-th largest sample value.  Any R is correct (rows below T_q are represented by floor
+// placeholders at T_q and the certificate decides); R trades emitted rows against queries with fewer
+// than K1 real candidates.  The samples are ~5 % of a query's rows, so about R / 0.05 rows reach T_q,
+// and a query falls short of K1 = 16 only when R of its 15 best rows were sampled: P ~ C(15, R) 0.05^R,
+// 2.5e-7 at R = 8 (R = 16: ~320 emitted rows per query at I1, R = 8: ~160).  PYR_STREAM_RANK overrides.
+static int stream_rank(int k1) {
+  const char *e = getenv("PYR_STREAM_RANK");
+  if (e) return std::max(1, atoi(e));
+  return std::max(1, k1 / 2);
+}
 // candidate region per (query, part) (PYR_STREAM_CAP) and rows per list chunk (PYR_STREAM_CHUNK)
 static int stream_cap() {
   const char *e = getenv("PYR_STREAM_CAP");
@@ -1885,7 +1895,7 @@ struct IvfFlatIndex : Index {
       PhaseTimer t(PH_SAMPLE, ws.st);
       launch_stream_prep(sa, metric, maxi, ws.st);
       launch_stream_scan(sa, metric, maxi, true, ws.st);
-      launch_stream_select(ws.ssamp.as<float>(), nq, probes * sv, k1, ws.sthr.as<float>(), ws.st);
+      launch_stream_select(ws.ssamp.as<float>(), nq, probes * sv, stream_rank(k1), ws.sthr.as<float>(), ws.st);
     }
     sa.work = ws.swork.as<int32_t>() + 1;
     {

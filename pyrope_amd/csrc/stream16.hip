@@ -52,54 +52,57 @@ constexpr int SAMPLE_TILES = 2 * SNW;
 __device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf(a, fmaxf(b, c)); }
 
 // ---- 1. query operands per (list, query) pair ----
+// A lane group of D / 8 lanes per query (8 dims a lane, the centroid's 8 dims held in registers for
+// the whole list), 64 / (D / 8) queries per wave at a time.
 template <int D, int MET>
 __global__ __launch_bounds__(256) void sprep_kernel(StreamArgs a) {
   const int item = blockIdx.x;
   if (item >= *a.n_items) return;
   const ScanItem it = a.items[item];
   if (it.part != 0) return;  // chunk-0 items cover every qlist position of their list once
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  constexpr int PL = (D + 63) / 64;
-  const float *cp = a.cents + (size_t)it.list * D;
-  for (int qi = w; qi < it.qcnt; qi += 4) {
-    const int pos = it.qbeg + qi;
+  constexpr int LQ = D / 8, QW = 64 / LQ;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, sub = lane % LQ, qsl = lane / LQ;
+  const float4 *cp = reinterpret_cast<const float4 *>(a.cents + (size_t)it.list * D + 8 * sub);
+  const float4 c0 = cp[0], c1 = cp[1];
+  const float cv[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+  for (int qi0 = QW * w; qi0 < it.qcnt; qi0 += 4 * QW) {
+    const int qi = qi0 + qsl;
+    const bool act = qi < it.qcnt;
+    const int pos = it.qbeg + (act ? qi : 0);
     const int q = a.qlist[pos] / a.nparts;
-    const float *qp = a.queries + (size_t)q * D;
-    float r[PL];
-    float cq = 0.0f, amax = 0.0f;
+    const float4 *qp = reinterpret_cast<const float4 *>(a.queries + (size_t)q * D + 8 * sub);
+    const float4 q0 = qp[0], q1 = qp[1];
+    const float qv[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+    float r[8], cq = 0.0f, amax = 0.0f;
 #pragma unroll
-    for (int u = 0; u < PL; ++u) {
-      const int d = lane + 64 * u;
-      r[u] = 0.0f;
-      if (d < D) {
-        const float qv = qp[d], cv = cp[d];
-        if (MET == L2) {
-          r[u] = qv - cv;
-          cq += r[u] * r[u];
-        } else {
-          r[u] = qv;
-          cq += qv * cv;
-        }
-        amax = fmaxf(amax, fabsf(r[u]));
+    for (int u = 0; u < 8; ++u) {
+      if (MET == L2) {
+        r[u] = qv[u] - cv[u];
+        cq += r[u] * r[u];
+      } else {
+        r[u] = qv[u];
+        cq += qv[u] * cv[u];
       }
+      amax = fmaxf(amax, fabsf(r[u]));
     }
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
+    for (int off = 1; off < LQ; off <<= 1) {
       cq += __shfl_xor(cq, off);
       amax = fmaxf(amax, __shfl_xor(amax, off));
     }
     const float sq = pow2_scale(amax);
+    if (act) {
+      h8v hv, lv;
 #pragma unroll
-    for (int u = 0; u < PL; ++u) {
-      const int d = lane + 64 * u;
-      if (d < D) {
+      for (int u = 0; u < 8; ++u) {
         const float v = r[u] * sq;  // exact (power of two)
-        const _Float16 h = (_Float16)v;
-        a.bq[(size_t)pos * D + d] = h;
-        if (a.bql) a.bql[(size_t)pos * D + d] = (_Float16)(v - (float)h);
+        hv[u] = (_Float16)v;
+        lv[u] = (_Float16)(v - (float)hv[u]);
       }
+      *reinterpret_cast<h8v *>(a.bq + (size_t)pos * D + 8 * sub) = hv;
+      if (a.bql) *reinterpret_cast<h8v *>(a.bql + (size_t)pos * D + 8 * sub) = lv;
+      if (sub == 0) a.qsc[pos] = make_float2((MET == L2 ? 2.0f : 1.0f) / (sq * a.sx), MET == L2 ? -cq : cq);
     }
-    if (lane == 0) a.qsc[pos] = make_float2((MET == L2 ? 2.0f : 1.0f) / (sq * a.sx), MET == L2 ? -cq : cq);
   }
 }
 
