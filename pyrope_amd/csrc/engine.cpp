@@ -68,6 +68,8 @@ void RowStore::reserve(int64_t slots, hipStream_t st) {
   HIPCHK(hipMemsetAsync(rsq.as<float>() + cap, 0, sizeof(float) * (nc - cap), st));
   if (cosine) HIPCHK(hipMemsetAsync(norms.as<float>() + cap, 0, sizeof(float) * (nc - cap), st));
   if (f16) {
+    rrm.grow_keep(sizeof(float) * nc * dim, sizeof(float) * cap * dim, st);
+    HIPCHK(hipMemsetAsync(rrm.as<float>() + cap * dim, 0, sizeof(float) * (nc - cap) * dim, st));
     if (center16) rsq16.grow_keep(sizeof(float) * nc, sizeof(float) * cap, st);
     h16.grow_keep(sizeof(uint16_t) * nc * dim, sizeof(uint16_t) * cap * dim, st);
     meta.grow_keep(sizeof(float) * nc, sizeof(float) * cap, st);
@@ -129,6 +131,7 @@ void RowStore::write(const float *x, const int64_t *slots, const int64_t *labs, 
   HIPCHK(hipMemcpyAsync(di, slots, sizeof(int64_t) * cnt, hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(di + cnt, labs, sizeof(int64_t) * cnt, hipMemcpyHostToDevice, st));
   launch_scatter_blocked(stage_x.as<float>(), di, cnt, dim, rows.as<float>(), st);
+  if (f16) launch_scatter_rowmajor(stage_x.as<float>(), di, cnt, dim, rrm.as<float>(), st);
   launch_scatter_i64(labels.as<int64_t>(), di, di + cnt, cnt, st);
   launch_scatter_u8(live.as<uint8_t>(), di, 1, cnt, st);
   if (cosine) launch_norms_slots(rows.as<float>(), di, cnt, dim, norms.as<float>(), st);
@@ -500,6 +503,7 @@ static int64_t filter_finish(Workspace &ws, int64_t nq, int nparts, int k1, int 
   HIPCHK(hipMemsetAsync(ws.fail_cnt.p, 0, sizeof(int32_t), ws.st));
   RefineArgs r{};
   r.rows = rs.rows.as<float>();
+  r.rows_rm = rs.f16 ? rs.rrm.as<float>() : nullptr;
   r.row_labels = rs.labels.as<int64_t>();
   r.queries = d_q;
   r.ms = ws.ms.as<float>();
@@ -1098,6 +1102,7 @@ struct DictBuffer {
     HIPCHK(hipStreamSynchronize(wst));
     if (st.cap > 65536) {  // a bulk-loaded buffer was compacted into lists: give the HBM back
       st.rows.release();
+      st.rrm.release();
       st.rsq.release();
       st.norms.release();
       st.live.release();
@@ -1502,6 +1507,7 @@ struct IvfFlatIndex : Index {
     dsr.ensure(sizeof(int64_t) * tot);
     HIPCHK(hipMemcpyAsync(dsr.p, srcrow.data(), sizeof(int64_t) * tot, hipMemcpyHostToDevice, wst));
     launch_to_blocked(X, dsr.as<int64_t>(), tot, dim, nl.rows.as<float>(), 0, wst);
+    if (nl.f16) launch_to_rowmajor(X, dsr.as<int64_t>(), tot, dim, nl.rrm.as<float>(), wst);
     std::vector<uint8_t> lv(tot);
     for (int64_t p = 0; p < tot; p++) lv[p] = srcrow[p] >= 0;
     HIPCHK(hipMemcpyAsync(nl.live.p, lv.data(), tot, hipMemcpyHostToDevice, wst));
@@ -1557,6 +1563,8 @@ struct IvfFlatIndex : Index {
     std::swap(lists.amaxd.n, nl.amaxd.n);
     std::swap(lists.rsq16.p, nl.rsq16.p);
     std::swap(lists.rsq16.n, nl.rsq16.n);
+    std::swap(lists.rrm.p, nl.rrm.p);
+    std::swap(lists.rrm.n, nl.rrm.n);
     lists.f16 = nl.f16;
     lists.met16 = nl.met16;
     lists.sx = nl.sx;
@@ -1929,6 +1937,7 @@ struct IvfFlatIndex : Index {
     HIPCHK(hipMemsetAsync(ws.fail_cnt2.p, 0, sizeof(int32_t), ws.st));
     RefineArgs r{};
     r.rows = lists.rows.as<float>();
+    r.rows_rm = lists.f16 ? lists.rrm.as<float>() : nullptr;
     r.row_labels = lists.labels.as<int64_t>();
     r.queries = d_q;
     r.ms = ws.ms.as<float>();

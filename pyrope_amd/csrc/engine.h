@@ -79,6 +79,9 @@ struct RowStore {
   bool resid = false;
   bool center16 = false;
   DevMem rsq16, center, rmax_r;
+  // f16 stores: a row-major fp32 copy of the rows for the exact refine (a candidate's 512 B read
+  // contiguously; the blocked layout spreads one row over D 32-B sectors)
+  DevMem rrm;
   const float *meta_norms() const { return resid ? rsq16.as<float>() : rsq.as<float>(); }
   std::vector<int64_t> hlabels;
   std::vector<uint8_t> hlive;

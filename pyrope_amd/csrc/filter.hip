@@ -458,16 +458,23 @@ __device__ __forceinline__ float hsum8_lanes(float v) {
 // exact_score with its 8 accumulator lanes spread over an 8-lane group: lane l (0..7) runs the
 // chains of accumulator l (a1..a4[l] for V = 4, acc[l] for the 8-wide loop), in the same order, and
 // the group reduces them as hsum8 does.  Every lane of the group returns the score.
-template <int V, int MET>
-__device__ float exact_score_l8(const float *q, const float *rows, int64_t r, int D, int l) {
+// DT > 0: the dimension as a compile-time constant (every loop unrolls, so all of a row's loads are in
+// flight at once; the additions keep their order)
+template <int V, int MET, int DT = 0, bool RM = false>
+__device__ float exact_score_l8(const float *q, const float *rows, int64_t r, int Dr, int l) {
+  const int D = DT > 0 ? DT : Dr;
+  // RM: rows is row-major (a row's dims contiguous: the 8 lanes of a group read 32 B together instead
+  // of 8 scattered sectors of the blocked store)
+  auto X = [&](int d) { return RM ? rows[(size_t)r * D + d] : rows[blk_off(r, d, D)]; };
   float sum = 0.0f;
   int i = 0;
   if (V == 4 && D >= 32) {
     float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll(DT > 0 ? DT / 32 : 1)
     for (; i <= D - 32; i += 32)
 #pragma unroll
       for (int v = 0; v < 4; v++) {
-        const float x = rows[blk_off(r, i + 8 * v + l, D)];
+        const float x = X(i + 8 * v + l);
         float t;
         if (MET == L2) {
           const float d = q[i + 8 * v + l] - x;
@@ -482,9 +489,9 @@ __device__ float exact_score_l8(const float *q, const float *rows, int64_t r, in
   }
   if (i <= D - 8) {
     float acc = 0.0f;
-#pragma unroll 4
+#pragma unroll(DT > 0 ? DT / 8 : 4)
     for (; i <= D - 8; i += 8) {
-      const float x = rows[blk_off(r, i + l, D)];
+      const float x = X(i + l);
       if (MET == L2) {
         const float d = q[i + l] - x;
         acc = acc + d * d;
@@ -510,7 +517,7 @@ __device__ float exact_score_l8(const float *q, const float *rows, int64_t r, in
 // in all, against c_err = 4 D + 64 (engine).  The bf16x3 filter adds c_bf u |q| X
 // (kernels.h filter_bf16x3_cerr) and an absolute term for flushed subnormal halves.  If fewer than K1 candidates exist no row
 // was excluded and the result is exact as it stands.
-template <int V, int MET>
+template <int V, int MET, int DT>
 __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
   const int lane = threadIdx.x & 63;
   int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -519,7 +526,7 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
     if (q >= *a.nsel) return;
     q = a.qsel[q];
   }
-  const int D = a.dim, k1 = a.k1, k = a.k;
+  const int D = DT > 0 ? DT : a.dim, k1 = a.k1, k = a.k;
   const int ld = a.ld > 0 ? a.ld : k1;
   const float *qp = a.queries + (size_t)q * D;
   float part = 0.0f;  // |q|^2, any order (covered by E)
@@ -544,7 +551,9 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
   for (int p = 0; 8 * p < k1; ++p) {
     const int c = 8 * p + (lane >> 3);
     const int32_t kc = __shfl((int)key, c);  // (k1 <= 64: every candidate's key sits on lane c)
-    const float sc = exact_score_l8<V, MET>(qp, a.rows, kc >= 0 ? (int64_t)kc : 0, D, lane & 7);
+    const int64_t rk = kc >= 0 ? (int64_t)kc : 0;
+    const float sc = a.rows_rm ? exact_score_l8<V, MET, DT, true>(qp, a.rows_rm, rk, D, lane & 7)
+                               : exact_score_l8<V, MET, DT, false>(qp, a.rows, rk, D, lane & 7);
     const float t = __shfl(sc, 8 * (lane & 7));
     if ((lane >> 3) == p && key != KEY_NONE) s = t;
   }
@@ -606,6 +615,7 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
         float d2 = 0.0f, c2 = 0.0f, qc = 0.0f;
         if (p < np) {
           const float *c = a.cents + (size_t)lp * D;
+#pragma unroll(DT > 0 ? DT / 8 : 4)
           for (int d = j; d < D; d += 8) {
             const float t = qp[d] - c[d];
             d2 += t * t;
@@ -818,12 +828,22 @@ void launch_filter(const FilterArgs &a, int metric, int max_items, hipStream_t s
 void launch_refine(const RefineArgs &a, int metric, int V, hipStream_t st) {
   if (a.nq <= 0) return;
   const dim3 g(nblk(a.nq, 4)), b(256);
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, g, b, 0, st, a); };
+  // the common dimensions as compile-time constants (fully unrolled row loads), others at run time
+  auto by_dim = [&](auto k0, auto k32, auto k64, auto k128) {
+    switch (a.dim) {
+      case 32: go(k32); return;
+      case 64: go(k64); return;
+      case 128: go(k128); return;
+      default: go(k0); return;
+    }
+  };
   if (V == 4) {
-    if (metric == L2) hipLaunchKernelGGL((refine_kernel<4, L2>), g, b, 0, st, a);
-    else hipLaunchKernelGGL((refine_kernel<4, IP>), g, b, 0, st, a);
+    if (metric == L2) by_dim(refine_kernel<4, L2, 0>, refine_kernel<4, L2, 32>, refine_kernel<4, L2, 64>, refine_kernel<4, L2, 128>);
+    else by_dim(refine_kernel<4, IP, 0>, refine_kernel<4, IP, 32>, refine_kernel<4, IP, 64>, refine_kernel<4, IP, 128>);
   } else {
-    if (metric == L2) hipLaunchKernelGGL((refine_kernel<1, L2>), g, b, 0, st, a);
-    else hipLaunchKernelGGL((refine_kernel<1, IP>), g, b, 0, st, a);
+    if (metric == L2) by_dim(refine_kernel<1, L2, 0>, refine_kernel<1, L2, 32>, refine_kernel<1, L2, 64>, refine_kernel<1, L2, 128>);
+    else by_dim(refine_kernel<1, IP, 0>, refine_kernel<1, IP, 32>, refine_kernel<1, IP, 64>, refine_kernel<1, IP, 128>);
   }
 }
 

@@ -369,6 +369,7 @@ void launch_cand_merge(const CandMergeArgs &m, hipStream_t st);
 
 struct RefineArgs {
   const float *rows;        // blocked store the keys index
+  const float *rows_rm;     // its row-major copy (RowStore::rrm: one contiguous row per key), or null
   const int64_t *row_labels;
   const float *queries;     // row-major nq x D
   const float *ms;          // merged approximate scores [nq][ld] (desc)
@@ -438,6 +439,11 @@ void launch_sqnorms(const float *rows, const int64_t *slots, int64_t n, int32_t 
 void launch_to_blocked(const float *src, const int64_t *src_idx, int64_t n, int32_t dim, float *dst, int64_t dst_row0,
                        hipStream_t st);
 // scattered writes: row i of src (row-major) -> blocked slot dst_slots[i]
+// row-major copies (RowStore::rrm): dst row i = src row src_idx[i] (zero when < 0; src_idx null = i);
+// src rows scattered to dst_slots
+void launch_to_rowmajor(const float *src, const int64_t *src_idx, int64_t n, int32_t dim, float *dst, hipStream_t st);
+void launch_scatter_rowmajor(const float *src, const int64_t *dst_slots, int64_t n, int32_t dim, float *dst,
+                             hipStream_t st);
 void launch_scatter_blocked(const float *src, const int64_t *dst_slots, int64_t n, int32_t dim, float *dst,
                             hipStream_t st);
 // gather blocked rows (src_slot[i]) into row-major out

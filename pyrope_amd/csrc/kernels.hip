@@ -1406,6 +1406,25 @@ __global__ void scatter_blocked_kernel(const float *src, const int64_t *slots, i
     dst[blk_off(slots[i], d, D)] = src[e];
   }
 }
+// row-major copies (RowStore::rrm, the refine's rows): dst row i = src row sidx[i] (0 when < 0), or the
+// rows scattered to their slots
+__global__ void to_rowmajor_kernel(const float *src, const int64_t *sidx, int64_t n, int D, float *dst) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * D;
+       e += (int64_t)gridDim.x * blockDim.x) {  // grid-stride: grids stay below 2^32 work-items
+    const int64_t i = e / D;
+    const int d = (int)(e % D);
+    const int64_t s = sidx ? sidx[i] : i;
+    dst[e] = s >= 0 ? src[(size_t)s * D + d] : 0.0f;
+  }
+}
+__global__ void scatter_rowmajor_kernel(const float *src, const int64_t *slots, int64_t n, int D, float *dst) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * D;
+       e += (int64_t)gridDim.x * blockDim.x) {  // grid-stride: grids stay below 2^32 work-items
+    const int64_t i = e / D;
+    const int d = (int)(e % D);
+    dst[(size_t)slots[i] * D + d] = src[e];
+  }
+}
 __global__ void gather_blocked_kernel(const float *src, const int64_t *slots, int64_t n, int D, float *out) {
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * D;
        e += (int64_t)gridDim.x * blockDim.x) {  // grid-stride: grids stay below 2^32 work-items
@@ -1828,6 +1847,15 @@ void launch_scatter_blocked(const float *src, const int64_t *dst_slots, int64_t 
                             hipStream_t st) {
   if (n <= 0) return;
   hipLaunchKernelGGL(scatter_blocked_kernel, dim3(gblk(n * dim)), dim3(256), 0, st, src, dst_slots, n, dim, dst);
+}
+void launch_to_rowmajor(const float *src, const int64_t *src_idx, int64_t n, int32_t dim, float *dst, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(to_rowmajor_kernel, dim3(gblk(n * dim)), dim3(256), 0, st, src, src_idx, n, dim, dst);
+}
+void launch_scatter_rowmajor(const float *src, const int64_t *dst_slots, int64_t n, int32_t dim, float *dst,
+                             hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(scatter_rowmajor_kernel, dim3(gblk(n * dim)), dim3(256), 0, st, src, dst_slots, n, dim, dst);
 }
 void launch_gather_blocked(const float *src, const int64_t *src_slots, int64_t n, int32_t dim, float *out,
                            hipStream_t st) {

@@ -132,6 +132,7 @@ __global__ __launch_bounds__(64 * SNW, 1) void stream16_kernel(StreamArgs a) {
     const ScanItem it = a.items[item];
     if (SAMPLE && it.part != 0) continue;
     const int qcnt = it.qcnt, ng = (qcnt + 15) >> 4;
+    const int ng2 = SAMPLE ? ng : (ng + 1) & ~1;  // MAIN runs groups in pairs (an odd count gets an empty one)
 
     // ---- prologue: query operands (LDS-DMA; a lane of piece (j, s) carries dims 32s + 8g .. +7 of
     // query 16j + c, the 16x16x32 B layout) and per-query scalars ----
@@ -144,8 +145,10 @@ __global__ __launch_bounds__(64 * SNW, 1) void stream16_kernel(StreamArgs a) {
         const _Float16 *src = (term ? a.bql : a.bq) + (size_t)(it.qbeg + qi) * D + 32 * s + 8 * g;
         glds<16>(src, bl_base + (uint32_t)((term * PIECES + pp) * 1024));
       }
-      for (int i = tid; i < ng * 16; i += 64 * SNW) {
-        float2 v = make_float2(0.0f, INFINITY);  // an unused query slot takes no rows
+      // records of every slot of the (even-padded) groups; an unused slot's threshold is NaN, so no
+      // row is ever emitted for it (not even a +inf-meta row, whose y would reach a +inf threshold)
+      for (int i = tid; i < ng2 * 16; i += 64 * SNW) {
+        float2 v = make_float2(0.0f, __builtin_nanf(""));
         float cqv = 0.0f;
         int o = -1;
         if (i < qcnt) {
@@ -296,46 +299,34 @@ __global__ __launch_bounds__(64 * SNW, 1) void stream16_kernel(StreamArgs a) {
         }
         if (__builtin_amdgcn_ballot_w64(mx >= rq.y)) emit(y, rq, 16 * j + c, rt);
       };
-      // one tile against every group, software-pipelined over pairs of groups: group j + 1's record and
-      // operands are read while group j's MFMAs run (the record first, so waiting for it never waits for
-      // operand reads issued after it), and group j - 1's epilogue runs behind group j's MFMAs
+      // one tile against every group, software-pipelined over pairs of groups with two fixed register
+      // sets: group j + 1's record and operands are read while group j's MFMAs run (the record first,
+      // so waiting for it never waits for operand reads issued after it), group j - 1's epilogue runs
+      // behind group j's MFMAs.  The group count is even (a padded group has NaN thresholds) and the
+      // reads ahead are unconditional (clamped): no exit or conditional read inside the pipeline, which
+      // the compiler otherwise rotates into a one-group loop that waits for its reads at the back edge.
       auto tile = [&](const h8v (&A)[KS][2], const f4v (&M)[2], int t) {
         float mr[8];
         row_terms(M, t, mr);
         const int rt = r0 + 32 * t;
         h8v b0[KS], b1[KS], o0[KS], o1[KS];
         f4v a0[2], a1[2];
-        // (the reads ahead are unconditional, clamped to the last group: a conditional read would make
-        // the compiler's lgkmcnt accounting wait for every outstanding LDS read at the join)
-        float4 r0q = qr[c], r1q = r0q, r0n = r0q, r1p = r0q;
+        float4 q0 = qr[c], q1 = q0, qp = q0;
         read_b(0, b0, o0);
-        for (int j = 0;;) {
-          {
-            const int jn = min(j + 1, ng - 1);
-            r1q = qr[16 * jn + c];
-            read_b(jn, b1, o1);
-          }
+        for (int j = 0; j < ng2; j += 2) {
+          q1 = qr[16 * (j + 1) + c];
+          read_b(j + 1, b1, o1);
           mma(A, b0, o0, a0);
-          if (j > 0) epi(a1, mr, j - 1, r1p, rt);
-          if (j + 1 >= ng) {
-            epi(a0, mr, j, r0q, rt);
-            break;
-          }
-          {
-            const int jn = min(j + 2, ng - 1);
-            r0n = qr[16 * jn + c];
-            read_b(jn, b0, o0);
-          }
+          if (j > 0) epi(a1, mr, j - 1, qp, rt);
+          const float4 qj = q0;
+          const int jn = min(j + 2, ng2 - 1);
+          q0 = qr[16 * jn + c];
+          read_b(jn, b0, o0);
           mma(A, b1, o1, a1);
-          epi(a0, mr, j, r0q, rt);
-          r0q = r0n;
-          r1p = r1q;
-          j += 2;
-          if (j >= ng) {
-            epi(a1, mr, j - 1, r1p, rt);
-            break;
-          }
+          epi(a0, mr, j, qj, rt);
+          qp = q1;
         }
+        epi(a1, mr, ng2 - 1, qp, rt);
       };
       // double-buffered tiles; the prefetch of tile t + 8 is unconditional (the last tile is re-read when
       // there is none): a conditional load makes the compiler's vmcnt accounting wait for the
