@@ -463,6 +463,7 @@ __device__ __forceinline__ float hsum8_lanes(float v) {
 template <int V, int MET, int DT = 0, bool RM = false>
 __device__ float exact_score_l8(const float *q, const float *rows, int64_t r, int Dr, int l) {
   const int D = DT > 0 ? DT : Dr;
+  constexpr int UNR32 = DT > 0 ? DT / 32 : 1, UNR8 = DT > 0 ? DT / 8 : 4;
   // RM: rows is row-major (a row's dims contiguous: the 8 lanes of a group read 32 B together instead
   // of 8 scattered sectors of the blocked store)
   auto X = [&](int d) { return RM ? rows[(size_t)r * D + d] : rows[blk_off(r, d, D)]; };
@@ -470,7 +471,7 @@ __device__ float exact_score_l8(const float *q, const float *rows, int64_t r, in
   int i = 0;
   if (V == 4 && D >= 32) {
     float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll(DT > 0 ? DT / 32 : 1)
+#pragma unroll UNR32
     for (; i <= D - 32; i += 32)
 #pragma unroll
       for (int v = 0; v < 4; v++) {
@@ -489,7 +490,7 @@ __device__ float exact_score_l8(const float *q, const float *rows, int64_t r, in
   }
   if (i <= D - 8) {
     float acc = 0.0f;
-#pragma unroll(DT > 0 ? DT / 8 : 4)
+#pragma unroll UNR8
     for (; i <= D - 8; i += 8) {
       const float x = X(i + l);
       if (MET == L2) {
@@ -527,6 +528,7 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
     q = a.qsel[q];
   }
   const int D = DT > 0 ? DT : a.dim, k1 = a.k1, k = a.k;
+  constexpr int UNR8 = DT > 0 ? DT / 8 : 4;
   const int ld = a.ld > 0 ? a.ld : k1;
   const float *qp = a.queries + (size_t)q * D;
   float part = 0.0f;  // |q|^2, any order (covered by E)
@@ -615,7 +617,7 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
         float d2 = 0.0f, c2 = 0.0f, qc = 0.0f;
         if (p < np) {
           const float *c = a.cents + (size_t)lp * D;
-#pragma unroll(DT > 0 ? DT / 8 : 4)
+#pragma unroll UNR8
           for (int d = j; d < D; d += 8) {
             const float t = qp[d] - c[d];
             d2 += t * t;
