@@ -17,11 +17,14 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 #include "kernels.h"
 
 namespace pyr {
 namespace {
+
+#include "wselect.h"
 
 constexpr int CT = 32;  // queries / centroids per tile
 
@@ -171,16 +174,12 @@ __device__ __forceinline__ void key_insert(uint64_t (&l)[P], uint64_t v) {
   l[0] = b[0] ? v : l[0];
 }
 
+// the wave's selection over one score row (every lane holds the P best keys of its 64th share)
 template <int P>
-__global__ __launch_bounds__(256) void coarse_select_reg_kernel(const float *scores, int64_t nq, int nc, int nprobe,
-                                                                int32_t *probes) {
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t q = (int64_t)blockIdx.x * 4 + w;
-  if (q >= nq) return;  // no block barrier below
+__device__ __forceinline__ void select_row_reg(const float *row, int nc, int nprobe, int32_t *out, int lane) {
   uint64_t l[P];
 #pragma unroll
   for (int j = 0; j < P; ++j) l[j] = 0;  // below every real key
-  const float *row = scores + q * nc;
   constexpr int U = 8;  // independent loads in flight per lane before the (branchy) insertions
   for (int c0 = lane; c0 < nc; c0 += 64 * U) {
     float v[U];
@@ -204,10 +203,209 @@ __global__ __launch_bounds__(256) void coarse_select_reg_kernel(const float *sco
 #pragma unroll
       for (int j = 0; j < P - 1; ++j) l[j] = l[j + 1];
       l[P - 1] = 0;
-      if (best != 0) probes[q * nprobe + p] = 0x7FFFFFFF - (int)(uint32_t)best;
+      if (best != 0) out[p] = 0x7FFFFFFF - (int)(uint32_t)best;
     }
-    if (best == 0 && lane == 0) probes[q * nprobe + p] = -1;  // fewer centroids than nprobe (as the LDS kernel)
+    if (best == 0 && lane == 0) out[p] = -1;  // fewer centroids than nprobe (as the LDS kernel)
   }
+}
+
+template <int P>
+__global__ __launch_bounds__(256) void coarse_select_reg_kernel(const float *scores, int64_t nq, int nc, int nprobe,
+                                                                int32_t *probes) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.x * 4 + w;
+  if (q >= nq) return;  // no block barrier below
+  select_row_reg<P>(scores + q * nc, nc, nprobe, probes + q * nprobe, lane);
+}
+
+// ---- the coarse ranking on the matrix cores (L2 / IP, D % 16 == 0) ----
+// 1. coarse_approx_kernel: fp32 MFMA dot products (v_mfma_f32_16x16x4_f32), one wave per 32 queries x 32
+//    centroids; approx = 2 q.c - |c|^2 (L2: the score + |q|^2) or q.c (IP).  The k order inside a
+//    16-dim block is permuted the same way for both operands (lane group h, step j -> dim 16s + 4h + j),
+//    so every lane feeds its MFMAs from float4 loads.
+// 2. coarse_pick_kernel: the nprobe-th largest approximate score aP, the exact ComputeScore of every
+//    centroid within 2E of it (E bounds |approx - (score + |q|^2)|) and the first nprobe of those.
+// 3. coarse_select_list_kernel: the dense exact ranking of the queries the pick could not settle.
+template <int MET>
+__global__ __launch_bounds__(64) void coarse_approx_kernel(const float *q, const float *c, const float *c2, int64_t nq,
+                                                           int nc, int D, float *out) {
+  const int64_t q0 = (int64_t)blockIdx.y * 32;
+  const int c0 = blockIdx.x * 32;
+  const int l = threadIdx.x, r = l & 15, h = l >> 4;
+  const float4 *qa[2], *cb[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    qa[i] = reinterpret_cast<const float4 *>(q + (size_t)min(q0 + 16 * i + r, nq - 1) * D) + h;
+    cb[i] = reinterpret_cast<const float4 *>(c + (size_t)min(c0 + 16 * i + r, nc - 1) * D) + h;
+  }
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  f4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+  for (int s = 0; s < D / 16; ++s) {
+    const float4 a0 = qa[0][4 * s], a1 = qa[1][4 * s], b0 = cb[0][4 * s], b1 = cb[1][4 * s];
+    const float av[2][4] = {{a0.x, a0.y, a0.z, a0.w}, {a1.x, a1.y, a1.z, a1.w}};
+    const float bv[2][4] = {{b0.x, b0.y, b0.z, b0.w}, {b1.x, b1.y, b1.z, b1.w}};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i][j], bv[t][j], acc[i][t], 0, 0, 0);
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int ci = c0 + 16 * t + r;
+    if (ci >= nc) continue;
+    const float cc = MET == L2 ? c2[ci] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int64_t qi = q0 + 16 * i + 4 * h + g;
+        if (qi < nq) out[qi * nc + ci] = MET == L2 ? 2.0f * acc[i][t][g] - cc : acc[i][t][g];
+      }
+  }
+}
+
+// ComputeScore (safe VectorMath form, as coarse_scores_kernel) spread over an 8-lane group: lane j runs
+// accumulator j over dims j, j + 8, ...; the group sums as hsum8 does; every lane returns the score
+template <int MET>
+__device__ __forceinline__ float exact_cs_l8(const float *qp, const float *cp, int D, int j) {
+  float acc = 0.0f;
+  for (int d = j; d < (D & ~7); d += 8) {
+    if (MET == L2) {
+      const float t = qp[d] - cp[d];
+      acc = acc + t * t;
+    } else {
+      acc = acc + qp[d] * cp[d];
+    }
+  }
+  acc = acc + __shfl_xor(acc, 1);
+  acc = acc + __shfl_xor(acc, 2);
+  float sum = (D & ~7) > 0 ? 0.0f + (acc + __shfl_xor(acc, 4)) : 0.0f;
+  for (int d = D & ~7; d < D; ++d) {  // the scalar tail (D % 16 == 0 here: none)
+    if (MET == L2) {
+      const float t = qp[d] - cp[d];
+      sum = sum + t * t;
+    } else {
+      sum = sum + qp[d] * cp[d];
+    }
+  }
+  return MET == L2 ? -sum : sum;
+}
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t sort64_desc(uint64_t v, int lane) {
+#pragma unroll
+  for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+    for (int j = k >> 1; j >= 1; j >>= 1) {
+      const uint64_t o = shfl_xor64(v, j);
+      const bool desc = (lane & k) == 0, lower = (lane & j) == 0;
+      v = (lower == desc) ? (v > o ? v : o) : (v < o ? v : o);
+    }
+  return v;
+}
+
+// One wave per query: aP = the nprobe-th largest approximate score (wselect.h radix select over score
+// keys), the candidates = every centroid whose approximate
+// score reaches aP - 2E (at most 64, in index order), their exact ComputeScore and the first nprobe of
+// them by (score desc, index asc).  Every centroid left out scores exactly below the nprobe centroids
+// whose approximate score reached aP.  More than 64 candidates, or a non-finite query: the exact
+// scores of every centroid go to the row and the query to the fail list (coarse_select_list_kernel).
+template <int MET>
+__global__ __launch_bounds__(256) void coarse_pick_kernel(const float *q, const float *c, float *scores, int64_t nq,
+                                                          int nc, int D, int P, double cnmax, double c_err,
+                                                          int32_t *probes, int32_t *fail, int32_t *nfail) {
+  __shared__ int hist[4][256];
+  __shared__ int cl[4][64];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t qi = (int64_t)blockIdx.x * 4 + w;
+  if (qi >= nq) return;  // no block barrier below
+  const float *qp = q + (size_t)qi * D;
+  float *row = scores + qi * nc;
+  float part = 0.0f;
+  for (int d = lane; d < D; d += 64) part += qp[d] * qp[d];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) part += __shfl_xor(part, o);
+  const double qn = sqrt((double)part) * (1.0 + 1e-5);
+  bool ok = isfinite(qn);
+  int n = 0;
+  if (ok) {
+    // 1. the P-th largest score key
+    float cv[16];
+    const uint32_t prefix = wave_kth_key_lm<16>(row, nc, P, hist[w], cl[w], lane, cv);
+    const float aP = key_score(prefix);
+    const double u = 5.9604644775390625e-8;  // 2^-24
+    const double E = MET == L2 ? c_err * u * (qn + cnmax) * (qn + cnmax) : c_err * u * qn * cnmax;
+    const double tb = (double)aP - 2.0 * E;
+    float th = (float)tb;
+    if ((double)th > tb) th = nextafterf(th, -INFINITY);  // at or below aP - 2E
+    ok = ok && isfinite(aP) && isfinite(th);
+    // 2. the candidates, in index order
+    if (ok) {
+      auto take = [&](int cc, float val) {
+        const bool pr = cc < nc && val >= th;
+        const uint64_t m = __builtin_amdgcn_ballot_w64(pr);
+        const int pos = n + (int)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+        if (pr && pos < 64) cl[w][pos] = cc;
+        n += (int)__builtin_popcountll(m);
+      };
+      if (nc <= 64 * 16) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (64 * u < nc) take(64 * u + lane, cv[u]);
+      } else {
+        for (int c0 = 0; c0 < nc; c0 += 64) take(c0 + lane, c0 + lane < nc ? row[c0 + lane] : 0.0f);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      ok = n <= 64;
+    }
+  }
+  if (ok) {
+    const int cid = lane < n ? cl[w][lane] : -1;
+    float sc = -INFINITY;
+    for (int p = 0; 8 * p < n; ++p) {
+      const int cc = 8 * p + (lane >> 3);
+      const int id = __shfl(cid, cc);
+      const float v = exact_cs_l8<MET>(qp, c + (size_t)max(id, 0) * D, D, lane & 7);
+      const float t = __shfl(v, 8 * (lane & 7));
+      if ((lane >> 3) == p) sc = t;  // lane 8p + g took candidate 8p + g's score from group g
+    }
+    uint64_t key = cid >= 0 ? rank_key(sc, cid) : 0ull;
+    key = sort64_desc(key, lane);
+    if (lane < P) probes[qi * P + lane] = key != 0ull ? 0x7FFFFFFF - (int)(uint32_t)key : -1;
+    return;
+  }
+  // fallback: the exact scores of every centroid into the row, selection by coarse_select_list_kernel
+  for (int c0 = 0; c0 < nc; c0 += 8) {
+    const int id = c0 + (lane >> 3);
+    const float v = exact_cs_l8<MET>(qp, c + (size_t)min(id, nc - 1) * D, D, lane & 7);
+    if ((lane & 7) == 0 && id < nc) row[id] = v;
+  }
+  if (lane == 0) fail[atomicAdd(nfail, 1)] = (int32_t)qi;
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void coarse_select_list_kernel(const float *scores, const int32_t *fail,
+                                                                 const int32_t *nfail, int nc, int nprobe,
+                                                                 int32_t *probes) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + w;
+  if (i >= *nfail) return;
+  const int64_t qi = fail[i];
+  select_row_reg<W>(scores + qi * nc, nc, nprobe, probes + qi * nprobe, lane);
 }
 
 }  // namespace
@@ -252,6 +450,42 @@ void launch_coarse_dense(const float *q, const float *cents_rm, const float *qn,
     hipLaunchKernelGGL(coarse_select_kernel, dim3((unsigned)((nq + wpb - 1) / wpb)), dim3(64 * wpb),
                        (size_t)wpb * nlist * sizeof(uint64_t), st, scores, nq, nlist, nprobe, wpb, probes);
   }
+}
+
+// the register-list capacity for selecting n of nlist centroids (launch_coarse_dense's choice)
+template <class F>
+static void with_list_cap(int nlist, int n, F &&f) {
+  const int per_lane = (nlist + 63) / 64;
+  if (per_lane <= 8) f(std::integral_constant<int, 8>{});
+  else if (n <= 16 || per_lane <= 16) f(std::integral_constant<int, 16>{});
+  else if (n <= 32 || per_lane <= 32) f(std::integral_constant<int, 32>{});
+  else f(std::integral_constant<int, 64>{});
+}
+
+bool coarse_mfma_supported(int nlist, int dim, int metric, int nprobe) {
+  return (metric == L2 || metric == IP) && dim > 0 && dim % 16 == 0 && nlist >= 1 && nprobe >= 1 && nprobe <= 64;
+}
+
+void launch_coarse_mfma(const float *q, const float *cents_rm, const float *c2, int64_t nq, int32_t nlist,
+                        int32_t dim, int32_t metric, int32_t nprobe, double cnmax, double c_err, float *scores,
+                        int32_t *fail, int32_t *nfail, int32_t *probes, hipStream_t st) {
+  if (nq <= 0 || nlist <= 0 || nprobe <= 0) return;
+  const int P = std::min(nprobe, nlist);
+  const dim3 ga((unsigned)((nlist + 31) / 32), (unsigned)((nq + 31) / 32));
+  if (metric == L2) hipLaunchKernelGGL(coarse_approx_kernel<L2>, ga, dim3(64), 0, st, q, cents_rm, c2, nq, nlist, dim, scores);
+  else hipLaunchKernelGGL(coarse_approx_kernel<IP>, ga, dim3(64), 0, st, q, cents_rm, c2, nq, nlist, dim, scores);
+  const dim3 g4((unsigned)((nq + 3) / 4));
+  (void)hipMemsetAsync(nfail, 0, sizeof(int32_t), st);
+  if (metric == L2)
+    hipLaunchKernelGGL(coarse_pick_kernel<L2>, g4, dim3(256), 0, st, q, cents_rm, scores, nq, nlist, dim, P, cnmax,
+                       c_err, probes, fail, nfail);
+  else
+    hipLaunchKernelGGL(coarse_pick_kernel<IP>, g4, dim3(256), 0, st, q, cents_rm, scores, nq, nlist, dim, P, cnmax,
+                       c_err, probes, fail, nfail);
+  with_list_cap(nlist, P, [&](auto W) {
+    hipLaunchKernelGGL(coarse_select_list_kernel<decltype(W)::value>, g4, dim3(256), 0, st, scores, fail, nfail, nlist,
+                       P, probes);
+  });
 }
 
 }  // namespace pyr

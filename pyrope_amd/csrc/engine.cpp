@@ -1116,6 +1116,14 @@ struct DictBuffer {
 };
 
 // coarse quantizer shared by IVF_FLAT and IVF_PQ: centroids blocked + row-major
+// error-bound constant of the matrix-core coarse ranking (coarse.hip coarse_pick_kernel): 4 D + 64
+// covers (2.2 D + 8) u (|q| + |c|)^2; PYR_COARSE_CERR overrides it for tests (huge: every query takes
+// the dense exact fallback)
+static double coarse_cerr(int dim) {
+  if (const char *e = getenv("PYR_COARSE_CERR")) return atof(e);
+  return 4.0 * dim + 64.0;
+}
+
 struct Coarse {
   int nlist = 0;
   RowStore cs;
@@ -1126,6 +1134,11 @@ struct Coarse {
   // (ComputeScore) of K1 candidates and the certificate, failures re-run exactly; ids and order
   // equal the dense exact ranking
   std::unique_ptr<FlatIndex> flat;
+  // the matrix-core ranking (coarse.hip launch_coarse_mfma): |c|^2 per centroid, max |c|, and whether
+  // every centroid value is finite (otherwise the dense exact ranking runs)
+  DevMem c2;
+  double cnmax = 0.0;
+  bool cfinite = false;
 
   void set(const float *d_cents_rm, int k, int dim, int met, hipStream_t st) {
     nlist = k;
@@ -1143,6 +1156,25 @@ struct Coarse {
     HIPCHK(hipMemcpyAsync(host.data(), d_cents_rm, sizeof(float) * k * dim, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     cs.n = k;
+    {
+      std::vector<float> n2((size_t)k);
+      double mx = 0.0;
+      cfinite = true;
+      for (int i = 0; i < k; ++i) {
+        double a = 0.0;
+        for (int d = 0; d < dim; ++d) {
+          const float v = host[(size_t)i * dim + d];
+          cfinite = cfinite && std::isfinite(v);
+          a += (double)v * v;
+        }
+        n2[i] = (float)a;
+        mx = std::max(mx, std::sqrt(a));
+      }
+      cnmax = mx * (1.0 + 1e-6);
+      c2.ensure(sizeof(float) * std::max(k, 1));
+      HIPCHK(hipMemcpyAsync(c2.p, n2.data(), sizeof(float) * k, hipMemcpyHostToDevice, st));
+      HIPCHK(hipStreamSynchronize(st));
+    }
     flat.reset();
     if (filter_on() && met != COS && store16(dim, met)) {
       pyr_index_desc d{};
@@ -1188,6 +1220,24 @@ struct Coarse {
       flat->search_filter(d_q, nq, nprobe, k1, nlist, cw.cpr_s.as<float>(), cw.cpr_l.as<int64_t>(), nullptr, cw);
       ws.probes.ensure(sizeof(int32_t) * nq * nprobe);
       launch_labels_to_i32(cw.cpr_l.as<int64_t>(), nq * nprobe, ws.probes.as<int32_t>(), ws.st);
+      return;
+    }
+    // the matrix-core ranking (PYR_COARSE_MFMA=0: the dense exact ranking below; same probes)
+    const char *cm = getenv("PYR_COARSE_MFMA");
+    if (!(cm && atoi(cm) == 0) && cfinite && coarse_mfma_supported(nlist, cs.dim, met, nprobe) &&
+        coarse_dense_supported(nlist)) {
+      ws.probes.ensure(sizeof(int32_t) * nq * nprobe);
+      const int64_t qb = std::max<int64_t>(1, std::min<int64_t>(int64_t(1) << 21, (int64_t(1) << 26) / nlist));
+      const int64_t nb = std::min<int64_t>(nq, qb);
+      ws.cpart_s.ensure(sizeof(float) * (size_t)nb * nlist);
+      ws.cfail.ensure(sizeof(int32_t) * (size_t)nb);
+      ws.cnfail.ensure(sizeof(int32_t));
+      for (int64_t a = 0; a < nq; a += qb) {
+        const int64_t n = std::min<int64_t>(qb, nq - a);
+        launch_coarse_mfma(d_q + a * cs.dim, rm.as<float>(), c2.as<float>(), n, nlist, cs.dim, met, nprobe, cnmax,
+                           coarse_cerr(cs.dim), ws.cpart_s.as<float>(), ws.cfail.as<int32_t>(),
+                           ws.cnfail.as<int32_t>(), ws.probes.as<int32_t>() + a * nprobe, ws.st);
+      }
       return;
     }
     const char *ce = getenv("PYR_COARSE_DENSE");  // 0: the top-k scan below (A/B only, same ranking)
@@ -1982,27 +2032,36 @@ struct IvfFlatIndex : Index {
       }
       HIPCHK(hipGetLastError());
     }
-    HIPCHK(hipMemcpyAsync(&nf, ws.fail_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, ws.st));
-    HIPCHK(hipStreamSynchronize(ws.st));
-    if (getenv("PYR_STREAM_DEBUG")) stream_debug(nq, k, k1, nparts, cap, nf, d_s, ws);
-    // what neither certificate covers: the exact scan over the failing queries' own probe lists
-    pyr_search_params ex{probes, 0, -1};
-    filter_fallback(ws, nf, d_q, dim, k, d_s, d_l, d_c,
-                    [&](const float *q2p, int64_t n2, float *s2, int64_t *l2, int32_t *c2) {
-                      Workspace &sw = ws.nested();
-                      sw.fprobes.ensure(sizeof(int32_t) * n2 * probes);
-                      launch_gather_rows_i32(ws.probes.as<int32_t>(), ws.fail.as<int32_t>(), n2, probes,
-                                             sw.fprobes.as<int32_t>(), ws.st);
-                      sw.ext_probes = sw.fprobes.as<int32_t>();
-                      sw.ext_nprobe = probes;
-                      try {
-                        search_exact(q2p, n2, k, ex, s2, l2, c2, sw);
-                      } catch (...) {
-                        sw.ext_probes = nullptr;
-                        throw;
-                      }
-                      sw.ext_probes = nullptr;
-                    });
+    // measurement only (the profiler's re-run count, PYR_STREAM_DEBUG): read the failure count back
+    const bool dbg = getenv("PYR_STREAM_DEBUG") != nullptr;
+    if (prof().on || dbg) {
+      HIPCHK(hipMemcpyAsync(&nf, ws.fail_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, ws.st));
+      HIPCHK(hipStreamSynchronize(ws.st));
+      if (dbg) stream_debug(nq, k, k1, nparts, cap, nf, d_s, ws);
+    }
+    // what neither certificate covers: the exact scan of the failing queries' own probe lists, driven by
+    // the device-side fail list (no host round trip: pyr_index_search_device stays asynchronous)
+    IvfRerunArgs ra{};
+    ra.rows = lists.rows.as<float>();
+    ra.live = lists.live.as<uint8_t>();
+    ra.labels = lists.labels.as<int64_t>();
+    ra.queries = d_q;
+    ra.probes = ws.probes.as<int32_t>();
+    ra.nprobe = probes;
+    ra.lb = dlb.as<int32_t>();
+    ra.le = dle.as<int32_t>();
+    ra.fail = ws.fail.as<int32_t>();
+    ra.nfail = ws.fail_cnt.as<int32_t>();
+    ra.dim = dim;
+    ra.k = k;
+    ra.out_s = d_s;
+    ra.out_l = d_l;
+    ra.out_c = d_c;
+    {
+      PhaseTimer t(PH_FALLBACK, ws.st, nf);
+      launch_ivf_exact_rerun(ra, metric, nq, ws.st);
+    }
+    HIPCHK(hipGetLastError());
   }
 
   int probe_only(const float *d_q, int64_t nq, int nprobe, int32_t *d_out, Workspace &ws) override {

@@ -104,6 +104,7 @@ struct Workspace {
   hipStream_t st = nullptr;
   bool own_stream = false;
   std::mutex m;
+  DevMem cfail, cnfail;  // coarse ranking on the matrix cores (coarse.hip launch_coarse_mfma)
   DevMem cpr_s, cpr_l;  // coarse step through the FLAT filter (on nested()): probe scores, centroid ids
   DevMem q, qn, qt, items, nitems, items2, nitems2, items3, nitems3, qlist, part_s, part_k, probes, cpart_s, cpart_k,
       limits;

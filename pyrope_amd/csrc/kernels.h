@@ -145,6 +145,26 @@ struct MergeIvf {
   int32_t nprobe = 0;
   IvfChunking ch{8, 1, 0};
 };
+// Exact IVF re-run of the queries whose certificate failed, on the device: the fail list and its
+// count stay in HBM (no host round trip).  One block per failing query, persistent over the list: the
+// exact ComputeScore (safe VectorMath form) of every live row of its probed lists, the top k (<= 64)
+// by (score desc, storage slot asc), written to out_* at the query's row.
+struct IvfRerunArgs {
+  const float *rows;        // blocked list store
+  const uint8_t *live;
+  const int64_t *labels;
+  const float *queries;     // row-major, the batch
+  const int32_t *probes;    // [nq][nprobe]
+  int32_t nprobe;
+  const int32_t *lb, *le;   // device list bounds
+  const int32_t *fail, *nfail;
+  int32_t dim, k;
+  float *out_s;
+  int64_t *out_l;
+  int32_t *out_c;
+};
+void launch_ivf_exact_rerun(const IvfRerunArgs &a, int metric, int64_t max_fail, hipStream_t st);
+
 void launch_merge_keys(const float *ps, const uint32_t *pk, int64_t nq, int32_t nparts, int32_t k,
                        const int64_t *row_labels, const int64_t *buf_labels, float *out_s, int64_t *out_l,
                        int32_t *out_keys, int32_t *out_cnt, hipStream_t st, const MergeIvf *ivf = nullptr);
@@ -223,6 +243,17 @@ bool coarse_dense_supported(int nlist);
 void launch_coarse_dense(const float *q, const float *cents_rm, const float *qn, const float *cn, int64_t nq,
                          int32_t nlist, int32_t dim, int32_t metric, int32_t nprobe, float *scores, int32_t *probes,
                          hipStream_t st);
+
+// The same ranking with the scores on the matrix cores (L2 / IP, dim % 16 == 0, nprobe <= 64): fp32 MFMA
+// approximate scores, aP = the nprobe-th largest of them, the exact ComputeScore of every centroid whose
+// approximate score reaches aP - 2E (E bounds the approximation) and the top nprobe of those; a query
+// with more than 64 such centroids gets the dense exact ranking.  c2: |c|^2 per centroid; cnmax >=
+// max |c|; c_err: the error-bound constant.  scores: nq x nlist scratch, fail: nq, nfail: 1 (device
+// scratch).  Nothing synchronizes.
+bool coarse_mfma_supported(int nlist, int dim, int metric, int nprobe);
+void launch_coarse_mfma(const float *q, const float *cents_rm, const float *c2, int64_t nq, int32_t nlist,
+                        int32_t dim, int32_t metric, int32_t nprobe, double cnmax, double c_err, float *scores,
+                        int32_t *fail, int32_t *nfail, int32_t *probes, hipStream_t st);
 
 // ---- 8-bit search mode of the FLAT index (sq8.hip; BruteForceVectorIndex EnableQuantization) ----
 struct Sq8Args {

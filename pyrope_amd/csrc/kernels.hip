@@ -1597,6 +1597,89 @@ void launch_fast_v(const ScanArgs &a, int metric, int V, int max_items, hipStrea
   else launch_fast_m<D, 1>(a, metric, max_items, st);
 }
 
+
+// ---- exact IVF re-run of certificate failures, device-driven (IvfRerunArgs, kernels.h) ----
+__device__ __forceinline__ uint64_t rr_shfl_xor64(uint64_t v, int m) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t rr_shfl64(uint64_t v, int src) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t rr_sort64_desc(uint64_t v, int lane) {
+#pragma unroll
+  for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+    for (int j = k >> 1; j >= 1; j >>= 1) {
+      const uint64_t o = rr_shfl_xor64(v, j);
+      const bool desc = (lane & k) == 0, lower = (lane & j) == 0;
+      v = (lower == desc) ? (v > o ? v : o) : (v < o ? v : o);
+    }
+  return v;
+}
+__device__ __forceinline__ uint64_t rr_merge64_desc(uint64_t v, int lane) {  // bitonic -> sorted desc
+#pragma unroll
+  for (int j = 32; j >= 1; j >>= 1) {
+    const uint64_t o = rr_shfl_xor64(v, j);
+    v = (lane & j) == 0 ? (v > o ? v : o) : (v < o ? v : o);
+  }
+  return v;
+}
+// rank key: score desc, then storage slot asc (~slot); 0 = no entry
+__device__ __forceinline__ uint64_t rr_key(float s, uint32_t slot) { return ((uint64_t)score_key(s) << 32) | (uint32_t)~slot; }
+
+template <int MET>
+__global__ __launch_bounds__(256) void ivf_exact_rerun_kernel(IvfRerunArgs a) {
+  __shared__ uint64_t wl[4][64];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int D = a.dim, k = a.k;
+  for (int i = blockIdx.x; i < *a.nfail; i += gridDim.x) {
+    const int64_t q = a.fail[i];
+    const float *qp = a.queries + (size_t)q * D;
+    uint64_t cur = 0ull;  // lane j: the wave's j-th best so far
+    for (int p = 0; p < a.nprobe; ++p) {
+      const int lst = a.probes[(size_t)q * a.nprobe + p];
+      if (lst < 0) continue;
+      const int e = a.le[lst];
+      for (int r0 = a.lb[lst] + 64 * w; r0 < e; r0 += 256) {
+        const int r = r0 + lane;
+        uint64_t key = 0ull;
+        if (r < e && a.live[r]) {
+          const float sc = em_score<1, MET>(Lin{qp}, Blk{a.rows, D, r}, D, 0.0f, 0.0f);
+          if (!isnan(sc)) key = rr_key(sc, (uint32_t)r);  // NaN never ranks (as better() in the scans)
+        }
+        const uint64_t kth = rr_shfl64(cur, k - 1);
+        if (!__builtin_amdgcn_ballot_w64(key > kth)) continue;
+        key = rr_sort64_desc(key, lane);
+        const uint64_t rv = rr_shfl64(key, 63 - lane);
+        cur = rr_merge64_desc(cur > rv ? cur : rv, lane);
+      }
+    }
+    wl[w][lane] = cur;
+    __syncthreads();
+    if (w == 0) {
+#pragma unroll
+      for (int o = 1; o < 4; ++o) {
+        const uint64_t rv = wl[o][63 - lane];
+        cur = rr_merge64_desc(cur > rv ? cur : rv, lane);
+      }
+      const uint64_t real = __builtin_amdgcn_ballot_w64(lane < k && cur != 0ull);
+      if (lane < k) {
+        float s = -INFINITY;
+        int64_t lab = -1;
+        if (cur != 0ull) {
+          s = key_score((uint32_t)(cur >> 32));
+          lab = a.labels[~(uint32_t)cur];
+        }
+        a.out_s[(size_t)q * k + lane] = s;
+        a.out_l[(size_t)q * k + lane] = lab;
+      }
+      if (lane == 0 && a.out_c) a.out_c[q] = (int32_t)__builtin_popcountll(real);
+    }
+    __syncthreads();
+  }
+}
 }  // namespace
 
 bool fast_path(int dim, int k) { return k <= KMAX_FAST && (dim == 32 || dim == 64 || dim == 96 || dim == 128); }
@@ -1941,6 +2024,13 @@ void launch_fill_results(float *s, int64_t *l, int32_t *c, int64_t nq, int32_t k
 void fill_u8(uint8_t *p, uint8_t v, int64_t n, hipStream_t st) {
   if (n <= 0) return;
   hipLaunchKernelGGL(fill_u8_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, p, v, n);
+}
+
+void launch_ivf_exact_rerun(const IvfRerunArgs &a, int metric, int64_t max_fail, hipStream_t st) {
+  if (max_fail <= 0 || a.k <= 0 || a.k > 64) return;
+  const unsigned grid = (unsigned)std::min<int64_t>(max_fail, 2048);
+  if (metric == L2) hipLaunchKernelGGL(ivf_exact_rerun_kernel<L2>, dim3(grid), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(ivf_exact_rerun_kernel<IP>, dim3(grid), dim3(256), 0, st, a);
 }
 
 }  // namespace pyr

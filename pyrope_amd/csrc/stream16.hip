@@ -44,6 +44,7 @@ namespace pyr {
 namespace {
 
 #include "f16util.h"
+#include "wselect.h"
 
 constexpr int SNW = 8;         // waves per stream block
 constexpr int SV = SNW * 4;    // sample values per (query, probe)
@@ -354,9 +355,10 @@ __global__ __launch_bounds__(64 * SNW, 1) void stream16_kernel(StreamArgs a) {
   }
 }
 
-// ---- 3. T_q = the K-th largest sample value (radix select over score keys, 8 bits a pass) ----
+// ---- 3. T_q = the K-th largest sample value (radix select over score keys, wselect.h) ----
 __global__ __launch_bounds__(256) void sselect_kernel(const float *samp, int64_t nq, int n, int K, float *thr) {
   __shared__ int hist[4][256];
+  __shared__ int buf[4][64];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t q = (int64_t)blockIdx.x * 4 + w;
   if (q >= nq) return;
@@ -364,56 +366,10 @@ __global__ __launch_bounds__(256) void sselect_kernel(const float *samp, int64_t
     if (lane == 0) thr[q] = -INFINITY;
     return;
   }
-  const float *v = samp + (size_t)q * n;
-  uint32_t prefix = 0u, pmask = 0u;
-  int rem = K;
-  for (int shift = 24; shift >= 0; shift -= 8) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) hist[w][lane + 64 * i] = 0;
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    for (int i = lane; i < n; i += 64) {
-      const uint32_t u = score_key(v[i]);
-      if ((u & pmask) == prefix) atomicAdd(&hist[w][(u >> shift) & 255], 1);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    // lane l holds bins 4l .. 4l+3; above(l) = rows in bins of higher lanes
-    int h4[4], s4 = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      h4[i] = hist[w][4 * lane + i];
-      s4 += h4[i];
-    }
-    int incl = s4;  // suffix sum over lanes >= l
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int o = __shfl_down(incl, off);
-      if (lane + off < 64) incl += o;
-    }
-    const int above = incl - s4;
-    int bin = -1, before = 0;
-    if (above < rem && incl >= rem) {
-      int acc = above;
-      for (int i = 3; i >= 0; --i) {
-        if (acc + h4[i] >= rem) {
-          bin = 4 * lane + i;
-          before = acc;
-          break;
-        }
-        acc += h4[i];
-      }
-    }
-    const uint64_t m = __builtin_amdgcn_ballot_w64(bin >= 0);
-    const int src = (int)__builtin_ctzll(m);  // exactly one lane found it
-    bin = __shfl(bin, src);
-    before = __shfl(before, src);
-    prefix |= (uint32_t)bin << shift;
-    pmask |= 255u << shift;
-    rem -= before;
-    __builtin_amdgcn_wave_barrier();
-  }
-  if (lane == 0) thr[q] = key_score(prefix);
+  float cv[16];
+  const uint32_t key = K <= 64 ? wave_kth_key_lm<16>(samp + (size_t)q * n, n, K, hist[w], buf[w], lane, cv)
+                               : wave_kth_key<16>(samp + (size_t)q * n, n, K, hist[w], lane, cv);
+  if (lane == 0) thr[q] = key_score(key);
 }
 
 // ---- 5. per query: the best KO emitted rows (+ floor placeholders), wave bitonic sort ----

@@ -128,3 +128,50 @@ def test_ivf_pq_p1_geometry(hiplib, oracle, nlist, nprobe):
         assert int(c[i]) == len(os_)
         np.testing.assert_array_equal(l[i][: len(ok)], labels[ok])
         assert np.array_equal(s[i][: len(os_)].view(np.uint32), os_.view(np.uint32))
+
+
+def _probe_sets(idx, qh, npb, **env):
+    import torch
+
+    from pyrope_amd import SearchOptions
+    q = torch.from_numpy(qh).cuda()
+    pr = torch.empty((len(qh), npb), dtype=torch.int32, device="cuda")
+    with _env(**env):
+        assert idx.probe_device(q.data_ptr(), len(qh), pr.data_ptr(), 0, SearchOptions(nprobe=npb)) == npb
+    torch.cuda.synchronize()
+    return pr.cpu().numpy()
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+@pytest.mark.parametrize("nlist,npb", [(1024, 32), (8192, 32), (8192, 64), (300, 16), (40, 40)])
+def test_mfma_coarse_ranking_equals_dense_exact(hiplib, metric, nlist, npb):
+    """The matrix-core coarse ranking (fp32 MFMA approximate scores, the exact ComputeScore of every
+    centroid within the error band of the nprobe-th; coarse.hip launch_coarse_mfma) gives the dense
+    exact ranking's probe lists, in order, for every query -- also when every query is forced through the in-kernel fallback
+    (PYR_COARSE_CERR=1e15), and on clustered queries whose centroid scores are tightly packed."""
+    from pyrope_amd import generate_synthetic
+    idx, x = _ivf(nlist, 12 if nlist > 1024 else 40, metric)
+    rng = np.random.default_rng(3)
+    qh = np.concatenate([generate_synthetic(300, 128, 11),
+                         (x[rng.choice(len(x), 200)] + 1e-3 * rng.standard_normal((200, 128))).astype(np.float32)])
+    ref = _probe_sets(idx, qh, npb, PYR_COARSE_MFMA=0)
+    np.testing.assert_array_equal(_probe_sets(idx, qh, npb), ref)
+    np.testing.assert_array_equal(_probe_sets(idx, qh, npb, PYR_COARSE_CERR="1e15"), ref)
+
+
+def test_mfma_coarse_ranking_ties_and_duplicate_centroids(hiplib):
+    """Duplicated centroids give exactly tied scores: the lower centroid index ranks first
+    (IvfFlatVectorIndex.cs:186-198 sorted with the index as the tie rule)."""
+    from pyrope_amd import IvfFlatVectorIndex, generate_synthetic
+    base = generate_synthetic(128, 128, 5)
+    cents = np.repeat(base, 4, axis=0)  # every centroid four times
+    x = generate_synthetic(4096, 128, 6)
+    idx = IvfFlatVectorIndex(128, 0, n_list=len(cents))
+    idx.set_centroids(cents)
+    idx.add_labels(np.arange(len(x), dtype=np.int64), x)
+    idx.build()
+    qh = generate_synthetic(200, 128, 7)
+    ref = _probe_sets(idx, qh, 24, PYR_COARSE_MFMA=0)
+    got = _probe_sets(idx, qh, 24)
+    np.testing.assert_array_equal(got, ref)
+    assert (np.diff(got[:, :4], axis=1) == 1).all()  # the four copies of the best centroid, in index order
