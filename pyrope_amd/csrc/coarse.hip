@@ -226,9 +226,11 @@ __global__ __launch_bounds__(256) void coarse_select_reg_kernel(const float *sco
 // 2. coarse_pick_kernel: the nprobe-th largest approximate score aP, the exact ComputeScore of every
 //    centroid within 2E of it (E bounds |approx - (score + |q|^2)|) and the first nprobe of those.
 // 3. coarse_select_list_kernel: the dense exact ranking of the queries the pick could not settle.
-template <int MET>
+template <int MET, int DT>
 __global__ __launch_bounds__(64) void coarse_approx_kernel(const float *q, const float *c, const float *c2, int64_t nq,
-                                                           int nc, int D, float *out) {
+                                                           int nc, int Dr, float *out) {
+  const int D = DT > 0 ? DT : Dr;  // a compile-time D unrolls the loop: every operand load is issued up front
+  constexpr int UNS = DT > 0 ? DT / 16 : 1;
   const int64_t q0 = (int64_t)blockIdx.y * 32;
   const int c0 = blockIdx.x * 32;
   const int l = threadIdx.x, r = l & 15, h = l >> 4;
@@ -244,6 +246,7 @@ __global__ __launch_bounds__(64) void coarse_approx_kernel(const float *q, const
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll UNS
   for (int s = 0; s < D / 16; ++s) {
     const float4 a0 = qa[0][4 * s], a1 = qa[1][4 * s], b0 = cb[0][4 * s], b1 = cb[1][4 * s];
     const float av[2][4] = {{a0.x, a0.y, a0.z, a0.w}, {a1.x, a1.y, a1.z, a1.w}};
@@ -272,9 +275,12 @@ __global__ __launch_bounds__(64) void coarse_approx_kernel(const float *q, const
 
 // ComputeScore (safe VectorMath form, as coarse_scores_kernel) spread over an 8-lane group: lane j runs
 // accumulator j over dims j, j + 8, ...; the group sums as hsum8 does; every lane returns the score
-template <int MET>
-__device__ __forceinline__ float exact_cs_l8(const float *qp, const float *cp, int D, int j) {
+template <int MET, int DT = 0>
+__device__ __forceinline__ float exact_cs_l8(const float *qp, const float *cp, int Dr, int j) {
+  const int D = DT > 0 ? DT : Dr;
+  constexpr int U = DT > 0 ? DT / 8 : 4;
   float acc = 0.0f;
+#pragma unroll U
   for (int d = j; d < (D & ~7); d += 8) {
     if (MET == L2) {
       const float t = qp[d] - cp[d];
@@ -323,10 +329,11 @@ __device__ __forceinline__ uint64_t sort64_desc(uint64_t v, int lane) {
 // them by (score desc, index asc).  Every centroid left out scores exactly below the nprobe centroids
 // whose approximate score reached aP.  More than 64 candidates, or a non-finite query: the exact
 // scores of every centroid go to the row and the query to the fail list (coarse_select_list_kernel).
-template <int MET>
+template <int MET, int DT>
 __global__ __launch_bounds__(256) void coarse_pick_kernel(const float *q, const float *c, float *scores, int64_t nq,
-                                                          int nc, int D, int P, double cnmax, double c_err,
+                                                          int nc, int Dr, int P, double cnmax, double c_err,
                                                           int32_t *probes, int32_t *fail, int32_t *nfail) {
+  const int D = DT > 0 ? DT : Dr;
   __shared__ int hist[4][256];
   __shared__ int cl[4][64];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -379,7 +386,7 @@ __global__ __launch_bounds__(256) void coarse_pick_kernel(const float *q, const 
     for (int p = 0; 8 * p < n; ++p) {
       const int cc = 8 * p + (lane >> 3);
       const int id = __shfl(cid, cc);
-      const float v = exact_cs_l8<MET>(qp, c + (size_t)max(id, 0) * D, D, lane & 7);
+      const float v = exact_cs_l8<MET, DT>(qp, c + (size_t)max(id, 0) * D, D, lane & 7);
       const float t = __shfl(v, 8 * (lane & 7));
       if ((lane >> 3) == p) sc = t;  // lane 8p + g took candidate 8p + g's score from group g
     }
@@ -391,7 +398,7 @@ __global__ __launch_bounds__(256) void coarse_pick_kernel(const float *q, const 
   // fallback: the exact scores of every centroid into the row, selection by coarse_select_list_kernel
   for (int c0 = 0; c0 < nc; c0 += 8) {
     const int id = c0 + (lane >> 3);
-    const float v = exact_cs_l8<MET>(qp, c + (size_t)min(id, nc - 1) * D, D, lane & 7);
+    const float v = exact_cs_l8<MET, DT>(qp, c + (size_t)min(id, nc - 1) * D, D, lane & 7);
     if ((lane & 7) == 0 && id < nc) row[id] = v;
   }
   if (lane == 0) fail[atomicAdd(nfail, 1)] = (int32_t)qi;
@@ -472,16 +479,24 @@ void launch_coarse_mfma(const float *q, const float *cents_rm, const float *c2, 
   if (nq <= 0 || nlist <= 0 || nprobe <= 0) return;
   const int P = std::min(nprobe, nlist);
   const dim3 ga((unsigned)((nlist + 31) / 32), (unsigned)((nq + 31) / 32));
-  if (metric == L2) hipLaunchKernelGGL(coarse_approx_kernel<L2>, ga, dim3(64), 0, st, q, cents_rm, c2, nq, nlist, dim, scores);
-  else hipLaunchKernelGGL(coarse_approx_kernel<IP>, ga, dim3(64), 0, st, q, cents_rm, c2, nq, nlist, dim, scores);
   const dim3 g4((unsigned)((nq + 3) / 4));
-  (void)hipMemsetAsync(nfail, 0, sizeof(int32_t), st);
-  if (metric == L2)
-    hipLaunchKernelGGL(coarse_pick_kernel<L2>, g4, dim3(256), 0, st, q, cents_rm, scores, nq, nlist, dim, P, cnmax,
+  auto go = [&](auto met, auto dt) {
+    constexpr int M = decltype(met)::value, DT = decltype(dt)::value;
+    hipLaunchKernelGGL((coarse_approx_kernel<M, DT>), ga, dim3(64), 0, st, q, cents_rm, c2, nq, nlist, dim, scores);
+    (void)hipMemsetAsync(nfail, 0, sizeof(int32_t), st);
+    hipLaunchKernelGGL((coarse_pick_kernel<M, DT>), g4, dim3(256), 0, st, q, cents_rm, scores, nq, nlist, dim, P, cnmax,
                        c_err, probes, fail, nfail);
-  else
-    hipLaunchKernelGGL(coarse_pick_kernel<IP>, g4, dim3(256), 0, st, q, cents_rm, scores, nq, nlist, dim, P, cnmax,
-                       c_err, probes, fail, nfail);
+  };
+  auto by_dim = [&](auto met) {
+    switch (dim) {
+      case 32: go(met, std::integral_constant<int, 32>{}); return;
+      case 64: go(met, std::integral_constant<int, 64>{}); return;
+      case 128: go(met, std::integral_constant<int, 128>{}); return;
+      default: go(met, std::integral_constant<int, 0>{}); return;
+    }
+  };
+  if (metric == L2) by_dim(std::integral_constant<int, L2>{});
+  else by_dim(std::integral_constant<int, IP>{});
   with_list_cap(nlist, P, [&](auto W) {
     hipLaunchKernelGGL(coarse_select_list_kernel<decltype(W)::value>, g4, dim3(256), 0, st, scores, fail, nfail, nlist,
                        P, probes);
