@@ -1817,7 +1817,7 @@ struct IvfFlatIndex : Index {
   // (list chunk, <= 512 queries) item every row whose approximate score reaches the query's sampled
   // threshold T_q is emitted; the best 64 per query are re-scored exactly and certified (depth K1, then
   // depth 64 for the failures); what still fails is re-run by the exact scan.  Query batches are
-  // sliced so that the candidate regions stay within 2 GiB.
+  // sliced so that the candidate regions stay within 16 GiB.
   void search_stream(const float *d_q, int64_t nq, int k, int k1, int probes, float *d_s, int64_t *d_l, int32_t *d_c,
                      Workspace &ws) {
     const bool q2 = stream_prec() == FILTER_F16X2;
@@ -1834,7 +1834,7 @@ struct IvfFlatIndex : Index {
     const int nparts = probes * ch.cmax;
     if (nparts > MAX_PARTS) throw Error(PYR_E_ARG, "nprobe too large");
     const int64_t per_q = (int64_t)nparts * cap * 8;
-    const int64_t qs = std::max<int64_t>(1, std::min<int64_t>(nq, (int64_t(2) << 30) / per_q));
+    const int64_t qs = std::max<int64_t>(1, std::min<int64_t>(nq, (int64_t(16) << 30) / per_q));
     for (int64_t a0 = 0; a0 < nq; a0 += qs) {
       const int64_t n = std::min(qs, nq - a0);
       const int32_t *ext = ws.ext_probes;
@@ -1854,13 +1854,14 @@ struct IvfFlatIndex : Index {
   void stream_debug(int64_t nq, int k, int k1, int nparts, int cap, int32_t nf, const float *d_s, Workspace &ws) {
     const size_t nslot = (size_t)nq * nparts;
     std::vector<float> ms((size_t)nq * STREAM_KO), thr(nq), res((size_t)nq * k);
-    std::vector<int32_t> mk((size_t)nq * STREAM_KO), cn(nslot), f1(nq);
+    std::vector<int32_t> mk((size_t)nq * STREAM_KO), f1(nq);
     std::vector<uint32_t> cf(nslot);
     int32_t n1 = 0;
     HIPCHK(hipMemcpyAsync(ms.data(), ws.ms.p, sizeof(float) * ms.size(), hipMemcpyDeviceToHost, ws.st));
     HIPCHK(hipMemcpyAsync(mk.data(), ws.mk.p, sizeof(int32_t) * mk.size(), hipMemcpyDeviceToHost, ws.st));
     HIPCHK(hipMemcpyAsync(thr.data(), ws.sthr.p, sizeof(float) * nq, hipMemcpyDeviceToHost, ws.st));
     HIPCHK(hipMemcpyAsync(res.data(), d_s, sizeof(float) * res.size(), hipMemcpyDeviceToHost, ws.st));
+    std::vector<int32_t> cn(nslot);
     HIPCHK(hipMemcpyAsync(cn.data(), ws.scn.p, sizeof(int32_t) * nslot, hipMemcpyDeviceToHost, ws.st));
     HIPCHK(hipMemcpyAsync(cf.data(), ws.scf.p, sizeof(uint32_t) * nslot, hipMemcpyDeviceToHost, ws.st));
     HIPCHK(hipMemcpyAsync(&n1, ws.fail_cnt2.p, sizeof(int32_t), hipMemcpyDeviceToHost, ws.st));
@@ -1868,7 +1869,7 @@ struct IvfFlatIndex : Index {
     HIPCHK(hipStreamSynchronize(ws.st));
     int64_t emitted = 0, full = 0, shallow = 0;
     for (size_t i = 0; i < nslot; ++i) {
-      emitted += cn[i];
+      emitted += cn[i];  // rows kept (runs of <= 8 per writer)
       full += cf[i] != 0u;
     }
     for (int64_t q = 0; q < nq; ++q) {
@@ -2057,9 +2058,12 @@ struct IvfFlatIndex : Index {
     ra.out_s = d_s;
     ra.out_l = d_l;
     ra.out_c = d_c;
-    {
+    // (measurement-only knobs that change the candidates skip the re-run: PYR_FILTER_ABLATE,
+    // PYR_STREAM_THR_BIAS)
+    if (!filter_ablate() && !getenv("PYR_STREAM_THR_BIAS")) {
       PhaseTimer t(PH_FALLBACK, ws.st, nf);
-      launch_ivf_exact_rerun(ra, metric, nq, ws.st);
+      ws.rrpart.ensure(sizeof(uint64_t) * std::max<int64_t>(1, nq * probes * k));
+      launch_ivf_exact_rerun(ra, metric, nq, ws.rrpart.as<uint64_t>(), ws.st);
     }
     HIPCHK(hipGetLastError());
   }

@@ -116,6 +116,7 @@ struct Workspace {
   DevMem q8q, q8qs;                               // 8-bit search mode: quantized queries, their sums
   // stream-and-emit list scan (stream16.hip): query operands, samples, thresholds, candidate regions
   DevMem sbq, sbql, sqsc, ssamp, sthr, scs, sck, scn, scf, swork, fail2, fail_cnt2;
+  DevMem rrpart;  // device re-run of certificate failures: per (query, probe) top-k keys
   const int32_t *ext_probes = nullptr;            // caller-ranked probe lists [nq][ext_nprobe] (multi-GPU)
   int32_t ext_nprobe = 0;
   // the re-run of certificate failures searches with its own buffers on the same stream

@@ -146,9 +146,10 @@ struct MergeIvf {
   IvfChunking ch{8, 1, 0};
 };
 // Exact IVF re-run of the queries whose certificate failed, on the device: the fail list and its
-// count stay in HBM (no host round trip).  One block per failing query, persistent over the list: the
-// exact ComputeScore (safe VectorMath form) of every live row of its probed lists, the top k (<= 64)
-// by (score desc, storage slot asc), written to out_* at the query's row.
+// count stay in HBM (no host round trip).  One block per (failing query, probed list), persistent over
+// them: the exact ComputeScore (safe VectorMath form) of every live row, the list's top k (<= 64) by
+// (score desc, storage slot asc); then one wave per failing query merges its lists and writes out_* at
+// the query's row.
 struct IvfRerunArgs {
   const float *rows;        // blocked list store
   const uint8_t *live;
@@ -163,7 +164,8 @@ struct IvfRerunArgs {
   int64_t *out_l;
   int32_t *out_c;
 };
-void launch_ivf_exact_rerun(const IvfRerunArgs &a, int metric, int64_t max_fail, hipStream_t st);
+// part: max_fail x nprobe x k rank keys of scratch (one block per (failing query, probe), then a merge)
+void launch_ivf_exact_rerun(const IvfRerunArgs &a, int metric, int64_t max_fail, uint64_t *part, hipStream_t st);
 
 void launch_merge_keys(const float *ps, const uint32_t *pk, int64_t nq, int32_t nparts, int32_t k,
                        const int64_t *row_labels, const int64_t *buf_labels, float *out_s, int64_t *out_l,

@@ -1629,24 +1629,58 @@ __device__ __forceinline__ uint64_t rr_merge64_desc(uint64_t v, int lane) {  // 
 // rank key: score desc, then storage slot asc (~slot); 0 = no entry
 __device__ __forceinline__ uint64_t rr_key(float s, uint32_t slot) { return ((uint64_t)score_key(s) << 32) | (uint32_t)~slot; }
 
-template <int MET>
-__global__ __launch_bounds__(256) void ivf_exact_rerun_kernel(IvfRerunArgs a) {
-  __shared__ uint64_t wl[4][64];
+// one block per (failing query, probe): the exact scores of the list's live rows, the block's top k
+// (<= 64) to part[(i * nprobe + p) * k ..] as rank keys (score desc, slot asc; 0 = none)
+// em_score<1, MET> (the safe L2Squared / DotProduct) of blocked row r for a compile-time D: every load
+// of the row issued before the arithmetic, which keeps the reference order
+template <int MET, int DT>
+__device__ __forceinline__ float rr_score(const float *qs, const float *rows, int64_t r) {
+  float x[DT];
+#pragma unroll
+  for (int d = 0; d < DT; ++d) x[d] = rows[blk_off(r, d, DT)];
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < DT; i += 8)
+#pragma unroll
+    for (int l = 0; l < 8; l++) {
+      if (MET == L2) {
+        const float d = qs[i + l] - x[i + l];
+        acc[l] = acc[l] + d * d;
+      } else {
+        acc[l] = acc[l] + qs[i + l] * x[i + l];
+      }
+    }
+  const float sum = 0.0f + hsum8(acc);
+  return MET == L2 ? -sum : sum;
+}
+
+template <int MET, int DT>
+__global__ __launch_bounds__(512) void ivf_rerun_scan_kernel(IvfRerunArgs a, uint64_t *part) {
+  __shared__ uint64_t wl[8][64];
+  __shared__ float qsh[DT > 0 ? DT : 1];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int D = a.dim, k = a.k;
-  for (int i = blockIdx.x; i < *a.nfail; i += gridDim.x) {
+  const int D = DT > 0 ? DT : a.dim, k = a.k;  // a compile-time D issues a row's loads at once
+  const int64_t units = (int64_t)(*a.nfail) * a.nprobe;
+  for (int64_t u = blockIdx.x; u < units; u += gridDim.x) {
+    const int64_t i = u / a.nprobe;
+    const int p = (int)(u % a.nprobe);
     const int64_t q = a.fail[i];
     const float *qp = a.queries + (size_t)q * D;
+    if constexpr (DT > 0) {
+      if (threadIdx.x < DT) qsh[threadIdx.x] = qp[threadIdx.x];
+      __syncthreads();
+    }
+    const int lst = a.probes[(size_t)q * a.nprobe + p];
     uint64_t cur = 0ull;  // lane j: the wave's j-th best so far
-    for (int p = 0; p < a.nprobe; ++p) {
-      const int lst = a.probes[(size_t)q * a.nprobe + p];
-      if (lst < 0) continue;
+    if (lst >= 0) {
       const int e = a.le[lst];
-      for (int r0 = a.lb[lst] + 64 * w; r0 < e; r0 += 256) {
+      for (int r0 = a.lb[lst] + 64 * w; r0 < e; r0 += 512) {
         const int r = r0 + lane;
         uint64_t key = 0ull;
         if (r < e && a.live[r]) {
-          const float sc = em_score<1, MET>(Lin{qp}, Blk{a.rows, D, r}, D, 0.0f, 0.0f);
+          float sc;
+          if constexpr (DT > 0) sc = rr_score<MET, DT>(qsh, a.rows, r);
+          else sc = em_score<1, MET>(Lin{qp}, Blk{a.rows, D, r}, D, 0.0f, 0.0f);
           if (!isnan(sc)) key = rr_key(sc, (uint32_t)r);  // NaN never ranks (as better() in the scans)
         }
         const uint64_t kth = rr_shfl64(cur, k - 1);
@@ -1659,26 +1693,46 @@ __global__ __launch_bounds__(256) void ivf_exact_rerun_kernel(IvfRerunArgs a) {
     wl[w][lane] = cur;
     __syncthreads();
     if (w == 0) {
-#pragma unroll
-      for (int o = 1; o < 4; ++o) {
+      for (int o = 1; o < 8; ++o) {
         const uint64_t rv = wl[o][63 - lane];
         cur = rr_merge64_desc(cur > rv ? cur : rv, lane);
       }
-      const uint64_t real = __builtin_amdgcn_ballot_w64(lane < k && cur != 0ull);
-      if (lane < k) {
-        float s = -INFINITY;
-        int64_t lab = -1;
-        if (cur != 0ull) {
-          s = key_score((uint32_t)(cur >> 32));
-          lab = a.labels[~(uint32_t)cur];
-        }
-        a.out_s[(size_t)q * k + lane] = s;
-        a.out_l[(size_t)q * k + lane] = lab;
-      }
-      if (lane == 0 && a.out_c) a.out_c[q] = (int32_t)__builtin_popcountll(real);
+      if (lane < k) part[u * k + lane] = cur;
     }
     __syncthreads();
   }
+}
+
+// one wave per failing query: the nprobe partial lists merged, the top k written at the query's row
+__global__ __launch_bounds__(256) void ivf_rerun_merge_kernel(IvfRerunArgs a, const uint64_t *part) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + w;
+  if (i >= *a.nfail) return;
+  const int k = a.k;
+  const int64_t q = a.fail[i];
+  const uint64_t *pp = part + (size_t)i * a.nprobe * k;
+  const int n = a.nprobe * k;
+  uint64_t cur = 0ull;
+  for (int b = 0; b < n; b += 64) {
+    uint64_t v = b + lane < n ? pp[b + lane] : 0ull;
+    const uint64_t kth = rr_shfl64(cur, k - 1);
+    if (!__builtin_amdgcn_ballot_w64(v > kth)) continue;
+    v = rr_sort64_desc(v, lane);
+    const uint64_t rv = rr_shfl64(v, 63 - lane);
+    cur = rr_merge64_desc(cur > rv ? cur : rv, lane);
+  }
+  const uint64_t real = __builtin_amdgcn_ballot_w64(lane < k && cur != 0ull);
+  if (lane < k) {
+    float s = -INFINITY;
+    int64_t lab = -1;
+    if (cur != 0ull) {
+      s = key_score((uint32_t)(cur >> 32));
+      lab = a.labels[~(uint32_t)cur];
+    }
+    a.out_s[(size_t)q * k + lane] = s;
+    a.out_l[(size_t)q * k + lane] = lab;
+  }
+  if (lane == 0 && a.out_c) a.out_c[q] = (int32_t)__builtin_popcountll(real);
 }
 }  // namespace
 
@@ -2026,11 +2080,18 @@ void fill_u8(uint8_t *p, uint8_t v, int64_t n, hipStream_t st) {
   hipLaunchKernelGGL(fill_u8_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, p, v, n);
 }
 
-void launch_ivf_exact_rerun(const IvfRerunArgs &a, int metric, int64_t max_fail, hipStream_t st) {
-  if (max_fail <= 0 || a.k <= 0 || a.k > 64) return;
-  const unsigned grid = (unsigned)std::min<int64_t>(max_fail, 2048);
-  if (metric == L2) hipLaunchKernelGGL(ivf_exact_rerun_kernel<L2>, dim3(grid), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(ivf_exact_rerun_kernel<IP>, dim3(grid), dim3(256), 0, st, a);
+void launch_ivf_exact_rerun(const IvfRerunArgs &a, int metric, int64_t max_fail, uint64_t *part, hipStream_t st) {
+  if (max_fail <= 0 || a.k <= 0 || a.k > 64 || a.nprobe <= 0) return;
+  const unsigned grid = (unsigned)std::min<int64_t>(max_fail * a.nprobe, 1024);
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(512), 0, st, a, part); };
+  const bool l2 = metric == L2;
+  switch (a.dim) {
+    case 32: l2 ? go(ivf_rerun_scan_kernel<L2, 32>) : go(ivf_rerun_scan_kernel<IP, 32>); break;
+    case 64: l2 ? go(ivf_rerun_scan_kernel<L2, 64>) : go(ivf_rerun_scan_kernel<IP, 64>); break;
+    case 128: l2 ? go(ivf_rerun_scan_kernel<L2, 128>) : go(ivf_rerun_scan_kernel<IP, 128>); break;
+    default: l2 ? go(ivf_rerun_scan_kernel<L2, 0>) : go(ivf_rerun_scan_kernel<IP, 0>); break;
+  }
+  hipLaunchKernelGGL(ivf_rerun_merge_kernel, dim3((unsigned)((max_fail + 3) / 4)), dim3(256), 0, st, a, part);
 }
 
 }  // namespace pyr

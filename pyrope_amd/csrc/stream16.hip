@@ -108,7 +108,7 @@ __global__ __launch_bounds__(256) void sprep_kernel(StreamArgs a) {
 }
 
 // ---- 2. / 4. the list scan ----
-template <int D, int MET, bool Q2, bool SAMPLE>
+template <int D, int MET, bool Q2, bool SAMPLE, bool AB = false>
 __global__ __launch_bounds__(64 * SNW, 1) void stream16_kernel(StreamArgs a) {
   constexpr int KS = D / 32;            // 16x16x32 k-steps
   constexpr int TB = 64 * D;            // h16 bytes per 32-row tile
@@ -260,7 +260,6 @@ __global__ __launch_bounds__(64 * SNW, 1) void stream16_kernel(StreamArgs a) {
         if (qi < qcnt) a.samp[(size_t)__float_as_int(rq.w) * SV + w * 4 + g] = mx + rq.z;
       }
     } else {
-      const bool ABL = (a.ablate & 64) != 0;
       // rows whose score can reach T_q -> the query's region of the part: the lane counts its passing
       // rows, reserves that many slots with ONE returning LDS atomic, then stores them (a region that
       // is full keeps the best score it had to drop as its floor)
@@ -294,11 +293,12 @@ __global__ __launch_bounds__(64 * SNW, 1) void stream16_kernel(StreamArgs a) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) y[4 * b + i] = fmaf(rq.x, acc[b][i], mr[4 * b + i]);
         const float mx = max3f(max3f(y[0], y[1], y[2]), max3f(y[3], y[4], y[5]), fmaxf(y[6], y[7]));
-        if (ABL) {
-          if (mx == 12345.0f) cnt_l[0] = 1;  // measurement only: keep the scores live
+        if constexpr (AB) {  // measurement only (PYR_FILTER_ABLATE=64): no emission
+          if (mx == 12345.0f) cnt_l[0] = 1;  // keep the scores live
           return;
         }
-        if (__builtin_amdgcn_ballot_w64(mx >= rq.y)) emit(y, rq, 16 * j + c, rt);
+        // rare (about 1 group-tile in 4 at I1): the emit code is laid out off the fall-through path
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(mx >= rq.y) != 0ull, 0)) emit(y, rq, 16 * j + c, rt);
       };
       // one tile against every group, software-pipelined over pairs of groups with two fixed register
       // sets: group j + 1's record and operands are read while group j's MFMAs run (the record first,
@@ -486,6 +486,7 @@ template <int D, int MET, bool Q2>
 void launch_stream_dm(const StreamArgs &a, int max_items, bool sample, hipStream_t st) {
   const int grid = std::max(1, std::min(max_items, device_cus()));
   if (sample) hipLaunchKernelGGL((stream16_kernel<D, MET, Q2, true>), dim3(grid), dim3(64 * SNW), 0, st, a);
+  else if (a.ablate & 64) hipLaunchKernelGGL((stream16_kernel<D, MET, Q2, false, true>), dim3(grid), dim3(64 * SNW), 0, st, a);
   else hipLaunchKernelGGL((stream16_kernel<D, MET, Q2, false>), dim3(grid), dim3(64 * SNW), 0, st, a);
 }
 
