@@ -437,18 +437,26 @@ static int stream_prec() {
 }
 // T_q = the R-th largest sample value.  Any R is correct (rows below T_q are represented by floor
 // placeholders at T_q and the certificate decides); R trades emitted rows against queries with fewer
-// than K1 real candidates.  The samples are ~5 % of a query's rows, so about R / 0.05 rows reach T_q,
-// and a query falls short of K1 = 16 only when R of its 15 best rows were sampled: P ~ C(15, R) 0.05^R,
-// 2.5e-7 at R = 8 (R = 16: ~320 emitted rows per query at I1, R = 8: ~160).  PYR_STREAM_RANK overrides.
-static int stream_rank(int k1) {
-  const char *e = getenv("PYR_STREAM_RANK");
-  if (e) return std::max(1, atoi(e));
-  return std::max(1, k1 / 2);
+// than k real candidates.  The sample holds a fraction f of a query's probed rows (I1: ~5 %), so about
+// R / f rows reach T_q, and a query falls short of K1 = 16 only when R of its 15 best rows were
+// sampled: P ~ C(15, R) f^R, 2.5e-7 at R = 8, f = 0.05.  Short lists sample most of their rows
+// (f -> 1): there R = K1/2 leaves ~R real candidates, below k, and every such query fails its
+// certificate -- so R = clamp(ceil(8 K1 f), K1/2, K1) per query (sselect_kernel): ~8 K1 emitted rows
+// at small f, R = K1 once f >= 1/8.  PYR_STREAM_RANK fixes R.
+static void stream_rank(int k1, int32_t &rmin, int32_t &rmax, double &et) {
+  if (const char *e = getenv("PYR_STREAM_RANK")) {
+    rmin = rmax = std::max(1, atoi(e));
+    et = 0.0;
+    return;
+  }
+  rmin = std::max(1, k1 / 2);
+  rmax = std::max(1, k1);
+  et = 8.0 * k1;
 }
 // candidate region per (query, part) (PYR_STREAM_CAP) and rows per list chunk (PYR_STREAM_CHUNK)
 static int stream_cap() {
   const char *e = getenv("PYR_STREAM_CAP");
-  return e ? std::max(8, atoi(e)) : 128;
+  return e ? std::max(8, atoi(e)) : 256;
 }
 static int64_t stream_chunk() {
   const char *e = getenv("PYR_STREAM_CHUNK");
@@ -1950,11 +1958,26 @@ struct IvfFlatIndex : Index {
     sa.row_limit = 0xFFFFFFFFu;
     sa.ablate = filter_ablate();
     sa.thr_bias = getenv("PYR_STREAM_THR_BIAS") ? (float)atof(getenv("PYR_STREAM_THR_BIAS")) : 0.0f;
+    const int prec = q2 ? FILTER_F16X2 : FILTER_F16X1;
+    sa.rsq16 = lists.rsq16.as<float>();
+    sa.rsq = lists.rsq.as<float>();
+    stream_ub_terms(dim, metric, filter_f16_cerr(dim, metric, prec), filter_cerr(dim),
+                    filter_f16_abs(dim, metric, lists.sx, prec), sa);
     {
       PhaseTimer t(PH_SAMPLE, ws.st);
       launch_stream_prep(sa, metric, maxi, ws.st);
       launch_stream_scan(sa, metric, maxi, true, ws.st);
-      launch_stream_select(ws.ssamp.as<float>(), nq, probes * sv, stream_rank(k1), ws.sthr.as<float>(), ws.st);
+      StreamSelectArgs sel{};
+      sel.samp = ws.ssamp.as<float>();
+      sel.nq = nq;
+      sel.n = probes * sv;
+      stream_rank(k1, sel.rmin, sel.rmax, sel.et);
+      sel.probes = ws.probes.as<int32_t>();
+      sel.nprobe = probes;
+      sel.lb = dlb.as<int32_t>();
+      sel.le = dle.as<int32_t>();
+      sel.thr = ws.sthr.as<float>();
+      launch_stream_select(sel, ws.st);
     }
     sa.work = ws.swork.as<int32_t>() + 1;
     {
@@ -2003,8 +2026,8 @@ struct IvfFlatIndex : Index {
     r.k = k;
     r.dim = dim;
     r.c_err = filter_cerr(dim);
-    const int prec = q2 ? FILTER_F16X2 : FILTER_F16X1;
     r.c_bf = filter_f16_cerr(dim, metric, prec);
+    r.ub = 1;
     r.c_abs = filter_f16_abs(dim, metric, lists.sx, prec);
     r.q16 = 1;
     r.resid = 1;
@@ -2062,7 +2085,8 @@ struct IvfFlatIndex : Index {
     // PYR_STREAM_THR_BIAS)
     if (!filter_ablate() && !getenv("PYR_STREAM_THR_BIAS")) {
       PhaseTimer t(PH_FALLBACK, ws.st, nf);
-      ws.rrpart.ensure(sizeof(uint64_t) * std::max<int64_t>(1, nq * probes * k));
+      ra.nchunk = (int32_t)std::max<int64_t>(1, std::min<int64_t>(64, (max_len + 1023) / 1024));
+      ws.rrpart.ensure(sizeof(uint64_t) * ivf_rerun_part_keys(nq, probes, k));
       launch_ivf_exact_rerun(ra, metric, nq, ws.rrpart.as<uint64_t>(), ws.st);
     }
     HIPCHK(hipGetLastError());

@@ -589,6 +589,16 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
     }
     const double u = 5.9604644775390625e-8;  // 2^-24
     const double qn = sqrt((double)qsq) * (1.0 + 1e-5);
+    if (a.resid && a.ub) {
+      // upper-bound candidates (stream16.hip, stream_ub_terms): every row left out -- below T_q, a
+      // region's floor, or merged below the K1-th -- has a reference score at most the K1-th entry
+      ok = nout == k && skth > ms[k1 - 1];
+      if (lane == 0) {
+        if (a.out_c) a.out_c[q] = nout;
+        if (!ok) a.fail_list[atomicAdd(a.fail_cnt, 1)] = (int32_t)q;
+      }
+      return;
+    }
     if (a.resid) {
       // IVF fp16 filter over residual tiles (filter16.hip, stream16.hip): approx estimates the score
       // itself,  L2: -|q - x|^2 = 2 (q-c).(x-c) - |x-c|^2 - |q-c|^2,  IP: q.x = q.(x-c) + q.c,

@@ -160,11 +160,14 @@ struct IvfRerunArgs {
   const int32_t *lb, *le;   // device list bounds
   const int32_t *fail, *nfail;
   int32_t dim, k;
+  int32_t nchunk;           // most chunks a probed list is cut into (>= 1; few failures use them all)
   float *out_s;
   int64_t *out_l;
   int32_t *out_c;
 };
-// part: max_fail x nprobe x k rank keys of scratch (one block per (failing query, probe), then a merge)
+// part: ivf_rerun_part_keys() rank keys of scratch (one block per (failing query, probe, chunk), then
+// a merge per query)
+int64_t ivf_rerun_part_keys(int64_t max_fail, int nprobe, int k);
 void launch_ivf_exact_rerun(const IvfRerunArgs &a, int metric, int64_t max_fail, uint64_t *part, hipStream_t st);
 
 void launch_merge_keys(const float *ps, const uint32_t *pk, int64_t nq, int32_t nparts, int32_t k,
@@ -380,7 +383,17 @@ struct StreamArgs {
   uint32_t key_base, row_limit;
   int32_t ablate;             // measurement only (PYR_FILTER_ABLATE=64: no emission)
   float thr_bias;             // measurement only (PYR_STREAM_THR_BIAS: added to T_q; results then differ)
+  // Upper-bound scores (stream_ub_terms): every emitted / sampled score is approx + E_row + E_pair,
+  // an upper bound of the reference's score of that row.  E_row = kr |x - c|^2 (+ kx |x|^2, IP) per
+  // row, E_pair = kq A^2 + kqa A (+ kqc |q| |c|, IP) per (query, list), A = |q - c| (L2) / |q| (IP).
+  const float *rsq16;         // per row |x - c|^2
+  const float *rsq;           // per row |x|^2 (IP)
+  float kr, kx, kq, kqa, kqc;
 };
+// The per-row / per-pair split of the fp16 residual filter's error bound (refine_kernel's resid branch,
+// filter.hip): products A X go to (A^2 + X^2) / 2, (A + X)^2 to 2 (A^2 + X^2), so the bound of a row
+// no longer depends on its list's largest residual; the reference's own sum deviation (g) is folded in.
+void stream_ub_terms(int dim, int metric, double c_bf, double c_err, double c_abs, StreamArgs &a);
 struct CandMergeArgs {
   const float *cand_s;
   const uint32_t *cand_k;
@@ -397,7 +410,20 @@ int stream16_qmax(bool q2);          // queries per work item
 int stream16_sample_values();        // sample values per (query, probe)
 void launch_stream_prep(const StreamArgs &a, int metric, int max_items, hipStream_t st);
 void launch_stream_scan(const StreamArgs &a, int metric, int max_items, bool sample, hipStream_t st);
-void launch_stream_select(const float *samp, int64_t nq, int n, int k1, float *thr, hipStream_t st);
+// T_q per query: the R-th largest of its n sample values, R from the sampled fraction f of its probed
+// rows: R = clamp(ceil(et f), rmin, rmax) (rmin == rmax: fixed)
+struct StreamSelectArgs {
+  const float *samp;
+  int64_t nq;
+  int32_t n;
+  int32_t rmin, rmax;
+  double et;
+  const int32_t *probes;  // [nq][nprobe]
+  int32_t nprobe;
+  const int32_t *lb, *le;
+  float *thr;
+};
+void launch_stream_select(const StreamSelectArgs &a, hipStream_t st);
 void launch_cand_merge(const CandMergeArgs &m, hipStream_t st);
 
 struct RefineArgs {
@@ -426,6 +452,7 @@ struct RefineArgs {
   const float *cents;
   const uint32_t *list_rmax_r;
   int32_t resid;
+  int32_t ub;               // resid: candidate scores are upper bounds (StreamArgs kr ..): no error term
   float *out_s;
   int64_t *out_l;
   int32_t *out_c;

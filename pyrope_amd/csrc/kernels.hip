@@ -1629,41 +1629,56 @@ __device__ __forceinline__ uint64_t rr_merge64_desc(uint64_t v, int lane) {  // 
 // rank key: score desc, then storage slot asc (~slot); 0 = no entry
 __device__ __forceinline__ uint64_t rr_key(float s, uint32_t slot) { return ((uint64_t)score_key(s) << 32) | (uint32_t)~slot; }
 
-// one block per (failing query, probe): the exact scores of the list's live rows, the block's top k
-// (<= 64) to part[(i * nprobe + p) * k ..] as rank keys (score desc, slot asc; 0 = none)
-// em_score<1, MET> (the safe L2Squared / DotProduct) of blocked row r for a compile-time D: every load
-// of the row issued before the arithmetic, which keeps the reference order
+// Work units are (failing query i, probe p, chunk c): every probed list is cut into nc near-equal
+// chunks of whole 64-row groups, nc = min(a.nchunk, ceil(RR_UNITS / (nfail * nprobe))) -- a few
+// failures spread over every CU, many keep one unit per (query, probe).  One block per unit: the
+// exact scores of the chunk's live rows, its top k (<= 64) to part[u * k ..] as rank keys (score
+// desc, slot asc; 0 = none).
+constexpr int64_t RR_UNITS = 8192;
+__device__ __forceinline__ int rr_nchunks(int64_t pairs, int nchunk) {
+  if (pairs <= 0) return 1;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(nchunk, (RR_UNITS + pairs - 1) / pairs));
+}
+// em_score<1, MET> (the safe L2Squared / DotProduct) of blocked row r for a compile-time D, the row
+// read 32 dims at a time (the sums keep the reference order: acc[l] over i ascending, then hsum8)
 template <int MET, int DT>
 __device__ __forceinline__ float rr_score(const float *qs, const float *rows, int64_t r) {
-  float x[DT];
-#pragma unroll
-  for (int d = 0; d < DT; ++d) x[d] = rows[blk_off(r, d, DT)];
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll 1
+  for (int i0 = 0; i0 < DT; i0 += 32) {
+    float x[32];
 #pragma unroll
-  for (int i = 0; i < DT; i += 8)
+    for (int d = 0; d < 32; ++d) x[d] = rows[blk_off(r, i0 + d, DT)];
 #pragma unroll
-    for (int l = 0; l < 8; l++) {
-      if (MET == L2) {
-        const float d = qs[i + l] - x[i + l];
-        acc[l] = acc[l] + d * d;
-      } else {
-        acc[l] = acc[l] + qs[i + l] * x[i + l];
+    for (int i = 0; i < 32; i += 8)
+#pragma unroll
+      for (int l = 0; l < 8; l++) {
+        if (MET == L2) {
+          const float d = qs[i0 + i + l] - x[i + l];
+          acc[l] = acc[l] + d * d;
+        } else {
+          acc[l] = acc[l] + qs[i0 + i + l] * x[i + l];
+        }
       }
-    }
+  }
   const float sum = 0.0f + hsum8(acc);
   return MET == L2 ? -sum : sum;
 }
 
 template <int MET, int DT>
-__global__ __launch_bounds__(512) void ivf_rerun_scan_kernel(IvfRerunArgs a, uint64_t *part) {
-  __shared__ uint64_t wl[8][64];
+__global__ __launch_bounds__(256) void ivf_rerun_scan_kernel(IvfRerunArgs a, uint64_t *part) {
+  __shared__ uint64_t wl[4][64];
   __shared__ float qsh[DT > 0 ? DT : 1];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int D = DT > 0 ? DT : a.dim, k = a.k;  // a compile-time D issues a row's loads at once
-  const int64_t units = (int64_t)(*a.nfail) * a.nprobe;
+  const int D = DT > 0 ? DT : a.dim, k = a.k;
+  const int64_t pairs = (int64_t)(*a.nfail) * a.nprobe;
+  const int nc = rr_nchunks(pairs, a.nchunk);
+  const int64_t units = pairs * nc;
   for (int64_t u = blockIdx.x; u < units; u += gridDim.x) {
-    const int64_t i = u / a.nprobe;
-    const int p = (int)(u % a.nprobe);
+    const int64_t pi = u / nc;
+    const int c = (int)(u - pi * nc);
+    const int64_t i = pi / a.nprobe;
+    const int p = (int)(pi - i * a.nprobe);
     const int64_t q = a.fail[i];
     const float *qp = a.queries + (size_t)q * D;
     if constexpr (DT > 0) {
@@ -1673,11 +1688,13 @@ __global__ __launch_bounds__(512) void ivf_rerun_scan_kernel(IvfRerunArgs a, uin
     const int lst = a.probes[(size_t)q * a.nprobe + p];
     uint64_t cur = 0ull;  // lane j: the wave's j-th best so far
     if (lst >= 0) {
-      const int e = a.le[lst];
-      for (int r0 = a.lb[lst] + 64 * w; r0 < e; r0 += 512) {
+      const int b = a.lb[lst], e = a.le[lst];
+      const int cl = (((e - b) + nc - 1) / nc + 63) & ~63;
+      const int cb = b + c * cl, ce = min(e, cb + cl);
+      for (int r0 = cb + 64 * w; r0 < ce; r0 += 256) {
         const int r = r0 + lane;
         uint64_t key = 0ull;
-        if (r < e && a.live[r]) {
+        if (r < ce && a.live[r]) {
           float sc;
           if constexpr (DT > 0) sc = rr_score<MET, DT>(qsh, a.rows, r);
           else sc = em_score<1, MET>(Lin{qp}, Blk{a.rows, D, r}, D, 0.0f, 0.0f);
@@ -1693,7 +1710,7 @@ __global__ __launch_bounds__(512) void ivf_rerun_scan_kernel(IvfRerunArgs a, uin
     wl[w][lane] = cur;
     __syncthreads();
     if (w == 0) {
-      for (int o = 1; o < 8; ++o) {
+      for (int o = 1; o < 4; ++o) {
         const uint64_t rv = wl[o][63 - lane];
         cur = rr_merge64_desc(cur > rv ? cur : rv, lane);
       }
@@ -1703,15 +1720,17 @@ __global__ __launch_bounds__(512) void ivf_rerun_scan_kernel(IvfRerunArgs a, uin
   }
 }
 
-// one wave per failing query: the nprobe partial lists merged, the top k written at the query's row
+// one wave per failing query: its nprobe x nc partial lists merged, the top k written at the query's row
 __global__ __launch_bounds__(256) void ivf_rerun_merge_kernel(IvfRerunArgs a, const uint64_t *part) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * 4 + w;
-  if (i >= *a.nfail) return;
+  const int64_t nfail = *a.nfail;
+  if (i >= nfail) return;
   const int k = a.k;
   const int64_t q = a.fail[i];
-  const uint64_t *pp = part + (size_t)i * a.nprobe * k;
-  const int n = a.nprobe * k;
+  const int nc = rr_nchunks(nfail * a.nprobe, a.nchunk);
+  const uint64_t *pp = part + (size_t)i * a.nprobe * nc * k;
+  const int n = a.nprobe * nc * k;
   uint64_t cur = 0ull;
   for (int b = 0; b < n; b += 64) {
     uint64_t v = b + lane < n ? pp[b + lane] : 0ull;
@@ -2080,10 +2099,14 @@ void fill_u8(uint8_t *p, uint8_t v, int64_t n, hipStream_t st) {
   hipLaunchKernelGGL(fill_u8_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, p, v, n);
 }
 
+int64_t ivf_rerun_part_keys(int64_t max_fail, int nprobe, int k) {
+  return (int64_t)k * std::max<int64_t>(max_fail * nprobe, 2 * RR_UNITS);
+}
+
 void launch_ivf_exact_rerun(const IvfRerunArgs &a, int metric, int64_t max_fail, uint64_t *part, hipStream_t st) {
-  if (max_fail <= 0 || a.k <= 0 || a.k > 64 || a.nprobe <= 0) return;
-  const unsigned grid = (unsigned)std::min<int64_t>(max_fail * a.nprobe, 1024);
-  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(512), 0, st, a, part); };
+  if (max_fail <= 0 || a.k <= 0 || a.k > 64 || a.nprobe <= 0 || a.nchunk <= 0) return;
+  const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(max_fail * a.nprobe, 2 * RR_UNITS), 2048);
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, a, part); };
   const bool l2 = metric == L2;
   switch (a.dim) {
     case 32: l2 ? go(ivf_rerun_scan_kernel<L2, 32>) : go(ivf_rerun_scan_kernel<IP, 32>); break;

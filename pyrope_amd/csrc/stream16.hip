@@ -74,7 +74,7 @@ __global__ __launch_bounds__(256) void sprep_kernel(StreamArgs a) {
     const float4 *qp = reinterpret_cast<const float4 *>(a.queries + (size_t)q * D + 8 * sub);
     const float4 q0 = qp[0], q1 = qp[1];
     const float qv[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
-    float r[8], cq = 0.0f, amax = 0.0f;
+    float r[8], cq = 0.0f, amax = 0.0f, q2 = 0.0f, c2 = 0.0f;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       if (MET == L2) {
@@ -83,6 +83,8 @@ __global__ __launch_bounds__(256) void sprep_kernel(StreamArgs a) {
       } else {
         r[u] = qv[u];
         cq += qv[u] * cv[u];
+        q2 += qv[u] * qv[u];
+        c2 += cv[u] * cv[u];
       }
       amax = fmaxf(amax, fabsf(r[u]));
     }
@@ -90,6 +92,18 @@ __global__ __launch_bounds__(256) void sprep_kernel(StreamArgs a) {
     for (int off = 1; off < LQ; off <<= 1) {
       cq += __shfl_xor(cq, off);
       amax = fmaxf(amax, __shfl_xor(amax, off));
+      if (MET == IP) {
+        q2 += __shfl_xor(q2, off);
+        c2 += __shfl_xor(c2, off);
+      }
+    }
+    // the pair's share of the error bound (stream_ub_terms), rounded up by the 1e-3 in its constants
+    float ep = 0.0f;
+    if (MET == L2) {
+      ep = a.kq * cq + a.kqa * sqrtf(cq);
+    } else {
+      const float qn = sqrtf(q2);
+      ep = a.kq * q2 + a.kqa * qn + a.kqc * qn * sqrtf(c2);
     }
     const float sq = pow2_scale(amax);
     if (act) {
@@ -102,7 +116,7 @@ __global__ __launch_bounds__(256) void sprep_kernel(StreamArgs a) {
       }
       *reinterpret_cast<h8v *>(a.bq + (size_t)pos * D + 8 * sub) = hv;
       if (a.bql) *reinterpret_cast<h8v *>(a.bql + (size_t)pos * D + 8 * sub) = lv;
-      if (sub == 0) a.qsc[pos] = make_float2((MET == L2 ? 2.0f : 1.0f) / (sq * a.sx), MET == L2 ? -cq : cq);
+      if (sub == 0) a.qsc[pos] = make_float2((MET == L2 ? 2.0f : 1.0f) / (sq * a.sx), (MET == L2 ? -cq : cq) + ep);
     }
   }
 }
@@ -183,9 +197,23 @@ __global__ __launch_bounds__(64 * SNW, 1) void stream16_kernel(StreamArgs a) {
         A[s][0] = *reinterpret_cast<const h8v *>(tb + s * 2048);
         A[s][1] = *reinterpret_cast<const h8v *>(tb + s * 2048 + 256);
       }
-      const float *mp = a.meta + (size_t)(r0 + 32 * t) + 4 * g;
-      M[0] = *reinterpret_cast<const f4v *>(mp);
-      M[1] = *reinterpret_cast<const f4v *>(mp + 16);
+      const size_t mo = (size_t)(r0 + 32 * t) + 4 * g;
+      const f4v m0 = *reinterpret_cast<const f4v *>(a.meta + mo), m1 = *reinterpret_cast<const f4v *>(a.meta + mo + 16);
+      const f4v x0 = *reinterpret_cast<const f4v *>(a.rsq16 + mo), x1 = *reinterpret_cast<const f4v *>(a.rsq16 + mo + 16);
+      // the row's share of the error bound (stream_ub_terms): -inf (dead, NaN) and +inf (Inf) meta stay
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        M[0][i] = fmaf(a.kr, x0[i], m0[i]);
+        M[1][i] = fmaf(a.kr, x1[i], m1[i]);
+      }
+      if constexpr (MET == IP) {
+        const f4v n0 = *reinterpret_cast<const f4v *>(a.rsq + mo), n1 = *reinterpret_cast<const f4v *>(a.rsq + mo + 16);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          M[0][i] = fmaf(a.kx, n0[i], M[0][i]);
+          M[1][i] = fmaf(a.kx, n1[i], M[1][i]);
+        }
+      }
     };
     // query group j's operands from LDS (one term: 4 x ds_read_b128 at D = 128; the split adds 4)
     auto read_b = [&](int j, h8v (&B)[KS], h8v (&B2)[KS]) {
@@ -355,21 +383,44 @@ __global__ __launch_bounds__(64 * SNW, 1) void stream16_kernel(StreamArgs a) {
   }
 }
 
-// ---- 3. T_q = the K-th largest sample value (radix select over score keys, wselect.h) ----
-__global__ __launch_bounds__(256) void sselect_kernel(const float *samp, int64_t nq, int n, int K, float *thr) {
+// ---- 3. T_q = the R-th largest sample value (radix select over score keys, wselect.h) ----
+// The sample holds min(len, 512) rows of each probed list, so about R / f rows of the probed lists
+// reach T_q (f = the sampled fraction of the query's probed rows).  R adapts to f: the rows it
+// guarantees (R) stay at least rmin, the rows it emits (~R / f) near et, R <= rmax -- short lists
+// (f ~ 1) take R = rmax = K1 so the k-th row sits well above T_q, long ones R = rmin (I1: f ~ 0.05).
+__global__ __launch_bounds__(256) void sselect_kernel(StreamSelectArgs a) {
   __shared__ int hist[4][256];
   __shared__ int buf[4][64];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t q = (int64_t)blockIdx.x * 4 + w;
-  if (q >= nq) return;
+  if (q >= a.nq) return;
+  int K = a.rmax;
+  if (a.rmin < a.rmax) {
+    int64_t tot = 0, smp = 0;
+    for (int p = lane; p < a.nprobe; p += 64) {
+      const int l = a.probes[(size_t)q * a.nprobe + p];
+      if (l < 0) continue;
+      const int64_t len = a.le[l] - a.lb[l];
+      tot += len;
+      smp += min(len, (int64_t)(SAMPLE_TILES * 32));
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      tot += __shfl_xor(tot, off);
+      smp += __shfl_xor(smp, off);
+    }
+    const double f = tot > 0 ? (double)smp / (double)tot : 1.0;
+    K = (int)fmin((double)a.rmax, fmax((double)a.rmin, ceil(a.et * f)));
+  }
+  const int n = a.n;
   if (n < K) {
-    if (lane == 0) thr[q] = -INFINITY;
+    if (lane == 0) a.thr[q] = -INFINITY;
     return;
   }
   float cv[16];
-  const uint32_t key = K <= 64 ? wave_kth_key_lm<16>(samp + (size_t)q * n, n, K, hist[w], buf[w], lane, cv)
-                               : wave_kth_key<16>(samp + (size_t)q * n, n, K, hist[w], lane, cv);
-  if (lane == 0) thr[q] = key_score(key);
+  const uint32_t key = K <= 64 ? wave_kth_key_lm<16>(a.samp + (size_t)q * n, n, K, hist[w], buf[w], lane, cv)
+                               : wave_kth_key<16>(a.samp + (size_t)q * n, n, K, hist[w], lane, cv);
+  if (lane == 0) a.thr[q] = key_score(key);
 }
 
 // ---- 5. per query: the best KO emitted rows (+ floor placeholders), wave bitonic sort ----
@@ -527,9 +578,33 @@ void launch_stream_scan(const StreamArgs &a, int metric, int max_items, bool sam
   }
 }
 
-void launch_stream_select(const float *samp, int64_t nq, int n, int k1, float *thr, hipStream_t st) {
-  if (nq <= 0) return;
-  hipLaunchKernelGGL(sselect_kernel, dim3(nblk(nq, 4)), dim3(256), 0, st, samp, nq, n, k1, thr);
+void stream_ub_terms(int dim, int metric, double c_bf, double c_err, double c_abs, StreamArgs &a) {
+  const double u = 5.9604644775390625e-8;         // 2^-24
+  const double t = 1.4551915228366852e-11 * std::sqrt((double)dim);  // the query's fp16 subnormals, 2^-36 sqrt(D)
+  const double g = (dim / 8.0 + 8.0) * u;         // the reference's own sum (refine_kernel)
+  const double up = 1.0 + 1e-3;                   // the fp32 evaluation of the terms themselves
+  if (metric == L2) {
+    // c_bf u A X + c_err u (A + X)^2 + c_abs A + 2 t A X, and g |q - x|^2 <= g (A + X)^2
+    const double k = (c_bf * u / 2.0 + 2.0 * c_err * u + t + 2.0 * g) * up + 8.0 * u;
+    a.kr = (float)k;
+    a.kq = (float)k;
+    a.kqa = (float)(c_abs * up);
+    a.kx = 0.0f;
+    a.kqc = 0.0f;
+  } else {
+    // c_bf u |q| X + c_err u |q| X + c_abs |q| + t |q| X + c_err u |q||c| + g |q||x|
+    const double k = ((c_bf + c_err) * u + t) / 2.0 * up + 8.0 * u;
+    a.kr = (float)k;
+    a.kq = (float)(k + g / 2.0 * up);
+    a.kx = (float)(g / 2.0 * up + 8.0 * u);
+    a.kqa = (float)(c_abs * up);
+    a.kqc = (float)(c_err * u * up);
+  }
+}
+
+void launch_stream_select(const StreamSelectArgs &a, hipStream_t st) {
+  if (a.nq <= 0) return;
+  hipLaunchKernelGGL(sselect_kernel, dim3(nblk(a.nq, 4)), dim3(256), 0, st, a);
 }
 
 void launch_cand_merge(const CandMergeArgs &m, hipStream_t st) {

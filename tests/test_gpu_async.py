@@ -114,3 +114,26 @@ def test_search_device_graph_capture_and_replay(hiplib):
     g.replay()
     torch.cuda.synchronize()
     _same(out, ra)
+
+
+@pytest.mark.parametrize("nq", [1, 3, 40])
+def test_device_rerun_chunks_long_lists(hiplib, nq):
+    """A few failing queries split every probed list into up to 64 row chunks (kernels.hip
+    ivf_rerun_scan_kernel: units (query, probe, chunk), then a merge over nprobe x chunks partial
+    lists): long ragged lists (4 lists over 50,001 rows, some rows deleted) give the exact results."""
+    from pyrope_amd import IvfFlatVectorIndex, SearchOptions, generate_synthetic
+    x = generate_synthetic(50_001, 128, 7)
+    idx = IvfFlatVectorIndex(128, 0, n_list=4)
+    idx.add_labels(np.arange(len(x), dtype=np.int64), x)
+    idx.build()
+    for lab in range(0, 50_001, 97):
+        assert idx.delete(str(lab))
+    q = generate_synthetic(nq, 128, 8)
+    opts = SearchOptions(nprobe=3)
+    with _env(PYR_FILTER=0):
+        exact = idx.search_batch(q, 10, opts)
+    with _env(PYR_FILTER_CERR="1e15"):
+        got = idx.search_batch(q, 10, opts)
+    np.testing.assert_array_equal(got[2], exact[2])
+    np.testing.assert_array_equal(got[1], exact[1])
+    assert np.array_equal(got[0].view(np.uint32), exact[0].view(np.uint32))

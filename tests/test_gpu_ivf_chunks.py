@@ -184,15 +184,18 @@ def test_per_list_certificate_on_skewed_data(hiplib, metric):
             got_g, nfb_global = _fallbacks(hiplib, lambda: idx.search_batch(q, 10, opts))
     _same(got, ref)
     _same(got_g, ref)
-    # the default fp16 residual-tile filter: hub lists far from the query make its residual error
-    # bound large, so more queries go to the re-run tiers -- results stay exact
+    # the default path (stream16.hip over fp16 residual tiles): candidates carry per-row upper bounds
+    # (stream_ub_terms), so an outlier inflates only its own row's bound, not its list's; the sample
+    # rank adapts to these short, mostly-sampled lists (sselect_kernel).  Round 2 re-ran 254 / 296 of
+    # the 400 queries here; now at most 1 % may fail.
     got16, nfb16 = _fallbacks(hiplib, lambda: idx.search_batch(q, 10, opts))
     _same(got16, ref)
     print(f"\n[cert] metric={metric}: bf16x3 exact re-runs per-list bound {nfb_list}/{len(q)}, "
-          f"index-wide bound {nfb_global}/{len(q)}; fp16 tiles re-runs (all tiers) {nfb16}")
+          f"index-wide bound {nfb_global}/{len(q)}; fp16 stream re-runs {nfb16}/{len(q)}")
     assert nfb_list <= nfb_global
     if metric == 0:
         assert nfb_list < len(q) // 10
+    assert nfb16 <= len(q) // 100
 
 
 @pytest.mark.parametrize("metric", [0, 1])
