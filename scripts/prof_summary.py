@@ -79,7 +79,7 @@ def main(src: str, dst: str) -> None:
         md.append(f"| `{short(r[0])}` | {r[1]} | {r[6]} | {r[8] / 1e6:.4f} | {r[4]} | {r[3]} |")
     md.append("")
     for key, v in counters.items():
-        if ("scan" not in key[0] and "mfma_filter" not in key[0]) or v.get("avg_ns_profiled", 0) < 1e6:
+        if not any(s in key[0] for s in ("scan", "mfma_filter", "stream16_kernel")) or v.get("avg_ns_profiled", 0) < 1e6:
             continue
         line = [f"## `{key[0]}` grid {key[1]}", "",
                 f"- dispatches profiled: {v['dispatches']}, avg duration under counters: "
