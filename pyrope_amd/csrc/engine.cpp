@@ -742,6 +742,12 @@ struct FlatIndex : Index {
   // forms (ComputeScore of the IVF coarse step, when this store holds an index's centroids)
   int exact_v = 4;
 
+  // Cosine on the filter path: an L2 FLAT index over the unit rows x / |x| of the same slots (its labels
+  // are the slots), searched with the unit queries; its exact top-K2 are the candidates whose exact
+  // Cosine (:354) cos_rerank_kernel ranks and certifies (filter.hip).  zflag: a zero-norm row was written
+  std::unique_ptr<FlatIndex> unit;
+  DevMem zflag;
+
   explicit FlatIndex(const pyr_index_desc &d) : Index(d) {
     st.dim = dim;
     st.cosine = metric == COS;  // norm cached at Add (:146)
@@ -749,12 +755,47 @@ struct FlatIndex : Index {
     st.center16 = st.f16 && metric == L2;  // fp16 tiles of x - mean (engine.h RowStore)
     st.met16 = metric;
     dp = sq8_dp(dim);
+    if (metric == COS && store16(dim, L2)) unit_reset();
+  }
+  void unit_reset() {
+    pyr_index_desc u = desc;
+    u.metric = L2;
+    unit = std::make_unique<FlatIndex>(u);
+    zflag.ensure(sizeof(uint32_t));
+    HIPCHK(hipMemsetAsync(zflag.p, 0, sizeof(uint32_t), wst));
+    HIPCHK(hipStreamSynchronize(wst));
+  }
+  // the unit rows of the slots just written (device norms: the reference's ComputeNorm and its 1e-6 rule)
+  void unit_write(int64_t n, const std::vector<int64_t> &slots) {
+    if (!unit || n <= 0) return;
+    stage_b.ensure(sizeof(float) * n * dim);
+    launch_unit_rows(st.rows.as<float>(), stage_i.as<int64_t>(), st.norms.as<float>(), n, dim, stage_b.as<float>(),
+                     wst, zflag.as<uint32_t>());
+    std::vector<float> xu((size_t)n * dim);
+    HIPCHK(hipMemcpyAsync(xu.data(), stage_b.p, sizeof(float) * xu.size(), hipMemcpyDeviceToHost, wst));
+    HIPCHK(hipStreamSynchronize(wst));
+    // straight into the unit store at the same slots (labels = slots): a batch with a repeated id keeps
+    // its rows out of slot order, so the unit index's own append order could differ
+    FlatIndex &u = *unit;
+    int64_t next = u.st.n;
+    for (int64_t s : slots) next = std::max(next, s + 1);
+    u.st.reserve(next, u.wst);
+    u.st.hlabels.resize(next, -1);
+    u.st.hlive.resize(next, 0);
+    u.st.write(xu.data(), slots.data(), slots.data(), n, u.wst, u.stage_x, u.stage_i);
+    for (int64_t s : slots) {
+      u.st.hlabels[s] = s;
+      u.st.hlive[s] = 1;
+      u.slot_of[s] = s;
+    }
+    u.st.n = next;
   }
 
   void set_quantization(bool on) override { quant = on; }
   void reserve(int64_t rows) override {
     st.reserve(st.n + rows, wst);
     slot_of.reserve(slot_of.size() + (size_t)rows);
+    if (unit) unit->reserve(rows);
   }
 
   void q8_reserve() {
@@ -803,6 +844,7 @@ struct FlatIndex : Index {
       launch_scatter_u8(q8ok.as<uint8_t>(), stage_i.as<int64_t>(), 0, n, wst);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(wst));
+    unit_write(n, slots);  // (stage_i: the slots; the unit index appends new slots in the same order)
     for (int64_t i = 0; i < n; i++) {
       st.hlabels[slots[i]] = labels[i];
       st.hlive[slots[i]] = 1;
@@ -867,6 +909,7 @@ struct FlatIndex : Index {
       slot_of.erase(f);
     }
     st.set_live(dead, 0, wst, stage_b);
+    if (unit && !dead.empty()) unit->remove(dead.data(), (int64_t)dead.size(), nullptr);
   }
 
   void search(const float *d_q, int64_t nq, int k, const pyr_search_params &prm, float *d_s, int64_t *d_l,
@@ -899,7 +942,70 @@ struct FlatIndex : Index {
       search_filter(d_q, nq, k, k1, cutoff, d_s, d_l, d_c, ws);
       return;
     }
+    if (unit && filter_enabled() && k <= KMAX_FAST && k1 > 0 && filter_supported(dim, L2, k1)) {
+      search_cosine(d_q, nq, k, k1, prm, cutoff, d_s, d_l, d_c, ws);
+      return;
+    }
     search_exact(d_q, nq, k, cutoff, d_s, d_l, d_c, ws);
+  }
+
+  // Cosine (:339-354): the unit index's exact L2 top-K2 (K2 = K1 - margin >= k, the same
+  // filter capacity k would use) of the unit queries, then the exact Cosine of those candidates, ranked
+  // and certified (filter.hip cos_rerank_kernel); failures re-run the exact scan
+  void search_cosine(const float *d_q, int64_t nq, int k, int k1, const pyr_search_params &prm, int64_t cutoff,
+                     float *d_s, int64_t *d_l, int32_t *d_c, Workspace &ws) {
+    // PYR_COS_EXTRA: candidates beyond the filter capacity k itself uses (measurement knob)
+    const char *ce = getenv("PYR_COS_EXTRA");
+    if (ce && atoi(ce) > 0) k1 = std::max(k1, filter_k1(k + atoi(ce)));
+    if (k1 <= 0) k1 = filter_k1(k);
+    const int kc = std::max(k, k1 - 4);
+    ws.qn.ensure(sizeof(float) * std::max<int64_t>(nq, 1));
+    launch_norms(d_q, nq, dim, 0, ws.qn.as<float>(), ws.st);  // VectorMath.ComputeNorm (:339)
+    ws.cq.ensure(sizeof(float) * nq * dim);
+    launch_unit_rows(d_q, nullptr, ws.qn.as<float>(), nq, dim, ws.cq.as<float>(), ws.st);
+    ws.ccs.ensure(sizeof(float) * nq * kc);
+    ws.ccl.ensure(sizeof(int64_t) * nq * kc);
+    ws.ccc.ensure(sizeof(int32_t) * nq);
+    {
+      std::shared_lock<std::shared_mutex> g(unit->mu);
+      unit->search(ws.cq.as<float>(), nq, kc, prm, ws.ccs.as<float>(), ws.ccl.as<int64_t>(), ws.ccc.as<int32_t>(), ws);
+    }
+    ws.fail.ensure(sizeof(int32_t) * nq);
+    ws.fail_cnt.ensure(sizeof(int32_t));
+    HIPCHK(hipMemsetAsync(ws.fail_cnt.p, 0, sizeof(int32_t), ws.st));
+    CosRerankArgs r{};
+    r.rows = st.rows.as<float>();
+    r.rows_rm = st.f16 ? st.rrm.as<float>() : nullptr;
+    r.rnorm = st.norms.as<float>();
+    r.row_labels = st.labels.as<int64_t>();
+    r.max_rsq = st.rmax.as<uint32_t>();
+    r.zflag = zflag.as<uint32_t>();
+    r.queries = d_q;
+    r.qnorm = ws.qn.as<float>();
+    r.cand_s = ws.ccs.as<float>();
+    r.cand_l = ws.ccl.as<int64_t>();
+    r.cand_c = ws.ccc.as<int32_t>();
+    r.kc = kc;
+    r.k = k;
+    r.dim = dim;
+    r.nq = nq;
+    r.out_s = d_s;
+    r.out_l = d_l;
+    r.out_c = d_c;
+    r.fail_list = ws.fail.as<int32_t>();
+    r.fail_cnt = ws.fail_cnt.as<int32_t>();
+    {
+      PhaseTimer t(PH_REFINE, ws.st, nq * kc);
+      launch_cos_rerank(r, ws.st);
+    }
+    HIPCHK(hipGetLastError());
+    int32_t nf = 0;
+    HIPCHK(hipMemcpyAsync(&nf, ws.fail_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, ws.st));
+    HIPCHK(hipStreamSynchronize(ws.st));
+    filter_fallback(ws, nf, d_q, dim, k, d_s, d_l, d_c,
+                    [&](const float *q2, int64_t n2, float *s2, int64_t *l2, int32_t *c2) {
+                      search_exact(q2, n2, k, cutoff, s2, l2, c2, ws.nested());
+                    });
   }
 
   // MFMA candidate filter over slots [0, cutoff), exact refine with the *Unsafe form (V = 4)
@@ -1029,6 +1135,7 @@ struct FlatIndex : Index {
     HIPCHK(hipStreamSynchronize(wst));
     st.clear();
     slot_of.clear();
+    if (unit) unit_reset();
     if (n) add(rows.data(), n, labels.data(), false);  // codes iff EnableQuantization now (:166-178)
   }
 };

@@ -26,6 +26,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 
@@ -719,6 +720,105 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
   }
 }
 
+// ---- Cosine on the filter path (BruteForceVectorIndex.cs:354) ----
+// The candidates come from an exact L2 search of the unit queries q^ = q * (1 / |q|) over the unit rows
+// x^ (an L2 FLAT index over the same slots, its labels = the slots; its fp16 tiles are centred on the
+// unit rows' mean, so the filter's error is relative to the residuals).  On unit vectors the L2 order
+// is the cosine order: 1 - |q^ - x^|^2 / 2 = q^.x^.  Its scores s_j = -L2SquaredUnsafe(q^, x^) are
+// exact, so p_j = 1 + s_j / 2 <= p_K2 for every row left out.  With cos_j the real-arithmetic cosine
+// and u = 2^-24:
+//   ComputeNorm (VectorMath.cs:72-99) sums non-negative squares in 8 lanes of D/8 terms, a 3-level
+//   tree and a scalar tail: relative error <= (D/8 + 8) u, so the norm's <= (D/16 + 5) u, and a unit
+//   component x_i * fl(1 / |x|) is within e = (D/16 + 7) u of x_i / |x|;
+//   |q^|^2, |x^|^2 are within 2e of 1 and q^.x^ within 2e of cos_j, so 1 - |q^ - x^|^2 / 2 is within
+//   4e of cos_j; L2SquaredUnsafe adds non-negative terms (4 x 8 lanes, trees, tails): relative error
+//   <= (D/8 + 18) u of a distance <= 4.1, i.e. (D/4 + 37) u in p;  |p_j - cos_j| <= (D/2 + 66) u;
+//   the reference Cosine dot / (|q| |x|) (DotProductUnsafe, within (D/8 + 16) u sum |q_i x_i|) is
+//   within (D/4 + 28) u of cos_j.
+// A row left out therefore has a reference score <= p_K2 + (3D/4 + 94) u, and the exact top-k of the
+// candidates is the search's when the k-th exact score exceeds p_K2 + E, E = (2D + 256) u.  A row with
+// a norm below 1e-6 scores 0 (VectorMath.cs:105) but sits at unit distance (x^ = 0): once the store has
+// held such a row (zflag) the k-th score must also exceed 0.  A query with a zero or non-finite norm,
+// or a store holding a non-finite row, fails the certificate.
+template <int DT>
+__global__ __launch_bounds__(256) void cos_rerank_kernel(CosRerankArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= a.nq) return;
+  const int D = DT > 0 ? DT : a.dim, kc = a.kc, k = a.k;
+  const float *qp = a.queries + (size_t)q * D;
+  const float qn = a.qnorm[q];
+  const int ccount = a.cand_c[q];
+  uint32_t key = KEY_NONE;
+  if (lane < kc && lane < ccount && a.cand_l[(size_t)q * kc + lane] >= 0) key = (uint32_t)a.cand_l[(size_t)q * kc + lane];
+  float s = -INFINITY;
+  for (int p = 0; 8 * p < kc; ++p) {
+    const int c = 8 * p + (lane >> 3);
+    const int32_t kk = __shfl((int)key, c);
+    const int64_t rk = kk >= 0 ? (int64_t)kk : 0;
+    const float dot = a.rows_rm ? exact_score_l8<4, IP, DT, true>(qp, a.rows_rm, rk, D, lane & 7)
+                                : exact_score_l8<4, IP, DT, false>(qp, a.rows, rk, D, lane & 7);
+    const float xn = a.rnorm[rk];
+    const float sc = (qn < 1e-6f || xn < 1e-6f) ? 0.0f : dot / (qn * xn);
+    const float t = __shfl(sc, 8 * (lane & 7));
+    if ((lane >> 3) == p && key != KEY_NONE) s = t;
+  }
+  int rank = 0, valid = 0;
+  for (int c = 0; c < kc; ++c) {
+    const float sc = __shfl(s, c);
+    const uint32_t kk = __shfl(key, c);
+    if (kk == KEY_NONE) continue;
+    ++valid;
+    if (key != KEY_NONE && better(sc, kk, s, key)) ++rank;
+  }
+  const int nout = min(valid, k);
+  if (key != KEY_NONE && rank < k) {
+    a.out_s[(size_t)q * k + rank] = s;
+    a.out_l[(size_t)q * k + rank] = a.row_labels[key];
+  }
+  if (lane >= nout && lane < k) {
+    a.out_s[(size_t)q * k + lane] = -INFINITY;
+    a.out_l[(size_t)q * k + lane] = -1;
+  }
+  bool ok = true;
+  if (ccount >= kc) {  // rows were left out: the margin against the K2-th inner product
+    float skth = -INFINITY;
+    for (int c = 0; c < kc; ++c) {
+      const int rc = __shfl(rank, c);
+      const uint32_t kk = __shfl(key, c);
+      const float sc = __shfl(s, c);
+      if (kk != KEY_NONE && rc == k - 1) skth = sc;
+    }
+    const double u = 5.9604644775390625e-8;  // 2^-24
+    const double pk = 1.0 + 0.5 * (double)a.cand_s[(size_t)q * kc + kc - 1];
+    ok = nout == k && (double)skth > pk + (2.0 * D + 256.0) * u;
+    if (a.zflag && *a.zflag != 0u && !(skth > 0.0f)) ok = false;
+  }
+  if (!(qn >= 1e-6f) || !isfinite(qn) || (a.max_rsq && a.max_rsq[1] != 0u)) ok = false;
+  if (lane == 0) {
+    if (a.out_c) a.out_c[q] = nout;
+    if (!ok) a.fail_list[atomicAdd(a.fail_cnt, 1)] = (int32_t)q;
+  }
+}
+
+// unit vectors: out row i = x_i * (1 / n_i), or 0 when n_i < 1e-6 (the reference's zero-norm rule) or
+// n_i is not finite.  blocked: rows of a blocked store at slots[i] (norms indexed by slot), else
+// row-major x with norms[i].
+__global__ void unit_rows_kernel(const float *x, const int64_t *slots, const float *norms, int64_t n, int D,
+                                 float *out, uint32_t *zflag) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * D;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = e / D;
+    const int d = (int)(e % D);
+    const int64_t r = slots ? slots[i] : i;
+    const float nr = norms[r];
+    const float v = slots ? x[blk_off(r, d, D)] : x[e];
+    const bool unit = nr >= 1e-6f && isfinite(nr);
+    out[e] = unit ? v * (1.0f / nr) : 0.0f;
+    if (zflag && d == 0 && !unit) *zflag = 1u;
+  }
+}
+
 // result rows of the exact re-run (sub-batch order) back to their queries
 __global__ void scatter_results_kernel(const int32_t *qidx, int64_t n, int k, const float *ss, const int64_t *sl,
                                        const int32_t *sc, float *out_s, int64_t *out_l, int32_t *out_c) {
@@ -835,6 +935,25 @@ void launch_filter(const FilterArgs &a, int metric, int max_items, hipStream_t s
     case 64: launch_filter_d<64>(a, metric, max_items, st); return;
     default: launch_filter_d<128>(a, metric, max_items, st); return;
   }
+}
+
+void launch_cos_rerank(const CosRerankArgs &a, hipStream_t st) {
+  if (a.nq <= 0) return;
+  const dim3 g(nblk(a.nq, 4)), b(256);
+  switch (a.dim) {
+    case 32: hipLaunchKernelGGL(cos_rerank_kernel<32>, g, b, 0, st, a); return;
+    case 64: hipLaunchKernelGGL(cos_rerank_kernel<64>, g, b, 0, st, a); return;
+    case 128: hipLaunchKernelGGL(cos_rerank_kernel<128>, g, b, 0, st, a); return;
+    default: hipLaunchKernelGGL(cos_rerank_kernel<0>, g, b, 0, st, a); return;
+  }
+}
+
+void launch_unit_rows(const float *x, const int64_t *slots, const float *norms, int64_t n, int32_t dim, float *out,
+                      hipStream_t st, uint32_t *zflag) {
+  if (n <= 0) return;
+  const int64_t blocks = std::min<int64_t>((n * dim + 255) / 256, int64_t(1) << 22);
+  hipLaunchKernelGGL(unit_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, slots, norms, n, dim, out,
+                     zflag);
 }
 
 void launch_refine(const RefineArgs &a, int metric, int V, hipStream_t st) {

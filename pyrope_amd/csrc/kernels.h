@@ -459,6 +459,34 @@ struct RefineArgs {
   int32_t *fail_list;       // queries whose certificate failed
   int32_t *fail_cnt;
 };
+// Cosine on the filter path (filter.hip cos_rerank_kernel): candidates = the exact L2 top-kc of the unit
+// queries over the unit rows (cand_l: slots, cand_s: their scores -|q^ - x^|^2 desc, cand_c: count);
+// exact Cosine (BruteForceVectorIndex.cs:354) of each, top-k, certificate -> fail_list
+struct CosRerankArgs {
+  const float *rows;        // blocked store (the slots index it)
+  const float *rows_rm;     // its row-major copy, or null
+  const float *rnorm;       // ComputeNorm per slot
+  const int64_t *row_labels;
+  const uint32_t *max_rsq;  // the store's rmax pair ([1] != 0: a non-finite row), or null
+  const uint32_t *zflag;    // != 0 once a row with a norm below 1e-6 was written, or null
+  const float *queries;     // raw queries, row-major nq x D
+  const float *qnorm;       // ComputeNorm per query
+  const float *cand_s;
+  const int64_t *cand_l;
+  const int32_t *cand_c;
+  int32_t kc, k, dim;
+  int64_t nq;
+  float *out_s;
+  int64_t *out_l;
+  int32_t *out_c;
+  int32_t *fail_list;
+  int32_t *fail_cnt;
+};
+void launch_cos_rerank(const CosRerankArgs &a, hipStream_t st);
+// unit rows (x / n, 0 when n < 1e-6 or not finite): blocked rows at slots (norms by slot), or row-major
+// x (norms[i]) when slots is null; out row-major n x dim; zflag (may be null) set to 1 by a zero row
+void launch_unit_rows(const float *x, const int64_t *slots, const float *norms, int64_t n, int32_t dim, float *out,
+                      hipStream_t st, uint32_t *zflag = nullptr);
 bool filter_supported(int dim, int metric, int k1);
 int filter16_max_rows();  // rows per scan item the fp16 filter accepts
 bool filter16_supported(int dim, int metric, int k1);
