@@ -127,7 +127,9 @@ pyr_status pyr_index_search(pyr_index *index, const float *q, int64_t nq, int32_
  * turns it off (the default). */
 pyr_status pyr_index_set_coalescing(pyr_index *index, int32_t max_batch, int32_t max_wait_us);
 /* Same on device-resident buffers (HBM), enqueued on `stream` (hipStream_t, NULL = default).
- * Does not synchronize the stream. */
+ * On a built IVF_FLAT index with an empty buffer (the stream scan: L2 / IP / Cosine, d = 32 / 64 / 128)
+ * it only enqueues work: no host synchronisation, capturable into a hipGraph.  The FLAT filter and
+ * the exact / PQ paths may synchronize `stream` once to size the re-run of certificate failures. */
 pyr_status pyr_index_search_device(pyr_index *index, const float *d_q, int64_t nq, int32_t k,
                                    const pyr_search_params *params, float *d_scores, int64_t *d_labels,
                                    int32_t *d_counts, void *stream);

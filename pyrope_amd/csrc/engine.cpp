@@ -1509,6 +1509,9 @@ struct IvfFlatIndex : Index {
   DevMem dlb, dle, dllive;
   DevMem dlmax;                           // per-list max |x|^2 (score_key): refine certificate bound
   DevMem dlmax_r;                         // per-list max |x - c|^2 (residual fp16 tiles)
+  // Cosine: the fp16 tiles hold unit residuals x/|x| - c/|c| (ucents: the unit centroids) scanned as L2
+  // (on unit vectors the L2 order is the cosine order); zflag: a list row with a norm below 1e-6
+  DevMem ucents, zflag;
   void reserve(int64_t rows) override { buf.reserve(rows, wst); }
   Coarse coarse;
   bool built = false;                     // _isBuilt (:20)
@@ -1665,8 +1668,9 @@ struct IvfFlatIndex : Index {
     RowStore nl;
     nl.dim = dim;
     nl.cosine = metric == COS;
-    nl.f16 = store16(dim, metric);
-    nl.met16 = metric;
+    const bool unit = metric == COS && store16(dim, L2);
+    nl.f16 = unit || store16(dim, metric);
+    nl.met16 = unit ? L2 : metric;
     nl.reserve(std::max<int64_t>(tot, 32), wst);
     DevMem dsr;
     dsr.ensure(sizeof(int64_t) * tot);
@@ -1691,18 +1695,37 @@ struct IvfFlatIndex : Index {
       HIPCHK(hipMemcpyAsync(dtl.p, tl.data(), sizeof(int32_t) * tl.size(), hipMemcpyHostToDevice, wst));
       nl.resid = true;
       nl.rsq16.ensure(sizeof(float) * nl.cap);
-      launch_resid_sq(nl.rows.as<float>(), nl.cap, dim, C, dtl.as<int32_t>(), nl.rsq16.as<float>(), wst);
+      // Cosine: tiles of the unit rows x/|x| (0 below the 1e-6 norm rule) around the unit centroids
+      const float *TR = nl.rows.as<float>(), *TC = C;
+      DevMem urm, ublk, cn;
+      if (unit) {
+        zflag.ensure(sizeof(uint32_t));
+        HIPCHK(hipMemsetAsync(zflag.p, 0, sizeof(uint32_t), wst));
+        urm.ensure(sizeof(float) * nl.cap * dim);
+        ublk.ensure(sizeof(float) * nl.cap * dim);
+        launch_unit_rows(nl.rrm.as<float>(), nullptr, nl.norms.as<float>(), tot, dim, urm.as<float>(), wst,
+                         zflag.as<uint32_t>(), nl.live.as<uint8_t>());
+        HIPCHK(hipMemsetAsync(ublk.p, 0, sizeof(float) * nl.cap * dim, wst));
+        launch_to_blocked(urm.as<float>(), nullptr, tot, dim, ublk.as<float>(), 0, wst);
+        cn.ensure(sizeof(float) * k);
+        launch_norms(C, k, dim, 0, cn.as<float>(), wst);
+        ucents.ensure(sizeof(float) * k * dim);
+        launch_unit_rows(C, nullptr, cn.as<float>(), k, dim, ucents.as<float>(), wst);
+        TR = ublk.as<float>();
+        TC = ucents.as<float>();
+      }
+      launch_resid_sq(TR, nl.cap, dim, TC, dtl.as<int32_t>(), nl.rsq16.as<float>(), wst);
       HIPCHK(hipMemsetAsync(nl.amaxd.p, 0, sizeof(uint32_t), wst));
-      launch_absmax(nl.rows.as<float>(), nullptr, nl.cap, dim, nl.amaxd.as<uint32_t>(), wst, C, dtl.as<int32_t>());
+      launch_absmax(TR, nullptr, nl.cap, dim, nl.amaxd.as<uint32_t>(), wst, TC, dtl.as<int32_t>());
       uint32_t bits = 0;
       HIPCHK(hipMemcpyAsync(&bits, nl.amaxd.p, sizeof(bits), hipMemcpyDeviceToHost, wst));
       HIPCHK(hipStreamSynchronize(wst));
       std::memcpy(&nl.amax, &bits, sizeof(bits));
       nl.sx = pow2_scale_host(nl.amax);
-      launch_encode16(nl.rows.as<float>(), nullptr, nl.cap, dim, nl.sx, nl.h16.p, wst, C, dtl.as<int32_t>(),
-                      nl.rsq16.as<float>());
-      launch_meta16(nullptr, nl.cap, metric, nl.rsq16.as<float>(), nl.live.as<uint8_t>(), nl.meta.as<float>(), wst);
+      launch_encode16(TR, nullptr, nl.cap, dim, nl.sx, nl.h16.p, wst, TC, dtl.as<int32_t>(), nl.rsq16.as<float>());
+      launch_meta16(nullptr, nl.cap, nl.met16, nl.rsq16.as<float>(), nl.live.as<uint8_t>(), nl.meta.as<float>(), wst);
       HIPCHK(hipGetLastError());
+      HIPCHK(hipStreamSynchronize(wst));  // urm / ublk / cn are freed at the end of this block
     }
     HIPCHK(hipStreamSynchronize(wst));
     nl.n = tot;
@@ -1768,6 +1791,13 @@ struct IvfFlatIndex : Index {
     if (filter_enabled() && probes > 0 && buf.live_count() == 0 && prm.max_scans < 0 && k <= KMAX_FAST &&
         probes < MAX_PARTS && filter_supported(dim, metric, k1)) {
       search_filter(d_q, nq, k, k1, probes, d_s, d_l, d_c, ws);
+      return;
+    }
+    // Cosine: the stream scan over the unit residual tiles (commit_lists), exact Cosine in the refine
+    if (metric == COS && filter_enabled() && probes > 0 && buf.live_count() == 0 && prm.max_scans < 0 &&
+        k <= KMAX_FAST && probes < MAX_PARTS && k1 > 0 && stream_enabled() && prec16(filter_prec()) && lists.f16 &&
+        lists.resid && lists.met16 == L2 && stream16_supported(dim, L2, k1)) {
+      search_stream(d_q, nq, k, k1, probes, d_s, d_l, d_c, ws);
       return;
     }
     search_exact(d_q, nq, k, prm, d_s, d_l, d_c, ws);
@@ -2011,9 +2041,22 @@ struct IvfFlatIndex : Index {
 
   void stream_slice(const float *d_q, int64_t nq, int k, int k1, int probes, IvfChunking ch, int nparts, int cap,
                     bool q2, float *d_s, int64_t *d_l, int32_t *d_c, Workspace &ws) {
+    const bool cosine = metric == COS;
+    const int met = cosine ? L2 : metric;  // Cosine: L2 over the unit vectors (commit_lists)
+    if (cosine) {
+      ws.qn.ensure(sizeof(float) * std::max<int64_t>(nq, 1));
+      launch_norms(d_q, nq, dim, 0, ws.qn.as<float>(), ws.st);  // VectorMath.ComputeNorm (:167)
+    }
     {
       PhaseTimer t(PH_COARSE, ws.st, nq * coarse.nlist);
-      coarse.probe(d_q, nullptr, nq, probes, metric, ws);  // exact coarse ranking (ComputeScore, :186-198)
+      // exact coarse ranking (ComputeScore, :186-198)
+      coarse.probe(d_q, cosine ? ws.qn.as<float>() : nullptr, nq, probes, metric, ws);
+    }
+    const float *d_qs = d_q;  // the queries the scan scores: the unit queries for Cosine
+    if (cosine) {
+      ws.cq.ensure(sizeof(float) * nq * dim);
+      launch_unit_rows(d_q, nullptr, ws.qn.as<float>(), nq, dim, ws.cq.as<float>(), ws.st);
+      d_qs = ws.cq.as<float>();
     }
     const int qmax = stream16_qmax(q2);
     int maxi;
@@ -2040,8 +2083,8 @@ struct IvfFlatIndex : Index {
     StreamArgs sa{};
     sa.h16 = lists.h16.p;
     sa.meta = lists.meta.as<float>();
-    sa.queries = d_q;
-    sa.cents = coarse.rm.as<float>();
+    sa.queries = d_qs;
+    sa.cents = cosine ? ucents.as<float>() : coarse.rm.as<float>();
     sa.sx = lists.sx;
     sa.items = ws.items.as<ScanItem>();
     sa.n_items = ws.nitems.as<int32_t>();
@@ -2068,12 +2111,12 @@ struct IvfFlatIndex : Index {
     const int prec = q2 ? FILTER_F16X2 : FILTER_F16X1;
     sa.rsq16 = lists.rsq16.as<float>();
     sa.rsq = lists.rsq.as<float>();
-    stream_ub_terms(dim, metric, filter_f16_cerr(dim, metric, prec), filter_cerr(dim),
-                    filter_f16_abs(dim, metric, lists.sx, prec), sa);
+    stream_ub_terms(dim, met, filter_f16_cerr(dim, met, prec), filter_cerr(dim), filter_f16_abs(dim, met, lists.sx, prec),
+                    sa);
     {
       PhaseTimer t(PH_SAMPLE, ws.st);
-      launch_stream_prep(sa, metric, maxi, ws.st);
-      launch_stream_scan(sa, metric, maxi, true, ws.st);
+      launch_stream_prep(sa, met, maxi, ws.st);
+      launch_stream_scan(sa, met, maxi, true, ws.st);
       StreamSelectArgs sel{};
       sel.samp = ws.ssamp.as<float>();
       sel.nq = nq;
@@ -2089,7 +2132,7 @@ struct IvfFlatIndex : Index {
     sa.work = ws.swork.as<int32_t>() + 1;
     {
       PhaseTimer t(PH_LIST_SCAN, ws.st, prof().on ? probed_rows(ws, nq, probes, le, lb) : 0);
-      launch_stream_scan(sa, metric, maxi, false, ws.st);
+      launch_stream_scan(sa, met, maxi, false, ws.st);
     }
     HIPCHK(hipGetLastError());
     ws.ms.ensure(sizeof(float) * nq * STREAM_KO);
@@ -2133,13 +2176,19 @@ struct IvfFlatIndex : Index {
     r.k = k;
     r.dim = dim;
     r.c_err = filter_cerr(dim);
-    r.c_bf = filter_f16_cerr(dim, metric, prec);
+    r.c_bf = filter_f16_cerr(dim, met, prec);
     r.ub = 1;
-    r.c_abs = filter_f16_abs(dim, metric, lists.sx, prec);
+    r.c_abs = filter_f16_abs(dim, met, lists.sx, prec);
     r.q16 = 1;
     r.resid = 1;
-    r.cents = coarse.rm.as<float>();
+    r.cents = cosine ? ucents.as<float>() : coarse.rm.as<float>();
     r.list_rmax_r = dlmax_r.as<uint32_t>();
+    if (cosine) {
+      r.cosine = 1;
+      r.qnorm = ws.qn.as<float>();
+      r.rnorm = lists.norms.as<float>();
+      r.zflag = zflag.as<uint32_t>();
+    }
     r.out_s = d_s;
     r.out_l = d_l;
     r.out_c = d_c;
@@ -2149,14 +2198,14 @@ struct IvfFlatIndex : Index {
       r.k1 = k1;
       r.fail_list = ws.fail2.as<int32_t>();
       r.fail_cnt = ws.fail_cnt2.as<int32_t>();
-      launch_refine(r, metric, 1, ws.st);
+      launch_refine(r, met, 1, ws.st);
       if (k1 < STREAM_KO && k + 4 <= STREAM_KO) {
         r.k1 = STREAM_KO;
         r.qsel = ws.fail2.as<int32_t>();
         r.nsel = ws.fail_cnt2.as<int32_t>();
         r.fail_list = ws.fail.as<int32_t>();
         r.fail_cnt = ws.fail_cnt.as<int32_t>();
-        launch_refine(r, metric, 1, ws.st);
+        launch_refine(r, met, 1, ws.st);
       } else {
         HIPCHK(hipMemcpyAsync(ws.fail.p, ws.fail2.p, sizeof(int32_t) * nq, hipMemcpyDeviceToDevice, ws.st));
         HIPCHK(hipMemcpyAsync(ws.fail_cnt.p, ws.fail_cnt2.p, sizeof(int32_t), hipMemcpyDeviceToDevice, ws.st));
@@ -2185,6 +2234,10 @@ struct IvfFlatIndex : Index {
     ra.nfail = ws.fail_cnt.as<int32_t>();
     ra.dim = dim;
     ra.k = k;
+    if (cosine) {
+      ra.qnorm = ws.qn.as<float>();
+      ra.rnorm = lists.norms.as<float>();
+    }
     ra.out_s = d_s;
     ra.out_l = d_l;
     ra.out_c = d_c;

@@ -555,8 +555,16 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
     const int c = 8 * p + (lane >> 3);
     const int32_t kc = __shfl((int)key, c);  // (k1 <= 64: every candidate's key sits on lane c)
     const int64_t rk = kc >= 0 ? (int64_t)kc : 0;
-    const float sc = a.rows_rm ? exact_score_l8<V, MET, DT, true>(qp, a.rows_rm, rk, D, lane & 7)
-                               : exact_score_l8<V, MET, DT, false>(qp, a.rows, rk, D, lane & 7);
+    float sc;
+    if (MET == L2 && a.cosine) {  // VectorMath.Cosine (:102-109) with the cached norms
+      const float dot = a.rows_rm ? exact_score_l8<V, IP, DT, true>(qp, a.rows_rm, rk, D, lane & 7)
+                                  : exact_score_l8<V, IP, DT, false>(qp, a.rows, rk, D, lane & 7);
+      const float qn = a.qnorm[q], xn = a.rnorm[rk];
+      sc = (qn < 1e-6f || xn < 1e-6f) ? 0.0f : dot / (qn * xn);
+    } else {
+      sc = a.rows_rm ? exact_score_l8<V, MET, DT, true>(qp, a.rows_rm, rk, D, lane & 7)
+                     : exact_score_l8<V, MET, DT, false>(qp, a.rows, rk, D, lane & 7);
+    }
     const float t = __shfl(sc, 8 * (lane & 7));
     if ((lane >> 3) == p && key != KEY_NONE) s = t;
   }
@@ -593,7 +601,16 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
     if (a.resid && a.ub) {
       // upper-bound candidates (stream16.hip, stream_ub_terms): every row left out -- below T_q, a
       // region's floor, or merged below the K1-th -- has a reference score at most the K1-th entry
-      ok = nout == k && skth > ms[k1 - 1];
+      if (MET == L2 && a.cosine) {
+        // the bounds are L2 scores s of the unit vectors: 1 + s / 2 bounds q^.x^, within (D/2 + 66) u of
+        // the real cosine, the reference Cosine within (D/4 + 28) u of it (cos_rerank_kernel)
+        const double pk = 1.0 + 0.5 * (double)ms[k1 - 1];
+        const float qn = a.qnorm[q];
+        ok = nout == k && (double)skth > pk + (2.0 * D + 256.0) * u && qn >= 1e-6f && isfinite(qn) &&
+             !(a.max_rsq && a.max_rsq[1] != 0u) && !(a.zflag && *a.zflag != 0u && !(skth > 0.0f));
+      } else {
+        ok = nout == k && skth > ms[k1 - 1];
+      }
       if (lane == 0) {
         if (a.out_c) a.out_c[q] = nout;
         if (!ok) a.fail_list[atomicAdd(a.fail_cnt, 1)] = (int32_t)q;
@@ -805,7 +822,7 @@ __global__ __launch_bounds__(256) void cos_rerank_kernel(CosRerankArgs a) {
 // n_i is not finite.  blocked: rows of a blocked store at slots[i] (norms indexed by slot), else
 // row-major x with norms[i].
 __global__ void unit_rows_kernel(const float *x, const int64_t *slots, const float *norms, int64_t n, int D,
-                                 float *out, uint32_t *zflag) {
+                                 float *out, uint32_t *zflag, const uint8_t *live) {
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * D;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t i = e / D;
@@ -815,7 +832,7 @@ __global__ void unit_rows_kernel(const float *x, const int64_t *slots, const flo
     const float v = slots ? x[blk_off(r, d, D)] : x[e];
     const bool unit = nr >= 1e-6f && isfinite(nr);
     out[e] = unit ? v * (1.0f / nr) : 0.0f;
-    if (zflag && d == 0 && !unit) *zflag = 1u;
+    if (zflag && d == 0 && !unit && (!live || live[r])) *zflag = 1u;
   }
 }
 
@@ -949,11 +966,11 @@ void launch_cos_rerank(const CosRerankArgs &a, hipStream_t st) {
 }
 
 void launch_unit_rows(const float *x, const int64_t *slots, const float *norms, int64_t n, int32_t dim, float *out,
-                      hipStream_t st, uint32_t *zflag) {
+                      hipStream_t st, uint32_t *zflag, const uint8_t *live) {
   if (n <= 0) return;
   const int64_t blocks = std::min<int64_t>((n * dim + 255) / 256, int64_t(1) << 22);
   hipLaunchKernelGGL(unit_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, slots, norms, n, dim, out,
-                     zflag);
+                     zflag, live);
 }
 
 void launch_refine(const RefineArgs &a, int metric, int V, hipStream_t st) {

@@ -161,6 +161,8 @@ struct IvfRerunArgs {
   const int32_t *fail, *nfail;
   int32_t dim, k;
   int32_t nchunk;           // most chunks a probed list is cut into (>= 1; few failures use them all)
+  const float *qnorm;       // Cosine: ComputeNorm per query and per row
+  const float *rnorm;
   float *out_s;
   int64_t *out_l;
   int32_t *out_c;
@@ -453,6 +455,11 @@ struct RefineArgs {
   const uint32_t *list_rmax_r;
   int32_t resid;
   int32_t ub;               // resid: candidate scores are upper bounds (StreamArgs kr ..): no error term
+  // Cosine over unit residual tiles (ub): the candidates' bounds are L2 scores s of the unit vectors;
+  // exact scores are VectorMath.Cosine(q, x, |q|, |x|), certified against 1 + s_K1 / 2 + (2D + 256) u
+  int32_t cosine;
+  const float *qnorm, *rnorm;
+  const uint32_t *zflag;    // != 0 once a row with a norm below 1e-6 was stored (k-th score must be > 0)
   float *out_s;
   int64_t *out_l;
   int32_t *out_c;
@@ -484,9 +491,10 @@ struct CosRerankArgs {
 };
 void launch_cos_rerank(const CosRerankArgs &a, hipStream_t st);
 // unit rows (x / n, 0 when n < 1e-6 or not finite): blocked rows at slots (norms by slot), or row-major
-// x (norms[i]) when slots is null; out row-major n x dim; zflag (may be null) set to 1 by a zero row
+// x (norms[i]) when slots is null; out row-major n x dim; zflag (may be null) set to 1 by a zero row that
+// is live (live: per row index, null = every row)
 void launch_unit_rows(const float *x, const int64_t *slots, const float *norms, int64_t n, int32_t dim, float *out,
-                      hipStream_t st, uint32_t *zflag = nullptr);
+                      hipStream_t st, uint32_t *zflag = nullptr, const uint8_t *live = nullptr);
 bool filter_supported(int dim, int metric, int k1);
 int filter16_max_rows();  // rows per scan item the fp16 filter accepts
 bool filter16_supported(int dim, int metric, int k1);

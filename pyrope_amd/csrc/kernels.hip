@@ -1696,8 +1696,17 @@ __global__ __launch_bounds__(256) void ivf_rerun_scan_kernel(IvfRerunArgs a, uin
         uint64_t key = 0ull;
         if (r < ce && a.live[r]) {
           float sc;
-          if constexpr (DT > 0) sc = rr_score<MET, DT>(qsh, a.rows, r);
-          else sc = em_score<1, MET>(Lin{qp}, Blk{a.rows, D, r}, D, 0.0f, 0.0f);
+          if constexpr (MET == COS) {  // VectorMath.Cosine (:102-109) with the cached norms
+            const float qn = a.qnorm[q], xn = a.rnorm[r];
+            float dot;
+            if constexpr (DT > 0) dot = rr_score<IP, DT>(qsh, a.rows, r);
+            else dot = em_score<1, IP>(Lin{qp}, Blk{a.rows, D, r}, D, 0.0f, 0.0f);
+            sc = (qn < 1e-6f || xn < 1e-6f) ? 0.0f : dot / (qn * xn);
+          } else if constexpr (DT > 0) {
+            sc = rr_score<MET, DT>(qsh, a.rows, r);
+          } else {
+            sc = em_score<1, MET>(Lin{qp}, Blk{a.rows, D, r}, D, 0.0f, 0.0f);
+          }
           if (!isnan(sc)) key = rr_key(sc, (uint32_t)r);  // NaN never ranks (as better() in the scans)
         }
         const uint64_t kth = rr_shfl64(cur, k - 1);
@@ -2107,13 +2116,23 @@ void launch_ivf_exact_rerun(const IvfRerunArgs &a, int metric, int64_t max_fail,
   if (max_fail <= 0 || a.k <= 0 || a.k > 64 || a.nprobe <= 0 || a.nchunk <= 0) return;
   const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(max_fail * a.nprobe, 2 * RR_UNITS), 2048);
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, a, part); };
-  const bool l2 = metric == L2;
-  switch (a.dim) {
-    case 32: l2 ? go(ivf_rerun_scan_kernel<L2, 32>) : go(ivf_rerun_scan_kernel<IP, 32>); break;
-    case 64: l2 ? go(ivf_rerun_scan_kernel<L2, 64>) : go(ivf_rerun_scan_kernel<IP, 64>); break;
-    case 128: l2 ? go(ivf_rerun_scan_kernel<L2, 128>) : go(ivf_rerun_scan_kernel<IP, 128>); break;
-    default: l2 ? go(ivf_rerun_scan_kernel<L2, 0>) : go(ivf_rerun_scan_kernel<IP, 0>); break;
-  }
+  auto by_dim = [&](auto k32, auto k64, auto k128, auto k0) {
+    switch (a.dim) {
+      case 32: go(k32); break;
+      case 64: go(k64); break;
+      case 128: go(k128); break;
+      default: go(k0); break;
+    }
+  };
+  if (metric == L2)
+    by_dim(ivf_rerun_scan_kernel<L2, 32>, ivf_rerun_scan_kernel<L2, 64>, ivf_rerun_scan_kernel<L2, 128>,
+           ivf_rerun_scan_kernel<L2, 0>);
+  else if (metric == IP)
+    by_dim(ivf_rerun_scan_kernel<IP, 32>, ivf_rerun_scan_kernel<IP, 64>, ivf_rerun_scan_kernel<IP, 128>,
+           ivf_rerun_scan_kernel<IP, 0>);
+  else
+    by_dim(ivf_rerun_scan_kernel<COS, 32>, ivf_rerun_scan_kernel<COS, 64>, ivf_rerun_scan_kernel<COS, 128>,
+           ivf_rerun_scan_kernel<COS, 0>);
   hipLaunchKernelGGL(ivf_rerun_merge_kernel, dim3((unsigned)((max_fail + 3) / 4)), dim3(256), 0, st, a, part);
 }
 

@@ -8,7 +8,7 @@ PYR_* knobs given on the command line (env values are read by the library per se
 --data mixture: a Gaussian mixture instead of the uniform bench rows -- `--clusters`
 centres ~ N(0, 1)^d, rows = centre + N(0, sigma^2)^d, a fraction `--outliers` of the rows scaled
 by `--outlier-scale`, queries drawn from the same mixture (no outliers) -- to measure how often the
-default fp16 certificate re-runs queries on data that clusters.  --metric ip uses DotProduct.
+default fp16 certificate re-runs queries on data that clusters.  --metric ip uses DotProduct, --metric cos VectorMath.Cosine.
 """
 from __future__ import annotations
 
@@ -51,7 +51,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--data", choices=["uniform", "mixture"], default="uniform")
     ap.add_argument("--train-rows", type=int, default=10_000_000, help="k-means rows (bench.py: all of I1)")
-    ap.add_argument("--metric", choices=["l2", "ip"], default="l2")
+    ap.add_argument("--metric", choices=["l2", "ip", "cos"], default="l2")
     ap.add_argument("--clusters", type=int, default=1000)
     ap.add_argument("--sigma", type=float, default=0.5)
     ap.add_argument("--outliers", type=float, default=1e-4)
@@ -67,7 +67,7 @@ def main():
     from pyrope_amd.vector import SearchOptions
     L = _lib.load()
     dev = torch.device("cuda", 0)
-    met = VectorMetric.L2 if args.metric == "l2" else VectorMetric.InnerProduct
+    met = {"l2": VectorMetric.L2, "ip": VectorMetric.InnerProduct, "cos": VectorMetric.Cosine}[args.metric]
     if args.data == "uniform":
         x = generate_synthetic_blocked(0, args.n, args.dim, 42)  # bench.py's row-blocked base set
         qh = generate_synthetic(args.nq, args.dim, 1337)

@@ -117,3 +117,79 @@ def test_cosine_writes_deletes_maxscans_snapshot(hiplib, oracle, tmp_path):
     idx2.load(path)
     got2 = _check(idx2, q, 10)[0]
     assert np.array_equal(got2[0].view(np.uint32), got[0].view(np.uint32))
+
+
+# ---- IVF_FLAT Cosine (IvfFlatVectorIndex.cs:167, :357): the stream scan over unit residual tiles ----
+
+def _list_scans(hiplib, fn):
+    """stream sample-phase launches (PH_SAMPLE = 9) while fn() runs: only the IVF stream scan has one"""
+    import ctypes as C
+    hiplib.pyr_profile_reset()
+    hiplib.pyr_profile_enable(1)
+    try:
+        fn()
+    finally:
+        hiplib.pyr_profile_enable(0)
+    ms, calls, work = C.c_double(), C.c_int64(), C.c_int64()
+    hiplib.pyr_profile_get(9, C.byref(ms), C.byref(calls), C.byref(work))
+    return calls.value
+
+
+def _ivf_cos(dim, x, nlist):
+    from pyrope_amd import IvfFlatVectorIndex
+    idx = IvfFlatVectorIndex(dim, COS, n_list=nlist)
+    idx.add_labels(np.arange(len(x), dtype=np.int64), x)
+    idx.build()
+    return idx
+
+
+def _ivf_oracle_check(idx, x, q, k, nprobe, oracle, step=1):
+    from pyrope_amd import SearchOptions
+    off, labels, live = idx.ivf_layout()
+    rows = x[np.where(labels >= 0, labels, 0)]
+    cents = idx.centroids_array()
+    s, l, c = idx.search_batch(q, k, SearchOptions(nprobe=nprobe))
+    for i in range(0, len(q), step):
+        os_, ok = oracle.ivf_search(q[i], k, cents, rows, off, live, metric=COS, nprobe=nprobe)
+        assert int(c[i]) == len(os_)
+        np.testing.assert_array_equal(l[i][: len(ok)], labels[ok])
+        assert np.array_equal(s[i][: len(os_)].view(np.uint32), os_.view(np.uint32))
+
+
+@pytest.mark.parametrize("k", [10, 20])
+@pytest.mark.parametrize("dim", [128, 64, 32])
+def test_ivf_cosine_stream_equals_exact_and_oracle(hiplib, oracle, dim, k):
+    from pyrope_amd import SearchOptions, generate_synthetic
+    x = generate_synthetic(30000, dim, 42)
+    q = generate_synthetic(200, dim, 1337)
+    idx = _ivf_cos(dim, x, 64)
+    got, nfb = _check(idx, q, k, SearchOptions(nprobe=8))
+    print(f"\n[cos-ivf] dim={dim} k={k}: exact re-runs {nfb}/{len(q)}")
+    assert _list_scans(hiplib, lambda: idx.search_batch(q, k, SearchOptions(nprobe=8))) > 0  # the stream path ran
+    _ivf_oracle_check(idx, x, q, k, 8, oracle, step=13)
+    assert nfb < len(q) // 10
+
+
+def test_ivf_cosine_signed_zero_rows_deletes(hiplib, oracle):
+    """Signed Gaussian clusters with norms over two decades, zero-norm rows (score 0), a zero query and
+    deletes after Build (tombstones); every result equals the exact scan's and the oracle's."""
+    from pyrope_amd import SearchOptions
+    rng = np.random.default_rng(8)
+    cent = rng.standard_normal((16, 128)).astype(np.float32)
+    x = (cent[rng.integers(0, 16, 20000)] + 0.4 * rng.standard_normal((20000, 128))).astype(np.float32)
+    x *= rng.uniform(0.01, 1.0, (20000, 1)).astype(np.float32)
+    x[5] = 0.0
+    x[77] = 1e-9
+    q = (cent[rng.integers(0, 16, 120)] + 0.4 * rng.standard_normal((120, 128))).astype(np.float32)
+    q[0] = 0.0
+    q[1] = -q[2]
+    idx = _ivf_cos(128, x, 32)
+    opts = SearchOptions(nprobe=6)
+    got, nfb = _check(idx, q, 10, opts)
+    print(f"\n[cos-ivf] signed: exact re-runs {nfb}/{len(q)}")
+    assert nfb >= 1 and nfb < len(q) // 4
+    _ivf_oracle_check(idx, x, q, 10, 6, oracle, step=7)
+    for i in range(0, 20000, 53):
+        idx.delete(str(i))
+    _check(idx, q, 10, opts)
+    _ivf_oracle_check(idx, x, q, 10, 6, oracle, step=11)
