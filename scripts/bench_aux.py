@@ -67,6 +67,21 @@ def timed(idx, q, Q, k, opts, steps, warmup, L):
     return Q * steps / el, el / steps * 1e3, phases, s.cpu().numpy(), lab.cpu().numpy()
 
 
+def pq_roofline(lookups_per_s):
+    """LDS-gather roofline of pq_adc4: one ds_read_b128 serves 64 rows x 4 queries = 256
+    (query, row, subspace) lookups in 4 LDS cycles (16-lane groups, MI355X_MICROARCH.md LDS table) when
+    conflict-free: 64 lookups/clk/CU x 256 CUs x 2.4 GHz.  Random 8-bit codes put a group's 16 lanes on
+    16 bank slots (code mod 16) at random: the expected busiest slot holds 3.08 of them (simulated), so
+    a random gather costs ~3.08x the conflict-free cycles -- `random_bank_peak`."""
+    peak = 64 * 256 * 2.4e9 / 1e12
+    rand = peak / 3.08
+    ach = lookups_per_s / 1e12
+    return {"bound": "lds", "achieved": ach, "peak": peak, "unit": "T lookups/s", "frac": ach / peak,
+            "random_bank_peak": rand, "frac_of_random_bank_peak": ach / rand,
+            "note": "peak = conflict-free ds_read_b128 gathers (64 lookups/clk/CU); random_bank_peak divides it "
+                    "by the expected 3.08-way bank-slot collision of 16 random codes"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("workload", choices=["flat", "ivfpq"])
@@ -236,7 +251,7 @@ def main():
                "qps": qps, "ms_per_step": ms, "phases_ms": {k_: v["ms"] for k_, v in phases.items()},
                "scan_rows": scan["work"],
                "lookups_per_s": scan["work"] * a.m / (scan["ms"] * 1e-3),
-               "code_bytes_GBps": scan["work"] * a.m / (scan["ms"] * 1e-3) / 1e9,
+               "roofline": pq_roofline(scan["work"] * a.m / (scan["ms"] * 1e-3)),
                "parity_sample": {"queries": a.check, "ids_and_bits_equal": ok}, "cpu_baseline": cpu}
     print(json.dumps(out), flush=True)
 
