@@ -8,6 +8,7 @@
 #include <map>
 #include <memory>
 #include <tuple>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -20,9 +21,9 @@ namespace {
 // Request coalescer (pyr_index_set_coalescing).  The reference serves one query per VEC.SEARCH
 // call (VectorCommandSet.cs:457-459), one call per Garnet session thread; the scan reaches its
 // throughput only on batches.  Concurrent pyr_index_search calls with the same (k, SearchOptions)
-// join an open batch.  The first caller (the leader) dispatches it as soon as the device has no
-// coalesced search of this index in flight (an idle device never waits: a lone caller pays no
-// added latency), else when the running search finishes, when the batch holds max_batch queries,
+// join an open batch.  The first caller (the leader) dispatches it as soon as fewer than
+// max_inflight (1) coalesced searches of this index are in flight (an idle device never waits: a lone
+// caller pays no added latency), else when a running search finishes, when the batch holds max_batch queries,
 // or at the latest max_wait_us after it opened; it runs ONE device search for all of them and
 // copies every caller's rows into that caller's buffers.  The other callers (followers) block until
 // then.  Each query's result is the same as a search of it alone (the engine is per query exact).
@@ -48,6 +49,12 @@ struct Coalescer {
   std::condition_variable cv;
   int32_t max_batch = 0, max_wait_us = 0;
   int32_t inflight = 0;  // coalesced device searches running
+  // batches that may run at once (each on its own stream and workspace).  PYR_COALESCE_INFLIGHT
+  // (measurement knob), default 1: two in flight measured no better (profiles/r3_serve/serve_if*.log)
+  int32_t max_inflight = [] {
+    const char *e = std::getenv("PYR_COALESCE_INFLIGHT");
+    return e ? std::max(1, std::atoi(e)) : 1;
+  }();
   std::map<std::tuple<int32_t, int32_t, int64_t>, std::shared_ptr<Batch>> open;  // (k, nprobe, max_scans)
 };
 }  // namespace
@@ -310,7 +317,7 @@ static pyr_status search_coalesced(pyr_index *index, const float *q, int64_t nq,
   }
   // dispatch when full, when no coalesced search is running (an idle device starts at once; a busy
   // one gathers every caller that arrives while it works), or at the deadline
-  co.cv.wait_until(lk, b->deadline, [&] { return b->closed || co.inflight == 0; });
+  co.cv.wait_until(lk, b->deadline, [&] { return b->closed || co.inflight < co.max_inflight; });
   if (!b->closed) {
     b->closed = true;
     auto f = co.open.find(key);
