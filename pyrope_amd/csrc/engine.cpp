@@ -495,10 +495,19 @@ static double filter_cerr(int dim) {
 
 // merge the K1-candidate partials, re-score exactly, certify; returns the number of
 // queries whose certificate failed (listed in ws.fail).  Synchronizes ws.st.
+// Cosine over a unit-row L2 store (FlatIndex::search_cosine): the candidates are re-scored with the
+// reference Cosine on the raw rows of the index itself, and the certificate is taken in cosine units
+struct CosRefine {
+  const RowStore *raw;     // the Cosine index's store (raw rows, norms, labels, non-finite flag)
+  const float *queries;    // raw queries
+  const float *qnorm;      // ComputeNorm per query
+  const uint32_t *zflag;   // a zero-norm row was written
+};
+
 static int64_t filter_finish(Workspace &ws, int64_t nq, int nparts, int k1, int k, int dim, int met, int V,
                              const float *d_q, const RowStore &rs, const MergeIvf *mi, float *d_s, int64_t *d_l,
                              int32_t *d_c, const uint32_t *list_rmax = nullptr, const float *resid_cents = nullptr,
-                             const uint32_t *list_rmax_r = nullptr, int prec = -1) {
+                             const uint32_t *list_rmax_r = nullptr, int prec = -1, const CosRefine *cr = nullptr) {
   ws.ms.ensure(sizeof(float) * nq * k1);
   ws.mk.ensure(sizeof(int32_t) * nq * k1);
   {
@@ -547,6 +556,19 @@ static int64_t filter_finish(Workspace &ws, int64_t nq, int nparts, int k1, int 
     }
   } else {
     r.c_bf = prec == FILTER_BF16X3 ? filter_bf16x3_cerr(dim, met) : 0.0;
+  }
+  if (cr) {
+    r.qcert = d_q;  // the unit queries the filter scored
+    r.tri = 0;      // the triangle bound reads skth as an L2 score
+    r.rows = cr->raw->rows.as<float>();
+    r.rows_rm = cr->raw->f16 ? cr->raw->rrm.as<float>() : nullptr;
+    r.row_labels = cr->raw->labels.as<int64_t>();
+    r.queries = cr->queries;
+    r.max_rsq = cr->raw->rmax.as<uint32_t>();
+    r.cosine = 1;
+    r.qnorm = cr->qnorm;
+    r.rnorm = cr->raw->norms.as<float>();
+    r.zflag = cr->zflag;
   }
   r.out_s = d_s;
   r.out_l = d_l;
@@ -963,6 +985,21 @@ struct FlatIndex : Index {
     launch_norms(d_q, nq, dim, 0, ws.qn.as<float>(), ws.st);  // VectorMath.ComputeNorm (:339)
     ws.cq.ensure(sizeof(float) * nq * dim);
     launch_unit_rows(d_q, nullptr, ws.qn.as<float>(), nq, dim, ws.cq.as<float>(), ws.st);
+    if (unit->centred_pass(cutoff, nq, k1)) {
+      // one certificate: the unit store's fp16 candidates re-scored with the reference Cosine on the raw
+      // rows, certified in cosine units (refine_kernel, cosine) -- no exact L2 pass in between
+      const CosRefine cr{&st, d_q, ws.qn.as<float>(), zflag.as<uint32_t>()};
+      int64_t nf;
+      {
+        std::shared_lock<std::shared_mutex> g(unit->mu);
+        nf = unit->filter_pass(ws.cq.as<float>(), nq, k, k1, cutoff, d_s, d_l, d_c, ws, &cr);
+      }
+      filter_fallback(ws, nf, d_q, dim, k, d_s, d_l, d_c,
+                      [&](const float *q2, int64_t n2, float *s2, int64_t *l2, int32_t *c2) {
+                        search_exact(q2, n2, k, cutoff, s2, l2, c2, ws.nested());
+                      });
+      return;
+    }
     ws.ccs.ensure(sizeof(float) * nq * kc);
     ws.ccl.ensure(sizeof(int64_t) * nq * kc);
     ws.ccc.ensure(sizeof(int32_t) * nq);
@@ -1011,6 +1048,27 @@ struct FlatIndex : Index {
   // MFMA candidate filter over slots [0, cutoff), exact refine with the *Unsafe form (V = 4)
   void search_filter(const float *d_q, int64_t nq, int k, int k1, int64_t cutoff, float *d_s, int64_t *d_l,
                      int32_t *d_c, Workspace &ws) {
+    const int64_t nf = filter_pass(d_q, nq, k, k1, cutoff, d_s, d_l, d_c, ws, nullptr);
+    const int k1_next = filter_k1_next(k, k1);
+    filter_fallback(ws, nf, d_q, dim, k, d_s, d_l, d_c,
+                    [&](const float *q2, int64_t n2, float *s2, int64_t *l2, int32_t *c2) {
+                      Workspace &sw = ws.nested();  // K1 = 64 filter first, then the exact scan
+                      if (k1_next > 0) search_filter(q2, n2, k, k1_next, cutoff, s2, l2, c2, sw);
+                      else search_exact(q2, n2, k, cutoff, s2, l2, c2, sw);
+                    });
+  }
+
+  // whether filter_pass runs the fp16 filter on centred tiles (the Cosine certificate needs them)
+  bool centred_pass(int64_t cutoff, int64_t nq, int k1) const {
+    if (getenv("PYR_FLAT_WAVES")) return false;
+    const ScanPlan p = plan_flat(cutoff, nq, dim, k1, MAX_PARTS);
+    return st.resid && st.center16 && prec16(filter_prec_for(filter_prec(), st.f16, p.chunk_rows));
+  }
+
+  // the filter, the merge and the certified refine over slots [0, cutoff); returns the failures (ws.fail).
+  // cr: this is the unit store of a Cosine index (re-score with the reference Cosine, cosine certificate)
+  int64_t filter_pass(const float *d_q, int64_t nq, int k, int k1, int64_t cutoff, float *d_s, int64_t *d_l,
+                      int32_t *d_c, Workspace &ws, const CosRefine *cr) {
     // 256-query items on 16-wave blocks (fp16 tiles, K1 = 16): each streamed tile serves twice the
     // queries (PYR_FLAT_WAVES=16)
     const char *fw = getenv("PYR_FLAT_WAVES");
@@ -1062,17 +1120,10 @@ struct FlatIndex : Index {
       if (prec16(fa.prec)) launch_filter16(fa, metric, p.nitems, ws.st);
       else launch_filter(fa, metric, p.nitems, ws.st);
     }
-    const int64_t nf =
-        filter_finish(ws, nq, p.nchunks, k1, k, dim, metric, exact_v, d_q, st, nullptr, d_s, d_l, d_c,
-                      centered ? st.rmax.as<uint32_t>() : nullptr, centered ? st.center.as<float>() : nullptr,
-                      centered ? st.rmax_r.as<uint32_t>() : nullptr, fa.prec);
-    const int k1_next = filter_k1_next(k, k1);
-    filter_fallback(ws, nf, d_q, dim, k, d_s, d_l, d_c,
-                    [&](const float *q2, int64_t n2, float *s2, int64_t *l2, int32_t *c2) {
-                      Workspace &sw = ws.nested();  // K1 = 64 filter first, then the exact scan
-                      if (k1_next > 0) search_filter(q2, n2, k, k1_next, cutoff, s2, l2, c2, sw);
-                      else search_exact(q2, n2, k, cutoff, s2, l2, c2, sw);
-                    });
+    if (cr && !centered) throw Error(PYR_E_STATE, "Cosine unit store without centred fp16 tiles");
+    return filter_finish(ws, nq, p.nchunks, k1, k, dim, metric, exact_v, d_q, st, nullptr, d_s, d_l, d_c,
+                         centered ? st.rmax.as<uint32_t>() : nullptr, centered ? st.center.as<float>() : nullptr,
+                         centered ? st.rmax_r.as<uint32_t>() : nullptr, fa.prec, cr);
   }
 
   // BruteForceVectorIndex.Search (:275-379) on the VALU, the reference's exact arithmetic

@@ -645,12 +645,14 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
         float d2 = 0.0f, c2 = 0.0f, qc = 0.0f;
         if (p < np) {
           const float *c = a.cents + (size_t)lp * D;
+          // the error terms follow the query the filter scored: the unit query for Cosine (qcert)
+          const float *qe = a.qcert ? a.qcert + (size_t)q * D : qp;
 #pragma unroll UNR8
           for (int d = j; d < D; d += 8) {
-            const float t = qp[d] - c[d];
+            const float t = qe[d] - c[d];
             d2 += t * t;
             c2 += c[d] * c[d];
-            qc += qp[d] * c[d];
+            qc += qe[d] * c[d];
           }
         }
 #pragma unroll
@@ -687,8 +689,18 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) emax = fmax(emax, __shfl_xor(emax, off));
       const double ak = (double)ms[k1 - 1];
-      if (MET == L2) ok = nout == k && (double)skth > (ak + emax) + g * fabs(ak + emax);
-      else ok = nout == k && (double)skth > ak + emax;
+      if (MET == L2 && a.cosine) {
+        // unit-row L2 approximations (FlatIndex::search_cosine): a row left out has -|q^ - x^|^2 <= ak + emax
+        // (real arithmetic), so q^.x^ <= 1 + (ak + emax) / 2, within (D/4 + 28) u of its cosine; the
+        // reference Cosine within (D/4 + 28) u of that (cos_rerank_kernel)
+        const float qn = a.qnorm[q];
+        ok = nout == k && (double)skth > 1.0 + 0.5 * (ak + emax) + (2.0 * D + 256.0) * u && qn >= 1e-6f &&
+             isfinite(qn) && !(a.max_rsq && a.max_rsq[1] != 0u) && !(a.zflag && *a.zflag != 0u && !(skth > 0.0f));
+      } else if (MET == L2) {
+        ok = nout == k && (double)skth > (ak + emax) + g * fabs(ak + emax);
+      } else {
+        ok = nout == k && (double)skth > ak + emax;
+      }
       if (lane == 0) {
         if (a.out_c) a.out_c[q] = nout;
         if (!ok) a.fail_list[atomicAdd(a.fail_cnt, 1)] = (int32_t)q;

@@ -459,6 +459,7 @@ struct RefineArgs {
   // exact scores are VectorMath.Cosine(q, x, |q|, |x|), certified against 1 + s_K1 / 2 + (2D + 256) u
   int32_t cosine;
   const float *qnorm, *rnorm;
+  const float *qcert;       // the queries the filter scored, for the error terms (null: queries)
   const uint32_t *zflag;    // != 0 once a row with a norm below 1e-6 was stored (k-th score must be > 0)
   float *out_s;
   int64_t *out_l;
