@@ -347,6 +347,7 @@ def run(args):
 
     # ---- recall@10 vs the exact FLAT top-10 over all N rows: per-rank FLAT shard + merge ----
     recall = None
+    truth_check = None
     s_fin = result[0].cpu().numpy()
     l_fin = result[1].cpu().numpy()
     if args.recall_queries > 0:
@@ -365,6 +366,18 @@ def run(args):
         hits = sum(len(set(gt[i].tolist()) & set(l_fin[i].tolist())) for i in range(R))
         recall = hits / (R * k)
         log(f"recall@10 over {R} queries: {recall:.4f} ({time.time() - t:.1f}s)")
+        # the ground truth itself against the CPU restatement of BruteForceVectorIndex.Search (checker only)
+        if rank == 0 and world == 1 and args.cpu_seconds > 0 and data is not None:
+            import oracle  # checker only
+            G = min(16, R)
+            t = time.time()
+            os_, ok_, _ = oracle.bf_search_batch(qh[:G], k, data, nthreads=args.cpu_threads or host_cpus()["usable"])
+            truth_check = {"queries": G, "ids_equal": bool(np.array_equal(ok_, fl[:G])),
+                           "scores_bit_identical": bool(np.array_equal(os_.view(np.uint32), fs[:G].view(np.uint32))),
+                           "note": "GPU FLAT ground truth of the first queries vs oracle/oracle.c BruteForce search "
+                                   "over all N rows"}
+            log(f"recall ground truth vs CPU oracle: {G} queries, ids {truth_check['ids_equal']}, bits "
+                f"{truth_check['scores_bit_identical']} ({time.time() - t:.1f}s)")
 
     # ---- CPU baseline: the oracle (CPU restatement of the reference engine) on the same index ----
     cpu = None
@@ -440,6 +453,7 @@ def run(args):
                        "merge": "RCCL all_gather of probe lists and of partial top-k + on-device merge"
                                 if world > 1 else "none"},
             "recall_at_10": recall,
+            "recall_truth_check": truth_check,
             "roofline": {"bound": "hbm", "achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": hbm_achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_src,
