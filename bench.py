@@ -369,7 +369,7 @@ def run(args):
         # the ground truth itself against the CPU restatement of BruteForceVectorIndex.Search (checker only)
         if rank == 0 and world == 1 and args.cpu_seconds > 0 and data is not None:
             import oracle  # checker only
-            G = min(16, R)
+            G = min(64, R)
             t = time.time()
             os_, ok_, _ = oracle.bf_search_batch(qh[:G], k, data, nthreads=args.cpu_threads or host_cpus()["usable"])
             truth_check = {"queries": G, "ids_equal": bool(np.array_equal(ok_, fl[:G])),
