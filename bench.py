@@ -166,7 +166,7 @@ def run(args):
     from pyrope_amd import (BruteForceVectorIndex, IvfFlatVectorIndex, VectorMetric, _lib, generate_synthetic,
                             generate_synthetic_blocked, kmeans_train)
     from pyrope_amd.build import build
-    from pyrope_amd.dist import gather_partials, merge_device, shard_blocks, sharded_ivf_step
+    from pyrope_amd.dist import ShardedIvfStep, all_gather_rows, gather_partials, merge_device, shard_blocks
     from pyrope_amd.vector import SearchOptions
     build()
     L = _lib.load()
@@ -244,15 +244,18 @@ def run(args):
                           torch.cuda.current_stream().cuda_stream, opts, d_probes=probes.data_ptr(), nprobe=width)
         return s_loc, l_loc
 
-    def merge(sp, lp, kk):  # RCCL all_gather'ed partial top-k -> on-device merge
-        return merge_device(sp, lp, kk, torch.cuda.current_stream().cuda_stream)
+    def merge(sp, lp, kk):  # RCCL all_gather'ed partial top-k [world, Q, k] -> on-device merge
+        return merge_device(sp, lp, kk, torch.cuda.current_stream().cuda_stream, part_major=True)
+
+    # the N > 1 step's probe lists and gathered partials: allocated once, reused by every step
+    sharded = ShardedIvfStep(args.nq, width, k, rank, world, device=dev) if world > 1 else None
 
     def step():
         if world == 1:
             idx.search_device(q.data_ptr(), Q, k, s_loc.data_ptr(), l_loc.data_ptr(), 0,
                               torch.cuda.current_stream().cuda_stream, opts)
             return
-        result[:] = sharded_ivf_step(q, args.nq, rank, world, probe, search, merge, k)
+        result[:] = sharded(q, probe, search, merge)
 
     def barrier():
         if world > 1:
@@ -279,12 +282,24 @@ def run(args):
 
     # ---- per-phase kernel times (HIP events on the search stream), outside the timed region ----
     phases = {}
+    coll = {}
     L.pyr_profile_reset()
     L.pyr_profile_enable(1)
+    if sharded is not None:
+        sharded.timing = True
     for _ in range(args.profile_steps):
         step()
+        if sharded is not None:
+            for kk, v in sharded.collective_ms.items():
+                coll[kk] = coll.get(kk, 0.0) + v / args.profile_steps
     torch.cuda.synchronize()
     L.pyr_profile_enable(0)
+    if sharded is not None:
+        sharded.timing = False
+    # rows of every rank's shard (weak scaling: each rank holds N / world of them)
+    rank_rows = [nrows]
+    if world > 1:
+        rank_rows = all_gather_rows(torch.tensor([nrows], dtype=torch.int64, device=dev), world).cpu().tolist()
     import ctypes as C
     names = {0: "coarse", 1: "work_lists", 9: "sample", 2: "list_scan", 3: "buffer_scan", 4: "merge", 7: "refine",
              8: "exact_rerun"}
@@ -478,6 +493,8 @@ def run(args):
                                 "note": "SURVEY.md 8(d): nprobe/nlist x N x D x 4 + nlist x D x 4 per query (no "
                                         "batching reuse); not a roofline"},
             "phases_ms": {k_: round(v["ms"], 4) for k_, v in phases.items()},
+            "collective_ms": {k_: round(v, 4) for k_, v in coll.items()} if world > 1 else None,
+            "rank_rows": rank_rows,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -216,6 +216,18 @@ pyr_status pyr_index_pq_state(const pyr_index *index, float *codebooks, int32_t 
  * writes the global top-k per query, ties by label asc.  Device buffers, async on stream. */
 pyr_status pyr_merge_topk_device(const float *d_scores, const int64_t *d_labels, int64_t nq, int32_t nparts,
                                  int32_t k, float *d_out_scores, int64_t *d_out_labels, void *stream);
+/* The same over either layout: part_major = 0 reads nq x nparts x k (as above); part_major = 1 reads
+ * nparts x nq x k, the buffer an all_gather of per-GPU nq x k partials leaves (no transpose). */
+pyr_status pyr_merge_topk_parts_device(const float *d_scores, const int64_t *d_labels, int64_t nq, int32_t nparts,
+                                       int32_t k, int32_t part_major, float *d_out_scores, int64_t *d_out_labels,
+                                       void *stream);
+
+/* HBM plan (host arithmetic, no device needed): the bytes an IVF_FLAT index of nrows rows in nlist
+ * lists (longest max_list_len rows) holds on one GPU, and the workspace one batched search of nq queries
+ * (nprobe, k) on the default list scan allocates.  A multi-GPU launcher sizes each rank with it before
+ * loading its shard (no reference counterpart: the reference is one process on the host heap). */
+pyr_status pyr_ivf_memory_plan(int32_t dim, int64_t nrows, int32_t nlist, int64_t max_list_len, int64_t nq,
+                               int32_t nprobe, int32_t k, int64_t *index_bytes, int64_t *workspace_bytes);
 
 /* Pyrope.Benchmarks synthetic generator (Program.cs:251-263): v[d] = (float)new Random(seed).NextDouble(),
  * row by row.  Host buffer count x dim.  Measurement-harness utility. */

@@ -106,6 +106,9 @@ SIGNATURES = {
     "pyr_scalar_quantize_minmax": (C.c_int, [C.c_int32, _f, C.c_int64, C.c_int32, _u8, _f, _f]),
     "pyr_scalar_dequantize": (C.c_int, [C.c_int32, _u8, C.c_int64, C.c_int32, _f, _f, _f]),
     "pyr_merge_topk_device": (C.c_int, [_vp, _vp, C.c_int64, C.c_int32, C.c_int32, _vp, _vp, _vp]),
+    "pyr_merge_topk_parts_device": (C.c_int, [_vp, _vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, _vp, _vp, _vp]),
+    "pyr_ivf_memory_plan": (C.c_int, [C.c_int32, C.c_int64, C.c_int32, C.c_int64, C.c_int64, C.c_int32, C.c_int32,
+                                      _i64, _i64]),
     "pyr_generate_synthetic": (C.c_int, [C.c_int64, C.c_int32, C.c_int32, _f]),
     "pyr_generate_synthetic_blocked": (C.c_int, [C.c_int64, C.c_int64, C.c_int32, C.c_int32, C.c_int64, _f]),
     "pyr_index_set_centroids": (C.c_int, [_vp, _f, C.c_int32]),

@@ -579,12 +579,27 @@ pyr_status pyr_scalar_dequantize(int32_t device, const uint8_t *codes, int64_t n
 
 pyr_status pyr_merge_topk_device(const float *d_scores, const int64_t *d_labels, int64_t nq, int32_t nparts,
                                  int32_t k, float *d_out_scores, int64_t *d_out_labels, void *stream) {
+  return pyr_merge_topk_parts_device(d_scores, d_labels, nq, nparts, k, 0, d_out_scores, d_out_labels, stream);
+}
+
+pyr_status pyr_merge_topk_parts_device(const float *d_scores, const int64_t *d_labels, int64_t nq, int32_t nparts,
+                                       int32_t k, int32_t part_major, float *d_out_scores, int64_t *d_out_labels,
+                                       void *stream) {
   if (nq < 0 || nparts <= 0 || nparts > pyr::MAX_PARTS || k <= 0 || k > pyr::KMAX)
     return fail(PYR_E_ARG, "bad merge shape");
   return guard([&] {
     pyr::launch_merge_labels(d_scores, d_labels, nq, nparts, k, d_out_scores, d_out_labels,
-                             reinterpret_cast<hipStream_t>(stream));
+                             reinterpret_cast<hipStream_t>(stream), part_major != 0);
     HIPCHK(hipGetLastError());
+  });
+}
+
+pyr_status pyr_ivf_memory_plan(int32_t dim, int64_t nrows, int32_t nlist, int64_t max_list_len, int64_t nq,
+                               int32_t nprobe, int32_t k, int64_t *index_bytes, int64_t *workspace_bytes) {
+  if (dim <= 0 || nrows < 0 || nlist <= 0 || max_list_len < 0 || nq < 0 || nprobe < 0 || k <= 0)
+    return fail(PYR_E_ARG, "bad memory-plan shape");
+  return guard([&] {
+    pyr::ivf_memory_plan(dim, nrows, nlist, max_list_len, nq, nprobe, k, index_bytes, workspace_bytes);
   });
 }
 

@@ -49,6 +49,7 @@ static int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 void RowStore::reserve(int64_t slots, hipStream_t st) {
   if (slots <= cap) return;
+  ++gen;
   // whole 32-slot tiles (the fp16 filter's unit; a multiple of the blocked layout's 8)
   int64_t nc = round_up(std::max<int64_t>(slots, std::max<int64_t>(cap * 3 / 2, 64)), 32);
   rows.grow_keep(sizeof(float) * nc * dim, sizeof(float) * cap * dim, st);
@@ -89,8 +90,29 @@ static float pow2_scale_host(float amax) {  // max |x_i| * sx < 2^14 (filter16.h
   return std::ldexp(1.0f, 14 - e);
 }
 
+// Concurrent searches share one store: the refresh runs under a lock and completes (stream
+// synchronized) before another search can take the cached pointer.  It runs only after a write or
+// a change of the error-bound constants, never in a steady-state search (hipGraph capture included).
+const float *RowStore::row_terms(int met, float kr, float kx, hipStream_t st) {
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lk(mu);
+  if (mub_gen == gen && mub_met == met && mub_kr == kr && mub_kx == kx && mub.n >= sizeof(float) * cap)
+    return mub.as<float>();
+  mub.ensure(sizeof(float) * std::max<int64_t>(cap, 1));
+  launch_row_terms(meta.as<float>(), resid || center16 ? rsq16.as<float>() : rsq.as<float>(), rsq.as<float>(), cap,
+                   met, kr, kx, mub.as<float>(), st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(st));
+  mub_gen = gen;
+  mub_met = met;
+  mub_kr = kr;
+  mub_kx = kx;
+  return mub.as<float>();
+}
+
 void RowStore::encode16(const int64_t *d_slots, int64_t cnt, hipStream_t st) {
   if (!f16 || cap == 0) return;
+  ++gen;
   if (!d_slots) cnt = cap;
   if (cnt <= 0) return;
   // FLAT L2 centering: tiles hold x - center (one "list"), meta -|x - center|^2
@@ -123,6 +145,7 @@ void RowStore::encode16(const int64_t *d_slots, int64_t cnt, hipStream_t st) {
 void RowStore::write(const float *x, const int64_t *slots, const int64_t *labs, int64_t cnt, hipStream_t st,
                      DevMem &stage_x, DevMem &stage_i) {
   if (cnt <= 0) return;
+  ++gen;
   const size_t xb = sizeof(float) * cnt * dim;
   stage_x.ensure(xb);
   stage_i.ensure(sizeof(int64_t) * cnt * 2);
@@ -167,6 +190,7 @@ void RowStore::write(const float *x, const int64_t *slots, const int64_t *labs, 
 
 void RowStore::set_live(const std::vector<int64_t> &slots, uint8_t v, hipStream_t st, DevMem &stage) {
   if (slots.empty()) return;
+  ++gen;
   stage.ensure(sizeof(int64_t) * slots.size());
   HIPCHK(hipMemcpyAsync(stage.p, slots.data(), sizeof(int64_t) * slots.size(), hipMemcpyHostToDevice, st));
   launch_scatter_u8(live.as<uint8_t>(), stage.as<int64_t>(), v, (int64_t)slots.size(), st);
@@ -461,6 +485,47 @@ static int stream_cap() {
 static int64_t stream_chunk() {
   const char *e = getenv("PYR_STREAM_CHUNK");
   return round_up(e ? std::max<int64_t>(32, atoll(e)) : 5120, 32);
+}
+
+// HBM plan of an IVF_FLAT index and of one stream-path search on it (pyr_ivf_memory_plan): the
+// allocations commit_lists and search_stream / stream_slice make, restated as arithmetic so that a
+// multi-GPU launch can size a rank before it allocates (the M8 rank shape: tests/test_host_logic.py).
+void ivf_memory_plan(int dim, int64_t nrows, int nlist, int64_t max_len, int64_t nq, int nprobe, int k,
+                     int64_t *index_bytes, int64_t *workspace_bytes) {
+  const int64_t D = dim;
+  const int64_t slots = round_up(nrows, 32) + (int64_t)nlist * 32;  // lists padded to 32-row tiles
+  // rows (blocked fp32) + row-major fp32 copy + fp16 tiles + meta, row terms, |x|^2, |x - c|^2, live, label
+  const int64_t per_row = 4 * D + 4 * D + 2 * D + 4 + 4 + 4 + 4 + 1 + 8;
+  const int64_t cent = (int64_t)nlist * (D * 4 * 3 + 4 * 6 + 8);  // centroids (blocked, row-major, unit), per-list
+  if (index_bytes) *index_bytes = slots * per_row + cent;
+  if (!workspace_bytes) return;
+  const int probes = std::max(0, std::min(nprobe, nlist));
+  // search_stream: chunking and the 16 GiB slice of candidate regions
+  const int cap = stream_cap();
+  IvfChunking ch{(int32_t)stream_chunk(), 1, 0};
+  ch.cmax = ivf_list_chunks((int)max_len, ch);
+  if ((int64_t)probes * ch.cmax > MAX_PARTS) {
+    const int64_t room = std::max<int64_t>(1, MAX_PARTS / std::max(probes, 1));
+    ch.chunk = (int32_t)round_up(std::max<int64_t>(32, (max_len + room - 1) / room), 32);
+    ch.cmax = ivf_list_chunks((int)max_len, ch);
+  }
+  const int64_t nparts = (int64_t)probes * ch.cmax;
+  const int64_t per_q = std::max<int64_t>(1, nparts * cap * 8);
+  const int64_t qs = std::max<int64_t>(1, std::min<int64_t>(nq, (int64_t(16) << 30) / per_q));
+  int64_t w = 0;
+  // coarse ranking: probe lists of the whole batch, <= 256 MB of centroid scores per launch
+  w += 4 * nq * probes;
+  const int64_t qb = std::max<int64_t>(1, std::min<int64_t>(int64_t(1) << 21, (int64_t(1) << 26) / std::max(nlist, 1)));
+  w += 4 * std::min(nq, qb) * nlist + 4 * std::min(nq, qb);
+  // per slice (the buffers are sized for the largest slice and reused)
+  const int64_t npos = qs * probes, nslot = qs * nparts;
+  w += (int64_t)sizeof(ScanItem) * ivf_max_items(qs, probes, nlist, stream16_qmax(false), ch, 0) + 4 * npos +
+       16 * ((int64_t)nlist + 1);
+  w += 2 * npos * D + 8 * npos + 4 * npos * stream16_sample_values() + 4 * qs;  // query operands, samples, T_q
+  w += 8 * nslot * cap + 8 * nslot;                                            // candidate regions + counts/floors
+  w += 8 * qs * STREAM_KO + 16 * qs;                                           // merged candidates, fail lists
+  w += 8 * ivf_rerun_part_keys(qs, probes, k);                                 // device re-run scratch
+  *workspace_bytes = w;
 }
 // XCD-major mapping of IVF filter items (FilterArgs::xcd); PYR_FILTER_XCD=0 disables it
 static int filter_xcd() {
@@ -1813,6 +1878,7 @@ struct IvfFlatIndex : Index {
     lists.cap = nl.cap;
     lists.hlabels.swap(nl.hlabels);
     lists.hlive.swap(nl.hlive);
+    ++lists.gen;
     lstate = lv;
     pos_of.clear();
     for (int64_t p = 0; p < tot; p++)
@@ -2164,6 +2230,7 @@ struct IvfFlatIndex : Index {
     sa.rsq = lists.rsq.as<float>();
     stream_ub_terms(dim, met, filter_f16_cerr(dim, met, prec), filter_cerr(dim), filter_f16_abs(dim, met, lists.sx, prec),
                     sa);
+    sa.mub = lists.row_terms(met, sa.kr, sa.kx, ws.st);
     {
       PhaseTimer t(PH_SAMPLE, ws.st);
       launch_stream_prep(sa, met, maxi, ws.st);

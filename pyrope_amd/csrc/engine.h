@@ -82,6 +82,14 @@ struct RowStore {
   // f16 stores: a row-major fp32 copy of the rows for the exact refine (a candidate's 512 B read
   // contiguously; the blocked layout spreads one row over D 32-B sectors)
   DevMem rrm;
+  // the stream scan's per-row term meta + E_row (launch_row_terms), cached for (gen, metric, kr, kx):
+  // gen advances with every change of the rows, meta or norms (reserve, write, set_live, encode16, an
+  // IVF commit)
+  DevMem mub;
+  uint64_t gen = 1, mub_gen = 0;
+  int mub_met = -1;
+  float mub_kr = 0.0f, mub_kx = 0.0f;
+  const float *row_terms(int met, float kr, float kx, hipStream_t st);
   const float *meta_norms() const { return resid ? rsq16.as<float>() : rsq.as<float>(); }
   std::vector<int64_t> hlabels;
   std::vector<uint8_t> hlive;
@@ -99,6 +107,11 @@ struct RowStore {
     hlive.clear();
   }
 };
+
+// HBM bytes of an IVF_FLAT index of nrows rows and of one stream-path search of nq queries on it
+// (engine.cpp; pyr_ivf_memory_plan)
+void ivf_memory_plan(int dim, int64_t nrows, int nlist, int64_t max_len, int64_t nq, int nprobe, int k,
+                     int64_t *index_bytes, int64_t *workspace_bytes);
 
 struct Workspace {
   hipStream_t st = nullptr;

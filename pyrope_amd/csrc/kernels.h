@@ -177,7 +177,7 @@ void launch_merge_keys(const float *ps, const uint32_t *pk, int64_t nq, int32_t 
                        int32_t *out_keys, int32_t *out_cnt, hipStream_t st, const MergeIvf *ivf = nullptr);
 // Merge partial lists that carry int64 labels (multi-GPU), ties by label asc.
 void launch_merge_labels(const float *ps, const int64_t *pl, int64_t nq, int32_t nparts, int32_t k, float *out_s,
-                         int64_t *out_l, hipStream_t st);
+                         int64_t *out_l, hipStream_t st, bool part_major = false);
 
 // IVF: from probes [nq][nprobe] build list-major work items.
 struct IvfItemWs {
@@ -391,7 +391,12 @@ struct StreamArgs {
   const float *rsq16;         // per row |x - c|^2
   const float *rsq;           // per row |x|^2 (IP)
   float kr, kx, kq, kqa, kqc;
+  const float *mub;           // per row meta + E_row (RowStore::row_terms; stream32_kernel)
 };
+// per row the stream scan's additive term: meta + kr |x - c|^2 (+ kx |x|^2, IP), in the fp32 order the
+// 16x16x32 kernel evaluates it in (fmaf(kr, rsq16, meta), then fmaf(kx, rsq, .))
+void launch_row_terms(const float *meta, const float *rsq16, const float *rsq, int64_t n, int metric, float kr,
+                      float kx, float *out, hipStream_t st);
 // The per-row / per-pair split of the fp16 residual filter's error bound (refine_kernel's resid branch,
 // filter.hip): products A X go to (A^2 + X^2) / 2, (A + X)^2 to 2 (A^2 + X^2), so the bound of a row
 // no longer depends on its list's largest residual; the reference's own sum deviation (g) is folded in.

@@ -702,21 +702,23 @@ __global__ __launch_bounds__(256) void merge_keys_kernel(const float *ps, const 
 
 constexpr int MERGE_LU = MAX_PARTS / 64;  // parts per lane (merge_labels_kernel)
 
+// element (q, part, j) of the partial lists at q * sq + part * sp + j: query-major [nq][nparts][k]
+// (sq = nparts k, sp = k) or part-major [nparts][nq][k] as an all_gather leaves it (sq = k, sp = nq k)
 __global__ __launch_bounds__(256) void merge_labels_kernel(const float *ps, const int64_t *pl, int64_t nq, int nparts,
-                                                           int k, float *out_s, int64_t *out_l) {
+                                                           int k, int64_t sq, int64_t sp, float *out_s, int64_t *out_l) {
   const int lane = threadIdx.x & 63;
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= nq) return;
   int h[MERGE_LU];
   float cs[MERGE_LU];
   int64_t cl[MERGE_LU];
-  const size_t base = (size_t)q * nparts * k;
+  const size_t base = (size_t)q * sq;
 #pragma unroll
   for (int u = 0; u < MERGE_LU; ++u) {
     const int p = lane + 64 * u;
     h[u] = 0;
-    cs[u] = p < nparts ? ps[base + (size_t)p * k] : -INFINITY;
-    cl[u] = p < nparts ? pl[base + (size_t)p * k] : -1;
+    cs[u] = p < nparts ? ps[base + (size_t)p * sp] : -INFINITY;
+    cl[u] = p < nparts ? pl[base + (size_t)p * sp] : -1;
   }
   int produced = 0;
   for (int r = 0; r < k; ++r) {
@@ -747,8 +749,8 @@ __global__ __launch_bounds__(256) void merge_labels_kernel(const float *ps, cons
       if (cl[u] == bl && cs[u] == bs) {
         const int p = lane + 64 * u;
         h[u]++;
-        cs[u] = h[u] < k ? ps[base + (size_t)p * k + h[u]] : -INFINITY;
-        cl[u] = h[u] < k ? pl[base + (size_t)p * k + h[u]] : -1;
+        cs[u] = h[u] < k ? ps[base + (size_t)p * sp + h[u]] : -INFINITY;
+        cl[u] = h[u] < k ? pl[base + (size_t)p * sp + h[u]] : -1;
       }
     produced++;
   }
@@ -1833,9 +1835,11 @@ void launch_labels_to_i32(const int64_t *in, int64_t n, int32_t *out, hipStream_
 }
 
 void launch_merge_labels(const float *ps, const int64_t *pl, int64_t nq, int32_t nparts, int32_t k, float *out_s,
-                         int64_t *out_l, hipStream_t st) {
+                         int64_t *out_l, hipStream_t st, bool part_major) {
   if (nq <= 0) return;
-  hipLaunchKernelGGL(merge_labels_kernel, dim3(nblk(nq, 4)), dim3(256), 0, st, ps, pl, nq, nparts, k, out_s, out_l);
+  const int64_t sq = part_major ? k : (int64_t)nparts * k, sp = part_major ? nq * k : k;
+  hipLaunchKernelGGL(merge_labels_kernel, dim3(nblk(nq, 4)), dim3(256), 0, st, ps, pl, nq, nparts, k, sq, sp, out_s,
+                     out_l);
 }
 
 int64_t ivf_max_items(int64_t nq, int32_t nprobe, int32_t nlist, int32_t qchunk, IvfChunking ch, int phase) {

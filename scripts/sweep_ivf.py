@@ -49,6 +49,7 @@ def main():
     ap.add_argument("--nq", type=int, default=10_000)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--prof-steps", type=int, default=3, help="profiled searches averaged per setting")
     ap.add_argument("--data", choices=["uniform", "mixture"], default="uniform")
     ap.add_argument("--train-rows", type=int, default=10_000_000, help="k-means rows (bench.py: all of I1)")
     ap.add_argument("--metric", choices=["l2", "ip", "cos"], default="l2")
@@ -114,7 +115,8 @@ def main():
         dt = (time.perf_counter() - t) / args.steps
         L.pyr_profile_reset()
         L.pyr_profile_enable(1)
-        run()
+        for _ in range(args.prof_steps):
+            run()
         torch.cuda.synchronize()
         L.pyr_profile_enable(0)
         ph = {}
@@ -122,7 +124,7 @@ def main():
             ms, calls, work = C.c_double(), C.c_int64(), C.c_int64()
             L.pyr_profile_get(i, C.byref(ms), C.byref(calls), C.byref(work))
             if calls.value:
-                ph[name] = round(ms.value, 3)
+                ph[name] = round(ms.value / args.prof_steps, 4)
             if i == 8 and calls.value:
                 ph["reran_queries"] = work.value
         res = (s.cpu().numpy().copy(), lab.cpu().numpy().copy())

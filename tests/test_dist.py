@@ -99,12 +99,14 @@ def _oracle_shard(oracle, data, cents, rank, world):
 
 
 def _step_worker(rank, world, port, data, cents, queries, out):
-    """bench.py's N > 1 step (pyrope_amd.dist.sharded_ivf_step) with the oracle as the scan."""
+    """bench.py's N > 1 step (pyrope_amd.dist.ShardedIvfStep: buffers allocated once, collectives timed,
+    partials merged in the all_gather's [world, Q, k] layout) with the oracle as the scan; two steps
+    through the same buffers."""
     import torch
     import torch.distributed as dist
 
     import oracle
-    from pyrope_amd.dist import sharded_ivf_step
+    from pyrope_amd.dist import ShardedIvfStep
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -125,11 +127,18 @@ def _step_worker(rank, world, port, data, cents, queries, out):
                 Lb[i, :len(s)] = labels[order[kk]]
             return torch.from_numpy(S), torch.from_numpy(Lb)
 
-        def merge(sp, lp, k):  # pyr_merge_topk_device
-            return tuple(torch.from_numpy(a) for a in _host_merge(sp.numpy(), lp.numpy(), k))
+        def merge(sp, lp, k):  # pyr_merge_topk_parts_device(part_major=1): [world, Q, k] as gathered
+            assert sp.shape[0] == world
+            return tuple(torch.from_numpy(a) for a in _host_merge(sp.numpy().transpose(1, 0, 2),
+                                                                 lp.numpy().transpose(1, 0, 2), k))
 
-        s, lab = sharded_ivf_step(torch.from_numpy(queries), len(queries) // world, rank, world, probe, search,
-                                  merge, K)
+        step = ShardedIvfStep(len(queries) // world, NPROBE, K, rank, world)
+        bufs = (step.probes_all.data_ptr(), step.s_all.data_ptr(), step.l_all.data_ptr())
+        step.timing = True
+        for _ in range(2):  # the same buffers serve every step
+            s, lab = step(torch.from_numpy(queries), probe, search, merge)
+        assert (step.probes_all.data_ptr(), step.s_all.data_ptr(), step.l_all.data_ptr()) == bufs
+        assert set(step.collective_ms) == {"probe_allgather", "partial_allgather"}
         np.save(os.path.join(out, f"s{rank}.npy"), s.numpy())
         np.save(os.path.join(out, f"l{rank}.npy"), lab.numpy())
         np.save(os.path.join(out, f"p{rank}.npy"), seen["probes"])
@@ -238,3 +247,50 @@ def test_gpu_split_coarse_ranking_equals_search(hiplib):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(lab.cpu().numpy(), ref_l)
     assert np.array_equal(s.cpu().numpy().view(np.uint32), ref_s.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_gpu_part_major_merge_equals_query_major(hiplib):
+    """pyr_merge_topk_parts_device reads the all_gather layout [world, Q, k] directly: same result as the
+    query-major [Q, world, k] merge of the transposed buffer, ties by label."""
+    import torch
+
+    from pyrope_amd.dist import merge_device
+
+    rng = np.random.default_rng(5)
+    W, Q, k = 8, 777, 10
+    s = np.sort(rng.integers(0, 50, (W, Q, k)).astype(np.float32), axis=2)[:, :, ::-1].copy()  # ties across ranks
+    lab = rng.permutation(W * Q * k).reshape(W, Q, k).astype(np.int64)
+    lab[:, :5, 7:] = -1  # short partial lists
+    s[:, :5, 7:] = -np.inf
+    sp, lp = torch.from_numpy(s).cuda(), torch.from_numpy(lab).cuda()
+    a_s, a_l = merge_device(sp, lp, k, part_major=True)
+    b_s, b_l = merge_device(sp.transpose(0, 1).contiguous(), lp.transpose(0, 1).contiguous(), k)
+    torch.cuda.synchronize()
+    ref_s, ref_l = _host_merge(s.transpose(1, 0, 2), lab.transpose(1, 0, 2), k)
+    np.testing.assert_array_equal(a_l.cpu().numpy(), ref_l)
+    np.testing.assert_array_equal(b_l.cpu().numpy(), ref_l)
+    assert np.array_equal(a_s.cpu().numpy().view(np.uint32), ref_s.view(np.uint32))
+
+
+def test_rank_memory_plan_at_m8_rank_shape(hiplib):
+    """a rank of the 8-GPU M8 run (80M rows / 8 = 10M rows, nlist 8192, the 80,000-query
+    weak-scaling batch every rank searches, nprobe 32, k 10) fits one MI355X (288 GB) with room to
+    spare, before any rank allocates.  Host arithmetic (pyr_ivf_memory_plan): no GPU needed."""
+    from pyrope_amd.dist import rank_memory_plan
+
+    hbm = 288e9
+    # list lengths of a 10M-row shard over 8192 lists: mean 1,221; 20,000 covers heavy k-means skew
+    ib, wb = rank_memory_plan(128, 10_000_000, 8192, 20_000, 80_000, 32, 10)
+    assert 10e9 < ib < 16e9, ib          # ~1.3 kB per row at d = 128 (fp32 blocked + row-major + fp16 tiles)
+    assert wb <= 20e9, wb                # candidate regions sliced at 16 GiB + the rest
+    assert ib + wb < 0.25 * hbm
+    # the I1 single-GPU workload and M8 on one GPU (80M rows, 10,000 queries)
+    ib1, wb1 = rank_memory_plan(128, 10_000_000, 1024, 30_000, 10_000, 32, 10)
+    assert ib1 + wb1 < 0.1 * hbm
+    ib8, wb8 = rank_memory_plan(128, 80_000_000, 8192, 40_000, 10_000, 32, 10)
+    assert ib8 + wb8 < 0.5 * hbm
+    # the workspace grows with the batch until the 16 GiB region slice caps it
+    w_small = rank_memory_plan(128, 10_000_000, 8192, 20_000, 1_000, 32, 10)[1]
+    w_big = rank_memory_plan(128, 10_000_000, 8192, 20_000, 1_000_000, 32, 10)[1]
+    assert w_small < wb < w_big < 40e9
