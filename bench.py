@@ -71,6 +71,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline time (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use")
     ap.add_argument("--profile-steps", type=int, default=3)
+    ap.add_argument("--graph", type=int, default=1,
+                    help="N = 1: replay each step from a HIP graph of the whole search (1, default) or launch it "
+                         "kernel by kernel (0); every replay runs every kernel of the search")
     return ap.parse_args(argv)
 
 
@@ -264,11 +267,30 @@ def run(args):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    timed_step = step
+    graph = None
+    if world == 1 and args.graph:
+        # the whole search (coarse ranking .. exact re-run) captured once on a side stream: the workspace
+        # is sized by the warm-up, pyr_index_search_device only enqueues (no host sync, no allocation),
+        # and a replay launches every kernel of the step with its launch gaps removed
+        gst = torch.cuda.Stream()
+        gst.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(gst):
+            step()  # the capture stream's own workspace
+        gst.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=gst):
+            step()
+        torch.cuda.synchronize()
+        for _ in range(max(1, args.warmup)):
+            graph.replay()
+        torch.cuda.synchronize()
+        timed_step = graph.replay
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        timed_step()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -492,6 +514,7 @@ def run(args):
             "per_query_bytes": {"bytes_per_query": bytes_per_query,
                                 "note": "SURVEY.md 8(d): nprobe/nlist x N x D x 4 + nlist x D x 4 per query (no "
                                         "batching reuse); not a roofline"},
+            "launch": "hipGraph replay of the whole search per step" if graph is not None else "kernel launches",
             "phases_ms": {k_: round(v["ms"], 4) for k_, v in phases.items()},
             "collective_ms": {k_: round(v, 4) for k_, v in coll.items()} if world > 1 else None,
             "rank_rows": rank_rows,

@@ -455,6 +455,12 @@ static bool stream_enabled() {
   return !(e && atoi(e) == 0);
 }
 // query terms of the stream scan: 3 = one fp16 term (default), 2 = the hi/lo split (2 MFMAs per k-step)
+// the round-4 list scan (scan.hip: fused sample, 32x32x16 MFMA, 16 waves); PYR_STREAM_MFMA=16 runs the
+// round-3 stream16.hip kernels (measurement only; results identical)
+static bool stream_r4() {
+  const char *e = getenv("PYR_STREAM_MFMA");
+  return !(e && atoi(e) == 16);
+}
 static int stream_prec() {
   const char *e = getenv("PYR_STREAM_PREC");
   return e && atoi(e) == 2 ? FILTER_F16X2 : FILTER_F16X1;
@@ -2231,10 +2237,20 @@ struct IvfFlatIndex : Index {
     stream_ub_terms(dim, met, filter_f16_cerr(dim, met, prec), filter_cerr(dim), filter_f16_abs(dim, met, lists.sx, prec),
                     sa);
     sa.mub = lists.row_terms(met, sa.kr, sa.kx, ws.st);
+    const bool timing = getenv("PYR_STREAM_TIMING") != nullptr;  // measurement only (syncs)
+    if (timing) {
+      ws.tdbg.ensure(sizeof(unsigned long long) * 8);
+      HIPCHK(hipMemsetAsync(ws.tdbg.p, 0, sizeof(unsigned long long) * 8, ws.st));
+    }
+    const bool r4 = !q2 && stream_r4();
     {
       PhaseTimer t(PH_SAMPLE, ws.st);
-      launch_stream_prep(sa, met, maxi, ws.st);
-      launch_stream_scan(sa, met, maxi, true, ws.st);
+      if (r4) {
+        launch_scan_sample(sa, met, maxi, ws.st);
+      } else {
+        launch_stream_prep(sa, met, maxi, ws.st);
+        launch_stream_scan(sa, met, maxi, true, ws.st);
+      }
       StreamSelectArgs sel{};
       sel.samp = ws.ssamp.as<float>();
       sel.nq = nq;
@@ -2250,7 +2266,19 @@ struct IvfFlatIndex : Index {
     sa.work = ws.swork.as<int32_t>() + 1;
     {
       PhaseTimer t(PH_LIST_SCAN, ws.st, prof().on ? probed_rows(ws, nq, probes, le, lb) : 0);
-      launch_stream_scan(sa, met, maxi, false, ws.st);
+      if (timing) sa.tdbg = ws.tdbg.as<unsigned long long>();
+      if (r4) launch_scan_main(sa, met, maxi, ws.st);
+      else launch_stream_scan(sa, met, maxi, false, ws.st);
+      sa.tdbg = nullptr;
+    }
+    if (timing) {
+      unsigned long long c[8];
+      HIPCHK(hipMemcpyAsync(c, ws.tdbg.p, sizeof(c), hipMemcpyDeviceToHost, ws.st));
+      HIPCHK(hipStreamSynchronize(ws.st));
+      const double tot = (double)(c[0] + c[1] + c[2] + c[3]);
+      fprintf(stderr, "[stream timing] wave-cycles %.3g: prologue %.1f%%, tiles %.1f%%, end barrier %.1f%%, flush "
+              "%.1f%%; wave-items %llu, cycles per wave-item %.0f\n", tot, 100 * c[0] / tot, 100 * c[1] / tot,
+              100 * c[2] / tot, 100 * c[3] / tot, c[4], c[4] ? tot / c[4] : 0.0);
     }
     HIPCHK(hipGetLastError());
     ws.ms.ensure(sizeof(float) * nq * STREAM_KO);

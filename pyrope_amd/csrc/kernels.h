@@ -392,6 +392,7 @@ struct StreamArgs {
   const float *rsq;           // per row |x|^2 (IP)
   float kr, kx, kq, kqa, kqc;
   const float *mub;           // per row meta + E_row (RowStore::row_terms; stream32_kernel)
+  unsigned long long *tdbg;   // measurement only (PYR_STREAM_TIMING=1): per-wave cycle buckets, or null
 };
 // per row the stream scan's additive term: meta + kr |x - c|^2 (+ kx |x|^2, IP), in the fp32 order the
 // 16x16x32 kernel evaluates it in (fmaf(kr, rsq16, meta), then fmaf(kx, rsq, .))
@@ -413,6 +414,12 @@ struct CandMergeArgs {
   int32_t *out_k;
 };
 bool stream16_supported(int dim, int metric, int k1);
+int device_cus();                   // compute units of the current device (persistent-grid launches)
+// round 4 (scan.hip): the fused query-operand + sample launch (replaces launch_stream_prep and the
+// sampling launch_stream_scan), and the 32x32x16 list scan; scan_sample_values() == stream16_sample_values()
+int scan_sample_values();
+void launch_scan_sample(const StreamArgs &a, int metric, int max_items, hipStream_t st);
+void launch_scan_main(const StreamArgs &a, int metric, int max_items, hipStream_t st);
 int stream16_qmax(bool q2);          // queries per work item
 int stream16_sample_values();        // sample values per (query, probe)
 void launch_stream_prep(const StreamArgs &a, int metric, int max_items, hipStream_t st);

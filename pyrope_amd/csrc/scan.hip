@@ -1,0 +1,408 @@
+// scan.hip -- the IVF list scan of round 4: stream-and-emit over fp16 residual tiles on
+// v_mfma_f32_32x32x16_f16 (gfx950).
+//
+// Contract of stream16.hip (approximate scores over the lists' fp16 residual tiles -> every row whose
+// bound reaches the query's sampled threshold T_q is emitted -> certified exact refine, filter.hip
+// refine_kernel), with three changes measured on the I1 configuration:
+//
+//  1. sample_kernel: ONE wave per (list, 32-query group).  It prepares the group's query operands
+//     itself (q - c or q, a power-of-two scale, fp16; {f, cq + E_pair}), writes them for the main pass,
+//     and scores the list's first SAMPLE_TILES tiles with them from registers -- no LDS, no barrier, no
+//     per-item query staging.  It replaces sprep_kernel + the sampling launch of the list scan.
+//  2. scan_kernel: the MFMA shape 32x32x16.  A 32-row tile is ONE A operand per 16-dim k-step (lane
+//     (r, h) holds row r, dims 16s + 8h .. +7: the tile layout is lane-linear for it as it stands), a
+//     query group is 32 queries, and the 32 x 32 result leaves lane (r, h) query r's scores of rows
+//     8b + 4h + i (b, i < 4): per (tile, group) 8 MFMAs against 8 ds_read_b128 and a 16-value epilogue.
+//     16 waves per block (4 per SIMD, <= 128 VGPRs): no register prefetch of a wave's next tile; it
+//     is pulled into L2 by one 4-byte LDS-DMA per line while the current one is scored, and tiles are
+//     taken from an LDS counter so the waves reach the item's end together.
+//  3. Emitted rows are staged in LDS and written to the candidate regions by the whole block at the
+//     item's end (64 rows per store instruction instead of one).
+//
+// Row terms (meta + the row's share of the error bound) come precomputed per store
+// (RowStore::row_terms, StreamArgs::mub).
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+
+#include "kernels.h"
+
+namespace pyr {
+namespace {
+
+#include "f16util.h"
+
+constexpr int NW = 16;                 // waves per scan block
+constexpr int SAMPLE_TILES = 16;       // tiles of a list the sample scores (stream16.hip: 2 x 8 waves)
+constexpr int SV = 2 * SAMPLE_TILES;   // sample values per (query, probe): one per (tile, lane half)
+
+__device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf(a, fmaxf(b, c)); }
+
+// ---- 1. query operands + sample ----
+// Wave (item, g): the item's queries 32g .. 32g + 31 (lane (r, h): query 32g + r, dims 16s + 8h .. +7).
+// Sample value (t, h) of a query = the best bound of rows 8b + 4h + i of tile t (distinct rows per value).
+template <int D, int MET>
+__global__ __launch_bounds__(256) void sample_kernel(StreamArgs a) {
+  constexpr int KS = D / 16, TB = 64 * D, QG = 512 / 32;
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int item = unit / QG, g = unit - item * QG;
+  if (item >= *a.n_items) return;
+  const ScanItem it = a.items[item];
+  if (it.part != 0 || 32 * g >= it.qcnt) return;  // chunk-0 items cover every (list, query) pair once
+  const int qi = min(32 * g + r, it.qcnt - 1);
+  const bool own = 32 * g + r < it.qcnt;
+  const int pos = it.qbeg + qi;
+  const int slot = a.qlist[pos];
+  const int q = slot / a.nparts;
+  // the residual q - c (L2) or q (IP) in registers, its norm terms and max |.|
+  float rv[KS][8];
+  float cq = 0.0f, amax = 0.0f, q2 = 0.0f, c2 = 0.0f;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const float4 *qp = reinterpret_cast<const float4 *>(a.queries + (size_t)q * D + 16 * s + 8 * h);
+    const float4 *cp = reinterpret_cast<const float4 *>(a.cents + (size_t)it.list * D + 16 * s + 8 * h);
+    const float4 qa = qp[0], qb = qp[1], ca = cp[0], cb = cp[1];
+    const float qv[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
+    const float cv[8] = {ca.x, ca.y, ca.z, ca.w, cb.x, cb.y, cb.z, cb.w};
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (MET == L2) {
+        rv[s][u] = qv[u] - cv[u];
+        cq += rv[s][u] * rv[s][u];
+      } else {
+        rv[s][u] = qv[u];
+        cq += qv[u] * cv[u];
+        q2 += qv[u] * qv[u];
+        c2 += cv[u] * cv[u];
+      }
+      amax = fmaxf(amax, fabsf(rv[s][u]));
+    }
+  }
+  cq += __shfl_xor(cq, 32);
+  amax = fmaxf(amax, __shfl_xor(amax, 32));
+  if (MET == IP) {
+    q2 += __shfl_xor(q2, 32);
+    c2 += __shfl_xor(c2, 32);
+  }
+  // the pair's share of the error bound (stream_ub_terms), rounded up by the 1e-3 in its constants
+  float ep;
+  if (MET == L2) {
+    ep = a.kq * cq + a.kqa * sqrtf(cq);
+  } else {
+    const float qn = sqrtf(q2);
+    ep = a.kq * q2 + a.kqa * qn + a.kqc * qn * sqrtf(c2);
+  }
+  const float sq = pow2_scale(amax);
+  const float f = (MET == L2 ? 2.0f : 1.0f) / (sq * a.sx);
+  const float cqe = (MET == L2 ? -cq : cq) + ep;
+  h8v B[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) B[s][u] = (_Float16)(rv[s][u] * sq);  // exact scaling (power of two)
+    if (own) *reinterpret_cast<h8v *>(a.bq + (size_t)pos * D + 16 * s + 8 * h) = B[s];
+  }
+  if (own && h == 0) a.qsc[pos] = make_float2(f, cqe);
+  // score the first SAMPLE_TILES tiles of the list with the group (rows as A, the queries as B)
+  const int r0 = it.row_begin;
+  const int nt = min((it.row_end - r0 + 31) >> 5, SAMPLE_TILES);
+  const char *hsrc = reinterpret_cast<const char *>(a.h16);
+  float mx[SAMPLE_TILES];
+#pragma unroll
+  for (int t = 0; t < SAMPLE_TILES; ++t) {
+    mx[t] = -INFINITY;
+    if (t < nt) {
+      const char *tb = hsrc + (size_t)(r0 / 32 + t) * TB + lane * 16;
+      h8v A[KS];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) A[s] = *reinterpret_cast<const h8v *>(tb + s * 1024);
+      const size_t mo = (size_t)(r0 + 32 * t) + 4 * h;
+      f4v M[4];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) M[b] = *reinterpret_cast<const f4v *>(a.mub + mo + 8 * b);
+      f16v acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[0], B[0], (f16v){}, 0, 0, 0);
+#pragma unroll
+      for (int s = 1; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[s], B[s], acc, 0, 0, 0);
+      const int rt = r0 + 32 * t, rlim = it.row_end;
+      float m = -INFINITY;
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float y = fmaf(f, acc[4 * b + i], M[b][i]);
+          m = rt + 8 * b + 4 * h + i < rlim ? fmaxf(m, y) : m;
+        }
+      mx[t] = m;
+    }
+  }
+  if (own) {
+    float *sp = a.samp + (size_t)(q * a.nprobe + (slot % a.nparts) / a.cmax) * SV + h;
+#pragma unroll
+    for (int t = 0; t < SAMPLE_TILES; ++t) sp[2 * t] = mx[t] + cqe;
+  }
+}
+
+// ---- 2. the list scan ----
+// AB (measurement only, PYR_FILTER_ABLATE): 1 (64) = no emission, 2 (128) = tile stream only (no MFMA),
+// 3 (256) = no emission and every tile read from the item's first one (compute without HBM)
+template <int D, int MET, int AB = 0>
+__global__ __launch_bounds__(64 * NW, 1) void scan_kernel(StreamArgs a) {
+  constexpr int KS = D / 16;         // 32x32x16 k-steps
+  constexpr int TB = 64 * D;         // h16 bytes per 32-row tile
+  constexpr int QMAX = 512;          // queries per item
+  constexpr int PIECES = QMAX / 32 * KS;
+  __shared__ __attribute__((aligned(16))) char bl[PIECES * 1024];
+  __shared__ float2 qf[QMAX];        // per query slot: {f, threshold in y = f acc + row term space}
+  __shared__ float2 qz[QMAX];        // {cq (score = y + cq), candidate region as int bits}
+  __shared__ int cnt_l[QMAX];        // rows of the region
+  __shared__ uint32_t flr_l[QMAX];   // score_key of the best row a full region dropped (0: none)
+  __shared__ int item_sh, eb_n, tnext;
+  __shared__ uint32_t pf_sink[64];   // the L2 prefetch's LDS-DMA target (never read)
+  // the item's emitted rows, staged in the LDS left over: (score bits, query slot << 23 | row offset)
+  constexpr int EB = (163840 - (int)sizeof(bl) - QMAX * 24 - 512) / 8;
+  __shared__ uint2 eb[EB];
+  const uint32_t bl_base = (uint32_t)(size_t)(lds_void *)bl;
+  const uint32_t sink = (uint32_t)(size_t)(lds_void *)pf_sink;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const char *hsrc = reinterpret_cast<const char *>(a.h16);
+
+  // measurement only (a.tdbg): per wave, cycles in the prologue, its tiles, the end-of-item barrier and
+  // the flush; items taken
+  uint64_t tb[5] = {0, 0, 0, 0, 0};
+  uint64_t tq = 0;
+  auto stamp = [&](int b) {
+    if (a.tdbg) {
+      const uint64_t now = __builtin_amdgcn_s_memtime();
+      if (b >= 0) tb[b] += now - tq;
+      tq = now;
+    }
+  };
+
+  for (;;) {
+    if (tid == 0) item_sh = atomicAdd(a.work, 1);
+    __syncthreads();
+    const int item = item_sh;
+    __syncthreads();  // every thread has read item_sh before thread 0 may rewrite it
+    if (item >= *a.n_items) {
+      if (a.tdbg && lane == 0)
+        for (int b = 0; b < 5; ++b) atomicAdd(a.tdbg + b, (unsigned long long)tb[b]);
+      return;
+    }
+    const ScanItem it = a.items[item];
+    stamp(-1);
+    tb[4] += 1;
+    const int qcnt = it.qcnt, ng = (qcnt + 31) >> 5;
+
+    // prologue: piece (j, s) = dims 16s + 8h .. +7 of query 32j + r in lane (r, h) (the B layout);
+    // an unused slot's threshold is NaN, so no row is ever emitted for it
+    {
+      const int npc = ng * KS;
+      for (int p = w; p < npc; p += NW) {
+        const int j = p / KS, s = p - j * KS;
+        const int qi = min(32 * j + r, qcnt - 1);
+        glds<16>(a.bq + (size_t)(it.qbeg + qi) * D + 16 * s + 8 * h, bl_base + (uint32_t)(p * 1024));
+      }
+      for (int i = tid; i < ng * 32; i += 64 * NW) {
+        float2 v = make_float2(0.0f, __builtin_nanf(""));
+        float cqv = 0.0f;
+        int o = -1;
+        if (i < qcnt) {
+          const int pos = it.qbeg + i;
+          const int slot = a.qlist[pos];
+          const float2 fc = a.qsc[pos];
+          const float T = a.thr ? a.thr[slot / a.nparts] + a.thr_bias : -INFINITY;
+          v = make_float2(fc.x, lower_thr(T, fc.y));
+          cqv = fc.y;
+          o = slot + it.part;
+        }
+        qf[i] = v;
+        qz[i] = make_float2(cqv, __int_as_float(o));
+        cnt_l[i] = 0;
+        flr_l[i] = 0u;
+      }
+      if (tid == 0) {
+        eb_n = 0;
+        tnext = NW;  // the waves' first tiles are taken in order
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces landed
+      __syncthreads();
+      stamp(0);
+    }
+
+    const int r0 = it.row_begin;  // multiple of 32
+    const int nt = (it.row_end - r0 + 31) >> 5;
+    const int rlim = (int)min((int64_t)it.row_end, (int64_t)a.row_limit);
+    const bool stage = it.row_end - r0 < (1 << 23);  // row offsets fit the staged word
+
+    // tile t for lane (r, h): the A fragments and the row terms of rows 8b + 4h .. +3
+    auto load = [&](int t, h8v (&A)[KS], f4v (&M)[4]) {
+      if constexpr (AB == 3) t = 0;
+      const char *tp = hsrc + (size_t)(r0 / 32 + t) * TB + lane * 16;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) A[s] = *reinterpret_cast<const h8v *>(tp + s * 1024);
+      const size_t mo = (size_t)(r0 + 32 * t) + 4 * h;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) M[b] = *reinterpret_cast<const f4v *>(a.mub + mo + 8 * b);
+    };
+    auto row_terms = [&](const f4v (&M)[4], int t, float (&mr)[16]) {
+      const int rt = r0 + 32 * t;
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mr[4 * b + i] = rt + 8 * b + 4 * h + i < rlim ? M[b][i] : -INFINITY;
+    };
+    auto read_b = [&](int j, h8v (&B)[KS]) {
+      const char *bp = bl + j * KS * 1024 + lane * 16;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) B[s] = *reinterpret_cast<const h8v *>(bp + s * 1024);
+    };
+    // a row of the candidate region of query slot qi (slot from its LDS counter; a full region keeps the
+    // best score it had to drop as its floor)
+    auto put = [&](int qi, float sc, int row) {
+      const int slot = atomicAdd(&cnt_l[qi], 1);
+      if (slot < a.cap) {
+        const size_t rb = (size_t)__float_as_int(qz[qi].y) * a.cap;
+        a.cand_s[rb + slot] = sc;
+        a.cand_k[rb + slot] = a.key_base | (uint32_t)row;
+      } else {
+        atomicMax(&flr_l[qi], score_key(sc));
+      }
+    };
+    // the rare emit branch: per row position e a wave-uniform test (one compare, a scalar branch)
+    auto emit_y = [&](const f16v &y, float thr, int qi, int rt) {
+      const float cq = qz[qi].x;
+      // the staged word of row position e is base + 8 (e >> 2) + (e & 3); the empty asm keeps the compiler
+      // from hoisting 16 per-position words out of the group loop (they spilled)
+      uint32_t base = ((uint32_t)qi << 23) | (uint32_t)(rt - r0 + 4 * h);
+      asm volatile("" : "+v"(base));
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const bool p = y[e] >= thr;
+        if (__builtin_amdgcn_ballot_w64(p) == 0ull) continue;
+        if (p) {
+          const float sc = y[e] + cq;
+          const uint32_t word = base + (uint32_t)(8 * (e >> 2) + (e & 3));
+          const int at = stage ? atomicAdd(&eb_n, 1) : EB;
+          if (at < EB) eb[at] = make_uint2(__float_as_uint(sc), word);
+          else put(qi, sc, r0 + (int)(word & 0x7FFFFFu));
+        }
+      }
+    };
+    // group j's scores y = f acc + row term, in place, and whether any can reach its query's threshold
+    auto epi_test = [&](f16v &acc, const float (&mr)[16], const float2 q) -> bool {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[v] = fmaf(q.x, acc[v], mr[v]);
+      float mx = max3f(acc[0], acc[1], acc[2]);
+      mx = max3f(mx, acc[3], acc[4]);
+      mx = max3f(mx, acc[5], acc[6]);
+      mx = max3f(mx, acc[7], acc[8]);
+      mx = max3f(mx, acc[9], acc[10]);
+      mx = max3f(mx, acc[11], acc[12]);
+      mx = max3f(mx, acc[13], acc[14]);
+      mx = fmaxf(mx, acc[15]);
+      if constexpr (AB == 1 || AB == 3) {
+        if (mx == 12345.0f) cnt_l[0] = 1;  // keep the scores live
+        return false;
+      }
+      return __builtin_amdgcn_ballot_w64(mx >= q.y) != 0ull;
+    };
+    // one tile against every group; tpf >= 0: the wave's next tile, pulled into L2 meanwhile
+    auto tile = [&](const h8v (&A)[KS], const float (&mr)[16], int t, int tpf) {
+      const int rt = r0 + 32 * t;
+      if constexpr (AB == 2) {  // consume the tile without scoring it
+        float v = mr[0];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) v += (float)A[s][0];
+        if (v == 12345.0f) cnt_l[0] = 1;
+        return;
+      }
+      for (int j = 0; j < ng; ++j) {
+        const float2 q = qf[32 * j + r];
+        h8v bj[KS];
+        read_b(j, bj);
+        f16v acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[0], bj[0], (f16v){}, 0, 0, 0);
+#pragma unroll
+        for (int s = 1; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[s], bj[s], acc, 0, 0, 0);
+        const bool e = epi_test(acc, mr, q);
+        // all of the group's operand reads before its chain (one LDS wait, not one per MFMA)
+        __builtin_amdgcn_sched_group_barrier(0x100, KS + 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, KS, 0);
+        if (j == 0 && tpf >= 0) {  // the tile's own loads were waited for before the chain: warm L2
+          glds<4>(hsrc + (size_t)(r0 / 32 + tpf) * TB + min(lane * 128, TB - 128), sink);
+          glds<4>(a.mub + r0 + 32 * tpf + (lane & 31), sink);
+        }
+        if (__builtin_expect(e, 0)) emit_y(acc, q.y, 32 * j + r, rt);
+      }
+    };
+
+    int t = w;
+    while (t < nt) {
+      h8v A[KS];
+      f4v M[4];
+      float mr[16];
+      load(t, A, M);
+      int tn = 0;
+      if (lane == 0) tn = atomicAdd(&tnext, 1);
+      tn = __builtin_amdgcn_readfirstlane(tn);
+      row_terms(M, t, mr);
+      tile(A, mr, t, tn < nt ? tn : -1);
+      t = tn;
+    }
+    stamp(1);
+    __syncthreads();
+    stamp(2);
+    for (int i = tid, n = min(eb_n, EB); i < n; i += 64 * NW) {  // the staged rows
+      const uint2 e = eb[i];
+      put((int)(e.y >> 23), __uint_as_float(e.x), r0 + (int)(e.y & 0x7FFFFFu));
+    }
+    __syncthreads();
+    for (int i = tid; i < qcnt; i += 64 * NW) {
+      const int o = __float_as_int(qz[i].y);
+      a.cand_n[o] = min(cnt_l[i], a.cap);
+      a.cand_f[o] = flr_l[i];
+    }
+    stamp(3);
+  }
+}
+
+template <int D, int MET>
+void launch_scan_dm(const StreamArgs &a, int max_items, hipStream_t st) {
+  const int grid = std::max(1, std::min(max_items, device_cus()));
+  if (a.ablate & 64) hipLaunchKernelGGL((scan_kernel<D, MET, 1>), dim3(grid), dim3(64 * NW), 0, st, a);
+  else if (a.ablate & 128) hipLaunchKernelGGL((scan_kernel<D, MET, 2>), dim3(grid), dim3(64 * NW), 0, st, a);
+  else if (a.ablate & 256) hipLaunchKernelGGL((scan_kernel<D, MET, 3>), dim3(grid), dim3(64 * NW), 0, st, a);
+  else hipLaunchKernelGGL((scan_kernel<D, MET>), dim3(grid), dim3(64 * NW), 0, st, a);
+}
+
+}  // namespace
+
+int scan_sample_values() { return SV; }
+
+void launch_scan_sample(const StreamArgs &a, int metric, int max_items, hipStream_t st) {
+  if (max_items <= 0) return;
+  const dim3 grid((unsigned)((int64_t)max_items * (512 / 32) / 4));
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, a); };
+  switch (a.dim) {
+    case 32: metric == L2 ? go(sample_kernel<32, L2>) : go(sample_kernel<32, IP>); return;
+    case 64: metric == L2 ? go(sample_kernel<64, L2>) : go(sample_kernel<64, IP>); return;
+    default: metric == L2 ? go(sample_kernel<128, L2>) : go(sample_kernel<128, IP>); return;
+  }
+}
+
+void launch_scan_main(const StreamArgs &a, int metric, int max_items, hipStream_t st) {
+  if (max_items <= 0) return;
+  switch (a.dim) {
+    case 32: metric == L2 ? launch_scan_dm<32, L2>(a, max_items, st) : launch_scan_dm<32, IP>(a, max_items, st); return;
+    case 64: metric == L2 ? launch_scan_dm<64, L2>(a, max_items, st) : launch_scan_dm<64, IP>(a, max_items, st); return;
+    default:
+      metric == L2 ? launch_scan_dm<128, L2>(a, max_items, st) : launch_scan_dm<128, IP>(a, max_items, st);
+      return;
+  }
+}
+
+}  // namespace pyr

@@ -383,268 +383,6 @@ __global__ __launch_bounds__(64 * SNW, 1) void stream16_kernel(StreamArgs a) {
   }
 }
 
-// the scheduling region of one group chain: each MFMA followed by the LDS read that refills its operand
-// registers for the next group and a share of the other accumulator's epilogue
-template <int KS>
-__device__ __forceinline__ void sched_pipe() {
-#pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // VALU
-  }
-}
-
-// ---- 2. / 4. the list scan on v_mfma_f32_32x32x16_f16 (round 4) ----
-// Same contract as stream16_kernel (one fp16 term), one MFMA shape up: a 32-row tile is ONE A operand
-// per 16-dim k-step (lane (r, h) holds row r, dims 16s + 8h .. +7: the tile layout is lane-linear for
-// it as it stands), a query group is 32 queries, and the 32 x 32 result leaves lane (r, h) query r's
-// scores of rows 8b + 4h + i (b, i < 4).  Per (tile, query group): 8 MFMAs of 32 cycles against
-// 8 ds_read_b128 of query operands and a 16-value epilogue -- half the LDS reads and half the MFMA
-// issue holds per flop of the 16x16x32 form, whose 8-cycle issue hold per 16-cycle MFMA plus the
-// epilogue left the SIMDs issue-bound (MFMA busy 39 %).
-// AB (measurement only, PYR_FILTER_ABLATE): 1 = no emission, 2 = tile stream only (no MFMA),
-// 3 = no emission and every tile read from the item's first one (compute without HBM)
-template <int D, int MET, bool SAMPLE, int AB = 0>
-__global__ __launch_bounds__(64 * SNW, 1) void stream32_kernel(StreamArgs a) {
-  constexpr int KS = D / 16;         // 32x32x16 k-steps
-  constexpr int TB = 64 * D;         // h16 bytes per 32-row tile
-  constexpr int QMAX = 512;          // queries per item
-  constexpr int PIECES = QMAX / 32 * KS;
-  __shared__ __attribute__((aligned(16))) char bl[PIECES * 1024];
-  __shared__ float2 qf[QMAX];        // per query slot: {f, threshold in y = f acc + row term space}
-  __shared__ float2 qz[QMAX];        // {cq (score = y + cq), region (MAIN) / sample row (SAMPLE) as int bits}
-  __shared__ int cnt_l[QMAX];
-  __shared__ uint32_t flr_l[QMAX];
-  __shared__ int item_sh;
-  const uint32_t bl_base = (uint32_t)(size_t)(lds_void *)bl;
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
-  const char *hsrc = reinterpret_cast<const char *>(a.h16);
-
-  for (;;) {
-    if (tid == 0) item_sh = atomicAdd(a.work, 1);
-    __syncthreads();
-    const int item = item_sh;
-    __syncthreads();
-    if (item >= *a.n_items) return;
-    const ScanItem it = a.items[item];
-    if (SAMPLE && it.part != 0) continue;
-    const int qcnt = it.qcnt, ng = (qcnt + 31) >> 5;
-    const int ng2 = SAMPLE ? ng : (ng + 1) & ~1;
-
-    // prologue: piece (j, s) = dims 16s + 8h .. +7 of query 32j + r in lane (r, h) (the B layout)
-    {
-      const int npc = ng * KS;
-      for (int p = w; p < npc; p += SNW) {
-        const int j = p / KS, s = p - j * KS;
-        const int qi = min(32 * j + r, qcnt - 1);
-        glds<16>(a.bq + (size_t)(it.qbeg + qi) * D + 16 * s + 8 * h, bl_base + (uint32_t)(p * 1024));
-      }
-      for (int i = tid; i < ng2 * 32; i += 64 * SNW) {
-        float2 v = make_float2(0.0f, __builtin_nanf(""));
-        float cqv = 0.0f;
-        int o = -1;
-        if (i < qcnt) {
-          const int pos = it.qbeg + i;
-          const int slot = a.qlist[pos];
-          const float2 fc = a.qsc[pos];
-          const int q = slot / a.nparts;
-          const float T = (!SAMPLE && a.thr) ? a.thr[q] + a.thr_bias : -INFINITY;
-          v = make_float2(fc.x, lower_thr(T, fc.y));
-          cqv = fc.y;
-          o = SAMPLE ? q * a.nprobe + (slot % a.nparts) / a.cmax : slot + it.part;
-        }
-        qf[i] = v;
-        qz[i] = make_float2(cqv, __int_as_float(o));
-        cnt_l[i] = 0;
-        flr_l[i] = 0u;
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-
-    const int r0 = it.row_begin;
-    int nt = (it.row_end - r0 + 31) >> 5;
-    if (SAMPLE) nt = min(nt, SAMPLE_TILES);
-    const int rlim = (int)min((int64_t)it.row_end, (int64_t)a.row_limit);
-
-    // tile t for lane (r, h): the A fragments and the row terms (RowStore::mub) of rows 8b + 4h .. +3
-    auto load = [&](int t, h8v (&A)[KS], f4v (&M)[4]) {
-      if constexpr (AB == 3) t = 0;
-      const char *tb = hsrc + (size_t)(r0 / 32 + t) * TB + lane * 16;
-#pragma unroll
-      for (int s = 0; s < KS; ++s) A[s] = *reinterpret_cast<const h8v *>(tb + s * 1024);
-      const size_t mo = (size_t)(r0 + 32 * t) + 4 * h;
-#pragma unroll
-      for (int b = 0; b < 4; ++b) M[b] = *reinterpret_cast<const f4v *>(a.mub + mo + 8 * b);
-    };
-    auto row_terms = [&](const f4v (&M)[4], int t, float (&mr)[16]) {
-      const int rt = r0 + 32 * t;
-#pragma unroll
-      for (int b = 0; b < 4; ++b)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) mr[4 * b + i] = rt + 8 * b + 4 * h + i < rlim ? M[b][i] : -INFINITY;
-    };
-    auto read_b = [&](int j, h8v (&B)[KS]) {
-      const char *bp = bl + j * KS * 1024 + lane * 16;
-#pragma unroll
-      for (int s = 0; s < KS; ++s) B[s] = *reinterpret_cast<const h8v *>(bp + s * 1024);
-    };
-    // group j's chain; behind each MFMA its operand registers take group jn's fragment of that k-step
-    auto mma_rot = [&](const h8v (&A)[KS], h8v (&B)[KS], f16v &acc, int jn) {
-      const char *bp = bl + jn * KS * 1024 + lane * 16;
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[0], B[0], (f16v){}, 0, 0, 0);
-      B[0] = *reinterpret_cast<const h8v *>(bp);
-#pragma unroll
-      for (int s = 1; s < KS; ++s) {
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[s], B[s], acc, 0, 0, 0);
-        B[s] = *reinterpret_cast<const h8v *>(bp + s * 1024);
-      }
-    };
-
-    if constexpr (SAMPLE) {
-      h8v A0[KS], A1[KS];
-      f4v M0[4], M1[4];
-      const bool h0 = w < nt, h1 = w + SNW < nt;
-      if (h0) load(w, A0, M0);
-      if (h1) load(w + SNW, A1, M1);
-      float mr0[16], mr1[16];
-      if (h0) row_terms(M0, w, mr0);
-      if (h1) row_terms(M1, w + SNW, mr1);
-      for (int j = 0; j < ng; ++j) {
-        const int qi = 32 * j + r;
-        const float f = qf[qi].x;
-        float mx0 = -INFINITY, mx1 = -INFINITY;
-        h8v B[KS];
-        read_b(j, B);
-        if (h0) {
-          f16v acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0[0], B[0], (f16v){}, 0, 0, 0);
-#pragma unroll
-          for (int s = 1; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0[s], B[s], acc, 0, 0, 0);
-#pragma unroll
-          for (int v = 0; v < 8; ++v) mx0 = fmaxf(mx0, fmaf(f, acc[v], mr0[v]));
-#pragma unroll
-          for (int v = 8; v < 16; ++v) mx1 = fmaxf(mx1, fmaf(f, acc[v], mr0[v]));
-        }
-        if (h1) {
-          f16v acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1[0], B[0], (f16v){}, 0, 0, 0);
-#pragma unroll
-          for (int s = 1; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1[s], B[s], acc, 0, 0, 0);
-#pragma unroll
-          for (int v = 0; v < 8; ++v) mx0 = fmaxf(mx0, fmaf(f, acc[v], mr1[v]));
-#pragma unroll
-          for (int v = 8; v < 16; ++v) mx1 = fmaxf(mx1, fmaf(f, acc[v], mr1[v]));
-        }
-        if (qi < qcnt) {
-          const float2 z = qz[qi];
-          float *sp = a.samp + (size_t)__float_as_int(z.y) * SV + w * 4 + 2 * h;
-          sp[0] = mx0 + z.x;
-          sp[1] = mx1 + z.x;
-        }
-      }
-    } else {
-      // the rare emit branch: every row of the lane with y >= the threshold goes to the query's region
-      // (one returning LDS atomic reserves the lane's slots; a full region keeps the best dropped score)
-      auto emit = [&](const f16v &acc, const float (&mr)[16], float f, float thr, int qi, int rt) {
-        uint32_t m = 0u;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) m |= (fmaf(f, acc[e], mr[e]) >= thr ? 1u : 0u) << e;
-        if (m == 0u) return;
-        int slot = atomicAdd(&cnt_l[qi], __builtin_popcount(m));
-        const float2 z = qz[qi];
-        const size_t rb = (size_t)__float_as_int(z.y) * a.cap;
-        // the passing rows in order (y recomputed: no 16-value array held across the atomic)
-        while (m) {
-          const int e = __builtin_ctz(m);
-          m &= m - 1u;
-          float acc_e = acc[0], mr_e = mr[0];
-#pragma unroll
-          for (int u = 1; u < 16; ++u)
-            if (e == u) acc_e = acc[u], mr_e = mr[u];
-          const float sc = fmaf(f, acc_e, mr_e) + z.x;
-          if (slot < a.cap) {
-            a.cand_s[rb + slot] = sc;
-            a.cand_k[rb + slot] = a.key_base | (uint32_t)(rt + 8 * (e >> 2) + 4 * h + (e & 3));
-          } else {
-            atomicMax(&flr_l[qi], score_key(sc));
-          }
-          ++slot;
-        }
-      };
-      auto epi = [&](const f16v &acc, const float (&mr)[16], int j, const float2 q, int rt) {
-        float y[16];
-#pragma unroll
-        for (int v = 0; v < 16; ++v) y[v] = fmaf(q.x, acc[v], mr[v]);
-        float mx = max3f(y[0], y[1], y[2]);
-        mx = max3f(mx, y[3], y[4]);
-        mx = max3f(mx, y[5], y[6]);
-        mx = max3f(mx, y[7], y[8]);
-        mx = max3f(mx, y[9], y[10]);
-        mx = max3f(mx, y[11], y[12]);
-        mx = max3f(mx, y[13], y[14]);
-        mx = fmaxf(mx, y[15]);
-        if constexpr (AB == 1 || AB == 3) {
-          if (mx == 12345.0f) cnt_l[0] = 1;
-          return;
-        }
-        if (__builtin_expect(__builtin_amdgcn_ballot_w64(mx >= q.y) != 0ull, 0))
-          emit(acc, mr, q.x, q.y, 32 * j + r, rt);
-      };
-      // one tile against every group: two accumulators, group j + 1's chain runs while group j's
-      // epilogue issues; the operand registers rotate (each k-step's fragment of the next group is
-      // read right behind the MFMA that consumed this group's)
-      auto tile = [&](const h8v (&A)[KS], const float (&mr)[16], int t) {
-        const int rt = r0 + 32 * t;
-        if constexpr (AB == 2) {  // consume the tile without scoring it
-          float v = mr[0];
-#pragma unroll
-          for (int s = 0; s < KS; ++s) v += (float)A[s][0];
-          if (v == 12345.0f) cnt_l[0] = 1;
-          return;
-        }
-        h8v b[KS];
-        f16v a0, a1;
-        read_b(0, b);
-        float2 q0 = qf[r], q1 = q0;
-        for (int j = 0; j < ng2; j += 2) {
-          mma_rot(A, b, a0, j + 1);
-          if (j > 0) epi(a1, mr, j - 1, q1, rt);
-          sched_pipe<KS>();
-          q1 = qf[32 * (j + 1) + r];
-          const int jn = min(j + 2, ng2 - 1);
-          mma_rot(A, b, a1, jn);
-          epi(a0, mr, j, q0, rt);
-          sched_pipe<KS>();
-          q0 = qf[32 * jn + r];
-        }
-        epi(a1, mr, ng2 - 1, q1, rt);
-      };
-      h8v A0[KS], A1[KS];
-      f4v M0[4], M1[4];
-      float mr[16];
-      int t = w;
-      if (t < nt) load(t, A0, M0);
-      while (t < nt) {
-        load(min(t + SNW, nt - 1), A1, M1);
-        row_terms(M0, t, mr);
-        tile(A0, mr, t);
-        t += SNW;
-        if (t >= nt) break;
-        load(min(t + SNW, nt - 1), A0, M0);
-        row_terms(M1, t, mr);
-        tile(A1, mr, t);
-        t += SNW;
-      }
-      __syncthreads();
-      for (int i = tid; i < qcnt; i += 64 * SNW) {
-        const int o = __float_as_int(qz[i].y);
-        a.cand_n[o] = min(cnt_l[i], a.cap);
-        a.cand_f[o] = flr_l[i];
-      }
-    }
-  }
-}
-
 // ---- 3. T_q = the R-th largest sample value (radix select over score keys, wselect.h) ----
 // The sample holds min(len, 512) rows of each probed list, so about R / f rows of the probed lists
 // reach T_q (f = the sampled fraction of the query's probed rows).  R adapts to f: the rows it
@@ -784,33 +522,12 @@ __global__ __launch_bounds__(256) void cand_merge_kernel(CandMergeArgs m) {
 
 inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
-int device_cus() {
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    hipDeviceProp_t p;
-    cus = hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0 ? p.multiProcessorCount : 256;
-  }
-  return cus;
-}
 
-int stream_mfma_shape() {  // PYR_STREAM_MFMA=16: the round-3 16x16x32 kernel (measurement only)
-  const char *e = getenv("PYR_STREAM_MFMA");
-  return e && atoi(e) == 16 ? 16 : 32;
-}
+
 
 template <int D, int MET, bool Q2>
 void launch_stream_dm(const StreamArgs &a, int max_items, bool sample, hipStream_t st) {
   const int grid = std::max(1, std::min(max_items, device_cus()));
-  if (!Q2 && stream_mfma_shape() == 32) {
-    if (sample) hipLaunchKernelGGL((stream32_kernel<D, MET, true>), dim3(grid), dim3(64 * SNW), 0, st, a);
-    else if (a.ablate & 64) hipLaunchKernelGGL((stream32_kernel<D, MET, false, 1>), dim3(grid), dim3(64 * SNW), 0, st, a);
-    else if (a.ablate & 128) hipLaunchKernelGGL((stream32_kernel<D, MET, false, 2>), dim3(grid), dim3(64 * SNW), 0, st, a);
-    else if (a.ablate & 256) hipLaunchKernelGGL((stream32_kernel<D, MET, false, 3>), dim3(grid), dim3(64 * SNW), 0, st, a);
-    else hipLaunchKernelGGL((stream32_kernel<D, MET, false>), dim3(grid), dim3(64 * SNW), 0, st, a);
-    return;
-  }
   if (sample) hipLaunchKernelGGL((stream16_kernel<D, MET, Q2, true>), dim3(grid), dim3(64 * SNW), 0, st, a);
   else if (a.ablate & 64) hipLaunchKernelGGL((stream16_kernel<D, MET, Q2, false, true>), dim3(grid), dim3(64 * SNW), 0, st, a);
   else hipLaunchKernelGGL((stream16_kernel<D, MET, Q2, false>), dim3(grid), dim3(64 * SNW), 0, st, a);
@@ -825,6 +542,17 @@ void launch_stream_d(const StreamArgs &a, int metric, int max_items, bool sample
 }
 
 }  // namespace
+
+int device_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    hipDeviceProp_t p;
+    cus = hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0 ? p.multiProcessorCount : 256;
+  }
+  return cus;
+}
 
 bool stream16_supported(int dim, int metric, int k1) {
   if (metric != L2 && metric != IP) return false;
