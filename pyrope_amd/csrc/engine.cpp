@@ -2610,6 +2610,14 @@ struct IvfPqIndex : Index {
   DevMem cb;                         // [M][ksub][sub]
   int ksub = 0;
   int64_t ncode_rows = 0;
+  // the matrix-core list scan (pq32.hip): tile code layout, |x^|^2 per position, fp16 codebook and its
+  // power-of-two scale, the per-position row terms (cached for (pq_gen, kr)); pq_gen advances with clive
+  bool pq32_ready = false;
+  DevMem cpack, nrm, cb16, pmeta, pmub;
+  float cbsx = 1.0f;
+  uint64_t pq_gen = 1, pmub_gen = 0;
+  float pmub_kr = 0.0f;
+  int64_t pq_max_len = 0;
   bool built = false;
   int nprobe_default;
   std::vector<float> given;
@@ -2654,6 +2662,7 @@ struct IvfPqIndex : Index {
     HIPCHK(hipMemcpyAsync(stage_b.p, slots.data(), sizeof(int64_t) * slots.size(), hipMemcpyHostToDevice, wst));
     launch_scatter_u8(clive.as<uint8_t>(), stage_b.as<int64_t>(), v, (int64_t)slots.size(), wst);
     HIPCHK(hipStreamSynchronize(wst));
+    ++pq_gen;
   }
 
   void add(const float *x, int64_t n, const int64_t *labels, bool) override {  // :37-47
@@ -2806,6 +2815,32 @@ struct IvfPqIndex : Index {
     dsrc.ensure(sizeof(int64_t) * std::max<int64_t>(tot, 1));
     HIPCHK(hipMemcpyAsync(dsrc.p, src.data(), sizeof(int64_t) * tot, hipMemcpyHostToDevice, wst));
     launch_pack_codes(codes_rm, dsrc.as<int64_t>(), tot, M, codes.as<uint8_t>(), wst);
+    pq32_ready = false;
+    if (pq32_supported(dim, M, ksub, 10)) {
+      // tile code layout + |x^|^2 per position; fp16 codebook with a power-of-two scale keeping max |C| < 2^14
+      const int64_t tiles = (tot + 31) / 32;
+      cpack.ensure((size_t)std::max<int64_t>(tiles, 1) * 64 * pq32_code_bytes(dim));
+      HIPCHK(hipMemsetAsync(cpack.p, 0, (size_t)std::max<int64_t>(tiles, 1) * 64 * pq32_code_bytes(dim), wst));
+      nrm.ensure(sizeof(float) * (size_t)std::max<int64_t>(tiles * 32, 1));
+      HIPCHK(hipMemsetAsync(nrm.p, 0, sizeof(float) * (size_t)std::max<int64_t>(tiles * 32, 1), wst));
+      launch_pq32_pack(codes_rm, dsrc.as<int64_t>(), tot, M, cb.as<float>(), ksub, cpack.as<uint8_t>(), nrm.as<float>(),
+                       wst);
+      std::vector<float> hcb((size_t)M * ksub * sub);
+      HIPCHK(hipMemcpyAsync(hcb.data(), cb.p, sizeof(float) * hcb.size(), hipMemcpyDeviceToHost, wst));
+      HIPCHK(hipStreamSynchronize(wst));
+      float am = 0.0f;
+      bool fin = true;
+      for (float v : hcb) {
+        fin = fin && std::isfinite(v);
+        am = std::max(am, std::fabs(v));
+      }
+      cbsx = pow2_scale_host(am);
+      cb16.ensure(sizeof(uint16_t) * (size_t)M * 256 * 8);
+      launch_pq32_cb16(cb.as<float>(), M, ksub, cbsx, cb16.as<_Float16>(), wst);
+      HIPCHK(hipGetLastError());
+      pq32_ready = fin;
+      ++pq_gen;
+    }
     hlive.assign(tot, 0);
     for (int64_t p = 0; p < tot; p++) hlive[p] = src[p] >= 0;
     clive.ensure(std::max<int64_t>(tot, 1));
@@ -2813,6 +2848,8 @@ struct IvfPqIndex : Index {
     HIPCHK(hipMemcpyAsync(clive.p, hlive.data(), tot, hipMemcpyHostToDevice, wst));
     HIPCHK(hipMemcpyAsync(clabels.p, hlabels.data(), sizeof(int64_t) * tot, hipMemcpyHostToDevice, wst));
     ncode_rows = tot;
+    pq_max_len = 0;
+    for (int32_t v : cnt) pq_max_len = std::max<int64_t>(pq_max_len, v);
     pos_of.clear();
     for (int64_t p = 0; p < tot; p++)
       if (hlabels[p] >= 0) pos_of[hlabels[p]] = p;
@@ -2833,6 +2870,211 @@ struct IvfPqIndex : Index {
     }
     const int nprobe = prm.nprobe < 0 ? nprobe_default : prm.nprobe;
     const int probes = (built && coarse.nlist > 0) ? std::max(0, std::min(nprobe, coarse.nlist)) : 0;
+    // the matrix-core scan: built lists only (no buffer rows), the P1 geometry (pq32_supported)
+    const char *pm = getenv("PYR_PQ_MFMA");  // 0: the LUT scan below (A/B and the re-run path)
+    if (!(pm && atoi(pm) == 0) && pq32_ready && probes > 0 && buf.live_count() == 0 && filter_enabled() &&
+        pq32_supported(dim, M, ksub, k)) {
+      search_pq32(d_q, nq, k, probes, d_s, d_l, d_c, ws);
+      return;
+    }
+    search_lut(d_q, nq, k, probes, d_s, d_l, d_c, ws);
+  }
+
+  // the per-position row terms of the fp16 filter: -|x^|^2 (or -inf when not visible) + kr |x^|^2
+  const float *pq_row_terms(float kr, Workspace &ws) {
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    const int64_t tot = (ncode_rows + 31) / 32 * 32;
+    if (pmub_gen == pq_gen && pmub_kr == kr && pmub.n >= sizeof(float) * tot) return pmub.as<float>();
+    pmeta.ensure(sizeof(float) * std::max<int64_t>(tot, 1));
+    pmub.ensure(sizeof(float) * std::max<int64_t>(tot, 1));
+    HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(pmeta.p), (int)0xFF800000u, tot, ws.st));
+    launch_pq32_meta(nrm.as<float>(), clive.as<uint8_t>(), ncode_rows, pmeta.as<float>(), ws.st);
+    launch_row_terms(pmeta.as<float>(), nrm.as<float>(), nullptr, tot, L2, kr, 0.0f, pmub.as<float>(), ws.st);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(ws.st));
+    pmub_gen = pq_gen;
+    pmub_kr = kr;
+    return pmub.as<float>();
+  }
+
+  // IvfPqVectorIndex.Search (:118-212) on the matrix cores (pq32.hip): coarse ranking, per (list chunk,
+  // <= 64 queries) item the decoded rows' approximate ADC bounds -> rows reaching the query's sampled
+  // threshold -> the reference's ADC sum of the best 64, certified; what fails re-runs on the LUT scan.
+  void search_pq32(const float *d_q, int64_t nq, int k, int probes, float *d_s, int64_t *d_l, int32_t *d_c,
+                   Workspace &ws) {
+    const int k1 = filter_k1(k);
+    const int cap = stream_cap();
+    IvfChunking ch{(int32_t)stream_chunk(), 1, 0};
+    ch.cmax = ivf_list_chunks((int)pq_max_len, ch);
+    if ((int64_t)probes * ch.cmax > MAX_PARTS) {
+      const int64_t room = std::max<int64_t>(1, MAX_PARTS / std::max(probes, 1));
+      ch.chunk = (int32_t)round_up(std::max<int64_t>(32, (pq_max_len + room - 1) / room), 32);
+      ch.cmax = ivf_list_chunks((int)pq_max_len, ch);
+    }
+    const int nparts = probes * ch.cmax;
+    if (nparts > MAX_PARTS) throw Error(PYR_E_ARG, "nprobe too large");
+    const int64_t per_q = (int64_t)nparts * cap * 8;
+    const int64_t qs = std::max<int64_t>(1, std::min<int64_t>(nq, (int64_t(16) << 30) / per_q));
+    for (int64_t a0 = 0; a0 < nq; a0 += qs) {
+      const int64_t n = std::min(qs, nq - a0);
+      pq32_slice(d_q + a0 * dim, n, k, k1, probes, ch, nparts, cap, d_s + a0 * k, d_l + a0 * k,
+                 d_c ? d_c + a0 : nullptr, ws);
+    }
+  }
+
+  void pq32_slice(const float *d_q, int64_t nq, int k, int k1, int probes, IvfChunking ch, int nparts, int cap,
+                  float *d_s, int64_t *d_l, int32_t *d_c, Workspace &ws) {
+    {
+      PhaseTimer t(PH_COARSE, ws.st, nq * coarse.nlist);
+      prep_queries(d_q, nq, dim, metric, ws);
+      coarse.probe(d_q, metric == COS ? ws.qn.as<float>() : nullptr, nq, probes, metric, ws);
+    }
+    int maxi;
+    {
+      PhaseTimer t(PH_ITEMS, ws.st);
+      maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, pq32_qmax(), ch, 0, true);
+    }
+    const int64_t npos = nq * probes;
+    const int sv = pq32_sample_values();
+    const size_t nslot = (size_t)nq * nparts;
+    ws.sbq.ensure(sizeof(uint16_t) * std::max<int64_t>(npos, 1) * dim);
+    ws.sqsc.ensure(sizeof(float2) * std::max<int64_t>(npos, 1));
+    ws.ssamp.ensure(sizeof(float) * std::max<int64_t>(npos, 1) * sv);
+    ws.sthr.ensure(sizeof(float) * nq);
+    ws.scs.ensure(sizeof(float) * nslot * cap);
+    ws.sck.ensure(sizeof(uint32_t) * nslot * cap);
+    ws.scn.ensure(sizeof(int32_t) * nslot);
+    ws.scf.ensure(sizeof(uint32_t) * nslot);
+    ws.swork.ensure(sizeof(int32_t) * 2);
+    HIPCHK(hipMemsetAsync(ws.scn.p, 0, sizeof(int32_t) * nslot, ws.st));
+    HIPCHK(hipMemsetAsync(ws.scf.p, 0, sizeof(uint32_t) * nslot, ws.st));
+    HIPCHK(hipMemsetAsync(ws.swork.p, 0, sizeof(int32_t) * 2, ws.st));
+    StreamArgs sa{};
+    sa.h16 = cpack.p;
+    sa.queries = d_q;
+    sa.cents = coarse.rm.as<float>();
+    sa.sx = cbsx;
+    sa.items = ws.items.as<ScanItem>();
+    sa.n_items = ws.nitems.as<int32_t>();
+    sa.qlist = ws.qlist.as<int32_t>();
+    sa.nparts = nparts;
+    sa.nprobe = probes;
+    sa.cmax = ch.cmax;
+    sa.dim = dim;
+    sa.bq = ws.sbq.as<_Float16>();
+    sa.qsc = ws.sqsc.as<float2>();
+    sa.samp = ws.ssamp.as<float>();
+    sa.thr = ws.sthr.as<float>();
+    sa.cand_s = ws.scs.as<float>();
+    sa.cand_k = ws.sck.as<uint32_t>();
+    sa.cand_n = ws.scn.as<int32_t>();
+    sa.cand_f = ws.scf.as<uint32_t>();
+    sa.cap = cap;
+    sa.work = ws.swork.as<int32_t>();
+    sa.key_base = 0;
+    sa.row_limit = 0xFFFFFFFFu;
+    sa.ablate = filter_ablate();
+    // the fp16 filter's bound with x^ in the role of x - c: X = |x^| (nrm), A = |r|
+    stream_ub_terms(dim, L2, filter_f16_cerr(dim, L2, FILTER_F16X1), filter_cerr(dim),
+                    filter_f16_abs(dim, L2, cbsx, FILTER_F16X1), sa);
+    sa.mub = pq_row_terms(sa.kr, ws);
+    {
+      PhaseTimer t(PH_SAMPLE, ws.st);
+      launch_pq32_prep(sa, maxi, ws.st);
+      launch_pq32_scan(sa, cb16.as<_Float16>(), maxi, true, ws.st);
+      StreamSelectArgs sel{};
+      sel.samp = ws.ssamp.as<float>();
+      sel.nq = nq;
+      sel.n = probes * sv;
+      stream_rank(k1, sel.rmin, sel.rmax, sel.et);
+      sel.probes = ws.probes.as<int32_t>();
+      sel.nprobe = probes;
+      sel.lb = dlb.as<int32_t>();
+      sel.le = dle.as<int32_t>();
+      sel.thr = ws.sthr.as<float>();
+      launch_stream_select(sel, ws.st);
+    }
+    sa.work = ws.swork.as<int32_t>() + 1;
+    {
+      PhaseTimer t(PH_PQ_SCAN, ws.st, prof().on ? probed_rows(ws, nq, probes, le, lb) : 0);
+      launch_pq32_scan(sa, cb16.as<_Float16>(), maxi, false, ws.st);
+    }
+    ws.ms.ensure(sizeof(float) * nq * STREAM_KO);
+    ws.mk.ensure(sizeof(int32_t) * nq * STREAM_KO);
+    {
+      PhaseTimer t(PH_MERGE, ws.st);
+      CandMergeArgs m{};
+      m.cand_s = ws.scs.as<float>();
+      m.cand_k = ws.sck.as<uint32_t>();
+      m.cand_n = ws.scn.as<int32_t>();
+      m.cand_f = ws.scf.as<uint32_t>();
+      m.thr = ws.sthr.as<float>();
+      m.nq = nq;
+      m.nparts = nparts;
+      m.cap = cap;
+      m.out_s = ws.ms.as<float>();
+      m.out_k = ws.mk.as<int32_t>();
+      launch_cand_merge(m, ws.st);
+    }
+    ws.fail.ensure(sizeof(int32_t) * nq);
+    ws.fail2.ensure(sizeof(int32_t) * nq);
+    ws.fail_cnt.ensure(sizeof(int32_t));
+    ws.fail_cnt2.ensure(sizeof(int32_t));
+    HIPCHK(hipMemsetAsync(ws.fail_cnt.p, 0, sizeof(int32_t), ws.st));
+    HIPCHK(hipMemsetAsync(ws.fail_cnt2.p, 0, sizeof(int32_t), ws.st));
+    PqRefineArgs r{};
+    r.queries = d_q;
+    r.cents = coarse.rm.as<float>();
+    r.codebooks = cb.as<float>();
+    r.cpack = cpack.as<uint8_t>();
+    r.labels = clabels.as<int64_t>();
+    r.lb = dlb.as<int32_t>();
+    r.ms = ws.ms.as<float>();
+    r.mk = ws.mk.as<int32_t>();
+    r.nq = nq;
+    r.ld = STREAM_KO;
+    r.k = k;
+    r.dim = dim;
+    r.M = M;
+    r.ksub = ksub;
+    r.mb = pq32_code_bytes(dim);
+    r.nlist = coarse.nlist;
+    r.out_s = d_s;
+    r.out_l = d_l;
+    r.out_c = d_c;
+    int32_t nf = 0;
+    {
+      PhaseTimer t(PH_REFINE, ws.st, nq * k1);
+      r.k1 = k1;
+      r.fail_list = ws.fail2.as<int32_t>();
+      r.fail_cnt = ws.fail_cnt2.as<int32_t>();
+      launch_pq32_refine(r, nq, ws.st);
+      r.k1 = STREAM_KO;  // the failures again at depth 64, from the same candidates
+      r.qsel = ws.fail2.as<int32_t>();
+      r.nsel = ws.fail_cnt2.as<int32_t>();
+      r.fail_list = ws.fail.as<int32_t>();
+      r.fail_cnt = ws.fail_cnt.as<int32_t>();
+      launch_pq32_refine(r, nq, ws.st);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemcpyAsync(&nf, ws.fail_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, ws.st));
+      HIPCHK(hipStreamSynchronize(ws.st));
+    }
+    if (getenv("PYR_STREAM_DEBUG")) {
+      int32_t n1 = 0;
+      HIPCHK(hipMemcpy(&n1, ws.fail_cnt2.p, sizeof(int32_t), hipMemcpyDeviceToHost));
+      fprintf(stderr, "[pq32] nq %lld: certificate failures depth %d %d, depth 64 %d\n", (long long)nq, k1, n1, nf);
+    }
+    // what neither depth certifies: the LUT scan of those queries (same coarse ranking, same arithmetic)
+    filter_fallback(ws, nf, d_q, dim, k, d_s, d_l, d_c,
+                    [&](const float *q2, int64_t n2, float *s2, int64_t *l2, int32_t *c2) {
+                      search_lut(q2, n2, k, probes, s2, l2, c2, ws.nested());
+                    });
+  }
+
+  // the reference's per-row LUT sum on the LDS (pq_adc4 / pq_adc / pq_scan)
+  void search_lut(const float *d_q, int64_t nq, int k, int probes, float *d_s, int64_t *d_l, int32_t *d_c,
+                  Workspace &ws) {
     const int64_t bcut = buf.st.n;
     // list-scan kernel: pq_adc4 (4 queries per LDS gather; lists split into PQ4_ROWS-row chunks),
     // else pq_adc, else the first-cut pq_scan; PYR_PQ_ADC=1 / 0 force the latter two (A/B only)

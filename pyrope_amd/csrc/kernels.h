@@ -402,6 +402,40 @@ void launch_row_terms(const float *meta, const float *rsq16, const float *rsq, i
 // filter.hip): products A X go to (A^2 + X^2) / 2, (A + X)^2 to 2 (A^2 + X^2), so the bound of a row
 // no longer depends on its list's largest residual; the reference's own sum deviation (g) is folded in.
 void stream_ub_terms(int dim, int metric, double c_bf, double c_err, double c_abs, StreamArgs &a);
+// ---- IVF_PQ on the matrix cores (pq32.hip): the stream pipeline of the IVF_FLAT scan over rows decoded
+// from their codes; dsub = 8 and D = 768 (P1) ----
+bool pq32_supported(int dim, int M, int ksub, int k);
+int pq32_qmax();                    // queries per item
+int pq32_sample_values();           // sample values per (query, probe)
+int pq32_code_bytes(int dim);       // code bytes per lane per 32-row tile (MB)
+// codes (row-major, source rows) -> the tile layout cpack [tile][64 lanes][MB] of the list-major positions
+// (src: position -> source row or -1) and |x^|^2 per position (fp32 codebooks [M][ksub][8])
+void launch_pq32_pack(const uint8_t *codes_rm, const int64_t *src, int64_t tot, int M, const float *cb, int ksub,
+                      uint8_t *cpack, float *nrm, hipStream_t st);
+void launch_pq32_cb16(const float *cb, int M, int ksub, float sc, _Float16 *cb16, hipStream_t st);
+void launch_pq32_meta(const float *nrm, const uint8_t *live, int64_t tot, float *meta, hipStream_t st);
+// StreamArgs as for the IVF_FLAT stream scan, with h16 = cpack, mub = the row terms, cents = coarse
+// centroids, sx = the codebook scale
+void launch_pq32_prep(const StreamArgs &a, int max_items, hipStream_t st);
+void launch_pq32_scan(const StreamArgs &a, const _Float16 *cb16, int max_items, bool sample, hipStream_t st);
+struct PqRefineArgs {
+  const float *queries;     // nq x D
+  const float *cents;       // coarse centroids, row-major
+  const float *codebooks;   // fp32 [M][ksub][8]
+  const uint8_t *cpack;     // tile code layout
+  const int64_t *labels;    // per position
+  const int32_t *lb;        // list starts (positions)
+  const float *ms;          // merged candidate bounds [nq][ld]
+  const int32_t *mk;        // their positions (-2 floor, -1 none)
+  const int32_t *qsel, *nsel;  // refine only these queries (null: all nq)
+  int64_t nq;
+  int32_t ld, k1, k, dim, M, ksub, mb, nlist;
+  float *out_s;
+  int64_t *out_l;
+  int32_t *out_c;
+  int32_t *fail_list, *fail_cnt;
+};
+void launch_pq32_refine(const PqRefineArgs &a, int64_t nq, hipStream_t st);
 struct CandMergeArgs {
   const float *cand_s;
   const uint32_t *cand_k;
