@@ -440,16 +440,8 @@ static int filter_waves_ivf(int k1, int prec) {
   if (w == 16 && prec16(prec) && k1 == 16) return 16;
   return (w == 8 && prec == FILTER_BF16X3) ? 8 : 4;
 }
-// rows-as-A list scan (filter16r.hip, 384 / 512-query items) for the fp16 IVF filter at K1 = 16 / 32;
-// PYR_F16_RK=1 selects it (A/B measurement while it is tuned; results identical), default the
-// round-2 mfma_filter16w
-static bool use_rk(int dim, int metric, int k1, int prec) {
-  const char *e = getenv("PYR_F16_RK");
-  if (!(e && atoi(e) != 0)) return false;
-  return prec16(prec) && filter16r_supported(dim, metric, k1);
-}
 // stream-and-emit list scan (stream16.hip) for the fp16 IVF filter: PYR_IVF_STREAM=0 -> the round-2
-// list scans (filter16.hip / filter16r.hip)
+// list scans (filter16.hip)
 static bool stream_enabled() {
   const char *e = getenv("PYR_IVF_STREAM");
   return !(e && atoi(e) == 0);
@@ -1947,17 +1939,16 @@ struct IvfFlatIndex : Index {
     uint32_t *gthr = shared_bounds(ws, nq);
     const int prec_used = filter_prec_for(filter_prec(), lists.f16, std::max(ch.chunk, ch.warm));
     const int waves = filter_waves_ivf(k1, prec_used);
-    const bool rk = use_rk(dim, metric, k1, prec_used);
-    const int qc = filter_qchunk(prec_used, waves, rk);
+    const int qc = filter_qchunk(prec_used, waves);
     int maxi, maxi_main = 0;
     {
       PhaseTimer t(PH_ITEMS, ws.st);
       if (seed) {
-        maxi = build_ivf_items_range(ws, 0, nq, probes, 0, 1, nparts, coarse.nlist, dlb, dle, qc, ch, rk);
-        maxi_main = build_ivf_items_range(ws, 1, nq, probes, 1, probes, nparts, coarse.nlist, dlb, dle, qc, ch, rk);
+        maxi = build_ivf_items_range(ws, 0, nq, probes, 0, 1, nparts, coarse.nlist, dlb, dle, qc, ch);
+        maxi_main = build_ivf_items_range(ws, 1, nq, probes, 1, probes, nparts, coarse.nlist, dlb, dle, qc, ch);
       } else {
-        maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qc, ch, 0, rk);
-        if (ch.warm > 0) maxi_main = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qc, ch, 1, rk);
+        maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qc, ch, 0);
+        if (ch.warm > 0) maxi_main = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qc, ch, 1);
       }
     }
     FilterArgs fa{};
@@ -1980,7 +1971,6 @@ struct IvfFlatIndex : Index {
     fa.pub_mask = filter_pub_mask();
     fa.prec = prec_used;
     fa.waves = waves;
-    fa.rk = rk ? 1 : 0;
     fa.xcd = filter_xcd();
     fa.single = getenv("PYR_FILTER_SB") ? atoi(getenv("PYR_FILTER_SB")) != 0 : 0;
     // 2: a wave with survivors appends at raised priority (I1 list scan -1.5 %, profiles/r2_wide/)
@@ -2001,8 +1991,7 @@ struct IvfFlatIndex : Index {
     {
       PhaseTimer t(PH_LIST_SCAN, ws.st, prof().on ? probed_rows(ws, nq, probes, le, lb) : 0);
       auto launch = [&](int mi) {
-        if (rk) launch_filter16r(fa, metric, mi, ws.st);
-        else if (use16) launch_filter16(fa, metric, mi, ws.st);
+        if (use16) launch_filter16(fa, metric, mi, ws.st);
         else launch_filter(fa, metric, mi, ws.st);
       };
       launch(maxi);
@@ -2017,23 +2006,11 @@ struct IvfFlatIndex : Index {
       uint32_t h[4] = {0, 0, 0, 0};
       HIPCHK(hipMemcpyAsync(h, dbg.p, 16, hipMemcpyDeviceToHost, ws.st));
       HIPCHK(hipStreamSynchronize(ws.st));
-      if (rk) fprintf(stderr, "[filter16r] wave insert passes %u\n", h[0]);
-      else fprintf(stderr, "[filter] %s %u, candidates %u, %s %u\n", use16 ? "survivor wave-tiles" : "wave insert-loop iterations",
+      fprintf(stderr, "[filter] %s %u, candidates %u, %s %u\n", use16 ? "survivor wave-tiles" : "wave insert-loop iterations",
               h[0], h[1], use16 ? "owner drains" : "owner stages", h[2]);
       if (use16) fprintf(stderr, "[filter] shared-bound refreshes that raised a threshold %u\n", h[3]);
     }
-    if (fa.tdbg && rk) {
-      unsigned long long c[8];
-      HIPCHK(hipMemcpyAsync(c, fa.tdbg, sizeof(c), hipMemcpyDeviceToHost, ws.st));
-      HIPCHK(hipStreamSynchronize(ws.st));
-      const double tot = (double)c[5];
-      fprintf(stderr,
-              "[filter16r cycles] total %.4g wave-cycles: prologue %.1f%%, wait+barrier %.1f%%, refresh+issue %.1f%%, "
-              "compute %.1f%%, epilogue %.1f%%; items %llu, wave-tiles %llu, cycles per wave-tile %.0f, "
-              "per item-wave %.0f\n",
-              tot, 100 * c[0] / tot, 100 * c[1] / tot, 100 * c[2] / tot, 100 * c[3] / tot, 100 * c[4] / tot, c[6],
-              c[7], c[7] ? tot / c[7] : 0.0, c[6] ? tot / c[6] / 8 : 0.0);
-    } else if (fa.tdbg) {
+    if (fa.tdbg) {
       unsigned long long c[8];
       HIPCHK(hipMemcpyAsync(c, fa.tdbg, sizeof(c), hipMemcpyDeviceToHost, ws.st));
       HIPCHK(hipStreamSynchronize(ws.st));

@@ -1,4 +1,4 @@
-// f16util.h -- device helpers shared by the fp16 tile list scans (filter16.hip, filter16r.hip).
+// f16util.h -- device helpers shared by the fp16 tile list scans (filter16.hip, stream16.hip, scan.hip, pq32.hip).
 // Internal to libpyrope_hip.so; include inside an anonymous namespace of a .hip file's pyr namespace.
 // (include after <hip/hip_runtime.h> and <cmath>)
 #pragma once

@@ -25,8 +25,8 @@ enum Metric { L2 = 0, IP = 1, COS = 2 };
 
 constexpr uint32_t KEY_NONE = 0xFFFFFFFFu;
 constexpr uint32_t KEY_BUF = 0x80000000u;  // buffer rows: KEY_BUF | slot (DESIGN.md "Tie rule")
-// a part-list placeholder of the rows-as-A list scan (filter16r.hip): a score that bounds rows the part
-// dropped; the merge ranks it like a row, the refine certifies against it and never re-scores it
+// a candidate-list placeholder of the stream scans (stream16.hip, scan.hip): a score that bounds rows a
+// region dropped; the merge ranks it like a row, the refine certifies against it and never re-scores it
 constexpr uint32_t KEY_FLOOR = 0xFFFFFFFEu;
 constexpr int QCHUNK = 128;                // queries per scan work item (fast kernel)
 constexpr int QCHUNK_GENERIC = 64;         // queries per scan work item (generic kernel)
@@ -324,16 +324,13 @@ struct FilterArgs {
   int32_t prio;              // filter16w: 1 = s_setprio 1 for waves 4-7 (PYR_F16_PRIO, measurement knob)
   unsigned long long *tdbg;  // measurement only (PYR_FILTER_DEBUG=2, filter16): per-wave cycle buckets
                              // [wait, refresh, compute, append, drain, total, prologue, wave-tiles]
-  int32_t rk;                // 1: rows-as-A list scan (filter16r.hip), items of filter16r_qpb() queries
 };
 constexpr int FILTER_FP32 = 0;    // v_mfma_f32_32x32x2_f32
 constexpr int FILTER_BF16X3 = 1;  // hi/lo bf16 split, 3 x v_mfma_f32_32x32x16_bf16
 constexpr int FILTER_F16X2 = 2;   // fp16 row tiles x two-term fp16 queries, 2 x v_mfma_f32_32x32x16_f16
 constexpr int FILTER_F16X1 = 3;   // fp16 row tiles x one-term fp16 queries, 1 MFMA per k-step
 // queries per filter work item (items must be built with this qchunk)
-int filter16r_qpb(int prec);  // queries per item of the rows-as-A list scan (filter16r.hip block shape)
-inline int filter_qchunk(int prec, int waves, int rk = 0) {
-  if (rk) return filter16r_qpb(prec);
+inline int filter_qchunk(int prec, int waves) {
   return (prec == FILTER_BF16X3 && waves == 8) || ((prec == FILTER_F16X2 || prec == FILTER_F16X1) && waves == 16)
              ? 256
              : 128;
@@ -546,9 +543,6 @@ bool filter_supported(int dim, int metric, int k1);
 int filter16_max_rows();  // rows per scan item the fp16 filter accepts
 bool filter16_supported(int dim, int metric, int k1);
 void launch_filter16(const FilterArgs &a, int metric, int max_items, hipStream_t st);
-// rows-as-A fp16 list scan (filter16r.hip): items of <= filter16r_qpb() queries, K1 16 / 32
-bool filter16r_supported(int dim, int metric, int k1);
-void launch_filter16r(const FilterArgs &a, int metric, int max_items, hipStream_t st);
 // fp16 tiles of blocked fp32 rows (slots[i], or rows [0, n)), scaled by sx; with cents (row-major)
 // and tile_list (list of each 32-row tile) the residuals x - c[list] (IVF lists)
 // rn (may be null): the rows' meta norms; a non-finite one zeroes the row's tile (encode16_kernel)

@@ -515,7 +515,7 @@ __global__ __launch_bounds__(256) void merge_keys_kernel(const float *ps, const 
       if (out_keys) out_keys[o] = (int32_t)bk;
       if (out_l) {
         int64_t lab;
-        if (bk == KEY_FLOOR) lab = -1;  // a part's floor placeholder (filter16r.hip): no row
+        if (bk == KEY_FLOOR) lab = -1;  // a region's floor placeholder (stream scans): no row
         else if (bk & KEY_BUF) lab = buf_labels ? buf_labels[bk & ~KEY_BUF] : (int64_t)(bk & ~KEY_BUF);
         else lab = row_labels ? row_labels[bk] : (int64_t)bk;
         out_l[o] = lab;
