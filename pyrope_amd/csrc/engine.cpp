@@ -814,6 +814,9 @@ static int64_t read_rows(ImageReader &r, uint32_t tag_labels, uint32_t tag_rows,
 // ---------------------------------------------------------------------------
 // FLAT = BruteForceVectorIndex (BruteForceVectorIndex.cs)
 // ---------------------------------------------------------------------------
+static int build_ivf_items(Workspace &ws, int64_t nq, int nprobe, int nparts, int nlist, const DevMem &lbeg,
+                           const DevMem &lend, int qchunk, IvfChunking ch, int phase = 0, bool balance = false);
+
 struct FlatIndex : Index {
   RowStore st;
   std::unordered_map<int64_t, int64_t> slot_of;  // _idMap (:15)
@@ -1023,6 +1026,10 @@ struct FlatIndex : Index {
       return;
     }
     const int k1 = filter_k1(k);
+    if (flat_stream_ok(k, k1, cutoff)) {
+      search_stream(d_q, nq, k, k1, cutoff, d_s, d_l, d_c, ws);
+      return;
+    }
     if (filter_enabled() && k <= KMAX_FAST && filter_supported(dim, metric, k1)) {
       search_filter(d_q, nq, k, k1, cutoff, d_s, d_l, d_c, ws);
       return;
@@ -1032,6 +1039,222 @@ struct FlatIndex : Index {
       return;
     }
     search_exact(d_q, nq, k, cutoff, d_s, d_l, d_c, ws);
+  }
+
+  // FLAT on the stream scan (scan.hip, round 4): slots [0, cutoff) cut into chunks that play the IVF
+  // path's lists (every query probes all of them, their centroid the store's center: mu for L2, 0 for IP),
+  // so the sample, the emit scan, the merge and the certified refine (the *Unsafe form, V = 4) run as
+  // for IVF_FLAT, and the exact re-run of certificate failures stays on the device: no host round trip.
+  // PYR_FLAT_STREAM=0: the round-3 filter (filter16.hip; measurement only)
+  bool flat_stream_ok(int k, int k1, int64_t cutoff) const {
+    const char *e = getenv("PYR_FLAT_STREAM");
+    if (e && atoi(e) == 0) return false;
+    if (!filter_enabled() || !stream_r4() || stream_prec() != FILTER_F16X1 || !prec16(filter_prec())) return false;
+    if (metric != L2 && metric != IP) return false;
+    if (!st.f16 || k > KMAX_FAST || k1 <= 0 || !stream16_supported(dim, metric, k1)) return false;
+    if (metric == L2 && !(st.resid && st.center16)) return false;
+    return cutoff > 0 && cutoff < (int64_t)KEY_BUF;
+  }
+
+  // the chunking of [0, cutoff): at most MAX_PARTS chunks of whole tiles, >= 10,240 rows (the sample
+  // scores the first 512 rows of each: <= 5 % of the rows)
+  static int64_t flat_chunk_rows(int64_t cutoff) {
+    int64_t c = 10240;
+    while ((cutoff + c - 1) / c > MAX_PARTS) c *= 2;
+    return c;
+  }
+  void search_stream(const float *d_q, int64_t nq, int k, int k1, int64_t cutoff, float *d_s, int64_t *d_l,
+                     int32_t *d_c, Workspace &ws) {
+    const int64_t crow = flat_chunk_rows(cutoff);
+    const int nch = (int)((cutoff + crow - 1) / crow);
+    const int cap = stream_cap();
+    const int nparts = nch;  // one chunk per "list"
+    const int64_t per_q = (int64_t)nparts * cap * 8;
+    const int64_t qs = std::max<int64_t>(1, std::min<int64_t>(nq, (int64_t(16) << 30) / per_q));
+    // the chunks as lists, on the device (no host work per search): bounds, the centroid copies (mu for
+    // L2, 0 for IP) and the probe lists (every chunk, in order) of the largest slice
+    ws.vlb.ensure(sizeof(int32_t) * nch);
+    ws.vle.ensure(sizeof(int32_t) * nch);
+    ws.vcents.ensure(sizeof(float) * nch * dim);
+    launch_chunk_lists(ws.vlb.as<int32_t>(), ws.vle.as<int32_t>(), nch, crow, cutoff,
+                       metric == L2 ? st.center.as<float>() : nullptr, dim, ws.vcents.as<float>(), ws.st);
+    for (int64_t a0 = 0; a0 < nq; a0 += qs) {
+      const int64_t n = std::min(qs, nq - a0);
+      stream_slice(d_q + a0 * dim, n, k, k1, cutoff, nch, nparts, cap, d_s + a0 * k, d_l + a0 * k,
+                   d_c ? d_c + a0 : nullptr, ws);
+    }
+  }
+
+  void stream_slice(const float *d_q, int64_t nq, int k, int k1, int64_t cutoff, int nch, int nparts, int cap,
+                    float *d_s, int64_t *d_l, int32_t *d_c, Workspace &ws) {
+    const int probes = nch;
+    const IvfChunking ch{(int32_t)flat_chunk_rows(cutoff), 1, 0};
+    ws.probes.ensure(sizeof(int32_t) * nq * probes);
+    launch_iota_rows(ws.probes.as<int32_t>(), nq, probes, ws.st);
+    DevMem &lbd = ws.vlb, &led = ws.vle;
+    int maxi;
+    {
+      PhaseTimer t(PH_ITEMS, ws.st);
+      maxi = build_ivf_items(ws, nq, probes, nparts, nch, lbd, led, stream16_qmax(false), ch, 0, true);
+    }
+    const int64_t npos = nq * probes;
+    const int sv = scan_sample_values();
+    const size_t nslot = (size_t)nq * nparts;
+    ws.sbq.ensure(sizeof(uint16_t) * std::max<int64_t>(npos, 1) * dim);
+    ws.sqsc.ensure(sizeof(float2) * std::max<int64_t>(npos, 1));
+    ws.ssamp.ensure(sizeof(float) * std::max<int64_t>(npos, 1) * sv);
+    ws.sthr.ensure(sizeof(float) * nq);
+    ws.scs.ensure(sizeof(float) * nslot * cap);
+    ws.sck.ensure(sizeof(uint32_t) * nslot * cap);
+    ws.scn.ensure(sizeof(int32_t) * nslot);
+    ws.scf.ensure(sizeof(uint32_t) * nslot);
+    ws.swork.ensure(sizeof(int32_t) * 2);
+    HIPCHK(hipMemsetAsync(ws.scn.p, 0, sizeof(int32_t) * nslot, ws.st));
+    HIPCHK(hipMemsetAsync(ws.scf.p, 0, sizeof(uint32_t) * nslot, ws.st));
+    HIPCHK(hipMemsetAsync(ws.swork.p, 0, sizeof(int32_t) * 2, ws.st));
+    StreamArgs sa{};
+    sa.h16 = st.h16.p;
+    sa.meta = st.meta.as<float>();
+    sa.queries = d_q;
+    sa.cents = ws.vcents.as<float>();
+    sa.sx = st.sx;
+    sa.items = ws.items.as<ScanItem>();
+    sa.n_items = ws.nitems.as<int32_t>();
+    sa.qlist = ws.qlist.as<int32_t>();
+    sa.nparts = nparts;
+    sa.nprobe = probes;
+    sa.cmax = 1;
+    sa.dim = dim;
+    sa.bq = ws.sbq.as<_Float16>();
+    sa.qsc = ws.sqsc.as<float2>();
+    sa.samp = ws.ssamp.as<float>();
+    sa.thr = ws.sthr.as<float>();
+    sa.cand_s = ws.scs.as<float>();
+    sa.cand_k = ws.sck.as<uint32_t>();
+    sa.cand_n = ws.scn.as<int32_t>();
+    sa.cand_f = ws.scf.as<uint32_t>();
+    sa.cap = cap;
+    sa.work = ws.swork.as<int32_t>();
+    sa.key_base = 0;
+    sa.row_limit = (uint32_t)cutoff;
+    sa.ablate = filter_ablate();
+    sa.rsq16 = metric == L2 ? st.rsq16.as<float>() : st.rsq.as<float>();
+    sa.rsq = st.rsq.as<float>();
+    stream_ub_terms(dim, metric, filter_f16_cerr(dim, metric, FILTER_F16X1), filter_cerr(dim),
+                    filter_f16_abs(dim, metric, st.sx, FILTER_F16X1), sa);
+    sa.mub = st.row_terms(metric, sa.kr, sa.kx, ws.st);
+    {
+      PhaseTimer t(PH_SAMPLE, ws.st);
+      launch_scan_sample(sa, metric, maxi, ws.st);
+      StreamSelectArgs sel{};
+      sel.samp = ws.ssamp.as<float>();
+      sel.nq = nq;
+      sel.n = probes * sv;
+      stream_rank(k1, sel.rmin, sel.rmax, sel.et);
+      sel.probes = ws.probes.as<int32_t>();
+      sel.nprobe = probes;
+      sel.lb = lbd.as<int32_t>();
+      sel.le = led.as<int32_t>();
+      sel.thr = ws.sthr.as<float>();
+      launch_stream_select(sel, ws.st);
+    }
+    sa.work = ws.swork.as<int32_t>() + 1;
+    {
+      PhaseTimer t(PH_FLAT_SCAN, ws.st, nq * cutoff);
+      launch_scan_main(sa, metric, maxi, ws.st);
+    }
+    ws.ms.ensure(sizeof(float) * nq * STREAM_KO);
+    ws.mk.ensure(sizeof(int32_t) * nq * STREAM_KO);
+    {
+      PhaseTimer t(PH_MERGE, ws.st);
+      CandMergeArgs m{};
+      m.cand_s = ws.scs.as<float>();
+      m.cand_k = ws.sck.as<uint32_t>();
+      m.cand_n = ws.scn.as<int32_t>();
+      m.cand_f = ws.scf.as<uint32_t>();
+      m.thr = ws.sthr.as<float>();
+      m.nq = nq;
+      m.nparts = nparts;
+      m.cap = cap;
+      m.out_s = ws.ms.as<float>();
+      m.out_k = ws.mk.as<int32_t>();
+      launch_cand_merge(m, ws.st);
+    }
+    ws.fail.ensure(sizeof(int32_t) * nq);
+    ws.fail2.ensure(sizeof(int32_t) * nq);
+    ws.fail_cnt.ensure(sizeof(int32_t));
+    ws.fail_cnt2.ensure(sizeof(int32_t));
+    HIPCHK(hipMemsetAsync(ws.fail_cnt.p, 0, sizeof(int32_t), ws.st));
+    HIPCHK(hipMemsetAsync(ws.fail_cnt2.p, 0, sizeof(int32_t), ws.st));
+    RefineArgs r{};
+    r.rows = st.rows.as<float>();
+    r.rows_rm = st.rrm.as<float>();
+    r.row_labels = st.labels.as<int64_t>();
+    r.queries = d_q;
+    r.ms = ws.ms.as<float>();
+    r.mk = ws.mk.as<int32_t>();
+    r.ld = STREAM_KO;
+    r.max_rsq = st.rmax.as<uint32_t>();
+    r.nq = nq;
+    r.k = k;
+    r.dim = dim;
+    r.c_err = filter_cerr(dim);
+    r.c_bf = filter_f16_cerr(dim, metric, FILTER_F16X1);
+    r.ub = 1;
+    r.resid = 1;
+    r.q16 = 1;
+    r.c_abs = filter_f16_abs(dim, metric, st.sx, FILTER_F16X1);
+    r.out_s = d_s;
+    r.out_l = d_l;
+    r.out_c = d_c;
+    {
+      PhaseTimer t(PH_REFINE, ws.st, nq * k1);
+      r.k1 = k1;
+      r.fail_list = ws.fail2.as<int32_t>();
+      r.fail_cnt = ws.fail_cnt2.as<int32_t>();
+      launch_refine(r, metric, exact_v, ws.st);
+      r.k1 = STREAM_KO;  // the failures at depth 64 from the same candidates
+      r.qsel = ws.fail2.as<int32_t>();
+      r.nsel = ws.fail_cnt2.as<int32_t>();
+      r.fail_list = ws.fail.as<int32_t>();
+      r.fail_cnt = ws.fail_cnt.as<int32_t>();
+      launch_refine(r, metric, exact_v, ws.st);
+      HIPCHK(hipGetLastError());
+    }
+    if (getenv("PYR_STREAM_DEBUG")) {
+      int32_t n1 = 0, n2 = 0;
+      HIPCHK(hipMemcpyAsync(&n1, ws.fail_cnt2.p, sizeof(int32_t), hipMemcpyDeviceToHost, ws.st));
+      HIPCHK(hipMemcpyAsync(&n2, ws.fail_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, ws.st));
+      HIPCHK(hipStreamSynchronize(ws.st));
+      fprintf(stderr, "[flat stream] nq %lld chunks %d: certificate failures depth %d %d, depth 64 %d\n",
+              (long long)nq, nch, k1, n1, n2);
+    }
+    // what neither certificate covers: the exact *Unsafe scan of the failing queries over every chunk,
+    // on the device from the device fail list (pyr_index_search_device stays asynchronous)
+    IvfRerunArgs ra{};
+    ra.rows = st.rows.as<float>();
+    ra.live = st.live.as<uint8_t>();
+    ra.labels = st.labels.as<int64_t>();
+    ra.queries = d_q;
+    ra.probes = ws.probes.as<int32_t>();
+    ra.nprobe = probes;
+    ra.lb = lbd.as<int32_t>();
+    ra.le = led.as<int32_t>();
+    ra.fail = ws.fail.as<int32_t>();
+    ra.nfail = ws.fail_cnt.as<int32_t>();
+    ra.dim = dim;
+    ra.k = k;
+    ra.v4 = exact_v == 4;
+    ra.out_s = d_s;
+    ra.out_l = d_l;
+    ra.out_c = d_c;
+    if (!filter_ablate() && !getenv("PYR_STREAM_THR_BIAS")) {
+      PhaseTimer t(PH_FALLBACK, ws.st);
+      ra.nchunk = (int32_t)std::max<int64_t>(1, std::min<int64_t>(64, (flat_chunk_rows(cutoff) + 1023) / 1024));
+      ws.rrpart.ensure(sizeof(uint64_t) * ivf_rerun_part_keys(nq, probes, k));
+      launch_ivf_exact_rerun(ra, metric, nq, ws.rrpart.as<uint64_t>(), ws.st);
+    }
+    HIPCHK(hipGetLastError());
   }
 
   // Cosine (:339-354): the unit index's exact L2 top-K2 (K2 = K1 - margin >= k, the same
@@ -1518,7 +1741,7 @@ static int64_t probed_rows(Workspace &ws, int64_t nq, int probes, const std::vec
 // list-major work items from ws.probes
 // phase 0 -> ws.items / ws.nitems, phase 1 -> ws.items3 / ws.nitems3 (IvfChunking, kernels.h)
 static int build_ivf_items(Workspace &ws, int64_t nq, int nprobe, int nparts, int nlist, const DevMem &lbeg,
-                           const DevMem &lend, int qchunk, IvfChunking ch, int phase = 0, bool balance = false) {
+                           const DevMem &lend, int qchunk, IvfChunking ch, int phase, bool balance) {
   const int64_t maxi64 = ivf_max_items(nq, nprobe, nlist, qchunk, ch, phase);
   if (maxi64 > INT32_MAX) throw Error(PYR_E_ARG, "query batch too large for one launch");
   const int maxi = (int)maxi64;

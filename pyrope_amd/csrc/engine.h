@@ -131,6 +131,7 @@ struct Workspace {
   DevMem sbq, sbql, sqsc, ssamp, sthr, scs, sck, scn, scf, swork, fail2, fail_cnt2;
   DevMem rrpart;  // device re-run of certificate failures: per (query, probe) top-k keys
   DevMem tdbg;    // measurement only (PYR_STREAM_TIMING)
+  DevMem vlb, vle, vcents;  // FLAT on the stream scan: its chunks as lists (FlatIndex::search_stream)
   DevMem cq, ccs, ccl, ccc;  // Cosine on the filter path: unit queries, inner-product candidates
   const int32_t *ext_probes = nullptr;            // caller-ranked probe lists [nq][ext_nprobe] (multi-GPU)
   int32_t ext_nprobe = 0;

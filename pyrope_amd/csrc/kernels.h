@@ -161,6 +161,7 @@ struct IvfRerunArgs {
   const int32_t *fail, *nfail;
   int32_t dim, k;
   int32_t nchunk;           // most chunks a probed list is cut into (>= 1; few failures use them all)
+  int32_t v4;               // 1: the *Unsafe forms (BruteForceVectorIndex, V = 4: FLAT chunks as lists)
   const float *qnorm;       // Cosine: ComputeNorm per query and per row
   const float *rnorm;
   float *out_s;
@@ -449,6 +450,12 @@ int device_cus();                   // compute units of the current device (pers
 // round 4 (scan.hip): the fused query-operand + sample launch (replaces launch_stream_prep and the
 // sampling launch_stream_scan), and the 32x32x16 list scan; scan_sample_values() == stream16_sample_values()
 int scan_sample_values();
+// FLAT chunks as lists: lb/le of nch chunks of crow rows over [0, cutoff), each with the centroid center
+// (null: 0) -> cents [nch][dim]
+void launch_chunk_lists(int32_t *lb, int32_t *le, int nch, int64_t crow, int64_t cutoff, const float *center,
+                        int dim, float *cents, hipStream_t st);
+// out[i][c] = c for i < rows, c < cols
+void launch_iota_rows(int32_t *out, int64_t rows, int cols, hipStream_t st);
 void launch_scan_sample(const StreamArgs &a, int metric, int max_items, hipStream_t st);
 void launch_scan_main(const StreamArgs &a, int metric, int max_items, hipStream_t st);
 int stream16_qmax(bool q2);          // queries per work item

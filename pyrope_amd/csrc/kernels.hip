@@ -1514,7 +1514,7 @@ __device__ __forceinline__ float rr_score(const float *qs, const float *rows, in
   return MET == L2 ? -sum : sum;
 }
 
-template <int MET, int DT>
+template <int MET, int DT, int V = 1>
 __global__ __launch_bounds__(256) void ivf_rerun_scan_kernel(IvfRerunArgs a, uint64_t *part) {
   __shared__ uint64_t wl[4][64];
   __shared__ float qsh[DT > 0 ? DT : 1];
@@ -1551,6 +1551,8 @@ __global__ __launch_bounds__(256) void ivf_rerun_scan_kernel(IvfRerunArgs a, uin
             if constexpr (DT > 0) dot = rr_score<IP, DT>(qsh, a.rows, r);
             else dot = em_score<1, IP>(Lin{qp}, Blk{a.rows, D, r}, D, 0.0f, 0.0f);
             sc = (qn < 1e-6f || xn < 1e-6f) ? 0.0f : dot / (qn * xn);
+          } else if constexpr (V == 4) {  // FLAT (BruteForceVectorIndex.cs:350-356): the *Unsafe forms
+            sc = em_score<4, MET>(Lin{qp}, Blk{a.rows, D, r}, D, 0.0f, 0.0f);
           } else if constexpr (DT > 0) {
             sc = rr_score<MET, DT>(qsh, a.rows, r);
           } else {
@@ -1975,7 +1977,11 @@ void launch_ivf_exact_rerun(const IvfRerunArgs &a, int metric, int64_t max_fail,
       default: go(k0); break;
     }
   };
-  if (metric == L2)
+  if (a.v4 && metric == L2)
+    go(ivf_rerun_scan_kernel<L2, 0, 4>);
+  else if (a.v4 && metric == IP)
+    go(ivf_rerun_scan_kernel<IP, 0, 4>);
+  else if (metric == L2)
     by_dim(ivf_rerun_scan_kernel<L2, 32>, ivf_rerun_scan_kernel<L2, 64>, ivf_rerun_scan_kernel<L2, 128>,
            ivf_rerun_scan_kernel<L2, 0>);
   else if (metric == IP)

@@ -379,7 +379,35 @@ void launch_scan_dm(const StreamArgs &a, int max_items, hipStream_t st) {
   else hipLaunchKernelGGL((scan_kernel<D, MET>), dim3(grid), dim3(64 * NW), 0, st, a);
 }
 
+__global__ void chunk_lists_kernel(int32_t *lb, int32_t *le, int nch, int64_t crow, int64_t cutoff, const float *center,
+                                   int dim, float *cents) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)nch * dim) return;
+  const int c = (int)(e / dim), d = (int)(e - (int64_t)c * dim);
+  cents[e] = center ? center[d] : 0.0f;
+  if (d == 0) {
+    lb[c] = (int32_t)(c * crow);
+    le[c] = (int32_t)min(cutoff, (int64_t)(c + 1) * crow);
+  }
+}
+__global__ void iota_rows_kernel(int32_t *out, int64_t rows, int cols) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < rows * cols; e += (int64_t)gridDim.x * blockDim.x)
+    out[e] = (int32_t)(e % cols);
+}
+
 }  // namespace
+
+void launch_chunk_lists(int32_t *lb, int32_t *le, int nch, int64_t crow, int64_t cutoff, const float *center,
+                        int dim, float *cents, hipStream_t st) {
+  const int64_t n = (int64_t)nch * dim;
+  if (n <= 0) return;
+  hipLaunchKernelGGL(chunk_lists_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, lb, le, nch, crow, cutoff,
+                     center, dim, cents);
+}
+void launch_iota_rows(int32_t *out, int64_t rows, int cols, hipStream_t st) {
+  if (rows <= 0 || cols <= 0) return;
+  hipLaunchKernelGGL(iota_rows_kernel, dim3(gblk(rows * cols)), dim3(256), 0, st, out, rows, cols);
+}
 
 int scan_sample_values() { return SV; }
 
