@@ -1221,13 +1221,16 @@ struct FlatIndex : Index {
       launch_refine(r, metric, exact_v, ws.st);
       HIPCHK(hipGetLastError());
     }
-    if (getenv("PYR_STREAM_DEBUG")) {
-      int32_t n1 = 0, n2 = 0;
+    // measurement only (the profiler's re-run count, PYR_STREAM_DEBUG): read the failure counts back
+    int32_t nf = 0;
+    if (prof().on || getenv("PYR_STREAM_DEBUG")) {
+      int32_t n1 = 0;
       HIPCHK(hipMemcpyAsync(&n1, ws.fail_cnt2.p, sizeof(int32_t), hipMemcpyDeviceToHost, ws.st));
-      HIPCHK(hipMemcpyAsync(&n2, ws.fail_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, ws.st));
+      HIPCHK(hipMemcpyAsync(&nf, ws.fail_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, ws.st));
       HIPCHK(hipStreamSynchronize(ws.st));
-      fprintf(stderr, "[flat stream] nq %lld chunks %d: certificate failures depth %d %d, depth 64 %d\n",
-              (long long)nq, nch, k1, n1, n2);
+      if (getenv("PYR_STREAM_DEBUG"))
+        fprintf(stderr, "[flat stream] nq %lld chunks %d: certificate failures depth %d %d, depth 64 %d\n",
+                (long long)nq, nch, k1, n1, nf);
     }
     // what neither certificate covers: the exact *Unsafe scan of the failing queries over every chunk,
     // on the device from the device fail list (pyr_index_search_device stays asynchronous)
@@ -1249,7 +1252,7 @@ struct FlatIndex : Index {
     ra.out_l = d_l;
     ra.out_c = d_c;
     if (!filter_ablate() && !getenv("PYR_STREAM_THR_BIAS")) {
-      PhaseTimer t(PH_FALLBACK, ws.st);
+      PhaseTimer t(PH_FALLBACK, ws.st, nf);
       ra.nchunk = (int32_t)std::max<int64_t>(1, std::min<int64_t>(64, (flat_chunk_rows(cutoff) + 1023) / 1024));
       ws.rrpart.ensure(sizeof(uint64_t) * ivf_rerun_part_keys(nq, probes, k));
       launch_ivf_exact_rerun(ra, metric, nq, ws.rrpart.as<uint64_t>(), ws.st);
