@@ -161,6 +161,12 @@ pyr_status pyr_index_snapshot(pyr_index *index, const char *path);
  * 144-165).  FLAT rows are re-added in slot order (BruteForceVectorIndex.cs:84-106: Clear, then
  * InternalAdd, so the 8-bit codes follow the loading index's EnableQuantization).  Exclusive. */
 pyr_status pyr_index_load(pyr_index *index, const char *path);
+/* The 16 random bytes every pyr_index_snapshot draws for its image (all zero for an image written
+ * before they were recorded).  No reference counterpart: the Python shim stores them in its
+ * path + ".ids" id map and ignores a map whose bytes differ from the image's, so a crash between the
+ * two renames cannot pair an image with another snapshot's ids (the reference keeps ids inside its
+ * DTOs, BruteForceVectorIndex.cs:58-82).  Host only; PYR_E_NOT_FOUND / PYR_E_FORMAT as pyr_index_load. */
+pyr_status pyr_image_nonce(const char *path, uint8_t *nonce);
 
 /* IVectorIndex.GetStats (IVectorIndex.cs:28): Count with the reference's semantics
  * (IvfFlat counts buffer + list rows, IvfFlatVectorIndex.cs:305; IvfPq reports 0, IvfPqVectorIndex.cs:230). */

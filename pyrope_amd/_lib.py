@@ -93,6 +93,7 @@ SIGNATURES = {
     "pyr_index_snapshot": (C.c_int, [_vp, C.c_char_p]),
     "pyr_index_set_coalescing": (C.c_int, [_vp, C.c_int32, C.c_int32]),
     "pyr_index_load": (C.c_int, [_vp, C.c_char_p]),
+    "pyr_image_nonce": (C.c_int, [C.c_char_p, _u8]),
     "pyr_index_get_centroids": (C.c_int, [_vp, _f, _i32]),
     "pyr_index_ivf_layout": (C.c_int, [_vp, _i64, _i64, _u8, _i64]),
     "pyr_index_pq_state": (C.c_int, [_vp, _f, _i32, _u8]),

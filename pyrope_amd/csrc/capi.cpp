@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "engine.h"
+#include "persist.h"
 
 namespace {
 // Request coalescer (pyr_index_set_coalescing).  The reference serves one query per VEC.SEARCH
@@ -453,6 +454,15 @@ pyr_status pyr_index_load(pyr_index *index, const char *path) {
     HIPCHK(hipSetDevice(index->impl->device));
     std::unique_lock<std::shared_mutex> g(index->impl->mu);
     index->impl->load(path);
+  });
+}
+
+pyr_status pyr_image_nonce(const char *path, uint8_t *nonce) {
+  if (!path || !nonce) return fail(PYR_E_ARG, "null argument");
+  return guard([&] {
+    pyr::ImageReader r(path);
+    std::memset(nonce, 0, pyr::NONCE_BYTES);
+    if (r.size(pyr::T_NONCE) == pyr::NONCE_BYTES) r.host(pyr::T_NONCE, nonce, pyr::NONCE_BYTES);
   });
 }
 

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cerrno>
 #include <cstring>
+#include <random>
 
 #include "engine.h"
 
@@ -67,6 +68,10 @@ void ImageWriter::device(uint32_t tag, const void *dp, uint64_t nbytes, hipStrea
 }
 
 void ImageWriter::commit() {
+  std::random_device rd;  // the image's identity (T_NONCE), fresh for every snapshot
+  uint32_t nonce[NONCE_BYTES / 4];
+  for (auto &w : nonce) w = rd();
+  host(T_NONCE, nonce, NONCE_BYTES);
   if (std::fseek(f, 8 + 16, SEEK_SET) != 0) throw Error(PYR_E_IO, "seek in " + tmp + " failed");
   put(&nsec, 4);
   if (std::fflush(f) != 0 || fsync(fileno(f)) != 0) throw Error(PYR_E_IO, "flush of " + tmp + " failed");

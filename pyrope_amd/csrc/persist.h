@@ -10,6 +10,8 @@
 //   header   : char magic[8] = "PYRIDX01", int32 version, kind, dim, metric, uint32 nsections
 //   section  : uint32 tag, uint32 reserved, uint64 nbytes, payload (padded to 8 bytes)
 //
+// The last section is T_NONCE: 16 random bytes per snapshot (pyr_image_nonce reads them back).
+//
 // Sections are looked up by tag; a section that is absent loads as empty (the reference's
 // Load_MissingFields_ShouldHandleGracefully, IvfFlatVectorIndexTests.cs:144-165).  Writes go to
 // path + ".tmp", are flushed and fsync'ed, and then renamed over path.
@@ -38,7 +40,11 @@ enum : uint32_t {
   T_CODEBOOKS = 10, // float [M][ksub][dim / M] (IVF_PQ)
   T_KSUB = 11,      // int32 codebook size per subspace
   T_LCODES = 12,    // uint8 [n][M] PQ codes, list-major
+  T_NONCE = 13,     // uint8 [16] random bytes drawn by every commit(): the image's identity, which
+                    // the shim's ".ids" map records so that it never pairs with another image
 };
+
+constexpr uint64_t NONCE_BYTES = 16;
 
 struct ImageWriter {
   std::string path, tmp;
@@ -50,7 +56,7 @@ struct ImageWriter {
   void host(uint32_t tag, const void *p, uint64_t nbytes);
   // device bytes, copied through a bounded host buffer
   void device(uint32_t tag, const void *dp, uint64_t nbytes, hipStream_t st);
-  void commit();  // flush + fsync + rename(tmp, path)
+  void commit();  // append T_NONCE, flush + fsync + rename(tmp, path)
 
  private:
   void put(const void *p, size_t n);

@@ -14,6 +14,7 @@ from __future__ import annotations
 import ctypes as C
 import enum
 import json
+import warnings
 import os
 import re
 import threading
@@ -271,14 +272,13 @@ class HipVectorIndex(IVectorIndex):
     def snapshot(self, path: str) -> None:
         """The library's binary image at `path` (pyr_index_snapshot) plus the shim's id <-> label map
         at path + ".ids" (JSON), each written through a temp file and a rename.  The map records the
-        image it belongs to (size and mtime of the renamed image), so a crash between the two renames
-        cannot pair a new image with the previous snapshot's map: load() then ignores
-        the stale map and falls back to str(label) ids."""
+        image's nonce (16 random bytes every snapshot draws, pyr_image_nonce), so a crash between the
+        two renames cannot pair a new image with the previous snapshot's map: load()
+        then warns, ignores the stale map and falls back to str(label) ids."""
         if path is None or str(path).strip() == "":
             raise ArgumentException("Path cannot be empty.")
         check(self._L.pyr_index_snapshot(self._h, os.fsencode(str(path))))
-        st = os.stat(str(path))
-        ids = {"next": self._next_label, "image": [st.st_size, st.st_mtime_ns],
+        ids = {"next": self._next_label, "image_nonce": self._image_nonce(path),
                "ids": [[i, lab] for i, lab in self._label_of.items()]}
         tmp = str(path) + ".ids.tmp"
         with open(tmp, "w") as f:
@@ -286,6 +286,11 @@ class HipVectorIndex(IVectorIndex):
             f.flush()
             os.fsync(f.fileno())
         os.replace(tmp, str(path) + ".ids")
+
+    def _image_nonce(self, path) -> str:
+        nonce = np.zeros(16, np.uint8)
+        check(self._L.pyr_image_nonce(os.fsencode(str(path)), ptr(nonce, C.c_uint8)))
+        return nonce.tobytes().hex()
 
     def load(self, path: str) -> None:
         if path is None or str(path).strip() == "":
@@ -299,10 +304,10 @@ class HipVectorIndex(IVectorIndex):
                 ids = json.load(f)
         except FileNotFoundError:
             pass
-        if ids is not None and "image" in ids:
-            st = os.stat(str(path))
-            if list(ids["image"]) != [st.st_size, st.st_mtime_ns]:
-                ids = None  # the map of another image
+        if ids is not None and ids.get("image_nonce") != self._image_nonce(path):
+            warnings.warn(f"{path}.ids belongs to another image (nonce mismatch); ids fall back to "
+                          "str(label)", RuntimeWarning, stacklevel=2)
+            ids = None
         if ids is None:
             # an image without (its own) shim map, e.g. written by pyr_index_snapshot directly or by
             # another client: every loaded row's id is str(label), new ids get labels above them all

@@ -94,3 +94,30 @@ def test_status_mapping():
         with pytest.raises(exc):
             _lib.check(st)
     _lib.check(_lib.PYR_OK)
+
+
+def _image(path, sections):
+    """a hand-written image (persist.h layout): header, then (tag, payload) sections padded to 8 bytes"""
+    import struct
+    with open(path, "wb") as f:
+        f.write(b"PYRIDX01" + struct.pack("<iiiiI", 1, 0, 4, 0, len(sections)))
+        for tag, payload in sections:
+            f.write(struct.pack("<IIQ", tag, 0, len(payload)) + payload + b"\0" * (-len(payload) % 8))
+
+
+def test_image_nonce_reads_the_nonce_section(hiplib, tmp_path):
+    """pyr_image_nonce (host only, no device): the T_NONCE section's 16 bytes; zeros for an image
+    written without one; PYR_E_NOT_FOUND / PYR_E_FORMAT like pyr_index_load."""
+    from pyrope_amd import _lib
+    out = (C.c_uint8 * 16)()
+    nonce = bytes(range(7, 23))
+    p = str(tmp_path / "a")
+    _image(p, [(8, b"\1" * 8), (13, nonce)])
+    assert hiplib.pyr_image_nonce(p.encode(), out) == _lib.PYR_OK
+    assert bytes(out) == nonce
+    _image(p, [(8, b"\1" * 8)])
+    assert hiplib.pyr_image_nonce(p.encode(), out) == _lib.PYR_OK
+    assert bytes(out) == b"\0" * 16
+    assert hiplib.pyr_image_nonce(str(tmp_path / "missing").encode(), out) == _lib.PYR_E_NOT_FOUND
+    open(p, "wb").write(b"not an image")
+    assert hiplib.pyr_image_nonce(p.encode(), out) == _lib.PYR_E_FORMAT

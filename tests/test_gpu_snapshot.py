@@ -204,8 +204,9 @@ def test_load_without_id_map_keeps_labels_unique(hiplib, tmp_path, kind):
 
 
 def test_stale_id_map_is_ignored(hiplib, tmp_path):
-    """the .ids map records the image it belongs to; an image replaced without its map
-    (a crash between the two renames) loads with str(label) ids instead of another image's ids."""
+    """the .ids map records the nonce of the image it belongs to; an image replaced
+    without its map (a crash between the two renames) loads with str(label) ids and a warning
+    instead of another image's ids -- also when both images have the same size."""
     from pyrope_amd import BruteForceVectorIndex, VectorMetric
     a = BruteForceVectorIndex(4, VectorMetric.L2)
     a.add("alpha", [1, 0, 0, 0])
@@ -220,9 +221,20 @@ def test_stale_id_map_is_ignored(hiplib, tmp_path):
     b.snapshot(path)
     open(path + ".ids", "w").write(ids_a)  # the previous snapshot's map next to the new image
     c = BruteForceVectorIndex(4, VectorMetric.L2)
-    c.load(path)
+    with pytest.warns(RuntimeWarning, match="nonce"):
+        c.load(path)
     assert c.search([0, 0, 1, 0], 1)[0].id == "0"
     assert c._next_label == 3
+    # same content, same size: the second snapshot's image still rejects the first one's map
+    b.snapshot(path)
+    ids_b = open(path + ".ids").read()
+    b.snapshot(path)
+    assert os.path.getsize(path) > 0
+    open(path + ".ids", "w").write(ids_b)
+    d = BruteForceVectorIndex(4, VectorMetric.L2)
+    with pytest.warns(RuntimeWarning, match="nonce"):
+        d.load(path)
+    assert d.search([0, 0, 1, 0], 1)[0].id == "0"
 
 
 def test_corrupt_images_raise_format_errors(hiplib, tmp_path):
