@@ -284,6 +284,7 @@ static pyr_status search_coalesced(pyr_index *index, const float *q, int64_t nq,
   const auto key = std::make_tuple(k, prm.nprobe, prm.max_scans);
   std::shared_ptr<Batch> b;
   bool leader = false;
+  size_t q0 = 0;  // b->q's size before this caller's rows
   try {  // no allocation failure may cross the C ABI or leave followers waiting
     auto it = co.open.find(key);
     if (it == co.open.end() || it->second->closed || it->second->nq + nq > co.max_batch) {
@@ -296,9 +297,12 @@ static pyr_status search_coalesced(pyr_index *index, const float *q, int64_t nq,
     } else {
       b = it->second;
     }
+    q0 = b->q.size();
     b->q.insert(b->q.end(), q, q + nq * dim);
     b->parts.push_back({b->nq, nq, out_scores, out_labels, out_counts});
   } catch (...) {
+    // leader or follower: the batch keeps exactly the rows of the callers in b->parts
+    if (b && b->q.size() > q0) b->q.resize(q0);
     if (leader) {  // nobody else joined yet (the lock is held): withdraw the batch
       auto f = co.open.find(key);
       if (f != co.open.end() && f->second == b) co.open.erase(f);

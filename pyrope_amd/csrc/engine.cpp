@@ -72,10 +72,10 @@ void RowStore::reserve(int64_t slots, hipStream_t st) {
     rrm.grow_keep(sizeof(float) * nc * dim, sizeof(float) * cap * dim, st);
     HIPCHK(hipMemsetAsync(rrm.as<float>() + cap * dim, 0, sizeof(float) * (nc - cap) * dim, st));
     if (center16) rsq16.grow_keep(sizeof(float) * nc, sizeof(float) * cap, st);
-    h16.grow_keep(sizeof(uint16_t) * nc * dim, sizeof(uint16_t) * cap * dim, st);
+    h16.grow_keep(sizeof(uint16_t) * nc * tdim(), sizeof(uint16_t) * cap * tdim(), st);
     meta.grow_keep(sizeof(float) * nc, sizeof(float) * cap, st);
-    HIPCHK(hipMemsetAsync(static_cast<char *>(h16.p) + sizeof(uint16_t) * cap * dim, 0,
-                          sizeof(uint16_t) * (nc - cap) * dim, st));
+    HIPCHK(hipMemsetAsync(static_cast<char *>(h16.p) + sizeof(uint16_t) * cap * tdim(), 0,
+                          sizeof(uint16_t) * (nc - cap) * tdim(), st));
     HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(meta.as<float>() + cap), (int)0xFF800000u, nc - cap,
                              st));  // -inf: not a row
     if (!amaxd.p) amaxd.ensure(sizeof(uint32_t));
@@ -131,11 +131,11 @@ void RowStore::encode16(const int64_t *d_slots, int64_t cnt, hipStream_t st) {
     sx = pow2_scale_host(amax);
     if (ctr && d_slots)  // every slot is re-encoded: their residual norms too
       launch_resid_sq(rows.as<float>(), cap, dim, ctr, nullptr, rsq16.as<float>(), st, nullptr, rmax_r.as<uint32_t>());
-    launch_encode16(rows.as<float>(), nullptr, cap, dim, sx, h16.p, st, ctr, nullptr, meta_norms());
+    launch_encode16(rows.as<float>(), nullptr, cap, dim, sx, h16.p, st, ctr, nullptr, meta_norms(), tdim());
     launch_meta16(nullptr, cap, met16, meta_norms(), live.as<uint8_t>(), meta.as<float>(), st);
   } else {
     amax = std::max(am, amax);
-    launch_encode16(rows.as<float>(), d_slots, cnt, dim, sx, h16.p, st, ctr, nullptr, meta_norms());
+    launch_encode16(rows.as<float>(), d_slots, cnt, dim, sx, h16.p, st, ctr, nullptr, meta_norms(), tdim());
     launch_meta16(d_slots, cnt, met16, meta_norms(), live.as<uint8_t>(), meta.as<float>(), st);
   }
   HIPCHK(hipGetLastError());
@@ -421,7 +421,12 @@ static int filter_prec() {
 }
 static bool prec16(int prec) { return prec == FILTER_F16X2 || prec == FILTER_F16X1; }
 // the fp16 tile copy is kept for stores the fp16 filter can scan
-static bool store16(int dim, int metric) { return filter16_supported(dim, metric, 16); }
+// fp16 tiles are kept where a filter can use them: the round-3 filter's dims, or the stream scan's
+static bool store16(int dim, int metric) {
+  return filter16_supported(dim, metric, 16) || ((metric == L2 || metric == IP) && scan_tile_dim(dim) > 0);
+}
+// the tile dimension of a store of dim (the stream scan's padding where the round-3 kernels have none)
+static int store16_dt(int dim) { return filter16_supported(dim, L2, 16) ? dim : scan_tile_dim(dim); }
 // the arithmetic a filter launch really runs: the fp16 tile filter needs the store's fp16 tiles and
 // items of at most filter16_max_rows() rows; otherwise an fp16 request runs as bf16x3
 static int filter_prec_for(int prec, bool f16_store, int64_t max_item_rows) {
@@ -490,10 +495,10 @@ static int64_t stream_chunk() {
 // multi-GPU launch can size a rank before it allocates (the M8 rank shape: tests/test_host_logic.py).
 void ivf_memory_plan(int dim, int64_t nrows, int nlist, int64_t max_len, int64_t nq, int nprobe, int k,
                      int64_t *index_bytes, int64_t *workspace_bytes) {
-  const int64_t D = dim;
+  const int64_t D = dim, DT = std::max(dim, scan_tile_dim(dim));  // DT: the fp16 tiles' (padded) dimension
   const int64_t slots = round_up(nrows, 32) + (int64_t)nlist * 32;  // lists padded to 32-row tiles
   // rows (blocked fp32) + row-major fp32 copy + fp16 tiles + meta, row terms, |x|^2, |x - c|^2, live, label
-  const int64_t per_row = 4 * D + 4 * D + 2 * D + 4 + 4 + 4 + 4 + 1 + 8;
+  const int64_t per_row = 4 * D + 4 * D + 2 * DT + 4 + 4 + 4 + 4 + 1 + 8;
   const int64_t cent = (int64_t)nlist * (D * 4 * 3 + 4 * 6 + 8);  // centroids (blocked, row-major, unit), per-list
   if (index_bytes) *index_bytes = slots * per_row + cent;
   if (!workspace_bytes) return;
@@ -517,9 +522,9 @@ void ivf_memory_plan(int dim, int64_t nrows, int nlist, int64_t max_len, int64_t
   w += 4 * std::min(nq, qb) * nlist + 4 * std::min(nq, qb);
   // per slice (the buffers are sized for the largest slice and reused)
   const int64_t npos = qs * probes, nslot = qs * nparts;
-  w += (int64_t)sizeof(ScanItem) * ivf_max_items(qs, probes, nlist, stream16_qmax(false), ch, 0) + 4 * npos +
+  w += (int64_t)sizeof(ScanItem) * ivf_max_items(qs, probes, nlist, scan_qmax(DT), ch, 0) + 4 * npos +
        16 * ((int64_t)nlist + 1);
-  w += 2 * npos * D + 8 * npos + 4 * npos * stream16_sample_values() + 4 * qs;  // query operands, samples, T_q
+  w += 2 * npos * DT + 8 * npos + 4 * npos * scan_sample_values() + 4 * qs;  // query operands, samples, T_q
   w += 8 * nslot * cap + 8 * nslot;                                            // candidate regions + counts/floors
   w += 8 * qs * STREAM_KO + 16 * qs;                                           // merged candidates, fail lists
   w += 8 * ivf_rerun_part_keys(qs, probes, k);                                 // device re-run scratch
@@ -840,6 +845,7 @@ struct FlatIndex : Index {
     st.dim = dim;
     st.cosine = metric == COS;  // norm cached at Add (:146)
     st.f16 = store16(dim, metric);
+    st.dt = st.f16 ? store16_dt(dim) : 0;
     st.center16 = st.f16 && metric == L2;  // fp16 tiles of x - mean (engine.h RowStore)
     st.met16 = metric;
     dp = sq8_dp(dim);
@@ -1030,6 +1036,10 @@ struct FlatIndex : Index {
       search_stream(d_q, nq, k, k1, cutoff, d_s, d_l, d_c, ws);
       return;
     }
+    if (unit && metric == COS && unit->flat_stream_ok(k, k1, cutoff)) {
+      search_cosine_stream(d_q, nq, k, k1, cutoff, d_s, d_l, d_c, ws);
+      return;
+    }
     if (filter_enabled() && k <= KMAX_FAST && filter_supported(dim, metric, k1)) {
       search_filter(d_q, nq, k, k1, cutoff, d_s, d_l, d_c, ws);
       return;
@@ -1051,7 +1061,7 @@ struct FlatIndex : Index {
     if (e && atoi(e) == 0) return false;
     if (!filter_enabled() || !stream_r4() || stream_prec() != FILTER_F16X1 || !prec16(filter_prec())) return false;
     if (metric != L2 && metric != IP) return false;
-    if (!st.f16 || k > KMAX_FAST || k1 <= 0 || !stream16_supported(dim, metric, k1)) return false;
+    if (!st.f16 || k > KMAX_FAST || k1 <= 0 || !scan_supported(dim, metric, k1)) return false;
     if (metric == L2 && !(st.resid && st.center16)) return false;
     return cutoff > 0 && cutoff < (int64_t)KEY_BUF;
   }
@@ -1063,8 +1073,23 @@ struct FlatIndex : Index {
     while ((cutoff + c - 1) / c > MAX_PARTS) c *= 2;
     return c;
   }
+  // Cosine (:339-354) on the stream scan: the unit index's scan of the unit queries over the unit rows'
+  // fp16 tiles (L2 bounds of -|q^ - x^|^2), the exact Cosine -- DotProductUnsafe / (|q| |x|) with the zero
+  // rule -- of the candidates on the raw rows, certified in cosine units (refine_kernel, cosine), and the
+  // exact Cosine re-run of failures on the device: no host round trip, as for L2 / IP
+  void search_cosine_stream(const float *d_q, int64_t nq, int k, int k1, int64_t cutoff, float *d_s, int64_t *d_l,
+                            int32_t *d_c, Workspace &ws) {
+    ws.qn.ensure(sizeof(float) * std::max<int64_t>(nq, 1));
+    launch_norms(d_q, nq, dim, 0, ws.qn.as<float>(), ws.st);  // VectorMath.ComputeNorm (:339)
+    ws.cq.ensure(sizeof(float) * std::max<int64_t>(nq, 1) * dim);
+    launch_unit_rows(d_q, nullptr, ws.qn.as<float>(), nq, dim, ws.cq.as<float>(), ws.st);
+    const CosRefine cr{&st, d_q, ws.qn.as<float>(), zflag.as<uint32_t>()};
+    std::shared_lock<std::shared_mutex> g(unit->mu);
+    unit->search_stream(ws.cq.as<float>(), nq, k, k1, cutoff, d_s, d_l, d_c, ws, &cr);
+  }
+
   void search_stream(const float *d_q, int64_t nq, int k, int k1, int64_t cutoff, float *d_s, int64_t *d_l,
-                     int32_t *d_c, Workspace &ws) {
+                     int32_t *d_c, Workspace &ws, const CosRefine *cr = nullptr) {
     const int64_t crow = flat_chunk_rows(cutoff);
     const int nch = (int)((cutoff + crow - 1) / crow);
     const int cap = stream_cap();
@@ -1080,13 +1105,21 @@ struct FlatIndex : Index {
                        metric == L2 ? st.center.as<float>() : nullptr, dim, ws.vcents.as<float>(), ws.st);
     for (int64_t a0 = 0; a0 < nq; a0 += qs) {
       const int64_t n = std::min(qs, nq - a0);
-      stream_slice(d_q + a0 * dim, n, k, k1, cutoff, nch, nparts, cap, d_s + a0 * k, d_l + a0 * k,
-                   d_c ? d_c + a0 : nullptr, ws);
+      if (cr) {  // the slice's raw queries and norms
+        CosRefine c2 = *cr;
+        c2.queries = cr->queries + a0 * dim;
+        c2.qnorm = cr->qnorm + a0;
+        stream_slice(d_q + a0 * dim, n, k, k1, cutoff, nch, nparts, cap, d_s + a0 * k, d_l + a0 * k,
+                     d_c ? d_c + a0 : nullptr, ws, &c2);
+      } else {
+        stream_slice(d_q + a0 * dim, n, k, k1, cutoff, nch, nparts, cap, d_s + a0 * k, d_l + a0 * k,
+                     d_c ? d_c + a0 : nullptr, ws);
+      }
     }
   }
 
   void stream_slice(const float *d_q, int64_t nq, int k, int k1, int64_t cutoff, int nch, int nparts, int cap,
-                    float *d_s, int64_t *d_l, int32_t *d_c, Workspace &ws) {
+                    float *d_s, int64_t *d_l, int32_t *d_c, Workspace &ws, const CosRefine *cr = nullptr) {
     const int probes = nch;
     const IvfChunking ch{(int32_t)flat_chunk_rows(cutoff), 1, 0};
     ws.probes.ensure(sizeof(int32_t) * nq * probes);
@@ -1095,12 +1128,12 @@ struct FlatIndex : Index {
     int maxi;
     {
       PhaseTimer t(PH_ITEMS, ws.st);
-      maxi = build_ivf_items(ws, nq, probes, nparts, nch, lbd, led, stream16_qmax(false), ch, 0, true);
+      maxi = build_ivf_items(ws, nq, probes, nparts, nch, lbd, led, scan_qmax(st.tdim()), ch, 0, true);
     }
     const int64_t npos = nq * probes;
     const int sv = scan_sample_values();
     const size_t nslot = (size_t)nq * nparts;
-    ws.sbq.ensure(sizeof(uint16_t) * std::max<int64_t>(npos, 1) * dim);
+    ws.sbq.ensure(sizeof(uint16_t) * std::max<int64_t>(npos, 1) * st.tdim());
     ws.sqsc.ensure(sizeof(float2) * std::max<int64_t>(npos, 1));
     ws.ssamp.ensure(sizeof(float) * std::max<int64_t>(npos, 1) * sv);
     ws.sthr.ensure(sizeof(float) * nq);
@@ -1125,6 +1158,7 @@ struct FlatIndex : Index {
     sa.nprobe = probes;
     sa.cmax = 1;
     sa.dim = dim;
+    sa.dt = st.tdim();
     sa.bq = ws.sbq.as<_Float16>();
     sa.qsc = ws.sqsc.as<float2>();
     sa.samp = ws.ssamp.as<float>();
@@ -1140,8 +1174,11 @@ struct FlatIndex : Index {
     sa.ablate = filter_ablate();
     sa.rsq16 = metric == L2 ? st.rsq16.as<float>() : st.rsq.as<float>();
     sa.rsq = st.rsq.as<float>();
-    stream_ub_terms(dim, metric, filter_f16_cerr(dim, metric, FILTER_F16X1), filter_cerr(dim),
-                    filter_f16_abs(dim, metric, st.sx, FILTER_F16X1), sa);
+    // the scan's error terms at the tile dimension (the padded dims' products are exact zeros: the
+    // larger D only widens the bound)
+    const int dt = st.tdim();
+    stream_ub_terms(dt, metric, filter_f16_cerr(dt, metric, FILTER_F16X1), filter_cerr(dt),
+                    filter_f16_abs(dt, metric, st.sx, FILTER_F16X1), sa);
     sa.mub = st.row_terms(metric, sa.kr, sa.kx, ws.st);
     {
       PhaseTimer t(PH_SAMPLE, ws.st);
@@ -1204,6 +1241,17 @@ struct FlatIndex : Index {
     r.resid = 1;
     r.q16 = 1;
     r.c_abs = filter_f16_abs(dim, metric, st.sx, FILTER_F16X1);
+    if (cr) {  // Cosine: the candidates' exact Cosine on the raw rows, certified in cosine units
+      r.rows = cr->raw->rows.as<float>();
+      r.rows_rm = cr->raw->f16 ? cr->raw->rrm.as<float>() : nullptr;
+      r.row_labels = cr->raw->labels.as<int64_t>();
+      r.queries = cr->queries;
+      r.max_rsq = cr->raw->rmax.as<uint32_t>();
+      r.cosine = 1;
+      r.qnorm = cr->qnorm;
+      r.rnorm = cr->raw->norms.as<float>();
+      r.zflag = cr->zflag;
+    }
     r.out_s = d_s;
     r.out_l = d_l;
     r.out_c = d_c;
@@ -1248,6 +1296,13 @@ struct FlatIndex : Index {
     ra.dim = dim;
     ra.k = k;
     ra.v4 = exact_v == 4;
+    if (cr) {  // the exact Cosine (:354) over the raw rows
+      ra.rows = cr->raw->rows.as<float>();
+      ra.labels = cr->raw->labels.as<int64_t>();
+      ra.queries = cr->queries;
+      ra.qnorm = cr->qnorm;
+      ra.rnorm = cr->raw->norms.as<float>();
+    }
     ra.out_s = d_s;
     ra.out_l = d_l;
     ra.out_c = d_c;
@@ -1255,7 +1310,7 @@ struct FlatIndex : Index {
       PhaseTimer t(PH_FALLBACK, ws.st, nf);
       ra.nchunk = (int32_t)std::max<int64_t>(1, std::min<int64_t>(64, (flat_chunk_rows(cutoff) + 1023) / 1024));
       ws.rrpart.ensure(sizeof(uint64_t) * ivf_rerun_part_keys(nq, probes, k));
-      launch_ivf_exact_rerun(ra, metric, nq, ws.rrpart.as<uint64_t>(), ws.st);
+      launch_ivf_exact_rerun(ra, cr ? COS : metric, nq, ws.rrpart.as<uint64_t>(), ws.st);
     }
     HIPCHK(hipGetLastError());
   }
@@ -2010,6 +2065,7 @@ struct IvfFlatIndex : Index {
     nl.cosine = metric == COS;
     const bool unit = metric == COS && store16(dim, L2);
     nl.f16 = unit || store16(dim, metric);
+    nl.dt = nl.f16 ? store16_dt(dim) : 0;
     nl.met16 = unit ? L2 : metric;
     nl.reserve(std::max<int64_t>(tot, 32), wst);
     DevMem dsr;
@@ -2062,7 +2118,8 @@ struct IvfFlatIndex : Index {
       HIPCHK(hipStreamSynchronize(wst));
       std::memcpy(&nl.amax, &bits, sizeof(bits));
       nl.sx = pow2_scale_host(nl.amax);
-      launch_encode16(TR, nullptr, nl.cap, dim, nl.sx, nl.h16.p, wst, TC, dtl.as<int32_t>(), nl.rsq16.as<float>());
+      launch_encode16(TR, nullptr, nl.cap, dim, nl.sx, nl.h16.p, wst, TC, dtl.as<int32_t>(), nl.rsq16.as<float>(),
+                      nl.tdim());
       launch_meta16(nullptr, nl.cap, nl.met16, nl.rsq16.as<float>(), nl.live.as<uint8_t>(), nl.meta.as<float>(), wst);
       HIPCHK(hipGetLastError());
       HIPCHK(hipStreamSynchronize(wst));  // urm / ublk / cn are freed at the end of this block
@@ -2094,6 +2151,7 @@ struct IvfFlatIndex : Index {
     std::swap(lists.rrm.p, nl.rrm.p);
     std::swap(lists.rrm.n, nl.rrm.n);
     lists.f16 = nl.f16;
+    lists.dt = nl.dt;
     lists.met16 = nl.met16;
     lists.sx = nl.sx;
     lists.amax = nl.amax;
@@ -2129,24 +2187,34 @@ struct IvfFlatIndex : Index {
     const int nprobe = prm.nprobe < 0 ? nprobe_default : prm.nprobe;
     const int probes = (built && coarse.nlist > 0) ? std::max(0, std::min(nprobe, coarse.nlist)) : 0;
     const int k1 = filter_k1(k);
-    if (filter_enabled() && probes > 0 && buf.live_count() == 0 && prm.max_scans < 0 && k <= KMAX_FAST &&
-        probes < MAX_PARTS && filter_supported(dim, metric, k1)) {
-      search_filter(d_q, nq, k, k1, probes, d_s, d_l, d_c, ws);
+    const bool fast = filter_enabled() && probes > 0 && buf.live_count() == 0 && prm.max_scans < 0 &&
+                      k <= KMAX_FAST && probes < MAX_PARTS && k1 > 0;
+    // the stream scan (L2 / IP, and Cosine over the unit residual tiles with the exact Cosine in the refine)
+    if (fast && stream_ok(k1)) {
+      search_stream(d_q, nq, k, k1, probes, d_s, d_l, d_c, ws);
       return;
     }
-    // Cosine: the stream scan over the unit residual tiles (commit_lists), exact Cosine in the refine
-    if (metric == COS && filter_enabled() && probes > 0 && buf.live_count() == 0 && prm.max_scans < 0 &&
-        k <= KMAX_FAST && probes < MAX_PARTS && k1 > 0 && stream_enabled() && prec16(filter_prec()) && lists.f16 &&
-        lists.resid && lists.met16 == L2 && stream16_supported(dim, L2, k1)) {
-      search_stream(d_q, nq, k, k1, probes, d_s, d_l, d_c, ws);
+    // the round-2 MFMA filter (filter.hip): dims 32 / 64 / 128 with the stream scan switched off
+    if (fast && filter_supported(dim, metric, k1)) {
+      search_filter(d_q, nq, k, k1, probes, d_s, d_l, d_c, ws);
       return;
     }
     search_exact(d_q, nq, k, prm, d_s, d_l, d_c, ws);
   }
 
+  // the lists' fp16 residual tiles serve this search's stream scan: the round-4 kernels (scan.hip) at every
+  // tile dimension, the round-3 ones (stream16.hip; PYR_STREAM_MFMA=16 or two-term queries) at 32 / 64 / 128
+  bool stream_ok(int k1) const {
+    if (!stream_enabled() || !prec16(filter_prec()) || !lists.f16 || !lists.resid) return false;
+    const int met = metric == COS ? L2 : metric;
+    if (metric == COS && lists.met16 != L2) return false;
+    const bool r4 = stream_prec() != FILTER_F16X2 && stream_r4();
+    return r4 ? scan_supported(dim, met, k1) : lists.tdim() == dim && stream16_supported(dim, met, k1);
+  }
+
   void search_filter(const float *d_q, int64_t nq, int k, int k1, int probes, float *d_s, int64_t *d_l, int32_t *d_c,
                      Workspace &ws) {
-    if (stream_enabled() && prec16(filter_prec()) && lists.f16 && lists.resid && stream16_supported(dim, metric, k1)) {
+    if (stream_ok(k1)) {
       search_stream(d_q, nq, k, k1, probes, d_s, d_l, d_c, ws);
       return;
     }
@@ -2384,7 +2452,8 @@ struct IvfFlatIndex : Index {
       launch_unit_rows(d_q, nullptr, ws.qn.as<float>(), nq, dim, ws.cq.as<float>(), ws.st);
       d_qs = ws.cq.as<float>();
     }
-    const int qmax = stream16_qmax(q2);
+    const bool r4 = !q2 && stream_r4();
+    const int qmax = r4 ? scan_qmax(lists.tdim()) : stream16_qmax(q2);
     int maxi;
     {
       PhaseTimer t(PH_ITEMS, ws.st);
@@ -2393,8 +2462,8 @@ struct IvfFlatIndex : Index {
     const int64_t npos = nq * probes;
     const int sv = stream16_sample_values();
     const size_t nslot = (size_t)nq * nparts;
-    ws.sbq.ensure(sizeof(uint16_t) * std::max<int64_t>(npos, 1) * dim);
-    if (q2) ws.sbql.ensure(sizeof(uint16_t) * std::max<int64_t>(npos, 1) * dim);
+    ws.sbq.ensure(sizeof(uint16_t) * std::max<int64_t>(npos, 1) * lists.tdim());
+    if (q2) ws.sbql.ensure(sizeof(uint16_t) * std::max<int64_t>(npos, 1) * lists.tdim());
     ws.sqsc.ensure(sizeof(float2) * std::max<int64_t>(npos, 1));
     ws.ssamp.ensure(sizeof(float) * std::max<int64_t>(npos, 1) * sv);
     ws.sthr.ensure(sizeof(float) * nq);
@@ -2419,6 +2488,7 @@ struct IvfFlatIndex : Index {
     sa.nprobe = probes;
     sa.cmax = ch.cmax;
     sa.dim = dim;
+    sa.dt = lists.tdim();
     sa.bq = ws.sbq.as<_Float16>();
     sa.bql = q2 ? ws.sbql.as<_Float16>() : nullptr;
     sa.qsc = ws.sqsc.as<float2>();
@@ -2437,7 +2507,8 @@ struct IvfFlatIndex : Index {
     const int prec = q2 ? FILTER_F16X2 : FILTER_F16X1;
     sa.rsq16 = lists.rsq16.as<float>();
     sa.rsq = lists.rsq.as<float>();
-    stream_ub_terms(dim, met, filter_f16_cerr(dim, met, prec), filter_cerr(dim), filter_f16_abs(dim, met, lists.sx, prec),
+    const int dt = lists.tdim();  // the scan's error terms at the tile dimension (FlatIndex::stream_slice)
+    stream_ub_terms(dt, met, filter_f16_cerr(dt, met, prec), filter_cerr(dt), filter_f16_abs(dt, met, lists.sx, prec),
                     sa);
     sa.mub = lists.row_terms(met, sa.kr, sa.kx, ws.st);
     const bool timing = getenv("PYR_STREAM_TIMING") != nullptr;  // measurement only (syncs)
@@ -2445,7 +2516,6 @@ struct IvfFlatIndex : Index {
       ws.tdbg.ensure(sizeof(unsigned long long) * 8);
       HIPCHK(hipMemsetAsync(ws.tdbg.p, 0, sizeof(unsigned long long) * 8, ws.st));
     }
-    const bool r4 = !q2 && stream_r4();
     {
       PhaseTimer t(PH_SAMPLE, ws.st);
       if (r4) {

@@ -70,6 +70,10 @@ struct RowStore {
   // ever stored (amax) below 2^14.  Kept only when f16 is set (FLAT slots, IVF lists).
   bool f16 = false;
   int met16 = 0;
+  // tile dimension (scan_tile_dim): dim, or the stream scan's padded dimension (96 for 65..96 ...); the
+  // tiles are zero-padded, the fp32 rows and everything exact keep dim
+  int dt = 0;
+  int tdim() const { return dt > 0 ? dt : dim; }
   float sx = 0.0f;
   float amax = 0.0f;
   DevMem h16, meta, amaxd;

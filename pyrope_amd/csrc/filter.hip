@@ -445,7 +445,7 @@ __device__ __forceinline__ float hsum8(const float *v) {
 }
 
 // V = 1: L2Squared (VectorMath.cs:39-70) / DotProduct (:8-37);
-// V = 4: L2SquaredUnsafe (:188-253) / DotProductUnsafe (:128-186).  D % 8 == 0.
+// V = 4: L2SquaredUnsafe (:188-253) / DotProductUnsafe (:128-186).  Any D (the tail runs in order).
 // (kernels.hip em_* hold the one-lane form; the refine spreads it over 8 lanes, below.)
 
 // hsum8 over the 8 lanes of an aligned lane group, lane l holding v[l]: the same three levels of
@@ -502,6 +502,17 @@ __device__ float exact_score_l8(const float *q, const float *rows, int64_t r, in
       }
     }
     sum = sum + hsum8_lanes(acc);
+  }
+  // the scalar tail (VectorMath.cs:243-250 / :182-185 and the safe forms' remainder loops), in order;
+  // every lane of the group adds the same terms
+  for (; i < D; ++i) {
+    const float x = X(i);
+    if (MET == L2) {
+      const float d = q[i] - x;
+      sum = sum + d * d;
+    } else {
+      sum = sum + q[i] * x;
+    }
   }
   return MET == L2 ? -sum : sum;
 }

@@ -934,8 +934,9 @@ __device__ __forceinline__ float resid_val(const float *rows, const float *cents
 // zero (an Inf times a zero or opposite-signed query half would make the whole score NaN), and
 // meta16_kernel makes it always (Inf) or never (NaN) a candidate.
 __global__ void encode16_kernel(const float *rows, const int64_t *slots, int64_t n, int D, float sx,
-                                const float *cents, const int32_t *tile_list, const float *rn, _Float16 *h16) {
-  const int G = D / 8;
+                                const float *cents, const int32_t *tile_list, const float *rn, _Float16 *h16,
+                                int Dp) {
+  const int G = Dp / 8;  // Dp >= D: the tile dimension, dims past D zero
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * G;
        e += (int64_t)gridDim.x * blockDim.x) {  // grid-stride: grids stay below 2^32 work-items
     const int64_t i = e / G;
@@ -945,8 +946,9 @@ __global__ void encode16_kernel(const float *rows, const int64_t *slots, int64_t
     const bool special = rn && !isfinite(rn[r]);
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-      v[j] = special ? (_Float16)0.0f : (_Float16)(resid_val(rows, cents, tile_list, r, 8 * g + j, D) * sx);
-    const size_t off = (((size_t)(r >> 5) * (D / 16) + (g >> 1)) * 2 + (g & 1)) * 32 + (r & 31);
+      v[j] = special || 8 * g + j >= D ? (_Float16)0.0f
+                                         : (_Float16)(resid_val(rows, cents, tile_list, r, 8 * g + j, D) * sx);
+    const size_t off = (((size_t)(r >> 5) * (Dp / 16) + (g >> 1)) * 2 + (g & 1)) * 32 + (r & 31);
     *reinterpret_cast<h8v *>(h16 + off * 8) = v;
   }
 }
@@ -1014,10 +1016,11 @@ void launch_filter16(const FilterArgs &a, int metric, int max_items, hipStream_t
 }
 
 void launch_encode16(const float *rows, const int64_t *slots, int64_t n, int32_t dim, float sx, void *h16,
-                     hipStream_t st, const float *cents, const int32_t *tile_list, const float *rn) {
+                     hipStream_t st, const float *cents, const int32_t *tile_list, const float *rn, int32_t dpad) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(encode16_kernel, dim3(gblk(n * (dim / 8))), dim3(256), 0, st, rows, slots, n, dim, sx, cents,
-                     tile_list, rn, reinterpret_cast<_Float16 *>(h16));
+  const int dp = dpad > dim ? dpad : dim;
+  hipLaunchKernelGGL(encode16_kernel, dim3(gblk(n * (dp / 8))), dim3(256), 0, st, rows, slots, n, dim, sx, cents,
+                     tile_list, rn, reinterpret_cast<_Float16 *>(h16), dp);
 }
 
 void launch_resid_sq(const float *rows, int64_t n, int32_t dim, const float *cents, const int32_t *tile_list,

@@ -370,6 +370,7 @@ struct StreamArgs {
   const int32_t *n_items;
   const int32_t *qlist;       // per (list, query) position: q * nparts + probe * cmax
   int32_t nparts, nprobe, cmax, dim;
+  int32_t dt;                 // tile dimension D (scan_tile_dim; 0: dim): tiles and bq rows; queries / cents keep dim
   _Float16 *bq, *bql;         // [pos][D] scaled query residuals: one fp16 term (+ the low term, or null)
   float2 *qsc;                // [pos] {f, cq}
   float *samp;                // [q * nprobe + probe][stream16_sample_values()] sampled scores
@@ -450,6 +451,11 @@ int device_cus();                   // compute units of the current device (pers
 // round 4 (scan.hip): the fused query-operand + sample launch (replaces launch_stream_prep and the
 // sampling launch_stream_scan), and the 32x32x16 list scan; scan_sample_values() == stream16_sample_values()
 int scan_sample_values();
+// tile dimension of the stream scan for a row dimension: dims <= 128 rounded up to 32, then 256 / 512 / 768
+// (tiles and query operands zero-padded; the fp32 rows and the exact refine keep dim); 0 = none
+int scan_tile_dim(int dim);
+int scan_qmax(int dt);               // queries per work item at tile dimension dt
+bool scan_supported(int dim, int metric, int k1);
 // FLAT chunks as lists: lb/le of nch chunks of crow rows over [0, cutoff), each with the centroid center
 // (null: 0) -> cents [nch][dim]
 void launch_chunk_lists(int32_t *lb, int32_t *le, int nch, int64_t crow, int64_t cutoff, const float *center,
@@ -555,7 +561,8 @@ void launch_filter16(const FilterArgs &a, int metric, int max_items, hipStream_t
 // rn (may be null): the rows' meta norms; a non-finite one zeroes the row's tile (encode16_kernel)
 void launch_encode16(const float *rows, const int64_t *slots, int64_t n, int32_t dim, float sx, void *h16,
                      hipStream_t st, const float *cents = nullptr, const int32_t *tile_list = nullptr,
-                     const float *rn = nullptr);
+                     const float *rn = nullptr, int32_t dpad = 0);
+// (dpad > dim: tiles of dpad dims, the dims past dim zero -- scan_tile_dim)
 // |x - c[list]|^2 of rows [0, n)
 void launch_resid_sq(const float *rows, int64_t n, int32_t dim, const float *cents, const int32_t *tile_list,
                      float *out, hipStream_t st, const int64_t *slots = nullptr, uint32_t *out_max = nullptr);

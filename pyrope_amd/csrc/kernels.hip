@@ -1548,7 +1548,8 @@ __global__ __launch_bounds__(256) void ivf_rerun_scan_kernel(IvfRerunArgs a, uin
           if constexpr (MET == COS) {  // VectorMath.Cosine (:102-109) with the cached norms
             const float qn = a.qnorm[q], xn = a.rnorm[r];
             float dot;
-            if constexpr (DT > 0) dot = rr_score<IP, DT>(qsh, a.rows, r);
+            if constexpr (V == 4) dot = em_score<4, IP>(Lin{qp}, Blk{a.rows, D, r}, D, 0.0f, 0.0f);  // FLAT (:354)
+            else if constexpr (DT > 0) dot = rr_score<IP, DT>(qsh, a.rows, r);
             else dot = em_score<1, IP>(Lin{qp}, Blk{a.rows, D, r}, D, 0.0f, 0.0f);
             sc = (qn < 1e-6f || xn < 1e-6f) ? 0.0f : dot / (qn * xn);
           } else if constexpr (V == 4) {  // FLAT (BruteForceVectorIndex.cs:350-356): the *Unsafe forms
@@ -1981,6 +1982,8 @@ void launch_ivf_exact_rerun(const IvfRerunArgs &a, int metric, int64_t max_fail,
     go(ivf_rerun_scan_kernel<L2, 0, 4>);
   else if (a.v4 && metric == IP)
     go(ivf_rerun_scan_kernel<IP, 0, 4>);
+  else if (a.v4 && metric == COS)
+    go(ivf_rerun_scan_kernel<COS, 0, 4>);
   else if (metric == L2)
     by_dim(ivf_rerun_scan_kernel<L2, 32>, ivf_rerun_scan_kernel<L2, 64>, ivf_rerun_scan_kernel<L2, 128>,
            ivf_rerun_scan_kernel<L2, 0>);

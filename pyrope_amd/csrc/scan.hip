@@ -28,6 +28,8 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <stdexcept>
+#include <string>
 
 #include "kernels.h"
 
@@ -36,18 +38,43 @@ namespace {
 
 #include "f16util.h"
 
-constexpr int NW = 16;                 // waves per scan block
 constexpr int SAMPLE_TILES = 16;       // tiles of a list the sample scores (stream16.hip: 2 x 8 waves)
 constexpr int SV = 2 * SAMPLE_TILES;   // sample values per (query, probe): one per (tile, lane half)
 
+// Tile dimensions (scan_tile_dim): dims up to 128 rounded up to 32; 256, 512, 768.  Per tile dimension
+// the queries per item (the item's fp16 query operands fill <= 128 KB of LDS) and the waves per block
+// (16 while a tile's A operands and a group's B operands fit 128 VGPRs, else 8).
+constexpr int tile_dim_of(int dim) {
+  return dim <= 0 ? 0 : dim <= 128 ? (dim + 31) / 32 * 32 : dim <= 256 ? 256 : dim <= 512 ? 512 : dim <= 768 ? 768 : 0;
+}
+constexpr int qmax_of(int D) { return D <= 128 ? 512 : D == 256 ? 256 : D == 512 ? 128 : 64; }
+constexpr int nw_of(int D) { return D <= 128 ? 16 : 8; }
+
 __device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf(a, fmaxf(b, c)); }
+
+// dims d0 .. d0 + 7 of a row of `dim` floats; PAD: the row is shorter than the tile dimension, dims past
+// it read as zero (the zero-padded tiles' counterpart)
+template <bool PAD>
+__device__ __forceinline__ void load8(const float *row, int d0, int dim, float (&v)[8]) {
+  if constexpr (!PAD) {
+    const float4 x = *reinterpret_cast<const float4 *>(row + d0), y = *reinterpret_cast<const float4 *>(row + d0 + 4);
+    v[0] = x.x, v[1] = x.y, v[2] = x.z, v[3] = x.w, v[4] = y.x, v[5] = y.y, v[6] = y.z, v[7] = y.w;
+  } else {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = d0 + u < dim ? row[d0 + u] : 0.0f;
+  }
+}
 
 // ---- 1. query operands + sample ----
 // Wave (item, g): the item's queries 32g .. 32g + 31 (lane (r, h): query 32g + r, dims 16s + 8h .. +7).
 // Sample value (t, h) of a query = the best bound of rows 8b + 4h + i of tile t (distinct rows per value).
-template <int D, int MET>
+// D <= 128: the query's residual stays in registers; larger D: a first pass takes the norms, the operands
+// are rebuilt per k-step (no per-lane array of D / 2 values).
+template <int D, int MET, bool PAD>
 __global__ __launch_bounds__(256) void sample_kernel(StreamArgs a) {
-  constexpr int KS = D / 16, TB = 64 * D, QG = 512 / 32;
+  constexpr int KS = D / 16, TB = 64 * D, QG = qmax_of(D) / 32;
+  constexpr bool REG = KS <= 8;
+  constexpr int UN = REG ? KS : 2;  // k-step loops: unrolled in the register form, lean otherwise
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int item = unit / QG, g = unit - item * QG;
@@ -59,28 +86,45 @@ __global__ __launch_bounds__(256) void sample_kernel(StreamArgs a) {
   const int pos = it.qbeg + qi;
   const int slot = a.qlist[pos];
   const int q = slot / a.nparts;
-  // the residual q - c (L2) or q (IP) in registers, its norm terms and max |.|
-  float rv[KS][8];
+  const int dim = a.dim;
+  const float *qrow = a.queries + (size_t)q * dim, *crow = a.cents + (size_t)it.list * dim;
+  // the residual q - c (L2) or q (IP) of dims 16s + 8h .. +7
+  auto resid8 = [&](int s, float (&v)[8]) {
+    float qv[8], cv[8];
+    load8<PAD>(qrow, 16 * s + 8 * h, dim, qv);
+    if (MET == L2) {
+      load8<PAD>(crow, 16 * s + 8 * h, dim, cv);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = qv[u] - cv[u];
+    } else {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = qv[u];
+    }
+  };
+  // its norm terms and max |.|
+  float rv[REG ? KS : 1][8];
   float cq = 0.0f, amax = 0.0f, q2 = 0.0f, c2 = 0.0f;
-#pragma unroll
+#pragma unroll UN
   for (int s = 0; s < KS; ++s) {
-    const float4 *qp = reinterpret_cast<const float4 *>(a.queries + (size_t)q * D + 16 * s + 8 * h);
-    const float4 *cp = reinterpret_cast<const float4 *>(a.cents + (size_t)it.list * D + 16 * s + 8 * h);
-    const float4 qa = qp[0], qb = qp[1], ca = cp[0], cb = cp[1];
-    const float qv[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
-    const float cv[8] = {ca.x, ca.y, ca.z, ca.w, cb.x, cb.y, cb.z, cb.w};
+    float v[8];
+    resid8(s, v);
+    if (MET == IP) {
+      float cv[8];
+      load8<PAD>(crow, 16 * s + 8 * h, dim, cv);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      if (MET == L2) {
-        rv[s][u] = qv[u] - cv[u];
-        cq += rv[s][u] * rv[s][u];
-      } else {
-        rv[s][u] = qv[u];
-        cq += qv[u] * cv[u];
-        q2 += qv[u] * qv[u];
+      for (int u = 0; u < 8; ++u) {
+        cq += v[u] * cv[u];
+        q2 += v[u] * v[u];
         c2 += cv[u] * cv[u];
       }
-      amax = fmaxf(amax, fabsf(rv[s][u]));
+    } else {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) cq += v[u] * v[u];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      amax = fmaxf(amax, fabsf(v[u]));
+      if constexpr (REG) rv[s][u] = v[u];
     }
   }
   cq += __shfl_xor(cq, 32);
@@ -100,12 +144,26 @@ __global__ __launch_bounds__(256) void sample_kernel(StreamArgs a) {
   const float sq = pow2_scale(amax);
   const float f = (MET == L2 ? 2.0f : 1.0f) / (sq * a.sx);
   const float cqe = (MET == L2 ? -cq : cq) + ep;
-  h8v B[KS];
+  // the fp16 operand of k-step s (exact scaling: a power of two)
+  auto operand = [&](int s) -> h8v {
+    h8v b;
+    if constexpr (REG) {
 #pragma unroll
+      for (int u = 0; u < 8; ++u) b[u] = (_Float16)(rv[s][u] * sq);
+    } else {
+      float v[8];
+      resid8(s, v);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) b[u] = (_Float16)(v[u] * sq);
+    }
+    return b;
+  };
+  h8v B[REG ? KS : 1];
+#pragma unroll UN
   for (int s = 0; s < KS; ++s) {
-#pragma unroll
-    for (int u = 0; u < 8; ++u) B[s][u] = (_Float16)(rv[s][u] * sq);  // exact scaling (power of two)
-    if (own) *reinterpret_cast<h8v *>(a.bq + (size_t)pos * D + 16 * s + 8 * h) = B[s];
+    const h8v b = operand(s);
+    if constexpr (REG) B[s] = b;
+    if (own) *reinterpret_cast<h8v *>(a.bq + (size_t)pos * D + 16 * s + 8 * h) = b;
   }
   if (own && h == 0) a.qsc[pos] = make_float2(f, cqe);
   // score the first SAMPLE_TILES tiles of the list with the group (rows as A, the queries as B)
@@ -118,16 +176,23 @@ __global__ __launch_bounds__(256) void sample_kernel(StreamArgs a) {
     mx[t] = -INFINITY;
     if (t < nt) {
       const char *tb = hsrc + (size_t)(r0 / 32 + t) * TB + lane * 16;
-      h8v A[KS];
-#pragma unroll
-      for (int s = 0; s < KS; ++s) A[s] = *reinterpret_cast<const h8v *>(tb + s * 1024);
       const size_t mo = (size_t)(r0 + 32 * t) + 4 * h;
       f4v M[4];
 #pragma unroll
       for (int b = 0; b < 4; ++b) M[b] = *reinterpret_cast<const f4v *>(a.mub + mo + 8 * b);
-      f16v acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[0], B[0], (f16v){}, 0, 0, 0);
+      f16v acc = {};
+      if constexpr (REG) {
+        h8v A[KS];
 #pragma unroll
-      for (int s = 1; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[s], B[s], acc, 0, 0, 0);
+        for (int s = 0; s < KS; ++s) A[s] = *reinterpret_cast<const h8v *>(tb + s * 1024);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[s], B[s], acc, 0, 0, 0);
+      } else {
+#pragma unroll 2
+        for (int s = 0; s < KS; ++s)
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(*reinterpret_cast<const h8v *>(tb + s * 1024), operand(s), acc,
+                                                       0, 0, 0);
+      }
       const int rt = r0 + 32 * t, rlim = it.row_end;
       float m = -INFINITY;
 #pragma unroll
@@ -151,11 +216,16 @@ __global__ __launch_bounds__(256) void sample_kernel(StreamArgs a) {
 // AB (measurement only, PYR_FILTER_ABLATE): 1 (64) = no emission, 2 (128) = tile stream only (no MFMA),
 // 3 (256) = no emission and every tile read from the item's first one (compute without HBM)
 template <int D, int MET, int AB = 0>
-__global__ __launch_bounds__(64 * NW, 1) void scan_kernel(StreamArgs a) {
+__global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
+  constexpr int NW = nw_of(D);       // waves per block
   constexpr int KS = D / 16;         // 32x32x16 k-steps
+  constexpr int KC = KS < 16 ? KS : 16;  // k-steps of A held in registers at a time (D > 256: chunks)
+  constexpr int NC = KS / KC;
   constexpr int TB = 64 * D;         // h16 bytes per 32-row tile
-  constexpr int QMAX = 512;          // queries per item
-  constexpr int PIECES = QMAX / 32 * KS;
+  constexpr int QMAX = qmax_of(D);   // queries per item
+  constexpr int NG = QMAX / 32;      // query groups per item
+  constexpr int PIECES = NG * KS;
+  static_assert(KS % KC == 0 && QMAX <= 512, "tile dimension");
   __shared__ __attribute__((aligned(16))) char bl[PIECES * 1024];
   __shared__ float2 qf[QMAX];        // per query slot: {f, threshold in y = f acc + row term space}
   __shared__ float2 qz[QMAX];        // {cq (score = y + cq), candidate region as int bits}
@@ -240,11 +310,13 @@ __global__ __launch_bounds__(64 * NW, 1) void scan_kernel(StreamArgs a) {
     const bool stage = it.row_end - r0 < (1 << 23);  // row offsets fit the staged word
 
     // tile t for lane (r, h): the A fragments and the row terms of rows 8b + 4h .. +3
-    auto load = [&](int t, h8v (&A)[KS], f4v (&M)[4]) {
+    auto load = [&](int t, h8v (&A)[KC], f4v (&M)[4]) {
       if constexpr (AB == 3) t = 0;
       const char *tp = hsrc + (size_t)(r0 / 32 + t) * TB + lane * 16;
+      if constexpr (NC == 1) {
 #pragma unroll
-      for (int s = 0; s < KS; ++s) A[s] = *reinterpret_cast<const h8v *>(tp + s * 1024);
+        for (int s = 0; s < KS; ++s) A[s] = *reinterpret_cast<const h8v *>(tp + s * 1024);
+      }
       const size_t mo = (size_t)(r0 + 32 * t) + 4 * h;
 #pragma unroll
       for (int b = 0; b < 4; ++b) M[b] = *reinterpret_cast<const f4v *>(a.mub + mo + 8 * b);
@@ -311,8 +383,49 @@ __global__ __launch_bounds__(64 * NW, 1) void scan_kernel(StreamArgs a) {
       }
       return __builtin_amdgcn_ballot_w64(mx >= q.y) != 0ull;
     };
+    // the wave's next tile and its row terms into L2 (one 4-byte LDS-DMA per 128-byte line)
+    auto prefetch = [&](int tpf) {
+      const char *tp = hsrc + (size_t)(r0 / 32 + tpf) * TB;
+#pragma unroll
+      for (int o = 0; o < TB; o += 64 * 128) glds<4>(tp + min(o + lane * 128, TB - 128), sink);
+      glds<4>(a.mub + r0 + 32 * tpf + (lane & 31), sink);
+    };
+    // D > 256: the tile's A operands in chunks of KC k-steps, every group's accumulator live meanwhile
+    // (NG <= 4); the chunk's loads are waited for once, the next tile is pulled into L2 after the first
+    auto tile_chunked = [&](const float (&mr)[16], int t, int tpf) {
+      const int rt = r0 + 32 * t;
+      const char *tp = hsrc + (size_t)(r0 / 32 + (AB == 3 ? 0 : t)) * TB + lane * 16;
+      f16v acc[NG];
+#pragma unroll
+      for (int j = 0; j < NG; ++j) acc[j] = (f16v){};
+#pragma unroll 1
+      for (int c = 0; c < NC; ++c) {
+        h8v A[KC];
+#pragma unroll
+        for (int s = 0; s < KC; ++s) A[s] = *reinterpret_cast<const h8v *>(tp + (c * KC + s) * 1024);
+#pragma unroll
+        for (int j = 0; j < NG; ++j) {
+          if (j < ng) {
+            const char *bp = bl + (j * KS + c * KC) * 1024 + lane * 16;
+#pragma unroll
+            for (int s = 0; s < KC; ++s)
+              acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[s], *reinterpret_cast<const h8v *>(bp + s * 1024),
+                                                              acc[j], 0, 0, 0);
+          }
+        }
+        if (c == 0 && tpf >= 0) prefetch(tpf);
+      }
+#pragma unroll
+      for (int j = 0; j < NG; ++j) {
+        if (j < ng) {
+          const float2 q = qf[32 * j + r];
+          const bool e = epi_test(acc[j], mr, q);
+          if (__builtin_expect(e, 0)) emit_y(acc[j], q.y, 32 * j + r, rt);
+        }
+      }
+    };
     // one tile against every group; tpf >= 0: the wave's next tile, pulled into L2 meanwhile
-    auto tile = [&](const h8v (&A)[KS], const float (&mr)[16], int t, int tpf) {
+    auto tile = [&](const h8v (&A)[KC], const float (&mr)[16], int t, int tpf) {
       const int rt = r0 + 32 * t;
       if constexpr (AB == 2) {  // consume the tile without scoring it
         float v = mr[0];
@@ -333,7 +446,9 @@ __global__ __launch_bounds__(64 * NW, 1) void scan_kernel(StreamArgs a) {
         __builtin_amdgcn_sched_group_barrier(0x100, KS + 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x008, KS, 0);
         if (j == 0 && tpf >= 0) {  // the tile's own loads were waited for before the chain: warm L2
-          glds<4>(hsrc + (size_t)(r0 / 32 + tpf) * TB + min(lane * 128, TB - 128), sink);
+#pragma unroll
+          for (int o = 0; o < TB; o += 64 * 128)
+            glds<4>(hsrc + (size_t)(r0 / 32 + tpf) * TB + min(o + lane * 128, TB - 128), sink);
           glds<4>(a.mub + r0 + 32 * tpf + (lane & 31), sink);
         }
         if (__builtin_expect(e, 0)) emit_y(acc, q.y, 32 * j + r, rt);
@@ -342,7 +457,7 @@ __global__ __launch_bounds__(64 * NW, 1) void scan_kernel(StreamArgs a) {
 
     int t = w;
     while (t < nt) {
-      h8v A[KS];
+      h8v A[KC];
       f4v M[4];
       float mr[16];
       load(t, A, M);
@@ -350,7 +465,8 @@ __global__ __launch_bounds__(64 * NW, 1) void scan_kernel(StreamArgs a) {
       if (lane == 0) tn = atomicAdd(&tnext, 1);
       tn = __builtin_amdgcn_readfirstlane(tn);
       row_terms(M, t, mr);
-      tile(A, mr, t, tn < nt ? tn : -1);
+      if constexpr (NC == 1) tile(A, mr, t, tn < nt ? tn : -1);
+      else tile_chunked(mr, t, tn < nt ? tn : -1);
       t = tn;
     }
     stamp(1);
@@ -373,10 +489,46 @@ __global__ __launch_bounds__(64 * NW, 1) void scan_kernel(StreamArgs a) {
 template <int D, int MET>
 void launch_scan_dm(const StreamArgs &a, int max_items, hipStream_t st) {
   const int grid = std::max(1, std::min(max_items, device_cus()));
-  if (a.ablate & 64) hipLaunchKernelGGL((scan_kernel<D, MET, 1>), dim3(grid), dim3(64 * NW), 0, st, a);
-  else if (a.ablate & 128) hipLaunchKernelGGL((scan_kernel<D, MET, 2>), dim3(grid), dim3(64 * NW), 0, st, a);
-  else if (a.ablate & 256) hipLaunchKernelGGL((scan_kernel<D, MET, 3>), dim3(grid), dim3(64 * NW), 0, st, a);
-  else hipLaunchKernelGGL((scan_kernel<D, MET>), dim3(grid), dim3(64 * NW), 0, st, a);
+  const dim3 b(64 * nw_of(D));
+  if constexpr (D == 128) {  // the ablations (measurement only) at the I1 dimension
+    if (a.ablate & 64) {
+      hipLaunchKernelGGL((scan_kernel<D, MET, 1>), dim3(grid), b, 0, st, a);
+      return;
+    }
+    if (a.ablate & 128) {
+      hipLaunchKernelGGL((scan_kernel<D, MET, 2>), dim3(grid), b, 0, st, a);
+      return;
+    }
+    if (a.ablate & 256) {
+      hipLaunchKernelGGL((scan_kernel<D, MET, 3>), dim3(grid), b, 0, st, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((scan_kernel<D, MET>), dim3(grid), b, 0, st, a);
+}
+
+template <int D, int MET>
+void launch_sample_dm(const StreamArgs &a, int max_items, hipStream_t st) {
+  const dim3 grid((unsigned)((int64_t)max_items * (qmax_of(D) / 32) / 4));
+  if (a.dim == D) hipLaunchKernelGGL((sample_kernel<D, MET, false>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((sample_kernel<D, MET, true>), grid, dim3(256), 0, st, a);
+}
+
+// every tile dimension, both metrics
+#define PYR_SCAN_BY_DIM(fn)                                                                 \
+  switch (dt) {                                                                             \
+    case 32: return metric == L2 ? fn<32, L2>(a, max_items, st) : fn<32, IP>(a, max_items, st);    \
+    case 64: return metric == L2 ? fn<64, L2>(a, max_items, st) : fn<64, IP>(a, max_items, st);    \
+    case 96: return metric == L2 ? fn<96, L2>(a, max_items, st) : fn<96, IP>(a, max_items, st);    \
+    case 128: return metric == L2 ? fn<128, L2>(a, max_items, st) : fn<128, IP>(a, max_items, st); \
+    case 256: return metric == L2 ? fn<256, L2>(a, max_items, st) : fn<256, IP>(a, max_items, st); \
+    case 512: return metric == L2 ? fn<512, L2>(a, max_items, st) : fn<512, IP>(a, max_items, st); \
+    case 768: return metric == L2 ? fn<768, L2>(a, max_items, st) : fn<768, IP>(a, max_items, st); \
+    default: throw_unsupported(dt);                                                         \
+  }
+
+[[noreturn]] void throw_unsupported(int dt) {
+  throw std::invalid_argument("stream scan: no tile dimension " + std::to_string(dt));
 }
 
 __global__ void chunk_lists_kernel(int32_t *lb, int32_t *le, int nch, int64_t crow, int64_t cutoff, const float *center,
@@ -410,27 +562,22 @@ void launch_iota_rows(int32_t *out, int64_t rows, int cols, hipStream_t st) {
 }
 
 int scan_sample_values() { return SV; }
+int scan_tile_dim(int dim) { return tile_dim_of(dim); }
+int scan_qmax(int dt) { return qmax_of(dt); }
+bool scan_supported(int dim, int metric, int k1) {
+  return (metric == L2 || metric == IP) && tile_dim_of(dim) > 0 && k1 >= 1 && k1 <= STREAM_KO;
+}
 
 void launch_scan_sample(const StreamArgs &a, int metric, int max_items, hipStream_t st) {
   if (max_items <= 0) return;
-  const dim3 grid((unsigned)((int64_t)max_items * (512 / 32) / 4));
-  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, a); };
-  switch (a.dim) {
-    case 32: metric == L2 ? go(sample_kernel<32, L2>) : go(sample_kernel<32, IP>); return;
-    case 64: metric == L2 ? go(sample_kernel<64, L2>) : go(sample_kernel<64, IP>); return;
-    default: metric == L2 ? go(sample_kernel<128, L2>) : go(sample_kernel<128, IP>); return;
-  }
+  const int dt = a.dt > 0 ? a.dt : a.dim;
+  PYR_SCAN_BY_DIM(launch_sample_dm)
 }
 
 void launch_scan_main(const StreamArgs &a, int metric, int max_items, hipStream_t st) {
   if (max_items <= 0) return;
-  switch (a.dim) {
-    case 32: metric == L2 ? launch_scan_dm<32, L2>(a, max_items, st) : launch_scan_dm<32, IP>(a, max_items, st); return;
-    case 64: metric == L2 ? launch_scan_dm<64, L2>(a, max_items, st) : launch_scan_dm<64, IP>(a, max_items, st); return;
-    default:
-      metric == L2 ? launch_scan_dm<128, L2>(a, max_items, st) : launch_scan_dm<128, IP>(a, max_items, st);
-      return;
-  }
+  const int dt = a.dt > 0 ? a.dt : a.dim;
+  PYR_SCAN_BY_DIM(launch_scan_dm)
 }
 
 }  // namespace pyr
