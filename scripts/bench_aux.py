@@ -172,7 +172,9 @@ def main():
                "qps": qps, "ms_per_step": ms, "phases_ms": {k_: v["ms"] for k_, v in phases.items()},
                "scan_pairs": scan["work"],
                "scan_tflops_2d": scan["work"] * 2 * d / (scan["ms"] * 1e-3) / 1e12,
-               "hbm_equiv_GBps": qps * n * d * 4 / 1e9,
+               # (query, row) pairs per second over the whole step; not a memory rate (the scan reads each
+               # fp16 tile once per item of up to 512 queries, not once per query)
+               "pairs_per_s": qps * n,
                "parity_sample": {"queries": a.check, "ids_and_bits_equal": ok}, "cpu_baseline": cpu}
     else:
         n, d = a.n or 3_200_000, a.dim or 768
