@@ -348,11 +348,19 @@ def run(args):
     wide = os.environ.get("PYR_F16_WIDE", "1") != "0"
     if stream:
         q2 = os.environ.get("PYR_STREAM_PREC", "3") == "2"
-        kernel_tag = "stream16"
+        r4 = not q2 and os.environ.get("PYR_STREAM_MFMA", "32") != "16"
         mfma_mult, mfma_peak = (2 if q2 else 1), BF16_PEAK_TFLOPS
-        kernel_name = (f"stream16_kernel<{D},L2,{'f16x2' if q2 else 'f16x1'},MAIN> (IVF list scan, stream-and-emit over "
-                       f"fp16 residual tiles: persistent 8-wave blocks, tiles straight from HBM into registers, rows "
-                       f"as the A operand of v_mfma_f32_16x16x32_f16, {2 if q2 else 1} MFMA per k-step)")
+        if r4:
+            kernel_tag = "scan32"
+            kernel_name = (f"scan_kernel<{D},L2> (scan.hip: IVF list scan, stream-and-emit over fp16 residual tiles: "
+                           f"persistent 16-wave blocks, tiles from HBM into registers as the A operand of "
+                           f"v_mfma_f32_32x32x16_f16, queries from LDS, one MFMA per 16-dim k-step)")
+        else:
+            kernel_tag = "stream16"
+            kernel_name = (f"stream16_kernel<{D},L2,{'f16x2' if q2 else 'f16x1'},MAIN> (IVF list scan, stream-and-emit "
+                           f"over fp16 residual tiles: persistent 8-wave blocks, tiles straight from HBM into "
+                           f"registers, rows as the A operand of v_mfma_f32_16x16x32_f16, {2 if q2 else 1} MFMA per "
+                           f"k-step)")
     else:
         kernel_tag = {2: "filter16w" if wide else "filter16", 3: "filter16"}.get(prec, "filter")
         mfma_mult, mfma_peak = {2: (2, BF16_PEAK_TFLOPS), 3: (1, BF16_PEAK_TFLOPS), 1: (3, BF16_PEAK_TFLOPS),
@@ -494,6 +502,8 @@ def run(args):
             "roofline": {"bound": "hbm", "achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": hbm_achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_src,
+                         # the bytes the kernel physically moved (FETCH_SIZE pass) at this launch's time
+                         "frac_physical": (traffic / (scan["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
                          "unique_bytes_per_launch": unique_bytes, "lists_probed": int(len(probed)),
                          "kernel": kernel_name,
                          "stored_bytes_per_launch": stored_bytes,
@@ -503,7 +513,8 @@ def run(args):
                                   "4 B, the reference's fp32 rows) + queries, over the HIP-event time of the launch "
                                   "(rank 0); stored_bytes = what the fp16 tile kernel actually streams for them "
                                   "(D x 2 + 4 B per padded row), stored_frac = their rate vs the peak; traffic (FETCH_SIZE x 2, its "
-                                  "own rocprofv3 pass, per launch) is in profiles/*/summary.md")},
+                                  "own rocprofv3 pass, per launch; traffic.json) and frac_physical = traffic over the same "
+                                  "launch time vs the peak")},
             "mfma": {"achieved": achieved * mfma_mult, "peak": mfma_peak, "unit": "TFLOP/s",
                      "frac": achieved * mfma_mult / mfma_peak,
                      "note": (f"as-executed MFMA flops: probed (query,row) pairs x 2*D x {mfma_mult} (MFMAs per "

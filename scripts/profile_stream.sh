@@ -14,7 +14,7 @@ ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 P=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$P"
 cd "$ROOT" || exit 1
-REGEX=${PYR_PROF_REGEX:-stream32_kernel}
+REGEX=${PYR_PROF_REGEX:-scan_kernel}
 S="python scripts/sweep_ivf.py --steps 3"
 
 timeout -k 10 240 $S "$@" > "$P/sweep.log" 2>&1 || exit $?
