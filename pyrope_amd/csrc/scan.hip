@@ -509,7 +509,7 @@ void launch_scan_dm(const StreamArgs &a, int max_items, hipStream_t st) {
 
 template <int D, int MET>
 void launch_sample_dm(const StreamArgs &a, int max_items, hipStream_t st) {
-  const dim3 grid((unsigned)((int64_t)max_items * (qmax_of(D) / 32) / 4));
+  const dim3 grid((unsigned)(((int64_t)max_items * (qmax_of(D) / 32) + 3) / 4));  // 4 waves per block
   if (a.dim == D) hipLaunchKernelGGL((sample_kernel<D, MET, false>), grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL((sample_kernel<D, MET, true>), grid, dim3(256), 0, st, a);
 }

@@ -259,8 +259,11 @@ def test_gpu_part_major_merge_equals_query_major(hiplib):
 
     rng = np.random.default_rng(5)
     W, Q, k = 8, 777, 10
-    s = np.sort(rng.integers(0, 50, (W, Q, k)).astype(np.float32), axis=2)[:, :, ::-1].copy()  # ties across ranks
+    s = rng.integers(0, 50, (W, Q, k)).astype(np.float32)  # ties within and across ranks
     lab = rng.permutation(W * Q * k).reshape(W, Q, k).astype(np.int64)
+    # every partial list in merge order, (score desc, label asc), as a rank's search returns it
+    order = np.lexsort((lab, -s), axis=2)
+    s, lab = np.take_along_axis(s, order, 2).copy(), np.take_along_axis(lab, order, 2).copy()
     lab[:, :5, 7:] = -1  # short partial lists
     s[:, :5, 7:] = -np.inf
     sp, lp = torch.from_numpy(s).cuda(), torch.from_numpy(lab).cuda()
