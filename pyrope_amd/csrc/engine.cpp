@@ -1066,10 +1066,15 @@ struct FlatIndex : Index {
     return cutoff > 0 && cutoff < (int64_t)KEY_BUF;
   }
 
-  // the chunking of [0, cutoff): at most MAX_PARTS chunks of whole tiles, >= 10,240 rows (the sample
-  // scores the first 512 rows of each: <= 5 % of the rows)
+  // the chunking of [0, cutoff): at most MAX_PARTS chunks of whole tiles, 10,240 rows where the store is
+  // large (the sample scores the first 512 rows of each: 5 % of the rows).  A query emits about
+  // R / f = R c / 512 rows in all (R <= K1 sample rank, f = 512 / c the sampled fraction), R c^2 / (512
+  // cutoff) per chunk; a small store therefore takes chunks of ~sqrt(512 cutoff) rows so that a chunk's
+  // region (stream_cap, 256) does not fill -- a full region's floor sits among the best rows and fails
+  // the certificate (20,000 rows, k = 20: 7 % of queries with 10,240-row chunks).
   static int64_t flat_chunk_rows(int64_t cutoff) {
-    int64_t c = 10240;
+    const int64_t small = round_up((int64_t)std::sqrt(512.0 * (double)std::max<int64_t>(cutoff, 1)), 32);
+    int64_t c = std::max<int64_t>(1024, std::min<int64_t>(10240, small));
     while ((cutoff + c - 1) / c > MAX_PARTS) c *= 2;
     return c;
   }
