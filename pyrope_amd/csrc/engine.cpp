@@ -458,6 +458,21 @@ static bool stream_r4() {
   const char *e = getenv("PYR_STREAM_MFMA");
   return !(e && atoi(e) == 16);
 }
+// the query operands and the sample of the round-4 scan: at the dims the round-3 kernels are built for
+// (tile dim = dim = 32 / 64 / 128) sprep + the 8-wave sample pass, which share each sampled tile across
+// the item's queries through LDS (0.14 ms at I1); elsewhere scan.hip's one-wave-per-32-queries sample
+// (0.30 ms at I1: every group re-reads the sampled tiles).  Both write the same bq / qsc / samp.
+// PYR_SCAN_SAMPLE=1: scan.hip's sample at every dim (measurement only).
+static void stream_sample(const StreamArgs &sa, int met, int maxi, hipStream_t st) {
+  const char *e = getenv("PYR_SCAN_SAMPLE");
+  const int dt = sa.dt > 0 ? sa.dt : sa.dim;
+  if (!(e && atoi(e) == 1) && dt == sa.dim && stream16_supported(sa.dim, met, 1)) {
+    launch_stream_prep(sa, met, maxi, st);
+    launch_stream_scan(sa, met, maxi, true, st);
+  } else {
+    launch_scan_sample(sa, met, maxi, st);
+  }
+}
 static int stream_prec() {
   const char *e = getenv("PYR_STREAM_PREC");
   return e && atoi(e) == 2 ? FILTER_F16X2 : FILTER_F16X1;
@@ -476,9 +491,11 @@ static void stream_rank(int k1, int32_t &rmin, int32_t &rmax, double &et) {
     et = 0.0;
     return;
   }
-  rmin = std::max(1, k1 / 2);
-  rmax = std::max(1, k1);
-  et = 8.0 * k1;
+  // PYR_STREAM_RMIN / PYR_STREAM_ET (measurement only): the floor of R and the emitted-row target per K1
+  const char *rm = getenv("PYR_STREAM_RMIN"), *ev = getenv("PYR_STREAM_ET");
+  rmin = std::max(1, rm ? atoi(rm) : k1 / 2);
+  rmax = std::max(rmin, k1);
+  et = (ev ? atof(ev) : 8.0) * k1;
 }
 // candidate region per (query, part) (PYR_STREAM_CAP) and rows per list chunk (PYR_STREAM_CHUNK)
 static int stream_cap() {
@@ -1187,7 +1204,7 @@ struct FlatIndex : Index {
     sa.mub = st.row_terms(metric, sa.kr, sa.kx, ws.st);
     {
       PhaseTimer t(PH_SAMPLE, ws.st);
-      launch_scan_sample(sa, metric, maxi, ws.st);
+      stream_sample(sa, metric, maxi, ws.st);
       StreamSelectArgs sel{};
       sel.samp = ws.ssamp.as<float>();
       sel.nq = nq;
@@ -2524,7 +2541,7 @@ struct IvfFlatIndex : Index {
     {
       PhaseTimer t(PH_SAMPLE, ws.st);
       if (r4) {
-        launch_scan_sample(sa, met, maxi, ws.st);
+        stream_sample(sa, met, maxi, ws.st);
       } else {
         launch_stream_prep(sa, met, maxi, ws.st);
         launch_stream_scan(sa, met, maxi, true, ws.st);

@@ -28,6 +28,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -215,9 +216,11 @@ __global__ __launch_bounds__(256) void sample_kernel(StreamArgs a) {
 // ---- 2. the list scan ----
 // AB (measurement only, PYR_FILTER_ABLATE): 1 (64) = no emission, 2 (128) = tile stream only (no MFMA),
 // 3 (256) = no emission and every tile read from the item's first one (compute without HBM)
-template <int D, int MET, int AB = 0>
-__global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
-  constexpr int NW = nw_of(D);       // waves per block
+// PIPE (D <= 128, PYR_SCAN_PIPE=n): n = 8 or 12 waves (<= 256 / 170 VGPRs), the next group's B operands read
+// from LDS while the current group's MFMA chain runs (two operand buffers, groups taken in pairs)
+template <int D, int MET, int AB = 0, int PIPE = 0>
+__global__ __launch_bounds__(64 * (PIPE ? PIPE : nw_of(D)), 1) void scan_kernel(StreamArgs a) {
+  constexpr int NW = PIPE ? PIPE : nw_of(D);  // waves per block
   constexpr int KS = D / 16;         // 32x32x16 k-steps
   constexpr int KC = KS < 16 ? KS : 16;  // k-steps of A held in registers at a time (D > 256: chunks)
   constexpr int NC = KS / KC;
@@ -434,6 +437,34 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
         if (v == 12345.0f) cnt_l[0] = 1;
         return;
       }
+      if constexpr (PIPE) {
+        // groups in pairs: b1 <- group j + 1 while group j's chain runs on b0, b0 <- group j + 2 during j + 1's
+        h8v b0[KS], b1[KS];
+        read_b(0, b0);
+        auto group = [&](int j, const h8v (&B)[KS]) {
+          const float2 q = qf[32 * j + r];
+          f16v acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[0], B[0], (f16v){}, 0, 0, 0);
+#pragma unroll
+          for (int s = 1; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[s], B[s], acc, 0, 0, 0);
+          if (j == 0 && tpf >= 0) {
+#pragma unroll
+            for (int o = 0; o < TB; o += 64 * 128)
+              glds<4>(hsrc + (size_t)(r0 / 32 + tpf) * TB + min(o + lane * 128, TB - 128), sink);
+            glds<4>(a.mub + r0 + 32 * tpf + (lane & 31), sink);
+          }
+          const bool e = epi_test(acc, mr, q);
+          if (__builtin_expect(e, 0)) emit_y(acc, q.y, 32 * j + r, rt);
+        };
+        for (int j = 0; j < ng; j += 2) {
+          if (j + 1 < ng) read_b(j + 1, b1);
+          group(j, b0);
+          if (j + 1 < ng) {
+            if (j + 2 < ng) read_b(j + 2, b0);
+            group(j + 1, b1);
+          }
+        }
+        return;
+      }
       for (int j = 0; j < ng; ++j) {
         const float2 q = qf[32 * j + r];
         h8v bj[KS];
@@ -490,7 +521,16 @@ template <int D, int MET>
 void launch_scan_dm(const StreamArgs &a, int max_items, hipStream_t st) {
   const int grid = std::max(1, std::min(max_items, device_cus()));
   const dim3 b(64 * nw_of(D));
-  if constexpr (D == 128) {  // the ablations (measurement only) at the I1 dimension
+  if constexpr (D == 128) {  // the ablations and the pipelined variant (measurement only) at the I1 dimension
+    static const int pipe = getenv("PYR_SCAN_PIPE") ? atoi(getenv("PYR_SCAN_PIPE")) : 0;
+    if (pipe == 8 && !a.ablate) {
+      hipLaunchKernelGGL((scan_kernel<D, MET, 0, 8>), dim3(grid), dim3(64 * 8), 0, st, a);
+      return;
+    }
+    if (pipe == 12 && !a.ablate) {
+      hipLaunchKernelGGL((scan_kernel<D, MET, 0, 12>), dim3(grid), dim3(64 * 12), 0, st, a);
+      return;
+    }
     if (a.ablate & 64) {
       hipLaunchKernelGGL((scan_kernel<D, MET, 1>), dim3(grid), b, 0, st, a);
       return;

@@ -137,3 +137,55 @@ def test_device_rerun_chunks_long_lists(hiplib, nq):
     np.testing.assert_array_equal(got[2], exact[2])
     np.testing.assert_array_equal(got[1], exact[1])
     assert np.array_equal(got[0].view(np.uint32), exact[0].view(np.uint32))
+
+
+_FLAT = {}
+
+
+def _flat_index(metric):
+    from pyrope_amd import BruteForceVectorIndex, generate_synthetic
+    if metric not in _FLAT:
+        x = generate_synthetic(60_000, 128, 42)
+        idx = BruteForceVectorIndex(128, metric)
+        idx.add_labels(np.arange(len(x), dtype=np.int64), x)
+        _FLAT[metric] = idx
+    return _FLAT[metric]
+
+
+@pytest.mark.parametrize("force_fail", [False, True])
+@pytest.mark.parametrize("metric", [0, 1, 2])
+def test_flat_search_device_graph_capture_and_replay(hiplib, metric, force_fail):
+    """FLAT search_device on the stream scan (L2, IP and Cosine) enqueues only -- the
+    certificates and the exact re-run of failures run from device-side counts -- so it captures into a
+    HIP graph (a host synchronization inside the capture would fail it) and replays with new queries,
+    also when every certificate fails (PYR_FILTER_CERR: every query takes the device re-run)."""
+    import torch
+
+    from pyrope_amd import generate_synthetic
+    idx = _flat_index(metric)
+    n = 300
+    qa, qb = generate_synthetic(n, 128, 3), generate_synthetic(n, 128, 4)
+    env = {"PYR_FILTER_CERR": "1e15"} if force_fail else {}
+    with _env(**env):
+        ra, rb = idx.search_batch(qa, 10), idx.search_batch(qb, 10)
+        st = torch.cuda.Stream()
+        qbuf = torch.from_numpy(qa).cuda()
+        with torch.cuda.stream(st):
+            out = _dev_search(idx, qbuf, 10, None, st)  # warm-up: workspace and row terms sized
+        st.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=st):
+            idx.search_device(qbuf.data_ptr(), n, 10, out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(),
+                              st.cuda_stream, None)
+        qbuf.copy_(torch.from_numpy(qb))
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        _same(out, rb)
+        qbuf.copy_(torch.from_numpy(qa))
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        _same(out, ra)
+    with _env(PYR_FILTER=0):
+        _same(out, idx.search_batch(qa, 10))

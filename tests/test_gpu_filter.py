@@ -134,8 +134,10 @@ def test_flat_duplicates_force_exact_rerun(hiplib, oracle):
     """Exact ties at the k-th place cannot be certified: those queries are re-run exactly and
     the tie rule (score desc, storage slot asc) still holds."""
     from pyrope_amd import generate_synthetic
-    base = generate_synthetic(200, 128, 7)
-    x = np.repeat(base, 25, axis=0)  # every vector 25 times
+    base = generate_synthetic(50, 128, 7)
+    # every vector 100 times: the 64 best candidates of a query are copies of one vector, so neither the
+    # depth-K1 nor the depth-64 certificate can hold
+    x = np.repeat(base, 100, axis=0)
     q = generate_synthetic(64, 128, 8)
     idx = _flat(128, 0, x)
     got, nfb = _fallbacks(hiplib, lambda: idx.search_batch(q, 10))
