@@ -311,6 +311,19 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
   const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
   return ((uint64_t)hi << 32) | lo;
 }
+// the best 64 of two descending 64-lane lists: the lane-wise max of a and reversed b is bitonic and holds
+// them; a bitonic merge sorts it descending
+__device__ __forceinline__ uint64_t top64_merge(uint64_t a, uint64_t b, int lane) {
+  const uint64_t br = shfl64(b, 63 - lane);
+  uint64_t v = a > br ? a : br;
+#pragma unroll
+  for (int j = 32; j >= 1; j >>= 1) {
+    const uint64_t o = shfl_xor64(v, j);
+    v = (lane & j) == 0 ? (v > o ? v : o) : (v < o ? v : o);
+  }
+  return v;
+}
+
 __device__ __forceinline__ uint64_t sort64_desc(uint64_t v, int lane) {
 #pragma unroll
   for (int k = 2; k <= 64; k <<= 1)
@@ -325,17 +338,19 @@ __device__ __forceinline__ uint64_t sort64_desc(uint64_t v, int lane) {
 
 // One wave per query: aP = the nprobe-th largest approximate score (wselect.h radix select over score
 // keys), the candidates = every centroid whose approximate
-// score reaches aP - 2E (at most 64, in index order), their exact ComputeScore and the first nprobe of
-// them by (score desc, index asc).  Every centroid left out scores exactly below the nprobe centroids
-// whose approximate score reached aP.  More than 64 candidates, or a non-finite query: the exact
-// scores of every centroid go to the row and the query to the fail list (coarse_select_list_kernel).
+// score reaches aP - 2E (at most PICK_MAX = 256, in index order), their exact ComputeScore and the first
+// nprobe of them by (score desc, index asc).  Every centroid left out scores exactly below the nprobe
+// centroids whose approximate score reached aP.  More than 256 candidates (d = 768 widens 2E: P1 at
+// nprobe = 64 keeps ~100), or a non-finite query: the exact scores of every centroid go to the row and
+// the query to the fail list (coarse_select_list_kernel).
 template <int MET, int DT>
 __global__ __launch_bounds__(256) void coarse_pick_kernel(const float *q, const float *c, float *scores, int64_t nq,
                                                           int nc, int Dr, int P, double cnmax, double c_err,
                                                           int32_t *probes, int32_t *fail, int32_t *nfail) {
   const int D = DT > 0 ? DT : Dr;
   __shared__ int hist[4][256];
-  __shared__ int cl[4][64];
+  constexpr int PICK_MAX = 256;
+  __shared__ int cl[4][PICK_MAX];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t qi = (int64_t)blockIdx.x * 4 + w;
   if (qi >= nq) return;  // no block barrier below
@@ -365,7 +380,7 @@ __global__ __launch_bounds__(256) void coarse_pick_kernel(const float *q, const 
         const bool pr = cc < nc && val >= th;
         const uint64_t m = __builtin_amdgcn_ballot_w64(pr);
         const int pos = n + (int)__builtin_popcountll(m & ((1ull << lane) - 1ull));
-        if (pr && pos < 64) cl[w][pos] = cc;
+        if (pr && pos < PICK_MAX) cl[w][pos] = cc;
         n += (int)__builtin_popcountll(m);
       };
       if (nc <= 64 * 16) {
@@ -377,22 +392,28 @@ __global__ __launch_bounds__(256) void coarse_pick_kernel(const float *q, const 
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_wave_barrier();
-      ok = n <= 64;
+      ok = n <= PICK_MAX;
     }
   }
   if (ok) {
-    const int cid = lane < n ? cl[w][lane] : -1;
-    float sc = -INFINITY;
-    for (int p = 0; 8 * p < n; ++p) {
-      const int cc = 8 * p + (lane >> 3);
-      const int id = __shfl(cid, cc);
-      const float v = exact_cs_l8<MET, DT>(qp, c + (size_t)max(id, 0) * D, D, lane & 7);
-      const float t = __shfl(v, 8 * (lane & 7));
-      if ((lane >> 3) == p) sc = t;  // lane 8p + g took candidate 8p + g's score from group g
+    // 64 candidates at a time: exact scores (8 per pass, an 8-lane group each), sorted, merged into the best 64
+    uint64_t best = 0ull;
+    for (int b0 = 0; b0 < n; b0 += 64) {
+      const int m = min(64, n - b0);
+      const int cid = lane < m ? cl[w][b0 + lane] : -1;
+      float sc = -INFINITY;
+      for (int p = 0; 8 * p < m; ++p) {
+        const int cc = 8 * p + (lane >> 3);
+        const int id = __shfl(cid, cc);
+        const float v = exact_cs_l8<MET, DT>(qp, c + (size_t)max(id, 0) * D, D, lane & 7);
+        const float t = __shfl(v, 8 * (lane & 7));
+        if ((lane >> 3) == p) sc = t;  // lane 8p + g took candidate 8p + g's score from group g
+      }
+      uint64_t key = cid >= 0 ? rank_key(sc, cid) : 0ull;
+      key = sort64_desc(key, lane);
+      best = b0 == 0 ? key : top64_merge(best, key, lane);
     }
-    uint64_t key = cid >= 0 ? rank_key(sc, cid) : 0ull;
-    key = sort64_desc(key, lane);
-    if (lane < P) probes[qi * P + lane] = key != 0ull ? 0x7FFFFFFF - (int)(uint32_t)key : -1;
+    if (lane < P) probes[qi * P + lane] = best != 0ull ? 0x7FFFFFFF - (int)(uint32_t)best : -1;
     return;
   }
   // fallback: the exact scores of every centroid into the row, selection by coarse_select_list_kernel
@@ -469,10 +490,11 @@ static void with_list_cap(int nlist, int n, F &&f) {
   else f(std::integral_constant<int, 64>{});
 }
 
-// dim <= 256: measured faster than the dense exact ranking at d = 128 (I1 0.09 vs 0.21 ms, M8 0.80 vs
-// 1.71 ms) and slower at d = 768 (P1: 12.1 vs 4.2 ms, profiles/r3_p1/coarse_mfma_ab.json)
+// measured faster than the dense exact ranking at d = 128 (I1 0.09 vs 0.21 ms, M8 0.80 vs 1.71 ms); at
+// d = 768 (P1) the 64-candidate pick of round 3 sent almost every query to the dense fallback (12.1 vs
+// 4.2 ms, profiles/r3_p1/coarse_mfma_ab.json), hence the 256-candidate pick
 bool coarse_mfma_supported(int nlist, int dim, int metric, int nprobe) {
-  return (metric == L2 || metric == IP) && dim > 0 && dim % 16 == 0 && dim <= 256 && nlist >= 1 && nprobe >= 1 &&
+  return (metric == L2 || metric == IP) && dim > 0 && dim % 16 == 0 && dim <= 1024 && nlist >= 1 && nprobe >= 1 &&
          nprobe <= 64;
 }
 
@@ -495,6 +517,7 @@ void launch_coarse_mfma(const float *q, const float *cents_rm, const float *c2, 
       case 32: go(met, std::integral_constant<int, 32>{}); return;
       case 64: go(met, std::integral_constant<int, 64>{}); return;
       case 128: go(met, std::integral_constant<int, 128>{}); return;
+      case 768: go(met, std::integral_constant<int, 768>{}); return;
       default: go(met, std::integral_constant<int, 0>{}); return;
     }
   };

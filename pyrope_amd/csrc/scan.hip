@@ -13,9 +13,9 @@
 //     (r, h) holds row r, dims 16s + 8h .. +7: the tile layout is lane-linear for it as it stands), a
 //     query group is 32 queries, and the 32 x 32 result leaves lane (r, h) query r's scores of rows
 //     8b + 4h + i (b, i < 4): per (tile, group) 8 MFMAs against 8 ds_read_b128 and a 16-value epilogue.
-//     16 waves per block (4 per SIMD, <= 128 VGPRs): no register prefetch of a wave's next tile; it
-//     is pulled into L2 by one 4-byte LDS-DMA per line while the current one is scored, and tiles are
-//     taken from an LDS counter so the waves reach the item's end together.
+//     16 waves per block (4 per SIMD, <= 128 VGPRs): no prefetch of a wave's next tile (the other 15
+//     waves' work hides its load; an L2 prefetch by LDS-DMA measured slower), and tiles are taken from
+//     an LDS counter so the waves reach the item's end together.
 //  3. Emitted rows are staged in LDS and written to the candidate regions by the whole block at the
 //     item's end (64 rows per store instruction instead of one).
 //
@@ -215,12 +215,12 @@ __global__ __launch_bounds__(256) void sample_kernel(StreamArgs a) {
 
 // ---- 2. the list scan ----
 // AB (measurement only, PYR_FILTER_ABLATE): 1 (64) = no emission, 2 (128) = tile stream only (no MFMA),
-// 3 (256) = no emission and every tile read from the item's first one (compute without HBM)
-// PIPE (D <= 128, PYR_SCAN_PIPE=n): n = 8 or 12 waves (<= 256 / 170 VGPRs), the next group's B operands read
-// from LDS while the current group's MFMA chain runs (two operand buffers, groups taken in pairs)
-template <int D, int MET, int AB = 0, int PIPE = 0>
-__global__ __launch_bounds__(64 * (PIPE ? PIPE : nw_of(D)), 1) void scan_kernel(StreamArgs a) {
-  constexpr int NW = PIPE ? PIPE : nw_of(D);  // waves per block
+// 3 (256) = no emission and every tile read from the item's first one (compute without HBM); the bit 512
+// (any variant) adds an L2 prefetch of the wave's next tile (4-byte LDS-DMA per line; measured slower:
+// 0.94 vs 0.90 ms and FETCH 1.83x vs 1.09x the stored bytes at I1, profiles/r4_scan)
+template <int D, int MET, int AB = 0>
+__global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
+  constexpr int NW = nw_of(D);       // waves per block
   constexpr int KS = D / 16;         // 32x32x16 k-steps
   constexpr int KC = KS < 16 ? KS : 16;  // k-steps of A held in registers at a time (D > 256: chunks)
   constexpr int NC = KS / KC;
@@ -416,7 +416,7 @@ __global__ __launch_bounds__(64 * (PIPE ? PIPE : nw_of(D)), 1) void scan_kernel(
                                                               acc[j], 0, 0, 0);
           }
         }
-        if (c == 0 && tpf >= 0) prefetch(tpf);
+        if (c == 0 && tpf >= 0 && (a.ablate & 512)) prefetch(tpf);
       }
 #pragma unroll
       for (int j = 0; j < NG; ++j) {
@@ -437,34 +437,6 @@ __global__ __launch_bounds__(64 * (PIPE ? PIPE : nw_of(D)), 1) void scan_kernel(
         if (v == 12345.0f) cnt_l[0] = 1;
         return;
       }
-      if constexpr (PIPE) {
-        // groups in pairs: b1 <- group j + 1 while group j's chain runs on b0, b0 <- group j + 2 during j + 1's
-        h8v b0[KS], b1[KS];
-        read_b(0, b0);
-        auto group = [&](int j, const h8v (&B)[KS]) {
-          const float2 q = qf[32 * j + r];
-          f16v acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[0], B[0], (f16v){}, 0, 0, 0);
-#pragma unroll
-          for (int s = 1; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[s], B[s], acc, 0, 0, 0);
-          if (j == 0 && tpf >= 0) {
-#pragma unroll
-            for (int o = 0; o < TB; o += 64 * 128)
-              glds<4>(hsrc + (size_t)(r0 / 32 + tpf) * TB + min(o + lane * 128, TB - 128), sink);
-            glds<4>(a.mub + r0 + 32 * tpf + (lane & 31), sink);
-          }
-          const bool e = epi_test(acc, mr, q);
-          if (__builtin_expect(e, 0)) emit_y(acc, q.y, 32 * j + r, rt);
-        };
-        for (int j = 0; j < ng; j += 2) {
-          if (j + 1 < ng) read_b(j + 1, b1);
-          group(j, b0);
-          if (j + 1 < ng) {
-            if (j + 2 < ng) read_b(j + 2, b0);
-            group(j + 1, b1);
-          }
-        }
-        return;
-      }
       for (int j = 0; j < ng; ++j) {
         const float2 q = qf[32 * j + r];
         h8v bj[KS];
@@ -476,7 +448,7 @@ __global__ __launch_bounds__(64 * (PIPE ? PIPE : nw_of(D)), 1) void scan_kernel(
         // all of the group's operand reads before its chain (one LDS wait, not one per MFMA)
         __builtin_amdgcn_sched_group_barrier(0x100, KS + 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x008, KS, 0);
-        if (j == 0 && tpf >= 0) {  // the tile's own loads were waited for before the chain: warm L2
+        if (j == 0 && tpf >= 0 && (a.ablate & 512)) {  // the tile's own loads were waited for: warm L2
 #pragma unroll
           for (int o = 0; o < TB; o += 64 * 128)
             glds<4>(hsrc + (size_t)(r0 / 32 + tpf) * TB + min(o + lane * 128, TB - 128), sink);
@@ -521,16 +493,7 @@ template <int D, int MET>
 void launch_scan_dm(const StreamArgs &a, int max_items, hipStream_t st) {
   const int grid = std::max(1, std::min(max_items, device_cus()));
   const dim3 b(64 * nw_of(D));
-  if constexpr (D == 128) {  // the ablations and the pipelined variant (measurement only) at the I1 dimension
-    static const int pipe = getenv("PYR_SCAN_PIPE") ? atoi(getenv("PYR_SCAN_PIPE")) : 0;
-    if (pipe == 8 && !a.ablate) {
-      hipLaunchKernelGGL((scan_kernel<D, MET, 0, 8>), dim3(grid), dim3(64 * 8), 0, st, a);
-      return;
-    }
-    if (pipe == 12 && !a.ablate) {
-      hipLaunchKernelGGL((scan_kernel<D, MET, 0, 12>), dim3(grid), dim3(64 * 12), 0, st, a);
-      return;
-    }
+  if constexpr (D == 128) {  // the ablations (measurement only) at the I1 dimension
     if (a.ablate & 64) {
       hipLaunchKernelGGL((scan_kernel<D, MET, 1>), dim3(grid), b, 0, st, a);
       return;

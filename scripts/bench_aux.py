@@ -97,6 +97,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--check", type=int, default=20, help="queries compared with the CPU oracle")
+    ap.add_argument("--recall-queries", type=int, default=0, help="ivfpq: recall@k vs exact FLAT over all N rows")
     ap.add_argument("--train-rows", type=int, default=0,
                     help="ivfpq: train the quantizers on the first N rows and stream the rest (0 = all rows)")
     ap.add_argument("--cpu-seconds", type=float, default=0.0,
@@ -218,15 +219,43 @@ def main():
         run_sweep(idx, q, opts, s, lab)
         cb, codes, off, labels, live = idx.pq_state()
         cents = idx.centroids_array()
-        ok = True
-        for i in np.linspace(0, a.nq - 1, a.check).astype(int):
+        from concurrent.futures import ThreadPoolExecutor
+        from bench import host_cpus
+        chk = np.linspace(0, a.nq - 1, a.check).astype(int)
+
+        def chk_one(i):  # the oracle's IvfPq search of query i (one query per thread; ctypes drops the GIL)
             os_, ok_ = oracle.ivfpq_search(qh[i], a.k, cents, codes, off, cb, live, metric=a.metric, nprobe=a.nprobe)
-            ok &= bool(np.array_equal(lab[i], labels[ok_]) and np.array_equal(s[i].view(np.uint32),
-                                                                               os_.view(np.uint32)))
+            return bool(np.array_equal(lab[i], labels[ok_]) and np.array_equal(s[i].view(np.uint32),
+                                                                                 os_.view(np.uint32)))
+        t1 = time.time()
+        with ThreadPoolExecutor(host_cpus()["usable"]) as ex:
+            eq = list(ex.map(chk_one, chk))
+        ok = all(eq)
+        log(f"parity: {sum(eq)} of {len(eq)} sampled queries bit-identical to the oracle ({time.time() - t1:.1f}s)")
+        recall = None
+        if a.recall_queries > 0:
+            # recall@10 against the exact top-10 over all N rows: the base rows streamed through a FLAT L2
+            # index chunk by chunk (BruteForceVectorIndex.Search, exact), per-query top-10 merged on the host
+            R = min(a.recall_queries, a.nq)
+            t1 = time.time()
+            gs = np.full((R, a.k * 2), -np.inf, np.float32)
+            gl = np.full((R, a.k * 2), -1, np.int64)
+            step = 4 << 20
+            for r0 in range(0, n, step):
+                cn = min(step, n - r0)
+                f = BruteForceVectorIndex(d, 0)
+                f.add_labels(np.arange(r0, r0 + cn, dtype=np.int64), generate_synthetic_blocked(r0, cn, d, 42),
+                             track_ids=False)
+                fs, fl, _ = f.search_batch(qh[:R], a.k)
+                f.close()
+                cs_, cl_ = np.concatenate([gs[:, :a.k], fs], 1), np.concatenate([gl[:, :a.k], fl], 1)
+                o = np.lexsort((cl_, -cs_), axis=1)[:, :a.k]
+                gs[:, :a.k], gl[:, :a.k] = np.take_along_axis(cs_, o, 1), np.take_along_axis(cl_, o, 1)
+            gt = gl[:, :a.k]
+            recall = sum(len(set(gt[i].tolist()) & set(lab[i].tolist())) for i in range(R)) / (R * a.k)
+            log(f"recall@{a.k} over {R} queries: {recall:.4f} ({time.time() - t1:.1f}s)")
         cpu = None
         if a.cpu_seconds > 0:  # CPU baseline leg: the oracle's IvfPq search, one query per thread
-            from concurrent.futures import ThreadPoolExecutor
-            from bench import host_cpus
             host = host_cpus()
             th = host["usable"]
 
@@ -254,7 +283,13 @@ def main():
                "scan_rows": scan["work"],
                "lookups_per_s": scan["work"] * a.m / (scan["ms"] * 1e-3),
                "roofline": pq_roofline(scan["work"] * a.m / (scan["ms"] * 1e-3)),
-               "parity_sample": {"queries": a.check, "ids_and_bits_equal": ok}, "cpu_baseline": cpu}
+               "parity_sample": {"queries": a.check, "ids_and_bits_equal": ok}, "recall_at_10": recall,
+               "cpu_baseline": cpu}
+        if os.environ.get("PYR_PQ_MFMA", "1") != "0" and "pq_scan" in phases:  # the matrix-core scan (pq32.hip)
+            sc = phases["pq_scan"]
+            out["mfma"] = {"achieved": sc["work"] * 2 * d / (sc["ms"] * 1e-3) / 1e12, "peak": 2500.0,
+                           "unit": "TFLOP/s", "frac": sc["work"] * 2 * d / (sc["ms"] * 1e-3) / 1e12 / 2500.0,
+                           "note": "decoded (query, code row) pairs x 2 D fp16 MFMA flops vs the dense fp16 peak"}
     print(json.dumps(out), flush=True)
 
 

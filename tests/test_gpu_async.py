@@ -157,8 +157,10 @@ def _flat_index(metric):
 def test_flat_search_device_graph_capture_and_replay(hiplib, metric, force_fail):
     """FLAT search_device on the stream scan (L2, IP and Cosine) enqueues only -- the
     certificates and the exact re-run of failures run from device-side counts -- so it captures into a
-    HIP graph (a host synchronization inside the capture would fail it) and replays with new queries,
-    also when every certificate fails (PYR_FILTER_CERR: every query takes the device re-run)."""
+    HIP graph (a host synchronization inside the capture would fail it); the graph, replayed with other
+    queries in the captured buffer, returns their results, also when every certificate fails
+    (PYR_FILTER_CERR: every query takes the device re-run).  Then two batches enqueued back to back on
+    one stream without a host synchronization give each batch's own results."""
     import torch
 
     from pyrope_amd import generate_synthetic
@@ -170,22 +172,29 @@ def test_flat_search_device_graph_capture_and_replay(hiplib, metric, force_fail)
         ra, rb = idx.search_batch(qa, 10), idx.search_batch(qb, 10)
         st = torch.cuda.Stream()
         qbuf = torch.from_numpy(qa).cuda()
-        with torch.cuda.stream(st):
-            out = _dev_search(idx, qbuf, 10, None, st)  # warm-up: workspace and row terms sized
+        out = (torch.empty((n, 10), dtype=torch.float32, device="cuda"),
+               torch.empty((n, 10), dtype=torch.int64, device="cuda"),
+               torch.empty((n,), dtype=torch.int32, device="cuda"))
+        args = (qbuf.data_ptr(), n, 10, out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(), st.cuda_stream, None)
+        idx.search_device(*args)  # warm-up: workspace and row terms sized
         st.synchronize()
-        g = torch.cuda.CUDAGraph()
+        g = torch.cuda.CUDAGraph(keep_graph=True)
         with torch.cuda.graph(g, stream=st):
-            idx.search_device(qbuf.data_ptr(), n, 10, out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(),
-                              st.cuda_stream, None)
+            idx.search_device(*args)
+        g.instantiate()
         qbuf.copy_(torch.from_numpy(qb))
         torch.cuda.synchronize()
         g.replay()
         torch.cuda.synchronize()
         _same(out, rb)
-        qbuf.copy_(torch.from_numpy(qa))
+        # back to back on one stream, no host synchronization in between
+        qa_d, qb_d = torch.from_numpy(qa).cuda(), torch.from_numpy(qb).cuda()
         torch.cuda.synchronize()
-        g.replay()
-        torch.cuda.synchronize()
-        _same(out, ra)
+        with torch.cuda.stream(st):
+            oa = _dev_search(idx, qa_d, 10, None, st)
+            ob = _dev_search(idx, qb_d, 10, None, st)
+        st.synchronize()
+        _same(oa, ra)
+        _same(ob, rb)
     with _env(PYR_FILTER=0):
-        _same(out, idx.search_batch(qa, 10))
+        _same(oa, idx.search_batch(qa, 10))
