@@ -248,6 +248,7 @@ def main():
                              track_ids=False)
                 fs, fl, _ = f.search_batch(qh[:R], a.k)
                 f.close()
+                log(f"recall truth: rows [{r0}, {r0 + cn}) ({time.time() - t1:.1f}s)")
                 cs_, cl_ = np.concatenate([gs[:, :a.k], fs], 1), np.concatenate([gl[:, :a.k], fl], 1)
                 o = np.lexsort((cl_, -cs_), axis=1)[:, :a.k]
                 gs[:, :a.k], gl[:, :a.k] = np.take_along_axis(cs_, o, 1), np.take_along_axis(cl_, o, 1)
