@@ -38,8 +38,8 @@ __device__ __forceinline__ size_t blk_off(int64_t r, int d, int D) {
 }
 #include "vmath.h"
 
-constexpr int PNW = 8;       // waves per scan block
-constexpr int PQG = 2;       // 32-query groups per item (64 queries: 96 KiB of operands at D = 768)
+constexpr int PNW = 16;      // waves per scan block
+constexpr int PQG = 3;       // 32-query groups per item (96 queries: 144 KiB of operands at D = 768)
 constexpr int PQMAX = 32 * PQG;
 constexpr int PSAMPLE_TILES = 2 * PNW;
 constexpr int PSV = 2 * PNW;  // sample values per (query, probe): one per (wave, lane half)
@@ -129,7 +129,7 @@ __global__ __launch_bounds__(64 * PNW, 1) void pq_scan_kernel(StreamArgs a, cons
   __shared__ int cnt_l[PQMAX];
   __shared__ uint32_t flr_l[PQMAX];
   __shared__ int item_sh, eb_n;
-  constexpr int EB = 1024;
+  constexpr int EB = 768;
   __shared__ uint2 eb[EB];
   const uint32_t bl_base = (uint32_t)(size_t)(lds_void *)bl;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
@@ -189,7 +189,9 @@ __global__ __launch_bounds__(64 * PNW, 1) void pq_scan_kernel(StreamArgs a, cons
         atomicMax(&flr_l[qi], score_key(sc));
       }
     };
-    float smx[2] = {-INFINITY, -INFINITY};  // SAMPLE: this lane's best bound per query group
+    float smx[PQG];  // SAMPLE: this lane's best bound per query group
+#pragma unroll
+    for (int g = 0; g < PQG; ++g) smx[g] = -INFINITY;
 #pragma unroll 1
     for (int t = w; t < nt; t += PNW) {
       const uint4 *cp = reinterpret_cast<const uint4 *>(cpk + ((size_t)(r0 / 32 + t) * 64 + lane) * MB);
@@ -224,6 +226,7 @@ __global__ __launch_bounds__(64 * PNW, 1) void pq_scan_kernel(StreamArgs a, cons
           else A = *reinterpret_cast<const h8v *>(cbb + (size_t)(2 * s) * 256 * 16 + c * 16);
 #pragma unroll
           for (int g = 0; g < PQG; ++g) {
+            if (g >= ng) break;  // (wave-uniform) a short item skips the empty groups' MFMAs
             const h8v B = *reinterpret_cast<const h8v *>(bl + (g * KS + s) * 1024 + lane * 16);
             acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, B, acc[g], 0, 0, 0);
           }
