@@ -481,10 +481,13 @@ static int stream_prec() {
 // placeholders at T_q and the certificate decides); R trades emitted rows against queries with fewer
 // than k real candidates.  The sample holds a fraction f of a query's probed rows (I1: ~5 %), so about
 // R / f rows reach T_q, and a query falls short of K1 = 16 only when R of its 15 best rows were
-// sampled: P ~ C(15, R) f^R, 2.5e-7 at R = 8, f = 0.05.  Short lists sample most of their rows
-// (f -> 1): there R = K1/2 leaves ~R real candidates, below k, and every such query fails its
-// certificate -- so R = clamp(ceil(8 K1 f), K1/2, K1) per query (sselect_kernel): ~8 K1 emitted rows
-// at small f, R = K1 once f >= 1/8.  PYR_STREAM_RANK fixes R.
+// sampled: P ~ C(15, R) f^R, 7.8e-5 at R = 6, f = 0.05.  Short lists sample most of their rows
+// (f -> 1): there a small R leaves ~R real candidates, below k, and every such query fails its
+// certificate -- so R = clamp(ceil(6 K1 f), 3 K1 / 8, K1) per query (sselect_kernel): ~6 K1 emitted rows
+// at small f, R = K1 once f >= 1/6.  Every emitted row costs the scan a wave-uniform branch and an LDS
+// atomic: at I1, R = 8 -> 6 cuts the scan from 0.904 to 0.853 ms with no re-run, R = 5 re-runs 9 of 10,000
+// queries (+0.16 ms), R = 4 51 (+0.55 ms) (profiles/r4_scan/sweep_sample_rank*.log).  PYR_STREAM_RANK
+// fixes R.
 static void stream_rank(int k1, int32_t &rmin, int32_t &rmax, double &et) {
   if (const char *e = getenv("PYR_STREAM_RANK")) {
     rmin = rmax = std::max(1, atoi(e));
@@ -493,9 +496,9 @@ static void stream_rank(int k1, int32_t &rmin, int32_t &rmax, double &et) {
   }
   // PYR_STREAM_RMIN / PYR_STREAM_ET (measurement only): the floor of R and the emitted-row target per K1
   const char *rm = getenv("PYR_STREAM_RMIN"), *ev = getenv("PYR_STREAM_ET");
-  rmin = std::max(1, rm ? atoi(rm) : k1 / 2);
+  rmin = std::max(1, rm ? atoi(rm) : (3 * k1 + 7) / 8);
   rmax = std::max(rmin, k1);
-  et = (ev ? atof(ev) : 8.0) * k1;
+  et = (ev ? atof(ev) : 6.0) * k1;
 }
 // candidate region per (query, part) (PYR_STREAM_CAP) and rows per list chunk (PYR_STREAM_CHUNK)
 static int stream_cap() {

@@ -1573,11 +1573,15 @@ __global__ __launch_bounds__(256) void ivf_rerun_scan_kernel(IvfRerunArgs a, uin
 }
 
 // one wave per failing query: its nprobe x nc partial lists merged, the top k written at the query's row
+__device__ void rerun_merge_one(IvfRerunArgs a, const uint64_t *part, int64_t i, int lane);
 __global__ __launch_bounds__(256) void ivf_rerun_merge_kernel(IvfRerunArgs a, const uint64_t *part) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t i = (int64_t)blockIdx.x * 4 + w;
   const int64_t nfail = *a.nfail;
-  if (i >= nfail) return;
+  // grid-stride over the failing queries (a small grid: it exits at once when nothing failed)
+  for (int64_t i = (int64_t)blockIdx.x * 4 + w; i < nfail; i += (int64_t)gridDim.x * 4) rerun_merge_one(a, part, i, lane);
+}
+__device__ void rerun_merge_one(IvfRerunArgs a, const uint64_t *part, int64_t i, int lane) {
+  const int64_t nfail = *a.nfail;
   const int k = a.k;
   const int64_t q = a.fail[i];
   const int nc = rr_nchunks(nfail * a.nprobe, a.nchunk);
@@ -1959,7 +1963,8 @@ void launch_ivf_exact_rerun(const IvfRerunArgs &a, int metric, int64_t max_fail,
   else
     by_dim(ivf_rerun_scan_kernel<COS, 32>, ivf_rerun_scan_kernel<COS, 64>, ivf_rerun_scan_kernel<COS, 128>,
            ivf_rerun_scan_kernel<COS, 0>);
-  hipLaunchKernelGGL(ivf_rerun_merge_kernel, dim3((unsigned)((max_fail + 3) / 4)), dim3(256), 0, st, a, part);
+  hipLaunchKernelGGL(ivf_rerun_merge_kernel, dim3((unsigned)std::min<int64_t>((max_fail + 3) / 4, 256)), dim3(256), 0,
+                     st, a, part);
 }
 
 }  // namespace pyr
