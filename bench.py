@@ -339,39 +339,19 @@ def run(args):
     # (PYR_FILTER=0): sub, mul, add per element, 3*D
     flops = scan["pairs"] * (2 if filt else 3) * D
     achieved = flops / (scan["ms"] * 1e-3) / 1e12
-    # the list-scan kernel and arithmetic (engine.cpp search_filter / search_stream): by default the
-    # stream-and-emit scan (stream16.hip) with one fp16 MFMA per k-step (PYR_STREAM_PREC=2: the hi/lo
-    # query split, 2); PYR_IVF_STREAM=0 -> the round-2 filter kernels (PYR_FILTER_PREC: 2 = fp16 tiles
-    # with the hi/lo split, 3 = one fp16 MFMA, 1 = bf16x3, 0 = fp32 MFMA)
-    prec = int(os.environ.get("PYR_FILTER_PREC", "2")) if filt else -1
-    stream = filt and prec in (2, 3) and os.environ.get("PYR_IVF_STREAM", "1") != "0" and D in (32, 64, 128)
-    wide = os.environ.get("PYR_F16_WIDE", "1") != "0"
-    if stream:
-        q2 = os.environ.get("PYR_STREAM_PREC", "3") == "2"
-        r4 = not q2 and os.environ.get("PYR_STREAM_MFMA", "32") != "16"
-        mfma_mult, mfma_peak = (2 if q2 else 1), BF16_PEAK_TFLOPS
-        if r4:
-            kernel_tag = "scan32"
-            kernel_name = (f"scan_kernel<{D},L2> (scan.hip: IVF list scan, stream-and-emit over fp16 residual tiles: "
-                           f"persistent 16-wave blocks, tiles from HBM into registers as the A operand of "
-                           f"v_mfma_f32_32x32x16_f16, queries from LDS, one MFMA per 16-dim k-step)")
-        else:
-            kernel_tag = "stream16"
-            kernel_name = (f"stream16_kernel<{D},L2,{'f16x2' if q2 else 'f16x1'},MAIN> (IVF list scan, stream-and-emit "
-                           f"over fp16 residual tiles: persistent 8-wave blocks, tiles straight from HBM into "
-                           f"registers, rows as the A operand of v_mfma_f32_16x16x32_f16, {2 if q2 else 1} MFMA per "
-                           f"k-step)")
+    # the list-scan kernel (engine.cpp search_stream): the stream-and-emit scan (scan.hip), one fp16 MFMA
+    # per 16-dim k-step; PYR_FILTER=0: the exact VALU scan (kernels.hip scan_fast)
+    prec = 3 if filt else -1
+    if filt:
+        mfma_mult, mfma_peak = 1, BF16_PEAK_TFLOPS
+        kernel_tag = "scan32"
+        kernel_name = (f"scan_kernel<{D},L2> (scan.hip: IVF list scan, stream-and-emit over fp16 residual tiles: "
+                       f"persistent 16-wave blocks, tiles from HBM into registers as the A operand of "
+                       f"v_mfma_f32_32x32x16_f16, queries from LDS, one MFMA per 16-dim k-step)")
     else:
-        kernel_tag = {2: "filter16w" if wide else "filter16", 3: "filter16"}.get(prec, "filter")
-        mfma_mult, mfma_peak = {2: (2, BF16_PEAK_TFLOPS), 3: (1, BF16_PEAK_TFLOPS), 1: (3, BF16_PEAK_TFLOPS),
-                                0: (1, FP32_PEAK_TFLOPS)}.get(prec, (1, FP32_PEAK_TFLOPS))
-        kernel_name = {2: ("mfma_filter16w<128,L2,16,f16x2> (IVF list scan, fp16 residual tiles, 8 waves x 16 queries, "
-                           "2 v_mfma_f32_16x16x32_f16 per k-step)") if wide else
-                          "mfma_filter16<128,L2,16,f16x2> (IVF list scan, fp16 residual tiles, 2 fp16 MFMAs per k-step)",
-                       3: "mfma_filter16<128,L2,16,f16x1> (IVF list scan, fp16 residual tiles, 1 fp16 MFMA per k-step)",
-                       1: "mfma_filter<128,L2,IVF> (IVF list scan, bf16x3 MFMA candidate filter)",
-                       0: "mfma_filter<128,L2,IVF> (IVF list scan, fp32 MFMA candidate filter)"}.get(
-                           prec, "scan_fast<128,1,L2,IVF> (IVF list scan, exact VALU)")
+        kernel_tag = "scan_fast"
+        mfma_mult, mfma_peak = 1, FP32_PEAK_TFLOPS
+        kernel_name = "scan_fast<128,1,L2,IVF> (IVF list scan, exact VALU)"
     # unique algorithmic bytes of one list-scan launch on this rank: every list probed by any query
     # of the batch read once (its live rows of this shard x D x 4 B) plus the batch's queries -- the
     # HBM floor of a batched, list-major scan (SURVEY.md 8(d) "unique-bytes roofline")

@@ -400,82 +400,28 @@ static int pq_adc_mode() {
 }
 
 // ---------------------------------------------------------------------------
-// MFMA candidate filter + exact refine (filter.hip).  Same results as the exact scans
-// (certified per query, failures re-run exactly); PYR_FILTER=0 forces the exact scans,
-// PYR_FILTER_MARGIN sets the minimum K1 - k (default 4, see filter_k1).
+// Stream-and-emit scan + certified exact refine (scan.hip, stream16.hip, filter.hip).  Same results as
+// the exact scans (certified per query, failures re-run exactly on the device); PYR_FILTER=0 forces the
+// exact scans, PYR_FILTER_MARGIN sets the minimum K1 - k (default 4, see filter_k1).
 // ---------------------------------------------------------------------------
 static bool filter_enabled() {
   const char *e = getenv("PYR_FILTER");
   return !(e && atoi(e) == 0);
 }
-static int filter_pub_mask() {  // FilterArgs::pub_mask; PYR_FILTER_PUB overrides (2^n - 1)
-  const char *e = getenv("PYR_FILTER_PUB");
-  return e ? atoi(e) : 15;  // 15 vs 7: I1 list scan 2.88 -> 2.81 ms (profiles/r2_wide/sweep_knobs_ablations.log)
-}
-// approximate-score arithmetic of the filter: bf16x3 (default) or fp32 (PYR_FILTER_PREC=0)
-static int filter_prec() {
-  const char *e = getenv("PYR_FILTER_PREC");
-  if (!e) return FILTER_F16X2;
-  const int v = atoi(e);
-  return (v >= FILTER_FP32 && v <= FILTER_F16X1) ? v : FILTER_F16X2;
-}
-static bool prec16(int prec) { return prec == FILTER_F16X2 || prec == FILTER_F16X1; }
-// the fp16 tile copy is kept for stores the fp16 filter can scan
-// fp16 tiles are kept where a filter can use them: the round-3 filter's dims, or the stream scan's
-static bool store16(int dim, int metric) {
-  return filter16_supported(dim, metric, 16) || ((metric == L2 || metric == IP) && scan_tile_dim(dim) > 0);
-}
-// the tile dimension of a store of dim (the stream scan's padding where the round-3 kernels have none)
-static int store16_dt(int dim) { return filter16_supported(dim, L2, 16) ? dim : scan_tile_dim(dim); }
-// the arithmetic a filter launch really runs: the fp16 tile filter needs the store's fp16 tiles and
-// items of at most filter16_max_rows() rows; otherwise an fp16 request runs as bf16x3
-static int filter_prec_for(int prec, bool f16_store, int64_t max_item_rows) {
-  if (!prec16(prec)) return prec;
-  return f16_store && max_item_rows <= filter16_max_rows() ? prec : FILTER_BF16X3;
-}
-// waves per filter block for IVF items (FilterArgs::waves): 4 = 128-query items (default);
-// PYR_FILTER_WAVES=8 -> 256-query items, one block per CU (bf16x3 only): half the row
-// traffic but measured slower, 4.98 -> 7.42 ms at the bench config (profiles/r1_sweeps/sweep23).
-// FLAT items always use 4.
-// waves per IVF filter block: 8 (bf16x3, 256-query items), 16 (fp16 tiles, K1 = 16 only: 256-query
-// items on the 16-wave mfma_filter16w), else 4 (128-query items)
-static int filter_waves_ivf(int k1, int prec) {
-  const char *e = getenv("PYR_FILTER_WAVES");
-  const int w = e ? atoi(e) : 4;
-  if (w == 16 && prec16(prec) && k1 == 16) return 16;
-  return (w == 8 && prec == FILTER_BF16X3) ? 8 : 4;
-}
-// stream-and-emit list scan (stream16.hip) for the fp16 IVF filter: PYR_IVF_STREAM=0 -> the round-2
-// list scans (filter16.hip)
-static bool stream_enabled() {
-  const char *e = getenv("PYR_IVF_STREAM");
-  return !(e && atoi(e) == 0);
-}
-// query terms of the stream scan: 3 = one fp16 term (default), 2 = the hi/lo split (2 MFMAs per k-step)
-// the round-4 list scan (scan.hip: fused sample, 32x32x16 MFMA, 16 waves); PYR_STREAM_MFMA=16 runs the
-// round-3 stream16.hip kernels (measurement only; results identical)
-static bool stream_r4() {
-  const char *e = getenv("PYR_STREAM_MFMA");
-  return !(e && atoi(e) == 16);
-}
-// the query operands and the sample of the round-4 scan: at the dims the round-3 kernels are built for
-// (tile dim = dim = 32 / 64 / 128) sprep + the 8-wave sample pass, which share each sampled tile across
-// the item's queries through LDS (0.14 ms at I1); elsewhere scan.hip's one-wave-per-32-queries sample
-// (0.30 ms at I1: every group re-reads the sampled tiles).  Both write the same bq / qsc / samp.
-// PYR_SCAN_SAMPLE=1: scan.hip's sample at every dim (measurement only).
+// fp16 tiles are kept where the stream scan can use them (L2 / IP, tile dims up to 768)
+static bool store16(int dim, int metric) { return (metric == L2 || metric == IP) && scan_tile_dim(dim) > 0; }
+// the tile dimension of a store of dim (zero-padded for the stream scan)
+static int store16_dt(int dim) { return scan_tile_dim(dim); }
+// the query operands and the sample of the stream scan: at tile dim = dim = 32 / 64 / 128 sprep + the
+// 8-wave sample (sample16.hip), which shares each sampled tile across the item's queries through LDS
+// (0.15 ms at I1); elsewhere scan.hip's one-wave-per-32-queries sample (0.29 ms at I1: every group
+// re-reads the sampled tiles).  Both write the same bq / qsc / samp.  PYR_SCAN_SAMPLE=1: scan.hip's
+// sample at every dim (measurement only).
 static void stream_sample(const StreamArgs &sa, int met, int maxi, hipStream_t st) {
   const char *e = getenv("PYR_SCAN_SAMPLE");
   const int dt = sa.dt > 0 ? sa.dt : sa.dim;
-  if (!(e && atoi(e) == 1) && dt == sa.dim && stream16_supported(sa.dim, met, 1)) {
-    launch_stream_prep(sa, met, maxi, st);
-    launch_stream_scan(sa, met, maxi, true, st);
-  } else {
-    launch_scan_sample(sa, met, maxi, st);
-  }
-}
-static int stream_prec() {
-  const char *e = getenv("PYR_STREAM_PREC");
-  return e && atoi(e) == 2 ? FILTER_F16X2 : FILTER_F16X1;
+  if (!(e && atoi(e) == 1) && dt == sa.dim && sample16_supported(sa.dim, met)) launch_sample16(sa, met, maxi, st);
+  else launch_scan_sample(sa, met, maxi, st);
 }
 // T_q = the R-th largest sample value.  Any R is correct (rows below T_q are represented by floor
 // placeholders at T_q and the certificate decides); R trades emitted rows against queries with fewer
@@ -550,12 +496,7 @@ void ivf_memory_plan(int dim, int64_t nrows, int nlist, int64_t max_len, int64_t
   w += 8 * ivf_rerun_part_keys(qs, probes, k);                                 // device re-run scratch
   *workspace_bytes = w;
 }
-// XCD-major mapping of IVF filter items (FilterArgs::xcd); PYR_FILTER_XCD=0 disables it
-static int filter_xcd() {
-  const char *e = getenv("PYR_FILTER_XCD");
-  return e ? (atoi(e) != 0) : 1;
-}
-static int filter_ablate() {  // measurement only (FilterArgs::ablate)
+static int filter_ablate() {  // measurement only (StreamArgs::ablate)
   const char *e = getenv("PYR_FILTER_ABLATE");
   return e ? atoi(e) : 0;
 }
@@ -568,12 +509,6 @@ static int filter_k1(int k) {
     if (k + m <= c) return c;
   return 0;
 }
-// K1 of the filter re-run of certificate failures: 64 when that widens the margin, else 0 (exact)
-static int filter_k1_next(int k, int k1) {
-  const char *e = getenv("PYR_FILTER_TIER");
-  if (e && atoi(e) == 0) return 0;
-  return (k1 < 64 && k + 4 <= 64) ? 64 : 0;
-}
 // error-bound constant of the refine certificate (filter.hip refine_kernel); PYR_FILTER_CERR
 // overrides it for tests (a huge value fails every certificate -> every query re-runs exactly)
 static double filter_cerr(int dim) {
@@ -581,98 +516,14 @@ static double filter_cerr(int dim) {
   return 4.0 * dim + 64.0;
 }
 
-// merge the K1-candidate partials, re-score exactly, certify; returns the number of
-// queries whose certificate failed (listed in ws.fail).  Synchronizes ws.st.
-// Cosine over a unit-row L2 store (FlatIndex::search_cosine): the candidates are re-scored with the
-// reference Cosine on the raw rows of the index itself, and the certificate is taken in cosine units
+// Cosine over a unit-row L2 store (FlatIndex::search_cosine_stream): the candidates are re-scored with
+// the reference Cosine on the raw rows of the index itself, and the certificate is taken in cosine units
 struct CosRefine {
   const RowStore *raw;     // the Cosine index's store (raw rows, norms, labels, non-finite flag)
   const float *queries;    // raw queries
   const float *qnorm;      // ComputeNorm per query
   const uint32_t *zflag;   // a zero-norm row was written
 };
-
-static int64_t filter_finish(Workspace &ws, int64_t nq, int nparts, int k1, int k, int dim, int met, int V,
-                             const float *d_q, const RowStore &rs, const MergeIvf *mi, float *d_s, int64_t *d_l,
-                             int32_t *d_c, const uint32_t *list_rmax = nullptr, const float *resid_cents = nullptr,
-                             const uint32_t *list_rmax_r = nullptr, int prec = -1, const CosRefine *cr = nullptr) {
-  ws.ms.ensure(sizeof(float) * nq * k1);
-  ws.mk.ensure(sizeof(int32_t) * nq * k1);
-  {
-    PhaseTimer t(PH_MERGE, ws.st);
-    launch_merge_keys(ws.part_s.as<float>(), ws.part_k.as<uint32_t>(), nq, nparts, k1, nullptr, nullptr,
-                      ws.ms.as<float>(), nullptr, ws.mk.as<int32_t>(), nullptr, ws.st, mi);
-  }
-  ws.fail.ensure(sizeof(int32_t) * nq);
-  ws.fail_cnt.ensure(sizeof(int32_t));
-  HIPCHK(hipMemsetAsync(ws.fail_cnt.p, 0, sizeof(int32_t), ws.st));
-  RefineArgs r{};
-  r.rows = rs.rows.as<float>();
-  r.rows_rm = rs.f16 ? rs.rrm.as<float>() : nullptr;
-  r.row_labels = rs.labels.as<int64_t>();
-  r.queries = d_q;
-  r.ms = ws.ms.as<float>();
-  r.mk = ws.mk.as<int32_t>();
-  r.max_rsq = rs.rmax.as<uint32_t>();
-  // PYR_CERT_GLOBAL=1: bound row norms by the whole store's max only -- no per-list maxima, no
-  // triangle bound (A/B measurement of the refined certificate)
-  const char *cg = getenv("PYR_CERT_GLOBAL");
-  const bool global = cg && atoi(cg) != 0;
-  r.tri = !global;
-  if (list_rmax && mi && !global) {
-    r.list_rmax = list_rmax;
-    r.probes = mi->probes;
-    r.nprobe = mi->nprobe;
-  }
-  r.nq = nq;
-  r.k1 = k1;
-  r.k = k;
-  r.dim = dim;
-  r.c_err = filter_cerr(dim);
-  if (prec < 0) prec = filter_prec();
-  if (prec16(prec) && rs.f16) {
-    r.c_bf = filter_f16_cerr(dim, met, prec);
-    r.c_abs = filter_f16_abs(dim, met, rs.sx, prec);
-    r.q16 = 1;
-    if (resid_cents && list_rmax && list_rmax_r) {  // residual tiles: the certificate of refine_kernel
-      r.resid = 1;
-      r.cents = resid_cents;
-      r.list_rmax_r = list_rmax_r;
-      r.list_rmax = list_rmax;
-      r.probes = mi ? mi->probes : nullptr;  // FLAT: one center (list 0)
-      r.nprobe = mi ? mi->nprobe : 1;
-    }
-  } else {
-    r.c_bf = prec == FILTER_BF16X3 ? filter_bf16x3_cerr(dim, met) : 0.0;
-  }
-  if (cr) {
-    r.qcert = d_q;  // the unit queries the filter scored
-    r.tri = 0;      // the triangle bound reads skth as an L2 score
-    r.rows = cr->raw->rows.as<float>();
-    r.rows_rm = cr->raw->f16 ? cr->raw->rrm.as<float>() : nullptr;
-    r.row_labels = cr->raw->labels.as<int64_t>();
-    r.queries = cr->queries;
-    r.max_rsq = cr->raw->rmax.as<uint32_t>();
-    r.cosine = 1;
-    r.qnorm = cr->qnorm;
-    r.rnorm = cr->raw->norms.as<float>();
-    r.zflag = cr->zflag;
-  }
-  r.out_s = d_s;
-  r.out_l = d_l;
-  r.out_c = d_c;
-  r.fail_list = ws.fail.as<int32_t>();
-  r.fail_cnt = ws.fail_cnt.as<int32_t>();
-  {
-    PhaseTimer t(PH_REFINE, ws.st, nq * k1);
-    launch_refine(r, met, V, ws.st);
-  }
-  HIPCHK(hipGetLastError());
-  int32_t nf = 0;
-  HIPCHK(hipMemcpyAsync(&nf, ws.fail_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, ws.st));
-  HIPCHK(hipStreamSynchronize(ws.st));
-  return nf;
-}
 
 // re-run the listed queries through the exact scan and put their rows in place
 template <class F>
@@ -1060,26 +911,16 @@ struct FlatIndex : Index {
       search_cosine_stream(d_q, nq, k, k1, cutoff, d_s, d_l, d_c, ws);
       return;
     }
-    if (filter_enabled() && k <= KMAX_FAST && filter_supported(dim, metric, k1)) {
-      search_filter(d_q, nq, k, k1, cutoff, d_s, d_l, d_c, ws);
-      return;
-    }
-    if (unit && filter_enabled() && k <= KMAX_FAST && k1 > 0 && filter_supported(dim, L2, k1)) {
-      search_cosine(d_q, nq, k, k1, prm, cutoff, d_s, d_l, d_c, ws);
-      return;
-    }
-    search_exact(d_q, nq, k, cutoff, d_s, d_l, d_c, ws);
+    search_exact(d_q, nq, k, cutoff, d_s, d_l, d_c, ws);  // the one fallback: the reference's arithmetic
   }
 
   // FLAT on the stream scan (scan.hip, round 4): slots [0, cutoff) cut into chunks that play the IVF
   // path's lists (every query probes all of them, their centroid the store's center: mu for L2, 0 for IP),
   // so the sample, the emit scan, the merge and the certified refine (the *Unsafe form, V = 4) run as
   // for IVF_FLAT, and the exact re-run of certificate failures stays on the device: no host round trip.
-  // PYR_FLAT_STREAM=0: the round-3 filter (filter16.hip; measurement only)
+  // Anything else (k > 60, dims past 768, an L2 store without its centre) takes the exact scan.
   bool flat_stream_ok(int k, int k1, int64_t cutoff) const {
-    const char *e = getenv("PYR_FLAT_STREAM");
-    if (e && atoi(e) == 0) return false;
-    if (!filter_enabled() || !stream_r4() || stream_prec() != FILTER_F16X1 || !prec16(filter_prec())) return false;
+    if (!filter_enabled()) return false;
     if (metric != L2 && metric != IP) return false;
     if (!st.f16 || k > KMAX_FAST || k1 <= 0 || !scan_supported(dim, metric, k1)) return false;
     if (metric == L2 && !(st.resid && st.center16)) return false;
@@ -1340,161 +1181,6 @@ struct FlatIndex : Index {
     HIPCHK(hipGetLastError());
   }
 
-  // Cosine (:339-354): the unit index's exact L2 top-K2 (K2 = K1 - margin >= k, the same
-  // filter capacity k would use) of the unit queries, then the exact Cosine of those candidates, ranked
-  // and certified (filter.hip cos_rerank_kernel); failures re-run the exact scan
-  void search_cosine(const float *d_q, int64_t nq, int k, int k1, const pyr_search_params &prm, int64_t cutoff,
-                     float *d_s, int64_t *d_l, int32_t *d_c, Workspace &ws) {
-    // PYR_COS_EXTRA: candidates beyond the filter capacity k itself uses (measurement knob)
-    const char *ce = getenv("PYR_COS_EXTRA");
-    if (ce && atoi(ce) > 0) k1 = std::max(k1, filter_k1(k + atoi(ce)));
-    if (k1 <= 0) k1 = filter_k1(k);
-    const int kc = std::max(k, k1 - 4);
-    ws.qn.ensure(sizeof(float) * std::max<int64_t>(nq, 1));
-    launch_norms(d_q, nq, dim, 0, ws.qn.as<float>(), ws.st);  // VectorMath.ComputeNorm (:339)
-    ws.cq.ensure(sizeof(float) * nq * dim);
-    launch_unit_rows(d_q, nullptr, ws.qn.as<float>(), nq, dim, ws.cq.as<float>(), ws.st);
-    if (unit->centred_pass(cutoff, nq, k1)) {
-      // one certificate: the unit store's fp16 candidates re-scored with the reference Cosine on the raw
-      // rows, certified in cosine units (refine_kernel, cosine) -- no exact L2 pass in between
-      const CosRefine cr{&st, d_q, ws.qn.as<float>(), zflag.as<uint32_t>()};
-      int64_t nf;
-      {
-        std::shared_lock<std::shared_mutex> g(unit->mu);
-        nf = unit->filter_pass(ws.cq.as<float>(), nq, k, k1, cutoff, d_s, d_l, d_c, ws, &cr);
-      }
-      filter_fallback(ws, nf, d_q, dim, k, d_s, d_l, d_c,
-                      [&](const float *q2, int64_t n2, float *s2, int64_t *l2, int32_t *c2) {
-                        search_exact(q2, n2, k, cutoff, s2, l2, c2, ws.nested());
-                      });
-      return;
-    }
-    ws.ccs.ensure(sizeof(float) * nq * kc);
-    ws.ccl.ensure(sizeof(int64_t) * nq * kc);
-    ws.ccc.ensure(sizeof(int32_t) * nq);
-    {
-      std::shared_lock<std::shared_mutex> g(unit->mu);
-      unit->search(ws.cq.as<float>(), nq, kc, prm, ws.ccs.as<float>(), ws.ccl.as<int64_t>(), ws.ccc.as<int32_t>(), ws);
-    }
-    ws.fail.ensure(sizeof(int32_t) * nq);
-    ws.fail_cnt.ensure(sizeof(int32_t));
-    HIPCHK(hipMemsetAsync(ws.fail_cnt.p, 0, sizeof(int32_t), ws.st));
-    CosRerankArgs r{};
-    r.rows = st.rows.as<float>();
-    r.rows_rm = st.f16 ? st.rrm.as<float>() : nullptr;
-    r.rnorm = st.norms.as<float>();
-    r.row_labels = st.labels.as<int64_t>();
-    r.max_rsq = st.rmax.as<uint32_t>();
-    r.zflag = zflag.as<uint32_t>();
-    r.queries = d_q;
-    r.qnorm = ws.qn.as<float>();
-    r.cand_s = ws.ccs.as<float>();
-    r.cand_l = ws.ccl.as<int64_t>();
-    r.cand_c = ws.ccc.as<int32_t>();
-    r.kc = kc;
-    r.k = k;
-    r.dim = dim;
-    r.nq = nq;
-    r.out_s = d_s;
-    r.out_l = d_l;
-    r.out_c = d_c;
-    r.fail_list = ws.fail.as<int32_t>();
-    r.fail_cnt = ws.fail_cnt.as<int32_t>();
-    {
-      PhaseTimer t(PH_REFINE, ws.st, nq * kc);
-      launch_cos_rerank(r, ws.st);
-    }
-    HIPCHK(hipGetLastError());
-    int32_t nf = 0;
-    HIPCHK(hipMemcpyAsync(&nf, ws.fail_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, ws.st));
-    HIPCHK(hipStreamSynchronize(ws.st));
-    filter_fallback(ws, nf, d_q, dim, k, d_s, d_l, d_c,
-                    [&](const float *q2, int64_t n2, float *s2, int64_t *l2, int32_t *c2) {
-                      search_exact(q2, n2, k, cutoff, s2, l2, c2, ws.nested());
-                    });
-  }
-
-  // MFMA candidate filter over slots [0, cutoff), exact refine with the *Unsafe form (V = 4)
-  void search_filter(const float *d_q, int64_t nq, int k, int k1, int64_t cutoff, float *d_s, int64_t *d_l,
-                     int32_t *d_c, Workspace &ws) {
-    const int64_t nf = filter_pass(d_q, nq, k, k1, cutoff, d_s, d_l, d_c, ws, nullptr);
-    const int k1_next = filter_k1_next(k, k1);
-    filter_fallback(ws, nf, d_q, dim, k, d_s, d_l, d_c,
-                    [&](const float *q2, int64_t n2, float *s2, int64_t *l2, int32_t *c2) {
-                      Workspace &sw = ws.nested();  // K1 = 64 filter first, then the exact scan
-                      if (k1_next > 0) search_filter(q2, n2, k, k1_next, cutoff, s2, l2, c2, sw);
-                      else search_exact(q2, n2, k, cutoff, s2, l2, c2, sw);
-                    });
-  }
-
-  // whether filter_pass runs the fp16 filter on centred tiles (the Cosine certificate needs them)
-  bool centred_pass(int64_t cutoff, int64_t nq, int k1) const {
-    if (getenv("PYR_FLAT_WAVES")) return false;
-    const ScanPlan p = plan_flat(cutoff, nq, dim, k1, MAX_PARTS);
-    return st.resid && st.center16 && prec16(filter_prec_for(filter_prec(), st.f16, p.chunk_rows));
-  }
-
-  // the filter, the merge and the certified refine over slots [0, cutoff); returns the failures (ws.fail).
-  // cr: this is the unit store of a Cosine index (re-score with the reference Cosine, cosine certificate)
-  int64_t filter_pass(const float *d_q, int64_t nq, int k, int k1, int64_t cutoff, float *d_s, int64_t *d_l,
-                      int32_t *d_c, Workspace &ws, const CosRefine *cr) {
-    // 256-query items on 16-wave blocks (fp16 tiles, K1 = 16): each streamed tile serves twice the
-    // queries (PYR_FLAT_WAVES=16)
-    const char *fw = getenv("PYR_FLAT_WAVES");
-    int waves = 4;
-    ScanPlan p = plan_flat(cutoff, nq, dim, k1, MAX_PARTS);
-    if (fw && atoi(fw) == 16 && k1 == 16 && nq > 128) {
-      const ScanPlan p16 = plan_flat(cutoff, nq, dim, k1, MAX_PARTS, 256);
-      if (prec16(filter_prec_for(filter_prec(), st.f16, p16.chunk_rows))) {
-        p = p16;
-        waves = 16;
-      }
-    }
-    const size_t np = (size_t)nq * p.nchunks * k1;
-    ws.part_s.ensure(sizeof(float) * np);
-    ws.part_k.ensure(sizeof(uint32_t) * np);
-    uint32_t *gthr = shared_bounds(ws, nq);
-    ws.items.ensure(sizeof(ScanItem) * std::max(p.nitems, 1));
-    ws.nitems.ensure(sizeof(int32_t) * 4);
-    make_flat_items(ws.items.as<ScanItem>(), ws.nitems.as<int32_t>(), cutoff, p.chunk_rows, nq, 0, p.qchunk, ws.st);
-    FilterArgs fa{};
-    fa.rows = st.rows.as<float>();
-    fa.live = st.live.as<uint8_t>();
-    fa.rsq = st.rsq.as<float>();
-    fa.queries = d_q;
-    fa.items = ws.items.as<ScanItem>();
-    fa.n_items = ws.nitems.as<int32_t>();
-    fa.qlist = nullptr;
-    fa.nparts = p.nchunks;
-    fa.k1 = k1;
-    fa.dim = dim;
-    fa.key_base = 0;
-    fa.row_limit = (uint32_t)cutoff;
-    fa.part_s = ws.part_s.as<float>();
-    fa.part_k = ws.part_k.as<uint32_t>();
-    fa.gthr = gthr;
-    fa.ablate = filter_ablate();
-    fa.pub_mask = filter_pub_mask();
-    fa.prec = filter_prec_for(filter_prec(), st.f16, p.chunk_rows);
-    fa.waves = prec16(fa.prec) ? waves : 4;  // items of p.qchunk queries (plan_flat)
-    if (fa.waves == 16 && p.qchunk != 256) throw Error(PYR_E_STATE, "filter items / block size mismatch");
-    fa.xcd = getenv("PYR_FLAT_XCD") ? atoi(getenv("PYR_FLAT_XCD")) != 0 : 0;  // measurement knob
-    fa.h16 = st.h16.p;
-    fa.meta = st.meta.as<float>();
-    fa.sx = st.sx;
-    const bool centered = prec16(fa.prec) && st.resid;
-    fa.cents = centered ? st.center.as<float>() : nullptr;
-    {
-      PhaseTimer t(PH_FLAT_SCAN, ws.st, nq * cutoff);
-      if (prec16(fa.prec)) launch_filter16(fa, metric, p.nitems, ws.st);
-      else launch_filter(fa, metric, p.nitems, ws.st);
-    }
-    if (cr && !centered) throw Error(PYR_E_STATE, "Cosine unit store without centred fp16 tiles");
-    return filter_finish(ws, nq, p.nchunks, k1, k, dim, metric, exact_v, d_q, st, nullptr, d_s, d_l, d_c,
-                         centered ? st.rmax.as<uint32_t>() : nullptr, centered ? st.center.as<float>() : nullptr,
-                         centered ? st.rmax_r.as<uint32_t>() : nullptr, fa.prec, cr);
-  }
-
   // BruteForceVectorIndex.Search (:275-379) on the VALU, the reference's exact arithmetic
   void search_exact(const float *d_q, int64_t nq, int k, int64_t cutoff, float *d_s, int64_t *d_l, int32_t *d_c,
                     Workspace &ws) {
@@ -1664,11 +1350,6 @@ struct Coarse {
   RowStore cs;
   DevMem rm;  // row-major centroids
   std::vector<float> host;
-  // optionally (PYR_COARSE_FILTER=1) the centroids once more as a FLAT store (fp16 tiles): the coarse
-  // ranking as a FLAT search with k = nprobe -- MFMA filter, then the exact safe-form scores
-  // (ComputeScore) of K1 candidates and the certificate, failures re-run exactly; ids and order
-  // equal the dense exact ranking
-  std::unique_ptr<FlatIndex> flat;
   // the matrix-core ranking (coarse.hip launch_coarse_mfma): |c|^2 per centroid, max |c|, and whether
   // every centroid value is finite (otherwise the dense exact ranking runs)
   DevMem c2;
@@ -1710,28 +1391,6 @@ struct Coarse {
       HIPCHK(hipMemcpyAsync(c2.p, n2.data(), sizeof(float) * k, hipMemcpyHostToDevice, st));
       HIPCHK(hipStreamSynchronize(st));
     }
-    flat.reset();
-    if (filter_on() && met != COS && store16(dim, met)) {
-      pyr_index_desc d{};
-      d.kind = PYR_FLAT;
-      d.dim = dim;
-      d.metric = met;
-      HIPCHK(hipGetDevice(&d.device));
-      flat.reset(new FlatIndex(d));
-      flat->exact_v = 1;
-      std::vector<int64_t> ids((size_t)k);
-      for (int i = 0; i < k; ++i) ids[i] = i;
-      flat->add(host.data(), k, ids.data(), false);
-    }
-  }
-
-  // PYR_COARSE_FILTER=1 (read when the centroids are set): rank through the FLAT filter.  Same probes,
-  // but slower on the bench data (I1 coarse 2.4 vs 0.21 ms, M8 3.5 vs 1.65 ms: the coarse scores of
-  // uniform data are packed too tightly for the certificate at K1 = 64, so most queries re-run the
-  // exact scan); off by default (profiles/r2_wide/sweep_coarse_filter.log)
-  static bool filter_on() {
-    const char *e = getenv("PYR_COARSE_FILTER");
-    return e && atoi(e) != 0;
   }
 
   // score all centroids (ComputeScore, safe VectorMath), rank desc (ties by index), keep nprobe
@@ -1742,19 +1401,6 @@ struct Coarse {
       ws.probes.ensure(sizeof(int32_t) * nq * nprobe);
       HIPCHK(hipMemcpyAsync(ws.probes.p, ws.ext_probes, sizeof(int32_t) * nq * nprobe, hipMemcpyDeviceToDevice,
                             ws.st));
-      return;
-    }
-    const int k1 = filter_k1(nprobe);
-    if (flat && filter_enabled() && k1 > 0 && nprobe <= KMAX_FAST && nprobe <= nlist &&
-        filter_supported(cs.dim, met, k1)) {
-      // on the nested workspace (same stream): the caller may already hold partials and shared bounds
-      // in ws (the exact IVF search sets them up before ranking)
-      Workspace &cw = ws.nested();
-      cw.cpr_s.ensure(sizeof(float) * nq * nprobe);
-      cw.cpr_l.ensure(sizeof(int64_t) * nq * nprobe);
-      flat->search_filter(d_q, nq, nprobe, k1, nlist, cw.cpr_s.as<float>(), cw.cpr_l.as<int64_t>(), nullptr, cw);
-      ws.probes.ensure(sizeof(int32_t) * nq * nprobe);
-      launch_labels_to_i32(cw.cpr_l.as<int64_t>(), nq * nprobe, ws.probes.as<int32_t>(), ws.st);
       return;
     }
     // the matrix-core ranking (PYR_COARSE_MFMA=0: the dense exact ranking below; same probes)
@@ -2219,172 +1865,25 @@ struct IvfFlatIndex : Index {
       search_stream(d_q, nq, k, k1, probes, d_s, d_l, d_c, ws);
       return;
     }
-    // the round-2 MFMA filter (filter.hip): dims 32 / 64 / 128 with the stream scan switched off
-    if (fast && filter_supported(dim, metric, k1)) {
-      search_filter(d_q, nq, k, k1, probes, d_s, d_l, d_c, ws);
-      return;
-    }
     search_exact(d_q, nq, k, prm, d_s, d_l, d_c, ws);
   }
 
-  // the lists' fp16 residual tiles serve this search's stream scan: the round-4 kernels (scan.hip) at every
-  // tile dimension, the round-3 ones (stream16.hip; PYR_STREAM_MFMA=16 or two-term queries) at 32 / 64 / 128
+  // the lists' fp16 residual tiles serve this search's stream scan (scan.hip) at every tile dimension;
+  // anything else (k > 60, MaxScans, dims past 768, an unbuilt index) takes the exact scan
   bool stream_ok(int k1) const {
-    if (!stream_enabled() || !prec16(filter_prec()) || !lists.f16 || !lists.resid) return false;
+    if (!lists.f16 || !lists.resid) return false;
     const int met = metric == COS ? L2 : metric;
     if (metric == COS && lists.met16 != L2) return false;
-    const bool r4 = stream_prec() != FILTER_F16X2 && stream_r4();
-    return r4 ? scan_supported(dim, met, k1) : lists.tdim() == dim && stream16_supported(dim, met, k1);
+    return scan_supported(dim, met, k1);
   }
 
-  void search_filter(const float *d_q, int64_t nq, int k, int k1, int probes, float *d_s, int64_t *d_l, int32_t *d_c,
-                     Workspace &ws) {
-    if (stream_ok(k1)) {
-      search_stream(d_q, nq, k, k1, probes, d_s, d_l, d_c, ws);
-      return;
-    }
-    prep_queries(d_q, nq, dim, metric, ws);
-    {
-      PhaseTimer t(PH_COARSE, ws.st, nq * coarse.nlist);
-      coarse.probe(d_q, nullptr, nq, probes, metric, ws);  // exact coarse ranking (ComputeScore, :186-198)
-    }
-    IvfChunking ch = ivf_chunking(max_len, probes, 0, nq, k1, bounds_enabled());
-    const bool seed = ivf_seed_enabled() && bounds_enabled() && probes > 1;
-    if (seed) ch.warm = 0;
-    const int nparts = probes * ch.cmax;
-    const size_t np = (size_t)nq * nparts * k1;
-    ws.part_s.ensure(sizeof(float) * np);
-    ws.part_k.ensure(sizeof(uint32_t) * np);
-    uint32_t *gthr = shared_bounds(ws, nq);
-    const int prec_used = filter_prec_for(filter_prec(), lists.f16, std::max(ch.chunk, ch.warm));
-    const int waves = filter_waves_ivf(k1, prec_used);
-    const int qc = filter_qchunk(prec_used, waves);
-    int maxi, maxi_main = 0;
-    {
-      PhaseTimer t(PH_ITEMS, ws.st);
-      if (seed) {
-        maxi = build_ivf_items_range(ws, 0, nq, probes, 0, 1, nparts, coarse.nlist, dlb, dle, qc, ch);
-        maxi_main = build_ivf_items_range(ws, 1, nq, probes, 1, probes, nparts, coarse.nlist, dlb, dle, qc, ch);
-      } else {
-        maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qc, ch, 0);
-        if (ch.warm > 0) maxi_main = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qc, ch, 1);
-      }
-    }
-    FilterArgs fa{};
-    fa.rows = lists.rows.as<float>();
-    fa.live = lists.live.as<uint8_t>();
-    fa.rsq = lists.rsq.as<float>();
-    fa.queries = d_q;
-    fa.items = ws.items.as<ScanItem>();
-    fa.n_items = ws.nitems.as<int32_t>();
-    fa.qlist = ws.qlist.as<int32_t>();
-    fa.nparts = nparts;
-    fa.k1 = k1;
-    fa.dim = dim;
-    fa.key_base = 0;
-    fa.row_limit = 0xFFFFFFFFu;
-    fa.part_s = ws.part_s.as<float>();
-    fa.part_k = ws.part_k.as<uint32_t>();
-    fa.gthr = gthr;
-    fa.ablate = filter_ablate();
-    fa.pub_mask = filter_pub_mask();
-    fa.prec = prec_used;
-    fa.waves = waves;
-    fa.xcd = filter_xcd();
-    fa.single = getenv("PYR_FILTER_SB") ? atoi(getenv("PYR_FILTER_SB")) != 0 : 0;
-    // 2: a wave with survivors appends at raised priority (I1 list scan -1.5 %, profiles/r2_wide/)
-    fa.prio = getenv("PYR_F16_PRIO") ? atoi(getenv("PYR_F16_PRIO")) : 2;
-    fa.h16 = lists.h16.p;
-    fa.meta = lists.meta.as<float>();
-    fa.sx = lists.sx;
-    fa.cents = lists.resid ? coarse.rm.as<float>() : nullptr;
-    const bool use16 = prec16(fa.prec);
-    DevMem dbg;
-    const int dbg_mode = getenv("PYR_FILTER_DEBUG") ? atoi(getenv("PYR_FILTER_DEBUG")) : 0;
-    if (dbg_mode) {  // measurement only: 1 insert statistics, 2 filter16 cycle buckets, to stderr
-      dbg.ensure(128);
-      HIPCHK(hipMemsetAsync(dbg.p, 0, 128, ws.st));
-      if (dbg_mode == 2) fa.tdbg = reinterpret_cast<unsigned long long *>(dbg.p) + 8;
-      else fa.dbg = dbg.as<uint32_t>();
-    }
-    {
-      PhaseTimer t(PH_LIST_SCAN, ws.st, prof().on ? probed_rows(ws, nq, probes, le, lb) : 0);
-      auto launch = [&](int mi) {
-        if (use16) launch_filter16(fa, metric, mi, ws.st);
-        else launch_filter(fa, metric, mi, ws.st);
-      };
-      launch(maxi);
-      if (seed || ch.warm > 0) {
-        fa.items = ws.items3.as<ScanItem>();
-        fa.n_items = ws.nitems3.as<int32_t>();
-        if (seed) fa.qlist = ws.qlist2.as<int32_t>();
-        launch(maxi_main);
-      }
-    }
-    if (fa.dbg) {
-      uint32_t h[4] = {0, 0, 0, 0};
-      HIPCHK(hipMemcpyAsync(h, dbg.p, 16, hipMemcpyDeviceToHost, ws.st));
-      HIPCHK(hipStreamSynchronize(ws.st));
-      fprintf(stderr, "[filter] %s %u, candidates %u, %s %u\n", use16 ? "survivor wave-tiles" : "wave insert-loop iterations",
-              h[0], h[1], use16 ? "owner drains" : "owner stages", h[2]);
-      if (use16) fprintf(stderr, "[filter] shared-bound refreshes that raised a threshold %u\n", h[3]);
-    }
-    if (fa.tdbg) {
-      unsigned long long c[8];
-      HIPCHK(hipMemcpyAsync(c, fa.tdbg, sizeof(c), hipMemcpyDeviceToHost, ws.st));
-      HIPCHK(hipStreamSynchronize(ws.st));
-      const double tot = (double)c[5];
-      fprintf(stderr,
-              "[filter16 cycles] total %.3g (wave-cycles), wait %.1f%%, refresh %.1f%%, compute %.1f%%, append %.1f%%, "
-              "drain %.1f%%, prologue %.1f%%; active wave-tiles %llu, compute cycles per wave-tile %.0f\n",
-              tot, 100 * c[0] / tot, 100 * c[1] / tot, 100 * c[2] / tot, 100 * c[3] / tot, 100 * c[4] / tot,
-              100 * c[6] / tot, c[7], c[7] ? (double)c[2] / c[7] : 0.0);
-    }
-    MergeIvf mi;
-    mi.probes = ws.probes.as<int32_t>();
-    mi.lb = dlb.as<int32_t>();
-    mi.le = dle.as<int32_t>();
-    mi.nprobe = probes;
-    mi.ch = ch;
-    const int64_t nf = filter_finish(ws, nq, nparts, k1, k, dim, metric, 1, d_q, lists, &mi, d_s, d_l, d_c,
-                                     dlmax.as<uint32_t>(), use16 && lists.resid ? coarse.rm.as<float>() : nullptr,
-                                     dlmax_r.as<uint32_t>(), fa.prec);
-    // The exact re-run scans the failing queries' OWN probe lists: ws.probes holds the batch's
-    // ranking (computed above or handed in by the caller, pyr_index_search_probed_device), so its
-    // rows are gathered in fail-list order and passed as caller-ranked lists.  (Re-ranking is
-    // only equivalent when this index ranked them itself; caller lists may differ.)
-    // Failures are re-run on their own buffers (ws.nested()): first by the filter with K1 = 64
-    // candidates (a 64-deep margin certifies almost every query the K1 = 16 list could not), what
-    // still fails by the exact scan.  PYR_FILTER_TIER=0 sends failures straight to the exact scan.
-    pyr_search_params ex{probes, 0, -1};
-    const int k1_next = filter_k1_next(k, k1);
-    filter_fallback(ws, nf, d_q, dim, k, d_s, d_l, d_c,
-                    [&](const float *q2, int64_t n2, float *s2, int64_t *l2, int32_t *c2) {
-                      Workspace &sw = ws.nested();
-                      sw.fprobes.ensure(sizeof(int32_t) * n2 * probes);
-                      launch_gather_rows_i32(ws.probes.as<int32_t>(), ws.fail.as<int32_t>(), n2, probes,
-                                             sw.fprobes.as<int32_t>(), ws.st);
-                      sw.ext_probes = sw.fprobes.as<int32_t>();
-                      sw.ext_nprobe = probes;
-                      try {
-                        if (k1_next > 0) search_filter(q2, n2, k, k1_next, probes, s2, l2, c2, sw);
-                        else search_exact(q2, n2, k, ex, s2, l2, c2, sw);
-                      } catch (...) {
-                        sw.ext_probes = nullptr;
-                        throw;
-                      }
-                      sw.ext_probes = nullptr;
-                    });
-  }
-
-  // IvfFlatVectorIndex.Search (:147-231) as stream-and-emit (stream16.hip): the coarse ranking, then per
+  // IvfFlatVectorIndex.Search (:147-231) as stream-and-emit (scan.hip): the coarse ranking, then per
   // (list chunk, <= 512 queries) item every row whose approximate score reaches the query's sampled
   // threshold T_q is emitted; the best 64 per query are re-scored exactly and certified (depth K1, then
   // depth 64 for the failures); what still fails is re-run by the exact scan.  Query batches are
   // sliced so that the candidate regions stay within 16 GiB.
   void search_stream(const float *d_q, int64_t nq, int k, int k1, int probes, float *d_s, int64_t *d_l, int32_t *d_c,
                      Workspace &ws) {
-    const bool q2 = stream_prec() == FILTER_F16X2;
     const int cap = stream_cap();
     int64_t chunk = stream_chunk();
     IvfChunking ch{(int32_t)chunk, 1, 0};
@@ -2404,7 +1903,7 @@ struct IvfFlatIndex : Index {
       const int32_t *ext = ws.ext_probes;
       if (ext) ws.ext_probes = ext + a0 * ws.ext_nprobe;
       try {
-        stream_slice(d_q + a0 * dim, n, k, k1, probes, ch, nparts, cap, q2, d_s + a0 * k, d_l + a0 * k,
+        stream_slice(d_q + a0 * dim, n, k, k1, probes, ch, nparts, cap, d_s + a0 * k, d_l + a0 * k,
                      d_c ? d_c + a0 : nullptr, ws);
       } catch (...) {
         ws.ext_probes = ext;
@@ -2459,7 +1958,7 @@ struct IvfFlatIndex : Index {
   }
 
   void stream_slice(const float *d_q, int64_t nq, int k, int k1, int probes, IvfChunking ch, int nparts, int cap,
-                    bool q2, float *d_s, int64_t *d_l, int32_t *d_c, Workspace &ws) {
+                    float *d_s, int64_t *d_l, int32_t *d_c, Workspace &ws) {
     const bool cosine = metric == COS;
     const int met = cosine ? L2 : metric;  // Cosine: L2 over the unit vectors (commit_lists)
     if (cosine) {
@@ -2477,18 +1976,16 @@ struct IvfFlatIndex : Index {
       launch_unit_rows(d_q, nullptr, ws.qn.as<float>(), nq, dim, ws.cq.as<float>(), ws.st);
       d_qs = ws.cq.as<float>();
     }
-    const bool r4 = !q2 && stream_r4();
-    const int qmax = r4 ? scan_qmax(lists.tdim()) : stream16_qmax(q2);
+    const int qmax = scan_qmax(lists.tdim());
     int maxi;
     {
       PhaseTimer t(PH_ITEMS, ws.st);
       maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qmax, ch, 0, true);
     }
     const int64_t npos = nq * probes;
-    const int sv = stream16_sample_values();
+    const int sv = scan_sample_values();
     const size_t nslot = (size_t)nq * nparts;
     ws.sbq.ensure(sizeof(uint16_t) * std::max<int64_t>(npos, 1) * lists.tdim());
-    if (q2) ws.sbql.ensure(sizeof(uint16_t) * std::max<int64_t>(npos, 1) * lists.tdim());
     ws.sqsc.ensure(sizeof(float2) * std::max<int64_t>(npos, 1));
     ws.ssamp.ensure(sizeof(float) * std::max<int64_t>(npos, 1) * sv);
     ws.sthr.ensure(sizeof(float) * nq);
@@ -2515,7 +2012,6 @@ struct IvfFlatIndex : Index {
     sa.dim = dim;
     sa.dt = lists.tdim();
     sa.bq = ws.sbq.as<_Float16>();
-    sa.bql = q2 ? ws.sbql.as<_Float16>() : nullptr;
     sa.qsc = ws.sqsc.as<float2>();
     sa.samp = ws.ssamp.as<float>();
     sa.thr = ws.sthr.as<float>();
@@ -2529,7 +2025,7 @@ struct IvfFlatIndex : Index {
     sa.row_limit = 0xFFFFFFFFu;
     sa.ablate = filter_ablate();
     sa.thr_bias = getenv("PYR_STREAM_THR_BIAS") ? (float)atof(getenv("PYR_STREAM_THR_BIAS")) : 0.0f;
-    const int prec = q2 ? FILTER_F16X2 : FILTER_F16X1;
+    const int prec = FILTER_F16X1;
     sa.rsq16 = lists.rsq16.as<float>();
     sa.rsq = lists.rsq.as<float>();
     const int dt = lists.tdim();  // the scan's error terms at the tile dimension (FlatIndex::stream_slice)
@@ -2543,12 +2039,7 @@ struct IvfFlatIndex : Index {
     }
     {
       PhaseTimer t(PH_SAMPLE, ws.st);
-      if (r4) {
-        stream_sample(sa, met, maxi, ws.st);
-      } else {
-        launch_stream_prep(sa, met, maxi, ws.st);
-        launch_stream_scan(sa, met, maxi, true, ws.st);
-      }
+      stream_sample(sa, met, maxi, ws.st);
       StreamSelectArgs sel{};
       sel.samp = ws.ssamp.as<float>();
       sel.nq = nq;
@@ -2565,8 +2056,7 @@ struct IvfFlatIndex : Index {
     {
       PhaseTimer t(PH_LIST_SCAN, ws.st, prof().on ? probed_rows(ws, nq, probes, le, lb) : 0);
       if (timing) sa.tdbg = ws.tdbg.as<unsigned long long>();
-      if (r4) launch_scan_main(sa, met, maxi, ws.st);
-      else launch_stream_scan(sa, met, maxi, false, ws.st);
+      launch_scan_main(sa, met, maxi, ws.st);
       sa.tdbg = nullptr;
     }
     if (timing) {

@@ -1,27 +1,17 @@
-// filter.hip -- MFMA candidate filter + exact refine for the FLAT / IVF-Flat scans (gfx950).
+// filter.hip -- the certified exact refine of the stream scan's candidates (gfx950), plus the small
+// kernels around it (unit rows, query gathers, row norms, per-list norm maxima).
 //
-// The reference's scores are fixed fp32 operation sequences (VectorMath.cs): sub, mul,
-// add per element, 8-lane Vector accumulators and a horizontal tree.  Those can only be
-// reproduced on the VALU (3 instructions per element, kernels.hip scan_fast).  This file
-// gets the same answers at matrix-core rate:
+// The reference's scores are fixed fp32 operation sequences (VectorMath.cs): sub, mul, add per element,
+// 8-lane Vector accumulators and a horizontal tree.  The stream scan (scan.hip) ranks rows by fp16
+// matrix-core scores with a per-row error bound; refine_kernel takes each query's best 64 of those,
+// re-scores them with the reference's exact arithmetic (the same restatement as the exact scan and the
+// oracle), ranks them by (score desc, key asc), and certifies the top-k: every row it did not see scored
+// at most s~_K1 + E, so if the k-th exact score beats that no excluded row can enter the top-k and the
+// result equals the exact scan's.  Queries whose certificate fails are listed and re-run exactly on
+// the device (kernels.hip ivf_rerun_*).
 //
-//   1. mfma_filter: for every (query, row) pair of a work item an APPROXIMATE score from
-//      fp32 MFMA (v_mfma_f32_32x32x2_f32): L2 -> 2 q.x - |x|^2 (the per-query constant
-//      -|q|^2 is added later), IP -> q.x.  Each (query, slot) keeps its top-K1 (K1 = k +
-//      margin) by approximate score, with the same shared per-query bound machinery as
-//      the exact scan (ScanArgs::gthr).
-//   2. the partial lists are merged (merge_keys_kernel) into each query's top-K1 by
-//      approximate score; s~_K1 = the K1-th approximate score.
-//   3. refine_kernel: exact reference scores of the K1 candidates (the same restatement
-//      as the exact scan and the oracle), top-k by (score desc, key asc), and a
-//      certificate: every row outside the candidate set has approximate score <= s~_K1,
-//      and |approx - reference| <= E(q) for every row (fp32 error bounds, see
-//      refine_kernel), so if the k-th exact candidate score is > s~_K1 + E no excluded
-//      row can be in the top-k and the result equals the exact scan's.  Queries whose
-//      certificate fails are listed and re-run through the exact scan by the engine.
-//
-// So the returned ids and scores stay bit-identical to the CPU restatement; only the
-// work per pair moves from 3 VALU instructions per dimension to fp32 MFMA.
+// (Rounds 1-3 also kept an fp32 / bf16x3 MFMA filter here and an fp16 tile filter in filter16.hip;
+// the stream scan superseded both and round 4 removed them.)
 #pragma clang fp contract(off)
 
 #include <hip/hip_runtime.h>
@@ -35,403 +25,12 @@
 namespace pyr {
 namespace {
 
-typedef float f16v __attribute__((ext_vector_type(16)));
-typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
-
 __device__ __forceinline__ bool better(float s1, uint32_t k1, float s2, uint32_t k2) {
   return s1 > s2 || (s1 == s2 && k1 < k2);
 }
 
 __device__ __forceinline__ size_t blk_off(int64_t r, int d, int D) {
   return ((size_t)(r >> 3) * (size_t)D + (size_t)d) * 8 + (size_t)(r & 7);
-}
-
-constexpr int RT = 32;       // rows per stage (one 32x32 MFMA tile per wave)
-constexpr int SCR = RT + 4;  // score-transpose row stride (floats)
-constexpr int CB = 16;       // candidate buffer entries per owner
-constexpr int CBS = CB + 1;  // buffer stride (odd: the owners' appends hit distinct banks)
-
-// LDS layout of mfma_filter.  fp32 mode: [2 buffers][RT][RSTR] floats.  bf16x3 mode:
-// [2 buffers][hi, lo][RT][BSTR] bf16 (BSTR = D + 8: the 16-byte row pad makes the
-// ds_read_b128 B fragments conflict-free); then the score transpose [4][32][SCR] and the
-// owners' candidate buffers (scores [128][CB], keys [128][CB]).
-template <int D, bool BF, int NW = 4>
-struct FilterLds {
-  static constexpr int RSTR = D + 4;      // padded row stride: conflict-free ds_read_b128 / ds_write_b32
-  static constexpr int BSTR = D + 8;      // bf16 row stride
-  static constexpr int TILE = BF ? RT * BSTR : RT * RSTR;  // floats per fp32 tile / bf16 per hi or lo tile
-  static constexpr size_t tiles_bytes() { return BF ? sizeof(uint16_t) * 4 * TILE : sizeof(float) * 2 * TILE; }
-  static constexpr size_t bytes() { return tiles_bytes() + sizeof(float) * NW * 32 * SCR + 8 * NW * 32 * CBS; }
-};
-
-// ---------------------------------------------------------------------------
-// mfma_filter: one work item (ScanItem) = up to 128 queries x a row range.  Wave w owns
-// queries 32w..32w+31 of the item; its A operand (the queries) stays in registers for the
-// whole item: lane l holds query (l & 31), dims [(l >> 5) * D/2, (l >> 5) * D/2 + D/2).
-// Rows stream HBM -> registers -> LDS (row-major, padded) 32 at a time, double buffered.
-// Per stage each wave runs D/2 MFMAs of 32x32x2 (C[query][row] += 2 dims per step; the
-// two lane halves split the dimension range), then moves its C tile through a
-// wave-private LDS transpose so that lane i (< 32) sees query i's 32 row scores, filters
-// them against the query's K1-th best / shared bound and inserts survivors into the
-// query's LDS list.
-// ---------------------------------------------------------------------------
-// Insert (v, key) into a register-resident sorted (desc) list of compile-time length KR:
-// a branch-free compare-and-shift network (no LDS round trips; the owner lanes of a wave
-// run it together whenever any of them has a candidate, so it must be cheap).
-template <int KR>
-__device__ __forceinline__ void reg_insert(float (&s)[KR], uint32_t (&kk)[KR], float v, uint32_t key) {
-  bool b[KR];
-#pragma unroll
-  for (int j = 0; j < KR; ++j) b[j] = better(v, key, s[j], kk[j]);  // monotone: false..false true..true
-#pragma unroll
-  for (int j = KR - 1; j >= 1; --j) {
-    s[j] = b[j - 1] ? s[j - 1] : (b[j] ? v : s[j]);
-    kk[j] = b[j - 1] ? kk[j - 1] : (b[j] ? key : kk[j]);
-  }
-  s[0] = b[0] ? v : s[0];
-  kk[0] = b[0] ? key : kk[0];
-}
-
-// BF = bf16x3 mode: q.x as qh.xh + qh.xl + ql.xh on v_mfma_f32_32x32x16_bf16, where
-// q = qh + ql (+ |eps| <= 2^-16 |q|) is the two-term bf16 split of each fp32 value (x
-// likewise, split once per block while staging rows into LDS).  Relative error per
-// product <= 3.1 * 2^-16 plus fp32 accumulation over 3D terms; refine_kernel's c_bf term
-// covers it, so the certified results stay exact.  5.3x the fp32 MFMA rate.
-// NW = waves per block (32 queries each): 4 (two blocks per CU) or 8 (one block per CU,
-// every staged row tile serves 256 queries: half the HBM / L2 row traffic of NW = 4).
-template <int D, int MET, bool IVF, int KR, bool BF, int NW>
-__global__ __launch_bounds__(64 * NW, 8 / NW) void mfma_filter(FilterArgs a) {
-  using L = FilterLds<D, BF, NW>;
-  constexpr int NT = 64 * NW;  // threads per block
-  static_assert(NW == 4 || (BF && NW == 8), "8-wave blocks only in bf16x3 mode");
-  constexpr int KH = D / 2;  // fp32 k-steps: lanes 0-31 take dims [0, KH), lanes 32-63 [KH, D)
-  constexpr int KS = D / 16;  // bf16 k-steps: lane half h takes dims 16s + 8h .. +7 of step s
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  // XCD-major item mapping (a.xcd; grid a multiple of 8): block b runs on XCD b % 8, so
-  // giving each XCD a contiguous run of items puts a list chunk's query groups (adjacent
-  // items) on one XCD at about the same time -- the later groups read the rows from its L2
-  int item = blockIdx.x;
-  if (a.xcd) {
-    const int per = (*a.n_items + 7) >> 3;
-    item = ((int)blockIdx.x & 7) * per + ((int)blockIdx.x >> 3);
-    if ((int)(blockIdx.x >> 3) >= per) return;
-  }
-  if (item >= *a.n_items) return;
-  const ScanItem it = a.items[item];
-  float *rt = smem;                                          // fp32: [2][RT][RSTR]
-  uint16_t *bt = reinterpret_cast<uint16_t *>(smem);         // bf16: [2][hi, lo][RT][BSTR]
-  // a.single (bf16x3): one row-tile buffer (two barriers per stage) so that three blocks fit a CU
-  const bool single = BF && a.single;
-  float *scw = smem + (single ? L::tiles_bytes() / 2 : L::tiles_bytes()) / sizeof(float);  // [NW][32][SCR]
-
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const int i32 = lane & 31, h = lane >> 5;
-  float *sc = scw + w * 32 * SCR;
-
-  // A operand, bf16x3 mode: query 32w + i32, split into hi / lo fragments per k-step
-  bf8v qh[BF ? KS : 1], ql[BF ? KS : 1];
-  if constexpr (BF) {
-    const int i = 32 * w + i32;
-    const int qi = i < it.qcnt ? (IVF ? a.qlist[it.qbeg + i] / a.nparts : it.qbeg + i) : -1;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      float v[8];
-      if (qi >= 0) {
-        const float4 *qp = reinterpret_cast<const float4 *>(a.queries + (size_t)qi * D + 16 * s + 8 * h);
-        const float4 v0 = qp[0], v1 = qp[1];
-        v[0] = v0.x; v[1] = v0.y; v[2] = v0.z; v[3] = v0.w;
-        v[4] = v1.x; v[5] = v1.y; v[6] = v1.z; v[7] = v1.w;
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = 0.0f;
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        qh[s][j] = (__bf16)v[j];
-        ql[s][j] = (__bf16)(v[j] - (float)qh[s][j]);
-      }
-    }
-  }
-  // A operand, fp32 mode: query 32w + i32 of the item, dims h*KH .. h*KH + KH - 1
-  float qa[BF ? 1 : KH];
-  if constexpr (!BF) {
-    const int i = 32 * w + i32;
-    if (i < it.qcnt) {
-      const int qi = IVF ? a.qlist[it.qbeg + i] / a.nparts : it.qbeg + i;
-      const float4 *qp = reinterpret_cast<const float4 *>(a.queries + (size_t)qi * D + h * KH);
-#pragma unroll
-      for (int p = 0; p < KH / 4; ++p) {
-        const float4 v = qp[p];
-        qa[4 * p] = v.x;
-        qa[4 * p + 1] = v.y;
-        qa[4 * p + 2] = v.z;
-        qa[4 * p + 3] = v.w;
-      }
-    } else {
-#pragma unroll
-      for (int s = 0; s < KH; ++s) qa[s] = 0.0f;
-    }
-  }
-  const bool wave_active = 32 * w < it.qcnt;
-
-  // owners: lane i32 of wave w (lower half) owns query 32w + i32
-  const int oq = 32 * w + i32;
-  const bool owner = h == 0 && oq < it.qcnt;
-  int oslot = 0, qown = 0;
-  float gs = -INFINITY;
-  uint32_t published = 0;
-  if (owner) {
-    oslot = IVF ? a.qlist[it.qbeg + oq] + it.part : (it.qbeg + oq) * a.nparts + it.part;
-    qown = IVF ? a.qlist[it.qbeg + oq] / a.nparts : it.qbeg + oq;
-    if (a.gthr) gs = key_score(__hip_atomic_load(a.gthr + qown, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  }
-  // this owner's candidate buffer (scores, keys) in LDS, nbuf entries
-  float *bs = scw + NW * 32 * SCR + (w * 32 + i32) * CBS;
-  uint32_t *bk = reinterpret_cast<uint32_t *>(scw + NW * 32 * SCR + NW * 32 * CBS) + (w * 32 + i32) * CBS;
-  int nbuf = 0;
-  float ts[KR];  // this owner's top-KR by approximate score, sorted desc; (-inf, NONE) = empty
-  uint32_t tk[KR];
-#pragma unroll
-  for (int j = 0; j < KR; ++j) {
-    ts[j] = -INFINITY;
-    tk[j] = KEY_NONE;
-  }
-
-  // stage staging: RT rows of the blocked store = RT/8 groups of [D][8]; float4 v of a
-  // group holds rows (v&1)*4 .. +3 at dim v>>1 (kernels.hip blk_off)
-  const int r0 = it.row_begin;  // multiple of 8
-  const int nst = (it.row_end - r0 + RT - 1) / RT;
-  constexpr int NV = RT * D / 4;  // float4 per stage
-  constexpr int LOADS = BF ? 1 : NV / NT;
-  static_assert(BF || NV % NT == 0, "stage must split evenly over the block");
-  // bf16x3 staging works on float4 pairs (dims 2p, 2p+1 of the same 4 rows: float4 v and
-  // v + 2 of a group) so each row's two bf16 halves are written as one 32-bit word
-  constexpr int NP = NV / 2;                   // float4 pairs per stage
-  constexpr int PL = BF ? (NP + NT - 1) / NT : 1;  // pairs per thread
-  const float4 *src = reinterpret_cast<const float4 *>(a.rows);
-  const int gmax = ((it.row_end + 7) >> 3) - 1;  // last group with rows of this item
-  float4 pf[LOADS];
-  float4 pa[PL], pb[PL];
-  auto load_stage = [&](int stg) {
-    if constexpr (BF) {
-#pragma unroll
-      for (int i = 0; i < PL; ++i) {
-        const int pr = tid + NT * i;
-        if (NP % NT == 0 || pr < NP) {
-          const int gl = pr / D, pp = pr % D;
-          const int v0 = 4 * (pp >> 1) + (pp & 1);
-          const int g = min((r0 >> 3) + stg * (RT / 8) + gl, gmax);  // clamp: rows past the end unused
-          pa[i] = src[(size_t)g * (2 * D) + v0];
-          pb[i] = src[(size_t)g * (2 * D) + v0 + 2];
-        }
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < LOADS; ++i) {
-        const int v = tid + NT * i;
-        const int g = min((r0 >> 3) + stg * (RT / 8) + v / (2 * D), gmax);  // clamp: rows past the end unused
-        pf[i] = src[(size_t)g * (2 * D) + v % (2 * D)];
-      }
-    }
-  };
-  auto split2 = [](float x0, float x1, uint32_t &hi, uint32_t &lo) {
-    const __bf16 h0 = (__bf16)x0, h1 = (__bf16)x1;
-    const __bf16 l0 = (__bf16)(x0 - (float)h0), l1 = (__bf16)(x1 - (float)h1);
-    hi = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
-    lo = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
-  };
-  auto store_stage = [&](int buf) {
-    if constexpr (BF) {
-#pragma unroll
-      for (int i = 0; i < PL; ++i) {
-        const int pr = tid + NT * i;
-        if (NP % NT == 0 || pr < NP) {
-          const int gl = pr / D, pp = pr % D;
-          const int row = gl * 8 + (pp & 1) * 4;
-          uint32_t *dh = reinterpret_cast<uint32_t *>(bt + (2 * buf) * L::TILE + row * L::BSTR + 2 * (pp >> 1));
-          uint32_t *dl = dh + L::TILE / 2;
-          constexpr int W = L::BSTR / 2;  // row stride in 32-bit words
-          uint32_t hi, lo;
-          split2(pa[i].x, pb[i].x, hi, lo);
-          dh[0] = hi;
-          dl[0] = lo;
-          split2(pa[i].y, pb[i].y, hi, lo);
-          dh[W] = hi;
-          dl[W] = lo;
-          split2(pa[i].z, pb[i].z, hi, lo);
-          dh[2 * W] = hi;
-          dl[2 * W] = lo;
-          split2(pa[i].w, pb[i].w, hi, lo);
-          dh[3 * W] = hi;
-          dl[3 * W] = lo;
-        }
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < LOADS; ++i) {
-        const int v = tid + NT * i;
-        const int gl = v / (2 * D), vv = v % (2 * D);
-        float *dst = rt + buf * L::TILE + (gl * 8 + (vv & 1) * 4) * L::RSTR + (vv >> 1);
-        dst[0] = pf[i].x;
-        dst[L::RSTR] = pf[i].y;
-        dst[2 * L::RSTR] = pf[i].z;
-        dst[3 * L::RSTR] = pf[i].w;
-      }
-    }
-  };
-
-  // this lane's C column (a row) per stage: visibility and |x|^2 are loaded one stage
-  // ahead, with that stage's rows, so the stage that uses them never waits on a load
-  // (vmcnt is in order: a load issued behind the row prefetch would drain it)
-  uint8_t lv_next = 0;
-  float xsq_next = 0.0f;
-  auto load_meta = [&](int stg) {
-    const int rc = min(r0 + stg * RT + i32, it.row_end - 1);
-    lv_next = a.live[rc];
-    if (MET == L2) xsq_next = a.rsq[rc];
-  };
-  if (nst > 0) {
-    load_meta(0);
-    load_stage(0);
-    store_stage(0);
-  }
-  __syncthreads();
-
-  for (int st = 0; st < nst; ++st) {
-    const int cur = single ? 0 : st & 1;
-    const int row = r0 + st * RT + i32;
-    const bool rvalid = row < it.row_end && (uint32_t)row < a.row_limit && lv_next;
-    const float xsq = xsq_next;
-    if (st + 1 < nst) {
-      load_meta(st + 1);
-      if (!(a.ablate & 4)) load_stage(st + 1);
-    }
-    if (wave_active && !(a.ablate & 8)) {
-      f16v acc;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-      if constexpr (BF) {
-        const uint16_t *bh = bt + (2 * cur) * L::TILE + i32 * L::BSTR + 8 * h;
-        const uint16_t *bl = bh + L::TILE;
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          const bf8v xh = *reinterpret_cast<const bf8v *>(bh + 16 * s);
-          const bf8v xl = *reinterpret_cast<const bf8v *>(bl + 16 * s);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ql[s], xh, acc, 0, 0, 0);  // small terms first
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh[s], xl, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh[s], xh, acc, 0, 0, 0);
-        }
-      } else {
-        const float *bp = rt + cur * L::TILE + i32 * L::RSTR + h * KH;
-#pragma unroll
-        for (int s4 = 0; s4 < KH / 4; ++s4) {
-          const float4 b = *reinterpret_cast<const float4 *>(bp + 4 * s4);
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qa[4 * s4 + 0], b.x, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qa[4 * s4 + 1], b.y, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qa[4 * s4 + 2], b.z, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(qa[4 * s4 + 3], b.w, acc, 0, 0, 0);
-        }
-      }
-      // C[i][j]: lane column j = i32 (row), register r -> query (r&3) + 8(r>>2) + 4h
-      if (!(a.ablate & 2)) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int qi = (r & 3) + 8 * (r >> 2) + 4 * h;
-          const float s = MET == L2 ? 2.0f * acc[r] - xsq : acc[r];
-          sc[qi * SCR + i32] = rvalid ? s : -INFINITY;
-        }
-      } else if (acc[0] == 12345.0f) {
-        sc[i32] = acc[1];  // keep the MFMAs alive in the ablated build
-      }
-    }
-    if (!single && st + 1 < nst && !(a.ablate & 4)) store_stage(cur ^ 1);
-    __syncthreads();  // next tile staged (single: every wave done with this tile); score transpose visible
-    if (single && st + 1 < nst && !(a.ablate & 4)) store_stage(0);
-
-    // pre-filter against the owner's bound (the full (score, key) test follows): lane half
-    // h tests rows 16h .. 16h + 15 of query i32, the owner joins the two masks
-    const float lo = __shfl(fmaxf(gs, ts[KR - 1]), i32);
-    uint32_t hmask = 0;
-    if (oq < it.qcnt && !(a.ablate & 1)) {
-      const float *sch = sc + i32 * SCR + (RT / 2) * h;
-#pragma unroll
-      for (int j = 0; j < RT / 2; ++j) {
-        const float v = sch[j];
-        if (v > -INFINITY && v >= lo) hmask |= 1u << j;
-      }
-    }
-    const uint32_t upper = __shfl(hmask, i32 + 32);
-    if (owner && !(a.ablate & 1)) {
-      const float *scp = sc + i32 * SCR;
-      const int rb = r0 + st * RT;
-      uint32_t pass = hmask | (upper << (RT / 2));
-      if (a.ablate & 16) {  // measurement: filter without inserting
-        if (pass == 0x12345u) ts[0] = lo;
-        pass = 0;
-      }
-      if (a.dbg) {  // measurement only
-        const uint32_t np = __popc(pass);
-        atomicAdd(a.dbg + 1, np);
-        atomicAdd(a.dbg + 2, 1u);
-        uint32_t mx = np;
-        for (int o = 16; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 32));
-        if (i32 == 0) atomicAdd(a.dbg, mx);
-      }
-      // Survivors go to the owner's LDS buffer (cheap appends); the register list is
-      // updated only when some owner's buffer would overflow (then every owner of the wave
-      // drains its buffer and inserts this stage directly).  The 32 owners run the insert
-      // network in lockstep, so draining CB buffered candidates at once costs max-over-owners
-      // of the buffered counts instead of a sum over stages of per-stage maxima.
-      const bool direct = (a.ablate & 32) || __any(nbuf + __popc(pass) > CB);
-      if (direct) {
-        for (int i = 0; i < nbuf; ++i) {
-          const float v = bs[i];
-          const uint32_t key = bk[i];
-          if (better(v, key, ts[KR - 1], tk[KR - 1])) reg_insert<KR>(ts, tk, v, key);
-        }
-        nbuf = 0;
-        while (pass) {
-          const int j = __builtin_ctz(pass);
-          pass &= pass - 1;
-          const float v = scp[j];
-          const uint32_t key = a.key_base | (uint32_t)(rb + j);
-          if (better(v, key, ts[KR - 1], tk[KR - 1])) reg_insert<KR>(ts, tk, v, key);
-        }
-      } else {
-        while (pass) {
-          const int j = __builtin_ctz(pass);
-          pass &= pass - 1;
-          bs[nbuf] = scp[j];
-          bk[nbuf] = a.key_base | (uint32_t)(rb + j);
-          ++nbuf;
-        }
-      }
-      if (a.gthr && (st & a.pub_mask) == a.pub_mask) {  // publish this list's KR-th best, refresh the bound
-        if (tk[KR - 1] != KEY_NONE && score_key(ts[KR - 1]) > published) {
-          published = score_key(ts[KR - 1]);
-          atomicMax(a.gthr + qown, published);
-        }
-        gs = fmaxf(gs, key_score(__hip_atomic_load(a.gthr + qown, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
-      }
-    }
-    if (single) __syncthreads();  // the next tile is staged
-  }
-  if (owner) {
-    for (int i = 0; i < nbuf; ++i) {  // drain the candidate buffer
-      const float v = bs[i];
-      const uint32_t key = bk[i];
-      if (better(v, key, ts[KR - 1], tk[KR - 1])) reg_insert<KR>(ts, tk, v, key);
-    }
-    if (a.gthr && tk[KR - 1] != KEY_NONE && score_key(ts[KR - 1]) > published)
-      atomicMax(a.gthr + qown, score_key(ts[KR - 1]));
-    float *ps = a.part_s + (size_t)oslot * KR;
-    uint32_t *pk = a.part_k + (size_t)oslot * KR;
-#pragma unroll
-    for (int j = 0; j < KR; ++j) {
-      ps[j] = ts[j];
-      pk[j] = tk[j];
-    }
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -760,90 +359,6 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
   }
 }
 
-// ---- Cosine on the filter path (BruteForceVectorIndex.cs:354) ----
-// The candidates come from an exact L2 search of the unit queries q^ = q * (1 / |q|) over the unit rows
-// x^ (an L2 FLAT index over the same slots, its labels = the slots; its fp16 tiles are centred on the
-// unit rows' mean, so the filter's error is relative to the residuals).  On unit vectors the L2 order
-// is the cosine order: 1 - |q^ - x^|^2 / 2 = q^.x^.  Its scores s_j = -L2SquaredUnsafe(q^, x^) are
-// exact, so p_j = 1 + s_j / 2 <= p_K2 for every row left out.  With cos_j the real-arithmetic cosine
-// and u = 2^-24:
-//   ComputeNorm (VectorMath.cs:72-99) sums non-negative squares in 8 lanes of D/8 terms, a 3-level
-//   tree and a scalar tail: relative error <= (D/8 + 8) u, so the norm's <= (D/16 + 5) u, and a unit
-//   component x_i * fl(1 / |x|) is within e = (D/16 + 7) u of x_i / |x|;
-//   |q^|^2, |x^|^2 are within 2e of 1 and q^.x^ within 2e of cos_j, so 1 - |q^ - x^|^2 / 2 is within
-//   4e of cos_j; L2SquaredUnsafe adds non-negative terms (4 x 8 lanes, trees, tails): relative error
-//   <= (D/8 + 18) u of a distance <= 4.1, i.e. (D/4 + 37) u in p;  |p_j - cos_j| <= (D/2 + 66) u;
-//   the reference Cosine dot / (|q| |x|) (DotProductUnsafe, within (D/8 + 16) u sum |q_i x_i|) is
-//   within (D/4 + 28) u of cos_j.
-// A row left out therefore has a reference score <= p_K2 + (3D/4 + 94) u, and the exact top-k of the
-// candidates is the search's when the k-th exact score exceeds p_K2 + E, E = (2D + 256) u.  A row with
-// a norm below 1e-6 scores 0 (VectorMath.cs:105) but sits at unit distance (x^ = 0): once the store has
-// held such a row (zflag) the k-th score must also exceed 0.  A query with a zero or non-finite norm,
-// or a store holding a non-finite row, fails the certificate.
-template <int DT>
-__global__ __launch_bounds__(256) void cos_rerank_kernel(CosRerankArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (q >= a.nq) return;
-  const int D = DT > 0 ? DT : a.dim, kc = a.kc, k = a.k;
-  const float *qp = a.queries + (size_t)q * D;
-  const float qn = a.qnorm[q];
-  const int ccount = a.cand_c[q];
-  uint32_t key = KEY_NONE;
-  if (lane < kc && lane < ccount && a.cand_l[(size_t)q * kc + lane] >= 0) key = (uint32_t)a.cand_l[(size_t)q * kc + lane];
-  float s = -INFINITY;
-  for (int p = 0; 8 * p < kc; ++p) {
-    const int c = 8 * p + (lane >> 3);
-    const int32_t kk = __shfl((int)key, c);
-    const int64_t rk = kk >= 0 ? (int64_t)kk : 0;
-    const float dot = a.rows_rm ? exact_score_l8<4, IP, DT, true>(qp, a.rows_rm, rk, D, lane & 7)
-                                : exact_score_l8<4, IP, DT, false>(qp, a.rows, rk, D, lane & 7);
-    const float xn = a.rnorm[rk];
-    const float sc = (qn < 1e-6f || xn < 1e-6f) ? 0.0f : dot / (qn * xn);
-    const float t = __shfl(sc, 8 * (lane & 7));
-    if ((lane >> 3) == p && key != KEY_NONE) s = t;
-  }
-  int rank = 0, valid = 0;
-  for (int c = 0; c < kc; ++c) {
-    const float sc = __shfl(s, c);
-    const uint32_t kk = __shfl(key, c);
-    if (kk == KEY_NONE) continue;
-    ++valid;
-    if (key != KEY_NONE && better(sc, kk, s, key)) ++rank;
-  }
-  const int nout = min(valid, k);
-  if (key != KEY_NONE && rank < k) {
-    a.out_s[(size_t)q * k + rank] = s;
-    a.out_l[(size_t)q * k + rank] = a.row_labels[key];
-  }
-  if (lane >= nout && lane < k) {
-    a.out_s[(size_t)q * k + lane] = -INFINITY;
-    a.out_l[(size_t)q * k + lane] = -1;
-  }
-  bool ok = true;
-  if (ccount >= kc) {  // rows were left out: the margin against the K2-th inner product
-    float skth = -INFINITY;
-    for (int c = 0; c < kc; ++c) {
-      const int rc = __shfl(rank, c);
-      const uint32_t kk = __shfl(key, c);
-      const float sc = __shfl(s, c);
-      if (kk != KEY_NONE && rc == k - 1) skth = sc;
-    }
-    const double u = 5.9604644775390625e-8;  // 2^-24
-    const double pk = 1.0 + 0.5 * (double)a.cand_s[(size_t)q * kc + kc - 1];
-    ok = nout == k && (double)skth > pk + (2.0 * D + 256.0) * u;
-    if (a.zflag && *a.zflag != 0u && !(skth > 0.0f)) ok = false;
-  }
-  if (!(qn >= 1e-6f) || !isfinite(qn) || (a.max_rsq && a.max_rsq[1] != 0u)) ok = false;
-  if (lane == 0) {
-    if (a.out_c) a.out_c[q] = nout;
-    if (!ok) a.fail_list[atomicAdd(a.fail_cnt, 1)] = (int32_t)q;
-  }
-}
-
-// unit vectors: out row i = x_i * (1 / n_i), or 0 when n_i < 1e-6 (the reference's zero-norm rule) or
-// n_i is not finite.  blocked: rows of a blocked store at slots[i] (norms indexed by slot), else
-// row-major x with norms[i].
 __global__ void unit_rows_kernel(const float *x, const int64_t *slots, const float *norms, int64_t n, int D,
                                  float *out, uint32_t *zflag, const uint8_t *live) {
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * D;
@@ -922,71 +437,7 @@ __global__ __launch_bounds__(256) void list_rmax_kernel(const float *rsq, const 
 
 inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
-template <int D, int MET, bool IVF, int KR, bool BF, int NW>
-void launch_filter_p(const FilterArgs &a, int max_items, hipStream_t st) {
-  static std::atomic<uint64_t> attr{0};
-  allow_max_lds(reinterpret_cast<const void *>(&mfma_filter<D, MET, IVF, KR, BF, NW>), attr);
-  const size_t lds = FilterLds<D, BF, NW>::bytes() - (BF && a.single ? FilterLds<D, BF, NW>::tiles_bytes() / 2 : 0);
-  const int grid = a.xcd ? (max_items + 7) / 8 * 8 : max_items;
-  hipLaunchKernelGGL((mfma_filter<D, MET, IVF, KR, BF, NW>), dim3(grid), dim3(64 * NW), lds, st, a);
-}
-
-template <int D, int MET, bool IVF, int KR>
-void launch_filter_t(const FilterArgs &a, int max_items, hipStream_t st) {
-  if (a.prec == FILTER_BF16X3) {
-    if (a.waves == 8) launch_filter_p<D, MET, IVF, KR, true, 8>(a, max_items, st);
-    else launch_filter_p<D, MET, IVF, KR, true, 4>(a, max_items, st);
-  } else {
-    launch_filter_p<D, MET, IVF, KR, false, 4>(a, max_items, st);
-  }
-}
-
-template <int D, int MET, bool IVF>
-void launch_filter_k(const FilterArgs &a, int max_items, hipStream_t st) {
-  if (a.k1 == 16) launch_filter_t<D, MET, IVF, 16>(a, max_items, st);
-  else if (a.k1 == 32) launch_filter_t<D, MET, IVF, 32>(a, max_items, st);
-  else launch_filter_t<D, MET, IVF, 64>(a, max_items, st);
-}
-
-template <int D>
-void launch_filter_d(const FilterArgs &a, int metric, int max_items, hipStream_t st) {
-  const bool ivf = a.qlist != nullptr;
-  if (metric == L2) {
-    if (ivf) launch_filter_k<D, L2, true>(a, max_items, st);
-    else launch_filter_k<D, L2, false>(a, max_items, st);
-  } else {
-    if (ivf) launch_filter_k<D, IP, true>(a, max_items, st);
-    else launch_filter_k<D, IP, false>(a, max_items, st);
-  }
-}
-
 }  // namespace
-
-bool filter_supported(int dim, int metric, int k1) {
-  if (metric != L2 && metric != IP) return false;
-  if (dim != 32 && dim != 64 && dim != 128) return false;
-  return k1 == 16 || k1 == 32 || k1 == 64;  // register list capacities (mfma_filter KR)
-}
-
-void launch_filter(const FilterArgs &a, int metric, int max_items, hipStream_t st) {
-  if (max_items <= 0) return;
-  switch (a.dim) {
-    case 32: launch_filter_d<32>(a, metric, max_items, st); return;
-    case 64: launch_filter_d<64>(a, metric, max_items, st); return;
-    default: launch_filter_d<128>(a, metric, max_items, st); return;
-  }
-}
-
-void launch_cos_rerank(const CosRerankArgs &a, hipStream_t st) {
-  if (a.nq <= 0) return;
-  const dim3 g(nblk(a.nq, 4)), b(256);
-  switch (a.dim) {
-    case 32: hipLaunchKernelGGL(cos_rerank_kernel<32>, g, b, 0, st, a); return;
-    case 64: hipLaunchKernelGGL(cos_rerank_kernel<64>, g, b, 0, st, a); return;
-    case 128: hipLaunchKernelGGL(cos_rerank_kernel<128>, g, b, 0, st, a); return;
-    default: hipLaunchKernelGGL(cos_rerank_kernel<0>, g, b, 0, st, a); return;
-  }
-}
 
 void launch_unit_rows(const float *x, const int64_t *slots, const float *norms, int64_t n, int32_t dim, float *out,
                       hipStream_t st, uint32_t *zflag, const uint8_t *live) {

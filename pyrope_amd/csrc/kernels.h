@@ -292,61 +292,12 @@ void launch_sq8_dequantize(const uint8_t *codes, int64_t n, int32_t dim, const f
                            float *out, hipStream_t st);
 void launch_sq8_scan(const Sq8Args &a, int metric, int max_items, hipStream_t st);
 
-// ---- MFMA candidate filter + exact refine (filter.hip) ----
-struct FilterArgs {
-  const float *rows;       // blocked [row/8][D][8]
-  const uint8_t *live;     // per row
-  const float *rsq;        // per row |x|^2 (L2)
-  const float *queries;    // row-major nq x D
-  const ScanItem *items;
-  const int32_t *n_items;
-  const int32_t *qlist;    // IVF partial-slot ids, or null (FLAT items)
-  int32_t nparts, k1, dim;
-  uint32_t key_base;
-  uint32_t row_limit;      // rows >= row_limit are not scanned (FLAT MaxScans cutoff)
-  float *part_s;           // [slot][k1] approximate scores
-  uint32_t *part_k;        // [slot][k1] keys
-  uint32_t *gthr;          // shared per-query bound in approximate-score space, or null
-  int32_t ablate;          // measurement only (PYR_FILTER_ABLATE; results are wrong when set):
-                           // 1 skip the owner filter, 2 skip the score transpose, 4 skip row loads, 8 skip MFMA,
-                           // 16 filter without inserting, 32 insert directly (no candidate buffer)
-  int32_t pub_mask;        // publish / refresh the shared bound when (stage & pub_mask) == pub_mask
-  uint32_t *dbg;           // measurement only (PYR_FILTER_DEBUG): [0] insert-loop iterations of
-                           // all waves, [1] candidates inserted, [2] owner stages, or null
-  int32_t prec;            // FILTER_FP32 or FILTER_BF16X3 (approximate-score arithmetic)
-  int32_t waves;           // waves per block = items' queries / 32: 4, or 8 (bf16x3 only)
-  int32_t xcd;             // 1: XCD-major item -> block mapping
-  int32_t single;          // 1: single-buffered row tiles (bf16x3; smaller LDS, 2 barriers per stage)
-  // fp16 tile filter (filter16.hip, prec FILTER_F16X2 / FILTER_F16X1)
-  const void *h16;         // fp16 row tiles of the store (RowStore::h16)
-  const float *meta;       // per row: L2 -|x|^2, IP 0, -inf dead / padding (RowStore::meta)
-  float sx;                // the store's power-of-two fp16 scale
-  const float *cents;      // IVF residual tiles: list centroids (row-major), item.list selects; null = raw rows
-  int32_t prio;              // filter16w: 1 = s_setprio 1 for waves 4-7 (PYR_F16_PRIO, measurement knob)
-  unsigned long long *tdbg;  // measurement only (PYR_FILTER_DEBUG=2, filter16): per-wave cycle buckets
-                             // [wait, refresh, compute, append, drain, total, prologue, wave-tiles]
-};
-constexpr int FILTER_FP32 = 0;    // v_mfma_f32_32x32x2_f32
-constexpr int FILTER_BF16X3 = 1;  // hi/lo bf16 split, 3 x v_mfma_f32_32x32x16_bf16
-constexpr int FILTER_F16X2 = 2;   // fp16 row tiles x two-term fp16 queries, 2 x v_mfma_f32_32x32x16_f16
-constexpr int FILTER_F16X1 = 3;   // fp16 row tiles x one-term fp16 queries, 1 MFMA per k-step
-// queries per filter work item (items must be built with this qchunk)
-inline int filter_qchunk(int prec, int waves) {
-  return (prec == FILTER_BF16X3 && waves == 8) || ((prec == FILTER_F16X2 || prec == FILTER_F16X1) && waves == 16)
-             ? 256
-             : 128;
-}
-// refine_kernel error-bound constant of the bf16x3 approximation (per u |q| max|x|)
-inline double filter_bf16x3_cerr(int dim, int metric) {
-  // q.x: <= 3.02 * 2^-16 per product from the splits, <= 2u per addition over 3D terms;
-  // doubled for L2 (approx = 2 q.x - ...)
-  const double c = 6.3 * dim + 800.0;
-  return metric == 0 ? 2.0 * c : c;
-}
-// refine_kernel constants of the fp16 tile filter: relative c_bf (per u |q| max|x|) and the absolute
-// term (per |q|) from fp16 subnormals of the rows, 2^-25 sqrt(D) / sx; doubled for L2.  x's fp16
-// rounding is 2^-11 = 8192 u relative; the two-term query split 2^-22 = 4 u; fp32 accumulation of
-// 2D exact products <= 2D u; one-term queries add q's own 2^-11.
+// ---- fp16 tiles (tiles16.hip) + the certified exact refine (filter.hip) ----
+constexpr int FILTER_F16X1 = 3;   // the stream scan's arithmetic: fp16 row tiles x one-term fp16 queries
+// refine_kernel constants of the fp16 tiles: relative c_bf (per u |q| max|x|) and the absolute term
+// (per |q|) from fp16 subnormals of the rows, 2^-25 sqrt(D) / sx; doubled for L2.  x's fp16 rounding is
+// 2^-11 = 8192 u relative; 4 u of slack (rounds 1-3's two-term query split); fp32 accumulation of 2D
+// exact products <= 2D u; the one-term queries add q's own 2^-11 (+ 64).
 inline double filter_f16_cerr(int dim, int metric, int prec) {
   const double c = 8192.0 + 4.0 + 2.0 * dim + 64.0 + (prec == FILTER_F16X1 ? 8192.0 + 64.0 : 0.0);
   return metric == 0 ? 2.0 * c : c;
@@ -358,7 +309,7 @@ inline double filter_f16_abs(int dim, int metric, float sx, int prec) {
   (void)prec;
   return metric == 0 ? 2.0 * a : a;
 }
-// ---- IVF list scan as stream-and-emit (stream16.hip) ----
+// ---- the IVF / FLAT list scan as stream-and-emit (scan.hip; sample and merge: sample16.hip) ----
 constexpr int STREAM_KO = 64;  // merged candidates per query (the deep certificate's K1)
 struct StreamArgs {
   const void *h16;            // fp16 residual tiles of the lists (RowStore::h16)
@@ -371,9 +322,9 @@ struct StreamArgs {
   const int32_t *qlist;       // per (list, query) position: q * nparts + probe * cmax
   int32_t nparts, nprobe, cmax, dim;
   int32_t dt;                 // tile dimension D (scan_tile_dim; 0: dim): tiles and bq rows; queries / cents keep dim
-  _Float16 *bq, *bql;         // [pos][D] scaled query residuals: one fp16 term (+ the low term, or null)
+  _Float16 *bq;               // [pos][D] scaled query residuals (one fp16 term)
   float2 *qsc;                // [pos] {f, cq}
-  float *samp;                // [q * nprobe + probe][stream16_sample_values()] sampled scores
+  float *samp;                // [q * nprobe + probe][scan_sample_values()] sampled scores
   const float *thr;           // [q] T_q (score space), or null
   float *cand_s;              // [q * nparts + part][cap] emitted scores
   uint32_t *cand_k;           // keys
@@ -390,14 +341,14 @@ struct StreamArgs {
   const float *rsq16;         // per row |x - c|^2
   const float *rsq;           // per row |x|^2 (IP)
   float kr, kx, kq, kqa, kqc;
-  const float *mub;           // per row meta + E_row (RowStore::row_terms; stream32_kernel)
+  const float *mub;           // per row meta + E_row (RowStore::row_terms)
   unsigned long long *tdbg;   // measurement only (PYR_STREAM_TIMING=1): per-wave cycle buckets, or null
 };
-// per row the stream scan's additive term: meta + kr |x - c|^2 (+ kx |x|^2, IP), in the fp32 order the
-// 16x16x32 kernel evaluates it in (fmaf(kr, rsq16, meta), then fmaf(kx, rsq, .))
+// per row the stream scan's additive term: meta + kr |x - c|^2 (+ kx |x|^2, IP): fmaf(kr, rsq16, meta),
+// then fmaf(kx, rsq, .)
 void launch_row_terms(const float *meta, const float *rsq16, const float *rsq, int64_t n, int metric, float kr,
                       float kx, float *out, hipStream_t st);
-// The per-row / per-pair split of the fp16 residual filter's error bound (refine_kernel's resid branch,
+// The per-row / per-pair split of the fp16 residual tiles' error bound (refine_kernel's resid branch,
 // filter.hip): products A X go to (A^2 + X^2) / 2, (A + X)^2 to 2 (A^2 + X^2), so the bound of a row
 // no longer depends on its list's largest residual; the reference's own sum deviation (g) is folded in.
 void stream_ub_terms(int dim, int metric, double c_bf, double c_err, double c_abs, StreamArgs &a);
@@ -446,10 +397,10 @@ struct CandMergeArgs {
   float *out_s;               // [nq][STREAM_KO] desc; floor placeholders key -2, none -1
   int32_t *out_k;
 };
-bool stream16_supported(int dim, int metric, int k1);
 int device_cus();                   // compute units of the current device (persistent-grid launches)
-// round 4 (scan.hip): the fused query-operand + sample launch (replaces launch_stream_prep and the
-// sampling launch_stream_scan), and the 32x32x16 list scan; scan_sample_values() == stream16_sample_values()
+// scan.hip: the one-wave-per-32-queries sample (query operands + sample values, any tile dimension) and
+// the 32x32x16 list scan; sample16.hip: sprep + the 8-wave sample of tile dims 32 / 64 / 128 (same
+// outputs: bq, qsc, samp with scan_sample_values() values per (query, probe))
 int scan_sample_values();
 // tile dimension of the stream scan for a row dimension: dims <= 128 rounded up to 32, then 256 / 512 / 768
 // (tiles and query operands zero-padded; the fp32 rows and the exact refine keep dim); 0 = none
@@ -464,10 +415,8 @@ void launch_chunk_lists(int32_t *lb, int32_t *le, int nch, int64_t crow, int64_t
 void launch_iota_rows(int32_t *out, int64_t rows, int cols, hipStream_t st);
 void launch_scan_sample(const StreamArgs &a, int metric, int max_items, hipStream_t st);
 void launch_scan_main(const StreamArgs &a, int metric, int max_items, hipStream_t st);
-int stream16_qmax(bool q2);          // queries per work item
-int stream16_sample_values();        // sample values per (query, probe)
-void launch_stream_prep(const StreamArgs &a, int metric, int max_items, hipStream_t st);
-void launch_stream_scan(const StreamArgs &a, int metric, int max_items, bool sample, hipStream_t st);
+bool sample16_supported(int dim, int metric);  // dim == tile dim in {32, 64, 128}, L2 / IP
+void launch_sample16(const StreamArgs &a, int metric, int max_items, hipStream_t st);
 // T_q per query: the R-th largest of its n sample values, R from the sampled fraction f of its probed
 // rows: R = clamp(ceil(et f), rmin, rmax) (rmin == rmax: fixed)
 struct StreamSelectArgs {
@@ -523,39 +472,11 @@ struct RefineArgs {
   int32_t *fail_list;       // queries whose certificate failed
   int32_t *fail_cnt;
 };
-// Cosine on the filter path (filter.hip cos_rerank_kernel): candidates = the exact L2 top-kc of the unit
-// queries over the unit rows (cand_l: slots, cand_s: their scores -|q^ - x^|^2 desc, cand_c: count);
-// exact Cosine (BruteForceVectorIndex.cs:354) of each, top-k, certificate -> fail_list
-struct CosRerankArgs {
-  const float *rows;        // blocked store (the slots index it)
-  const float *rows_rm;     // its row-major copy, or null
-  const float *rnorm;       // ComputeNorm per slot
-  const int64_t *row_labels;
-  const uint32_t *max_rsq;  // the store's rmax pair ([1] != 0: a non-finite row), or null
-  const uint32_t *zflag;    // != 0 once a row with a norm below 1e-6 was written, or null
-  const float *queries;     // raw queries, row-major nq x D
-  const float *qnorm;       // ComputeNorm per query
-  const float *cand_s;
-  const int64_t *cand_l;
-  const int32_t *cand_c;
-  int32_t kc, k, dim;
-  int64_t nq;
-  float *out_s;
-  int64_t *out_l;
-  int32_t *out_c;
-  int32_t *fail_list;
-  int32_t *fail_cnt;
-};
-void launch_cos_rerank(const CosRerankArgs &a, hipStream_t st);
 // unit rows (x / n, 0 when n < 1e-6 or not finite): blocked rows at slots (norms by slot), or row-major
 // x (norms[i]) when slots is null; out row-major n x dim; zflag (may be null) set to 1 by a zero row that
 // is live (live: per row index, null = every row)
 void launch_unit_rows(const float *x, const int64_t *slots, const float *norms, int64_t n, int32_t dim, float *out,
                       hipStream_t st, uint32_t *zflag = nullptr, const uint8_t *live = nullptr);
-bool filter_supported(int dim, int metric, int k1);
-int filter16_max_rows();  // rows per scan item the fp16 filter accepts
-bool filter16_supported(int dim, int metric, int k1);
-void launch_filter16(const FilterArgs &a, int metric, int max_items, hipStream_t st);
 // fp16 tiles of blocked fp32 rows (slots[i], or rows [0, n)), scaled by sx; with cents (row-major)
 // and tile_list (list of each 32-row tile) the residuals x - c[list] (IVF lists)
 // rn (may be null): the rows' meta norms; a non-finite one zeroes the row's tile (encode16_kernel)
@@ -572,7 +493,6 @@ void launch_meta16(const int64_t *slots, int64_t n, int32_t metric, const float 
 // atomicMax of the float bits of max |x_i| (finite) over the rows into *out
 void launch_absmax(const float *rows, const int64_t *slots, int64_t n, int32_t dim, uint32_t *out, hipStream_t st,
                    const float *cents = nullptr, const int32_t *tile_list = nullptr);
-void launch_filter(const FilterArgs &a, int metric, int max_items, hipStream_t st);
 // V: 1 = VectorMath safe form (IVF), 4 = *Unsafe form (FLAT)
 void launch_refine(const RefineArgs &a, int metric, int V, hipStream_t st);
 void launch_gather_queries(const float *q, const int32_t *qidx, int64_t n, int32_t dim, float *out, hipStream_t st);

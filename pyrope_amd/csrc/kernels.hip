@@ -1388,22 +1388,13 @@ void launch_fast_i(const ScanArgs &a, int max_items, hipStream_t st) {
   hipLaunchKernelGGL((scan_fast<D, V, MET, GPS, IVF, QS, W>), dim3(max_items), dim3(8 * QCHUNK / QS), lds, st, a);
 }
 
-// Register-tile variant of the fast scan (PYR_SCANVAR overrides for A/B measurement):
-//   0: QS=4, 256 threads (~140 VGPRs, 3 waves/SIMD)
-//   1: QS=2, 512 threads (~98 VGPRs, 4 waves/SIMD)
-//   2: QS=2, 512 threads, register cap for 6 waves/SIMD (80 VGPRs, small spill)
-int scan_variant(int V) {
-  if (const char *e = getenv("PYR_SCANVAR")) return std::min(2, std::max(0, atoi(e)));
-  return V == 1 ? 2 : 1;
-}
-
+// Register-tile variant of the fast scan: QS = 2 (512 threads); the safe form (V = 1) with a register
+// cap for 6 waves per SIMD (80 VGPRs, a small spill), the *Unsafe form (V = 4) at 4 waves (~98 VGPRs).
+// (Round 2 also measured QS = 4 / 256 threads: slower at both.)
 template <int D, int V, int MET, int GPS, bool IVF>
 void launch_fast_var(const ScanArgs &a, int max_items, hipStream_t st) {
-  switch (scan_variant(V)) {
-    case 0: launch_fast_i<D, V, MET, GPS, IVF, 4, 1>(a, max_items, st); return;
-    case 1: launch_fast_i<D, V, MET, GPS, IVF, 2, 1>(a, max_items, st); return;
-    default: launch_fast_i<D, V, MET, GPS, IVF, 2, 6>(a, max_items, st); return;
-  }
+  if constexpr (V == 1) launch_fast_i<D, V, MET, GPS, IVF, 2, 6>(a, max_items, st);
+  else launch_fast_i<D, V, MET, GPS, IVF, 2, 1>(a, max_items, st);
 }
 
 template <int D, int V, int MET>

@@ -77,10 +77,10 @@ def test_incremental_rebuild_recompiles_only_the_touched_source(tmp_path):
     log = tmp_path / "calls.log"
     _run_builders(pkg, fake, log, 1)
     n0 = len(log.read_text().split("\n")[:-1])
-    src = pkg / "csrc" / "stream16.hip"
+    src = pkg / "csrc" / "sample16.hip"
     t = os.path.getmtime(pkg / "libpyrope_hip.so") + 1
     os.utime(src, (t, t))
     time.sleep(1.2)  # the rebuilt objects and library are newer than the touched source
     _run_builders(pkg, fake, log, 2)
     new = log.read_text().split("\n")[:-1][n0:]
-    assert len(new) == 2 and new[0] == "compile stream16.o.tmp.o" and new[1].startswith("link "), new
+    assert len(new) == 2 and new[0] == "compile sample16.o.tmp.o" and new[1].startswith("link "), new

@@ -195,17 +195,3 @@ def test_ivf_cosine_signed_zero_rows_deletes(hiplib, oracle):
     _ivf_oracle_check(idx, x, q, 10, 6, oracle, step=11)
 
 
-def test_cosine_two_stage_path_bf16x3(hiplib, oracle):
-    """When the unit store's pass would not run on centred fp16 tiles (bf16x3: PYR_FILTER_PREC=1, or items
-    over 65,536 rows) the unit store's exact L2 top-K2 is re-ranked by cos_rerank_kernel instead."""
-    from pyrope_amd import generate_synthetic
-    x = generate_synthetic(20000, 128, 42)
-    q = generate_synthetic(200, 128, 1337)
-    idx = _cos_index(128, x)
-    with _env(PYR_FILTER_PREC=1):
-        got, nfb = _check(idx, q, 10)
-    print(f"\n[cos] two-stage bf16x3: exact re-runs {nfb}/{len(q)}")
-    for i in range(0, len(q), 29):
-        os_, ok = oracle.bf_search(x, None, COS, q[i], 10)
-        np.testing.assert_array_equal(got[1][i], ok)
-        assert np.array_equal(got[0][i].view(np.uint32), os_.view(np.uint32))
