@@ -392,8 +392,8 @@ static uint32_t *shared_bounds(Workspace &ws, int64_t nq) {
   return ws.gthr.as<uint32_t>();
 }
 
-// IVF-PQ list scan kernel: 2 = pq_adc4 (default), 1 = pq_adc, 0 = the first-cut pq_scan
-// (PYR_PQ_ADC; A/B only, same results); unsupported shapes step down
+// IVF-PQ LUT list scan kernel: 2 = pq_adc4 (default), 0 = the first-cut pq_scan (PYR_PQ_ADC=0; A/B
+// only, same results; also what k > 64 or an unsupported shape takes)
 static int pq_adc_mode() {
   const char *e = getenv("PYR_PQ_ADC");
   return e ? atoi(e) : 2;
@@ -446,10 +446,11 @@ static void stream_rank(int k1, int32_t &rmin, int32_t &rmax, double &et) {
   rmax = std::max(rmin, k1);
   et = (ev ? atof(ev) : 6.0) * k1;
 }
-// candidate region per (query, part) (PYR_STREAM_CAP) and rows per list chunk (PYR_STREAM_CHUNK)
+// candidate buffer per query (PYR_STREAM_CAP; a query emits ~6 K1 rows, 96 at I1: a full buffer only
+// raises its floor, and the certificate decides) and rows per list chunk (PYR_STREAM_CHUNK)
 static int stream_cap() {
   const char *e = getenv("PYR_STREAM_CAP");
-  return e ? std::max(8, atoi(e)) : 256;
+  return e ? std::max(8, atoi(e)) : 2048;
 }
 static int64_t stream_chunk() {
   const char *e = getenv("PYR_STREAM_CHUNK");
@@ -469,7 +470,7 @@ void ivf_memory_plan(int dim, int64_t nrows, int nlist, int64_t max_len, int64_t
   if (index_bytes) *index_bytes = slots * per_row + cent;
   if (!workspace_bytes) return;
   const int probes = std::max(0, std::min(nprobe, nlist));
-  // search_stream: chunking and the 16 GiB slice of candidate regions
+  // search_stream: chunking and the 16 GiB slice of candidate buffers
   const int cap = stream_cap();
   IvfChunking ch{(int32_t)stream_chunk(), 1, 0};
   ch.cmax = ivf_list_chunks((int)max_len, ch);
@@ -479,7 +480,7 @@ void ivf_memory_plan(int dim, int64_t nrows, int nlist, int64_t max_len, int64_t
     ch.cmax = ivf_list_chunks((int)max_len, ch);
   }
   const int64_t nparts = (int64_t)probes * ch.cmax;
-  const int64_t per_q = std::max<int64_t>(1, nparts * cap * 8);
+  const int64_t per_q = (int64_t)cap * 8 + 2 * 4;
   const int64_t qs = std::max<int64_t>(1, std::min<int64_t>(nq, (int64_t(16) << 30) / per_q));
   int64_t w = 0;
   // coarse ranking: probe lists of the whole batch, <= 256 MB of centroid scores per launch
@@ -487,11 +488,12 @@ void ivf_memory_plan(int dim, int64_t nrows, int nlist, int64_t max_len, int64_t
   const int64_t qb = std::max<int64_t>(1, std::min<int64_t>(int64_t(1) << 21, (int64_t(1) << 26) / std::max(nlist, 1)));
   w += 4 * std::min(nq, qb) * nlist + 4 * std::min(nq, qb);
   // per slice (the buffers are sized for the largest slice and reused)
-  const int64_t npos = qs * probes, nslot = qs * nparts;
+  const int64_t npos = qs * probes;
+  (void)nparts;
   w += (int64_t)sizeof(ScanItem) * ivf_max_items(qs, probes, nlist, scan_qmax(DT), ch, 0) + 4 * npos +
        16 * ((int64_t)nlist + 1);
   w += 2 * npos * DT + 8 * npos + 4 * npos * scan_sample_values() + 4 * qs;  // query operands, samples, T_q
-  w += 8 * nslot * cap + 8 * nslot;                                            // candidate regions + counts/floors
+  w += 8 * qs * cap + 8 * qs;                                                  // candidate buffers + counts/floors
   w += 8 * qs * STREAM_KO + 16 * qs;                                           // merged candidates, fail lists
   w += 8 * ivf_rerun_part_keys(qs, probes, k);                                 // device re-run scratch
   *workspace_bytes = w;
@@ -960,7 +962,7 @@ struct FlatIndex : Index {
     const int nch = (int)((cutoff + crow - 1) / crow);
     const int cap = stream_cap();
     const int nparts = nch;  // one chunk per "list"
-    const int64_t per_q = (int64_t)nparts * cap * 8;
+    const int64_t per_q = (int64_t)cap * 8 + 2 * 4;
     const int64_t qs = std::max<int64_t>(1, std::min<int64_t>(nq, (int64_t(16) << 30) / per_q));
     // the chunks as lists, on the device (no host work per search): bounds, the centroid copies (mu for
     // L2, 0 for IP) and the probe lists (every chunk, in order) of the largest slice
@@ -998,18 +1000,16 @@ struct FlatIndex : Index {
     }
     const int64_t npos = nq * probes;
     const int sv = scan_sample_values();
-    const size_t nslot = (size_t)nq * nparts;
     ws.sbq.ensure(sizeof(uint16_t) * std::max<int64_t>(npos, 1) * st.tdim());
     ws.sqsc.ensure(sizeof(float2) * std::max<int64_t>(npos, 1));
     ws.ssamp.ensure(sizeof(float) * std::max<int64_t>(npos, 1) * sv);
     ws.sthr.ensure(sizeof(float) * nq);
-    ws.scs.ensure(sizeof(float) * nslot * cap);
-    ws.sck.ensure(sizeof(uint32_t) * nslot * cap);
-    ws.scn.ensure(sizeof(int32_t) * nslot);
-    ws.scf.ensure(sizeof(uint32_t) * nslot);
+    ws.scand.ensure(sizeof(uint2) * (size_t)std::max<int64_t>(nq, 1) * cap);
+    ws.scn.ensure(sizeof(int32_t) * std::max<int64_t>(nq, 1));
+    ws.scf.ensure(sizeof(uint32_t) * std::max<int64_t>(nq, 1));
     ws.swork.ensure(sizeof(int32_t) * 2);
-    HIPCHK(hipMemsetAsync(ws.scn.p, 0, sizeof(int32_t) * nslot, ws.st));
-    HIPCHK(hipMemsetAsync(ws.scf.p, 0, sizeof(uint32_t) * nslot, ws.st));
+    HIPCHK(hipMemsetAsync(ws.scn.p, 0, sizeof(int32_t) * nq, ws.st));
+    HIPCHK(hipMemsetAsync(ws.scf.p, 0, sizeof(uint32_t) * nq, ws.st));
     HIPCHK(hipMemsetAsync(ws.swork.p, 0, sizeof(int32_t) * 2, ws.st));
     StreamArgs sa{};
     sa.h16 = st.h16.p;
@@ -1029,8 +1029,7 @@ struct FlatIndex : Index {
     sa.qsc = ws.sqsc.as<float2>();
     sa.samp = ws.ssamp.as<float>();
     sa.thr = ws.sthr.as<float>();
-    sa.cand_s = ws.scs.as<float>();
-    sa.cand_k = ws.sck.as<uint32_t>();
+    sa.cand = ws.scand.as<uint2>();
     sa.cand_n = ws.scn.as<int32_t>();
     sa.cand_f = ws.scf.as<uint32_t>();
     sa.cap = cap;
@@ -1071,13 +1070,11 @@ struct FlatIndex : Index {
     {
       PhaseTimer t(PH_MERGE, ws.st);
       CandMergeArgs m{};
-      m.cand_s = ws.scs.as<float>();
-      m.cand_k = ws.sck.as<uint32_t>();
+      m.cand = ws.scand.as<uint2>();
       m.cand_n = ws.scn.as<int32_t>();
       m.cand_f = ws.scf.as<uint32_t>();
       m.thr = ws.sthr.as<float>();
       m.nq = nq;
-      m.nparts = nparts;
       m.cap = cap;
       m.out_s = ws.ms.as<float>();
       m.out_k = ws.mk.as<int32_t>();
@@ -1896,7 +1893,7 @@ struct IvfFlatIndex : Index {
     }
     const int nparts = probes * ch.cmax;
     if (nparts > MAX_PARTS) throw Error(PYR_E_ARG, "nprobe too large");
-    const int64_t per_q = (int64_t)nparts * cap * 8;
+    const int64_t per_q = (int64_t)cap * 8 + 2 * 4;
     const int64_t qs = std::max<int64_t>(1, std::min<int64_t>(nq, (int64_t(16) << 30) / per_q));
     for (int64_t a0 = 0; a0 < nq; a0 += qs) {
       const int64_t n = std::min(qs, nq - a0);
@@ -1915,7 +1912,8 @@ struct IvfFlatIndex : Index {
 
   // measurement only (PYR_STREAM_DEBUG): candidate pool and certificate statistics of one slice, to stderr
   void stream_debug(int64_t nq, int k, int k1, int nparts, int cap, int32_t nf, const float *d_s, Workspace &ws) {
-    const size_t nslot = (size_t)nq * nparts;
+    (void)nparts;
+    const size_t nslot = (size_t)nq;  // per query: rows emitted (may exceed cap) and floor
     std::vector<float> ms((size_t)nq * STREAM_KO), thr(nq), res((size_t)nq * k);
     std::vector<int32_t> mk((size_t)nq * STREAM_KO), f1(nq);
     std::vector<uint32_t> cf(nslot);
@@ -1932,15 +1930,15 @@ struct IvfFlatIndex : Index {
     HIPCHK(hipStreamSynchronize(ws.st));
     int64_t emitted = 0, full = 0, shallow = 0;
     for (size_t i = 0; i < nslot; ++i) {
-      emitted += cn[i];  // rows kept (runs of <= 8 per writer)
-      full += cf[i] != 0u;
+      emitted += cn[i];
+      full += cn[i] > cap || cf[i] != 0u;
     }
     for (int64_t q = 0; q < nq; ++q) {
       int real = 0;
       for (int i = 0; i < STREAM_KO; ++i) real += mk[q * STREAM_KO + i] >= 0;
       shallow += real < STREAM_KO;
     }
-    fprintf(stderr, "[stream] nq %lld: emitted %lld (%.1f per query), full regions %lld, queries with < %d real "
+    fprintf(stderr, "[stream] nq %lld: emitted %lld (%.1f per query), full buffers %lld, queries with < %d real "
             "candidates %lld; certificate failures: depth %d %d, depth %d %d\n", (long long)nq, (long long)emitted,
             (double)emitted / std::max<int64_t>(nq, 1), (long long)full, STREAM_KO, (long long)shallow, k1, n1,
             STREAM_KO, nf);
@@ -1984,18 +1982,16 @@ struct IvfFlatIndex : Index {
     }
     const int64_t npos = nq * probes;
     const int sv = scan_sample_values();
-    const size_t nslot = (size_t)nq * nparts;
     ws.sbq.ensure(sizeof(uint16_t) * std::max<int64_t>(npos, 1) * lists.tdim());
     ws.sqsc.ensure(sizeof(float2) * std::max<int64_t>(npos, 1));
     ws.ssamp.ensure(sizeof(float) * std::max<int64_t>(npos, 1) * sv);
     ws.sthr.ensure(sizeof(float) * nq);
-    ws.scs.ensure(sizeof(float) * nslot * cap);
-    ws.sck.ensure(sizeof(uint32_t) * nslot * cap);
-    ws.scn.ensure(sizeof(int32_t) * nslot);
-    ws.scf.ensure(sizeof(uint32_t) * nslot);
+    ws.scand.ensure(sizeof(uint2) * (size_t)std::max<int64_t>(nq, 1) * cap);
+    ws.scn.ensure(sizeof(int32_t) * std::max<int64_t>(nq, 1));
+    ws.scf.ensure(sizeof(uint32_t) * std::max<int64_t>(nq, 1));
     ws.swork.ensure(sizeof(int32_t) * 2);
-    HIPCHK(hipMemsetAsync(ws.scn.p, 0, sizeof(int32_t) * nslot, ws.st));
-    HIPCHK(hipMemsetAsync(ws.scf.p, 0, sizeof(uint32_t) * nslot, ws.st));
+    HIPCHK(hipMemsetAsync(ws.scn.p, 0, sizeof(int32_t) * nq, ws.st));
+    HIPCHK(hipMemsetAsync(ws.scf.p, 0, sizeof(uint32_t) * nq, ws.st));
     HIPCHK(hipMemsetAsync(ws.swork.p, 0, sizeof(int32_t) * 2, ws.st));
     StreamArgs sa{};
     sa.h16 = lists.h16.p;
@@ -2015,8 +2011,7 @@ struct IvfFlatIndex : Index {
     sa.qsc = ws.sqsc.as<float2>();
     sa.samp = ws.ssamp.as<float>();
     sa.thr = ws.sthr.as<float>();
-    sa.cand_s = ws.scs.as<float>();
-    sa.cand_k = ws.sck.as<uint32_t>();
+    sa.cand = ws.scand.as<uint2>();
     sa.cand_n = ws.scn.as<int32_t>();
     sa.cand_f = ws.scf.as<uint32_t>();
     sa.cap = cap;
@@ -2074,13 +2069,11 @@ struct IvfFlatIndex : Index {
     {
       PhaseTimer t(PH_MERGE, ws.st);
       CandMergeArgs m{};
-      m.cand_s = ws.scs.as<float>();
-      m.cand_k = ws.sck.as<uint32_t>();
+      m.cand = ws.scand.as<uint2>();
       m.cand_n = ws.scn.as<int32_t>();
       m.cand_f = ws.scf.as<uint32_t>();
       m.thr = ws.sthr.as<float>();
       m.nq = nq;
-      m.nparts = nparts;
       m.cap = cap;
       m.out_s = ws.ms.as<float>();
       m.out_k = ws.mk.as<int32_t>();
@@ -2702,7 +2695,7 @@ struct IvfPqIndex : Index {
     }
     const int nparts = probes * ch.cmax;
     if (nparts > MAX_PARTS) throw Error(PYR_E_ARG, "nprobe too large");
-    const int64_t per_q = (int64_t)nparts * cap * 8;
+    const int64_t per_q = (int64_t)cap * 8 + 2 * 4;
     const int64_t qs = std::max<int64_t>(1, std::min<int64_t>(nq, (int64_t(16) << 30) / per_q));
     for (int64_t a0 = 0; a0 < nq; a0 += qs) {
       const int64_t n = std::min(qs, nq - a0);
@@ -2725,18 +2718,16 @@ struct IvfPqIndex : Index {
     }
     const int64_t npos = nq * probes;
     const int sv = pq32_sample_values();
-    const size_t nslot = (size_t)nq * nparts;
     ws.sbq.ensure(sizeof(uint16_t) * std::max<int64_t>(npos, 1) * dim);
     ws.sqsc.ensure(sizeof(float2) * std::max<int64_t>(npos, 1));
     ws.ssamp.ensure(sizeof(float) * std::max<int64_t>(npos, 1) * sv);
     ws.sthr.ensure(sizeof(float) * nq);
-    ws.scs.ensure(sizeof(float) * nslot * cap);
-    ws.sck.ensure(sizeof(uint32_t) * nslot * cap);
-    ws.scn.ensure(sizeof(int32_t) * nslot);
-    ws.scf.ensure(sizeof(uint32_t) * nslot);
+    ws.scand.ensure(sizeof(uint2) * (size_t)std::max<int64_t>(nq, 1) * cap);
+    ws.scn.ensure(sizeof(int32_t) * std::max<int64_t>(nq, 1));
+    ws.scf.ensure(sizeof(uint32_t) * std::max<int64_t>(nq, 1));
     ws.swork.ensure(sizeof(int32_t) * 2);
-    HIPCHK(hipMemsetAsync(ws.scn.p, 0, sizeof(int32_t) * nslot, ws.st));
-    HIPCHK(hipMemsetAsync(ws.scf.p, 0, sizeof(uint32_t) * nslot, ws.st));
+    HIPCHK(hipMemsetAsync(ws.scn.p, 0, sizeof(int32_t) * nq, ws.st));
+    HIPCHK(hipMemsetAsync(ws.scf.p, 0, sizeof(uint32_t) * nq, ws.st));
     HIPCHK(hipMemsetAsync(ws.swork.p, 0, sizeof(int32_t) * 2, ws.st));
     StreamArgs sa{};
     sa.h16 = cpack.p;
@@ -2754,8 +2745,7 @@ struct IvfPqIndex : Index {
     sa.qsc = ws.sqsc.as<float2>();
     sa.samp = ws.ssamp.as<float>();
     sa.thr = ws.sthr.as<float>();
-    sa.cand_s = ws.scs.as<float>();
-    sa.cand_k = ws.sck.as<uint32_t>();
+    sa.cand = ws.scand.as<uint2>();
     sa.cand_n = ws.scn.as<int32_t>();
     sa.cand_f = ws.scf.as<uint32_t>();
     sa.cap = cap;
@@ -2793,13 +2783,11 @@ struct IvfPqIndex : Index {
     {
       PhaseTimer t(PH_MERGE, ws.st);
       CandMergeArgs m{};
-      m.cand_s = ws.scs.as<float>();
-      m.cand_k = ws.sck.as<uint32_t>();
+      m.cand = ws.scand.as<uint2>();
       m.cand_n = ws.scn.as<int32_t>();
       m.cand_f = ws.scf.as<uint32_t>();
       m.thr = ws.sthr.as<float>();
       m.nq = nq;
-      m.nparts = nparts;
       m.cap = cap;
       m.out_s = ws.ms.as<float>();
       m.out_k = ws.mk.as<int32_t>();
@@ -2860,12 +2848,12 @@ struct IvfPqIndex : Index {
                     });
   }
 
-  // the reference's per-row LUT sum on the LDS (pq_adc4 / pq_adc / pq_scan)
+  // the reference's per-row LUT sum on the LDS (pq_adc4 / pq_scan)
   void search_lut(const float *d_q, int64_t nq, int k, int probes, float *d_s, int64_t *d_l, int32_t *d_c,
                   Workspace &ws) {
     const int64_t bcut = buf.st.n;
-    // list-scan kernel: pq_adc4 (4 queries per LDS gather; lists split into PQ4_ROWS-row chunks),
-    // else pq_adc, else the first-cut pq_scan; PYR_PQ_ADC=1 / 0 force the latter two (A/B only)
+    // list-scan kernel: pq_adc4 (4 queries per LDS gather; lists split into PQ4_ROWS-row chunks), else
+    // the first-cut pq_scan; PYR_PQ_ADC=0 forces the latter (A/B only)
     const int mode = pq_adc_mode();
     IvfChunking ch{1 << 30, 1, 0};
     int kern = 0;
@@ -2877,7 +2865,6 @@ struct IvfPqIndex : Index {
       if ((int64_t)probes * ch.cmax < MAX_PARTS) kern = 2;
       else ch = IvfChunking{1 << 30, 1, 0};
     }
-    if (kern == 0 && mode >= 1 && pq_adc_supported(dim, M, ksub, k)) kern = 1;
     const int lparts = probes * ch.cmax;
     ScanPlan bp;
     if (buf.live_count() > 0) bp = plan_flat(bcut, nq, dim, k, MAX_PARTS - lparts);
@@ -2925,7 +2912,6 @@ struct IvfPqIndex : Index {
         throw Error(PYR_E_ARG, "PQ lookup table exceeds LDS");
       PhaseTimer t(PH_PQ_SCAN, ws.st, prof().on ? probed_rows(ws, nq, probes, le, lb) : 0);
       if (kern == 2) launch_pq_adc4(a, maxi, ws.st);
-      else if (kern == 1) launch_pq_adc(a, maxi, ws.st);
       else launch_pq_scan(a, maxi, ws.st);
     }
     if (bp.nchunks > 0) {  // :130-136 exact buffer scan

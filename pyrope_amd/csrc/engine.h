@@ -132,7 +132,7 @@ struct Workspace {
   DevMem fprobes;                                 // probe lists of the failing queries (IVF exact re-run)
   DevMem q8q, q8qs;                               // 8-bit search mode: quantized queries, their sums
   // stream-and-emit list scan (stream16.hip): query operands, samples, thresholds, candidate regions
-  DevMem sbq, sqsc, ssamp, sthr, scs, sck, scn, scf, swork, fail2, fail_cnt2;
+  DevMem sbq, sqsc, ssamp, sthr, scand, scn, scf, swork, fail2, fail_cnt2;
   DevMem rrpart;  // device re-run of certificate failures: per (query, probe) top-k keys
   DevMem tdbg;    // measurement only (PYR_STREAM_TIMING)
   DevMem vlb, vle, vcents;  // FLAT on the stream scan: its chunks as lists (FlatIndex::search_stream)

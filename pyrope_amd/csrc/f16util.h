@@ -1,4 +1,4 @@
-// f16util.h -- device helpers shared by the fp16 tile list scans (filter16.hip, stream16.hip, scan.hip, pq32.hip).
+// f16util.h -- device helpers shared by the fp16 tile kernels (tiles16.hip, sample16.hip, scan.hip, pq32.hip).
 // Internal to libpyrope_hip.so; include inside an anonymous namespace of a .hip file's pyr namespace.
 // (include after <hip/hip_runtime.h> and <cmath>)
 #pragma once
@@ -70,3 +70,39 @@ __device__ __forceinline__ float lower_thr(float t, float c) {
   const float lowered = (t - c) - 0x1p-20f * (fabsf(t) + fabsf(c));
   return isinf(t) ? (t > 0.0f ? t : -3.402823466e+38f) : fmaxf(lowered, -3.402823466e+38f);
 }
+
+#ifdef PYR_STREAM_EMIT
+// ---- the stream scans' candidate emission (scan.hip, pq32.hip): query-major buffers (StreamArgs::cand)
+// one row straight to query q's buffer (a row that finds it full raises the query's floor)
+__device__ __forceinline__ void cand_put(const StreamArgs &a, int q, float sc, uint32_t key) {
+  const int slot = atomicAdd(a.cand_n + q, 1);
+  if (slot < a.cap) a.cand[(size_t)q * a.cap + slot] = make_uint2(__float_as_uint(sc), key);
+  else atomicMax(a.cand_f + q, score_key(sc));
+}
+// An item's staged rows eb[0, n) ({score bits, query slot << 23 | row offset}) to their queries'
+// buffers: the rows per query slot are counted (LDS), each query reserves its run with ONE global
+// atomic, then every row takes its place in the run.  cnt / base: per query slot LDS arrays (cnt zero
+// on entry; the next item's prologue zeroes it again); qid(i): the query of slot i.  Block-wide (NT
+// threads, barriers).
+template <int NT, class QID>
+__device__ __forceinline__ void cand_flush(const StreamArgs &a, const uint2 *eb, int n, int qcnt, int r0, int *cnt,
+                                           int *base, QID qid) {
+  const int tid = threadIdx.x;
+  for (int i = tid; i < n; i += NT) atomicAdd(&cnt[eb[i].y >> 23], 1);
+  __syncthreads();
+  for (int i = tid; i < qcnt; i += NT) {
+    const int c = cnt[i];
+    base[i] = c > 0 ? atomicAdd(a.cand_n + qid(i), c) : 0;
+    cnt[i] = 0;
+  }
+  __syncthreads();
+  for (int i = tid; i < n; i += NT) {
+    const uint2 e = eb[i];
+    const int qi = (int)(e.y >> 23);
+    const int slot = base[qi] + atomicAdd(&cnt[qi], 1);
+    const int q = qid(qi);
+    if (slot < a.cap) a.cand[(size_t)q * a.cap + slot] = make_uint2(e.x, a.key_base | (uint32_t)(r0 + (int)(e.y & 0x7FFFFFu)));
+    else atomicMax(a.cand_f + q, score_key(__uint_as_float(e.x)));
+  }
+}
+#endif

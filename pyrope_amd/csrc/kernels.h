@@ -223,9 +223,6 @@ struct PqArgs {
   int32_t ablate;          // measurement only (PYR_PQ_ABLATE): 1 LUT once per item, 2 no top-k
 };
 void launch_pq_scan(const PqArgs &a, int max_items, hipStream_t st);
-// LDS-rate ADC scan (512-thread blocks, wave-distributed top-k); k <= 64, M <= 128
-bool pq_adc_supported(int dim, int M, int ksub, int k);
-void launch_pq_adc(const PqArgs &a, int max_items, hipStream_t st);
 // four queries per LDS gather (float4 LUT entries, 8-subspace double-buffered LUT passes);
 // items of at most pq_adc4_rows() rows (IvfChunking chunk), k <= 64, ksub <= 256
 bool pq_adc4_supported(int dim, int M, int ksub, int k);
@@ -326,10 +323,12 @@ struct StreamArgs {
   float2 *qsc;                // [pos] {f, cq}
   float *samp;                // [q * nprobe + probe][scan_sample_values()] sampled scores
   const float *thr;           // [q] T_q (score space), or null
-  float *cand_s;              // [q * nparts + part][cap] emitted scores
-  uint32_t *cand_k;           // keys
-  int32_t *cand_n;            // [q * nparts + part] rows kept (<= cap)
-  uint32_t *cand_f;           // score_key of the best dropped row (0: none)
+  // the emitted rows, query-major: query q's rows at cand[q * cap + i] = {score bits, key}, i < cand_n[q]
+  // (reserved with one atomic per (item, query); past cap a row only raises the floor cand_f[q] =
+  // score_key of the best row dropped, 0: none)
+  uint2 *cand;
+  int32_t *cand_n;
+  uint32_t *cand_f;
   int32_t cap;
   int32_t *work;              // persistent-block item counter (zeroed before each launch)
   uint32_t key_base, row_limit;
@@ -387,13 +386,12 @@ struct PqRefineArgs {
 };
 void launch_pq32_refine(const PqRefineArgs &a, int64_t nq, hipStream_t st);
 struct CandMergeArgs {
-  const float *cand_s;
-  const uint32_t *cand_k;
+  const uint2 *cand;          // StreamArgs::cand / cand_n / cand_f
   const int32_t *cand_n;
   const uint32_t *cand_f;
   const float *thr;
   int64_t nq;
-  int32_t nparts, cap;
+  int32_t cap;
   float *out_s;               // [nq][STREAM_KO] desc; floor placeholders key -2, none -1
   int32_t *out_k;
 };

@@ -876,25 +876,10 @@ __global__ __launch_bounds__(256) void pq_scan_kernel(PqArgs a) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// pq_adc: the IVF-PQ list scan at LDS rate.  One 512-thread block (8 waves) per work item
-// (list, <= qchunk queries); per query of the item:
-//   1. residual q - c_list and its LUT (ProductQuantizer.cs:107-117, M x ksub fp32) in LDS,
-//      built by all 512 threads;
-//   2. every wave streams 64-row code blocks (one row per lane, codes double-buffered in
-//      registers) and sums LUT entries in m order (IvfPqVectorIndex.cs:182-186) -- the LDS
-//      gathers are the bound (ds_read_b32, random banks);
-//   3. each wave keeps its top-k spread over lanes 0..k-1 (lane j = j-th best): candidates
-//      beating the wave's k-th (and the query's shared bound) are found with one ballot and
-//      inserted with a shuffle, so the common no-candidate case costs two compares;
-//   4. the 8 wave lists are merged by wave 0 into the item's partial top-k and the k-th
-//      best is published to the shared per-query bound.
-// Scores, tie rule and partial slots are those of pq_scan_kernel (bit-identical results).
-// Blocks are mapped XCD-major (block b runs on XCD b % 8): each XCD walks its own
-// contiguous range of the list-major items, so the items of one list run side by side on
-// one XCD and share its L2 copy of the list's codes.
-// ---------------------------------------------------------------------------
-constexpr int PQ_MAX_WAVES = 16;
+// Top-k of a wave spread over lanes 0..k-1 (lane j = j-th best): candidates beating the wave's k-th
+// (and the query's shared bound) are found with one ballot and inserted with a shuffle, so the common
+// no-candidate case costs two compares.  (Rounds 1-3 also had pq_adc, one query per pass; pq_adc4
+// superseded it.)
 
 // wave-wide insertion of the candidates flagged in `cand` into the lane-distributed list
 __device__ __forceinline__ void wave_list_insert(bool cand, float sc, uint32_t key, float &ls, uint32_t &lk, float &kth,
@@ -919,105 +904,6 @@ __device__ __forceinline__ void wave_list_insert(bool cand, float sc, uint32_t k
     kthk = __shfl(lk, k - 1);
     m &= m - 1;
     m &= __ballot(cand && better(sc, key, kth, kthk));
-  }
-}
-
-template <int NCH, bool K256, int NT>
-__global__ __launch_bounds__(NT) void pq_adc_kernel(PqArgs a) {
-  constexpr int PQ_THREADS = NT, PQ_WAVES = NT / 64;
-  constexpr bool DB = NT <= 512;  // double-buffered code registers (1024 threads: VGPR cap 128)
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int nit = *a.n_items;
-  const int per = (nit + 7) >> 3;  // items per XCD (the grid has >= 8 * per blocks)
-  if ((int)(blockIdx.x >> 3) >= per) return;
-  const int item = ((int)blockIdx.x & 7) * per + ((int)blockIdx.x >> 3);
-  if (item >= nit) return;
-  const ScanItem it = a.items[item];
-  const int D = a.dim, M = a.M, ksub = K256 ? 256 : a.ksub, k = a.k, sub = D / M;
-  float *lut = smem;                                           // [M][ksub]
-  float *res = lut + M * ksub;                                 // [D]
-  float *mrs = res + ((D + 3) & ~3);                           // [PQ_WAVES][k] wave lists
-  uint32_t *mrk = reinterpret_cast<uint32_t *>(mrs + PQ_WAVES * k);
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const float *cent = a.cents + (size_t)it.list * D;
-  const int rb = it.row_begin, re = it.row_end;  // rb: multiple of 64 (64-row code blocks)
-  const int ngrp = (re - rb + 63) >> 6;
-  const uint4 *codes = reinterpret_cast<const uint4 *>(a.codes);
-
-  for (int i = 0; i < it.qcnt; ++i) {
-    const int slot = a.qlist[it.qbeg + i] + it.part;
-    const int qi = slot / a.nparts;
-    const float *qp = a.queries + (size_t)qi * D;
-    for (int d = tid; d < D; d += PQ_THREADS) res[d] = qp[d] - cent[d];  // IvfPqVectorIndex.cs:161-163
-    __syncthreads();
-    if (!(a.ablate & 1) || i == 0)
-      for (int e = tid; e < M * ksub; e += PQ_THREADS) {  // ProductQuantizer.cs:112-117
-        const int m = e / ksub, j = e - m * ksub;
-        lut[e] = em_l2sq_unsafe(Off{res + m * sub}, Off{a.codebooks + ((size_t)m * ksub + j) * sub}, sub);
-      }
-    __syncthreads();
-
-    float ls = -INFINITY, kth = -INFINITY;  // lane j < k holds the wave's j-th best
-    uint32_t lk = KEY_NONE, kthk = KEY_NONE;
-    float gs = a.gthr ? key_score(__hip_atomic_load(a.gthr + qi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                      : -INFINITY;
-    uint4 cur[NCH], nxt[NCH];
-    auto load = [&](uint4 (&dst)[NCH], int g) {
-      const size_t base = ((size_t)((rb >> 6) + g) * NCH) * 64 + lane;
-#pragma unroll
-      for (int c = 0; c < NCH; ++c) dst[c] = codes[base + (size_t)c * 64];
-    };
-    if (DB && w < ngrp) load(cur, w);
-    for (int g = w, it2 = 0; g < ngrp; g += PQ_WAVES, ++it2) {
-      if (!DB) load(cur, g);
-      else if (g + PQ_WAVES < ngrp) load(nxt, g + PQ_WAVES);
-      const int r = rb + g * 64 + lane;
-      const bool valid = r < re && a.live[r];
-      float dist = 0.0f;  // IvfPqVectorIndex.cs:182-186, m order
-#pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        const uint32_t ws[4] = {cur[c].x, cur[c].y, cur[c].z, cur[c].w};
-#pragma unroll
-        for (int b = 0; b < 16; ++b) {
-          const int m = c * 16 + b;
-          if (c < NCH - 1 || m < M) dist = dist + lut[m * ksub + ((ws[b >> 2] >> (8 * (b & 3))) & 0xFF)];
-        }
-      }
-      const float score = -dist;  // :194
-      const uint32_t key = (uint32_t)r;
-      if (a.gthr && (it2 & 3) == 3)
-        gs = fmaxf(gs, key_score(__hip_atomic_load(a.gthr + qi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
-      const bool cand = valid && score >= gs && better(score, key, kth, kthk);
-      if (a.ablate & 2) {
-        if (score == 12345.0f) ls = score;  // keep the scan alive without the top-k work
-      } else {
-        wave_list_insert(cand, score, key, ls, lk, kth, kthk, k, lane);
-      }
-      if (DB)
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) cur[c] = nxt[c];
-    }
-    if (lane < k) {
-      mrs[w * k + lane] = ls;
-      mrk[w * k + lane] = lk;
-    }
-    __syncthreads();
-    if (w == 0) {
-      for (int e0 = k; e0 < PQ_WAVES * k; e0 += 64) {
-        const int e = e0 + lane;
-        const float s = e < PQ_WAVES * k ? mrs[e] : -INFINITY;
-        const uint32_t kk = e < PQ_WAVES * k ? mrk[e] : KEY_NONE;
-        const bool cand = kk != KEY_NONE && better(s, kk, kth, kthk);
-        wave_list_insert(cand, s, kk, ls, lk, kth, kthk, k, lane);
-      }
-      if (lane < k) {
-        a.part_s[(size_t)slot * k + lane] = ls;
-        a.part_k[(size_t)slot * k + lane] = lk;
-      }
-      if (lane == 0 && a.gthr && kthk != KEY_NONE) atomicMax(a.gthr + qi, score_key(kth));
-    }
-    // the next query rewrites res / lut only after the barrier that follows its res stores;
-    // wave 0 reads mrs / mrk before it reaches that barrier
   }
 }
 
@@ -1047,7 +933,7 @@ __global__ __launch_bounds__(NT) void pq_adc4_kernel(PqArgs a) {
   constexpr int PQ4_NT = NT, PQ4_NW = NT / 64, PQ4_G = PQ4_ROWS / NT;  // row groups per wave
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int nit = *a.n_items;
-  const int per = (nit + 7) >> 3;  // XCD-major item mapping as in pq_adc_kernel
+  const int per = (nit + 7) >> 3;  // XCD-major item mapping: the items of one list run on one XCD
   if ((int)(blockIdx.x >> 3) >= per) return;
   const int item = ((int)blockIdx.x & 7) * per + ((int)blockIdx.x >> 3);
   if (item >= nit) return;
@@ -1724,17 +1610,6 @@ size_t pq_scan_lds_bytes(int dim, int M, int ksub, int k) {
   return (size_t)(((dim + 3) & ~3) + M * ksub + 2 * k + 2 * 256 + 4) * 4;
 }
 
-size_t pq_adc_lds_bytes(int dim, int M, int ksub, int k) {  // sized for the largest block
-  return (size_t)(M * ksub + ((dim + 3) & ~3) + 2 * PQ_MAX_WAVES * k) * 4;
-}
-static int pq_adc_threads() {  // PYR_PQ_THREADS=1024: measurement variant
-  const char *e = getenv("PYR_PQ_THREADS");
-  return e && atoi(e) == 1024 ? 1024 : 512;
-}
-bool pq_adc_supported(int dim, int M, int ksub, int k) {
-  return k >= 1 && k <= 64 && (M + 15) / 16 <= 8 && pq_adc_lds_bytes(dim, M, ksub, k) <= 160 * 1024;
-}
-
 size_t pq_adc4_lds_bytes(int dim, int ksub, int k) {  // sized for the largest block
   return (size_t)(2 * PQ4_SC * ksub * 4 + 4 * dim + 2 * 4 * PQ4_MAX_NW * k) * 4;
 }
@@ -1752,9 +1627,7 @@ static void launch_pq_adc4_nt(const PqArgs &a, int max_items, hipStream_t st) {
 }
 template <int SUB, bool K256>
 static void launch_pq_adc4_t(const PqArgs &a, int max_items, hipStream_t st) {
-  const char *e = getenv("PYR_PQ4_THREADS");  // 512: measurement variant (1024 measured 1.5x faster)
-  if (e && atoi(e) == 512) launch_pq_adc4_nt<SUB, K256, 512>(a, max_items, st);
-  else launch_pq_adc4_nt<SUB, K256, 1024>(a, max_items, st);
+  launch_pq_adc4_nt<SUB, K256, 1024>(a, max_items, st);  // 1024 threads measured 1.5x faster than 512
 }
 void launch_pq_adc4(const PqArgs &a, int max_items, hipStream_t st) {
   if (max_items <= 0) return;
@@ -1773,43 +1646,6 @@ void launch_pq_adc4(const PqArgs &a, int max_items, hipStream_t st) {
     if (k256) launch_pq_adc4_t<0, true>(a, max_items, st);
     else launch_pq_adc4_t<0, false>(a, max_items, st);
   }
-}
-
-template <int NCH, bool K256, int NT>
-static void launch_pq_adc_nt(const PqArgs &a, int max_items, hipStream_t st) {
-  static std::atomic<uint64_t> attr{0};
-  allow_max_lds(reinterpret_cast<const void *>(&pq_adc_kernel<NCH, K256, NT>), attr);
-  const int grid = (max_items + 7) / 8 * 8;  // XCD-major item mapping needs a multiple of 8 blocks
-  hipLaunchKernelGGL((pq_adc_kernel<NCH, K256, NT>), dim3(grid), dim3(NT), pq_adc_lds_bytes(a.dim, a.M, a.ksub, a.k),
-                     st, a);
-}
-template <int NCH, bool K256>
-static void launch_pq_adc_t(const PqArgs &a, int max_items, hipStream_t st) {
-  if (pq_adc_threads() == 1024) launch_pq_adc_nt<NCH, K256, 1024>(a, max_items, st);
-  else launch_pq_adc_nt<NCH, K256, 512>(a, max_items, st);
-}
-
-void launch_pq_adc(const PqArgs &a, int max_items, hipStream_t st) {
-  if (max_items <= 0) return;
-  const int nch = (a.M + 15) / 16;
-  const bool k256 = a.ksub == 256;
-#define PQ_CASE(N)                                               \
-  case N:                                                        \
-    if (k256) launch_pq_adc_t<N, true>(a, max_items, st);       \
-    else launch_pq_adc_t<N, false>(a, max_items, st);           \
-    break;
-  switch (nch) {
-    PQ_CASE(1)
-    PQ_CASE(2)
-    PQ_CASE(3)
-    PQ_CASE(4)
-    PQ_CASE(5)
-    PQ_CASE(6)
-    PQ_CASE(7)
-    PQ_CASE(8)
-    default: break;
-  }
-#undef PQ_CASE
 }
 
 void launch_pq_scan(const PqArgs &a, int max_items, hipStream_t st) {

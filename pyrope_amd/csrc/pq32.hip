@@ -31,6 +31,7 @@
 namespace pyr {
 namespace {
 
+#define PYR_STREAM_EMIT
 #include "f16util.h"
 
 __device__ __forceinline__ size_t blk_off(int64_t r, int d, int D) {
@@ -126,8 +127,8 @@ __global__ __launch_bounds__(64 * PNW, 1) void pq_scan_kernel(StreamArgs a, cons
   constexpr int PIECES = PQG * KS;
   __shared__ __attribute__((aligned(16))) char bl[PIECES * 1024];
   __shared__ float2 qf[PQMAX], qz[PQMAX];
-  __shared__ int cnt_l[PQMAX];
-  __shared__ uint32_t flr_l[PQMAX];
+  __shared__ int cnt_l[PQMAX];       // the item's staged rows per query slot (cand_flush)
+  __shared__ int base_l[PQMAX];
   __shared__ int item_sh, eb_n;
   constexpr int EB = 768;
   __shared__ uint2 eb[EB];
@@ -162,12 +163,11 @@ __global__ __launch_bounds__(64 * PNW, 1) void pq_scan_kernel(StreamArgs a, cons
           const float T = (!SAMPLE && a.thr) ? a.thr[q] : -INFINITY;
           v = make_float2(fc.x, lower_thr(T, fc.y));
           cqv = fc.y;
-          o = SAMPLE ? q * a.nprobe + (slot % a.nparts) / a.cmax : slot + it.part;
+          o = SAMPLE ? q * a.nprobe + (slot % a.nparts) / a.cmax : q;
         }
         qf[i] = v;
         qz[i] = make_float2(cqv, __int_as_float(o));
         cnt_l[i] = 0;
-        flr_l[i] = 0u;
       }
       if (tid == 0) eb_n = 0;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -179,16 +179,7 @@ __global__ __launch_bounds__(64 * PNW, 1) void pq_scan_kernel(StreamArgs a, cons
     const int rlim = it.row_end;
     const bool stage = it.row_end - r0 < (1 << 23);
 
-    auto put = [&](int qi, float sc, int row) {
-      const int slot = atomicAdd(&cnt_l[qi], 1);
-      if (slot < a.cap) {
-        const size_t rb = (size_t)__float_as_int(qz[qi].y) * a.cap;
-        a.cand_s[rb + slot] = sc;
-        a.cand_k[rb + slot] = a.key_base | (uint32_t)row;
-      } else {
-        atomicMax(&flr_l[qi], score_key(sc));
-      }
-    };
+    auto put = [&](int qi, float sc, int row) { cand_put(a, __float_as_int(qz[qi].y), sc, a.key_base | (uint32_t)row); };
     float smx[PQG];  // SAMPLE: this lane's best bound per query group
 #pragma unroll
     for (int g = 0; g < PQG; ++g) smx[g] = -INFINITY;
@@ -280,16 +271,7 @@ __global__ __launch_bounds__(64 * PNW, 1) void pq_scan_kernel(StreamArgs a, cons
       continue;
     }
     __syncthreads();
-    for (int i = tid, n = min(eb_n, EB); i < n; i += 64 * PNW) {
-      const uint2 e = eb[i];
-      put((int)(e.y >> 23), __uint_as_float(e.x), r0 + (int)(e.y & 0x7FFFFFu));
-    }
-    __syncthreads();
-    for (int i = tid; i < qcnt; i += 64 * PNW) {
-      const int o = __float_as_int(qz[i].y);
-      a.cand_n[o] = min(cnt_l[i], a.cap);
-      a.cand_f[o] = flr_l[i];
-    }
+    cand_flush<64 * PNW>(a, eb, min(eb_n, EB), qcnt, r0, cnt_l, base_l, [&](int i) { return __float_as_int(qz[i].y); });
   }
 }
 

@@ -16,8 +16,9 @@
 //     sample -- one wave per 32-query group, or the tiles staged in LDS -- measured slower at I1: 0.29 and
 //     0.19-0.26 ms against 0.15 ms, profiles/r4_scan/sample_lds_attempt.log.)
 //  3. sselect_kernel: T_q = the R-th largest of the query's sample values (radix select).
-//  4. cand_merge_kernel: per query the best KO (64) of its emitted rows, ranked with KO copies of the
-//     floor placeholder max(T_q, floors) (KEY_FLOOR): every row left out scores <= the merged KO-th.
+//  4. cand_merge_kernel: per query the best KO (64) of its emitted rows (its query-major buffer, read
+//     64 contiguous entries at a time), ranked with KO copies of the floor placeholder max(T_q, floor)
+//     (KEY_FLOOR): every row left out scores <= the merged KO-th.
 #pragma clang fp contract(off)
 
 #include <hip/hip_runtime.h>
@@ -49,6 +50,7 @@ __global__ __launch_bounds__(256) void sprep_kernel(StreamArgs a) {
   if (item >= *a.n_items) return;
   const ScanItem it = a.items[item];
   if (it.part != 0) return;  // chunk-0 items cover every qlist position of their list once
+  // (a bounded grid walking 64-item windows of chunk-0 items measured slower: 0.165 vs 0.146 ms, r4g)
   constexpr int LQ = D / 8, QW = 64 / LQ;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, sub = lane % LQ, qsl = lane / LQ;
   const float4 *cp = reinterpret_cast<const float4 *>(a.cents + (size_t)it.list * D + 8 * sub);
@@ -298,48 +300,21 @@ __device__ __forceinline__ uint64_t merge64_desc(uint64_t v, int lane) {  // v b
 
 template <int KO>
 __global__ __launch_bounds__(256) void cand_merge_kernel(CandMergeArgs m) {
-  __shared__ int pre[4][MAX_PARTS + 1];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t q = (int64_t)blockIdx.x * 4 + w;
   if (q >= m.nq) return;
-  const size_t sb = (size_t)q * m.nparts;
-  int tot = 0;
-  uint32_t fk = 0u;
-  for (int base = 0; base < m.nparts; base += 64) {
-    const int p = base + lane;
-    int n = 0;
-    if (p < m.nparts) {
-      n = m.cand_n[sb + p];
-      fk = max(fk, m.cand_f[sb + p]);
-    }
-    int x = n;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int y = __shfl_up(x, off);
-      if (lane >= off) x += y;
-    }
-    if (p < m.nparts) pre[w][p] = tot + x - n;
-    tot += __shfl(x, 63);
-  }
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) fk = max(fk, (uint32_t)__shfl_xor((int)fk, off));
+  const int tot = min(m.cand_n[q], m.cap);
+  const uint32_t fk = m.cand_f[q];
   float F = m.thr ? m.thr[q] : -INFINITY;
   if (fk != 0u) F = fmaxf(F, key_score(fk));
-  __builtin_amdgcn_wave_barrier();
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const uint2 *cq = m.cand + (size_t)q * m.cap;
   uint64_t cur = F > -INFINITY ? pack_cand(F, KEY_FLOOR) : 0ull;
   for (int base = 0; base < tot; base += 64) {
     const int idx = base + lane;
     uint64_t v = 0ull;
     if (idx < tot) {
-      int lo = 0, hi = m.nparts;  // pre[lo] <= idx < pre[hi] (pre[nparts] = tot)
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (pre[w][mid] <= idx) lo = mid;
-        else hi = mid;
-      }
-      const size_t e = (sb + lo) * m.cap + (idx - pre[w][lo]);
-      v = pack_cand(m.cand_s[e], m.cand_k[e]);
+      const uint2 e = cq[idx];
+      v = pack_cand(__uint_as_float(e.x), e.y);
     }
     const uint64_t kth = shfl64(cur, KO - 1);
     if (!__builtin_amdgcn_ballot_w64(v > kth)) continue;

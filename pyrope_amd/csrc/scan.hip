@@ -16,8 +16,8 @@
 //     16 waves per block (4 per SIMD, <= 128 VGPRs): no prefetch of a wave's next tile (the other 15
 //     waves' work hides its load; an L2 prefetch by LDS-DMA measured slower), and tiles are taken from
 //     an LDS counter so the waves reach the item's end together.
-//  3. Emitted rows are staged in LDS and written to the candidate regions by the whole block at the
-//     item's end (64 rows per store instruction instead of one).
+//  3. Emitted rows are staged in LDS and written to their queries' candidate buffers by the whole block
+//     at the item's end: one global atomic per (item, query) reserves the query's run (cand_flush).
 //
 // Row terms (meta + the row's share of the error bound) come precomputed per store
 // (RowStore::row_terms, StreamArgs::mub).
@@ -37,6 +37,7 @@
 namespace pyr {
 namespace {
 
+#define PYR_STREAM_EMIT
 #include "f16util.h"
 
 constexpr int SAMPLE_TILES = 16;       // tiles of a list the sample scores (stream16.hip: 2 x 8 waves)
@@ -231,9 +232,9 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
   static_assert(KS % KC == 0 && QMAX <= 512, "tile dimension");
   __shared__ __attribute__((aligned(16))) char bl[PIECES * 1024];
   __shared__ float2 qf[QMAX];        // per query slot: {f, threshold in y = f acc + row term space}
-  __shared__ float2 qz[QMAX];        // {cq (score = y + cq), candidate region as int bits}
-  __shared__ int cnt_l[QMAX];        // rows of the region
-  __shared__ uint32_t flr_l[QMAX];   // score_key of the best row a full region dropped (0: none)
+  __shared__ float2 qz[QMAX];        // {cq (score = y + cq), the query as int bits}
+  __shared__ int cnt_l[QMAX];        // the item's staged rows per query slot (cand_flush)
+  __shared__ int base_l[QMAX];       // and their run in the query's buffer
   __shared__ int item_sh, eb_n, tnext;
   __shared__ uint32_t pf_sink[64];   // the L2 prefetch's LDS-DMA target (never read)
   // the item's emitted rows, staged in the LDS left over: (score bits, query slot << 23 | row offset)
@@ -291,12 +292,11 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
           const float T = a.thr ? a.thr[slot / a.nparts] + a.thr_bias : -INFINITY;
           v = make_float2(fc.x, lower_thr(T, fc.y));
           cqv = fc.y;
-          o = slot + it.part;
+          o = slot / a.nparts;
         }
         qf[i] = v;
         qz[i] = make_float2(cqv, __int_as_float(o));
         cnt_l[i] = 0;
-        flr_l[i] = 0u;
       }
       if (tid == 0) {
         eb_n = 0;
@@ -336,18 +336,8 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
 #pragma unroll
       for (int s = 0; s < KS; ++s) B[s] = *reinterpret_cast<const h8v *>(bp + s * 1024);
     };
-    // a row of the candidate region of query slot qi (slot from its LDS counter; a full region keeps the
-    // best score it had to drop as its floor)
-    auto put = [&](int qi, float sc, int row) {
-      const int slot = atomicAdd(&cnt_l[qi], 1);
-      if (slot < a.cap) {
-        const size_t rb = (size_t)__float_as_int(qz[qi].y) * a.cap;
-        a.cand_s[rb + slot] = sc;
-        a.cand_k[rb + slot] = a.key_base | (uint32_t)row;
-      } else {
-        atomicMax(&flr_l[qi], score_key(sc));
-      }
-    };
+    // a row straight to query slot qi's buffer (staging full, or an item of 2^23+ rows)
+    auto put = [&](int qi, float sc, int row) { cand_put(a, __float_as_int(qz[qi].y), sc, a.key_base | (uint32_t)row); };
     // the rare emit branch: per row position e a wave-uniform test (one compare, a scalar branch)
     auto emit_y = [&](const f16v &y, float thr, int qi, int rt) {
       const float cq = qz[qi].x;
@@ -475,16 +465,7 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
     stamp(1);
     __syncthreads();
     stamp(2);
-    for (int i = tid, n = min(eb_n, EB); i < n; i += 64 * NW) {  // the staged rows
-      const uint2 e = eb[i];
-      put((int)(e.y >> 23), __uint_as_float(e.x), r0 + (int)(e.y & 0x7FFFFFu));
-    }
-    __syncthreads();
-    for (int i = tid; i < qcnt; i += 64 * NW) {
-      const int o = __float_as_int(qz[i].y);
-      a.cand_n[o] = min(cnt_l[i], a.cap);
-      a.cand_f[o] = flr_l[i];
-    }
+    cand_flush<64 * NW>(a, eb, min(eb_n, EB), qcnt, r0, cnt_l, base_l, [&](int i) { return __float_as_int(qz[i].y); });
     stamp(3);
   }
 }
