@@ -188,11 +188,11 @@ def test_flat_filter_respects_max_scans_and_deletes(hiplib, oracle):
 
 @pytest.mark.parametrize("metric", [0, 1])
 @pytest.mark.parametrize("scale", [1e-3, 1.0, 1e3])
-def test_bf16x3_near_duplicates_and_wide_range(hiplib, metric, scale):
-    """Rows that differ far below one bf16 ulp (clusters of near-duplicates, signed values,
-    magnitudes from 1e-3 to 1e3): the bf16x3 approximation cannot separate them, so its
-    certificate must fail rather than pass a wrong top-k -- results stay bit-identical to
-    the exact scan whatever the certificate decides."""
+def test_near_duplicates_and_wide_range(hiplib, metric, scale):
+    """Rows that differ far below one fp16 ulp (clusters of near-duplicates, signed values,
+    magnitudes from 1e-3 to 1e3): the fp16 tiles cannot separate them, so the certificate must
+    fail rather than pass a wrong top-k -- results stay bit-identical to the exact scan whatever
+    the certificate decides."""
     rng = np.random.default_rng(5)
     base = rng.standard_normal((150, 128)).astype(np.float32)
     x = (np.repeat(base, 40, axis=0) * (1 + 1e-6 * rng.standard_normal((6000, 128)))).astype(np.float32)
