@@ -273,6 +273,69 @@ __global__ __launch_bounds__(64) void coarse_approx_kernel(const float *q, const
   }
 }
 
+// The same approximate scores with both tiles staged in LDS: a 256-thread block computes 64 queries x 64
+// centroids (wave w: the 32 x 32 quadrant (w & 1, w >> 1)), the rows arriving as coalesced 512-B row
+// loads, KT = 64 dims at a time (34 KB of LDS: four blocks per CU), in a row stride of KT + 4 floats (the 16 rows a 16-lane group of
+// ds_read_b128 touches start 4 banks apart: conflict-free).  Each wave then issues exactly the MFMA
+// sequence of coarse_approx_kernel (same operands, same k order), so the approximate scores are the same
+// bits; the tiles cross L2 once per block instead of once per wave, as whole rows.
+constexpr int AKT = 64, AKS = AKT + 4;
+template <int MET>
+__global__ __launch_bounds__(256) void coarse_approx_lds_kernel(const float *q, const float *c, const float *c2,
+                                                                int64_t nq, int nc, int D, float *out) {
+  __shared__ __attribute__((aligned(16))) float qs[64 * AKS], cs[64 * AKS];
+  const int64_t q0 = (int64_t)blockIdx.y * 64;
+  const int c0 = blockIdx.x * 64;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, r = l & 15, h = l >> 4;
+  const int wq = 32 * (w & 1), wc = 32 * (w >> 1);
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  f4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+  for (int d0 = 0; d0 < D; d0 += AKT) {
+    const int kt = min(AKT, D - d0), k4 = kt / 4;
+    __syncthreads();  // the previous chunk is consumed
+    for (int e = tid; e < 64 * k4; e += 256) {
+      const int row = e / k4, col = 4 * (e - row * k4);
+      const float4 qv = *reinterpret_cast<const float4 *>(q + (size_t)min(q0 + row, nq - 1) * D + d0 + col);
+      const float4 cv = *reinterpret_cast<const float4 *>(c + (size_t)min(c0 + row, nc - 1) * D + d0 + col);
+      *reinterpret_cast<float4 *>(qs + row * AKS + col) = qv;
+      *reinterpret_cast<float4 *>(cs + row * AKS + col) = cv;
+    }
+    __syncthreads();
+    const float *qa[2] = {qs + (wq + r) * AKS + 4 * h, qs + (wq + 16 + r) * AKS + 4 * h};
+    const float *cb[2] = {cs + (wc + r) * AKS + 4 * h, cs + (wc + 16 + r) * AKS + 4 * h};
+#pragma unroll 2
+    for (int s = 0; s < kt / 16; ++s) {
+      const float4 a0 = *reinterpret_cast<const float4 *>(qa[0] + 16 * s), a1 = *reinterpret_cast<const float4 *>(qa[1] + 16 * s);
+      const float4 b0 = *reinterpret_cast<const float4 *>(cb[0] + 16 * s), b1 = *reinterpret_cast<const float4 *>(cb[1] + 16 * s);
+      const float av[2][4] = {{a0.x, a0.y, a0.z, a0.w}, {a1.x, a1.y, a1.z, a1.w}};
+      const float bv[2][4] = {{b0.x, b0.y, b0.z, b0.w}, {b1.x, b1.y, b1.z, b1.w}};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int t = 0; t < 2; ++t) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i][j], bv[t][j], acc[i][t], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int ci = c0 + wc + 16 * t + r;
+    if (ci >= nc) continue;
+    const float cc = MET == L2 ? c2[ci] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int64_t qi = q0 + wq + 16 * i + 4 * h + g;
+        if (qi < nq) out[qi * nc + ci] = MET == L2 ? 2.0f * acc[i][t][g] - cc : acc[i][t][g];
+      }
+  }
+}
+
 // ComputeScore (safe VectorMath form, as coarse_scores_kernel) spread over an 8-lane group: lane j runs
 // accumulator j over dims j, j + 8, ...; the group sums as hsum8 does; every lane returns the score
 template <int MET, int DT = 0>
@@ -505,9 +568,16 @@ void launch_coarse_mfma(const float *q, const float *cents_rm, const float *c2, 
   const int P = std::min(nprobe, nlist);
   const dim3 ga((unsigned)((nlist + 31) / 32), (unsigned)((nq + 31) / 32));
   const dim3 g4((unsigned)((nq + 3) / 4));
+  // PYR_COARSE_APPROX=0: the one-wave-per-tile kernel (A/B; the same approximate scores)
+  const char *ae = getenv("PYR_COARSE_APPROX");
+  const bool lds = !(ae && atoi(ae) == 0);
+  const dim3 gl((unsigned)((nlist + 63) / 64), (unsigned)((nq + 63) / 64));
   auto go = [&](auto met, auto dt) {
     constexpr int M = decltype(met)::value, DT = decltype(dt)::value;
-    hipLaunchKernelGGL((coarse_approx_kernel<M, DT>), ga, dim3(64), 0, st, q, cents_rm, c2, nq, nlist, dim, scores);
+    if (lds)
+      hipLaunchKernelGGL((coarse_approx_lds_kernel<M>), gl, dim3(256), 0, st, q, cents_rm, c2, nq, nlist, dim, scores);
+    else
+      hipLaunchKernelGGL((coarse_approx_kernel<M, DT>), ga, dim3(64), 0, st, q, cents_rm, c2, nq, nlist, dim, scores);
     (void)hipMemsetAsync(nfail, 0, sizeof(int32_t), st);
     hipLaunchKernelGGL((coarse_pick_kernel<M, DT>), g4, dim3(256), 0, st, q, cents_rm, scores, nq, nlist, dim, P, cnmax,
                        c_err, probes, fail, nfail);
