@@ -143,25 +143,37 @@ void RowStore::encode16(const int64_t *d_slots, int64_t cnt, hipStream_t st) {
 }
 
 void RowStore::write(const float *x, const int64_t *slots, const int64_t *labs, int64_t cnt, hipStream_t st,
-                     DevMem &stage_x, DevMem &stage_i) {
+                     DevMem &stage_x, DevMem &stage_i, bool x_dev) {
   if (cnt <= 0) return;
   ++gen;
   const size_t xb = sizeof(float) * cnt * dim;
-  stage_x.ensure(xb);
   stage_i.ensure(sizeof(int64_t) * cnt * 2);
   int64_t *di = stage_i.as<int64_t>();
-  HIPCHK(hipMemcpyAsync(stage_x.p, x, xb, hipMemcpyHostToDevice, st));
+  const float *src = x;
+  if (!x_dev) {
+    stage_x.ensure(xb);
+    HIPCHK(hipMemcpyAsync(stage_x.p, x, xb, hipMemcpyHostToDevice, st));
+    src = stage_x.as<float>();
+  }
   HIPCHK(hipMemcpyAsync(di, slots, sizeof(int64_t) * cnt, hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(di + cnt, labs, sizeof(int64_t) * cnt, hipMemcpyHostToDevice, st));
-  launch_scatter_blocked(stage_x.as<float>(), di, cnt, dim, rows.as<float>(), st);
-  if (f16) launch_scatter_rowmajor(stage_x.as<float>(), di, cnt, dim, rrm.as<float>(), st);
+  launch_scatter_blocked(src, di, cnt, dim, rows.as<float>(), st);
+  if (f16) launch_scatter_rowmajor(src, di, cnt, dim, rrm.as<float>(), st);
   launch_scatter_i64(labels.as<int64_t>(), di, di + cnt, cnt, st);
   launch_scatter_u8(live.as<uint8_t>(), di, 1, cnt, st);
   if (cosine) launch_norms_slots(rows.as<float>(), di, cnt, dim, norms.as<float>(), st);
   launch_sqnorms(rows.as<float>(), di, cnt, dim, rsq.as<float>(), rmax.as<uint32_t>(), st);
   HIPCHK(hipGetLastError());
   if (f16 && center16 && !resid) {
-    // the first rows written fix the center: their mean (finite values), computed on the host
+    // the first rows written fix the center: their mean (finite values), computed on the host (a device
+    // source is read back once, for this first write only)
+    std::vector<float> xh;
+    if (x_dev) {
+      xh.resize((size_t)cnt * dim);
+      HIPCHK(hipMemcpyAsync(xh.data(), x, xb, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      x = xh.data();
+    }
     std::vector<double> acc(dim, 0.0);
     std::vector<int64_t> num(dim, 0);
     for (int64_t i = 0; i < cnt; i++)
@@ -738,18 +750,16 @@ struct FlatIndex : Index {
     stage_b.ensure(sizeof(float) * n * dim);
     launch_unit_rows(st.rows.as<float>(), stage_i.as<int64_t>(), st.norms.as<float>(), n, dim, stage_b.as<float>(),
                      wst, zflag.as<uint32_t>());
-    std::vector<float> xu((size_t)n * dim);
-    HIPCHK(hipMemcpyAsync(xu.data(), stage_b.p, sizeof(float) * xu.size(), hipMemcpyDeviceToHost, wst));
-    HIPCHK(hipStreamSynchronize(wst));
-    // straight into the unit store at the same slots (labels = slots): a batch with a repeated id keeps
-    // its rows out of slot order, so the unit index's own append order could differ
+    // straight from stage_b into the unit store at the same slots (labels = slots), all on wst (no host
+    // hop; write() synchronizes wst at its end): a batch with a repeated id keeps its rows out of slot
+    // order, so the unit index's own append order could differ
     FlatIndex &u = *unit;
     int64_t next = u.st.n;
     for (int64_t s : slots) next = std::max(next, s + 1);
-    u.st.reserve(next, u.wst);
+    u.st.reserve(next, wst);
     u.st.hlabels.resize(next, -1);
     u.st.hlive.resize(next, 0);
-    u.st.write(xu.data(), slots.data(), slots.data(), n, u.wst, u.stage_x, u.stage_i);
+    u.st.write(stage_b.as<float>(), slots.data(), slots.data(), n, wst, u.stage_x, u.stage_i, true);
     for (int64_t s : slots) {
       u.st.hlabels[s] = s;
       u.st.hlive[s] = 1;

@@ -98,9 +98,10 @@ struct RowStore {
   std::vector<int64_t> hlabels;
   std::vector<uint8_t> hlive;
   void reserve(int64_t slots, hipStream_t st);
-  // write rows (host row-major x, n rows) into slots; updates labels/live/norms
+  // write rows (row-major x, n rows: host memory, or device memory when x_dev) into slots; updates
+  // labels/live/norms.  A device source is read in place (no staging copy, no host hop)
   void write(const float *x, const int64_t *slots, const int64_t *labs, int64_t cnt, hipStream_t st,
-             DevMem &stage_x, DevMem &stage_i);
+             DevMem &stage_x, DevMem &stage_i, bool x_dev = false);
   void set_live(const std::vector<int64_t> &slots, uint8_t v, hipStream_t st, DevMem &stage);
   // fp16 copy of slots (device list, or [0, cap) when null) with the current scale; raises the
   // scale (and re-encodes every slot) when a row exceeds it.  Synchronizes st.
