@@ -43,20 +43,26 @@ __device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf
 
 // ---- 1. query operands per (list, query) pair ----
 // A lane group of D / 8 lanes per query (8 dims a lane, the centroid's 8 dims held in registers for
-// the whole list), 64 / (D / 8) queries per wave at a time.
+// the whole list), 64 / (D / 8) queries per wave at a time.  An item's queries are split over
+// SPREP_SPLIT(D) blocks (block s takes every SPLIT-th run of 4 x QW queries): each wave's loop is a chain
+// of dependent loads (position -> query row), so more waves with fewer turns each hide its latency.
+template <int D>
+constexpr int SPREP_SPLIT = D / 16;
 template <int D, int MET>
 __global__ __launch_bounds__(256) void sprep_kernel(StreamArgs a) {
-  const int item = blockIdx.x;
+  constexpr int SPLIT = SPREP_SPLIT<D>;
+  const int item = blockIdx.x / SPLIT, part = blockIdx.x - item * SPLIT;
   if (item >= *a.n_items) return;
   const ScanItem it = a.items[item];
   if (it.part != 0) return;  // chunk-0 items cover every qlist position of their list once
   // (a bounded grid walking 64-item windows of chunk-0 items measured slower: 0.165 vs 0.146 ms, r4g)
   constexpr int LQ = D / 8, QW = 64 / LQ;
+  if (4 * QW * part >= it.qcnt) return;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, sub = lane % LQ, qsl = lane / LQ;
   const float4 *cp = reinterpret_cast<const float4 *>(a.cents + (size_t)it.list * D + 8 * sub);
   const float4 c0 = cp[0], c1 = cp[1];
   const float cv[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-  for (int qi0 = QW * w; qi0 < it.qcnt; qi0 += 4 * QW) {
+  for (int qi0 = QW * w + 4 * QW * part; qi0 < it.qcnt; qi0 += 4 * QW * SPLIT) {
     const int qi = qi0 + qsl;
     const bool act = qi < it.qcnt;
     const int pos = it.qbeg + (act ? qi : 0);
@@ -358,7 +364,8 @@ bool sample16_supported(int dim, int metric) { return (metric == L2 || metric ==
 
 void launch_sample16(const StreamArgs &a, int metric, int max_items, hipStream_t st) {
   if (max_items <= 0) return;
-  auto prep = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(max_items), dim3(256), 0, st, a); };
+  const int split = a.dim == 32 ? SPREP_SPLIT<32> : a.dim == 64 ? SPREP_SPLIT<64> : SPREP_SPLIT<128>;
+  auto prep = [&](auto kern) { hipLaunchKernelGGL(kern, dim3((unsigned)((int64_t)max_items * split)), dim3(256), 0, st, a); };
   const dim3 grid(std::max(1, std::min(max_items, device_cus())));
   auto samp = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(64 * SNW), 0, st, a); };
   switch (a.dim) {
