@@ -163,11 +163,17 @@ def run(args):
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # PYR_BENCH_REHEARSE=1 (rehearsal only, never a reported line): every rank on cuda:0 over gloo, so the
+    # N > 1 step runs end to end on a one-GPU box (RCCL refuses two ranks on one device)
+    rehearse = world > 1 and os.environ.get("PYR_BENCH_REHEARSE") == "1"
+    local = 0 if rehearse else int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from pyrope_amd import (BruteForceVectorIndex, IvfFlatVectorIndex, VectorMetric, _lib, generate_synthetic,
                             generate_synthetic_blocked, kmeans_train)
@@ -463,7 +469,8 @@ def run(args):
             "unit": "queries/s",
             "n_gpus": world,
             "ranks_seen": dist.get_world_size() if world > 1 else 1,
-            "backend": dist.get_backend() + " (RCCL)" if world > 1 else None,
+            "backend": (dist.get_backend() + (" (RCCL)" if dist.get_backend() == "nccl" else " (rehearsal: one GPU)"))
+                       if world > 1 else None,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
