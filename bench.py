@@ -55,10 +55,7 @@ def log(*a):
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # 100 steps (~0.13 s timed): the timed region carries a fixed ~1.5 ms (the first replay after the
-    # synchronize, the clock), 6 % of a 20-step region: 20 steps 26.7 ms, 100 steps 127.4 ms -> 1.259 ms
-    # per step + 1.55 ms (profiles/r4_scan/steps_20_vs_100.log)
-    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=10_000_000)
     ap.add_argument("--dim", type=int, default=128)
@@ -291,8 +288,16 @@ def run(args):
         with torch.cuda.graph(graph, stream=gst):
             step()
         torch.cuda.synchronize()
-        for _ in range(max(1, args.warmup)):
+        # untimed replays: at least W, and for at least 50 ms -- the capture leaves the GPU idle for ~15 ms and
+        # its clocks then take ~10 steps to return (the first timed replays of a 20-step region ran 1.5-1.7 ms
+        # instead of 1.25 ms, profiles/r5_start/kt20_steps.txt)
+        t_w = time.perf_counter()
+        n_w = 0
+        while n_w < max(1, args.warmup) or time.perf_counter() - t_w < 0.05:
             graph.replay()
+            n_w += 1
+            if n_w % 8 == 0:
+                torch.cuda.synchronize()
         torch.cuda.synchronize()
         timed_step = graph.replay
     barrier()
@@ -304,6 +309,19 @@ def run(args):
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    # the timed replays' answer (the last replay's results) against a plain kernel-by-kernel search of the same
+    # batch: bit-identical, so the graph replays computed the search (DESIGN.md §4 "hipGraph replays")
+    graph_check = None
+    if graph is not None:
+        g_s, g_l = s_loc.clone(), l_loc.clone()
+        s_loc.fill_(0.0)
+        l_loc.fill_(-7)
+        step()
+        torch.cuda.synchronize()
+        graph_check = {"replays": args.steps + n_w, "untimed_replays": n_w,
+                       "last_replay_equals_direct_search": bool(torch.equal(g_l, l_loc)) and
+                       bool(torch.equal(g_s.view(torch.int32), s_loc.view(torch.int32)))}
+        log(f"graph replay vs direct search: {graph_check}")
     if world > 1:
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -516,6 +534,7 @@ def run(args):
                                 "note": "SURVEY.md 8(d): nprobe/nlist x N x D x 4 + nlist x D x 4 per query (no "
                                         "batching reuse); not a roofline"},
             "launch": "hipGraph replay of the whole search per step" if graph is not None else "kernel launches",
+            "graph_check": graph_check,
             "phases_ms": {k_: round(v["ms"], 4) for k_, v in phases.items()},
             "collective_ms": {k_: round(v, 4) for k_, v in coll.items()} if world > 1 else None,
             "rank_rows": rank_rows,

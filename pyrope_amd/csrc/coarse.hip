@@ -228,7 +228,8 @@ __global__ __launch_bounds__(256) void coarse_select_reg_kernel(const float *sco
 // 3. coarse_select_list_kernel: the dense exact ranking of the queries the pick could not settle.
 template <int MET, int DT>
 __global__ __launch_bounds__(64) void coarse_approx_kernel(const float *q, const float *c, const float *c2, int64_t nq,
-                                                           int nc, int Dr, float *out) {
+                                                           int nc, int Dr, float *out, int32_t *zero) {
+  if (zero && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *zero = 0;  // the pick's failure count
   const int D = DT > 0 ? DT : Dr;  // a compile-time D unrolls the loop: every operand load is issued up front
   constexpr int UNS = DT > 0 ? DT / 16 : 1;
   const int64_t q0 = (int64_t)blockIdx.y * 32;
@@ -282,8 +283,9 @@ __global__ __launch_bounds__(64) void coarse_approx_kernel(const float *q, const
 constexpr int AKT = 64, AKS = AKT + 4;
 template <int MET>
 __global__ __launch_bounds__(256) void coarse_approx_lds_kernel(const float *q, const float *c, const float *c2,
-                                                                int64_t nq, int nc, int D, float *out) {
+                                                                int64_t nq, int nc, int D, float *out, int32_t *zero) {
   __shared__ __attribute__((aligned(16))) float qs[64 * AKS], cs[64 * AKS];
+  if (zero && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *zero = 0;  // the pick's failure count
   const int64_t q0 = (int64_t)blockIdx.y * 64;
   const int c0 = blockIdx.x * 64;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, r = l & 15, h = l >> 4;
@@ -574,11 +576,15 @@ void launch_coarse_mfma(const float *q, const float *cents_rm, const float *c2, 
   const dim3 gl((unsigned)((nlist + 63) / 64), (unsigned)((nq + 63) / 64));
   auto go = [&](auto met, auto dt) {
     constexpr int M = decltype(met)::value, DT = decltype(dt)::value;
+    // the approximate-score kernel also zeroes the pick's failure count (no hipMemsetAsync on a search path:
+    // the memset nodes of a captured graph write stale values from their second replay on,
+    // scripts/diag/graph_memset.py)
     if (lds)
-      hipLaunchKernelGGL((coarse_approx_lds_kernel<M>), gl, dim3(256), 0, st, q, cents_rm, c2, nq, nlist, dim, scores);
+      hipLaunchKernelGGL((coarse_approx_lds_kernel<M>), gl, dim3(256), 0, st, q, cents_rm, c2, nq, nlist, dim, scores,
+                         nfail);
     else
-      hipLaunchKernelGGL((coarse_approx_kernel<M, DT>), ga, dim3(64), 0, st, q, cents_rm, c2, nq, nlist, dim, scores);
-    (void)hipMemsetAsync(nfail, 0, sizeof(int32_t), st);
+      hipLaunchKernelGGL((coarse_approx_kernel<M, DT>), ga, dim3(64), 0, st, q, cents_rm, c2, nq, nlist, dim, scores,
+                         nfail);
     hipLaunchKernelGGL((coarse_pick_kernel<M, DT>), g4, dim3(256), 0, st, q, cents_rm, scores, nq, nlist, dim, P, cnmax,
                        c_err, probes, fail, nfail);
   };

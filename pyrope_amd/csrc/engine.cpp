@@ -20,9 +20,25 @@ namespace pyr {
 // ---------------------------------------------------------------------------
 // memory
 // ---------------------------------------------------------------------------
+// diagnostics only (PYR_DEBUG_ALLOC=<file>): every device allocation and free of the library appended to
+// the file, so that the address of a GPU memory fault can be matched to the buffer it falls in
+static void alloc_log(const char *what, const void *p, size_t n) {
+  static const char *path = getenv("PYR_DEBUG_ALLOC");
+  if (!path || !*path) return;
+  static std::mutex mu;
+  std::lock_guard<std::mutex> g(mu);
+  if (FILE *f = fopen(path, "a")) {
+    fprintf(f, "%s %p %zu\n", what, p, n);
+    fclose(f);
+  }
+}
+
 void DevMem::ensure(size_t bytes) {
   if (bytes <= n && p) return;
-  if (p) HIPCHK(hipFree(p));
+  if (p) {
+    alloc_log("free", p, n);
+    HIPCHK(hipFree(p));
+  }
   p = nullptr;
   n = 0;
   size_t want = std::max<size_t>(bytes, 256);
@@ -30,6 +46,7 @@ void DevMem::ensure(size_t bytes) {
     p = nullptr;
     throw Error(PYR_E_OOM, "device allocation of " + std::to_string(want) + " bytes failed");
   }
+  alloc_log("alloc", p, want);
   n = want;
 }
 
@@ -38,11 +55,24 @@ void DevMem::grow_keep(size_t bytes, size_t keep, hipStream_t st) {
   void *q = nullptr;
   size_t want = std::max<size_t>(bytes, 256);
   if (hipMalloc(&q, want) != hipSuccess) throw Error(PYR_E_OOM, "device allocation of " + std::to_string(want) + " bytes failed");
+  alloc_log("alloc", q, want);
   if (p && keep) HIPCHK(hipMemcpyAsync(q, p, std::min(keep, n), hipMemcpyDeviceToDevice, st));
   HIPCHK(hipStreamSynchronize(st));
-  if (p) HIPCHK(hipFree(p));
+  if (p) {
+    alloc_log("free", p, n);
+    HIPCHK(hipFree(p));
+  }
   p = q;
   n = want;
+}
+
+void DevMem::release() {
+  if (p) {
+    alloc_log("free", p, n);
+    (void)hipFree(p);
+  }
+  p = nullptr;
+  n = 0;
 }
 
 static int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
@@ -400,8 +430,34 @@ static bool bounds_enabled() {
 static uint32_t *shared_bounds(Workspace &ws, int64_t nq) {
   if (!bounds_enabled() || nq <= 0) return nullptr;
   ws.gthr.ensure(sizeof(uint32_t) * nq);
-  HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ws.gthr.p), (int)score_key(-INFINITY), nq, ws.st));
+  WordFill z;
+  z.add(ws.gthr.p, nq, score_key(-INFINITY));
+  launch_fill_words(z, ws.st);
   return ws.gthr.as<uint32_t>();
+}
+
+// The per-slice counters of a stream search (work-list histograms, candidate counts and floors, the
+// persistent-block item counters, the two certificate failure counts) reset by ONE kernel (WordFill).  A
+// search must stay capturable into a hipGraph and replayable: hipMemsetAsync nodes of a captured graph
+// write stale values from its second replay on in the HIP runtime PyTorch ships, which is what faulted the
+// second replay of a captured FLAT search (scripts/diag/graph_memset.py; DESIGN.md §4 "hipGraph replays").
+static void reset_stream_counters(Workspace &ws, int64_t nq, int nlist) {
+  ws.ivf_cnt.ensure(sizeof(int32_t) * std::max(nlist, 1));
+  ws.ivf_fill.ensure(sizeof(int32_t) * std::max(nlist, 1));
+  ws.scn.ensure(sizeof(int32_t) * std::max<int64_t>(nq, 1));
+  ws.scf.ensure(sizeof(uint32_t) * std::max<int64_t>(nq, 1));
+  ws.swork.ensure(sizeof(int32_t) * 2);
+  ws.fail_cnt.ensure(sizeof(int32_t));
+  ws.fail_cnt2.ensure(sizeof(int32_t));
+  WordFill z;
+  z.add(ws.ivf_cnt.p, nlist, 0);
+  z.add(ws.ivf_fill.p, nlist, 0);
+  z.add(ws.scn.p, nq, 0);
+  z.add(ws.scf.p, nq, 0);
+  z.add(ws.swork.p, 2, 0);
+  z.add(ws.fail_cnt.p, 1, 0);
+  z.add(ws.fail_cnt2.p, 1, 0);
+  launch_fill_words(z, ws.st);
 }
 
 // IVF-PQ LUT list scan kernel: 2 = pq_adc4 (default), 0 = the first-cut pq_scan (PYR_PQ_ADC=0; A/B
@@ -705,7 +761,8 @@ static int64_t read_rows(ImageReader &r, uint32_t tag_labels, uint32_t tag_rows,
 // FLAT = BruteForceVectorIndex (BruteForceVectorIndex.cs)
 // ---------------------------------------------------------------------------
 static int build_ivf_items(Workspace &ws, int64_t nq, int nprobe, int nparts, int nlist, const DevMem &lbeg,
-                           const DevMem &lend, int qchunk, IvfChunking ch, int phase = 0, bool balance = false);
+                           const DevMem &lend, int qchunk, IvfChunking ch, int phase = 0, bool balance = false,
+                           bool zeroed = false);
 
 struct FlatIndex : Index {
   RowStore st;
@@ -1000,13 +1057,14 @@ struct FlatIndex : Index {
                     float *d_s, int64_t *d_l, int32_t *d_c, Workspace &ws, const CosRefine *cr = nullptr) {
     const int probes = nch;
     const IvfChunking ch{(int32_t)flat_chunk_rows(cutoff), 1, 0};
+    reset_stream_counters(ws, nq, nch);
     ws.probes.ensure(sizeof(int32_t) * nq * probes);
     launch_iota_rows(ws.probes.as<int32_t>(), nq, probes, ws.st);
     DevMem &lbd = ws.vlb, &led = ws.vle;
     int maxi;
     {
       PhaseTimer t(PH_ITEMS, ws.st);
-      maxi = build_ivf_items(ws, nq, probes, nparts, nch, lbd, led, scan_qmax(st.tdim()), ch, 0, true);
+      maxi = build_ivf_items(ws, nq, probes, nparts, nch, lbd, led, scan_qmax(st.tdim()), ch, 0, true, true);
     }
     const int64_t npos = nq * probes;
     const int sv = scan_sample_values();
@@ -1018,9 +1076,6 @@ struct FlatIndex : Index {
     ws.scn.ensure(sizeof(int32_t) * std::max<int64_t>(nq, 1));
     ws.scf.ensure(sizeof(uint32_t) * std::max<int64_t>(nq, 1));
     ws.swork.ensure(sizeof(int32_t) * 2);
-    HIPCHK(hipMemsetAsync(ws.scn.p, 0, sizeof(int32_t) * nq, ws.st));
-    HIPCHK(hipMemsetAsync(ws.scf.p, 0, sizeof(uint32_t) * nq, ws.st));
-    HIPCHK(hipMemsetAsync(ws.swork.p, 0, sizeof(int32_t) * 2, ws.st));
     StreamArgs sa{};
     sa.h16 = st.h16.p;
     sa.meta = st.meta.as<float>();
@@ -1094,8 +1149,6 @@ struct FlatIndex : Index {
     ws.fail2.ensure(sizeof(int32_t) * nq);
     ws.fail_cnt.ensure(sizeof(int32_t));
     ws.fail_cnt2.ensure(sizeof(int32_t));
-    HIPCHK(hipMemsetAsync(ws.fail_cnt.p, 0, sizeof(int32_t), ws.st));
-    HIPCHK(hipMemsetAsync(ws.fail_cnt2.p, 0, sizeof(int32_t), ws.st));
     RefineArgs r{};
     r.rows = st.rows.as<float>();
     r.rows_rm = st.rrm.as<float>();
@@ -1406,8 +1459,7 @@ struct Coarse {
     if (ws.ext_probes) {  // ranked by the caller (pyr_index_search_probed_device)
       if (ws.ext_nprobe != nprobe) throw Error(PYR_E_ARG, "probe lists have the wrong width for this nprobe");
       ws.probes.ensure(sizeof(int32_t) * nq * nprobe);
-      HIPCHK(hipMemcpyAsync(ws.probes.p, ws.ext_probes, sizeof(int32_t) * nq * nprobe, hipMemcpyDeviceToDevice,
-                            ws.st));
+      launch_copy_words(ws.probes.p, ws.ext_probes, nq * nprobe, ws.st);
       return;
     }
     // the matrix-core ranking (PYR_COARSE_MFMA=0: the dense exact ranking below; same probes)
@@ -1477,7 +1529,7 @@ static int64_t probed_rows(Workspace &ws, int64_t nq, int probes, const std::vec
 // list-major work items from ws.probes
 // phase 0 -> ws.items / ws.nitems, phase 1 -> ws.items3 / ws.nitems3 (IvfChunking, kernels.h)
 static int build_ivf_items(Workspace &ws, int64_t nq, int nprobe, int nparts, int nlist, const DevMem &lbeg,
-                           const DevMem &lend, int qchunk, IvfChunking ch, int phase, bool balance) {
+                           const DevMem &lend, int qchunk, IvfChunking ch, int phase, bool balance, bool zeroed) {
   const int64_t maxi64 = ivf_max_items(nq, nprobe, nlist, qchunk, ch, phase);
   if (maxi64 > INT32_MAX) throw Error(PYR_E_ARG, "query batch too large for one launch");
   const int maxi = (int)maxi64;
@@ -1493,7 +1545,7 @@ static int build_ivf_items(Workspace &ws, int64_t nq, int nprobe, int nparts, in
   IvfItemWs iw{ws.ivf_cnt.as<int32_t>(), ws.ivf_fill.as<int32_t>(), ws.ivf_qoff.as<int32_t>(),
                ws.ivf_ioff.as<int32_t>(), ws.qlist.as<int32_t>(), items.as<ScanItem>(), nitems.as<int32_t>()};
   launch_ivf_items(ws.probes.as<int32_t>(), nq, nprobe, nparts, nlist, lbeg.as<int32_t>(), lend.as<int32_t>(), qchunk,
-                   ch, phase, iw, ws.st, 0, -1, balance);
+                   ch, phase, iw, ws.st, 0, -1, balance, zeroed);
   return maxi;
 }
 
@@ -1969,6 +2021,7 @@ struct IvfFlatIndex : Index {
                     float *d_s, int64_t *d_l, int32_t *d_c, Workspace &ws) {
     const bool cosine = metric == COS;
     const int met = cosine ? L2 : metric;  // Cosine: L2 over the unit vectors (commit_lists)
+    reset_stream_counters(ws, nq, coarse.nlist);
     if (cosine) {
       ws.qn.ensure(sizeof(float) * std::max<int64_t>(nq, 1));
       launch_norms(d_q, nq, dim, 0, ws.qn.as<float>(), ws.st);  // VectorMath.ComputeNorm (:167)
@@ -1988,7 +2041,7 @@ struct IvfFlatIndex : Index {
     int maxi;
     {
       PhaseTimer t(PH_ITEMS, ws.st);
-      maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qmax, ch, 0, true);
+      maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qmax, ch, 0, true, true);
     }
     const int64_t npos = nq * probes;
     const int sv = scan_sample_values();
@@ -2000,9 +2053,6 @@ struct IvfFlatIndex : Index {
     ws.scn.ensure(sizeof(int32_t) * std::max<int64_t>(nq, 1));
     ws.scf.ensure(sizeof(uint32_t) * std::max<int64_t>(nq, 1));
     ws.swork.ensure(sizeof(int32_t) * 2);
-    HIPCHK(hipMemsetAsync(ws.scn.p, 0, sizeof(int32_t) * nq, ws.st));
-    HIPCHK(hipMemsetAsync(ws.scf.p, 0, sizeof(uint32_t) * nq, ws.st));
-    HIPCHK(hipMemsetAsync(ws.swork.p, 0, sizeof(int32_t) * 2, ws.st));
     StreamArgs sa{};
     sa.h16 = lists.h16.p;
     sa.meta = lists.meta.as<float>();
@@ -2040,7 +2090,9 @@ struct IvfFlatIndex : Index {
     const bool timing = getenv("PYR_STREAM_TIMING") != nullptr;  // measurement only (syncs)
     if (timing) {
       ws.tdbg.ensure(sizeof(unsigned long long) * 8);
-      HIPCHK(hipMemsetAsync(ws.tdbg.p, 0, sizeof(unsigned long long) * 8, ws.st));
+      WordFill z;
+      z.add(ws.tdbg.p, 16, 0);
+      launch_fill_words(z, ws.st);
     }
     {
       PhaseTimer t(PH_SAMPLE, ws.st);
@@ -2094,8 +2146,6 @@ struct IvfFlatIndex : Index {
     ws.fail2.ensure(sizeof(int32_t) * nq);
     ws.fail_cnt.ensure(sizeof(int32_t));
     ws.fail_cnt2.ensure(sizeof(int32_t));
-    HIPCHK(hipMemsetAsync(ws.fail_cnt.p, 0, sizeof(int32_t), ws.st));
-    HIPCHK(hipMemsetAsync(ws.fail_cnt2.p, 0, sizeof(int32_t), ws.st));
     RefineArgs r{};
     r.rows = lists.rows.as<float>();
     r.rows_rm = lists.f16 ? lists.rrm.as<float>() : nullptr;
@@ -2144,8 +2194,8 @@ struct IvfFlatIndex : Index {
         r.fail_cnt = ws.fail_cnt.as<int32_t>();
         launch_refine(r, met, 1, ws.st);
       } else {
-        HIPCHK(hipMemcpyAsync(ws.fail.p, ws.fail2.p, sizeof(int32_t) * nq, hipMemcpyDeviceToDevice, ws.st));
-        HIPCHK(hipMemcpyAsync(ws.fail_cnt.p, ws.fail_cnt2.p, sizeof(int32_t), hipMemcpyDeviceToDevice, ws.st));
+        launch_copy_words(ws.fail.p, ws.fail2.p, nq, ws.st);
+        launch_copy_words(ws.fail_cnt.p, ws.fail_cnt2.p, 1, ws.st);
       }
       HIPCHK(hipGetLastError());
     }
@@ -2195,7 +2245,7 @@ struct IvfFlatIndex : Index {
     if (probes == 0 || nq == 0) return probes;
     prep_queries(d_q, nq, dim, metric, ws);
     coarse.probe(d_q, metric == COS ? ws.qn.as<float>() : nullptr, nq, probes, metric, ws);
-    HIPCHK(hipMemcpyAsync(d_out, ws.probes.p, sizeof(int32_t) * nq * probes, hipMemcpyDeviceToDevice, ws.st));
+    launch_copy_words(d_out, ws.probes.p, nq * probes, ws.st);
     return probes;
   }
 
@@ -2679,7 +2729,9 @@ struct IvfPqIndex : Index {
     if (pmub_gen == pq_gen && pmub_kr == kr && pmub.n >= sizeof(float) * tot) return pmub.as<float>();
     pmeta.ensure(sizeof(float) * std::max<int64_t>(tot, 1));
     pmub.ensure(sizeof(float) * std::max<int64_t>(tot, 1));
-    HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(pmeta.p), (int)0xFF800000u, tot, ws.st));
+    WordFill z;
+    z.add(pmeta.p, tot, 0xFF800000u);  // -inf: not a row
+    launch_fill_words(z, ws.st);
     launch_pq32_meta(nrm.as<float>(), clive.as<uint8_t>(), ncode_rows, pmeta.as<float>(), ws.st);
     launch_row_terms(pmeta.as<float>(), nrm.as<float>(), nullptr, tot, L2, kr, 0.0f, pmub.as<float>(), ws.st);
     HIPCHK(hipGetLastError());
@@ -2716,6 +2768,7 @@ struct IvfPqIndex : Index {
 
   void pq32_slice(const float *d_q, int64_t nq, int k, int k1, int probes, IvfChunking ch, int nparts, int cap,
                   float *d_s, int64_t *d_l, int32_t *d_c, Workspace &ws) {
+    reset_stream_counters(ws, nq, coarse.nlist);
     {
       PhaseTimer t(PH_COARSE, ws.st, nq * coarse.nlist);
       prep_queries(d_q, nq, dim, metric, ws);
@@ -2724,7 +2777,7 @@ struct IvfPqIndex : Index {
     int maxi;
     {
       PhaseTimer t(PH_ITEMS, ws.st);
-      maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, pq32_qmax(), ch, 0, true);
+      maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, pq32_qmax(), ch, 0, true, true);
     }
     const int64_t npos = nq * probes;
     const int sv = pq32_sample_values();
@@ -2736,9 +2789,6 @@ struct IvfPqIndex : Index {
     ws.scn.ensure(sizeof(int32_t) * std::max<int64_t>(nq, 1));
     ws.scf.ensure(sizeof(uint32_t) * std::max<int64_t>(nq, 1));
     ws.swork.ensure(sizeof(int32_t) * 2);
-    HIPCHK(hipMemsetAsync(ws.scn.p, 0, sizeof(int32_t) * nq, ws.st));
-    HIPCHK(hipMemsetAsync(ws.scf.p, 0, sizeof(uint32_t) * nq, ws.st));
-    HIPCHK(hipMemsetAsync(ws.swork.p, 0, sizeof(int32_t) * 2, ws.st));
     StreamArgs sa{};
     sa.h16 = cpack.p;
     sa.queries = d_q;
@@ -2807,8 +2857,6 @@ struct IvfPqIndex : Index {
     ws.fail2.ensure(sizeof(int32_t) * nq);
     ws.fail_cnt.ensure(sizeof(int32_t));
     ws.fail_cnt2.ensure(sizeof(int32_t));
-    HIPCHK(hipMemsetAsync(ws.fail_cnt.p, 0, sizeof(int32_t), ws.st));
-    HIPCHK(hipMemsetAsync(ws.fail_cnt2.p, 0, sizeof(int32_t), ws.st));
     PqRefineArgs r{};
     r.queries = d_q;
     r.cents = coarse.rm.as<float>();

@@ -38,18 +38,12 @@ struct DevMem {
   DevMem() = default;
   DevMem(const DevMem &) = delete;
   DevMem &operator=(const DevMem &) = delete;
-  ~DevMem() {
-    if (p) (void)hipFree(p);
-  }
+  ~DevMem() { release(); }
   // make room for `bytes`; content discarded
   void ensure(size_t bytes);
   // make room for `bytes`; first `keep` bytes preserved (stream-ordered copy, then sync)
   void grow_keep(size_t bytes, size_t keep, hipStream_t st);
-  void release() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    n = 0;
-  }
+  void release();
   template <class T>
   T *as() const {
     return reinterpret_cast<T *>(p);

@@ -198,7 +198,8 @@ int64_t ivf_max_items(int64_t nq, int32_t nprobe, int32_t nlist, int32_t qchunk,
 void launch_ivf_items(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t nparts, int32_t nlist,
                       const int32_t *list_begin, const int32_t *list_end, int32_t qchunk, IvfChunking ch,
                       int phase, IvfItemWs &ws, hipStream_t st, int32_t pb = 0, int32_t pe = -1,
-                      bool balance = false);  // balance: a list's query groups of equal size (multiples of 16)
+                      bool balance = false,   // balance: a list's query groups of equal size (multiples of 16)
+                      bool zeroed = false);   // zeroed: ws.cnt / ws.fill already zero (the caller's WordFill)
 // IVF max_scans limits per (query, probe, chunk) slot (IvfFlatVectorIndex.cs:200-212)
 void launch_ivf_limits(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t nparts, int64_t remaining,
                        const int32_t *list_begin, const int32_t *list_end, const int32_t *list_live,
@@ -536,6 +537,22 @@ void sort_by_key(const int32_t *keys, int64_t n, int32_t k, int32_t *keys_tmp, i
                  int32_t *counts, int32_t *coff, void *temp, size_t temp_bytes, hipStream_t st);
 
 void fill_u8(uint8_t *p, uint8_t v, int64_t n, hipStream_t st);
+// Up to 8 ranges of 32-bit words set to a value each, in ONE kernel.  Every per-search counter reset goes
+// through it: hipMemsetAsync / hipMemsetD32Async captured into a hipGraph write stale values from the
+// graph's second replay on in the HIP runtime PyTorch ships (scripts/diag/graph_memset.py), and
+// one kernel node also replaces up to 8 fill nodes of ~5 us each.
+struct WordFill {
+  static constexpr int MAXR = 8;
+  uint32_t *p[MAXR] = {};
+  int64_t n[MAXR] = {};
+  uint32_t v[MAXR] = {};
+  int cnt = 0;
+  void add(void *ptr, int64_t words, uint32_t value);  // ignored when ptr is null or words <= 0
+};
+void launch_fill_words(const WordFill &f, hipStream_t st);
+// device-to-device copy of 32-bit words on a search path (a kernel, not a hipMemcpyAsync node: the same
+// graph-replay rule as WordFill)
+void launch_copy_words(void *dst, const void *src, int64_t words, hipStream_t st);
 void launch_scatter_i64(int64_t *dst, const int64_t *idx, const int64_t *vals, int64_t n, hipStream_t st);
 void launch_scatter_u8(uint8_t *dst, const int64_t *idx, uint8_t v, int64_t n, hipStream_t st);
 // norms of blocked rows at the given slots (VectorMath.ComputeNorm)

@@ -18,6 +18,7 @@
 #include <cmath>
 #include <algorithm>
 #include <cstdlib>
+#include <stdexcept>
 
 #include "kernels.h"
 
@@ -1230,6 +1231,24 @@ __global__ void kmeans_commit_kernel(float *cents, const float *tmp, const int32
   }
 }
 
+// up to WordFill::MAXR ranges of 32-bit words set to their value in one grid-stride launch (the
+// per-search counter resets: no hipMemsetAsync on a search path, see launch_fill_words)
+__global__ void fill_words_kernel(WordFill f) {
+  int64_t tot = 0;
+  for (int r = 0; r < f.cnt; ++r) tot += f.n[r];
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
+    int64_t o = e;
+    int r = 0;
+    while (o >= f.n[r]) o -= f.n[r++];
+    f.p[r][o] = f.v[r];
+  }
+}
+
+__global__ void copy_words_kernel(uint32_t *dst, const uint32_t *src, int64_t n) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x)
+    dst[e] = src[e];
+}
+
 __global__ void fill_u8_kernel(uint8_t *p, uint8_t v, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = v;
@@ -1572,14 +1591,18 @@ int64_t ivf_max_items(int64_t nq, int32_t nprobe, int32_t nlist, int32_t qchunk,
 
 void launch_ivf_items(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t nparts, int32_t nlist,
                       const int32_t *list_begin, const int32_t *list_end, int32_t qchunk, IvfChunking ch,
-                      int phase, IvfItemWs &ws, hipStream_t st, int32_t pb, int32_t pe, bool balance) {
+                      int phase, IvfItemWs &ws, hipStream_t st, int32_t pb, int32_t pe, bool balance, bool zeroed) {
   if (pe < 0) pe = nprobe;
   const int64_t n = nq * (pe - pb);
   const bool lds = nlist <= IVF_LDS_BINS && !getenv("PYR_IVF_GLOBAL_HIST");  // (knob: measurement only)
   const size_t hb = sizeof(int) * (size_t)nlist;
   if (phase == 0) {
-    (void)hipMemsetAsync(ws.cnt, 0, sizeof(int32_t) * nlist, st);
-    (void)hipMemsetAsync(ws.fill, 0, sizeof(int32_t) * nlist, st);
+    if (!zeroed) {
+      WordFill z;
+      z.add(ws.cnt, nlist, 0);
+      z.add(ws.fill, nlist, 0);
+      launch_fill_words(z, st);
+    }
     if (n > 0 && lds)
       hipLaunchKernelGGL(ivf_count_lds_kernel, dim3(nblk(n, IVF_EPB)), dim3(256), hb, st, probes, nq, nprobe, pb, pe,
                          nlist, ws.cnt);
@@ -1752,6 +1775,29 @@ void launch_fill_results(float *s, int64_t *l, int32_t *c, int64_t nq, int32_t k
   const int64_t n = nq * (k > 1 ? k : 1) > nq ? nq * (k > 1 ? k : 1) : nq;
   if (n <= 0) return;
   hipLaunchKernelGGL(fill_results_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, s, l, c, nq, k);
+}
+
+void WordFill::add(void *ptr, int64_t words, uint32_t value) {
+  if (!ptr || words <= 0) return;
+  if (cnt == MAXR) throw std::invalid_argument("WordFill: more than 8 ranges");
+  p[cnt] = static_cast<uint32_t *>(ptr);
+  n[cnt] = words;
+  v[cnt] = value;
+  ++cnt;
+}
+
+void launch_fill_words(const WordFill &f, hipStream_t st) {
+  int64_t tot = 0;
+  for (int r = 0; r < f.cnt; ++r) tot += f.n[r];
+  if (tot <= 0) return;
+  hipLaunchKernelGGL(fill_words_kernel, dim3((unsigned)std::min<int64_t>((tot + 255) / 256, 1024)), dim3(256), 0, st,
+                     f);
+}
+
+void launch_copy_words(void *dst, const void *src, int64_t words, hipStream_t st) {
+  if (words <= 0) return;
+  hipLaunchKernelGGL(copy_words_kernel, dim3((unsigned)std::min<int64_t>((words + 255) / 256, 4096)), dim3(256), 0, st,
+                     static_cast<uint32_t *>(dst), static_cast<const uint32_t *>(src), words);
 }
 
 void fill_u8(uint8_t *p, uint8_t v, int64_t n, hipStream_t st) {

@@ -172,22 +172,26 @@ def test_flat_search_device_graph_capture_and_replay(hiplib, metric, force_fail)
         ra, rb = idx.search_batch(qa, 10), idx.search_batch(qb, 10)
         st = torch.cuda.Stream()
         qbuf = torch.from_numpy(qa).cuda()
-        out = (torch.empty((n, 10), dtype=torch.float32, device="cuda"),
-               torch.empty((n, 10), dtype=torch.int64, device="cuda"),
-               torch.empty((n,), dtype=torch.int32, device="cuda"))
-        args = (qbuf.data_ptr(), n, 10, out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(), st.cuda_stream, None)
-        idx.search_device(*args)  # warm-up: workspace and row terms sized
+        with torch.cuda.stream(st):
+            out = _dev_search(idx, qbuf, 10, None, st)  # warm-up: workspace and row terms sized
         st.synchronize()
-        g = torch.cuda.CUDAGraph(keep_graph=True)
+        if os.environ.get("PYR_DEBUG_ALLOC"):  # diagnostics: the caller's buffers beside the library's log
+            with open(os.environ["PYR_DEBUG_ALLOC"], "a") as f:
+                f.write(f"# test metric={metric} force_fail={force_fail} stream={st.cuda_stream:#x} "
+                        f"qbuf={qbuf.data_ptr():#x} out={[hex(t.data_ptr()) for t in out]}\n")
+        g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=st):
-            idx.search_device(*args)
-        g.instantiate()
-        qbuf.copy_(torch.from_numpy(qb))
-        torch.cuda.synchronize()
-        g.replay()
-        torch.cuda.synchronize()
-        _same(out, rb)
-        # back to back on one stream, no host synchronization in between
+            idx.search_device(qbuf.data_ptr(), n, 10, out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(),
+                              st.cuda_stream, None)
+        # replayed twice with other queries in the captured buffer (a search must be repeatable:
+        # BruteForceVectorIndex.cs:275-379)
+        for qv, ref in ((qb, rb), (qa, ra)):
+            qbuf.copy_(torch.from_numpy(qv))
+            torch.cuda.synchronize()
+            g.replay()
+            torch.cuda.synchronize()
+            _same(out, ref)
+        # back to back on the capture stream, no host synchronization in between ...
         qa_d, qb_d = torch.from_numpy(qa).cuda(), torch.from_numpy(qb).cuda()
         torch.cuda.synchronize()
         with torch.cuda.stream(st):
@@ -196,5 +200,11 @@ def test_flat_search_device_graph_capture_and_replay(hiplib, metric, force_fail)
         st.synchronize()
         _same(oa, ra)
         _same(ob, rb)
+        # ... and the graph replayed once more after those plain searches on its stream's workspace
+        qbuf.copy_(torch.from_numpy(qb))
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        _same(out, rb)
     with _env(PYR_FILTER=0):
         _same(oa, idx.search_batch(qa, 10))
