@@ -228,6 +228,60 @@ pyr_status pyr_merge_topk_parts_device(const float *d_scores, const int64_t *d_l
                                        int32_t k, int32_t part_major, float *d_out_scores, int64_t *d_out_labels,
                                        void *stream);
 
+/* ---- List-sharded multi-GPU IVF_FLAT search ("IVF lists shard naturally across the
+ * GPUs"; orchestration: pyrope_amd/dist.py ListShardedIvf).  The reference path split is
+ * the probed-list loop of IvfFlatVectorIndex.Search (IvfFlatVectorIndex.cs:198-218): every rank holds
+ * WHOLE lists (the rows FindNearestCentroid sends to a list it owns, in label order) plus the shared
+ * quantizer, so a (query, list) pair is scanned by exactly one rank.  A step:
+ *   home rank (its slice of the batch)  pyr_index_shard_prepare_device -> plan [nq][P + 1]
+ *   all ranks, all_gather(plans)        pyr_index_shard_search_device  -> one record per query
+ *   all_to_all(records) to the homes    pyr_shard_merge_device         -> results + failed certificates
+ *   all_gather(fail lists)              pyr_index_shard_rerun_device   -> exact records of the failures
+ *   all_to_all(records) to the homes    pyr_shard_merge_device(qsel)   -> their exact results
+ * Results equal the unsharded index's, ties included ((score desc, list asc, label asc) is the unsharded
+ * storage order).  Device buffers, enqueued on `stream`; no host synchronisation. */
+
+/* KMeansUtils.FindNearestCentroid (KMeansUtils.cs:70-93; the assignment of IvfFlatVectorIndex.Build,
+ * :128-132) of n host rows against nlist host centroids: assign[i] = the list row i belongs to (ties ->
+ * lowest index).  The row exchange that gives every rank its whole lists uses it. */
+pyr_status pyr_assign(int32_t device, const float *centroids, int32_t nlist, const float *x, int64_t n, int32_t dim,
+                      int32_t metric, int32_t *assign);
+/* Bytes of one record: k entries {int64 label, float score, int32 list} in (score desc, list asc, label
+ * asc) order (empty: label -1, score -inf), then {float bound, int32 n, 8 pad}: every row of the rank's
+ * probed lists that is not an entry scores at most `bound` (-inf: none was left out).  16 (k + 1). */
+int64_t pyr_shard_record_bytes(int32_t k);
+/* The replicated sample of every list, on a built shard index (L2 / IP): rows = the first counts[l] <= 512
+ * rows of each list l in list order, concatenated (sum counts x dim, host); list_len[l] = list l's full
+ * length on the rank that owns it.  It is what the unsharded index's sample pass scores, so the home
+ * rank's T_q equals the unsharded one. */
+pyr_status pyr_index_set_list_samples(pyr_index *index, const float *rows, const int64_t *counts,
+                                      const int64_t *list_len, int32_t nlist);
+/* Home rank: the coarse ranking (IvfFlatVectorIndex.cs:186-198) and the threshold T_q of nq queries:
+ * d_plan [nq][P + 1] int32 = P probe ids in rank order, then T_q's float bits; *width = P = min(nprobe, nlist). */
+pyr_status pyr_index_shard_prepare_device(pyr_index *index, const float *d_q, int64_t nq, int32_t k,
+                                          const pyr_search_params *params, int32_t *d_plan, int32_t *width,
+                                          void *stream);
+/* Every rank: the stream scan of the (query, list) pairs of the gathered plans whose list this rank owns
+ * (the others are empty here) against T_q, the exact refine of each query's best candidates, and one
+ * record per query (d_records: nq x pyr_shard_record_bytes(k)).  k <= 60. */
+pyr_status pyr_index_shard_search_device(pyr_index *index, const float *d_q, int64_t nq, int32_t k,
+                                         const int32_t *d_plan, int32_t width, void *d_records, void *stream);
+/* Merge nparts (<= 64) records per query and certify.  d_records: [nparts][nrec] (an all_to_all's
+ * output).  d_qsel = NULL: record i answers query i (i < nrec), results to row i, and with d_fail the
+ * certificate (the k-th merged score beats every bound) lists failing queries: d_fail[0] = their count
+ * (may exceed fcap: the caller must then re-run the excess), d_fail[1 .. fcap].  d_qsel = a fail list
+ * [1 + cap]: record i answers query d_qsel[1 + i], i < min(d_qsel[0], cap) (the re-run's answers). */
+pyr_status pyr_shard_merge_device(const void *d_records, int32_t nparts, int64_t nrec, int32_t k,
+                                  const int32_t *d_qsel, int32_t cap, float *d_scores, int64_t *d_labels,
+                                  int32_t *d_counts, int32_t *d_fail, int32_t fcap, void *stream);
+/* Every rank: the exact search (the *safe* VectorMath forms, IvfFlatVectorIndex.cs:200-218) of the
+ * gathered failures d_fails [nranks][1 + fcap] (home-local query ids; home s's queries are rows
+ * s * nq_home .. of d_q / d_plan) over this rank's lists: the answer to home s's j-th failure is record
+ * s * fcap + j of d_records ([nranks * fcap] records, bound -inf). */
+pyr_status pyr_index_shard_rerun_device(pyr_index *index, const float *d_q, int64_t nq, int32_t k,
+                                        const int32_t *d_plan, int32_t width, const int32_t *d_fails, int32_t nranks,
+                                        int32_t fcap, int64_t nq_home, void *d_records, void *stream);
+
 /* HBM plan (host arithmetic, no device needed): the bytes an IVF_FLAT index of nrows rows in nlist
  * lists (longest max_list_len rows) holds on one GPU, and the workspace one batched search of nq queries
  * (nprobe, k) on the default list scan allocates.  A multi-GPU launcher sizes each rank with it before

@@ -7,7 +7,7 @@ mirror of the reference's IVectorIndex plugin surface.
 from .vector import (BruteForceVectorIndex, DeltaVectorIndex, HipVectorIndex, ICentroidsProvider,  # noqa: F401
                      IndexStats, IvfFlatVectorIndex, IvfPqVectorIndex, IVectorIndex, ScalarQuantizer, SearchOptions,
                      SearchResult, VectorIndexRegistry, VectorMetric, generate_synthetic,
-                     generate_synthetic_blocked, kmeans_train)
+                     generate_synthetic_blocked, kmeans_train, assign)
 from ._lib import (ArgumentException, ArgumentNullException, ArgumentOutOfRangeException,  # noqa: F401
                    DeviceError, InvalidOperationException)
 

@@ -117,6 +117,17 @@ SIGNATURES = {
     "pyr_index_reserve": (C.c_int, [_vp, C.c_int64]),
     "pyr_kmeans_train": (C.c_int, [C.c_int32, _f, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                    _f, _i32]),
+    # list-sharded multi-GPU search (dist.py ListShardedIvf)
+    "pyr_assign": (C.c_int, [C.c_int32, _f, C.c_int32, _f, C.c_int64, C.c_int32, C.c_int32, _i32]),
+    "pyr_shard_record_bytes": (C.c_int64, [C.c_int32]),
+    "pyr_index_set_list_samples": (C.c_int, [_vp, _f, _i64, _i64, C.c_int32]),
+    "pyr_index_shard_prepare_device": (C.c_int, [_vp, _vp, C.c_int64, C.c_int32, C.POINTER(SearchParams), _vp,
+                                                 C.POINTER(C.c_int32), _vp]),
+    "pyr_index_shard_search_device": (C.c_int, [_vp, _vp, C.c_int64, C.c_int32, _vp, C.c_int32, _vp, _vp]),
+    "pyr_index_shard_rerun_device": (C.c_int, [_vp, _vp, C.c_int64, C.c_int32, _vp, C.c_int32, _vp, C.c_int32,
+                                               C.c_int32, C.c_int64, _vp, _vp]),
+    "pyr_shard_merge_device": (C.c_int, [_vp, C.c_int32, C.c_int64, C.c_int32, _vp, C.c_int32, _vp, _vp, _vp, _vp,
+                                         C.c_int32, _vp]),
     "pyr_profile_enable": (None, [C.c_int32]),
     "pyr_profile_reset": (None, []),
     "pyr_profile_get": (C.c_int, [C.c_int32, C.POINTER(C.c_double), _i64, _i64]),

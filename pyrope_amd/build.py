@@ -11,7 +11,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libpyrope_hip.so")
-SOURCES = ["kernels.hip", "sort.hip", "filter.hip", "tiles16.hip", "sample16.hip", "scan.hip", "pq32.hip", "sq8.hip", "coarse.hip", "engine.cpp", "persist.cpp", "capi.cpp"]
+SOURCES = ["kernels.hip", "sort.hip", "filter.hip", "tiles16.hip", "sample16.hip", "scan.hip", "pq32.hip", "sq8.hip", "coarse.hip", "shard.hip", "engine.cpp", "persist.cpp", "capi.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 # -ffp-contract=off: the parity contract (bit-identical scores) forbids FMA contraction.

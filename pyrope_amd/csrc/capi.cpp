@@ -219,6 +219,33 @@ pyr_status pyr_kmeans_train(int32_t device, const float *data, int64_t n, int32_
   });
 }
 
+pyr_status pyr_assign(int32_t device, const float *centroids, int32_t nlist, const float *x, int64_t n, int32_t dim,
+                      int32_t metric, int32_t *assign) {
+  if (!centroids || (n > 0 && (!x || !assign)) || n < 0 || dim <= 0 || nlist <= 0) return fail(PYR_E_ARG, "bad argument");
+  return guard([&] {
+    check_device(device);
+    HIPCHK(hipSetDevice(device));
+    if (n == 0) return;
+    hipStream_t st;
+    HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    try {
+      pyr::DevMem X, C, A;
+      X.ensure(sizeof(float) * (size_t)n * dim);
+      C.ensure(sizeof(float) * (size_t)nlist * dim);
+      A.ensure(sizeof(int32_t) * (size_t)n);
+      HIPCHK(hipMemcpyAsync(X.p, x, sizeof(float) * n * dim, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(C.p, centroids, sizeof(float) * (size_t)nlist * dim, hipMemcpyHostToDevice, st));
+      pyr::assign_gpu(X.as<float>(), n, dim, C.as<float>(), nlist, metric, A.as<int32_t>(), st);
+      HIPCHK(hipMemcpyAsync(assign, A.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+    } catch (...) {
+      (void)hipStreamDestroy(st);
+      throw;
+    }
+    (void)hipStreamDestroy(st);
+  });
+}
+
 void pyr_profile_enable(int32_t on) {
   std::lock_guard<std::mutex> g(pyr::prof().m);
   pyr::prof().on = on != 0;
@@ -604,6 +631,97 @@ pyr_status pyr_merge_topk_parts_device(const float *d_scores, const int64_t *d_l
   return guard([&] {
     pyr::launch_merge_labels(d_scores, d_labels, nq, nparts, k, d_out_scores, d_out_labels,
                              reinterpret_cast<hipStream_t>(stream), part_major != 0);
+    HIPCHK(hipGetLastError());
+  });
+}
+
+int64_t pyr_shard_record_bytes(int32_t k) { return k > 0 ? pyr::shard_record_bytes(k) : 0; }
+
+pyr_status pyr_index_set_list_samples(pyr_index *index, const float *rows, const int64_t *counts,
+                                      const int64_t *list_len, int32_t nlist) {
+  if (!index || !counts || !list_len || nlist <= 0) return fail(PYR_E_ARG, "null argument");
+  int64_t tot = 0;
+  for (int32_t l = 0; l < nlist; ++l) tot += counts[l] > 0 ? counts[l] : 0;
+  if (tot > 0 && !rows) return fail(PYR_E_ARG, "null argument");
+  return guard([&] {
+    HIPCHK(hipSetDevice(index->impl->device));
+    std::unique_lock<std::shared_mutex> g(index->impl->mu);
+    index->impl->set_list_samples(rows, counts, list_len, nlist);
+  });
+}
+
+pyr_status pyr_index_shard_prepare_device(pyr_index *index, const float *d_q, int64_t nq, int32_t k,
+                                          const pyr_search_params *params, int32_t *d_plan, int32_t *width,
+                                          void *stream) {
+  if (!index || nq < 0 || (nq > 0 && (!d_q || !d_plan))) return fail(PYR_E_ARG, "null argument");
+  return guard([&] {
+    pyr::Index &ix = *index->impl;
+    HIPCHK(hipSetDevice(ix.device));
+    std::shared_lock<std::shared_mutex> g(ix.mu);
+    pyr::Workspace &ws = ix.ws_for_stream(reinterpret_cast<hipStream_t>(stream));
+    std::lock_guard<std::mutex> wg(ws.m);
+    const int P = ix.shard_prepare(d_q, nq, k, defaults(params), d_plan, ws);
+    if (width) *width = P;
+    HIPCHK(hipGetLastError());
+  });
+}
+
+pyr_status pyr_index_shard_search_device(pyr_index *index, const float *d_q, int64_t nq, int32_t k,
+                                         const int32_t *d_plan, int32_t width, void *d_records, void *stream) {
+  if (!index || nq < 0 || (nq > 0 && (!d_q || !d_plan || !d_records))) return fail(PYR_E_ARG, "null argument");
+  return guard([&] {
+    pyr::Index &ix = *index->impl;
+    HIPCHK(hipSetDevice(ix.device));
+    std::shared_lock<std::shared_mutex> g(ix.mu);
+    pyr::Workspace &ws = ix.ws_for_stream(reinterpret_cast<hipStream_t>(stream));
+    std::lock_guard<std::mutex> wg(ws.m);
+    ix.shard_search(d_q, nq, k, d_plan, width, d_records, ws);
+    HIPCHK(hipGetLastError());
+  });
+}
+
+pyr_status pyr_index_shard_rerun_device(pyr_index *index, const float *d_q, int64_t nq, int32_t k,
+                                        const int32_t *d_plan, int32_t width, const int32_t *d_fails, int32_t nranks,
+                                        int32_t fcap, int64_t nq_home, void *d_records, void *stream) {
+  if (!index || nq < 0 || !d_plan || !d_fails || !d_records || nranks <= 0 || nranks > 64 || fcap <= 0)
+    return fail(PYR_E_ARG, "bad argument");
+  return guard([&] {
+    pyr::Index &ix = *index->impl;
+    HIPCHK(hipSetDevice(ix.device));
+    std::shared_lock<std::shared_mutex> g(ix.mu);
+    pyr::Workspace &ws = ix.ws_for_stream(reinterpret_cast<hipStream_t>(stream));
+    std::lock_guard<std::mutex> wg(ws.m);
+    ix.shard_rerun(d_q, nq, k, d_plan, width, d_fails, nranks, fcap, nq_home, d_records, ws);
+    HIPCHK(hipGetLastError());
+  });
+}
+
+pyr_status pyr_shard_merge_device(const void *d_records, int32_t nparts, int64_t nrec, int32_t k,
+                                  const int32_t *d_qsel, int32_t cap, float *d_scores, int64_t *d_labels,
+                                  int32_t *d_counts, int32_t *d_fail, int32_t fcap, void *stream) {
+  if (!d_records || nparts <= 0 || nparts > 64 || nrec < 0 || k <= 0 || k > 64 || !d_scores || !d_labels)
+    return fail(PYR_E_ARG, "bad merge shape");
+  if (d_qsel && cap <= 0) return fail(PYR_E_ARG, "bad merge shape");
+  return guard([&] {
+    pyr::ShardMergeArgs a{};
+    a.rec = static_cast<const uint8_t *>(d_records);
+    a.nparts = nparts;
+    a.nrec = nrec;
+    a.k = k;
+    a.qsel = d_qsel;
+    a.cap = cap;
+    a.out_s = d_scores;
+    a.out_l = d_labels;
+    a.out_c = d_counts;
+    a.fail = d_fail;
+    a.fcap = fcap;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (d_fail) {  // the failure count restarts at 0 (a kernel, not a memset node: stream capture)
+      pyr::WordFill z;
+      z.add(d_fail, 1, 0);
+      pyr::launch_fill_words(z, st);
+    }
+    pyr::launch_shard_merge(a, d_qsel ? std::min<int64_t>(cap, nrec) : nrec, st);
     HIPCHK(hipGetLastError());
   });
 }

@@ -485,10 +485,12 @@ static int store16_dt(int dim) { return scan_tile_dim(dim); }
 // (0.15 ms at I1); elsewhere scan.hip's one-wave-per-32-queries sample (0.29 ms at I1: every group
 // re-reads the sampled tiles).  Both write the same bq / qsc / samp.  PYR_SCAN_SAMPLE=1: scan.hip's
 // sample at every dim (measurement only).
-static void stream_sample(const StreamArgs &sa, int met, int maxi, hipStream_t st) {
+// prep_only: the operands without the sample where the native-dim pass allows it (the one-wave pass writes
+// both; its sample values are then simply not read)
+static void stream_sample(const StreamArgs &sa, int met, int maxi, hipStream_t st, bool prep_only = false) {
   const char *e = getenv("PYR_SCAN_SAMPLE");
   const int dt = sa.dt > 0 ? sa.dt : sa.dim;
-  if (!(e && atoi(e) == 1) && dt == sa.dim && sample16_supported(sa.dim, met)) launch_sample16(sa, met, maxi, st);
+  if (!(e && atoi(e) == 1) && dt == sa.dim && sample16_supported(sa.dim, met)) launch_sample16(sa, met, maxi, st, prep_only);
   else launch_scan_sample(sa, met, maxi, st);
 }
 // T_q = the R-th largest sample value.  Any R is correct (rows below T_q are represented by floor
@@ -593,6 +595,13 @@ struct CosRefine {
   const float *queries;    // raw queries
   const float *qnorm;      // ComputeNorm per query
   const uint32_t *zflag;   // a zero-norm row was written
+};
+
+// list-sharded search (IvfFlatIndex::shard_search, shard.hip): a slice's thresholds T_q (from the home
+// ranks' plans) and its record output (exact local top-k + the bound of the rows left out, per query)
+struct ShardCtx {
+  const float *thr;
+  uint8_t *rec;
 };
 
 // re-run the listed queries through the exact scan and put their rows in place
@@ -1942,7 +1951,7 @@ struct IvfFlatIndex : Index {
   // depth 64 for the failures); what still fails is re-run by the exact scan.  Query batches are
   // sliced so that the candidate regions stay within 16 GiB.
   void search_stream(const float *d_q, int64_t nq, int k, int k1, int probes, float *d_s, int64_t *d_l, int32_t *d_c,
-                     Workspace &ws) {
+                     Workspace &ws, const ShardCtx *sh = nullptr) {
     const int cap = stream_cap();
     int64_t chunk = stream_chunk();
     IvfChunking ch{(int32_t)chunk, 1, 0};
@@ -1961,9 +1970,11 @@ struct IvfFlatIndex : Index {
       const int64_t n = std::min(qs, nq - a0);
       const int32_t *ext = ws.ext_probes;
       if (ext) ws.ext_probes = ext + a0 * ws.ext_nprobe;
+      ShardCtx s2{};
+      if (sh) s2 = ShardCtx{sh->thr + a0, sh->rec + a0 * shard_record_bytes(k)};
       try {
-        stream_slice(d_q + a0 * dim, n, k, k1, probes, ch, nparts, cap, d_s + a0 * k, d_l + a0 * k,
-                     d_c ? d_c + a0 : nullptr, ws);
+        stream_slice(d_q + a0 * dim, n, k, k1, probes, ch, nparts, cap, d_s ? d_s + a0 * k : nullptr,
+                     d_l ? d_l + a0 * k : nullptr, d_c ? d_c + a0 : nullptr, ws, sh ? &s2 : nullptr);
       } catch (...) {
         ws.ext_probes = ext;
         throw;
@@ -2018,7 +2029,7 @@ struct IvfFlatIndex : Index {
   }
 
   void stream_slice(const float *d_q, int64_t nq, int k, int k1, int probes, IvfChunking ch, int nparts, int cap,
-                    float *d_s, int64_t *d_l, int32_t *d_c, Workspace &ws) {
+                    float *d_s, int64_t *d_l, int32_t *d_c, Workspace &ws, const ShardCtx *sh = nullptr) {
     const bool cosine = metric == COS;
     const int met = cosine ? L2 : metric;  // Cosine: L2 over the unit vectors (commit_lists)
     reset_stream_counters(ws, nq, coarse.nlist);
@@ -2096,22 +2107,27 @@ struct IvfFlatIndex : Index {
     }
     {
       PhaseTimer t(PH_SAMPLE, ws.st);
-      stream_sample(sa, met, maxi, ws.st);
-      StreamSelectArgs sel{};
-      sel.samp = ws.ssamp.as<float>();
-      sel.nq = nq;
-      sel.n = probes * sv;
-      stream_rank(k1, sel.rmin, sel.rmax, sel.et);
-      sel.probes = ws.probes.as<int32_t>();
-      sel.nprobe = probes;
-      sel.lb = dlb.as<int32_t>();
-      sel.le = dle.as<int32_t>();
-      sel.thr = ws.sthr.as<float>();
-      launch_stream_select(sel, ws.st);
+      // list-sharded: T_q comes from the home rank's plan (its sample of every list); only the operands here
+      stream_sample(sa, met, maxi, ws.st, sh != nullptr);
+      if (sh) {
+        sa.thr = sh->thr;
+      } else {
+        StreamSelectArgs sel{};
+        sel.samp = ws.ssamp.as<float>();
+        sel.nq = nq;
+        sel.n = probes * sv;
+        stream_rank(k1, sel.rmin, sel.rmax, sel.et);
+        sel.probes = ws.probes.as<int32_t>();
+        sel.nprobe = probes;
+        sel.lb = dlb.as<int32_t>();
+        sel.le = dle.as<int32_t>();
+        sel.thr = ws.sthr.as<float>();
+        launch_stream_select(sel, ws.st);
+      }
     }
     sa.work = ws.swork.as<int32_t>() + 1;
     {
-      PhaseTimer t(PH_LIST_SCAN, ws.st, prof().on ? probed_rows(ws, nq, probes, le, lb) : 0);
+      PhaseTimer t(PH_LIST_SCAN, ws.st, prof().on && !sh ? probed_rows(ws, nq, probes, le, lb) : 0);
       if (timing) sa.tdbg = ws.tdbg.as<unsigned long long>();
       launch_scan_main(sa, met, maxi, ws.st);
       sa.tdbg = nullptr;
@@ -2134,7 +2150,7 @@ struct IvfFlatIndex : Index {
       m.cand = ws.scand.as<uint2>();
       m.cand_n = ws.scn.as<int32_t>();
       m.cand_f = ws.scf.as<uint32_t>();
-      m.thr = ws.sthr.as<float>();
+      m.thr = sa.thr;
       m.nq = nq;
       m.cap = cap;
       m.out_s = ws.ms.as<float>();
@@ -2180,6 +2196,16 @@ struct IvfFlatIndex : Index {
     r.out_l = d_l;
     r.out_c = d_c;
     int32_t nf = 0;
+    if (sh) {  // list-sharded: the records (exact local top-k + bound); the home rank's merge certifies
+      PhaseTimer t(PH_REFINE, ws.st, nq * k1);
+      r.k1 = k1;
+      r.rec = sh->rec;
+      r.rec_lb = dlb.as<int32_t>();
+      r.rec_nlist = coarse.nlist;
+      launch_refine(r, met, 1, ws.st);
+      HIPCHK(hipGetLastError());
+      return;
+    }
     {
       PhaseTimer t(PH_REFINE, ws.st, nq * k1);
       r.k1 = k1;
@@ -2247,6 +2273,217 @@ struct IvfFlatIndex : Index {
     coarse.probe(d_q, metric == COS ? ws.qn.as<float>() : nullptr, nq, probes, metric, ws);
     launch_copy_words(d_out, ws.probes.p, nq * probes, ws.st);
     return probes;
+  }
+
+  // ---- list-sharded multi-GPU search (shard.hip) ----
+  // The rank holds whole lists (the others are empty here) with the shared quantizer, plus a replicated
+  // sample of EVERY list: its first <= 512 rows in list order as fp16 residual tiles (the rows the
+  // unsharded index's sample pass scores), so that a query's home rank computes the unsharded T_q.
+  std::unique_ptr<RowStore> ssamp;
+  DevMem sslb, ssle, sglb, sgle;
+
+  void set_list_samples(const float *rows, const int64_t *counts, const int64_t *glen, int nl) override {
+    if (!built || coarse.nlist <= 0) throw Error(PYR_E_STATE, "index is not built");
+    if (nl != coarse.nlist) throw Error(PYR_E_ARG, "the samples do not cover the quantizer's lists");
+    if (metric == COS || !store16(dim, metric)) throw Error(PYR_E_STATE, "list-sharded search serves L2 / IP");
+    std::vector<int32_t> slb(nl), sle(nl), z(nl, 0), gl(nl);
+    int64_t tot = 0, nrows = 0;
+    for (int l = 0; l < nl; ++l) {
+      if (counts[l] < 0 || counts[l] > 512 || counts[l] > glen[l])
+        throw Error(PYR_E_ARG, "a list sample holds more rows than 512 or than its list");
+      if (glen[l] > INT32_MAX) throw Error(PYR_E_ARG, "list longer than 2^31 rows");
+      slb[l] = (int32_t)tot;
+      sle[l] = (int32_t)(tot + counts[l]);
+      gl[l] = (int32_t)glen[l];
+      tot += round_up(counts[l], 32);
+      nrows += counts[l];
+    }
+    std::vector<int64_t> src((size_t)std::max<int64_t>(tot, 1), -1);
+    std::vector<uint8_t> lv((size_t)std::max<int64_t>(tot, 1), 0);
+    for (int l = 0, off = 0; l < nl; off += (int)counts[l], ++l)
+      for (int64_t j = 0; j < counts[l]; ++j) {
+        src[slb[l] + j] = off + j;
+        lv[slb[l] + j] = 1;
+      }
+    auto ss = std::make_unique<RowStore>();
+    RowStore &s = *ss;
+    s.dim = dim;
+    s.f16 = true;
+    s.dt = store16_dt(dim);
+    s.met16 = metric;
+    s.reserve(std::max<int64_t>(tot, 32), wst);
+    DevMem X, dsr, dtl;
+    X.ensure(sizeof(float) * std::max<int64_t>(nrows, 1) * dim);
+    if (nrows) HIPCHK(hipMemcpyAsync(X.p, rows, sizeof(float) * nrows * dim, hipMemcpyHostToDevice, wst));
+    dsr.ensure(sizeof(int64_t) * src.size());
+    HIPCHK(hipMemcpyAsync(dsr.p, src.data(), sizeof(int64_t) * src.size(), hipMemcpyHostToDevice, wst));
+    launch_to_blocked(X.as<float>(), dsr.as<int64_t>(), tot, dim, s.rows.as<float>(), 0, wst);
+    HIPCHK(hipMemcpyAsync(s.live.p, lv.data(), (size_t)tot, hipMemcpyHostToDevice, wst));
+    launch_sqnorms(s.rows.as<float>(), nullptr, tot, dim, s.rsq.as<float>(), s.rmax.as<uint32_t>(), wst);
+    std::vector<int32_t> tl((size_t)(s.cap / 32), 0);  // the list of every 32-row tile (residual tiles)
+    for (int l = 0; l < nl; ++l)
+      for (int64_t t = slb[l] / 32; t < (slb[l] + round_up(sle[l] - slb[l], 32)) / 32; ++t) tl[t] = l;
+    dtl.ensure(sizeof(int32_t) * tl.size());
+    HIPCHK(hipMemcpyAsync(dtl.p, tl.data(), sizeof(int32_t) * tl.size(), hipMemcpyHostToDevice, wst));
+    s.resid = true;
+    s.rsq16.ensure(sizeof(float) * s.cap);
+    const float *C = coarse.rm.as<float>();
+    launch_resid_sq(s.rows.as<float>(), s.cap, dim, C, dtl.as<int32_t>(), s.rsq16.as<float>(), wst);
+    HIPCHK(hipMemsetAsync(s.amaxd.p, 0, sizeof(uint32_t), wst));
+    launch_absmax(s.rows.as<float>(), nullptr, s.cap, dim, s.amaxd.as<uint32_t>(), wst, C, dtl.as<int32_t>());
+    uint32_t bits = 0;
+    HIPCHK(hipMemcpyAsync(&bits, s.amaxd.p, sizeof(bits), hipMemcpyDeviceToHost, wst));
+    HIPCHK(hipStreamSynchronize(wst));
+    std::memcpy(&s.amax, &bits, sizeof(bits));
+    s.sx = pow2_scale_host(s.amax);
+    launch_encode16(s.rows.as<float>(), nullptr, s.cap, dim, s.sx, s.h16.p, wst, C, dtl.as<int32_t>(),
+                    s.rsq16.as<float>(), s.tdim());
+    launch_meta16(nullptr, s.cap, s.met16, s.rsq16.as<float>(), s.live.as<uint8_t>(), s.meta.as<float>(), wst);
+    s.n = tot;
+    for (DevMem *d : {&sslb, &ssle, &sglb, &sgle}) d->ensure(sizeof(int32_t) * nl);
+    HIPCHK(hipMemcpyAsync(sslb.p, slb.data(), sizeof(int32_t) * nl, hipMemcpyHostToDevice, wst));
+    HIPCHK(hipMemcpyAsync(ssle.p, sle.data(), sizeof(int32_t) * nl, hipMemcpyHostToDevice, wst));
+    HIPCHK(hipMemcpyAsync(sglb.p, z.data(), sizeof(int32_t) * nl, hipMemcpyHostToDevice, wst));  // [0, glen): the
+    HIPCHK(hipMemcpyAsync(sgle.p, gl.data(), sizeof(int32_t) * nl, hipMemcpyHostToDevice, wst));  // true lengths
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(wst));
+    ssamp = std::move(ss);
+  }
+
+  int shard_prepare(const float *d_q, int64_t nq, int k, const pyr_search_params &prm, int32_t *d_plan,
+                    Workspace &ws) override {
+    if (!ssamp) throw Error(PYR_E_STATE, "no list samples (pyr_index_set_list_samples)");
+    const int k1 = filter_k1(k);
+    if (k <= 0 || k > KMAX_FAST || k1 <= 0) throw Error(PYR_E_ARG, "topK out of the list-sharded search's range");
+    const int nprobe = prm.nprobe < 0 ? nprobe_default : prm.nprobe;
+    const int P = std::max(0, std::min(nprobe, coarse.nlist));
+    if (P == 0 || nq == 0) return P;
+    if (P >= MAX_PARTS) throw Error(PYR_E_ARG, "nprobe too large");
+    RowStore &s = *ssamp;
+    const int dt = s.tdim(), sv = scan_sample_values();
+    // slices of <= 1 GiB of operands and samples
+    const int64_t per_q = (int64_t)P * (2 * dt + 8 + 4 * sv) + 64;
+    const int64_t qs = std::max<int64_t>(1, std::min<int64_t>(nq, (int64_t(1) << 30) / per_q));
+    for (int64_t a0 = 0; a0 < nq; a0 += qs) {
+      const int64_t n = std::min(qs, nq - a0);
+      const float *q = d_q + a0 * dim;
+      reset_stream_counters(ws, n, coarse.nlist);
+      {
+        PhaseTimer t(PH_COARSE, ws.st, n * coarse.nlist);
+        coarse.probe(q, nullptr, n, P, metric, ws);
+      }
+      const IvfChunking ch{512, 1, 0};  // a sample list is one chunk
+      const int maxi = build_ivf_items(ws, n, P, P, coarse.nlist, sslb, ssle, scan_qmax(dt), ch, 0, true, true);
+      const int64_t npos = n * P;
+      ws.sbq.ensure(sizeof(uint16_t) * npos * dt);
+      ws.sqsc.ensure(sizeof(float2) * npos);
+      ws.ssamp.ensure(sizeof(float) * npos * sv);
+      ws.sthr.ensure(sizeof(float) * n);
+      StreamArgs sa{};
+      sa.h16 = s.h16.p;
+      sa.meta = s.meta.as<float>();
+      sa.queries = q;
+      sa.cents = coarse.rm.as<float>();
+      sa.sx = s.sx;
+      sa.items = ws.items.as<ScanItem>();
+      sa.n_items = ws.nitems.as<int32_t>();
+      sa.qlist = ws.qlist.as<int32_t>();
+      sa.nparts = P;
+      sa.nprobe = P;
+      sa.cmax = 1;
+      sa.dim = dim;
+      sa.dt = dt;
+      sa.bq = ws.sbq.as<_Float16>();
+      sa.qsc = ws.sqsc.as<float2>();
+      sa.samp = ws.ssamp.as<float>();
+      sa.work = ws.swork.as<int32_t>();
+      sa.row_limit = 0xFFFFFFFFu;
+      sa.rsq16 = s.rsq16.as<float>();
+      sa.rsq = s.rsq.as<float>();
+      stream_ub_terms(dt, metric, filter_f16_cerr(dt, metric, FILTER_F16X1), filter_cerr(dt),
+                      filter_f16_abs(dt, metric, s.sx, FILTER_F16X1), sa);
+      sa.mub = s.row_terms(metric, sa.kr, sa.kx, ws.st);
+      {
+        PhaseTimer t(PH_SAMPLE, ws.st);
+        stream_sample(sa, metric, maxi, ws.st);
+        StreamSelectArgs sel{};
+        sel.samp = ws.ssamp.as<float>();
+        sel.nq = n;
+        sel.n = P * sv;
+        stream_rank(k1, sel.rmin, sel.rmax, sel.et);
+        sel.probes = ws.probes.as<int32_t>();
+        sel.nprobe = P;
+        sel.lb = sglb.as<int32_t>();  // the lists' true lengths: the sampled fraction of the unsharded scan
+        sel.le = sgle.as<int32_t>();
+        sel.thr = ws.sthr.as<float>();
+        launch_stream_select(sel, ws.st);
+      }
+      launch_pack_plan(ws.probes.as<int32_t>(), ws.sthr.as<float>(), n, P, d_plan + a0 * (P + 1), ws.st);
+      HIPCHK(hipGetLastError());
+    }
+    return P;
+  }
+
+  void shard_search(const float *d_q, int64_t nq, int k, const int32_t *d_plan, int P, void *d_rec,
+                    Workspace &ws) override {
+    if (!built || coarse.nlist <= 0) throw Error(PYR_E_STATE, "index is not built");
+    if (metric == COS) throw Error(PYR_E_STATE, "list-sharded search serves L2 / IP");
+    if (buf.live_count() > 0) throw Error(PYR_E_STATE, "list-sharded search needs every row in the lists (Build)");
+    const int k1 = filter_k1(k);
+    if (k <= 0 || k > KMAX_FAST || k1 <= 0 || !stream_ok(k1))
+      throw Error(PYR_E_ARG, "topK out of the list-sharded search's range");
+    if (P <= 0 || P > coarse.nlist || P >= MAX_PARTS) throw Error(PYR_E_ARG, "plan width does not fit the index");
+    if (nq == 0) return;
+    ws.shp.ensure(sizeof(int32_t) * nq * P);
+    ws.shthr.ensure(sizeof(float) * nq);
+    launch_unpack_plan(d_plan, nq, P, ws.shp.as<int32_t>(), ws.shthr.as<float>(), ws.st);
+    const ShardCtx sh{ws.shthr.as<float>(), static_cast<uint8_t *>(d_rec)};
+    ws.ext_probes = ws.shp.as<int32_t>();
+    ws.ext_nprobe = P;
+    try {
+      search_stream(d_q, nq, k, k1, P, nullptr, nullptr, nullptr, ws, &sh);
+    } catch (...) {
+      ws.ext_probes = nullptr;
+      throw;
+    }
+    ws.ext_probes = nullptr;
+  }
+
+  void shard_rerun(const float *d_q, int64_t nq, int k, const int32_t *d_plan, int P, const int32_t *d_fails,
+                   int nranks, int fcap, int64_t nq_home, void *d_rec, Workspace &ws) override {
+    (void)nq;
+    if (!built || coarse.nlist <= 0) throw Error(PYR_E_STATE, "index is not built");
+    if (k <= 0 || k > 64) throw Error(PYR_E_ARG, "topK out of the list-sharded search's range");
+    if (fcap <= 0 || nranks <= 0) return;
+    const int64_t mf = (int64_t)nranks * fcap;
+    ws.fail.ensure(sizeof(int32_t) * mf);
+    ws.rpos.ensure(sizeof(int32_t) * mf);
+    ws.fail_cnt.ensure(sizeof(int32_t));
+    launch_shard_fail_compact(d_fails, nranks, fcap, nq_home, ws.fail.as<int32_t>(), ws.rpos.as<int32_t>(),
+                              ws.fail_cnt.as<int32_t>(), ws.st);
+    IvfRerunArgs ra{};
+    ra.rows = lists.rows.as<float>();
+    ra.live = lists.live.as<uint8_t>();
+    ra.labels = lists.labels.as<int64_t>();
+    ra.queries = d_q;
+    ra.probes = d_plan;
+    ra.nprobe = P;
+    ra.pstride = P + 1;
+    ra.lb = dlb.as<int32_t>();
+    ra.le = dle.as<int32_t>();
+    ra.fail = ws.fail.as<int32_t>();
+    ra.nfail = ws.fail_cnt.as<int32_t>();
+    ra.dim = dim;
+    ra.k = k;
+    ra.nchunk = (int32_t)std::max<int64_t>(1, std::min<int64_t>(64, (max_len + 1023) / 1024));
+    ra.rec = d_rec;
+    ra.rec_pos = ws.rpos.as<int32_t>();
+    ra.rec_lb = dlb.as<int32_t>();
+    ra.rec_nlist = coarse.nlist;
+    PhaseTimer t(PH_FALLBACK, ws.st);
+    ws.rrpart.ensure(sizeof(uint64_t) * ivf_rerun_part_keys(mf, P, k));
+    launch_ivf_exact_rerun(ra, metric, mf, ws.rrpart.as<uint64_t>(), ws.st);
+    HIPCHK(hipGetLastError());
   }
 
   // IvfFlatVectorIndex.Search (:147-231) with the list scan on the VALU, the reference's exact arithmetic

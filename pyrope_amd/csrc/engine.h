@@ -132,6 +132,7 @@ struct Workspace {
   DevMem tdbg;    // measurement only (PYR_STREAM_TIMING)
   DevMem vlb, vle, vcents;  // FLAT on the stream scan: its chunks as lists (FlatIndex::search_stream)
   DevMem cq, ccs, ccl, ccc;  // Cosine on the filter path: unit queries, inner-product candidates
+  DevMem shp, shthr, rpos;  // list-sharded search: unpacked plan (probes, T_q), re-run record slots
   const int32_t *ext_probes = nullptr;            // caller-ranked probe lists [nq][ext_nprobe] (multi-GPU)
   int32_t ext_nprobe = 0;
   // the re-run of certificate failures searches with its own buffers on the same stream
@@ -217,6 +218,35 @@ struct Index {
     (void)m;
     (void)ksub;
     throw Error(PYR_E_STATE, "index kind has no product quantizer");
+  }
+  // ---- list-sharded multi-GPU search (IVF_FLAT; engine.cpp IvfFlatIndex, shard.hip) ----
+  // the replicated sample of every list: rows [sum counts][dim] in list order, counts[l] <= 512 rows of list
+  // l (its first rows), glen[l] its full length on the rank that owns it
+  virtual void set_list_samples(const float *rows, const int64_t *counts, const int64_t *glen, int nlist) {
+    (void)rows;
+    (void)counts;
+    (void)glen;
+    (void)nlist;
+    throw Error(PYR_E_STATE, "index kind has no list-sharded search (IVF_FLAT only)");
+  }
+  // home side: coarse ranking + T_q of nq queries -> plan [nq][P + 1]; returns P
+  virtual int shard_prepare(const float *d_q, int64_t nq, int k, const pyr_search_params &p, int32_t *d_plan,
+                            Workspace &ws) {
+    (void)d_q, (void)nq, (void)k, (void)p, (void)d_plan, (void)ws;
+    throw Error(PYR_E_STATE, "index kind has no list-sharded search (IVF_FLAT only)");
+  }
+  // every rank: its owned lists against the plans -> one record per query
+  virtual void shard_search(const float *d_q, int64_t nq, int k, const int32_t *d_plan, int P, void *d_rec,
+                            Workspace &ws) {
+    (void)d_q, (void)nq, (void)k, (void)d_plan, (void)P, (void)d_rec, (void)ws;
+    throw Error(PYR_E_STATE, "index kind has no list-sharded search (IVF_FLAT only)");
+  }
+  // every rank: the exact re-run of the gathered failures [nranks][1 + fcap] -> records [nranks * fcap]
+  virtual void shard_rerun(const float *d_q, int64_t nq, int k, const int32_t *d_plan, int P, const int32_t *d_fails,
+                           int nranks, int fcap, int64_t nq_home, void *d_rec, Workspace &ws) {
+    (void)d_q, (void)nq, (void)k, (void)d_plan, (void)P, (void)d_fails, (void)nranks, (void)fcap, (void)nq_home;
+    (void)d_rec, (void)ws;
+    throw Error(PYR_E_STATE, "index kind has no list-sharded search (IVF_FLAT only)");
   }
   // capacity hint: room for `rows` more rows without re-allocation (bulk loads of 10^7-10^8 rows,
   // where a grow-by-copy would need the old and the new store at once)

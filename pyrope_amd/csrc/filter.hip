@@ -187,6 +187,35 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
     if (key != KEY_NONE && better(sc, kc, s, key)) ++rank;
   }
   const int nout = min(valid, k);
+  if (a.rec) {
+    // list-sharded search (shard.hip): this rank's exact top-k and the bound of every row it left out (the
+    // K1-th merged bound: candidates past it, the rows below T_q and a full buffer's floor all score at
+    // most that), no certificate here -- the home rank's merge certifies against every rank's bound
+    uint8_t *rp = static_cast<uint8_t *>(a.rec) + (size_t)q * shard_record_bytes(k);
+    ShardEntry *ent = reinterpret_cast<ShardEntry *>(rp);
+    if (key != KEY_NONE && rank < k) {
+      ShardEntry e;
+      e.label = a.row_labels ? a.row_labels[key] : (int64_t)key;
+      e.score = s;
+      e.list = shard_list_of(a.rec_lb, a.rec_nlist, key);
+      ent[rank] = e;
+    }
+    if (lane >= nout && lane < k) {
+      ShardEntry e;
+      e.label = -1;
+      e.score = -INFINITY;
+      e.list = 0x7FFFFFFF;
+      ent[lane] = e;
+    }
+    if (lane == 0) {
+      ShardTrailer t;
+      t.bound = mk[k1 - 1] != -1 ? ms[k1 - 1] : -INFINITY;
+      t.n = nout;
+      t.pad = 0;
+      *reinterpret_cast<ShardTrailer *>(rp + 16 * (size_t)k) = t;
+    }
+    return;
+  }
   if (key != KEY_NONE && rank < k) {
     a.out_s[(size_t)q * k + rank] = s;
     a.out_l[(size_t)q * k + rank] = a.row_labels ? a.row_labels[key] : (int64_t)key;

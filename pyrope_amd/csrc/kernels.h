@@ -167,6 +167,14 @@ struct IvfRerunArgs {
   float *out_s;
   int64_t *out_l;
   int32_t *out_c;
+  int32_t pstride;          // row stride of probes (0: nprobe; a shard plan's P + 1)
+  // list-sharded search (shard.hip): failing query i's answer goes to record rec_pos[i] of rec (ShardEntry
+  // x k + ShardTrailer, bound -inf: exact) instead of out_* at its row; rec_lb / rec_nlist: the list
+  // bounds that name each row's list
+  void *rec;
+  const int32_t *rec_pos;
+  const int32_t *rec_lb;
+  int32_t rec_nlist;
 };
 // part: ivf_rerun_part_keys() rank keys of scratch (one block per (failing query, probe, chunk), then
 // a merge per query)
@@ -386,6 +394,53 @@ struct PqRefineArgs {
   int32_t *fail_list, *fail_cnt;
 };
 void launch_pq32_refine(const PqRefineArgs &a, int64_t nq, hipStream_t st);
+// ---- list-sharded multi-GPU search (shard.hip; pyrope_amd/dist.py ListShardedIvf) ----
+// One query's answer from one rank: k entries in (score desc, list asc, label asc) order (unused: label -1,
+// score -inf), then the trailer: every row of the rank's probed lists that is not an entry scores at most
+// `bound` (-inf: none was left out), n = the real entries.
+struct ShardEntry {
+  int64_t label;
+  float score;
+  int32_t list;
+};
+struct ShardTrailer {
+  float bound;
+  int32_t n;
+  int64_t pad;
+};
+__host__ __device__ inline int64_t shard_record_bytes(int k) { return 16 * (int64_t)(k + 1); }
+// the list of storage slot `key`: the last list whose start is <= key (lists laid out by id, an empty list
+// shares its start with the next one)
+__device__ __forceinline__ int32_t shard_list_of(const int32_t *lb, int nlist, uint32_t key) {
+  int lo = 0, hi = nlist - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if ((uint32_t)lb[mid] <= key) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+struct ShardMergeArgs {
+  const uint8_t *rec;       // [nparts][nrec] records (part-major: an all_to_all's output)
+  int32_t nparts;           // 1 .. 64
+  int64_t nrec;             // records per part
+  int32_t k;
+  const int32_t *qsel;      // null: record i answers query i; else record i answers qsel[1 + i], i < min(qsel[0], cap)
+  int32_t cap;
+  float *out_s;             // [nq][k]
+  int64_t *out_l;
+  int32_t *out_c;           // may be null
+  int32_t *fail;            // null: no certificate; else fail[0] = failures (may exceed fcap), fail[1 ..] queries
+  int32_t fcap;
+};
+void launch_shard_merge(const ShardMergeArgs &a, int64_t max_rec, hipStream_t st);
+// plan [nq][P + 1] <-> probes [nq][P] + T_q [nq]
+void launch_pack_plan(const int32_t *probes, const float *thr, int64_t nq, int P, int32_t *plan, hipStream_t st);
+void launch_unpack_plan(const int32_t *plan, int64_t nq, int P, int32_t *probes, float *thr, hipStream_t st);
+// gathered fail lists [nranks][1 + fcap] -> global failing queries fail[], their record slots pos[], *nfail
+void launch_shard_fail_compact(const int32_t *fails, int nranks, int fcap, int64_t nq_home, int32_t *fail, int32_t *pos,
+                               int32_t *nfail, hipStream_t st);
+
 struct CandMergeArgs {
   const uint2 *cand;          // StreamArgs::cand / cand_n / cand_f
   const int32_t *cand_n;
@@ -415,7 +470,8 @@ void launch_iota_rows(int32_t *out, int64_t rows, int cols, hipStream_t st);
 void launch_scan_sample(const StreamArgs &a, int metric, int max_items, hipStream_t st);
 void launch_scan_main(const StreamArgs &a, int metric, int max_items, hipStream_t st);
 bool sample16_supported(int dim, int metric);  // dim == tile dim in {32, 64, 128}, L2 / IP
-void launch_sample16(const StreamArgs &a, int metric, int max_items, hipStream_t st);
+// prep_only: the query operands (bq, qsc) without the sample (a list-sharded scan takes T_q from its plan)
+void launch_sample16(const StreamArgs &a, int metric, int max_items, hipStream_t st, bool prep_only = false);
 // T_q per query: the R-th largest of its n sample values, R from the sampled fraction f of its probed
 // rows: R = clamp(ceil(et f), rmin, rmax) (rmin == rmax: fixed)
 struct StreamSelectArgs {
@@ -470,6 +526,12 @@ struct RefineArgs {
   int32_t *out_c;
   int32_t *fail_list;       // queries whose certificate failed
   int32_t *fail_cnt;
+  // list-sharded search (shard.hip; resid + ub only): query q's exact top-k and the bound of the rows it
+  // left out go to record q of rec instead of out_*, with no certificate here (the home rank's merge
+  // certifies); rec_lb / rec_nlist: the list bounds that name each candidate's list
+  void *rec;
+  const int32_t *rec_lb;
+  int32_t rec_nlist;
 };
 // unit rows (x / n, 0 when n < 1e-6 or not finite): blocked rows at slots (norms by slot), or row-major
 // x (norms[i]) when slots is null; out row-major n x dim; zflag (may be null) set to 1 by a zero row that

@@ -1421,7 +1421,7 @@ __global__ __launch_bounds__(256) void ivf_rerun_scan_kernel(IvfRerunArgs a, uin
       if (threadIdx.x < DT) qsh[threadIdx.x] = qp[threadIdx.x];
       __syncthreads();
     }
-    const int lst = a.probes[(size_t)q * a.nprobe + p];
+    const int lst = a.probes[(size_t)q * (a.pstride > 0 ? a.pstride : a.nprobe) + p];
     uint64_t cur = 0ull;  // lane j: the wave's j-th best so far
     if (lst >= 0) {
       const int b = a.lb[lst], e = a.le[lst];
@@ -1493,6 +1493,30 @@ __device__ void rerun_merge_one(IvfRerunArgs a, const uint64_t *part, int64_t i,
     cur = rr_merge64_desc(cur > rv ? cur : rv, lane);
   }
   const uint64_t real = __builtin_amdgcn_ballot_w64(lane < k && cur != 0ull);
+  if (a.rec) {  // list-sharded re-run (shard.hip): the exact local top-k as record rec_pos[i], bound -inf
+    uint8_t *rp = static_cast<uint8_t *>(a.rec) + (size_t)a.rec_pos[i] * shard_record_bytes(k);
+    if (lane < k) {
+      ShardEntry e;
+      e.label = -1;
+      e.score = -INFINITY;
+      e.list = 0x7FFFFFFF;
+      if (cur != 0ull) {
+        const uint32_t slot = ~(uint32_t)cur;
+        e.label = a.labels[slot];
+        e.score = key_score((uint32_t)(cur >> 32));
+        e.list = shard_list_of(a.rec_lb, a.rec_nlist, slot);
+      }
+      reinterpret_cast<ShardEntry *>(rp)[lane] = e;
+    }
+    if (lane == 0) {
+      ShardTrailer t;
+      t.bound = -INFINITY;
+      t.n = (int32_t)__builtin_popcountll(real);
+      t.pad = 0;
+      *reinterpret_cast<ShardTrailer *>(rp + 16 * (size_t)k) = t;
+    }
+    return;
+  }
   if (lane < k) {
     float s = -INFINITY;
     int64_t lab = -1;

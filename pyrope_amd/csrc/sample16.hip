@@ -362,12 +362,14 @@ int device_cus() {
 
 bool sample16_supported(int dim, int metric) { return (metric == L2 || metric == IP) && (dim == 32 || dim == 64 || dim == 128); }
 
-void launch_sample16(const StreamArgs &a, int metric, int max_items, hipStream_t st) {
+void launch_sample16(const StreamArgs &a, int metric, int max_items, hipStream_t st, bool prep_only) {
   if (max_items <= 0) return;
   const int split = a.dim == 32 ? SPREP_SPLIT<32> : a.dim == 64 ? SPREP_SPLIT<64> : SPREP_SPLIT<128>;
   auto prep = [&](auto kern) { hipLaunchKernelGGL(kern, dim3((unsigned)((int64_t)max_items * split)), dim3(256), 0, st, a); };
   const dim3 grid(std::max(1, std::min(max_items, device_cus())));
-  auto samp = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(64 * SNW), 0, st, a); };
+  auto samp = [&](auto kern) {
+    if (!prep_only) hipLaunchKernelGGL(kern, grid, dim3(64 * SNW), 0, st, a);
+  };
   switch (a.dim) {
     case 32:
       metric == L2 ? prep(sprep_kernel<32, L2>) : prep(sprep_kernel<32, IP>);

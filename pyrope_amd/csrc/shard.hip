@@ -1,0 +1,175 @@
+// shard.hip -- the device side of the list-sharded multi-GPU search (IVF lists shard
+// whole across the GPUs; pyrope_amd/dist.py ListShardedIvf drives it).
+//
+// A query's home rank ranks the coarse quantizer and computes its threshold T_q from a replicated sample of
+// every list (the plan: P probe ids + T_q as float bits); every rank scans the (query, list) pairs whose
+// list it owns against the gathered plans and writes one RECORD per query: its exact local top-k and the
+// bound B_r every row it left out scores at most.  The home merges the records of all ranks and
+// certifies: the k-th merged score must beat every B_r, else the query is re-run exactly on every rank.
+//
+// Records (ShardEntry x k, then ShardTrailer; shard_record_bytes(k) = 16 (k + 1)): entries in the order
+// (score desc, list asc, label asc) -- the unsharded index's tie order, since a list keeps its rows in label
+// order on the rank that owns it and lists are laid out by id.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <stdexcept>
+
+#include "kernels.h"
+
+namespace pyr {
+namespace {
+
+inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
+
+// (score desc, list asc, label asc); NaN ranks below every number (as better() in the scans)
+__device__ __forceinline__ bool entry_better(float s1, int32_t l1, int64_t b1, float s2, int32_t l2, int64_t b2) {
+  if (isnan(s2) && !isnan(s1)) return true;
+  if (isnan(s1)) return false;
+  return s1 > s2 || (s1 == s2 && (l1 < l2 || (l1 == l2 && b1 < b2)));
+}
+
+// plan [nq][P + 1] = P probe ids, then T_q's float bits
+__global__ void pack_plan_kernel(const int32_t *probes, const float *thr, int64_t nq, int P, int32_t *plan) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nq * (P + 1)) return;
+  const int64_t q = e / (P + 1);
+  const int c = (int)(e - q * (P + 1));
+  plan[e] = c < P ? probes[q * P + c] : __float_as_int(thr[q]);
+}
+__global__ void unpack_plan_kernel(const int32_t *plan, int64_t nq, int P, int32_t *probes, float *thr) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nq * (P + 1)) return;
+  const int64_t q = e / (P + 1);
+  const int c = (int)(e - q * (P + 1));
+  if (c < P) probes[q * P + c] = plan[e];
+  else thr[q] = __int_as_float(plan[e]);
+}
+
+// One wave per record index i: a k-step merge of the nparts sorted entry lists (lane s holds the head of
+// part s), then the certificate.
+__global__ __launch_bounds__(256) void shard_merge_kernel(ShardMergeArgs a) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + w;
+  int64_t n = a.nrec;
+  if (a.qsel) n = min((int64_t)a.qsel[0], (int64_t)a.cap);
+  if (i >= n) return;
+  const int64_t q = a.qsel ? a.qsel[1 + i] : i;
+  const int k = a.k;
+  const int64_t rb = shard_record_bytes(k);
+  const bool mine = lane < a.nparts;
+  const uint8_t *rec = a.rec + ((size_t)(mine ? lane : 0) * a.nrec + i) * rb;
+  const ShardEntry *ent = reinterpret_cast<const ShardEntry *>(rec);
+  const ShardTrailer tr = *reinterpret_cast<const ShardTrailer *>(rec + 16 * (size_t)k);
+  float bound = mine ? tr.bound : -INFINITY;
+  const int cnt = mine ? min(tr.n, k) : 0;
+  int head = 0;
+  int produced = 0;
+  float kth = -INFINITY;
+  for (int r = 0; r < k; ++r) {
+    const bool has = head < cnt;
+    ShardEntry e;
+    if (has) e = ent[head];
+    float s = has ? e.score : -INFINITY;
+    int32_t l = has ? e.list : 0x7FFFFFFF;
+    int64_t b = has ? e.label : INT64_MAX;
+    int src = has ? lane : 64;
+    // wave argmax under entry_better (ties between parts cannot happen: a row lives on one rank)
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const float s2 = __shfl_xor(s, off);
+      const int32_t l2 = __shfl_xor(l, off);
+      const int64_t b2 = __shfl_xor(b, off);
+      const int src2 = __shfl_xor(src, off);
+      const bool take = src2 < 64 && (src == 64 || entry_better(s2, l2, b2, s, l, b) ||
+                                      (!entry_better(s, l, b, s2, l2, b2) && src2 < src));
+      if (take) {
+        s = s2;
+        l = l2;
+        b = b2;
+        src = src2;
+      }
+    }
+    if (src == 64) break;  // every part is exhausted
+    if (lane == src) ++head;
+    if (lane == 0) {
+      a.out_s[(size_t)q * k + r] = s;
+      a.out_l[(size_t)q * k + r] = b;
+    }
+    kth = s;
+    ++produced;
+  }
+  if (lane == 0)
+    for (int r = produced; r < k; ++r) {
+      a.out_s[(size_t)q * k + r] = -INFINITY;
+      a.out_l[(size_t)q * k + r] = -1;
+    }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) bound = fmaxf(bound, __shfl_xor(bound, off));
+  if (lane == 0) {
+    if (a.out_c) a.out_c[q] = produced;
+    if (a.fail) {
+      // every row a rank left out scores <= its bound: the merged top-k is exact when its k-th score beats
+      // every bound (or nothing was left out anywhere)
+      const bool ok = bound == -INFINITY || (produced == k && kth > bound);
+      if (!ok) {
+        const int at = atomicAdd(a.fail, 1);
+        if (at < a.fcap) a.fail[1 + at] = (int32_t)q;
+      }
+    }
+  }
+}
+
+// gathered fail lists [nranks][1 + fcap] (home-local query ids) -> the global failing queries in rank
+// order: fail[i] = s * nq_home + id, pos[i] = s * fcap + j (the record slot of the re-run's answer for
+// home s), *nfail = their count.  One block.
+__global__ __launch_bounds__(256) void shard_fail_compact_kernel(const int32_t *fails, int nranks, int fcap,
+                                                                int64_t nq_home, int32_t *fail, int32_t *pos,
+                                                                int32_t *nfail) {
+  __shared__ int base[65];
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int s = 0; s < nranks; ++s) {
+      base[s] = t;
+      t += min(max(fails[(size_t)s * (1 + fcap)], 0), fcap);
+    }
+    base[nranks] = t;
+    *nfail = t;
+  }
+  __syncthreads();
+  for (int s = 0; s < nranks; ++s) {
+    const int c = base[s + 1] - base[s];
+    for (int j = threadIdx.x; j < c; j += blockDim.x) {
+      fail[base[s] + j] = (int32_t)(s * nq_home + fails[(size_t)s * (1 + fcap) + 1 + j]);
+      pos[base[s] + j] = s * fcap + j;
+    }
+  }
+}
+
+}  // namespace
+
+void launch_pack_plan(const int32_t *probes, const float *thr, int64_t nq, int P, int32_t *plan, hipStream_t st) {
+  if (nq <= 0) return;
+  hipLaunchKernelGGL(pack_plan_kernel, dim3(nblk(nq * (P + 1), 256)), dim3(256), 0, st, probes, thr, nq, P, plan);
+}
+void launch_unpack_plan(const int32_t *plan, int64_t nq, int P, int32_t *probes, float *thr, hipStream_t st) {
+  if (nq <= 0) return;
+  hipLaunchKernelGGL(unpack_plan_kernel, dim3(nblk(nq * (P + 1), 256)), dim3(256), 0, st, plan, nq, P, probes, thr);
+}
+void launch_shard_merge(const ShardMergeArgs &a, int64_t max_rec, hipStream_t st) {
+  if (max_rec <= 0 || a.k <= 0) return;
+  if (a.nparts < 1 || a.nparts > 64) throw std::invalid_argument("shard merge: 1 to 64 parts");
+  hipLaunchKernelGGL(shard_merge_kernel, dim3(nblk(max_rec, 4)), dim3(256), 0, st, a);
+}
+void launch_shard_fail_compact(const int32_t *fails, int nranks, int fcap, int64_t nq_home, int32_t *fail, int32_t *pos,
+                               int32_t *nfail, hipStream_t st) {
+  if (nranks < 1 || nranks > 64) throw std::invalid_argument("shard re-run: 1 to 64 ranks");
+  hipLaunchKernelGGL(shard_fail_compact_kernel, dim3(1), dim3(256), 0, st, fails, nranks, fcap, nq_home, fail, pos,
+                     nfail);
+}
+
+}  // namespace pyr

@@ -1,6 +1,13 @@
 """Multi-GPU orchestration of the sharded scan (one process per GPU, torch.distributed).
 
-Sharding (option ii "rows within lists"): the base set is cut into
+Two partitions are implemented:
+
+* LIST-SHARDED (north_star's "IVF lists shard naturally across the GPUs"; the
+  default of bench.py since round 5): ListShardedIvf below.  Every rank owns whole lists (a size-balanced
+  assignment, list_owners), so each (query, list) pair is scanned by one rank and a rank's per-query work
+  shrinks as N grows.
+
+* rows within lists (option ii, rounds 1-4; ShardedIvfStep): the base set is cut into
 generator blocks of BLOCK_ROWS rows and rank r holds every block b with b % world == r
 (shard_blocks).  Every rank builds its shard with the SAME coarse quantizer (trained once
 and broadcast), so each rank's lists are row subsets of the unsharded lists, in the same
@@ -185,3 +192,297 @@ def rank_memory_plan(dim: int, nrows: int, nlist: int, max_list_len: int, nq: in
     ib, wb = C.c_int64(), C.c_int64()
     _lib.check(L.pyr_ivf_memory_plan(dim, nrows, nlist, max_list_len, nq, nprobe, k, C.byref(ib), C.byref(wb)))
     return ib.value, wb.value
+
+
+# =============================================================================================
+# List-sharded IVF_FLAT (C ABI: include/pyrope_ann.h "List-sharded multi-GPU")
+# =============================================================================================
+SAMPLE_ROWS = 512  # rows of every list replicated for the home rank's threshold (sample16.hip: 16 tiles)
+
+
+def list_owners(list_len, world: int) -> np.ndarray:
+    """Size-balanced owner of every list: lists by length (desc, ties by id) to the rank with the fewest rows
+    so far (ties: lowest rank) -- deterministic, so every rank computes the same table."""
+    import heapq
+
+    n = len(list_len)
+    owner = np.zeros(n, np.int32)
+    heap = [(0, r) for r in range(world)]
+    for l in sorted(range(n), key=lambda i: (-int(list_len[i]), i)):
+        load, r = heapq.heappop(heap)
+        owner[l] = r
+        heapq.heappush(heap, (load + int(list_len[l]), r))
+    return owner
+
+
+class Comm:
+    """The collectives of the list-sharded step over torch.distributed: RCCL ("nccl") works on CUDA tensors,
+    gloo on CPU tensors; a tensor on the other side is staged (the one-GPU gloo rehearsal stages CUDA
+    tensors through the host, a host-side row exchange under RCCL goes through the GPU).  world == 1:
+    plain copies."""
+
+    def __init__(self, world: int):
+        self.world = world
+
+    def _dev(self):
+        import torch
+        import torch.distributed as dist
+        if dist.get_backend() == "nccl":
+            return torch.device("cuda", torch.cuda.current_device())
+        return torch.device("cpu")
+
+    def _run(self, fn, out, *ins):
+        d = self._dev()
+        o = out if out.device == d else out.to(d)
+        i = [t.contiguous() if t.device == d else t.to(d).contiguous() for t in ins]
+        fn(o, *i)
+        if o is not out:
+            out.copy_(o)
+        return out
+
+    def all_gather_into(self, out, t):
+        """t [rows, ...] of every rank -> out [world * rows, ...] in rank order."""
+        import torch.distributed as dist
+        if self.world == 1:
+            return out.copy_(t)
+        if dist.get_backend() == "nccl":
+            return self._run(lambda o, i: dist.all_gather_into_tensor(o, i), out, t)
+        return self._run(lambda o, i: dist.all_gather(list(o.view((self.world,) + tuple(i.shape)).unbind(0)), i), out, t)
+
+    def all_to_all_single(self, out, t):
+        """Equal splits: rows [r * n / world, ...) of t go to rank r; out holds what every rank sent here."""
+        import torch.distributed as dist
+        if self.world == 1:
+            return out.copy_(t)
+        return self._run(lambda o, i: dist.all_to_all_single(o, i), out, t)
+
+    def all_reduce_sum(self, t):
+        import torch.distributed as dist
+        if self.world == 1:
+            return t
+        return self._run(lambda o, i: (o.copy_(i), dist.all_reduce(o)), t, t)
+
+    def all_to_all_v(self, t, send_counts):
+        """Rows of t ([n, ...], grouped by destination rank, send_counts[r] rows to rank r) -> the rows every
+        rank sent here, in source-rank order, and their counts."""
+        import torch
+        import torch.distributed as dist
+        if self.world == 1:
+            return t.clone(), list(send_counts)
+        sc = torch.tensor(send_counts, dtype=torch.int64)
+        rc = torch.empty_like(sc)
+        self._run(lambda o, i: dist.all_to_all_single(o, i), rc, sc)
+        out = torch.empty((int(rc.sum()),) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        self._run(lambda o, i: dist.all_to_all_single(o, i, output_split_sizes=rc.tolist(),
+                                                      input_split_sizes=sc.tolist()), out, t)
+        return out, rc.tolist()
+
+    def max_int(self, v: int, rank: int) -> int:
+        import torch
+        t = torch.zeros(self.world, dtype=torch.int64)
+        t[rank] = int(v)
+        return int(self.all_reduce_sum(t).max())
+
+
+class DeviceShardEngine:
+    """The list-sharded step's per-rank operations on libpyrope_hip (IVF_FLAT shard index, device buffers
+    as torch tensors, one stream)."""
+
+    def __init__(self, index, k: int, options=None, stream: int = 0):
+        self.index, self.k, self.options, self.stream = index, k, options, stream
+
+    def prepare(self, q_home, plan):
+        return self.index.shard_prepare_device(q_home.data_ptr(), q_home.shape[0], self.k, plan.data_ptr(),
+                                               self.stream, self.options)
+
+    def search(self, q_all, plan_all, width, rec):
+        self.index.shard_search_device(q_all.data_ptr(), q_all.shape[0], self.k, plan_all.data_ptr(), width,
+                                       rec.data_ptr(), self.stream)
+
+    def merge(self, rec_parts, out_s, out_l, fail):
+        from . import _lib
+        world, n = rec_parts.shape[0], rec_parts.shape[1]
+        _lib.check(_lib.load().pyr_shard_merge_device(rec_parts.data_ptr(), world, n, self.k, None, 0,
+                                                      out_s.data_ptr(), out_l.data_ptr(), None, fail.data_ptr(),
+                                                      fail.shape[0] - 1, self.stream))
+
+    def rerun(self, q_all, plan_all, width, fails_all, nq_home, rec):
+        world, f1 = fails_all.shape
+        self.index.shard_rerun_device(q_all.data_ptr(), q_all.shape[0], self.k, plan_all.data_ptr(), width,
+                                      fails_all.data_ptr(), world, f1 - 1, nq_home, rec.data_ptr(), self.stream)
+
+    def merge_rerun(self, rec_parts, fail_home, out_s, out_l):
+        from . import _lib
+        world, fcap = rec_parts.shape[0], rec_parts.shape[1]
+        _lib.check(_lib.load().pyr_shard_merge_device(rec_parts.data_ptr(), world, fcap, self.k, fail_home.data_ptr(),
+                                                      fcap, out_s.data_ptr(), out_l.data_ptr(), None, None, 0,
+                                                      self.stream))
+
+
+class ListShardedIvf:
+    """One list-sharded multi-GPU IVF_FLAT search step (include/pyrope_ann.h "List-sharded multi-GPU"):
+
+      1. plan: the home rank ranks the quantizer for its nq_local queries and takes T_q from its replicated
+         sample of every list (engine.prepare);
+      2. all_gather(plans): every rank gets every query's probe lists and threshold;
+      3. every rank scans the (query, list) pairs of the lists it owns -> one record per query (exact local
+         top-k + the bound of the rows it left out; engine.search);
+      4. all_to_all(records): each home receives its queries' records from every rank;
+      5. the home merges and certifies (k-th merged score > every rank's bound; engine.merge);
+      6. all_gather(fail lists) [world][1 + fcap];
+      7. every rank runs the exact scan of the failures over its lists (engine.rerun);
+      8. all_to_all(re-run records) and the home merges them into its results (engine.merge_rerun).
+
+    Steps 6-8 always run (their buffers are small and fixed: fcap failures per home), so the step needs no
+    host synchronisation.  A home with more than fcap failures sets `overflow` (the device count exceeds
+    fcap); check_overflow() reads it (host sync) and step(..., validate=True) re-runs the excess.
+    All buffers are allocated once (torch tensors on `device`).
+    """
+
+    def __init__(self, engine, comm, nq_local: int, k: int, width: int, rank: int, world: int, device=None,
+                 fcap: int = 256):
+        import torch
+
+        self.engine, self.comm = engine, comm
+        self.nq, self.k, self.width, self.rank, self.world, self.fcap = nq_local, k, width, rank, world, fcap
+        rb = 16 * (k + 1)
+        Q = nq_local * world
+        self.plan_home = torch.empty((nq_local, width + 1), dtype=torch.int32, device=device)
+        self.plan_all = torch.empty((Q, width + 1), dtype=torch.int32, device=device)
+        self.rec = torch.empty((Q, rb), dtype=torch.uint8, device=device)
+        self.rec_home = torch.empty((world, nq_local, rb), dtype=torch.uint8, device=device)
+        self.fail_home = torch.zeros((1 + fcap,), dtype=torch.int32, device=device)
+        self.fail_all = torch.zeros((world, 1 + fcap), dtype=torch.int32, device=device)
+        self.rrec = torch.zeros((world * fcap, rb), dtype=torch.uint8, device=device)
+        self.rrec_home = torch.zeros((world, fcap, rb), dtype=torch.uint8, device=device)
+        self.out_s = torch.empty((nq_local, k), dtype=torch.float32, device=device)
+        self.out_l = torch.empty((nq_local, k), dtype=torch.int64, device=device)
+        self.max_fail = torch.zeros((1,), dtype=torch.int32, device=device)  # the most failures of one step
+        self.timing = False
+        self.collective_ms = {}
+
+    def _timed(self, name, fn):
+        return ShardedIvfStep._timed(self, name, fn)
+
+    @property
+    def probes_all(self):  # ShardedIvfStep._timed checks .is_cuda on it
+        return self.plan_all
+
+    def __call__(self, q_all, validate: bool = False):
+        nq, w, r = self.nq, self.world, self.rank
+        e, c = self.engine, self.comm
+        q_home = q_all[r * nq:(r + 1) * nq]
+        P = e.prepare(q_home, self.plan_home)
+        if P != self.width:
+            raise ValueError(f"plan width {P} != {self.width}")
+        self._timed("plan_allgather", lambda: c.all_gather_into(self.plan_all, self.plan_home))
+        e.search(q_all, self.plan_all, P, self.rec)
+        self._timed("record_alltoall", lambda: c.all_to_all_single(self.rec_home.view(w * nq, -1), self.rec))
+        e.merge(self.rec_home, self.out_s, self.out_l, self.fail_home)
+        self._timed("fail_allgather", lambda: c.all_gather_into(self.fail_all, self.fail_home))
+        e.rerun(q_all, self.plan_all, P, self.fail_all, nq, self.rrec)
+        self._timed("rerun_alltoall", lambda: c.all_to_all_single(self.rrec_home.view(w * self.fcap, -1), self.rrec))
+        e.merge_rerun(self.rrec_home, self.fail_home, self.out_s, self.out_l)
+        import torch
+        torch.maximum(self.max_fail, self.fail_home[:1], out=self.max_fail)
+        if validate and self.check_overflow():
+            raise RuntimeError(f"more than {self.fcap} certificate failures at one home rank in a step: rerun with a "
+                               f"larger fcap")
+        return self.out_s, self.out_l
+
+    def check_overflow(self) -> bool:
+        """True if any step so far had more certificate failures at this home than fcap (host sync)."""
+        return int(self.max_fail.max().item()) > self.fcap
+
+
+def exchange_rows(comm, rank: int, world: int, chunks, centroids, metric, owner_of=None, device: int = 0,
+                  add=None, assign_fn=None):
+    """Give every rank its WHOLE lists.
+
+    chunks(): iterator over this rank's (labels, rows) in label order, the same number of calls on every rank
+    per round (bench.py shard_chunks: round i of every rank covers one contiguous range of generator blocks).
+    Pass 1 assigns every row to its list (KMeansUtils.FindNearestCentroid, assign_fn) and sums the list
+    lengths over the ranks; owners come from list_owners unless owner_of is given.  Pass 2 sends each row to
+    its list's owner (all_to_all_v) round by round; the receiver sorts a round by label, so every list gets
+    its rows in label order -- the unsharded index's list order -- and hands them to add(labels, rows).
+    The first SAMPLE_ROWS rows of each owned list are kept for the replicated sample.
+
+    Returns (list_len [nlist] int64, owner [nlist] int32, samples {list: rows}) of this rank."""
+    import torch
+
+    if assign_fn is None:
+        from .vector import assign as assign_fn_dev
+
+        def assign_fn(c, x):
+            return assign_fn_dev(c, x, metric, device)
+    nl = centroids.shape[0]
+    counts = np.zeros(nl, np.int64)
+    asg_rounds = []
+    for labs, x in chunks():
+        a = assign_fn(centroids, x)
+        asg_rounds.append(a)
+        counts += np.bincount(a, minlength=nl)
+    rounds = comm.max_int(len(asg_rounds), rank)  # a rank with fewer rounds sends nothing in the last ones
+    glen_t = torch.from_numpy(counts.copy())
+    comm.all_reduce_sum(glen_t)
+    glen = glen_t.numpy().astype(np.int64)
+    owner = list_owners(glen, world) if owner_of is None else np.asarray(owner_of, np.int32)
+    samples = {}
+    dim = centroids.shape[1]
+
+    def padded():
+        yield from zip(chunks(), asg_rounds)
+        for _ in range(rounds - len(asg_rounds)):
+            yield (np.zeros(0, np.int64), np.zeros((0, dim), np.float32)), np.zeros(0, np.int32)
+
+    for (labs, x), a in padded():
+        dst = owner[a]
+        order = np.argsort(dst, kind="stable")
+        send = np.bincount(dst, minlength=world).tolist()
+        payload = np.concatenate([x[order], labs[order].astype(np.int64).view(np.float32).reshape(-1, 2),
+                                  a[order].astype(np.int32).view(np.float32).reshape(-1, 1)], axis=1)
+        got, _ = comm.all_to_all_v(torch.from_numpy(np.ascontiguousarray(payload)), send)
+        got = got.numpy()
+        d = x.shape[1]
+        rl = np.ascontiguousarray(got[:, d:d + 2]).view(np.int64).reshape(-1)
+        ra = np.ascontiguousarray(got[:, d + 2:d + 3]).view(np.int32).reshape(-1)
+        o = np.argsort(rl, kind="stable")
+        rl, ra, rx = rl[o], ra[o], np.ascontiguousarray(got[o, :d])
+        if add is not None and len(rl):
+            add(rl, rx)
+        for li in np.unique(ra):
+            have = samples.get(int(li))
+            n0 = 0 if have is None else len(have)
+            if n0 >= SAMPLE_ROWS:
+                continue
+            rows = rx[ra == li][:SAMPLE_ROWS - n0]
+            samples[int(li)] = rows if have is None else np.concatenate([have, rows])
+    return glen, owner, samples
+
+
+def gather_samples(comm, rank: int, world: int, glen, owner, samples, dim: int):
+    """All ranks' owned-list samples -> (rows [sum counts, dim] in list order, counts [nlist]) everywhere."""
+    import torch
+
+    nl = len(glen)
+    mine = [l for l in range(nl) if owner[l] == rank]
+    block = np.concatenate([samples.get(l, np.zeros((0, dim), np.float32)) for l in mine]) if mine else \
+        np.zeros((0, dim), np.float32)
+    n_t = torch.tensor([block.shape[0]], dtype=torch.int64)
+    sizes = torch.zeros(world, dtype=torch.int64)
+    sizes[rank] = n_t[0]
+    comm.all_reduce_sum(sizes)
+    smax = int(sizes.max())
+    pad = np.zeros((max(smax, 1), dim), np.float32)
+    pad[:block.shape[0]] = block
+    allb = torch.empty((world, max(smax, 1), dim), dtype=torch.float32)
+    comm.all_gather_into(allb.view(world * max(smax, 1), dim), torch.from_numpy(pad))
+    allb = allb.numpy()
+    counts = np.minimum(np.asarray(glen, np.int64), SAMPLE_ROWS)
+    pos = np.zeros(world, np.int64)
+    out = []
+    for l in range(nl):  # each rank's block holds its owned lists in id order
+        o = int(owner[l])
+        out.append(allb[o, pos[o]:pos[o] + counts[l]])
+        pos[o] += counts[l]
+    return (np.concatenate(out) if out else np.zeros((0, dim), np.float32)), counts

@@ -254,6 +254,40 @@ class HipVectorIndex(IVectorIndex):
                                              C.byref(out), C.c_void_p(stream or None)))
         return out.value
 
+    # ---- list-sharded multi-GPU search (IVF_FLAT; pyrope_amd/dist.py ListShardedIvf) ----
+    def set_list_samples(self, rows: np.ndarray, counts: np.ndarray, list_len: np.ndarray) -> None:
+        """The replicated sample of every list: its first counts[l] <= 512 rows (in list order,
+        concatenated) and list_len[l], its full length on the rank that owns it."""
+        rows = np.ascontiguousarray(rows, dtype=np.float32).reshape(-1, self.dimension)
+        counts = np.ascontiguousarray(counts, dtype=np.int64)
+        list_len = np.ascontiguousarray(list_len, dtype=np.int64)
+        if counts.sum() != rows.shape[0] or len(list_len) != len(counts):
+            raise ArgumentException("sample rows do not match their counts")
+        check(self._L.pyr_index_set_list_samples(self._h, ptr(rows, C.c_float), ptr(counts, C.c_int64),
+                                                 ptr(list_len, C.c_int64), len(counts)))
+
+    def shard_prepare_device(self, d_q: int, nq: int, top_k: int, d_plan: int, stream: int = 0,
+                             options: Optional[SearchOptions] = None) -> int:
+        """Home rank: coarse ranking + T_q -> plan [nq][P + 1] at d_plan; returns P."""
+        p = self._params(options)
+        out = C.c_int32()
+        check(self._L.pyr_index_shard_prepare_device(self._h, C.c_void_p(d_q), nq, int(top_k), C.byref(p),
+                                                     C.c_void_p(d_plan), C.byref(out), C.c_void_p(stream or None)))
+        return out.value
+
+    def shard_search_device(self, d_q: int, nq: int, top_k: int, d_plan: int, width: int, d_records: int,
+                            stream: int = 0) -> None:
+        """Every rank: its owned lists against the gathered plans -> one record per query."""
+        check(self._L.pyr_index_shard_search_device(self._h, C.c_void_p(d_q), nq, int(top_k), C.c_void_p(d_plan),
+                                                    int(width), C.c_void_p(d_records), C.c_void_p(stream or None)))
+
+    def shard_rerun_device(self, d_q: int, nq: int, top_k: int, d_plan: int, width: int, d_fails: int, nranks: int,
+                           fcap: int, nq_home: int, d_records: int, stream: int = 0) -> None:
+        """Every rank: exact answers to the gathered failures [nranks][1 + fcap] -> records [nranks * fcap]."""
+        check(self._L.pyr_index_shard_rerun_device(self._h, C.c_void_p(d_q), nq, int(top_k), C.c_void_p(d_plan),
+                                                   int(width), C.c_void_p(d_fails), int(nranks), int(fcap),
+                                                   int(nq_home), C.c_void_p(d_records), C.c_void_p(stream or None)))
+
     def set_centroids(self, centroids: np.ndarray) -> None:
         """Supply the coarse quantizer used by the next build() (pyr_index_set_centroids)."""
         c = np.ascontiguousarray(centroids, dtype=np.float32).reshape(-1, self.dimension)
@@ -615,6 +649,17 @@ def kmeans_train(data: np.ndarray, k: int, metric: VectorMetric, max_iter: int =
     check(_lib.load().pyr_kmeans_train(device, ptr(x, C.c_float), n, dim, k, int(metric), max_iter, seed,
                                        ptr(out, C.c_float), C.byref(used)))
     return out[: used.value]
+
+
+def assign(centroids: np.ndarray, x: np.ndarray, metric: VectorMetric, device: int = 0) -> np.ndarray:
+    """KMeansUtils.FindNearestCentroid (KMeansUtils.cs:70-93) of every row of x on the GPU (pyr_assign):
+    the list IvfFlatVectorIndex.Build puts it in (ties -> lowest index)."""
+    c = np.ascontiguousarray(centroids, dtype=np.float32)
+    x = np.ascontiguousarray(x, dtype=np.float32).reshape(-1, c.shape[1])
+    out = np.empty(x.shape[0], np.int32)
+    check(_lib.load().pyr_assign(device, ptr(c, C.c_float), c.shape[0], ptr(x, C.c_float), x.shape[0], c.shape[1],
+                                 int(metric), ptr(out, C.c_int32)))
+    return out
 
 
 def scalar_quantize(x: np.ndarray, device: int = 0) -> np.ndarray:
