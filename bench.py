@@ -11,13 +11,17 @@ A step = one batched search of 10,000 queries per GPU, queries and results resid
 
 --gpus N: one process per GPU.  Launched by torch.distributed.run (RANK/WORLD_SIZE set) the
 ranks are used as they are; `python bench.py --gpus N` alone starts the N rank processes
-itself (spawn, before anything touches a GPU).  The base set is sharded by generator blocks
-(rank r owns the blocks b % N == r and generates only those), the coarse quantizer is trained
-once on rank 0 and broadcast, and each step runs pyrope_amd.dist.sharded_ivf_step: every rank
-ranks the quantizer for its 10,000-query slice, an RCCL all_gather assembles the probe lists,
-every rank scans its shard for the whole N x 10,000 batch, and an RCCL all_gather of the
-partial top-k plus an on-device merge gives the answer.  Per-GPU work is fixed as N grows
-("weak").
+itself (spawn, before anything touches a GPU).  The coarse quantizer is trained once on rank 0 and
+broadcast; rank r generates the generator blocks b % N == r.  Default partition (--shard lists,
+SURVEY.md 8(e)(i)): IVF lists shard WHOLE across the ranks (size-balanced, dist.list_owners); the
+rows are exchanged to their list's owner (RCCL all_to_all, label order kept) and every rank holds a
+replicated sample of every list.  A step (pyrope_amd.dist.ListShardedIvf) plans each rank's 10,000
+home queries (coarse ranking + threshold), all_gathers the plans, scans on every rank only the
+(query, list) pairs of its own lists, all_to_alls one record per query (exact local top-k + bound)
+to the query's home, merges + certifies there, and re-runs the (rare) failures exactly -- 4 RCCL
+collectives, the device work between them replayed from hipGraphs.  --shard rows: round 4's
+rows-within-list shards (every rank searches every query; A/B only).  Per-GPU queries are fixed
+as N grows ("weak").
 
 Besides the QPS line the JSON carries:
   roofline      the dominant kernel (IVF list scan) timed with HIP events on its own stream:
@@ -71,6 +75,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline time (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use")
     ap.add_argument("--profile-steps", type=int, default=3)
+    ap.add_argument("--shard", choices=["lists", "rows"], default="lists",
+                    help="N > 1 partition: whole IVF lists per rank (default) or rows within lists (round 4, A/B)")
+    ap.add_argument("--fcap", type=int, default=256, help="list-sharded: certificate failures a home re-runs per step")
     ap.add_argument("--graph", type=int, default=1,
                     help="N = 1: replay each step from a HIP graph of the whole search (1, default) or launch it "
                          "kernel by kernel (0); every replay runs every kernel of the search")
@@ -175,7 +182,8 @@ def run(args):
     from pyrope_amd import (BruteForceVectorIndex, IvfFlatVectorIndex, VectorMetric, _lib, generate_synthetic,
                             generate_synthetic_blocked, kmeans_train)
     from pyrope_amd.build import build
-    from pyrope_amd.dist import ShardedIvfStep, all_gather_rows, gather_partials, merge_device, shard_blocks
+    from pyrope_amd.dist import (Comm, DeviceShardEngine, ListShardedIvf, ShardedIvfStep, all_gather_rows,
+                                 exchange_rows, gather_partials, gather_samples, merge_device, shard_blocks)
     from pyrope_amd.vector import SearchOptions
     build()
     L = _lib.load()
@@ -220,14 +228,34 @@ def run(args):
     keep = world == 1 and args.cpu_seconds > 0  # the CPU baseline reads base rows
     kept = []
     nrows = 0
-    for labs, x in shard_chunks():
-        idx.add_labels(labs, x, track_ids=False)
-        nrows += len(labs)
-        if keep:
-            kept.append(x)
-        if nrows % (5 * args.add_rows) < len(labs):  # progress for long (M8-size) loads
-            log(f"rank {rank}: {nrows} rows added ({time.time() - t:.0f}s)")
-    idx.build()
+    lists_sharded = world > 1 and args.shard == "lists"
+    comm = Comm(world)
+    if lists_sharded:
+        # whole lists: every row to its list's owner (label order kept), then the replicated list samples
+        added = [0]
+
+        def add(labs, x):
+            idx.add_labels(labs, x, track_ids=False)
+            added[0] += len(labs)
+        glen, owner, samples = exchange_rows(comm, rank, world, shard_chunks, cents, VectorMetric.L2, device=local,
+                                             add=add)
+        nrows = added[0]
+        idx.build()
+        srows, scounts = gather_samples(comm, rank, world, glen, owner, samples, D)
+        idx.set_list_samples(srows, scounts, glen)
+        del srows, samples
+        log(f"rank {rank}: {int((owner == rank).sum())} whole lists, {nrows} rows (rank rows max/min "
+            f"{np.bincount(owner, weights=glen, minlength=world).max():.0f}/"
+            f"{np.bincount(owner, weights=glen, minlength=world).min():.0f})")
+    else:
+        for labs, x in shard_chunks():
+            idx.add_labels(labs, x, track_ids=False)
+            nrows += len(labs)
+            if keep:
+                kept.append(x)
+            if nrows % (5 * args.add_rows) < len(labs):  # progress for long (M8-size) loads
+                log(f"rank {rank}: {nrows} rows added ({time.time() - t:.0f}s)")
+        idx.build()
     data = np.concatenate(kept) if keep else None  # world == 1: rows in base-row (= label) order
     del kept
     log(f"rank {rank}: shard of {nrows} rows ({len(blocks)} blocks) generated + indexed in {time.time() - t:.1f}s")
@@ -256,13 +284,21 @@ def run(args):
     def merge(sp, lp, kk):  # RCCL all_gather'ed partial top-k [world, Q, k] -> on-device merge
         return merge_device(sp, lp, kk, torch.cuda.current_stream().cuda_stream, part_major=True)
 
-    # the N > 1 step's probe lists and gathered partials: allocated once, reused by every step
-    sharded = ShardedIvfStep(args.nq, width, k, rank, world, device=dev) if world > 1 else None
+    # the N > 1 step's buffers: allocated once, reused by every step
+    sharded = None
+    if world > 1 and lists_sharded:
+        sharded = ListShardedIvf(DeviceShardEngine(idx, k, opts), comm, args.nq, k, width, rank, world, device=dev,
+                                 fcap=args.fcap)
+    elif world > 1:
+        sharded = ShardedIvfStep(args.nq, width, k, rank, world, device=dev)
 
     def step():
         if world == 1:
             idx.search_device(q.data_ptr(), Q, k, s_loc.data_ptr(), l_loc.data_ptr(), 0,
                               torch.cuda.current_stream().cuda_stream, opts)
+            return
+        if lists_sharded:
+            result[:] = sharded(q)
             return
         result[:] = sharded(q, probe, search, merge)
 
@@ -300,6 +336,15 @@ def run(args):
                 torch.cuda.synchronize()
         torch.cuda.synchronize()
         timed_step = graph.replay
+    elif lists_sharded and args.graph:
+        # the device work between the collectives replayed from hipGraphs (ListShardedIvf.capture); every
+        # rank runs the same number of untimed steps (they synchronize in the collectives)
+        sharded.capture(q)
+        graph = sharded.graphs
+        n_w = max(10, args.warmup)
+        for _ in range(n_w):
+            step()
+        torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -313,14 +358,20 @@ def run(args):
     # batch: bit-identical, so the graph replays computed the search (DESIGN.md §4 "hipGraph replays")
     graph_check = None
     if graph is not None:
-        g_s, g_l = s_loc.clone(), l_loc.clone()
-        s_loc.fill_(0.0)
-        l_loc.fill_(-7)
-        step()
+        o_s, o_l = (s_loc, l_loc) if world == 1 else (result[0], result[1])
+        g_s, g_l = o_s.clone(), o_l.clone()
+        o_s.fill_(0.0)
+        o_l.fill_(-7)
+        if world > 1:
+            saved, sharded.graphs = sharded.graphs, {}
+            step()
+            sharded.graphs = saved
+        else:
+            step()
         torch.cuda.synchronize()
         graph_check = {"replays": args.steps + n_w, "untimed_replays": n_w,
-                       "last_replay_equals_direct_search": bool(torch.equal(g_l, l_loc)) and
-                       bool(torch.equal(g_s.view(torch.int32), s_loc.view(torch.int32)))}
+                       "last_replay_equals_direct_search": bool(torch.equal(g_l, o_l)) and
+                       bool(torch.equal(g_s.view(torch.int32), o_s.view(torch.int32)))}
         log(f"graph replay vs direct search: {graph_check}")
     if world > 1:
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -334,6 +385,9 @@ def run(args):
     coll = {}
     L.pyr_profile_reset()
     L.pyr_profile_enable(1)
+    saved_graphs = None
+    if lists_sharded and getattr(sharded, "graphs", None):
+        saved_graphs, sharded.graphs = sharded.graphs, {}  # the per-phase profile needs the plain launches
     if sharded is not None:
         sharded.timing = True
     for _ in range(args.profile_steps):
@@ -345,6 +399,8 @@ def run(args):
     L.pyr_profile_enable(0)
     if sharded is not None:
         sharded.timing = False
+    if saved_graphs is not None:
+        sharded.graphs = saved_graphs
     # rows of every rank's shard (weak scaling: each rank holds N / world of them)
     rank_rows = [nrows]
     if world > 1:
@@ -404,7 +460,7 @@ def run(args):
     l_fin = result[1].cpu().numpy()
     if args.recall_queries > 0:
         t = time.time()
-        R = min(args.recall_queries, Q)
+        R = min(args.recall_queries, Q, len(l_fin))  # list-sharded: rank 0 answers its home queries
         flat = BruteForceVectorIndex(D, VectorMetric.L2, device=local)
         for labs, x in shard_chunks():
             flat.add_labels(labs, x, track_ids=False)
@@ -415,9 +471,10 @@ def run(args):
             sp, lp = gather_partials(gs, gl, world)
             gs, gl = merge_device(sp, lp, k, torch.cuda.current_stream().cuda_stream)
         gt = gl.cpu().numpy()
-        hits = sum(len(set(gt[i].tolist()) & set(l_fin[i].tolist())) for i in range(R))
-        recall = hits / (R * k)
-        log(f"recall@10 over {R} queries: {recall:.4f} ({time.time() - t:.1f}s)")
+        if rank == 0 or not lists_sharded:  # list-sharded: rank 0 holds the answers of queries [0, nq)
+            hits = sum(len(set(gt[i].tolist()) & set(l_fin[i].tolist())) for i in range(R))
+            recall = hits / (R * k)
+            log(f"recall@10 over {R} queries: {recall:.4f} ({time.time() - t:.1f}s)")
         # the ground truth itself against the CPU restatement of BruteForceVectorIndex.Search (checker only)
         if rank == 0 and world == 1 and args.cpu_seconds > 0 and data is not None:
             import oracle  # checker only
@@ -501,9 +558,15 @@ def run(args):
             "config": {"workload": f"IVF_FLAT d={D} N={N} nlist={args.nlist} nprobe={args.nprobe} k={k}",
                        "n": N, "dim": D, "nlist": args.nlist, "nprobe": args.nprobe, "k": k,
                        "queries_per_step": Q, "queries_per_gpu": args.nq, "train_rows": T,
-                       "shard": "rows-within-list: generator blocks b % n_gpus == rank, shared quantizer "
-                                "(trained on rank 0, broadcast)",
-                       "merge": "RCCL all_gather of probe lists and of partial top-k + on-device merge"
+                       "shard": ("whole IVF lists per rank (size-balanced), rows exchanged to their list's owner, "
+                                 "replicated list samples; shared quantizer (trained on rank 0, broadcast)"
+                                 if lists_sharded else
+                                 "rows-within-list: generator blocks b % n_gpus == rank, shared quantizer "
+                                 "(trained on rank 0, broadcast)") if world > 1 else "none",
+                       "merge": ("RCCL all_gather of plans, all_to_all of per-query records to their home rank, "
+                                 "on-device merge + certificate, exact re-run of failures (all_gather + all_to_all)"
+                                 if lists_sharded else
+                                 "RCCL all_gather of probe lists and of partial top-k + on-device merge")
                                 if world > 1 else "none"},
             "recall_at_10": recall,
             "recall_truth_check": truth_check,

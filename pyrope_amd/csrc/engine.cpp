@@ -446,7 +446,7 @@ static void reset_stream_counters(Workspace &ws, int64_t nq, int nlist) {
   ws.ivf_fill.ensure(sizeof(int32_t) * std::max(nlist, 1));
   ws.scn.ensure(sizeof(int32_t) * std::max<int64_t>(nq, 1));
   ws.scf.ensure(sizeof(uint32_t) * std::max<int64_t>(nq, 1));
-  ws.swork.ensure(sizeof(int32_t) * 2);
+  ws.swork.ensure(sizeof(int32_t) * 16);
   ws.fail_cnt.ensure(sizeof(int32_t));
   ws.fail_cnt2.ensure(sizeof(int32_t));
   WordFill z;
@@ -454,7 +454,7 @@ static void reset_stream_counters(Workspace &ws, int64_t nq, int nlist) {
   z.add(ws.ivf_fill.p, nlist, 0);
   z.add(ws.scn.p, nq, 0);
   z.add(ws.scf.p, nq, 0);
-  z.add(ws.swork.p, 2, 0);
+  z.add(ws.swork.p, 16, 0);  // two item counters, or two sets of 8 per-XCD queue counters (pq32)
   z.add(ws.fail_cnt.p, 1, 0);
   z.add(ws.fail_cnt2.p, 1, 0);
   launch_fill_words(z, ws.st);
@@ -527,6 +527,17 @@ static int64_t stream_chunk() {
   return round_up(e ? std::max<int64_t>(32, atoll(e)) : 5120, 32);
 }
 
+// Queries per slice of a stream search: the per-query buffers (candidate buffer, counts, merged candidates,
+// fail lists, thresholds) and the per-(query, probe) ones (fp16 query operands of the tile dimension, their
+// scale pair, the sample values, the probe id and work-list slot) stay within 16 GiB (the
+// per-position buffers dominate at many probes, e.g. a FLAT store of 1,000 chunks).
+static int64_t stream_slice_queries(int64_t nq, int probes, int dt, int cap, int sv) {
+  const int64_t per_q = (int64_t)cap * 8 + 8 + 8 * STREAM_KO + 16 + (int64_t)probes * (2 * dt + 8 + 4 * sv + 8);
+  int64_t qs = (int64_t(16) << 30) / per_q;
+  if (const char *e = getenv("PYR_SLICE_QUERIES")) qs = std::min<int64_t>(qs, atoll(e));  // tests: force slicing
+  return std::max<int64_t>(1, std::min<int64_t>(nq, qs));
+}
+
 // HBM plan of an IVF_FLAT index and of one stream-path search on it (pyr_ivf_memory_plan): the
 // allocations commit_lists and search_stream / stream_slice make, restated as arithmetic so that a
 // multi-GPU launch can size a rank before it allocates (the M8 rank shape: tests/test_host_logic.py).
@@ -550,8 +561,7 @@ void ivf_memory_plan(int dim, int64_t nrows, int nlist, int64_t max_len, int64_t
     ch.cmax = ivf_list_chunks((int)max_len, ch);
   }
   const int64_t nparts = (int64_t)probes * ch.cmax;
-  const int64_t per_q = (int64_t)cap * 8 + 2 * 4;
-  const int64_t qs = std::max<int64_t>(1, std::min<int64_t>(nq, (int64_t(16) << 30) / per_q));
+  const int64_t qs = stream_slice_queries(nq, probes, (int)DT, cap, scan_sample_values());
   int64_t w = 0;
   // coarse ranking: probe lists of the whole batch, <= 256 MB of centroid scores per launch
   w += 4 * nq * probes;
@@ -596,6 +606,14 @@ struct CosRefine {
   const float *qnorm;      // ComputeNorm per query
   const uint32_t *zflag;   // a zero-norm row was written
 };
+
+// the stream scans' candidate merge and certified refine fused into one kernel (filter.hip
+// merge_refine_kernel); PYR_MERGE_REFINE=0 (A/B) and PYR_STREAM_DEBUG (it reads the merged candidates back)
+// take cand_merge + the two refine launches
+static bool merge_refine_fused() {
+  const char *e = getenv("PYR_MERGE_REFINE");
+  return !(e && atoi(e) == 0) && !getenv("PYR_STREAM_DEBUG");
+}
 
 // list-sharded search (IvfFlatIndex::shard_search, shard.hip): a slice's thresholds T_q (from the home
 // ranks' plans) and its record output (exact local top-k + the bound of the rows left out, per query)
@@ -1038,8 +1056,7 @@ struct FlatIndex : Index {
     const int nch = (int)((cutoff + crow - 1) / crow);
     const int cap = stream_cap();
     const int nparts = nch;  // one chunk per "list"
-    const int64_t per_q = (int64_t)cap * 8 + 2 * 4;
-    const int64_t qs = std::max<int64_t>(1, std::min<int64_t>(nq, (int64_t(16) << 30) / per_q));
+    const int64_t qs = stream_slice_queries(nq, nch, st.tdim(), cap, scan_sample_values());
     // the chunks as lists, on the device (no host work per search): bounds, the centroid copies (mu for
     // L2, 0 for IP) and the probe lists (every chunk, in order) of the largest slice
     ws.vlb.ensure(sizeof(int32_t) * nch);
@@ -1141,17 +1158,18 @@ struct FlatIndex : Index {
     }
     ws.ms.ensure(sizeof(float) * nq * STREAM_KO);
     ws.mk.ensure(sizeof(int32_t) * nq * STREAM_KO);
-    {
+    const bool fused = merge_refine_fused();
+    CandMergeArgs m{};
+    m.cand = ws.scand.as<uint2>();
+    m.cand_n = ws.scn.as<int32_t>();
+    m.cand_f = ws.scf.as<uint32_t>();
+    m.thr = ws.sthr.as<float>();
+    m.nq = nq;
+    m.cap = cap;
+    m.out_s = ws.ms.as<float>();
+    m.out_k = ws.mk.as<int32_t>();
+    if (!fused) {
       PhaseTimer t(PH_MERGE, ws.st);
-      CandMergeArgs m{};
-      m.cand = ws.scand.as<uint2>();
-      m.cand_n = ws.scn.as<int32_t>();
-      m.cand_f = ws.scf.as<uint32_t>();
-      m.thr = ws.sthr.as<float>();
-      m.nq = nq;
-      m.cap = cap;
-      m.out_s = ws.ms.as<float>();
-      m.out_k = ws.mk.as<int32_t>();
       launch_cand_merge(m, ws.st);
     }
     ws.fail.ensure(sizeof(int32_t) * nq);
@@ -1190,7 +1208,14 @@ struct FlatIndex : Index {
     r.out_s = d_s;
     r.out_l = d_l;
     r.out_c = d_c;
-    {
+    if (fused) {  // merge, depth K1, depth 64 for the failures: one kernel
+      PhaseTimer t(PH_REFINE, ws.st, nq * k1);
+      r.k1 = k1;
+      r.fail_list = ws.fail.as<int32_t>();
+      r.fail_cnt = ws.fail_cnt.as<int32_t>();
+      launch_merge_refine(m, r, metric, exact_v, ws.st);
+      HIPCHK(hipGetLastError());
+    } else {
       PhaseTimer t(PH_REFINE, ws.st, nq * k1);
       r.k1 = k1;
       r.fail_list = ws.fail2.as<int32_t>();
@@ -1550,7 +1575,7 @@ static int build_ivf_items(Workspace &ws, int64_t nq, int nprobe, int nparts, in
   ws.ivf_ioff.ensure(sizeof(int32_t) * (nlist + 1));
   ws.qlist.ensure(sizeof(int32_t) * std::max<int64_t>(nq * nprobe, 1));
   items.ensure(sizeof(ScanItem) * std::max(maxi, 1));
-  nitems.ensure(sizeof(int32_t) * 4);
+  nitems.ensure(sizeof(int32_t) * 16);  // the count, then (IvfChunking::xcd) the 9 queue bounds
   IvfItemWs iw{ws.ivf_cnt.as<int32_t>(), ws.ivf_fill.as<int32_t>(), ws.ivf_qoff.as<int32_t>(),
                ws.ivf_ioff.as<int32_t>(), ws.qlist.as<int32_t>(), items.as<ScanItem>(), nitems.as<int32_t>()};
   launch_ivf_items(ws.probes.as<int32_t>(), nq, nprobe, nparts, nlist, lbeg.as<int32_t>(), lend.as<int32_t>(), qchunk,
@@ -1954,18 +1979,19 @@ struct IvfFlatIndex : Index {
                      Workspace &ws, const ShardCtx *sh = nullptr) {
     const int cap = stream_cap();
     int64_t chunk = stream_chunk();
-    IvfChunking ch{(int32_t)chunk, 1, 0};
-    ch.cmax = ivf_list_chunks((int)max_len, ch);
+    // a list-sharded rank's lists it does not own are empty: their (query, list) pairs get no item.  Not
+    // otherwise: the sample pass writes the (empty) sample of an empty list's pairs through its item
+    IvfChunking ch{(int32_t)chunk, 1, 0, sh ? 1 : 0};
+    ch.cmax = std::max(1, ivf_list_chunks((int)max_len, ch));
     if ((int64_t)probes * ch.cmax > MAX_PARTS) {  // fewer, longer chunks
       const int64_t room = std::max<int64_t>(1, MAX_PARTS / std::max(probes, 1));
       chunk = round_up(std::max<int64_t>(32, (max_len + room - 1) / room), 32);
       ch.chunk = (int32_t)chunk;
-      ch.cmax = ivf_list_chunks((int)max_len, ch);
+      ch.cmax = std::max(1, ivf_list_chunks((int)max_len, ch));
     }
     const int nparts = probes * ch.cmax;
     if (nparts > MAX_PARTS) throw Error(PYR_E_ARG, "nprobe too large");
-    const int64_t per_q = (int64_t)cap * 8 + 2 * 4;
-    const int64_t qs = std::max<int64_t>(1, std::min<int64_t>(nq, (int64_t(16) << 30) / per_q));
+    const int64_t qs = stream_slice_queries(nq, probes, lists.tdim(), cap, scan_sample_values());
     for (int64_t a0 = 0; a0 < nq; a0 += qs) {
       const int64_t n = std::min(qs, nq - a0);
       const int32_t *ext = ws.ext_probes;
@@ -2144,17 +2170,18 @@ struct IvfFlatIndex : Index {
     HIPCHK(hipGetLastError());
     ws.ms.ensure(sizeof(float) * nq * STREAM_KO);
     ws.mk.ensure(sizeof(int32_t) * nq * STREAM_KO);
-    {
+    const bool fused = merge_refine_fused();
+    CandMergeArgs m{};
+    m.cand = ws.scand.as<uint2>();
+    m.cand_n = ws.scn.as<int32_t>();
+    m.cand_f = ws.scf.as<uint32_t>();
+    m.thr = sa.thr;
+    m.nq = nq;
+    m.cap = cap;
+    m.out_s = ws.ms.as<float>();
+    m.out_k = ws.mk.as<int32_t>();
+    if (!fused) {
       PhaseTimer t(PH_MERGE, ws.st);
-      CandMergeArgs m{};
-      m.cand = ws.scand.as<uint2>();
-      m.cand_n = ws.scn.as<int32_t>();
-      m.cand_f = ws.scf.as<uint32_t>();
-      m.thr = sa.thr;
-      m.nq = nq;
-      m.cap = cap;
-      m.out_s = ws.ms.as<float>();
-      m.out_k = ws.mk.as<int32_t>();
       launch_cand_merge(m, ws.st);
     }
     // certificate at depth K1, then the failures at depth 64 from the same candidates
@@ -2202,11 +2229,19 @@ struct IvfFlatIndex : Index {
       r.rec = sh->rec;
       r.rec_lb = dlb.as<int32_t>();
       r.rec_nlist = coarse.nlist;
-      launch_refine(r, met, 1, ws.st);
+      if (fused) launch_merge_refine(m, r, met, 1, ws.st);
+      else launch_refine(r, met, 1, ws.st);
       HIPCHK(hipGetLastError());
       return;
     }
-    {
+    if (fused) {  // merge, depth K1, depth 64 for the failures: one kernel
+      PhaseTimer t(PH_REFINE, ws.st, nq * k1);
+      r.k1 = k1;
+      r.fail_list = ws.fail.as<int32_t>();
+      r.fail_cnt = ws.fail_cnt.as<int32_t>();
+      launch_merge_refine(m, r, met, 1, ws.st);
+      HIPCHK(hipGetLastError());
+    } else {
       PhaseTimer t(PH_REFINE, ws.st, nq * k1);
       r.k1 = k1;
       r.fail_list = ws.fail2.as<int32_t>();
@@ -2372,7 +2407,7 @@ struct IvfFlatIndex : Index {
         PhaseTimer t(PH_COARSE, ws.st, n * coarse.nlist);
         coarse.probe(q, nullptr, n, P, metric, ws);
       }
-      const IvfChunking ch{512, 1, 0};  // a sample list is one chunk
+      const IvfChunking ch{512, 1, 0};  // a sample list is one chunk (an empty one too: its sample is empty)
       const int maxi = build_ivf_items(ws, n, P, P, coarse.nlist, sslb, ssle, scan_qmax(dt), ch, 0, true, true);
       const int64_t npos = n * P;
       ws.sbq.ensure(sizeof(uint16_t) * npos * dt);
@@ -2897,12 +2932,13 @@ struct IvfPqIndex : Index {
     if (pq32_supported(dim, M, ksub, 10)) {
       // tile code layout + |x^|^2 per position; fp16 codebook with a power-of-two scale keeping max |C| < 2^14
       const int64_t tiles = (tot + 31) / 32;
-      cpack.ensure((size_t)std::max<int64_t>(tiles, 1) * 64 * pq32_code_bytes(dim));
-      HIPCHK(hipMemsetAsync(cpack.p, 0, (size_t)std::max<int64_t>(tiles, 1) * 64 * pq32_code_bytes(dim), wst));
+      const size_t cbytes = (size_t)std::max<int64_t>(tiles, 1) * 32 * 16 * pq32_code_words(M);
+      cpack.ensure(cbytes);
+      HIPCHK(hipMemsetAsync(cpack.p, 0, cbytes, wst));
       nrm.ensure(sizeof(float) * (size_t)std::max<int64_t>(tiles * 32, 1));
       HIPCHK(hipMemsetAsync(nrm.p, 0, sizeof(float) * (size_t)std::max<int64_t>(tiles * 32, 1), wst));
-      launch_pq32_pack(codes_rm, dsrc.as<int64_t>(), tot, M, cb.as<float>(), ksub, cpack.as<uint8_t>(), nrm.as<float>(),
-                       wst);
+      launch_pq32_pack(codes_rm, dsrc.as<int64_t>(), tot, M, sub, cb.as<float>(), ksub, cpack.as<uint8_t>(),
+                       nrm.as<float>(), wst);
       std::vector<float> hcb((size_t)M * ksub * sub);
       HIPCHK(hipMemcpyAsync(hcb.data(), cb.p, sizeof(float) * hcb.size(), hipMemcpyDeviceToHost, wst));
       HIPCHK(hipStreamSynchronize(wst));
@@ -2913,8 +2949,8 @@ struct IvfPqIndex : Index {
         am = std::max(am, std::fabs(v));
       }
       cbsx = pow2_scale_host(am);
-      cb16.ensure(sizeof(uint16_t) * (size_t)M * 256 * 8);
-      launch_pq32_cb16(cb.as<float>(), M, ksub, cbsx, cb16.as<_Float16>(), wst);
+      cb16.ensure(sizeof(uint16_t) * (size_t)M * 256 * sub);
+      launch_pq32_cb16(cb.as<float>(), M, ksub, sub, cbsx, cb16.as<_Float16>(), wst);
       HIPCHK(hipGetLastError());
       pq32_ready = fin;
       ++pq_gen;
@@ -2986,7 +3022,8 @@ struct IvfPqIndex : Index {
     const int k1 = filter_k1(k);
     const int cap = stream_cap();
     IvfChunking ch{(int32_t)stream_chunk(), 1, 0};
-    ch.cmax = ivf_list_chunks((int)pq_max_len, ch);
+    ch.xcd = 1;  // a list's items on one XCD (pq32.hip: its code chunks leave HBM once per L2)
+    ch.cmax = std::max(1, ivf_list_chunks((int)pq_max_len, ch));
     if ((int64_t)probes * ch.cmax > MAX_PARTS) {
       const int64_t room = std::max<int64_t>(1, MAX_PARTS / std::max(probes, 1));
       ch.chunk = (int32_t)round_up(std::max<int64_t>(32, (pq_max_len + room - 1) / room), 32);
@@ -2994,12 +3031,19 @@ struct IvfPqIndex : Index {
     }
     const int nparts = probes * ch.cmax;
     if (nparts > MAX_PARTS) throw Error(PYR_E_ARG, "nprobe too large");
-    const int64_t per_q = (int64_t)cap * 8 + 2 * 4;
-    const int64_t qs = std::max<int64_t>(1, std::min<int64_t>(nq, (int64_t(16) << 30) / per_q));
+    const int64_t qs = stream_slice_queries(nq, probes, dim, cap, pq32_sample_values());
+    const int32_t *ext = ws.ext_probes;  // caller-ranked probe lists: each slice takes its own rows
     for (int64_t a0 = 0; a0 < nq; a0 += qs) {
       const int64_t n = std::min(qs, nq - a0);
-      pq32_slice(d_q + a0 * dim, n, k, k1, probes, ch, nparts, cap, d_s + a0 * k, d_l + a0 * k,
-                 d_c ? d_c + a0 : nullptr, ws);
+      if (ext) ws.ext_probes = ext + a0 * ws.ext_nprobe;
+      try {
+        pq32_slice(d_q + a0 * dim, n, k, k1, probes, ch, nparts, cap, d_s + a0 * k, d_l + a0 * k,
+                   d_c ? d_c + a0 : nullptr, ws);
+      } catch (...) {
+        ws.ext_probes = ext;
+        throw;
+      }
+      ws.ext_probes = ext;
     }
   }
 
@@ -3014,7 +3058,7 @@ struct IvfPqIndex : Index {
     int maxi;
     {
       PhaseTimer t(PH_ITEMS, ws.st);
-      maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, pq32_qmax(), ch, 0, true, true);
+      maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, pq32_qmax(dim, M), ch, 0, true, true);
     }
     const int64_t npos = nq * probes;
     const int sv = pq32_sample_values();
@@ -3030,6 +3074,7 @@ struct IvfPqIndex : Index {
     sa.h16 = cpack.p;
     sa.queries = d_q;
     sa.cents = coarse.rm.as<float>();
+    sa.probes = ws.probes.as<int32_t>();
     sa.sx = cbsx;
     sa.items = ws.items.as<ScanItem>();
     sa.n_items = ws.nitems.as<int32_t>();
@@ -3056,8 +3101,8 @@ struct IvfPqIndex : Index {
     sa.mub = pq_row_terms(sa.kr, ws);
     {
       PhaseTimer t(PH_SAMPLE, ws.st);
-      launch_pq32_prep(sa, maxi, ws.st);
-      launch_pq32_scan(sa, cb16.as<_Float16>(), maxi, true, ws.st);
+      launch_pq32_prep(sa, npos, ws.st);
+      launch_pq32_scan(sa, cb16.as<_Float16>(), M, maxi, true, ws.st);
       StreamSelectArgs sel{};
       sel.samp = ws.ssamp.as<float>();
       sel.nq = nq;
@@ -3070,10 +3115,10 @@ struct IvfPqIndex : Index {
       sel.thr = ws.sthr.as<float>();
       launch_stream_select(sel, ws.st);
     }
-    sa.work = ws.swork.as<int32_t>() + 1;
+    sa.work = ws.swork.as<int32_t>() + 8;  // the main pass's 8 queue counters
     {
       PhaseTimer t(PH_PQ_SCAN, ws.st, prof().on ? probed_rows(ws, nq, probes, le, lb) : 0);
-      launch_pq32_scan(sa, cb16.as<_Float16>(), maxi, false, ws.st);
+      launch_pq32_scan(sa, cb16.as<_Float16>(), M, maxi, false, ws.st);
     }
     ws.ms.ensure(sizeof(float) * nq * STREAM_KO);
     ws.mk.ensure(sizeof(int32_t) * nq * STREAM_KO);
@@ -3109,7 +3154,8 @@ struct IvfPqIndex : Index {
     r.dim = dim;
     r.M = M;
     r.ksub = ksub;
-    r.mb = pq32_code_bytes(dim);
+    r.mw = pq32_code_words(M);
+    r.dsub = sub;
     r.nlist = coarse.nlist;
     r.out_s = d_s;
     r.out_l = d_l;
@@ -3136,10 +3182,23 @@ struct IvfPqIndex : Index {
       HIPCHK(hipMemcpy(&n1, ws.fail_cnt2.p, sizeof(int32_t), hipMemcpyDeviceToHost));
       fprintf(stderr, "[pq32] nq %lld: certificate failures depth %d %d, depth 64 %d\n", (long long)nq, k1, n1, nf);
     }
-    // what neither depth certifies: the LUT scan of those queries (same coarse ranking, same arithmetic)
+    // what neither depth certifies: the LUT scan of those queries over the same probe lists (the slice's
+    // ranking or the caller's, gathered by the fail list), same arithmetic
     filter_fallback(ws, nf, d_q, dim, k, d_s, d_l, d_c,
                     [&](const float *q2, int64_t n2, float *s2, int64_t *l2, int32_t *c2) {
-                      search_lut(q2, n2, k, probes, s2, l2, c2, ws.nested());
+                      ws.fprobes.ensure(sizeof(int32_t) * n2 * probes);
+                      launch_gather_words(ws.probes.as<uint32_t>(), ws.fail.as<int32_t>(), n2, probes,
+                                          ws.fprobes.as<uint32_t>(), ws.st);
+                      Workspace &nw = ws.nested();
+                      nw.ext_probes = ws.fprobes.as<int32_t>();
+                      nw.ext_nprobe = probes;
+                      try {
+                        search_lut(q2, n2, k, probes, s2, l2, c2, nw);
+                      } catch (...) {
+                        nw.ext_probes = nullptr;
+                        throw;
+                      }
+                      nw.ext_probes = nullptr;
                     });
   }
 

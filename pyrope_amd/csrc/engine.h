@@ -124,7 +124,7 @@ struct Workspace {
   DevMem ivf_cnt2, ivf_fill2, ivf_qoff2, ivf_ioff2, qlist2;  // second item set (nearest-list seeding)
   DevMem out_s, out_l, out_c;
   DevMem ms, mk, fail, fail_cnt, fq, fs, fl, fc;  // MFMA filter: merged candidates, certificate failures
-  DevMem fprobes;                                 // probe lists of the failing queries (IVF exact re-run)
+  DevMem fprobes;                                 // probe lists of the failing queries (IVF_PQ LUT re-run)
   DevMem q8q, q8qs;                               // 8-bit search mode: quantized queries, their sums
   // stream-and-emit list scan (stream16.hip): query operands, samples, thresholds, candidate regions
   DevMem sbq, sqsc, ssamp, sthr, scand, scn, scf, swork, fail2, fail_cnt2;

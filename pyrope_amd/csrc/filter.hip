@@ -19,11 +19,14 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <stdexcept>
 
 #include "kernels.h"
 
 namespace pyr {
 namespace {
+
+#include "candmerge.h"
 
 __device__ __forceinline__ bool better(float s1, uint32_t k1, float s2, uint32_t k2) {
   return s1 > s2 || (s1 == s2 && k1 < k2);
@@ -142,13 +145,14 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
   constexpr int UNR8 = DT > 0 ? DT / 8 : 4;
   const int ld = a.ld > 0 ? a.ld : k1;
   const float *qp = a.queries + (size_t)q * D;
-  float part = 0.0f;  // |q|^2, any order (covered by E)
-  for (int d = lane; d < D; d += 64) part += qp[d] * qp[d];
+  float part = 0.0f;  // |q|^2, any order (covered by E); a shard record certifies nowhere here: not needed
+  if (!a.rec)
+    for (int d = lane; d < D; d += 64) part += qp[d] * qp[d];
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) part += __shfl_xor(part, off);
   const float qsq = part;
   float qa = 0.0f;  // max |q_i|: the fp16 filter's query scale (filter16.hip pow2_scale)
-  if (a.q16) {
+  if (a.q16 && !a.rec) {
     for (int d = lane; d < D; d += 64) qa = fmaxf(qa, fabsf(qp[d]));
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) qa = fmaxf(qa, __shfl_xor(qa, off));
@@ -161,7 +165,11 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
   if (lane < k1 && mk[lane] >= 0) key = (uint32_t)mk[lane];
   // exact scores, 8 candidates per pass (an 8-lane group per candidate), then candidate c's score
   // moves to lane c
+  const uint64_t real = __builtin_amdgcn_ballot_w64(key != KEY_NONE);
   for (int p = 0; 8 * p < k1; ++p) {
+    // a pass whose 8 candidates are all empty or floor placeholders scores nothing (a list-sharded rank
+    // often holds only a few of a query's candidates)
+    if (((real >> (8 * p)) & 0xFFull) == 0ull) continue;
     const int c = 8 * p + (lane >> 3);
     const int32_t kc = __shfl((int)key, c);  // (k1 <= 64: every candidate's key sits on lane c)
     const int64_t rk = kc >= 0 ? (int64_t)kc : 0;
@@ -388,6 +396,134 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
   }
 }
 
+// The stream scans' merge and certified refine in ONE wave per query (replaces cand_merge_kernel + the
+// depth-K1 refine + the depth-64 refine of the failures: no merged-candidate round trip through HBM, no
+// second launch).  The merge leaves lane j with the query's j-th best candidate bound (a row, or a floor
+// placeholder max(T_q, floor)); the candidates of depth K1 are re-scored exactly and certified as in
+// refine_kernel's upper-bound branch; a query that fails goes on to depth 64 in the same wave (its other 48
+// candidates scored then), and what fails there is listed for the exact re-run.  Shard records (a.rec): the
+// depth-K1 answer and bound, no certificate.
+template <int V, int MET, int DT>
+__global__ __launch_bounds__(256) void merge_refine_kernel(CandMergeArgs m, RefineArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= a.nq) return;
+  const uint64_t cur = cand_merge_wave<STREAM_KO>(m, q, lane);
+  const uint32_t kk = ~(uint32_t)cur;
+  const float msl = cur != 0ull ? key_score((uint32_t)(cur >> 32)) : -INFINITY;   // lane j: ms[j]
+  const int32_t mkl = cur == 0ull ? -1 : (kk == KEY_FLOOR ? -2 : (int32_t)kk);    // lane j: mk[j]
+  const int D = DT > 0 ? DT : a.dim, k = a.k, k1 = a.k1;
+  const float *qp = a.queries + (size_t)q * D;
+  const uint32_t key = mkl >= 0 ? (uint32_t)mkl : KEY_NONE;
+  const uint64_t real = __builtin_amdgcn_ballot_w64(key != KEY_NONE);
+  float s = -INFINITY;  // lane j: the exact score of candidate j (a row)
+  auto score_passes = [&](int p0, int p1) {
+    for (int p = p0; p < p1; ++p) {
+      if (((real >> (8 * p)) & 0xFFull) == 0ull) continue;  // 8 placeholders / empties: nothing to score
+      const int c = 8 * p + (lane >> 3);
+      const int32_t kc = __shfl((int)key, c);
+      const int64_t rk = kc >= 0 ? (int64_t)kc : 0;
+      float sc;
+      if (MET == L2 && a.cosine) {  // VectorMath.Cosine (:102-109) with the cached norms
+        const float dot = a.rows_rm ? exact_score_l8<V, IP, DT, true>(qp, a.rows_rm, rk, D, lane & 7)
+                                    : exact_score_l8<V, IP, DT, false>(qp, a.rows, rk, D, lane & 7);
+        const float qn = a.qnorm[q], xn = a.rnorm[rk];
+        sc = (qn < 1e-6f || xn < 1e-6f) ? 0.0f : dot / (qn * xn);
+      } else {
+        sc = a.rows_rm ? exact_score_l8<V, MET, DT, true>(qp, a.rows_rm, rk, D, lane & 7)
+                       : exact_score_l8<V, MET, DT, false>(qp, a.rows, rk, D, lane & 7);
+      }
+      const float t = __shfl(sc, 8 * (lane & 7));
+      if ((lane >> 3) == p && key != KEY_NONE) s = t;
+    }
+  };
+  int d = k1, rank = 0, nout = 0;
+  float skth = -INFINITY, bound = -INFINITY;
+  bool excluded = false;
+  // the ranking of depth d's candidates by (exact score desc, key asc), its k-th score and the bound of
+  // everything past depth d
+  auto rank_at = [&](int dd) {
+    const uint32_t kd = lane < dd ? key : KEY_NONE;
+    int valid = 0;
+    rank = 0;
+    for (int c = 0; c < dd; ++c) {
+      const float sc = __shfl(s, c);
+      const uint32_t kc = __shfl(kd, c);
+      if (kc == KEY_NONE) continue;
+      ++valid;
+      if (kd != KEY_NONE && better(sc, kc, s, kd)) ++rank;
+    }
+    nout = min(valid, k);
+    skth = -INFINITY;
+    for (int c = 0; c < dd; ++c) {
+      const int rc = __shfl(rank, c);
+      const uint32_t kc = __shfl(kd, c);
+      const float sc = __shfl(s, c);
+      if (kc != KEY_NONE && rc == k - 1) skth = sc;
+    }
+    excluded = __shfl(mkl, dd - 1) != -1;
+    bound = __shfl(msl, dd - 1);
+    if (lane >= dd) rank = 64;  // not a candidate at this depth
+  };
+  score_passes(0, k1 / 8);
+  rank_at(k1);
+  if (a.rec) {  // list-sharded record (see refine_kernel)
+    uint8_t *rp = static_cast<uint8_t *>(a.rec) + (size_t)q * shard_record_bytes(k);
+    ShardEntry *ent = reinterpret_cast<ShardEntry *>(rp);
+    if (key != KEY_NONE && rank < k) {
+      ShardEntry e;
+      e.label = a.row_labels ? a.row_labels[key] : (int64_t)key;
+      e.score = s;
+      e.list = shard_list_of(a.rec_lb, a.rec_nlist, key);
+      ent[rank] = e;
+    }
+    if (lane >= nout && lane < k) {
+      ShardEntry e;
+      e.label = -1;
+      e.score = -INFINITY;
+      e.list = 0x7FFFFFFF;
+      ent[lane] = e;
+    }
+    if (lane == 0) {
+      ShardTrailer t;
+      t.bound = excluded ? bound : -INFINITY;
+      t.n = nout;
+      t.pad = 0;
+      *reinterpret_cast<ShardTrailer *>(rp + 16 * (size_t)k) = t;
+    }
+    return;
+  }
+  const double u = 5.9604644775390625e-8;  // 2^-24
+  auto certified = [&]() -> bool {
+    if (!excluded) return true;  // no row was left out
+    if (MET == L2 && a.cosine) {
+      const float qn = a.qnorm[q];
+      return nout == k && (double)skth > 1.0 + 0.5 * (double)bound + (2.0 * D + 256.0) * u && qn >= 1e-6f &&
+             isfinite(qn) && !(a.max_rsq && a.max_rsq[1] != 0u) && !(a.zflag && *a.zflag != 0u && !(skth > 0.0f));
+    }
+    return nout == k && skth > bound;
+  };
+  bool ok = certified();
+  if (!ok && d < STREAM_KO && k + 4 <= STREAM_KO) {  // (wave-uniform) the same candidates at depth 64
+    score_passes(k1 / 8, STREAM_KO / 8);
+    d = STREAM_KO;
+    rank_at(d);
+    ok = certified();
+  }
+  if (key != KEY_NONE && rank < k) {
+    a.out_s[(size_t)q * k + rank] = s;
+    a.out_l[(size_t)q * k + rank] = a.row_labels ? a.row_labels[key] : (int64_t)key;
+  }
+  if (lane >= nout && lane < k) {
+    a.out_s[(size_t)q * k + lane] = -INFINITY;
+    a.out_l[(size_t)q * k + lane] = -1;
+  }
+  if (lane == 0) {
+    if (a.out_c) a.out_c[q] = nout;
+    if (!ok) a.fail_list[atomicAdd(a.fail_cnt, 1)] = (int32_t)q;
+  }
+}
+
 __global__ void unit_rows_kernel(const float *x, const int64_t *slots, const float *norms, int64_t n, int D,
                                  float *out, uint32_t *zflag, const uint8_t *live) {
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * D;
@@ -416,7 +552,8 @@ __global__ void scatter_results_kernel(const int32_t *qidx, int64_t n, int k, co
   if (j == 0 && out_c) out_c[q] = sc[i];
 }
 
-__global__ void gather_queries_kernel(const float *q, const int32_t *qidx, int64_t n, int D, float *out) {
+// rows qidx[i] of a [*][D] array of 32-bit words (queries, probe lists), copied bit for bit
+__global__ void gather_words_kernel(const uint32_t *q, const int32_t *qidx, int64_t n, int D, uint32_t *out) {
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * D;
        e += (int64_t)gridDim.x * blockDim.x) {  // grid-stride: grids stay below 2^32 work-items
     const int64_t i = e / D;
@@ -498,9 +635,45 @@ void launch_refine(const RefineArgs &a, int metric, int V, hipStream_t st) {
   }
 }
 
+void launch_merge_refine(const CandMergeArgs &m, const RefineArgs &a, int metric, int V, hipStream_t st) {
+  if (a.nq <= 0) return;
+  if (a.k1 % 8 != 0 || a.k1 > STREAM_KO || a.k1 < a.k) throw std::invalid_argument("merge_refine: depth");
+  const dim3 g(nblk(a.nq, 4)), b(256);
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, g, b, 0, st, m, a); };
+  auto by_dim = [&](auto k0, auto k32, auto k64, auto k128) {
+    switch (a.dim) {
+      case 32: go(k32); return;
+      case 64: go(k64); return;
+      case 128: go(k128); return;
+      default: go(k0); return;
+    }
+  };
+  if (V == 4) {
+    if (metric == L2)
+      by_dim(merge_refine_kernel<4, L2, 0>, merge_refine_kernel<4, L2, 32>, merge_refine_kernel<4, L2, 64>,
+             merge_refine_kernel<4, L2, 128>);
+    else
+      by_dim(merge_refine_kernel<4, IP, 0>, merge_refine_kernel<4, IP, 32>, merge_refine_kernel<4, IP, 64>,
+             merge_refine_kernel<4, IP, 128>);
+  } else {
+    if (metric == L2)
+      by_dim(merge_refine_kernel<1, L2, 0>, merge_refine_kernel<1, L2, 32>, merge_refine_kernel<1, L2, 64>,
+             merge_refine_kernel<1, L2, 128>);
+    else
+      by_dim(merge_refine_kernel<1, IP, 0>, merge_refine_kernel<1, IP, 32>, merge_refine_kernel<1, IP, 64>,
+             merge_refine_kernel<1, IP, 128>);
+  }
+}
+
 void launch_gather_queries(const float *q, const int32_t *qidx, int64_t n, int32_t dim, float *out, hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(gather_queries_kernel, dim3(gblk(n * dim)), dim3(256), 0, st, q, qidx, n, dim, out);
+  hipLaunchKernelGGL(gather_words_kernel, dim3(gblk(n * dim)), dim3(256), 0, st, reinterpret_cast<const uint32_t *>(q),
+                     qidx, n, dim, reinterpret_cast<uint32_t *>(out));
+}
+void launch_gather_words(const uint32_t *src, const int32_t *idx, int64_t n, int32_t width, uint32_t *out,
+                         hipStream_t st) {
+  if (n <= 0 || width <= 0) return;
+  hipLaunchKernelGGL(gather_words_kernel, dim3(gblk(n * width)), dim3(256), 0, st, src, idx, n, width, out);
 }
 
 void launch_scatter_results(const int32_t *qidx, int64_t n, int32_t k, const float *ss, const int64_t *sl,

@@ -64,8 +64,13 @@ struct IvfChunking {
   int32_t chunk;  // rows per main chunk
   int32_t cmax;   // max chunks of any list (slots reserved per probe)
   int32_t warm;   // rows of chunk 0 (0 = no warm-up chunk)
+  int32_t skip_empty = 0;  // an empty list gets no item (the stream scans: a list-sharded rank's lists it
+                           // does not own are empty, and their (query, list) pairs must cost nothing)
+  int32_t xcd = 0;         // items in 8 per-XCD queues (lists l with l % 8 == x, in list order), their
+                           // bounds at n_items[1 .. 9] (pq32.hip: one list's items on one XCD)
 };
 __host__ __device__ inline int ivf_list_chunks(int len, IvfChunking ch) {
+  if (len <= 0 && ch.skip_empty) return 0;
   if (ch.warm > 0) return len <= ch.warm ? 1 : 1 + (len - ch.warm + ch.chunk - 1) / ch.chunk;
   return len <= 0 ? 1 : (len + ch.chunk - 1) / ch.chunk;  // an empty list still gets one (empty) item
 }
@@ -322,6 +327,7 @@ struct StreamArgs {
   const float *meta;          // per row: L2 -|x - c|^2, IP 0, -inf dead / padding
   const float *queries;       // row-major nq x D
   const float *cents;         // row-major centroids
+  const int32_t *probes;      // [q][nprobe] probe lists (pq32 prep: a position's list)
   float sx;                   // the store's power-of-two fp16 scale
   const ScanItem *items;
   const int32_t *n_items;
@@ -361,25 +367,26 @@ void launch_row_terms(const float *meta, const float *rsq16, const float *rsq, i
 // no longer depends on its list's largest residual; the reference's own sum deviation (g) is folded in.
 void stream_ub_terms(int dim, int metric, double c_bf, double c_err, double c_abs, StreamArgs &a);
 // ---- IVF_PQ on the matrix cores (pq32.hip): the stream pipeline of the IVF_FLAT scan over rows decoded
-// from their codes; dsub = 8 and D = 768 (P1) ----
+// from their codes; D a multiple of 16 up to 1152, dsub 4 / 8 / 16 / 32 ----
 bool pq32_supported(int dim, int M, int ksub, int k);
-int pq32_qmax();                    // queries per item
+int pq32_qmax(int dim, int M);      // queries per item
 int pq32_sample_values();           // sample values per (query, probe)
-int pq32_code_bytes(int dim);       // code bytes per lane per 32-row tile (MB)
-// codes (row-major, source rows) -> the tile layout cpack [tile][64 lanes][MB] of the list-major positions
-// (src: position -> source row or -1) and |x^|^2 per position (fp32 codebooks [M][ksub][8])
-void launch_pq32_pack(const uint8_t *codes_rm, const int64_t *src, int64_t tot, int M, const float *cb, int ksub,
-                      uint8_t *cpack, float *nrm, hipStream_t st);
-void launch_pq32_cb16(const float *cb, int M, int ksub, float sc, _Float16 *cb16, hipStream_t st);
+int pq32_code_words(int M);         // 16-byte code words per row
+// codes (row-major, source rows) -> the tile layout cpack [tile][word][32 rows][16 B] of the list-major
+// positions (src: position -> source row or -1) and |x^|^2 per position (fp32 codebooks [M][ksub][dsub])
+void launch_pq32_pack(const uint8_t *codes_rm, const int64_t *src, int64_t tot, int M, int dsub, const float *cb,
+                      int ksub, uint8_t *cpack, float *nrm, hipStream_t st);
+void launch_pq32_cb16(const float *cb, int M, int ksub, int dsub, float sc, _Float16 *cb16, hipStream_t st);
 void launch_pq32_meta(const float *nrm, const uint8_t *live, int64_t tot, float *meta, hipStream_t st);
 // StreamArgs as for the IVF_FLAT stream scan, with h16 = cpack, mub = the row terms, cents = coarse
-// centroids, sx = the codebook scale
-void launch_pq32_prep(const StreamArgs &a, int max_items, hipStream_t st);
-void launch_pq32_scan(const StreamArgs &a, const _Float16 *cb16, int max_items, bool sample, hipStream_t st);
+// centroids, probes = the probe lists, sx = the codebook scale; items in XCD order (IvfChunking::xcd) and
+// work = 8 per-XCD queue counters
+void launch_pq32_prep(const StreamArgs &a, int64_t npos, hipStream_t st);
+void launch_pq32_scan(const StreamArgs &a, const _Float16 *cb16, int M, int max_items, bool sample, hipStream_t st);
 struct PqRefineArgs {
   const float *queries;     // nq x D
   const float *cents;       // coarse centroids, row-major
-  const float *codebooks;   // fp32 [M][ksub][8]
+  const float *codebooks;   // fp32 [M][ksub][dsub]
   const uint8_t *cpack;     // tile code layout
   const int64_t *labels;    // per position
   const int32_t *lb;        // list starts (positions)
@@ -387,7 +394,7 @@ struct PqRefineArgs {
   const int32_t *mk;        // their positions (-2 floor, -1 none)
   const int32_t *qsel, *nsel;  // refine only these queries (null: all nq)
   int64_t nq;
-  int32_t ld, k1, k, dim, M, ksub, mb, nlist;
+  int32_t ld, k1, k, dim, M, ksub, mw, dsub, nlist;
   float *out_s;
   int64_t *out_l;
   int32_t *out_c;
@@ -556,7 +563,15 @@ void launch_absmax(const float *rows, const int64_t *slots, int64_t n, int32_t d
                    const float *cents = nullptr, const int32_t *tile_list = nullptr);
 // V: 1 = VectorMath safe form (IVF), 4 = *Unsafe form (FLAT)
 void launch_refine(const RefineArgs &a, int metric, int V, hipStream_t st);
+// the stream scans' candidate merge + certified refine in one wave per query (filter.hip
+// merge_refine_kernel): depth a.k1 (a multiple of 8), the failures at depth STREAM_KO in the same wave,
+// what fails there into a.fail_list / a.fail_cnt; a.rec: shard records instead.  Upper-bound (resid, ub)
+// candidates only.
+void launch_merge_refine(const CandMergeArgs &m, const RefineArgs &a, int metric, int V, hipStream_t st);
 void launch_gather_queries(const float *q, const int32_t *qidx, int64_t n, int32_t dim, float *out, hipStream_t st);
+// rows idx[i] of a [*][width] array of 32-bit words (probe lists of the failing queries)
+void launch_gather_words(const uint32_t *src, const int32_t *idx, int64_t n, int32_t width, uint32_t *out,
+                         hipStream_t st);
 void launch_scatter_results(const int32_t *qidx, int64_t n, int32_t k, const float *ss, const int64_t *sl,
                             const int32_t *sc, float *out_s, int64_t *out_l, int32_t *out_c, hipStream_t st);
 // |x|^2 of blocked rows (at slots, or rows [0,n) when slots is null) + atomic running max

@@ -678,7 +678,24 @@ __device__ __forceinline__ int phase_chunks(const int32_t *lb, const int32_t *le
   return phase == 0 ? 1 : n - 1;
 }
 
+// IvfChunking::xcd: the list at position i of the queue-major order (queue x = lists l with l % 8 == x,
+// a + (x < b) of them for nlist = 8a + b), and whether i starts queue x
+__device__ __forceinline__ int xcd_order_list(int i, int nlist, int *x, bool *first) {
+  const int a = nlist >> 3, b = nlist & 7, head = b * (a + 1);
+  int j;
+  if (i < head) {
+    *x = i / (a + 1);
+    j = i - *x * (a + 1);
+  } else {
+    *x = b + (i - head) / a;
+    j = (i - head) - (*x - b) * a;
+  }
+  *first = j == 0;
+  return *x + 8 * j;
+}
+
 // single workgroup: qoff = exclusive scan of cnt, ioff = exclusive scan of ceil(cnt/qchunk) * chunks
+// (over the lists in XCD queue order when chk.xcd; n_items[1 + x] = the first item of queue x)
 __global__ __launch_bounds__(1024) void ivf_scan_kernel(const int32_t *cnt, int nlist, int qchunk, const int32_t *lb,
                                                         const int32_t *le, IvfChunking chk, int phase, int32_t *qoff,
                                                         int32_t *ioff, int32_t *n_items) {
@@ -686,10 +703,17 @@ __global__ __launch_bounds__(1024) void ivf_scan_kernel(const int32_t *cnt, int 
   const int tid = threadIdx.x;
   const int per = (nlist + 1023) / 1024;
   const int b = tid * per, e = min(nlist, b + per);
+  auto at = [&](int i) {
+    if (!chk.xcd) return i;
+    int x;
+    bool f;
+    return xcd_order_list(i, nlist, &x, &f);
+  };
   int lq = 0, li = 0;
   for (int i = b; i < e; ++i) {
-    lq += cnt[i];
-    li += (cnt[i] + qchunk - 1) / qchunk * phase_chunks(lb, le, i, chk, phase);
+    const int l = at(i);
+    lq += cnt[l];
+    li += (cnt[l] + qchunk - 1) / qchunk * phase_chunks(lb, le, l, chk, phase);
   }
   sq[tid] = lq;
   si[tid] = li;
@@ -704,15 +728,24 @@ __global__ __launch_bounds__(1024) void ivf_scan_kernel(const int32_t *cnt, int 
   }
   int rq = sq[tid] - lq, ri = si[tid] - li;
   for (int i = b; i < e; ++i) {
-    qoff[i] = rq;
-    ioff[i] = ri;
-    rq += cnt[i];
-    ri += (cnt[i] + qchunk - 1) / qchunk * phase_chunks(lb, le, i, chk, phase);
+    int l = i;
+    if (chk.xcd) {
+      int x;
+      bool first;
+      l = xcd_order_list(i, nlist, &x, &first);
+      if (first) n_items[1 + x] = ri;
+    }
+    qoff[l] = rq;
+    ioff[l] = ri;
+    rq += cnt[l];
+    ri += (cnt[l] + qchunk - 1) / qchunk * phase_chunks(lb, le, l, chk, phase);
   }
   if (tid == 1023) {
     qoff[nlist] = sq[1023];
     ioff[nlist] = si[1023];
     *n_items = si[1023];
+    if (chk.xcd)  // the end bound, and the bounds of queues with no list (nlist < 8)
+      for (int x = min(nlist, 8); x <= 8; ++x) n_items[1 + x] = si[1023];
   }
 }
 

@@ -1,4 +1,4 @@
-// pq32.hip -- the IVF_PQ list scan on the matrix cores (gfx950, round 4).
+// pq32.hip -- the IVF_PQ list scan on the matrix cores (gfx950).
 //
 // IvfPqVectorIndex.Search (src/Pyrope.GarnetServer/Vector/IvfPqVectorIndex.cs:118-212) scores a row of a
 // probed list by the ADC sum  distSq = sum_m table[m][code_m]  (:182-194) with
@@ -10,14 +10,24 @@
 //   -distSq  =  -|r - x^|^2  =  2 r.x^ - |x^|^2 - |r|^2        (real arithmetic)
 //
 // with x^ the decoded residual (the concatenated sub-centroids C[m][code_m]).  r.x^ runs on
-// v_mfma_f32_32x32x16_f16: a 32-row tile is decoded on the fly, k-step s (16 dims = subspaces 2s, 2s+1,
-// dsub = 8) of lane (r, h) being the fp16 sub-centroid C[2s + h][code] gathered from the fp16 codebook
-// (393 KB at P1, L2-resident).  |x^|^2 is a per-row term fixed at build.  The approximate score plus the
-// error bound of the fp16 filter (stream_ub_terms: the same terms as the IVF tiles' -- x^ plays x - c,
-// X = |x^|) bounds the reference's fp32 ADC sum from above; rows whose bound reaches the query's sampled
-// threshold are emitted, the best 64 per query merged (cand_merge_kernel), and pq_refine_kernel computes
-// the reference's own table sum for them, in m order, and certifies the top k (k-th exact > the K1-th
-// bound).  Queries that fail are re-run on the LUT path (engine.cpp).
+// v_mfma_f32_32x32x16_f16 with the rows as the A operand: lane (r, h) of k-step s holds dims
+// 16 s + 8 h .. +7 of row r, decoded from the fp16 codebook (cb16 [M][256][dsub], L2-resident) by the
+// code(s) of the subspace(s) those 8 dims fall in -- dsub 8: one 16-byte gather; 16 / 32: one 16-byte
+// gather at offset (16 s + 8 h) mod dsub; 4: two 8-byte gathers.  |x^|^2 is a per-row term fixed at
+// build.  The approximate score plus the error bound of the fp16 filter (stream_ub_terms: the same terms
+// as the IVF tiles' -- x^ plays x - c, X = |x^|) bounds the reference's fp32 ADC sum from above; rows whose
+// bound reaches the query's sampled threshold are emitted, the best 64 per query merged
+// (cand_merge_kernel), and pq_refine_kernel computes the reference's own table sum for them, in m order,
+// and certifies the top k (k-th exact > the K1-th bound).  Queries that fail re-run on the LUT scan.
+//
+// Two tile loops, by the k-step count KS = D / 16:
+//   * KS <= 8 (D <= 128, e.g. the registry's d=128 m=4 default): a tile's KS decoded A operands stay in
+//     registers while every query group of the item runs against them (up to 16 groups = 512 queries: the
+//     query operands fill 128 KiB of LDS);
+//   * KS > 8 (P1: D = 768): k-outer -- each decoded k-step feeds PQG groups (<= 144 KiB of query operands:
+//     PQG = 4 up to D = 576, 3 up to 768, 2 up to 1152), the accumulators of all groups in registers.
+// Items of one list chunk go to one XCD's queue (ivf items in XCD order, IvfChunking::xcd): their blocks
+// stream the same codes at about the same time, so the chunk leaves HBM once per XCD L2, not once per item.
 #pragma clang fp contract(off)
 
 #include <hip/hip_runtime.h>
@@ -25,6 +35,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <stdexcept>
 
 #include "kernels.h"
 
@@ -39,18 +50,46 @@ __device__ __forceinline__ size_t blk_off(int64_t r, int d, int D) {
 }
 #include "vmath.h"
 
-constexpr int PNW = 16;      // waves per scan block
-constexpr int PQG = 3;       // 32-query groups per item (96 queries: 144 KiB of operands at D = 768)
-constexpr int PQMAX = 32 * PQG;
-constexpr int PSAMPLE_TILES = 2 * PNW;
-constexpr int PSV = 2 * PNW;  // sample values per (query, probe): one per (wave, lane half)
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+
+constexpr int PNW = 16;                 // waves per scan block
+constexpr int PSAMPLE_TILES = 2 * PNW;  // the sample pass: the first 32 tiles (1,024 rows) of every list
+constexpr int PSV = 2 * PNW;            // sample values per (query, probe): one per (wave, lane half)
+constexpr int PEB = 768;                // LDS-staged emitted rows per item
+constexpr int PQ_KS_MAX = 72;           // D <= 1152
 
 __device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf(a, fmaxf(b, c)); }
 
+// ---- geometry ----
+struct PqGeo {
+  int ks;    // k-steps (D / 16)
+  int dsub;  // dims per subspace
+  int mw;    // 16-byte code words per row (16 subspaces each)
+  int res;   // 1: A-resident tile loop (KS <= 8)
+  int kp;    // A-resident: padded k-steps (8); k-outer: query groups per item
+  int qmax;  // queries per item
+};
+PqGeo pq_geo(int dim, int M) {
+  PqGeo g{};
+  g.ks = dim / 16;
+  g.dsub = M > 0 ? dim / M : 0;
+  g.mw = (M + 15) / 16;
+  g.res = g.ks <= 8;  // (16 resident k-steps spill: 64 VGPRs of A besides the accumulator and the row terms)
+  if (g.res) {
+    g.kp = 8;
+    g.qmax = 32 * 16;
+  } else {
+    g.kp = g.ks <= 36 ? 4 : g.ks <= 48 ? 3 : 2;
+    g.qmax = 32 * g.kp;
+  }
+  return g;
+}
+
 // ---- build: the tile layout of the codes, |x^|^2 per row, the fp16 codebook ----
-// tile t (rows 32t .. 32t + 31 of the list-major positions), lane l = 32h + r: bytes s = 0 .. M/2 - 1 are
-// code[row 32t + r][2s + h], at ((t * 64 + l) * MB + s)
-__global__ void pq_pack_kernel(const uint8_t *codes_rm, const int64_t *src, int64_t tot, int M, int MB,
+// tile t (positions 32t .. 32t + 31 of the list-major rows), row r: code word w (codes 16w .. 16w + 15,
+// zero past M) at byte ((t * mw + w) * 32 + r) * 16 -- a wave's 32 rows read one word in 512 contiguous bytes
+__global__ void pq_pack_kernel(const uint8_t *codes_rm, const int64_t *src, int64_t tot, int M, int mw, int dsub,
                                const float *cb, int ksub, uint8_t *cpack, float *nrm) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= tot) return;
@@ -58,23 +97,28 @@ __global__ void pq_pack_kernel(const uint8_t *codes_rm, const int64_t *src, int6
   const int64_t t = p >> 5;
   const int r = (int)(p & 31);
   float n = 0.0f;
-  for (int m = 0; m < M; ++m) {
-    const int c = sr >= 0 ? codes_rm[(size_t)sr * M + m] : 0;
-    cpack[((size_t)t * 64 + (m & 1) * 32 + r) * MB + (m >> 1)] = (uint8_t)c;
-    if (sr >= 0) {
-      const float *v = cb + ((size_t)m * ksub + c) * 8;
-#pragma unroll
-      for (int u = 0; u < 8; ++u) n += v[u] * v[u];
+  for (int w = 0; w < mw; ++w) {
+    uint32_t cw[4] = {0u, 0u, 0u, 0u};
+    for (int j = 0; j < 16; ++j) {
+      const int m = 16 * w + j;
+      if (m >= M || sr < 0) continue;
+      const int c = codes_rm[(size_t)sr * M + m];
+      cw[j >> 2] |= (uint32_t)c << (8 * (j & 3));
+      const float *v = cb + ((size_t)m * ksub + c) * dsub;
+      for (int u = 0; u < dsub; ++u) n += v[u] * v[u];
     }
+    *reinterpret_cast<u4v *>(cpack + (((size_t)t * mw + w) * 32 + r) * 16) = (u4v){cw[0], cw[1], cw[2], cw[3]};
   }
   nrm[p] = n;
 }
 
-__global__ void pq_cb16_kernel(const float *cb, int M, int ksub, float sc, _Float16 *cb16) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // [M][256][8]
-  if (e >= (int64_t)M * 256 * 8) return;
-  const int j = (int)((e >> 3) & 255), m = (int)(e >> 11), u = (int)(e & 7);
-  cb16[e] = j < ksub ? (_Float16)(cb[((size_t)m * ksub + j) * 8 + u] * sc) : (_Float16)0.0f;
+__global__ void pq_cb16_kernel(const float *cb, int M, int ksub, int dsub, float sc, _Float16 *cb16) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // [M][256][dsub]
+  if (e >= (int64_t)M * 256 * dsub) return;
+  const int u = (int)(e % dsub);
+  const int j = (int)((e / dsub) & 255);
+  const int m = (int)(e / ((int64_t)dsub * 256));
+  cb16[e] = j < ksub ? (_Float16)(cb[((size_t)m * ksub + j) * dsub + u] * sc) : (_Float16)0.0f;
 }
 
 // meta of a position: -|x^|^2 for a visible row, -inf otherwise (a shadowed or padding position)
@@ -85,26 +129,22 @@ __global__ void pq_meta_kernel(const float *nrm, const uint8_t *live, int64_t to
   meta[p] = !live[p] || isnan(n) ? -INFINITY : isinf(n) ? INFINITY : -n;
 }
 
-// ---- the query operands per (list, query) pair: one wave per pair ----
+// ---- the query operands per (list, query) position: one wave per position ----
 // r = q - c(list) as the reference forms resQuery (:162-164), its scale, {f, -|r|^2 + E_pair}
-template <int D>
-__global__ __launch_bounds__(256) void pq_prep_kernel(StreamArgs a) {
-  constexpr int PER = D / 64;  // dims per lane
+__global__ __launch_bounds__(256) void pq_prep_kernel(StreamArgs a, int64_t npos) {
   const int lane = threadIdx.x & 63;
-  const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int item = unit / PQMAX, qi = unit - item * PQMAX;
-  if (item >= *a.n_items) return;
-  const ScanItem it = a.items[item];
-  if (it.part != 0 || qi >= it.qcnt) return;
-  const int pos = it.qbeg + qi;
-  const int q = a.qlist[pos] / a.nparts;
-  float rv[PER], cq = 0.0f, amax = 0.0f;
-#pragma unroll
-  for (int u = 0; u < PER; ++u) {
-    const int d = lane + 64 * u;
-    rv[u] = a.queries[(size_t)q * D + d] - a.cents[(size_t)it.list * D + d];
-    cq += rv[u] * rv[u];
-    amax = fmaxf(amax, fabsf(rv[u]));
+  const int64_t pos = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (pos >= npos) return;
+  const int D = a.dim;
+  const int slot = a.qlist[pos];
+  const int q = slot / a.nparts;
+  const int lst = a.probes[(size_t)q * a.nprobe + (slot % a.nparts) / a.cmax];
+  const float *qp = a.queries + (size_t)q * D, *cp = a.cents + (size_t)lst * D;
+  float cq = 0.0f, amax = 0.0f;
+  for (int d = lane; d < D; d += 64) {
+    const float rv = qp[d] - cp[d];
+    cq += rv * rv;
+    amax = fmaxf(amax, fabsf(rv));
   }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
@@ -113,165 +153,325 @@ __global__ __launch_bounds__(256) void pq_prep_kernel(StreamArgs a) {
   }
   const float ep = a.kq * cq + a.kqa * sqrtf(cq);
   const float sq = pow2_scale(amax);
-#pragma unroll
-  for (int u = 0; u < PER; ++u) a.bq[(size_t)pos * D + lane + 64 * u] = (_Float16)(rv[u] * sq);
+  for (int d = lane; d < D; d += 64) a.bq[(size_t)pos * D + d] = (_Float16)((qp[d] - cp[d]) * sq);  // exact scaling
   if (lane == 0) a.qsc[pos] = make_float2(2.0f / (sq * a.sx), -cq + ep);
 }
 
-// ---- the scan (SAMPLE: the first PSAMPLE_TILES tiles of every list, maxima per (wave, lane half)) ----
-// a.h16: the tile code layout (pq_pack_kernel); a.cents doubles as nothing; pq: the fp16 codebook
-template <int D, bool SAMPLE, int AB = 0>
-__global__ __launch_bounds__(64 * PNW, 1) void pq_scan_kernel(StreamArgs a, const _Float16 *cb16) {
-  constexpr int KS = D / 16;                 // k-steps = subspace pairs
-  constexpr int MB = (KS + 15) / 16 * 16;    // code bytes per lane per tile
-  constexpr int PIECES = PQG * KS;
-  __shared__ __attribute__((aligned(16))) char bl[PIECES * 1024];
-  __shared__ float2 qf[PQMAX], qz[PQMAX];
-  __shared__ int cnt_l[PQMAX];       // the item's staged rows per query slot (cand_flush)
-  __shared__ int base_l[PQMAX];
-  __shared__ int item_sh, eb_n;
-  constexpr int EB = 768;
-  __shared__ uint2 eb[EB];
+// ---- decode: k-step u of code word w (16 subspaces = dsub k-steps), lane half h ----
+template <int DSUB>
+__device__ __forceinline__ h8v pq_decode(const uint32_t (&cw)[4], const _Float16 *cb16, int w, int u, int h) {
+  if constexpr (DSUB == 4) {  // dims 8h .. 8h+7 of the k-step: subspaces 4u + 2h, 4u + 2h + 1 of the word
+    const uint32_t sh = 16u * (uint32_t)h;
+    const uint32_t c0 = (cw[u] >> sh) & 0xFFu, c1 = (cw[u] >> (sh + 8u)) & 0xFFu;
+    const int m0 = 16 * w + 4 * u + 2 * h;
+    const u2v lo = *reinterpret_cast<const u2v *>(cb16 + ((size_t)m0 * 256 + c0) * 4);
+    const u2v hi = *reinterpret_cast<const u2v *>(cb16 + ((size_t)(m0 + 1) * 256 + c1) * 4);
+    return __builtin_bit_cast(h8v, ((u4v){lo.x, lo.y, hi.x, hi.y}));
+  } else if constexpr (DSUB == 8) {  // subspace 2u + h
+    const uint32_t c = (cw[u >> 1] >> (8u * (uint32_t)((2 * u) & 3) + 8u * (uint32_t)h)) & 0xFFu;
+    const int m = 16 * w + 2 * u + h;
+    return *reinterpret_cast<const h8v *>(cb16 + ((size_t)m * 256 + c) * 8);
+  } else {  // 16, 32: subspace u / (DSUB / 16), both halves; dims (16 u + 8 h) mod DSUB of its sub-centroid
+    constexpr int SPK = DSUB / 16;  // k-steps per subspace
+    const int j = u / SPK;
+    const uint32_t c = (cw[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+    const int m = 16 * w + j;
+    return *reinterpret_cast<const h8v *>(cb16 + ((size_t)m * 256 + c) * DSUB + 16 * (u % SPK) + 8 * h);
+  }
+}
+
+__device__ __forceinline__ void split_word(const u4v v, uint32_t (&cw)[4]) {
+  cw[0] = v.x;
+  cw[1] = v.y;
+  cw[2] = v.z;
+  cw[3] = v.w;
+}
+
+// ---- work: per-XCD item queues (n_items[1 .. 9]: the queues' item bounds; work[0 .. 7]: their counters).
+// A block takes items from the queue of its XCD group (blockIdx % 8: blocks b and b + 8 share an XCD),
+// then from the others'.  Thread 0 only; qx / tried persist across the block's items.
+__device__ __forceinline__ int pq_next_item(const StreamArgs &a, int &qx, int &tried) {
+  const int32_t *qb = a.n_items + 1;
+  while (tried < 8) {
+    const int t = atomicAdd(a.work + qx, 1);
+    if (qb[qx] + t < qb[qx + 1]) return qb[qx] + t;
+    qx = (qx + 1) & 7;
+    ++tried;
+  }
+  return -1;
+}
+
+// per-item LDS state shared by both tile loops
+template <int QMAX>
+struct PqItemLds {
+  float2 qf[QMAX], qz[QMAX];  // {f, lowered T - cq} / {cq, query (main) or sample slot (SAMPLE)}
+  int cnt_l[QMAX], base_l[QMAX];
+  uint2 eb[PEB];
+  int item, eb_n;
+};
+
+// prologue: the item's query operands into LDS (piece (j, s) = group j, k-step s at (j * kstride + s) KiB;
+// lane (r, h) carries dims 16 s + 8 h .. +7 of query 32 j + r) and its per-query scalars
+template <int QMAX, bool SAMPLE>
+__device__ __forceinline__ void pq_item_prologue(const StreamArgs &a, const ScanItem &it, int KS, int kstride,
+                                                 uint32_t bl_base, PqItemLds<QMAX> &L) {
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int qcnt = it.qcnt, ng = (qcnt + 31) >> 5;
+  for (int p = w; p < ng * KS; p += PNW) {
+    const int j = p / KS, s = p - j * KS;
+    const int qi = min(32 * j + r, qcnt - 1);
+    glds<16>(a.bq + (size_t)(it.qbeg + qi) * a.dim + 16 * s + 8 * h, bl_base + (uint32_t)((j * kstride + s) * 1024));
+  }
+  for (int i = tid; i < ng * 32; i += 64 * PNW) {
+    float2 v = make_float2(0.0f, __builtin_nanf(""));
+    float cqv = 0.0f;
+    int o = -1;
+    if (i < qcnt) {
+      const int pos = it.qbeg + i;
+      const int slot = a.qlist[pos];
+      const float2 fc = a.qsc[pos];
+      const int q = slot / a.nparts;
+      const float T = (!SAMPLE && a.thr) ? a.thr[q] : -INFINITY;
+      v = make_float2(fc.x, lower_thr(T, fc.y));
+      cqv = fc.y;
+      o = SAMPLE ? q * a.nprobe + (slot % a.nparts) / a.cmax : q;
+    }
+    L.qf[i] = v;
+    L.qz[i] = make_float2(cqv, __int_as_float(o));
+    L.cnt_l[i] = 0;
+  }
+  if (tid == 0) L.eb_n = 0;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+// the row terms of tile t: lane (r, h) holds rows rt + 8b + 4h + i (b < 4, i < 4), the 32x32 C layout
+__device__ __forceinline__ void pq_row_terms(const StreamArgs &a, int rt, int rlim, int h, float (&mr)[16]) {
+  const size_t mo = (size_t)rt + 4 * h;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const f4v m4 = *reinterpret_cast<const f4v *>(a.mub + mo + 8 * b);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) mr[4 * b + i] = rt + 8 * b + 4 * h + i < rlim ? m4[i] : -INFINITY;
+  }
+}
+
+// epilogue of group g against one tile (main pass): bounds -> emitted rows (LDS-staged, or straight to
+// the query's buffer when the stage is full / the chunk too long for the packed row offset)
+template <int QMAX>
+__device__ __forceinline__ void pq_emit(const StreamArgs &a, f16v acc, int g, int r, int h, int rt, int r0, bool stage,
+                                        const float (&mr)[16], PqItemLds<QMAX> &L) {
+  const int qi = 32 * g + r;
+  const float2 q = L.qf[qi];
+#pragma unroll
+  for (int v = 0; v < 16; ++v) acc[v] = fmaf(q.x, acc[v], mr[v]);
+  float mx = max3f(acc[0], acc[1], acc[2]);
+#pragma unroll
+  for (int v = 3; v < 15; v += 2) mx = max3f(mx, acc[v], acc[v + 1]);
+  mx = fmaxf(mx, acc[15]);
+  if (__builtin_amdgcn_ballot_w64(mx >= q.y) == 0ull) return;
+  const float cq = L.qz[qi].x;
+  uint32_t base = ((uint32_t)qi << 23) | (uint32_t)(rt - r0 + 4 * h);
+  asm volatile("" : "+v"(base));
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const bool p = acc[e] >= q.y;
+    if (__builtin_amdgcn_ballot_w64(p) == 0ull) continue;
+    if (p) {
+      const float sc = acc[e] + cq;
+      const uint32_t word = base + (uint32_t)(8 * (e >> 2) + (e & 3));
+      const int at = stage ? atomicAdd(&L.eb_n, 1) : PEB;
+      if (at < PEB) L.eb[at] = make_uint2(__float_as_uint(sc), word);
+      else cand_put(a, __float_as_int(L.qz[qi].y), sc, a.key_base | (uint32_t)(r0 + (int)(word & 0x7FFFFFu)));
+    }
+  }
+}
+
+__device__ __forceinline__ float pq_tile_max(const f16v &acc, float f, const float (&mr)[16]) {
+  float y[16];
+#pragma unroll
+  for (int v = 0; v < 16; ++v) y[v] = fmaf(f, acc[v], mr[v]);
+  float mx = max3f(y[0], y[1], y[2]);
+#pragma unroll
+  for (int v = 3; v < 15; v += 2) mx = max3f(mx, y[v], y[v + 1]);
+  return fmaxf(mx, y[15]);
+}
+
+// ---- tile loop 1 (KS <= 16): decoded A resident, every group against it ----
+template <int KSP, int DSUB, bool SAMPLE>
+__global__ __launch_bounds__(64 * PNW, 1) void pq_scan_res_kernel(StreamArgs a, const _Float16 *cb16, int mw) {
+  constexpr int QG = KSP <= 8 ? 16 : 8;
+  constexpr int QMAX = 32 * QG;
+  constexpr int NW = (KSP + DSUB - 1) / DSUB;  // code words covering KSP k-steps
+  __shared__ __attribute__((aligned(16))) char bl[QG * KSP * 1024];
+  __shared__ PqItemLds<QMAX> L;
   const uint32_t bl_base = (uint32_t)(size_t)(lds_void *)bl;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const uint8_t *cpk = reinterpret_cast<const uint8_t *>(a.h16);
+  const int KS = a.dim >> 4;
+  int qx = blockIdx.x & 7, tried = 0;
 
   for (;;) {
-    if (tid == 0) item_sh = atomicAdd(a.work, 1);
+    if (tid == 0) L.item = pq_next_item(a, qx, tried);
     __syncthreads();
-    const int item = item_sh;
+    const int item = L.item;
     __syncthreads();
-    if (item >= *a.n_items) return;
+    if (item < 0) return;
     const ScanItem it = a.items[item];
     if (SAMPLE && it.part != 0) continue;
+    pq_item_prologue<QMAX, SAMPLE>(a, it, KS, KSP, bl_base, L);
     const int qcnt = it.qcnt, ng = (qcnt + 31) >> 5;
-    {
-      for (int p = w; p < ng * KS; p += PNW) {
-        const int j = p / KS, s = p - j * KS;
-        const int qi = min(32 * j + r, qcnt - 1);
-        glds<16>(a.bq + (size_t)(it.qbeg + qi) * D + 16 * s + 8 * h, bl_base + (uint32_t)(p * 1024));
-      }
-      for (int i = tid; i < PQMAX; i += 64 * PNW) {
-        float2 v = make_float2(0.0f, __builtin_nanf(""));
-        float cqv = 0.0f;
-        int o = -1;
-        if (i < qcnt) {
-          const int pos = it.qbeg + i;
-          const int slot = a.qlist[pos];
-          const float2 fc = a.qsc[pos];
-          const int q = slot / a.nparts;
-          const float T = (!SAMPLE && a.thr) ? a.thr[q] : -INFINITY;
-          v = make_float2(fc.x, lower_thr(T, fc.y));
-          cqv = fc.y;
-          o = SAMPLE ? q * a.nprobe + (slot % a.nparts) / a.cmax : q;
-        }
-        qf[i] = v;
-        qz[i] = make_float2(cqv, __int_as_float(o));
-        cnt_l[i] = 0;
-      }
-      if (tid == 0) eb_n = 0;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
     const int r0 = it.row_begin;
     int nt = (it.row_end - r0 + 31) >> 5;
     if (SAMPLE) nt = min(nt, PSAMPLE_TILES);
     const int rlim = it.row_end;
     const bool stage = it.row_end - r0 < (1 << 23);
+    float smx[SAMPLE ? QG : 1];
+#pragma unroll
+    for (int g = 0; g < (SAMPLE ? QG : 1); ++g) smx[g] = -INFINITY;
+#pragma unroll 1
+    for (int t = w; t < nt; t += PNW) {
+      const int rt = r0 + 32 * t;
+      h8v A[KSP];
+      {
+        const u4v *cp = reinterpret_cast<const u4v *>(cpk + ((size_t)(rt >> 5) * mw * 32 + r) * 16);
+#pragma unroll
+        for (int wi = 0; wi < NW; ++wi) {
+          uint32_t cw[4] = {0u, 0u, 0u, 0u};
+          if (wi < mw) split_word(cp[wi * 32], cw);
+#pragma unroll
+          for (int u = 0; u < DSUB; ++u) {
+            const int s = wi * DSUB + u;
+            if (s >= KSP) break;
+            A[s] = s < KS ? pq_decode<DSUB>(cw, cb16, wi, u, h) : (h8v){};
+          }
+        }
+      }
+      float mr[16];
+      pq_row_terms(a, rt, rlim, h, mr);
+      auto group = [&](int g) {
+        f16v acc = {};
+#pragma unroll
+        for (int s = 0; s < KSP; ++s) {
+          if (s >= KS) break;
+          const h8v B = *reinterpret_cast<const h8v *>(bl + (g * KSP + s) * 1024 + lane * 16);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[s], B, acc, 0, 0, 0);
+        }
+        return acc;
+      };
+      if constexpr (SAMPLE) {
+#pragma unroll
+        for (int g = 0; g < QG; ++g) {
+          if (g >= ng) break;
+          smx[g] = fmaxf(smx[g], pq_tile_max(group(g), L.qf[32 * g + r].x, mr));
+        }
+      } else {
+#pragma unroll 1
+        for (int g = 0; g < ng; ++g) pq_emit<QMAX>(a, group(g), g, r, h, rt, r0, stage, mr, L);
+      }
+    }
+    if constexpr (SAMPLE) {
+#pragma unroll
+      for (int g = 0; g < QG; ++g) {
+        const int qi = 32 * g + r;
+        if (qi < qcnt) a.samp[(size_t)__float_as_int(L.qz[qi].y) * PSV + 2 * w + h] = smx[g] + L.qz[qi].x;
+      }
+      __syncthreads();
+      continue;
+    }
+    __syncthreads();
+    cand_flush<64 * PNW>(a, L.eb, min(L.eb_n, PEB), qcnt, r0, L.cnt_l, L.base_l,
+                         [&](int i) { return __float_as_int(L.qz[i].y); });
+  }
+}
 
-    auto put = [&](int qi, float sc, int row) { cand_put(a, __float_as_int(qz[qi].y), sc, a.key_base | (uint32_t)row); };
-    float smx[PQG];  // SAMPLE: this lane's best bound per query group
+// ---- tile loop 2 (KS > 16): k-outer, each decoded k-step against PQG groups ----
+template <int PQG, int DSUB, bool SAMPLE>
+__global__ __launch_bounds__(64 * PNW, 1) void pq_scan_kout_kernel(StreamArgs a, const _Float16 *cb16, int mw) {
+  constexpr int QMAX = 32 * PQG;
+  constexpr int WPI = DSUB >= 16 ? 1 : 16 / DSUB;  // code words per iteration (16 k-steps at dsub <= 16)
+  __shared__ __attribute__((aligned(16))) char bl[144 * 1024];
+  __shared__ PqItemLds<QMAX> L;
+  const uint32_t bl_base = (uint32_t)(size_t)(lds_void *)bl;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const uint8_t *cpk = reinterpret_cast<const uint8_t *>(a.h16);
+  const int KS = a.dim >> 4;
+  int qx = blockIdx.x & 7, tried = 0;
+
+  for (;;) {
+    if (tid == 0) L.item = pq_next_item(a, qx, tried);
+    __syncthreads();
+    const int item = L.item;
+    __syncthreads();
+    if (item < 0) return;
+    const ScanItem it = a.items[item];
+    if (SAMPLE && it.part != 0) continue;
+    pq_item_prologue<QMAX, SAMPLE>(a, it, KS, KS, bl_base, L);
+    const int qcnt = it.qcnt, ng = (qcnt + 31) >> 5;
+    const int r0 = it.row_begin;
+    int nt = (it.row_end - r0 + 31) >> 5;
+    if (SAMPLE) nt = min(nt, PSAMPLE_TILES);
+    const int rlim = it.row_end;
+    const bool stage = it.row_end - r0 < (1 << 23);
+    float smx[PQG];
 #pragma unroll
     for (int g = 0; g < PQG; ++g) smx[g] = -INFINITY;
 #pragma unroll 1
     for (int t = w; t < nt; t += PNW) {
-      const uint4 *cp = reinterpret_cast<const uint4 *>(cpk + ((size_t)(r0 / 32 + t) * 64 + lane) * MB);
-      float mr[16];
-      {
-        const int rt = r0 + 32 * t;
-        const size_t mo = (size_t)rt + 4 * h;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          const f4v m4 = *reinterpret_cast<const f4v *>(a.mub + mo + 8 * b);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) mr[4 * b + i] = rt + 8 * b + 4 * h + i < rlim ? m4[i] : -INFINITY;
-        }
-      }
-      // k-outer: decode k-step s (one 16-B gather per lane) and run it against every group, 16 k-steps
-      // (one 16-byte word of codes) at a time
+      const int rt = r0 + 32 * t;
+      const u4v *cp = reinterpret_cast<const u4v *>(cpk + ((size_t)(rt >> 5) * mw * 32 + r) * 16);
       f16v acc[PQG];
 #pragma unroll
       for (int g = 0; g < PQG; ++g) acc[g] = (f16v){};
-      const char *cbb = reinterpret_cast<const char *>(cb16) + (size_t)h * 256 * 16;
+      u4v nxt[WPI];  // the next iteration's code words, loaded one iteration ahead
+#pragma unroll
+      for (int wi = 0; wi < WPI; ++wi) nxt[wi] = wi < mw ? cp[wi * 32] : (u4v){0u, 0u, 0u, 0u};
 #pragma unroll 1
-      for (int i = 0; i < MB / 16; ++i) {
-        const uint4 cv = cp[i];
-        const uint32_t cw[4] = {cv.x, cv.y, cv.z, cv.w};
+      for (int w0 = 0; w0 < mw; w0 += WPI) {
+        uint32_t cw[WPI][4];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-          const int s = 16 * i + u;
-          if (s >= KS) break;
-          const uint32_t c = (cw[u >> 2] >> (8 * (u & 3))) & 0xFFu;
-          h8v A;
-          if constexpr (AB == 2) A = (h8v){};  // measurement only: no decode gathers
-          else A = *reinterpret_cast<const h8v *>(cbb + (size_t)(2 * s) * 256 * 16 + c * 16);
+        for (int wi = 0; wi < WPI; ++wi) {
+          split_word(nxt[wi], cw[wi]);
+          const int wn = w0 + WPI + wi;
+          nxt[wi] = wn < mw ? cp[wn * 32] : (u4v){0u, 0u, 0u, 0u};
+        }
 #pragma unroll
-          for (int g = 0; g < PQG; ++g) {
-            if (g >= ng) break;  // (wave-uniform) a short item skips the empty groups' MFMAs
-            const h8v B = *reinterpret_cast<const h8v *>(bl + (g * KS + s) * 1024 + lane * 16);
-            acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, B, acc[g], 0, 0, 0);
+        for (int wi = 0; wi < WPI; ++wi) {
+#pragma unroll
+          for (int u = 0; u < DSUB; ++u) {
+            const int s = (w0 + wi) * DSUB + u;
+            if (s >= KS) break;
+            const h8v A = pq_decode<DSUB>(cw[wi], cb16, w0 + wi, u, h);
+#pragma unroll
+            for (int g = 0; g < PQG; ++g) {
+              if (g >= ng) break;  // (wave-uniform) a short item skips the empty groups' MFMAs
+              const h8v B = *reinterpret_cast<const h8v *>(bl + (g * KS + s) * 1024 + lane * 16);
+              acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, B, acc[g], 0, 0, 0);
+            }
           }
         }
       }
-      const int rt = r0 + 32 * t;
+      float mr[16];
+      pq_row_terms(a, rt, rlim, h, mr);
 #pragma unroll
       for (int g = 0; g < PQG; ++g) {
         if (g >= ng) break;
-        const int qi = 32 * g + r;
-        const float2 q = qf[qi];
-#pragma unroll
-        for (int v = 0; v < 16; ++v) acc[g][v] = fmaf(q.x, acc[g][v], mr[v]);
-        float mx = max3f(acc[g][0], acc[g][1], acc[g][2]);
-#pragma unroll
-        for (int v = 3; v < 15; v += 2) mx = max3f(mx, acc[g][v], acc[g][v + 1]);
-        mx = fmaxf(mx, acc[g][15]);
-        if constexpr (SAMPLE) {
-          smx[g] = fmaxf(smx[g], mx);
-          continue;
-        }
-        if constexpr (AB == 1) {
-          if (mx == 12345.0f) cnt_l[0] = 1;
-          continue;
-        }
-        if (__builtin_amdgcn_ballot_w64(mx >= q.y) == 0ull) continue;
-        const float cq = qz[qi].x;
-        uint32_t base = ((uint32_t)qi << 23) | (uint32_t)(rt - r0 + 4 * h);
-        asm volatile("" : "+v"(base));
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const bool p = acc[g][e] >= q.y;
-          if (__builtin_amdgcn_ballot_w64(p) == 0ull) continue;
-          if (p) {
-            const float sc = acc[g][e] + cq;
-            const uint32_t word = base + (uint32_t)(8 * (e >> 2) + (e & 3));
-            const int at = stage ? atomicAdd(&eb_n, 1) : EB;
-            if (at < EB) eb[at] = make_uint2(__float_as_uint(sc), word);
-            else put(qi, sc, r0 + (int)(word & 0x7FFFFFu));
-          }
-        }
+        if constexpr (SAMPLE) smx[g] = fmaxf(smx[g], pq_tile_max(acc[g], L.qf[32 * g + r].x, mr));
+        else pq_emit<QMAX>(a, acc[g], g, r, h, rt, r0, stage, mr, L);
       }
     }
     if constexpr (SAMPLE) {
 #pragma unroll
       for (int g = 0; g < PQG; ++g) {
         const int qi = 32 * g + r;
-        if (qi < qcnt) a.samp[(size_t)__float_as_int(qz[qi].y) * PSV + 2 * w + h] = smx[g] + qz[qi].x;
+        if (qi < qcnt) a.samp[(size_t)__float_as_int(L.qz[qi].y) * PSV + 2 * w + h] = smx[g] + L.qz[qi].x;
       }
       __syncthreads();
       continue;
     }
     __syncthreads();
-    cand_flush<64 * PNW>(a, eb, min(eb_n, EB), qcnt, r0, cnt_l, base_l, [&](int i) { return __float_as_int(qz[i].y); });
+    cand_flush<64 * PNW>(a, L.eb, min(L.eb_n, PEB), qcnt, r0, L.cnt_l, L.base_l,
+                         [&](int i) { return __float_as_int(L.qz[i].y); });
   }
 }
 
@@ -279,6 +479,10 @@ __global__ __launch_bounds__(64 * PNW, 1) void pq_scan_kernel(StreamArgs a, cons
 // One wave per query; lane l holds merged candidate l (bound ms, position mk: >= 0 a row, -2 a floor,
 // -1 none).  A lane's exact score: resQuery of the row's list, then distSq += table[m][code_m] in m
 // order (IvfPqVectorIndex.cs:182-194; table entries L2SquaredUnsafe, ProductQuantizer.cs:107-117).
+struct Res {  // resQuery_m on the fly: q_i - c_i, the reference's fp32 subtraction
+  const float *q, *c;
+  __device__ float operator()(int i) const { return q[i] - c[i]; }
+};
 __global__ __launch_bounds__(256) void pq_refine_kernel(PqRefineArgs a) {
   const int lane = threadIdx.x & 63;
   const int64_t wq = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -297,14 +501,12 @@ __global__ __launch_bounds__(256) void pq_refine_kernel(PqRefineArgs a) {
     }
     const float *qv = a.queries + (size_t)q * a.dim;
     const float *cv = a.cents + (size_t)lo * a.dim;
-    const uint8_t *cp = a.cpack + ((size_t)(key >> 5) * 64 + (key & 31)) * a.mb;
+    const uint8_t *cp = a.cpack + ((size_t)(key >> 5) * a.mw * 32 + (key & 31)) * 16;
+    const int ds = a.dsub;
     float dist = 0.0f;
     for (int m = 0; m < a.M; ++m) {
-      const int c = cp[(size_t)(m & 1) * 32 * a.mb + (m >> 1)];
-      float rq[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) rq[u] = qv[8 * m + u] - cv[8 * m + u];
-      dist = dist + em_l2sq_unsafe(Lin{rq}, Off{a.codebooks + ((size_t)m * a.ksub + c) * 8}, 8);
+      const int c = cp[(size_t)(m >> 4) * 512 + (m & 15)];
+      dist = dist + em_l2sq_unsafe(Res{qv + m * ds, cv + m * ds}, Off{a.codebooks + ((size_t)m * a.ksub + c) * ds}, ds);
     }
     sc = -dist;
   }
@@ -345,45 +547,71 @@ __global__ __launch_bounds__(256) void pq_refine_kernel(PqRefineArgs a) {
   }
 }
 
-template <int D>
-void launch_pq_scan_d(const StreamArgs &a, const _Float16 *cb16, int max_items, bool sample, hipStream_t st) {
-  const int grid = std::max(1, std::min(max_items, device_cus()));
-  if (sample) hipLaunchKernelGGL((pq_scan_kernel<D, true>), dim3(grid), dim3(64 * PNW), 0, st, a, cb16);
-  else if (a.ablate & 64) hipLaunchKernelGGL((pq_scan_kernel<D, false, 1>), dim3(grid), dim3(64 * PNW), 0, st, a, cb16);
-  else if (a.ablate & 128) hipLaunchKernelGGL((pq_scan_kernel<D, false, 2>), dim3(grid), dim3(64 * PNW), 0, st, a, cb16);
-  else hipLaunchKernelGGL((pq_scan_kernel<D, false>), dim3(grid), dim3(64 * PNW), 0, st, a, cb16);
+template <class K>
+void pq_launch(K kern, int grid, const StreamArgs &a, const _Float16 *cb16, int mw, hipStream_t st) {
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * PNW), 0, st, a, cb16, mw);
+}
+template <int DSUB>
+void launch_scan_dsub(const StreamArgs &a, const _Float16 *cb16, const PqGeo &g, int grid, bool sample, hipStream_t st) {
+  if (g.res) {
+    if (sample) pq_launch(pq_scan_res_kernel<8, DSUB, true>, grid, a, cb16, g.mw, st);
+    else pq_launch(pq_scan_res_kernel<8, DSUB, false>, grid, a, cb16, g.mw, st);
+  } else if (g.kp == 4) {
+    if (sample) pq_launch(pq_scan_kout_kernel<4, DSUB, true>, grid, a, cb16, g.mw, st);
+    else pq_launch(pq_scan_kout_kernel<4, DSUB, false>, grid, a, cb16, g.mw, st);
+  } else if (g.kp == 3) {
+    if (sample) pq_launch(pq_scan_kout_kernel<3, DSUB, true>, grid, a, cb16, g.mw, st);
+    else pq_launch(pq_scan_kout_kernel<3, DSUB, false>, grid, a, cb16, g.mw, st);
+  } else {
+    if (sample) pq_launch(pq_scan_kout_kernel<2, DSUB, true>, grid, a, cb16, g.mw, st);
+    else pq_launch(pq_scan_kout_kernel<2, DSUB, false>, grid, a, cb16, g.mw, st);
+  }
 }
 
 }  // namespace
 
 bool pq32_supported(int dim, int M, int ksub, int k) {
-  return dim == 768 && dim == 8 * M && ksub >= 1 && ksub <= 256 && k >= 1 && k + 4 <= STREAM_KO;
+  if (M <= 0 || dim <= 0 || dim % 16 != 0 || dim % M != 0) return false;
+  const int dsub = dim / M;
+  return (dsub == 4 || dsub == 8 || dsub == 16 || dsub == 32) && dim / 16 <= PQ_KS_MAX && ksub >= 1 && ksub <= 256 &&
+         k >= 1 && k + 4 <= STREAM_KO;
 }
-int pq32_qmax() { return PQMAX; }
+int pq32_qmax(int dim, int M) { return pq_geo(dim, M).qmax; }
 int pq32_sample_values() { return PSV; }
-int pq32_code_bytes(int dim) { return (dim / 16 + 15) / 16 * 16; }
+int pq32_code_words(int M) { return (M + 15) / 16; }
 
-void launch_pq32_pack(const uint8_t *codes_rm, const int64_t *src, int64_t tot, int M, const float *cb, int ksub,
-                      uint8_t *cpack, float *nrm, hipStream_t st) {
+void launch_pq32_pack(const uint8_t *codes_rm, const int64_t *src, int64_t tot, int M, int dsub, const float *cb,
+                      int ksub, uint8_t *cpack, float *nrm, hipStream_t st) {
   if (tot <= 0) return;
   hipLaunchKernelGGL(pq_pack_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, codes_rm, src, tot, M,
-                     pq32_code_bytes(8 * M), cb, ksub, cpack, nrm);
+                     pq32_code_words(M), dsub, cb, ksub, cpack, nrm);
 }
-void launch_pq32_cb16(const float *cb, int M, int ksub, float sc, _Float16 *cb16, hipStream_t st) {
-  const int64_t n = (int64_t)M * 256 * 8;
-  hipLaunchKernelGGL(pq_cb16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, cb, M, ksub, sc, cb16);
+void launch_pq32_cb16(const float *cb, int M, int ksub, int dsub, float sc, _Float16 *cb16, hipStream_t st) {
+  const int64_t n = (int64_t)M * 256 * dsub;
+  hipLaunchKernelGGL(pq_cb16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, cb, M, ksub, dsub, sc,
+                     cb16);
 }
 void launch_pq32_meta(const float *nrm, const uint8_t *live, int64_t tot, float *meta, hipStream_t st) {
   if (tot <= 0) return;
   hipLaunchKernelGGL(pq_meta_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, nrm, live, tot, meta);
 }
-void launch_pq32_prep(const StreamArgs &a, int max_items, hipStream_t st) {
-  if (max_items <= 0) return;
-  hipLaunchKernelGGL(pq_prep_kernel<768>, dim3((unsigned)((int64_t)max_items * PQMAX / 4)), dim3(256), 0, st, a);
+void launch_pq32_prep(const StreamArgs &a, int64_t npos, hipStream_t st) {
+  if (npos <= 0) return;
+  hipLaunchKernelGGL(pq_prep_kernel, dim3((unsigned)((npos + 3) / 4)), dim3(256), 0, st, a, npos);
 }
-void launch_pq32_scan(const StreamArgs &a, const _Float16 *cb16, int max_items, bool sample, hipStream_t st) {
+void launch_pq32_scan(const StreamArgs &a, const _Float16 *cb16, int M, int max_items, bool sample, hipStream_t st) {
   if (max_items <= 0) return;
-  launch_pq_scan_d<768>(a, cb16, max_items, sample, st);
+  const PqGeo g = pq_geo(a.dim, M);
+  if (a.dim % 16 != 0 || g.ks > PQ_KS_MAX) throw std::runtime_error("pq32: unsupported dimension");
+  // one block per CU (launch_bounds 1 block): a multiple of the 8 XCDs keeps the queues' block counts equal
+  const int grid = std::max(8, std::min((max_items + 7) / 8 * 8, device_cus()));
+  switch (g.dsub) {
+    case 4: launch_scan_dsub<4>(a, cb16, g, grid, sample, st); break;
+    case 8: launch_scan_dsub<8>(a, cb16, g, grid, sample, st); break;
+    case 16: launch_scan_dsub<16>(a, cb16, g, grid, sample, st); break;
+    case 32: launch_scan_dsub<32>(a, cb16, g, grid, sample, st); break;
+    default: throw std::runtime_error("pq32: unsupported subspace size");
+  }
 }
 void launch_pq32_refine(const PqRefineArgs &a, int64_t nq, hipStream_t st) {
   if (nq <= 0) return;

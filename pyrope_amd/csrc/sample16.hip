@@ -34,6 +34,7 @@ namespace {
 
 #include "f16util.h"
 #include "wselect.h"
+#include "candmerge.h"
 
 constexpr int SNW = 8;         // waves per stream block
 constexpr int SV = SNW * 4;    // sample values per (query, probe)
@@ -49,10 +50,20 @@ __device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf
 template <int D>
 constexpr int SPREP_SPLIT = D / 16;
 template <int D, int MET>
+__device__ void sprep_unit(const StreamArgs &a, int item, int part);
+
+// grid-stride over (item, part) units up to the device item count: the grid is sized for the most items a
+// batch can have, and a list-sharded rank's batch has far fewer (only its own lists get items)
+template <int D, int MET>
 __global__ __launch_bounds__(256) void sprep_kernel(StreamArgs a) {
   constexpr int SPLIT = SPREP_SPLIT<D>;
-  const int item = blockIdx.x / SPLIT, part = blockIdx.x - item * SPLIT;
-  if (item >= *a.n_items) return;
+  const int64_t units = (int64_t)(*a.n_items) * SPLIT;
+  for (int64_t u = blockIdx.x; u < units; u += gridDim.x) sprep_unit<D, MET>(a, (int)(u / SPLIT), (int)(u % SPLIT));
+}
+
+template <int D, int MET>
+__device__ void sprep_unit(const StreamArgs &a, int item, int part) {
+  constexpr int SPLIT = SPREP_SPLIT<D>;
   const ScanItem it = a.items[item];
   if (it.part != 0) return;  // chunk-0 items cover every qlist position of their list once
   // (a bounded grid walking 64-item windows of chunk-0 items measured slower: 0.165 vs 0.146 ms, r4g)
@@ -272,63 +283,12 @@ __global__ __launch_bounds__(256) void sselect_kernel(StreamSelectArgs a) {
   if (lane == 0) a.thr[q] = key_score(key);
 }
 
-// ---- 5. per query: the best KO emitted rows (+ floor placeholders), wave bitonic sort ----
-__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
-  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src);
-  return ((uint64_t)hi << 32) | lo;
-}
-__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
-  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
-  return ((uint64_t)hi << 32) | lo;
-}
-// rank key: score desc, then storage key asc (~key); 0 = no entry
-__device__ __forceinline__ uint64_t pack_cand(float s, uint32_t k) { return ((uint64_t)score_key(s) << 32) | (uint32_t)~k; }
-
-__device__ __forceinline__ uint64_t sort64_desc(uint64_t v, int lane) {
-#pragma unroll
-  for (int k = 2; k <= 64; k <<= 1)
-#pragma unroll
-    for (int j = k >> 1; j >= 1; j >>= 1) {
-      const uint64_t o = shfl_xor64(v, j);
-      const bool desc = (lane & k) == 0, lower = (lane & j) == 0;
-      v = (lower == desc) ? (v > o ? v : o) : (v < o ? v : o);
-    }
-  return v;
-}
-__device__ __forceinline__ uint64_t merge64_desc(uint64_t v, int lane) {  // v bitonic -> sorted desc
-#pragma unroll
-  for (int j = 32; j >= 1; j >>= 1) {
-    const uint64_t o = shfl_xor64(v, j);
-    v = (lane & j) == 0 ? (v > o ? v : o) : (v < o ? v : o);
-  }
-  return v;
-}
-
 template <int KO>
 __global__ __launch_bounds__(256) void cand_merge_kernel(CandMergeArgs m) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t q = (int64_t)blockIdx.x * 4 + w;
   if (q >= m.nq) return;
-  const int tot = min(m.cand_n[q], m.cap);
-  const uint32_t fk = m.cand_f[q];
-  float F = m.thr ? m.thr[q] : -INFINITY;
-  if (fk != 0u) F = fmaxf(F, key_score(fk));
-  const uint2 *cq = m.cand + (size_t)q * m.cap;
-  uint64_t cur = F > -INFINITY ? pack_cand(F, KEY_FLOOR) : 0ull;
-  for (int base = 0; base < tot; base += 64) {
-    const int idx = base + lane;
-    uint64_t v = 0ull;
-    if (idx < tot) {
-      const uint2 e = cq[idx];
-      v = pack_cand(__uint_as_float(e.x), e.y);
-    }
-    const uint64_t kth = shfl64(cur, KO - 1);
-    if (!__builtin_amdgcn_ballot_w64(v > kth)) continue;
-    v = sort64_desc(v, lane);
-    const uint64_t r = shfl64(v, 63 - lane);
-    cur = cur > r ? cur : r;
-    cur = merge64_desc(cur, lane);
-  }
+  const uint64_t cur = cand_merge_wave<KO>(m, q, lane);
   if (lane < KO) {
     float s = -INFINITY;
     int32_t k = -1;
@@ -365,7 +325,10 @@ bool sample16_supported(int dim, int metric) { return (metric == L2 || metric ==
 void launch_sample16(const StreamArgs &a, int metric, int max_items, hipStream_t st, bool prep_only) {
   if (max_items <= 0) return;
   const int split = a.dim == 32 ? SPREP_SPLIT<32> : a.dim == 64 ? SPREP_SPLIT<64> : SPREP_SPLIT<128>;
-  auto prep = [&](auto kern) { hipLaunchKernelGGL(kern, dim3((unsigned)((int64_t)max_items * split)), dim3(256), 0, st, a); };
+  // at most 4 blocks per CU of the grid-stride units (I1: 3.3k items x 8 units; a rank's share of a sharded batch
+  // holds far fewer)
+  const int64_t pg = std::min<int64_t>((int64_t)max_items * split, 8 * (int64_t)device_cus());
+  auto prep = [&](auto kern) { hipLaunchKernelGGL(kern, dim3((unsigned)pg), dim3(256), 0, st, a); };
   const dim3 grid(std::max(1, std::min(max_items, device_cus())));
   auto samp = [&](auto kern) {
     if (!prep_only) hipLaunchKernelGGL(kern, grid, dim3(64 * SNW), 0, st, a);

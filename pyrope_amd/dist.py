@@ -288,8 +288,17 @@ class DeviceShardEngine:
     """The list-sharded step's per-rank operations on libpyrope_hip (IVF_FLAT shard index, device buffers
     as torch tensors, one stream)."""
 
-    def __init__(self, index, k: int, options=None, stream: int = 0):
-        self.index, self.k, self.options, self.stream = index, k, options, stream
+    def __init__(self, index, k: int, options=None, stream=None):
+        self.index, self.k, self.options, self._stream = index, k, options, stream
+
+    @property
+    def stream(self) -> int:
+        """The given stream, else torch's current stream at the time of the call (so a phase captured
+        under torch.cuda.graph enqueues on the capture stream)."""
+        if self._stream is not None:
+            return self._stream
+        import torch
+        return torch.cuda.current_stream().cuda_stream
 
     def prepare(self, q_home, plan):
         return self.index.shard_prepare_device(q_home.data_ptr(), q_home.shape[0], self.k, plan.data_ptr(),
@@ -368,23 +377,61 @@ class ListShardedIvf:
     def probes_all(self):  # ShardedIvfStep._timed checks .is_cuda on it
         return self.plan_all
 
-    def __call__(self, q_all, validate: bool = False):
-        nq, w, r = self.nq, self.world, self.rank
-        e, c = self.engine, self.comm
-        q_home = q_all[r * nq:(r + 1) * nq]
-        P = e.prepare(q_home, self.plan_home)
-        if P != self.width:
-            raise ValueError(f"plan width {P} != {self.width}")
-        self._timed("plan_allgather", lambda: c.all_gather_into(self.plan_all, self.plan_home))
-        e.search(q_all, self.plan_all, P, self.rec)
-        self._timed("record_alltoall", lambda: c.all_to_all_single(self.rec_home.view(w * nq, -1), self.rec))
-        e.merge(self.rec_home, self.out_s, self.out_l, self.fail_home)
-        self._timed("fail_allgather", lambda: c.all_gather_into(self.fail_all, self.fail_home))
-        e.rerun(q_all, self.plan_all, P, self.fail_all, nq, self.rrec)
-        self._timed("rerun_alltoall", lambda: c.all_to_all_single(self.rrec_home.view(w * self.fcap, -1), self.rrec))
-        e.merge_rerun(self.rrec_home, self.fail_home, self.out_s, self.out_l)
+    # the device work between two collectives (each may be replayed from a hipGraph: capture())
+    def _phase(self, name, q_all):
         import torch
-        torch.maximum(self.max_fail, self.fail_home[:1], out=self.max_fail)
+        g = getattr(self, "graphs", {}).get(name)
+        if g is not None:
+            g.replay()
+            return
+        nq, r, e, P = self.nq, self.rank, self.engine, self.width
+        if name == "prepare":
+            got = e.prepare(q_all[r * nq:(r + 1) * nq], self.plan_home)
+            if got != P:
+                raise ValueError(f"plan width {got} != {P}")
+        elif name == "search":
+            e.search(q_all, self.plan_all, P, self.rec)
+        elif name == "merge":
+            e.merge(self.rec_home, self.out_s, self.out_l, self.fail_home)
+        elif name == "rerun":
+            e.rerun(q_all, self.plan_all, P, self.fail_all, nq, self.rrec)
+        else:  # "finish"
+            e.merge_rerun(self.rrec_home, self.fail_home, self.out_s, self.out_l)
+            torch.maximum(self.max_fail, self.fail_home[:1], out=self.max_fail)
+
+    PHASES = ("prepare", "search", "merge", "rerun", "finish")
+
+    def capture(self, q_all):
+        """Capture the five device phases into hipGraphs (the collectives stay outside them), replayed by
+        every later call on the same q_all buffer.  One plain step on the capture stream sizes its
+        workspaces first (no allocation inside a capture)."""
+        import torch
+        gst = torch.cuda.Stream()
+        gst.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(gst):
+            self(q_all)
+        gst.synchronize()
+        graphs = {}
+        for name in self.PHASES:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=gst):
+                self._phase(name, q_all)
+            graphs[name] = g
+        torch.cuda.synchronize()
+        self.graphs = graphs
+
+    def __call__(self, q_all, validate: bool = False):
+        nq, w = self.nq, self.world
+        c = self.comm
+        self._phase("prepare", q_all)
+        self._timed("plan_allgather", lambda: c.all_gather_into(self.plan_all, self.plan_home))
+        self._phase("search", q_all)
+        self._timed("record_alltoall", lambda: c.all_to_all_single(self.rec_home.view(w * nq, -1), self.rec))
+        self._phase("merge", q_all)
+        self._timed("fail_allgather", lambda: c.all_gather_into(self.fail_all, self.fail_home))
+        self._phase("rerun", q_all)
+        self._timed("rerun_alltoall", lambda: c.all_to_all_single(self.rrec_home.view(w * self.fcap, -1), self.rrec))
+        self._phase("finish", q_all)
         if validate and self.check_overflow():
             raise RuntimeError(f"more than {self.fcap} certificate failures at one home rank in a step: rerun with a "
                                f"larger fcap")

@@ -1,0 +1,175 @@
+"""The list-sharded N-GPU step simulated on one GPU (measurement + parity at full size).
+
+Builds the I1 (or M8) data set, assigns every row, and builds ALL `--world` shard indexes on the one GPU
+(each owns its size-balanced whole lists, dist.list_owners, plus the replicated sample of every list).
+Then it runs the step phase by phase for every rank -- the collectives become tensor copies -- and:
+  * times rank `--rank`'s device work: prepare (its home slice), search (all world x nq queries against
+    its lists), merge (the world records of its home queries + certificate), rerun (the gathered failures);
+  * checks every home's answers against the unsharded index on the same data (ids and score bits);
+  * prints the per-rank failure counts and the collectives' byte counts (no collective runs on one GPU).
+
+    python scripts/rank_shape.py --world 8 [--n 10000000 --nlist 1024 --nprobe 32 --nq 10000 --steps 20]
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--rank", type=int, default=0)
+    ap.add_argument("--n", type=int, default=10_000_000)
+    ap.add_argument("--nlist", type=int, default=1024)
+    ap.add_argument("--nprobe", type=int, default=32)
+    ap.add_argument("--nq", type=int, default=10_000)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--dim", type=int, default=128)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--fcap", type=int, default=256)
+    ap.add_argument("--train-rows", type=int, default=10_000_000)
+    ap.add_argument("--parity", type=int, default=1, help="compare every home's answers with the unsharded index")
+    args = ap.parse_args()
+
+    import torch
+    torch.cuda.init()
+    from pyrope_amd import (IvfFlatVectorIndex, SearchOptions, _lib, assign, generate_synthetic,
+                            generate_synthetic_blocked, kmeans_train)
+    from pyrope_amd.dist import SAMPLE_ROWS, DeviceShardEngine, list_owners
+    L = _lib.load()
+    W, R, D, k, nq, F = args.world, args.rank, args.dim, args.k, args.nq, args.fcap
+    t = time.time()
+    data = generate_synthetic_blocked(0, args.n, D, 42, 65536)
+    cents = kmeans_train(data[:min(args.n, args.train_rows)], args.nlist, 0, 10, 42)
+    a = np.concatenate([assign(cents, data[i:i + 2_000_000], 0) for i in range(0, args.n, 2_000_000)])
+    glen = np.bincount(a, minlength=len(cents))
+    owner = list_owners(glen, W)
+    order = np.argsort(a, kind="stable")
+    off = np.concatenate([[0], np.cumsum(glen)])
+    counts = np.minimum(glen, SAMPLE_ROWS)
+    srows = np.concatenate([data[order[off[l]:off[l] + counts[l]]] for l in range(len(cents))])
+    opts = SearchOptions(nprobe=args.nprobe)
+
+    def index_of(labs):
+        ix = IvfFlatVectorIndex(D, 0, n_list=len(cents))
+        ix.set_centroids(cents)
+        ix.reserve(len(labs))
+        for i in range(0, len(labs), 2_000_000):
+            ix.add_labels(labs[i:i + 2_000_000], data[labs[i:i + 2_000_000]], track_ids=False)
+        ix.build()
+        return ix
+    shards = []
+    for r in range(W):
+        ix = index_of(np.nonzero(owner[a] == r)[0].astype(np.int64))
+        ix.set_list_samples(srows, counts, glen)
+        shards.append(ix)
+    Q = W * nq
+    qh = generate_synthetic(Q, D, 1337)
+    ref = None
+    if args.parity:
+        full = index_of(np.arange(args.n, dtype=np.int64))
+        ref = full.search_batch(qh, k, opts)
+        full.close()
+    del data, srows
+    rows = np.bincount(owner, weights=glen, minlength=W)
+    print(f"[rank_shape] world {W}: rank rows max/min {rows.max():.0f}/{rows.min():.0f}, built in "
+          f"{time.time() - t:.1f}s", flush=True)
+
+    q = torch.from_numpy(qh).cuda()
+    P = min(args.nprobe, len(cents))
+    rb = 16 * (k + 1)
+    eng = [DeviceShardEngine(ix, k, opts) for ix in shards]
+    plans = torch.empty((Q, P + 1), dtype=torch.int32, device="cuda")
+    recs = [torch.empty((Q, rb), dtype=torch.uint8, device="cuda") for _ in range(W)]
+    out_s = torch.empty((Q, k), dtype=torch.float32, device="cuda")
+    out_l = torch.empty((Q, k), dtype=torch.int64, device="cuda")
+    fails = torch.zeros((W, 1 + F), dtype=torch.int32, device="cuda")
+    rrec = [torch.zeros((W * F, rb), dtype=torch.uint8, device="cuda") for _ in range(W)]
+    rec_home = [torch.empty((W, nq, rb), dtype=torch.uint8, device="cuda") for _ in range(W)]
+    rrec_home = [torch.empty((W, F, rb), dtype=torch.uint8, device="cuda") for _ in range(W)]
+
+    def hs(h):
+        return slice(h * nq, (h + 1) * nq)
+
+    def prepare(r):
+        assert eng[r].prepare(q[hs(r)], plans[hs(r)]) == P
+
+    def search(r):
+        eng[r].search(q, plans, P, recs[r])
+
+    def merge(h):
+        for s in range(W):  # the record all_to_all's output at home h
+            rec_home[h][s].copy_(recs[s][hs(h)])
+        eng[h].merge(rec_home[h], out_s[hs(h)], out_l[hs(h)], fails[h])
+
+    def rerun(r):
+        eng[r].rerun(q, plans, P, fails, nq, rrec[r])
+
+    def finish(h):
+        for s in range(W):
+            rrec_home[h][s].copy_(rrec[s][h * F:(h + 1) * F])
+        eng[h].merge_rerun(rrec_home[h], fails[h], out_s[hs(h)], out_l[hs(h)])
+
+    def full_step():
+        for r in range(W):
+            prepare(r)
+        for r in range(W):
+            search(r)
+        for h in range(W):
+            merge(h)
+        for r in range(W):
+            rerun(r)
+        for h in range(W):
+            finish(h)
+
+    full_step()
+    torch.cuda.synchronize()
+    res = {"world": W, "rank": R, "rows": int(rows[R]), "lists": int((owner == R).sum()), "queries_all": Q,
+           "queries_home": nq, "nprobe": P, "failures_per_home": fails[:, 0].cpu().tolist()}
+    if ref is not None:
+        s_, l_ = out_s.cpu().numpy(), out_l.cpu().numpy()
+        res["parity"] = {"queries": Q, "ids_equal": bool(np.array_equal(l_, ref[1])),
+                         "scores_bit_identical": bool(np.array_equal(s_.view(np.uint32), ref[0].view(np.uint32)))}
+    # rank R's device phases, each timed over --steps repetitions (the other ranks' records stay as computed)
+    phases = {"prepare": lambda: prepare(R), "search": lambda: search(R), "merge": lambda: merge(R),
+              "rerun": lambda: (rerun(R), finish(R))}
+    ev = {}
+    for name, f in phases.items():
+        f()
+        a0, b0 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a0.record()
+        for _ in range(args.steps):
+            f()
+        b0.record()
+        b0.synchronize()
+        ev[name] = a0.elapsed_time(b0) / args.steps
+    res["phase_ms"] = {k_: round(v, 4) for k_, v in ev.items()}
+    res["rank_step_ms_no_collectives"] = round(sum(ev.values()), 4)
+    L.pyr_profile_reset()
+    L.pyr_profile_enable(1)
+    for f in phases.values():
+        f()
+    torch.cuda.synchronize()
+    L.pyr_profile_enable(0)
+    names = {0: "coarse", 1: "work_lists", 9: "sample", 2: "list_scan", 4: "merge", 7: "refine", 8: "exact_rerun"}
+    prof = {}
+    for ph, name in names.items():
+        ms, calls, work = C.c_double(), C.c_int64(), C.c_int64()
+        L.pyr_profile_get(ph, C.byref(ms), C.byref(calls), C.byref(work))
+        if calls.value:
+            prof[name] = round(ms.value, 4)
+    res["library_phases_ms"] = prof
+    res["collective_bytes_per_rank"] = {"plan_allgather_recv": Q * (P + 1) * 4, "record_alltoall_send": Q * rb,
+                                        "fail_allgather_recv": W * (1 + F) * 4, "rerun_alltoall_send": W * F * rb}
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
