@@ -536,6 +536,16 @@ def run(args):
                             tc.get("nq")) == (N, D, args.nlist, args.nprobe, k, args.nq):
             traffic, traffic_src = tj["hbm_read_bytes_per_launch"], tj["source"]
 
+    # list-sharded: the (query, list) pairs each rank scanned in the last step (every query of the batch,
+    # its probe lists from the all_gather'ed plan, counted by list owner) -- the per-rank work balance
+    pair_balance = None
+    if lists_sharded:
+        own = torch.from_numpy(owner.astype(np.int64)).to(dev)
+        pl = sharded.plan_all[:, :width].long()
+        per = torch.bincount(own[pl[pl >= 0]], minlength=world).cpu().tolist()
+        pair_balance = {"pairs_per_rank": per, "max_over_mean": max(per) / (sum(per) / world),
+                        "rows_per_rank": rank_rows,
+                        "note": "(query, probed list) pairs of the whole batch by the rank owning the list"}
     if rank == 0:
         bytes_per_query = args.nprobe / args.nlist * N * D * 4 + args.nlist * D * 4
         out = {
@@ -601,6 +611,7 @@ def run(args):
             "phases_ms": {k_: round(v["ms"], 4) for k_, v in phases.items()},
             "collective_ms": {k_: round(v, 4) for k_, v in coll.items()} if world > 1 else None,
             "rank_rows": rank_rows,
+            "pair_balance": pair_balance,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -308,6 +308,15 @@ void pyr_profile_enable(int32_t on);
 void pyr_profile_reset(void);
 pyr_status pyr_profile_get(int32_t phase, double *total_ms, int64_t *calls, int64_t *work);
 
+/* Measurement only (tests/test_gpu_bounds.py, scripts/bound_slack.py, scripts/write_path.py): the rows
+ * the last stream-scan query slice emitted (with the environment PYR_STREAM_EMIT_ALL=1 the stream scans
+ * emit every visible row of the scanned lists, without the sampled threshold, and with PYR_STREAM_CAP >=
+ * the rows a query scans all of them are kept): per query q, h_cnt[q] rows (h_cnt > cap: some were dropped) at [q * cap, ...) with
+ * h_ub = the row's upper-bound score (stream_ub_terms) and h_label = its label (-1: a row no longer
+ * visible).  nq / cap must be that slice's.  No reference counterpart. */
+pyr_status pyr_index_debug_candidates(pyr_index *index, int64_t nq, int32_t cap, float *h_ub, int64_t *h_label,
+                                      int32_t *h_cnt);
+
 /* thread-local message of the last failing call on this thread */
 const char *pyr_last_error(void);
 /* library / device information string, e.g. "pyrope_hip 0.1 gfx950" */

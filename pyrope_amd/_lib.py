@@ -130,6 +130,7 @@ SIGNATURES = {
                                          C.c_int32, _vp]),
     "pyr_profile_enable": (None, [C.c_int32]),
     "pyr_profile_reset": (None, []),
+    "pyr_index_debug_candidates": (C.c_int, [_vp, C.c_int64, C.c_int32, _vp, _vp, _vp]),
     "pyr_profile_get": (C.c_int, [C.c_int32, C.POINTER(C.c_double), _i64, _i64]),
     "pyr_last_error": (C.c_char_p, []),
     "pyr_version": (C.c_char_p, []),

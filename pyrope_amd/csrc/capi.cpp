@@ -139,6 +139,8 @@ static pyr_status write_op(pyr_index *index, const float *x, int64_t n, const in
     HIPCHK(hipSetDevice(index->impl->device));
     std::unique_lock<std::shared_mutex> g(index->impl->mu);
     if (n > 0) index->impl->add(x, n, labels, upsert);
+    index->impl->after_write();
+    index->impl->note_write();
   });
 }
 
@@ -264,6 +266,17 @@ pyr_status pyr_profile_get(int32_t phase, double *total_ms, int64_t *calls, int6
   if (calls) *calls = pyr::prof().calls[phase];
   if (work) *work = pyr::prof().work[phase];
   return PYR_OK;
+}
+
+pyr_status pyr_index_debug_candidates(pyr_index *index, int64_t nq, int32_t cap, float *h_ub, int64_t *h_label,
+                                      int32_t *h_cnt) {
+  if (!index || nq < 0 || cap <= 0 || (nq > 0 && (!h_ub || !h_label || !h_cnt))) return fail(PYR_E_ARG, "null argument");
+  return guard([&] {
+    pyr::Index &ix = *index->impl;
+    HIPCHK(hipSetDevice(ix.device));
+    std::shared_lock<std::shared_mutex> g(ix.mu);
+    ix.debug_candidates(nq, cap, h_ub, h_label, h_cnt);
+  });
 }
 
 static pyr_status search_host(pyr_index *index, const float *q, int64_t nq, int32_t k, const pyr_search_params *params,
@@ -475,6 +488,7 @@ pyr_status pyr_index_snapshot(pyr_index *index, const char *path) {
     // staging buffers, so snapshots serialize among themselves (wmu) but not with searches
     std::shared_lock<std::shared_mutex> g(index->impl->mu);
     std::lock_guard<std::mutex> w(index->impl->wmu);
+    HIPCHK(hipStreamSynchronize(index->impl->wst));  // writes the small-batch path left in flight
     index->impl->snapshot(path);
   });
 }
@@ -529,6 +543,7 @@ pyr_status pyr_index_pq_state(const pyr_index *index, float *codebooks, int32_t 
   return guard([&] {
     HIPCHK(hipSetDevice(index->impl->device));
     std::shared_lock<std::shared_mutex> g(index->impl->mu);
+    HIPCHK(hipStreamSynchronize(index->impl->wst));
     index->impl->pq_state(codebooks, ksub, codes);
   });
 }
@@ -552,6 +567,7 @@ pyr_status pyr_index_scan(pyr_index *index, int64_t *labels, float *x, int64_t *
   return guard([&] {
     HIPCHK(hipSetDevice(index->impl->device));
     std::unique_lock<std::shared_mutex> g(index->impl->mu);
+    HIPCHK(hipStreamSynchronize(index->impl->wst));  // writes the small-batch path left in flight
     index->impl->scan(labels, x, n);
   });
 }

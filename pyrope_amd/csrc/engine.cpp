@@ -123,16 +123,34 @@ static float pow2_scale_host(float amax) {  // max |x_i| * sx < 2^14 (filter16.h
 // Concurrent searches share one store: the refresh runs under a lock and completes (stream
 // synchronized) before another search can take the cached pointer.  It runs only after a write or
 // a change of the error-bound constants, never in a steady-state search (hipGraph capture included).
+static bool capturing(hipStream_t st) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  HIPCHK(hipStreamIsCapturing(st, &cs));
+  return cs == hipStreamCaptureStatusActive;
+}
+
 const float *RowStore::row_terms(int met, float kr, float kx, hipStream_t st) {
   static std::mutex mu;
   std::lock_guard<std::mutex> lk(mu);
-  if (mub_gen == gen && mub_met == met && mub_kr == kr && mub_kx == kx && mub.n >= sizeof(float) * cap)
+  if (mub_gen == gen && mub_met == met && mub_kr == kr && mub_kx == kx && mub.n >= sizeof(float) * cap) {
+    if (!mub_done && st != mub_st) {  // refreshed on another stream: order after it (once seen done, never again)
+      if (hipEventQuery(mub_ev) == hipSuccess) mub_done = true;
+      else if (capturing(st)) HIPCHK(hipEventSynchronize(mub_ev));  // (no event edge into a capture)
+      else HIPCHK(hipStreamWaitEvent(st, mub_ev, 0));
+    }
     return mub.as<float>();
+  }
+  if (capturing(st))
+    throw Error(PYR_E_STATE, "the index changed since its last search and its per-row terms must be refreshed: "
+                             "run one search outside the stream capture first");
   mub.ensure(sizeof(float) * std::max<int64_t>(cap, 1));
   launch_row_terms(meta.as<float>(), resid || center16 ? rsq16.as<float>() : rsq.as<float>(), rsq.as<float>(), cap,
                    met, kr, kx, mub.as<float>(), st);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(st));
+  if (!mub_ev) HIPCHK(hipEventCreateWithFlags(&mub_ev, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(mub_ev, st));
+  mub_st = st;
+  mub_done = false;
   mub_gen = gen;
   mub_met = met;
   mub_kr = kr;
@@ -172,10 +190,122 @@ void RowStore::encode16(const int64_t *d_slots, int64_t cnt, hipStream_t st) {
   HIPCHK(hipStreamSynchronize(st));
 }
 
-void RowStore::write(const float *x, const int64_t *slots, const int64_t *labs, int64_t cnt, hipStream_t st,
-                     DevMem &stage_x, DevMem &stage_i, bool x_dev) {
-  if (cnt <= 0) return;
+char *PinnedRing::take(size_t need, int *slot) {
+  if (need > bytes) {  // (re)allocate every slot: wait for their copies first
+    for (int i = 0; i < K; ++i) {
+      if (ev[i]) HIPCHK(hipEventSynchronize(ev[i]));
+      if (host[i]) HIPCHK(hipHostFree(host[i]));
+      host[i] = nullptr;
+    }
+    bytes = std::max<size_t>(need, 4096);
+    for (int i = 0; i < K; ++i) {
+      HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&host[i]), bytes, hipHostMallocDefault));
+      if (!ev[i]) HIPCHK(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+    }
+    next = 0;
+  }
+  const int i = next;
+  next = (next + 1) % K;
+  HIPCHK(hipEventSynchronize(ev[i]));  // its previous copy has run (normally long ago)
+  *slot = i;
+  return host[i];
+}
+void PinnedRing::done(int slot, hipStream_t st) { HIPCHK(hipEventRecord(ev[slot], st)); }
+PinnedRing::~PinnedRing() {
+  for (int i = 0; i < K; ++i) {
+    if (ev[i]) {
+      (void)hipEventSynchronize(ev[i]);
+      (void)hipEventDestroy(ev[i]);
+    }
+    if (host[i]) (void)hipHostFree(host[i]);
+  }
+}
+
+// rows a write may take through the small-batch path (RowStore::write)
+static int64_t small_write_rows() {
+  const char *e = getenv("PYR_SMALL_WRITE");  // 0: the bulk path always (A/B)
+  return e ? atoll(e) : 64;
+}
+
+// FLAT L2 tiles: the center becomes the mean of the live rows (fp64 sums on the device), every slot is
+// re-encoded against it (residual norms, scale, tiles, meta).  Synchronizes st.
+void RowStore::recenter(hipStream_t st) {
+  if (!(f16 && center16 && resid) || n <= 0) return;
+  DevMem sums;
+  sums.ensure(sizeof(double) * dim + sizeof(unsigned long long));
+  HIPCHK(hipMemsetAsync(sums.p, 0, sizeof(double) * dim + sizeof(unsigned long long), st));
+  double *ds = sums.as<double>();
+  launch_live_sums(rows.as<float>(), live.as<uint8_t>(), n, dim, ds, reinterpret_cast<unsigned long long *>(ds + dim),
+                   st);
+  std::vector<double> h(dim + 1);
+  HIPCHK(hipMemcpyAsync(h.data(), sums.p, sizeof(double) * (dim + 1), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  unsigned long long c;
+  std::memcpy(&c, &h[dim], sizeof(c));
+  center_rows = n;
+  if (c == 0) return;
+  for (int d = 0; d < dim; d++) hcenter[d] = (float)(h[d] / (double)c);
+  HIPCHK(hipMemcpyAsync(center.p, hcenter.data(), sizeof(float) * dim, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemsetAsync(rmax_r.p, 0, sizeof(uint32_t), st));
+  sx = 0.0f;  // a new scale from the new residuals, every slot re-encoded
+  amax = 0.0f;
+  encode16(nullptr, cap, st);
+}
+
+bool RowStore::write(const float *x, const int64_t *slots, const int64_t *labs, int64_t cnt, hipStream_t st,
+                     DevMem &stage_x, DevMem &stage_i, bool x_dev, uint8_t *q8ok) {
+  if (cnt <= 0) return true;
   ++gen;
+  // small-batch path: the rows' largest |x_i| (of x - center) is taken on the host, so the scale decision
+  // needs no device read-back; one pinned copy, one fused kernel, no synchronization
+  if (!x_dev && cnt <= small_write_rows() && (!f16 || (sx > 0.0f && (center16 ? resid : !resid)))) {
+    float am = 0.0f;
+    if (f16)
+      for (int64_t i = 0; i < cnt; i++)
+        for (int d = 0; d < dim; d++) {
+          const float v = std::fabs(resid ? x[(size_t)i * dim + d] - hcenter[d] : x[(size_t)i * dim + d]);
+          if (std::isfinite(v)) am = std::max(am, v);
+        }
+    if (!f16 || std::max(am, amax) * sx < 16384.0f) {
+      const size_t xb = sizeof(float) * cnt * dim, ib = sizeof(int64_t) * cnt;
+      int slot;
+      char *h = ring.take(xb + 2 * ib, &slot);
+      std::memcpy(h, x, xb);
+      std::memcpy(h + xb, slots, ib);
+      std::memcpy(h + xb + ib, labs, ib);
+      stage_x.ensure(xb + 2 * ib);
+      HIPCHK(hipMemcpyAsync(stage_x.p, h, xb + 2 * ib, hipMemcpyHostToDevice, st));
+      ring.done(slot, st);
+      SmallWriteArgs a{};
+      a.x = stage_x.as<float>();
+      a.slots = reinterpret_cast<const int64_t *>(stage_x.as<char>() + xb);
+      a.labs = a.slots + cnt;
+      a.cnt = (int32_t)cnt;
+      a.dim = dim;
+      a.dp = tdim();
+      a.rows = rows.as<float>();
+      a.rrm = f16 ? rrm.as<float>() : nullptr;
+      a.labels = labels.as<int64_t>();
+      a.live = live.as<uint8_t>();
+      a.norms = cosine ? norms.as<float>() : nullptr;
+      a.rsq = rsq.as<float>();
+      a.rmax = rmax.as<uint32_t>();
+      if (f16) {
+        a.h16 = h16.as<_Float16>();
+        a.sx = sx;
+        a.center = resid ? center.as<float>() : nullptr;
+        a.rsq16 = rsq16.as<float>();
+        a.rmax_r = rmax_r.as<uint32_t>();
+        a.meta = meta.as<float>();
+        a.met16 = met16;
+        amax = std::max(am, amax);
+      }
+      a.q8ok = q8ok;
+      launch_write_small(a, st);
+      HIPCHK(hipGetLastError());
+      return true;
+    }
+  }
   const size_t xb = sizeof(float) * cnt * dim;
   stage_i.ensure(sizeof(int64_t) * cnt * 2);
   int64_t *di = stage_i.as<int64_t>();
@@ -214,8 +344,10 @@ void RowStore::write(const float *x, const int64_t *slots, const int64_t *labs, 
           num[d]++;
         }
       }
-    std::vector<float> c(dim);
+    std::vector<float> &c = hcenter;
+    c.assign(dim, 0.0f);
     for (int d = 0; d < dim; d++) c[d] = num[d] ? (float)(acc[d] / (double)num[d]) : 0.0f;
+    center_rows = std::max<int64_t>(n, 1);
     center.ensure(sizeof(float) * dim);
     rmax_r.ensure(sizeof(uint32_t));
     HIPCHK(hipMemcpyAsync(center.p, c.data(), sizeof(float) * dim, hipMemcpyHostToDevice, st));
@@ -228,6 +360,7 @@ void RowStore::write(const float *x, const int64_t *slots, const int64_t *labs, 
   encode16(di, cnt, st);
   HIPCHK(hipStreamSynchronize(st));  // staging buffers are reused by the next call
   if (stage_x.n > (size_t(256) << 20)) stage_x.release();  // bulk loads: do not pin GBs of staging
+  return false;
 }
 
 void RowStore::set_live(const std::vector<int64_t> &slots, uint8_t v, hipStream_t st, DevMem &stage) {
@@ -290,21 +423,42 @@ Index::Index(const pyr_index_desc &d) : desc(d), dim(d.dim), metric(d.metric), d
 Index::~Index() {
   (void)hipSetDevice(device);
   if (wst) (void)hipStreamSynchronize(wst);
+  if (wev) (void)hipEventDestroy(wev);
   free_ws.clear();
   stream_ws.clear();
   if (wst) (void)hipStreamDestroy(wst);
 }
 
+void Index::note_write() {
+  if (!wev) HIPCHK(hipEventCreateWithFlags(&wev, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(wev, wst));
+  ++wgen;
+}
+
+void Index::order_after_writes(Workspace &ws) {
+  if (ws.wgen_seen == wgen || !wev) return;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  HIPCHK(hipStreamIsCapturing(ws.st, &cs));
+  if (cs == hipStreamCaptureStatusActive) HIPCHK(hipEventSynchronize(wev));  // (no cross-capture event edge)
+  else HIPCHK(hipStreamWaitEvent(ws.st, wev, 0));
+  ws.wgen_seen = wgen;
+}
+
 std::unique_ptr<Workspace> Index::take_ws() {
-  std::lock_guard<std::mutex> g(ws_mu);
-  if (!free_ws.empty()) {
-    auto w = std::move(free_ws.back());
-    free_ws.pop_back();
-    return w;
+  std::unique_ptr<Workspace> w;
+  {
+    std::lock_guard<std::mutex> g(ws_mu);
+    if (!free_ws.empty()) {
+      w = std::move(free_ws.back());
+      free_ws.pop_back();
+    }
   }
-  auto w = std::make_unique<Workspace>();
-  HIPCHK(hipStreamCreateWithFlags(&w->st, hipStreamNonBlocking));
-  w->own_stream = true;
+  if (!w) {
+    w = std::make_unique<Workspace>();
+    HIPCHK(hipStreamCreateWithFlags(&w->st, hipStreamNonBlocking));
+    w->own_stream = true;
+  }
+  order_after_writes(*w);
   return w;
 }
 
@@ -314,13 +468,18 @@ void Index::give_ws(std::unique_ptr<Workspace> w) {
 }
 
 Workspace &Index::ws_for_stream(hipStream_t st) {
-  std::lock_guard<std::mutex> g(ws_mu);
-  auto &p = stream_ws[st];
-  if (!p) {
-    p = std::make_unique<Workspace>();
-    p->st = st;
+  Workspace *w;
+  {
+    std::lock_guard<std::mutex> g(ws_mu);
+    auto &p = stream_ws[st];
+    if (!p) {
+      p = std::make_unique<Workspace>();
+      p->st = st;
+    }
+    w = p.get();
   }
-  return *p;
+  order_after_writes(*w);
+  return *w;
 }
 
 void Index::ivf_layout(int64_t *, int64_t *, uint8_t *, int64_t *total) const {
@@ -578,6 +737,37 @@ void ivf_memory_plan(int dim, int64_t nrows, int nlist, int64_t max_len, int64_t
   w += 8 * ivf_rerun_part_keys(qs, probes, k);                                 // device re-run scratch
   *workspace_bytes = w;
 }
+// measurement only (PYR_STREAM_EMIT_ALL=1; tests/test_gpu_bounds.py): the main list scans run without the
+// sampled thresholds, so every visible row of the scanned lists is emitted with its upper bound (with a
+// PYR_STREAM_CAP large enough, pyr_index_debug_candidates then returns every row's bound)
+static bool emit_all() {
+  const char *e = getenv("PYR_STREAM_EMIT_ALL");
+  return e && atoi(e) != 0;
+}
+static StreamArgs main_scan_args(const StreamArgs &sa) {
+  StreamArgs m = sa;
+  if (emit_all()) m.thr = nullptr;
+  return m;
+}
+void Index::note_stream_slice(Workspace &ws, int64_t nq, int cap) {
+  dbg_ws = &ws;
+  dbg_nq = nq;
+  dbg_cap = cap;
+}
+void Index::debug_candidates(int64_t nq, int32_t cap, float *h_ub, int64_t *h_label, int32_t *h_cnt) {
+  if (!dbg_ws) throw Error(PYR_E_STATE, "no stream-scan search ran on this index");
+  if (nq != dbg_nq || cap != dbg_cap) throw Error(PYR_E_ARG, "nq / cap differ from the last stream-scan slice");
+  Workspace &ws = *dbg_ws;
+  HIPCHK(hipStreamSynchronize(ws.st));
+  std::vector<uint2> c((size_t)nq * cap);
+  HIPCHK(hipMemcpy(c.data(), ws.scand.p, sizeof(uint2) * c.size(), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(h_cnt, ws.scn.p, sizeof(int32_t) * nq, hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < c.size(); ++i) {
+    uint32_t b = c[i].x;
+    memcpy(&h_ub[i], &b, 4);
+    h_label[i] = key_label(c[i].y);
+  }
+}
 static int filter_ablate() {  // measurement only (StreamArgs::ablate)
   const char *e = getenv("PYR_FILTER_ABLATE");
   return e ? atoi(e) : 0;
@@ -793,6 +983,9 @@ static int build_ivf_items(Workspace &ws, int64_t nq, int nprobe, int nparts, in
 
 struct FlatIndex : Index {
   RowStore st;
+  int64_t key_label(uint32_t key) const override {
+    return (int64_t)key < st.n && st.hlive[key] ? st.hlabels[key] : -1;
+  }
   std::unordered_map<int64_t, int64_t> slot_of;  // _idMap (:15)
   // 8-bit search mode (EnableQuantization, :25-40; _quantizedVectors, :20-21): per slot
   // ScalarQuantizer codes + sums of squares, and whether the slot has codes at all
@@ -853,6 +1046,24 @@ struct FlatIndex : Index {
   }
 
   void set_quantization(bool on) override { quant = on; }
+  // the stream scan's per-row terms for the rows just written, on the write stream (a search -- or a
+  // hipGraph capture of one -- right after a write then finds them current; FlatIndex::stream_slice's
+  // constants)
+  void after_write() override {
+    if (st.f16 && st.cap > 0 && st.sx > 0.0f) {
+      StreamArgs sa{};
+      const int dt = st.tdim();
+      stream_ub_terms(dt, metric, filter_f16_cerr(dt, metric, FILTER_F16X1), filter_cerr(dt),
+                      filter_f16_abs(dt, metric, st.sx, FILTER_F16X1), sa);
+      st.row_terms(metric, sa.kr, sa.kx, wst);
+    }
+    if (unit) unit->after_write();
+  }
+  // BruteForceVectorIndex.Build is a no-op for the results; here the FLAT L2 tiles are re-centred on the
+  // live rows (a Delta head is built after its compaction, DeltaVectorIndex.cs:124-158)
+  void build() override {
+    if (st.center16 && st.resid && !getenv("PYR_FROZEN_CENTER")) st.recenter(wst);
+  }
   void reserve(int64_t rows) override {
     st.reserve(st.n + rows, wst);
     slot_of.reserve(slot_of.size() + (size_t)rows);
@@ -894,24 +1105,31 @@ struct FlatIndex : Index {
     st.reserve(next, wst);
     st.hlabels.resize(next, -1);
     st.hlive.resize(next, 0);
-    st.write(x, slots.data(), labels, n, wst, stage_x, stage_i);
-    // :166-178 / :200-211: codes when quantization is on, otherwise the slot loses them
-    // (stage_i still holds the device copy of the slots)
     q8_reserve();
-    if (quant)
-      launch_sq8_quantize(st.rows.as<float>(), stage_i.as<int64_t>(), 1, n, dim, dp, 1, q8.as<uint8_t>(),
-                          q8s.as<int2>(), q8ok.as<uint8_t>(), wst);
-    else
-      launch_scatter_u8(q8ok.as<uint8_t>(), stage_i.as<int64_t>(), 0, n, wst);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(wst));
-    unit_write(n, slots);  // (stage_i: the slots; the unit index appends new slots in the same order)
+    // :166-178 / :200-211: codes when quantization is on, otherwise the slot loses them.  A few rows of a
+    // plain store go through RowStore::write's small-batch path (the q8ok reset fused in, no sync)
+    const bool small = !quant && !unit && st.write(x, slots.data(), labels, n, wst, stage_x, stage_i, false,
+                                                   q8ok.as<uint8_t>());
+    if (!small) {
+      if (quant || unit) st.write(x, slots.data(), labels, n, wst, stage_x, stage_i);
+      // (stage_i holds the device copy of the slots)
+      if (quant)
+        launch_sq8_quantize(st.rows.as<float>(), stage_i.as<int64_t>(), 1, n, dim, dp, 1, q8.as<uint8_t>(),
+                            q8s.as<int2>(), q8ok.as<uint8_t>(), wst);
+      else
+        launch_scatter_u8(q8ok.as<uint8_t>(), stage_i.as<int64_t>(), 0, n, wst);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipStreamSynchronize(wst));
+      unit_write(n, slots);  // (stage_i: the slots; the unit index appends new slots in the same order)
+    }
     for (int64_t i = 0; i < n; i++) {
       st.hlabels[slots[i]] = labels[i];
       st.hlive[slots[i]] = 1;
       slot_of[labels[i]] = slots[i];
     }
     st.n = next;
+    // the FLAT L2 tiles' center follows the rows: re-centred each time the store has doubled since
+    if (st.center16 && st.resid && st.n >= 2 * st.center_rows && !getenv("PYR_FROZEN_CENTER")) st.recenter(wst);
   }
 
   // BruteForceVectorIndex.Search with EnableQuantization (:296-336): quantize the queries,
@@ -1048,6 +1266,8 @@ struct FlatIndex : Index {
     const CosRefine cr{&st, d_q, ws.qn.as<float>(), zflag.as<uint32_t>()};
     std::shared_lock<std::shared_mutex> g(unit->mu);
     unit->search_stream(ws.cq.as<float>(), nq, k, k1, cutoff, d_s, d_l, d_c, ws, &cr);
+    // (measurement: the unit store's keys are this store's slots)
+    if (unit->dbg_ws) note_stream_slice(*unit->dbg_ws, unit->dbg_nq, unit->dbg_cap);
   }
 
   void search_stream(const float *d_q, int64_t nq, int k, int k1, int64_t cutoff, float *d_s, int64_t *d_l,
@@ -1154,8 +1374,9 @@ struct FlatIndex : Index {
     sa.work = ws.swork.as<int32_t>() + 1;
     {
       PhaseTimer t(PH_FLAT_SCAN, ws.st, nq * cutoff);
-      launch_scan_main(sa, metric, maxi, ws.st);
+      launch_scan_main(main_scan_args(sa), metric, maxi, ws.st);
     }
+    note_stream_slice(ws, nq, cap);
     ws.ms.ensure(sizeof(float) * nq * STREAM_KO);
     ws.mk.ensure(sizeof(int32_t) * nq * STREAM_KO);
     const bool fused = merge_refine_fused();
@@ -1667,6 +1888,13 @@ struct IvfFlatIndex : Index {
   int64_t max_len = 0;                    // longest list (rows incl. tombstones): row chunking
   DevMem dlb, dle, dllive;
   DevMem dlmax;                           // per-list max |x|^2 (score_key): refine certificate bound
+  int64_t key_label(uint32_t key) const override {
+    if (key & KEY_BUF) {
+      const int64_t s = key & ~KEY_BUF;
+      return s < buf.st.n && buf.st.hlive[s] ? buf.st.hlabels[s] : -1;
+    }
+    return (size_t)key < lstate.size() && lstate[key] == 1 ? lists.hlabels[key] : -1;
+  }
   DevMem dlmax_r;                         // per-list max |x - c|^2 (residual fp16 tiles)
   // Cosine: the fp16 tiles hold unit residuals x/|x| - c/|c| (ucents: the unit centroids) scanned as L2
   // (on unit vectors the L2 order is the cosine order); zflag: a list row with a norm below 1e-6
@@ -2155,9 +2383,10 @@ struct IvfFlatIndex : Index {
     {
       PhaseTimer t(PH_LIST_SCAN, ws.st, prof().on && !sh ? probed_rows(ws, nq, probes, le, lb) : 0);
       if (timing) sa.tdbg = ws.tdbg.as<unsigned long long>();
-      launch_scan_main(sa, met, maxi, ws.st);
+      launch_scan_main(main_scan_args(sa), met, maxi, ws.st);
       sa.tdbg = nullptr;
     }
+    note_stream_slice(ws, nq, cap);
     if (timing) {
       unsigned long long c[8];
       HIPCHK(hipMemcpyAsync(c, ws.tdbg.p, sizeof(c), hipMemcpyDeviceToHost, ws.st));
@@ -2716,6 +2945,9 @@ struct IvfPqIndex : Index {
   DevMem codes, clive, clabels;      // blocked codes, per code-row visibility, labels
   std::vector<int64_t> hlabels;      // per code row (-1 pad)
   std::vector<uint8_t> hlive;
+  int64_t key_label(uint32_t key) const override {
+    return (size_t)key < hlive.size() && hlive[key] ? hlabels[key] : -1;
+  }
   std::unordered_map<int64_t, int64_t> pos_of;
   std::vector<int32_t> lb, le, llen;
   DevMem dlb, dle;
@@ -3000,6 +3232,9 @@ struct IvfPqIndex : Index {
     std::lock_guard<std::mutex> lk(mu);
     const int64_t tot = (ncode_rows + 31) / 32 * 32;
     if (pmub_gen == pq_gen && pmub_kr == kr && pmub.n >= sizeof(float) * tot) return pmub.as<float>();
+    if (capturing(ws.st))
+      throw Error(PYR_E_STATE, "the index changed since its last search and its per-row terms must be "
+                               "refreshed: run one search outside the stream capture first");
     pmeta.ensure(sizeof(float) * std::max<int64_t>(tot, 1));
     pmub.ensure(sizeof(float) * std::max<int64_t>(tot, 1));
     WordFill z;
@@ -3118,8 +3353,9 @@ struct IvfPqIndex : Index {
     sa.work = ws.swork.as<int32_t>() + 8;  // the main pass's 8 queue counters
     {
       PhaseTimer t(PH_PQ_SCAN, ws.st, prof().on ? probed_rows(ws, nq, probes, le, lb) : 0);
-      launch_pq32_scan(sa, cb16.as<_Float16>(), M, maxi, false, ws.st);
+      launch_pq32_scan(main_scan_args(sa), cb16.as<_Float16>(), M, maxi, false, ws.st);
     }
+    note_stream_slice(ws, nq, cap);
     ws.ms.ensure(sizeof(float) * nq * STREAM_KO);
     ws.mk.ensure(sizeof(int32_t) * nq * STREAM_KO);
     {

@@ -50,6 +50,20 @@ struct DevMem {
   }
 };
 
+// Pinned host staging for small writes: K slots, each reusable once the copy that read it has run (an
+// event per slot), so a write never waits for the device (RowStore::write's small-batch path).
+struct PinnedRing {
+  static constexpr int K = 64;
+  char *host[K] = {};
+  hipEvent_t ev[K] = {};
+  size_t bytes = 0;
+  int next = 0;
+  // a slot of at least `need` bytes whose previous copy has completed; *slot = its index
+  char *take(size_t need, int *slot);
+  void done(int slot, hipStream_t st);  // the copy out of `slot` is enqueued on st
+  ~PinnedRing();
+};
+
 // Blocked fp32 row store on device (+ host mirrors of labels and visibility).
 struct RowStore {
   int dim = 0;
@@ -77,6 +91,12 @@ struct RowStore {
   bool resid = false;
   bool center16 = false;
   DevMem rsq16, center, rmax_r;
+  // the host copy of the center and the slots in use when it was set: the center follows the rows
+  // (recenter) each time the store has doubled since, and at a FLAT build (the Delta compaction)
+  std::vector<float> hcenter;
+  int64_t center_rows = 0;
+  void recenter(hipStream_t st);
+  PinnedRing ring;
   // f16 stores: a row-major fp32 copy of the rows for the exact refine (a candidate's 512 B read
   // contiguously; the blocked layout spreads one row over D 32-B sectors)
   DevMem rrm;
@@ -87,6 +107,13 @@ struct RowStore {
   uint64_t gen = 1, mub_gen = 0;
   int mub_met = -1;
   float mub_kr = 0.0f, mub_kx = 0.0f;
+  // the refresh is enqueued on the caller's stream without a host sync; another stream using the cached
+  // terms waits for mub_ev until it is seen complete.  A refresh cannot run while st is being captured
+  // (the index changed since its last search: PYR_E_STATE) -- writes refresh the FLAT store's terms on the
+  // write stream themselves (FlatIndex::after_write)
+  hipEvent_t mub_ev = nullptr;
+  hipStream_t mub_st = nullptr;
+  bool mub_done = true;
   const float *row_terms(int met, float kr, float kx, hipStream_t st);
   const float *meta_norms() const { return resid ? rsq16.as<float>() : rsq.as<float>(); }
   std::vector<int64_t> hlabels;
@@ -94,8 +121,11 @@ struct RowStore {
   void reserve(int64_t slots, hipStream_t st);
   // write rows (row-major x, n rows: host memory, or device memory when x_dev) into slots; updates
   // labels/live/norms.  A device source is read in place (no staging copy, no host hop)
-  void write(const float *x, const int64_t *slots, const int64_t *labs, int64_t cnt, hipStream_t st,
-             DevMem &stage_x, DevMem &stage_i, bool x_dev = false);
+  // Returns true when the small-batch path took the write (host rows, <= SMALL_WRITE rows, the fp16 scale
+  // unchanged): one pinned staging copy + one fused kernel, no host synchronization and no use of stage_i;
+  // otherwise the bulk path ran (stage_i then holds the device slots) and st is synchronized.
+  bool write(const float *x, const int64_t *slots, const int64_t *labs, int64_t cnt, hipStream_t st,
+             DevMem &stage_x, DevMem &stage_i, bool x_dev = false, uint8_t *q8ok = nullptr);
   void set_live(const std::vector<int64_t> &slots, uint8_t v, hipStream_t st, DevMem &stage);
   // fp16 copy of slots (device list, or [0, cap) when null) with the current scale; raises the
   // scale (and re-encodes every slot) when a row exceeds it.  Synchronizes st.
@@ -104,6 +134,12 @@ struct RowStore {
     n = 0;
     hlabels.clear();
     hlive.clear();
+  }
+  RowStore() = default;
+  RowStore(const RowStore &) = delete;
+  RowStore &operator=(const RowStore &) = delete;
+  ~RowStore() {
+    if (mub_ev) (void)hipEventDestroy(mub_ev);
   }
 };
 
@@ -133,6 +169,7 @@ struct Workspace {
   DevMem vlb, vle, vcents;  // FLAT on the stream scan: its chunks as lists (FlatIndex::search_stream)
   DevMem cq, ccs, ccl, ccc;  // Cosine on the filter path: unit queries, inner-product candidates
   DevMem shp, shthr, rpos;  // list-sharded search: unpacked plan (probes, T_q), re-run record slots
+  uint64_t wgen_seen = 0;                         // the index's write generation this stream is ordered after
   const int32_t *ext_probes = nullptr;            // caller-ranked probe lists [nq][ext_nprobe] (multi-GPU)
   int32_t ext_nprobe = 0;
   // the re-run of certificate failures searches with its own buffers on the same stream
@@ -159,6 +196,24 @@ struct Index {
   std::mutex ws_mu;
   std::vector<std::unique_ptr<Workspace>> free_ws;
   std::map<hipStream_t, std::unique_ptr<Workspace>> stream_ws;
+  // writes that return before the device ran them (RowStore::write's small-batch path): an event on wst
+  // after every write call; a search stream waits for it once per write generation (order_after_writes)
+  hipEvent_t wev = nullptr;
+  uint64_t wgen = 0;
+  void note_write();
+  void order_after_writes(Workspace &ws);
+  virtual void after_write() {}  // per-kind work at the end of a write call (on wst, no host sync)
+  // measurement only: the workspace, queries and candidate capacity of the last stream-scan slice, for
+  // pyr_index_debug_candidates (with PYR_STREAM_EMIT_ALL: every row's bound)
+  Workspace *dbg_ws = nullptr;
+  int64_t dbg_nq = 0;
+  int32_t dbg_cap = 0;
+  void note_stream_slice(Workspace &ws, int64_t nq, int cap);
+  virtual int64_t key_label(uint32_t key) const {  // the label of a stream-scan storage key (-1: none)
+    (void)key;
+    return -1;
+  }
+  void debug_candidates(int64_t nq, int32_t cap, float *h_ub, int64_t *h_label, int32_t *h_cnt);
 
   explicit Index(const pyr_index_desc &d);
   virtual ~Index();

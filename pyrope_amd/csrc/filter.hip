@@ -442,24 +442,24 @@ __global__ __launch_bounds__(256) void merge_refine_kernel(CandMergeArgs m, Refi
   bool excluded = false;
   // the ranking of depth d's candidates by (exact score desc, key asc), its k-th score and the bound of
   // everything past depth d
+  // (only the real candidates' lanes are visited: a list-sharded rank often holds few or none of a query's)
   auto rank_at = [&](int dd) {
     const uint32_t kd = lane < dd ? key : KEY_NONE;
-    int valid = 0;
+    const uint64_t rd = real & (dd >= 64 ? ~0ull : ((1ull << dd) - 1ull));
     rank = 0;
-    for (int c = 0; c < dd; ++c) {
+    for (uint64_t rm = rd; rm; rm &= rm - 1ull) {
+      const int c = (int)__builtin_ctzll(rm);
       const float sc = __shfl(s, c);
       const uint32_t kc = __shfl(kd, c);
-      if (kc == KEY_NONE) continue;
-      ++valid;
       if (kd != KEY_NONE && better(sc, kc, s, kd)) ++rank;
     }
-    nout = min(valid, k);
+    nout = min((int)__builtin_popcountll(rd), k);
     skth = -INFINITY;
-    for (int c = 0; c < dd; ++c) {
+    for (uint64_t rm = rd; rm; rm &= rm - 1ull) {
+      const int c = (int)__builtin_ctzll(rm);
       const int rc = __shfl(rank, c);
-      const uint32_t kc = __shfl(kd, c);
       const float sc = __shfl(s, c);
-      if (kc != KEY_NONE && rc == k - 1) skth = sc;
+      if (rc == k - 1) skth = sc;
     }
     excluded = __shfl(mkl, dd - 1) != -1;
     bound = __shfl(msl, dd - 1);

@@ -634,6 +634,35 @@ void launch_scatter_i64(int64_t *dst, const int64_t *idx, const int64_t *vals, i
 void launch_scatter_u8(uint8_t *dst, const int64_t *idx, uint8_t v, int64_t n, hipStream_t st);
 // norms of blocked rows at the given slots (VectorMath.ComputeNorm)
 void launch_norms_slots(const float *rows, const int64_t *slots, int64_t n, int32_t dim, float *out, hipStream_t st);
+// A few rows written in ONE launch (RowStore::write's small-batch path): everything the separate write
+// kernels do for them -- blocked rows, the row-major copy, label, live, |x|^2 (+ the store's max key or its
+// non-finite flag), the Cosine norm (ComputeNorm), and for fp16 stores the residual |x - center|^2, the
+// fp16 tile entries at the current scale and meta -- with the same arithmetic, in the same order.
+struct SmallWriteArgs {
+  const float *x;        // staged rows, row-major [cnt][dim]
+  const int64_t *slots;  // [cnt]
+  const int64_t *labs;   // [cnt]
+  int32_t cnt, dim, dp;  // dp: the tile dimension
+  float *rows, *rrm;     // blocked rows; the row-major copy (null: none)
+  int64_t *labels;
+  uint8_t *live;
+  float *norms;          // Cosine stores: ComputeNorm per slot (null: none)
+  float *rsq;
+  uint32_t *rmax;        // [0] max score key of the finite |x|^2, [1] non-finite flag
+  _Float16 *h16;         // fp16 tiles (null: none)
+  float sx;
+  const float *center;   // FLAT L2: the tiles hold x - center (null: x)
+  float *rsq16;
+  uint32_t *rmax_r;
+  float *meta;
+  int32_t met16;
+  uint8_t *q8ok;         // FLAT: the slot's 8-bit codes are invalid now (null: untouched)
+};
+void launch_write_small(const SmallWriteArgs &a, hipStream_t st);
+// per-dimension sums (fp64) of the live rows among [0, n) of a blocked store and their count -> sums[dim],
+// *count (both zeroed by the caller): the FLAT L2 tiles' re-centring (RowStore::recenter)
+void launch_live_sums(const float *rows, const uint8_t *live, int64_t n, int32_t dim, double *sums,
+                      unsigned long long *count, hipStream_t st);
 // empty result rows: score -inf, label -1, count 0
 void launch_fill_results(float *s, int64_t *l, int32_t *c, int64_t nq, int32_t k, hipStream_t st);
 bool fast_path(int dim, int k);

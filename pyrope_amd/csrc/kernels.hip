@@ -1824,6 +1824,87 @@ void launch_scatter_u8(uint8_t *dst, const int64_t *idx, uint8_t v, int64_t n, h
   if (n <= 0) return;
   hipLaunchKernelGGL(scatter_u8_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, dst, idx, v, n);
 }
+namespace {
+__global__ __launch_bounds__(64) void write_small_kernel(SmallWriteArgs a) {
+  const int i = blockIdx.x, lane = threadIdx.x, D = a.dim;
+  const int64_t r = a.slots[i];
+  const float *xs = a.x + (size_t)i * D;
+  for (int d = lane; d < D; d += 64) {
+    const float v = xs[d];
+    a.rows[blk_off(r, d, D)] = v;
+    if (a.rrm) a.rrm[(size_t)r * D + d] = v;
+  }
+  float s = 0.0f, s16 = 0.0f;
+  if (lane == 0) {
+    for (int d = 0; d < D; ++d) s = s + xs[d] * xs[d];  // sqnorms_kernel's order (filter.hip)
+    a.rsq[r] = s;
+    if (isfinite(s)) atomicMax(a.rmax, score_key(s));
+    else a.rmax[1] = 1u;
+    if (a.norms) a.norms[r] = em_norm(Lin{xs}, D);  // norms_slots_kernel: the reference ComputeNorm
+    if (a.h16 && a.center) {  // resid_sq_kernel (tiles16.hip)
+      for (int d = 0; d < D; ++d) {
+        const float v = xs[d] - a.center[d];
+        s16 += v * v;
+      }
+      a.rsq16[r] = s16;
+      if (isfinite(s16)) atomicMax(a.rmax_r, score_key(s16));
+    }
+    a.labels[r] = a.labs[i];
+    a.live[r] = 1;
+    if (a.q8ok) a.q8ok[r] = 0;
+  }
+  if (!a.h16) return;
+  // encode16_kernel + meta16_kernel (tiles16.hip) for this row
+  const float rn = __shfl(a.center ? s16 : s, 0);
+  const bool special = !isfinite(rn);
+  const int G = a.dp / 8;
+  for (int g = lane; g < G; g += 64) {
+    _Float16 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int d = 8 * g + j;
+      v[j] = special || d >= D ? (_Float16)0.0f : (_Float16)((a.center ? xs[d] - a.center[d] : xs[d]) * a.sx);
+    }
+    const size_t off = (((size_t)(r >> 5) * (a.dp / 16) + (g >> 1)) * 2 + (g & 1)) * 32 + (r & 31);
+    _Float16 *o = a.h16 + off * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = v[j];
+  }
+  if (lane == 0) a.meta[r] = isnan(rn) ? -INFINITY : isinf(rn) ? INFINITY : (a.met16 == L2 ? -rn : 0.0f);
+}
+
+__global__ __launch_bounds__(256) void live_sums_kernel(const float *rows, const uint8_t *live, int64_t n, int D,
+                                                        double *sums, unsigned long long *count) {
+  // block b: rows [b * 256, b * 256 + 256); thread d < D sums dimension d over the block's live rows
+  const int64_t r0 = (int64_t)blockIdx.x * 256;
+  const int64_t r1 = min(n, r0 + 256);
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    double acc = 0.0;
+    for (int64_t r = r0; r < r1; ++r)
+      if (live[r]) {
+        const float v = rows[blk_off(r, d, D)];
+        if (isfinite(v)) acc += (double)v;
+      }
+    if (acc != 0.0) atomicAdd(sums + d, acc);
+  }
+  if (threadIdx.x == 0) {
+    unsigned long long c = 0;
+    for (int64_t r = r0; r < r1; ++r) c += live[r] ? 1ull : 0ull;
+    if (c) atomicAdd(count, c);
+  }
+}
+}  // namespace
+
+void launch_write_small(const SmallWriteArgs &a, hipStream_t st) {
+  if (a.cnt <= 0) return;
+  hipLaunchKernelGGL(write_small_kernel, dim3((unsigned)a.cnt), dim3(64), 0, st, a);
+}
+void launch_live_sums(const float *rows, const uint8_t *live, int64_t n, int32_t dim, double *sums,
+                      unsigned long long *count, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(live_sums_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, rows, live, n, dim, sums, count);
+}
+
 void launch_norms_slots(const float *rows, const int64_t *slots, int64_t n, int32_t dim, float *out, hipStream_t st) {
   if (n <= 0) return;
   hipLaunchKernelGGL(norms_slots_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, rows, slots, n, dim, out);

@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 
 #include "kernels.h"
 
@@ -349,10 +350,20 @@ void launch_sample16(const StreamArgs &a, int metric, int max_items, hipStream_t
   }
 }
 
+// measurement only (scripts/bound_slack.py): PYR_EB_<BF|ERR|ABS|G|T> scale one constant of the bound, to find
+// how far each could shrink before some row's bound falls below its exact score (results may then differ)
+static double eb_scale(const char *name) {
+  const char *e = getenv(name);
+  return e ? atof(e) : 1.0;
+}
 void stream_ub_terms(int dim, int metric, double c_bf, double c_err, double c_abs, StreamArgs &a) {
   const double u = 5.9604644775390625e-8;         // 2^-24
-  const double t = 1.4551915228366852e-11 * std::sqrt((double)dim);  // the query's fp16 subnormals, 2^-36 sqrt(D)
-  const double g = (dim / 8.0 + 8.0) * u;         // the reference's own sum (refine_kernel)
+  c_bf *= eb_scale("PYR_EB_BF");
+  c_err *= eb_scale("PYR_EB_ERR");
+  c_abs *= eb_scale("PYR_EB_ABS");
+  // the query's fp16 subnormals, 2^-36 sqrt(D)
+  const double t = 1.4551915228366852e-11 * std::sqrt((double)dim) * eb_scale("PYR_EB_T");
+  const double g = (dim / 8.0 + 8.0) * u * eb_scale("PYR_EB_G");  // the reference's own sum (refine_kernel)
   const double up = 1.0 + 1e-3;                   // the fp32 evaluation of the terms themselves
   if (metric == L2) {
     // c_bf u A X + c_err u (A + X)^2 + c_abs A + 2 t A X, and g |q - x|^2 <= g (A + X)^2

@@ -200,6 +200,23 @@ def rank_memory_plan(dim: int, nrows: int, nlist: int, max_list_len: int, nq: in
 SAMPLE_ROWS = 512  # rows of every list replicated for the home rank's threshold (sample16.hip: 16 tiles)
 
 
+def rank_memory_plan_lists(dim: int, rank_rows: int, nlist: int, max_list_len: int, nq_home: int, world: int,
+                           nprobe: int, k: int, fcap: int = 256):
+    """(index_bytes, workspace_bytes) of one rank of the list-sharded step (ListShardedIvf), before it
+    allocates: its whole lists (rank_rows rows over the global quantizer's nlist lists) plus the replicated
+    sample store (min(len, 512) rows of every list, planned as a second index of nlist x 512 rows -- an
+    over-estimate: the sample store keeps no row-major copy), and one step's buffers: the search of all
+    world x nq_home queries against the rank's lists (pyr_ivf_memory_plan), the plans (home + gathered), the
+    records (sent + received), the failure lists and the re-run records."""
+    P = min(nprobe, nlist)
+    Q = world * nq_home
+    ib, wb = rank_memory_plan(dim, rank_rows, nlist, max_list_len, Q, P, k)
+    sb, swb = rank_memory_plan(dim, nlist * SAMPLE_ROWS, nlist, SAMPLE_ROWS, nq_home, P, k)
+    rb = 16 * (k + 1)
+    step = 4 * (P + 1) * (nq_home + Q) + 2 * rb * Q + 4 * world * (1 + fcap) * 2 + 2 * rb * world * fcap
+    return ib + sb, max(wb, swb) + step
+
+
 def list_owners(list_len, world: int) -> np.ndarray:
     """Size-balanced owner of every list: lists by length (desc, ties by id) to the rank with the fewest rows
     so far (ties: lowest rank) -- deterministic, so every rank computes the same table."""

@@ -9,6 +9,11 @@
 #   kt <name> <secs> [bench args]      the same under rocprofv3 --kernel-trace --stats (csv under <outdir>/<name>/)
 #   pmc <name> <counters> [bench args] one rocprofv3 --pmc pass (its own run; counters of one block budget)
 #   aux <name> <secs> <script> [args]  python -u <script> args -> <outdir>/<name>.log
+#   ktaux <name> <secs> <script> [args]  the same under rocprofv3 --kernel-trace --stats (csv under <outdir>/<name>/)
+#   pmcaux <name> <secs> <counters> <script> [args]  one rocprofv3 --pmc pass over a script
+# P1 (IVF_PQ d=768 N=50M nlist=4096 m=96 nprobe=64, 10k queries; ~5 min of build):
+#   bash scripts/measure.sh <outdir> aux p1 1100 scripts/bench_aux.py ivfpq --n 50000000 --train-rows 1048576 \
+#        --nlist 4096 --m 96 --nprobe 64 --nq 10000 --steps 3 --check 2000 --recall-queries 200
 #
 # Example: bash scripts/measure.sh gpurun_out/r5a tests 300 && bash scripts/measure.sh gpurun_out/r5a bench i1 400
 set -o pipefail
@@ -64,6 +69,20 @@ case "$step" in
     timeout -k 10 "$secs" python -u "$script" "$@" > "$O/$name.log" 2>&1
     rc=$?
     tail -n 12 "$O/$name.log"
+    exit $rc ;;
+  ktaux)
+    name=$1; secs=$2; script=$3; shift 3
+    timeout -k 10 "$secs" rocprofv3 --kernel-trace --stats --output-format csv -d "$O/$name" -o run -- \
+      python3 -u "$script" "$@" > "$O/$name.log" 2>&1
+    rc=$?
+    tail -n 12 "$O/$name.log"
+    exit $rc ;;
+  pmcaux)
+    name=$1; secs=$2; ctrs=$3; script=$4; shift 4
+    timeout -s KILL "$secs" rocprofv3 --pmc $ctrs --output-format csv -d "$O/$name" -o run -- python3 -u "$script" "$@" \
+      > "$O/$name.log" 2>&1
+    rc=$?
+    tail -n 6 "$O/$name.log"
     exit $rc ;;
   *)
     echo "unknown step $step" >&2; exit 2 ;;

@@ -131,8 +131,11 @@ def main():
 
     full_step()
     torch.cuda.synchronize()
+    per = np.bincount(owner[plans[:, :P].cpu().numpy().ravel()], minlength=W)
     res = {"world": W, "rank": R, "rows": int(rows[R]), "lists": int((owner == R).sum()), "queries_all": Q,
-           "queries_home": nq, "nprobe": P, "failures_per_home": fails[:, 0].cpu().tolist()}
+           "queries_home": nq, "nprobe": P, "failures_per_home": fails[:, 0].cpu().tolist(),
+           "pairs_per_rank": per.tolist(), "pairs_max_over_mean": round(float(per.max() / per.mean()), 4),
+           "rows_per_rank": rows.astype(np.int64).tolist()}
     if ref is not None:
         s_, l_ = out_s.cpu().numpy(), out_l.cpu().numpy()
         res["parity"] = {"queries": Q, "ids_equal": bool(np.array_equal(l_, ref[1])),

@@ -297,3 +297,18 @@ def test_rank_memory_plan_at_m8_rank_shape(hiplib):
     w_small = rank_memory_plan(128, 10_000_000, 8192, 20_000, 1_000, 32, 10)[1]
     w_big = rank_memory_plan(128, 10_000_000, 8192, 20_000, 1_000_000, 32, 10)[1]
     assert w_small < wb < w_big < 40e9
+
+
+def test_rank_memory_plan_list_sharded_m8(hiplib):
+    """the list-sharded step's rank at the M8 shape (80M rows over 8 ranks, nlist 8192, 10,000
+    home queries, every rank searching the 80,000-query batch against its own lists) fits one MI355X with
+    room to spare: its whole lists, the replicated 512-row sample of every list, and one step's buffers."""
+    from pyrope_amd.dist import rank_memory_plan, rank_memory_plan_lists
+    hbm = 288e9
+    ib, wb = rank_memory_plan_lists(128, 10_000_000, 8192, 40_000, 10_000, 8, 32, 10)
+    ib0, _ = rank_memory_plan(128, 10_000_000, 8192, 40_000, 80_000, 32, 10)
+    assert ib0 < ib < ib0 + 8192 * 512 * 1.5e3   # + the sample store (<= 1.5 kB per sampled row)
+    assert ib + wb < 0.25 * hbm, (ib, wb)
+    # the step's buffers grow with the batch; I1 at 8 ranks (nlist 1024) is far smaller
+    ib1, wb1 = rank_memory_plan_lists(128, 1_250_000, 1024, 20_000, 10_000, 8, 32, 10)
+    assert ib1 + wb1 < ib + wb
