@@ -557,7 +557,7 @@ static void flat_scan(const RowStore &rs, int64_t nrows, const ScanPlan &p, cons
   DevMem &items = second ? ws.items2 : ws.items;
   DevMem &nitems = second ? ws.nitems2 : ws.nitems;
   items.ensure(sizeof(ScanItem) * std::max(p.nitems, 1));
-  nitems.ensure(sizeof(int32_t) * 4);
+  nitems.ensure(sizeof(int32_t) * 16);  // the count + 9 queue bounds (ivf_scan_kernel)
   make_flat_items(items.as<ScanItem>(), nitems.as<int32_t>(), nrows, p.chunk_rows, nq, part_off, p.qchunk, ws.st);
   ScanArgs a{};
   a.rows = rs.rows.as<float>();
@@ -699,7 +699,9 @@ static int64_t stream_slice_queries(int64_t nq, int probes, int dt, int cap, int
 
 // HBM plan of an IVF_FLAT index and of one stream-path search on it (pyr_ivf_memory_plan): the
 // allocations commit_lists and search_stream / stream_slice make, restated as arithmetic so that a
-// multi-GPU launch can size a rank before it allocates (the M8 rank shape: tests/test_host_logic.py).
+// multi-GPU launch can size a rank before it allocates (the M8 rank shape: tests/test_dist.py).  These are
+// steady-state bytes: building a shard holds the new list store beside the old one plus the row-major and
+// blocked temporaries of every row (dist.rank_build_peak_bytes).
 void ivf_memory_plan(int dim, int64_t nrows, int nlist, int64_t max_len, int64_t nq, int nprobe, int k,
                      int64_t *index_bytes, int64_t *workspace_bytes) {
   const int64_t D = dim, DT = std::max(dim, scan_tile_dim(dim));  // DT: the fp16 tiles' (padded) dimension
@@ -1150,7 +1152,7 @@ struct FlatIndex : Index {
     ws.part_s.ensure(sizeof(float) * np);
     ws.part_k.ensure(sizeof(uint32_t) * np);
     ws.items.ensure(sizeof(ScanItem) * std::max<int64_t>(nqc * nchunks, 1));
-    ws.nitems.ensure(sizeof(int32_t) * 4);
+    ws.nitems.ensure(sizeof(int32_t) * 16);  // the count + 9 queue bounds (ivf_scan_kernel)
     const int ni = make_flat_items(ws.items.as<ScanItem>(), ws.nitems.as<int32_t>(), cutoff, (int32_t)chunk, nq, 0,
                                    sq8_qgroup(), ws.st);
     Sq8Args a{};
@@ -1823,7 +1825,7 @@ static int build_ivf_items_range(Workspace &ws, int set, int64_t nq, int nprobe,
   ioff.ensure(sizeof(int32_t) * (nlist + 1));
   qlist.ensure(sizeof(int32_t) * std::max<int64_t>(nq * (pe - pb), 1));
   items.ensure(sizeof(ScanItem) * std::max(maxi, 1));
-  nitems.ensure(sizeof(int32_t) * 4);
+  nitems.ensure(sizeof(int32_t) * 16);  // the count + 9 queue bounds (ivf_scan_kernel)
   IvfItemWs iw{cnt.as<int32_t>(), fill.as<int32_t>(), qoff.as<int32_t>(), ioff.as<int32_t>(), qlist.as<int32_t>(),
                items.as<ScanItem>(), nitems.as<int32_t>()};
   launch_ivf_items(ws.probes.as<int32_t>(), nq, nprobe, nparts, nlist, lbeg.as<int32_t>(), lend.as<int32_t>(), qchunk,
@@ -3164,7 +3166,7 @@ struct IvfPqIndex : Index {
     if (pq32_supported(dim, M, ksub, 10)) {
       // tile code layout + |x^|^2 per position; fp16 codebook with a power-of-two scale keeping max |C| < 2^14
       const int64_t tiles = (tot + 31) / 32;
-      const size_t cbytes = (size_t)std::max<int64_t>(tiles, 1) * 32 * 16 * pq32_code_words(M);
+      const size_t cbytes = (size_t)std::max<int64_t>(tiles, 1) * 64 * 16 * pq32_lane_words(dim, M);
       cpack.ensure(cbytes);
       HIPCHK(hipMemsetAsync(cpack.p, 0, cbytes, wst));
       nrm.ensure(sizeof(float) * (size_t)std::max<int64_t>(tiles * 32, 1));
@@ -3257,7 +3259,8 @@ struct IvfPqIndex : Index {
     const int k1 = filter_k1(k);
     const int cap = stream_cap();
     IvfChunking ch{(int32_t)stream_chunk(), 1, 0};
-    ch.xcd = 1;  // a list's items on one XCD (pq32.hip: its code chunks leave HBM once per L2)
+    // a list's items on one XCD (pq32.hip: its code chunks leave HBM once per L2); PYR_PQ_XCD=0: one queue (A/B)
+    ch.xcd = getenv("PYR_PQ_XCD") && atoi(getenv("PYR_PQ_XCD")) == 0 ? 0 : 1;
     ch.cmax = std::max(1, ivf_list_chunks((int)pq_max_len, ch));
     if ((int64_t)probes * ch.cmax > MAX_PARTS) {
       const int64_t room = std::max<int64_t>(1, MAX_PARTS / std::max(probes, 1));
@@ -3390,7 +3393,7 @@ struct IvfPqIndex : Index {
     r.dim = dim;
     r.M = M;
     r.ksub = ksub;
-    r.mw = pq32_code_words(M);
+    r.lw = pq32_lane_words(dim, M);
     r.dsub = sub;
     r.nlist = coarse.nlist;
     r.out_s = d_s;

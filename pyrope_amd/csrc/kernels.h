@@ -371,9 +371,10 @@ void stream_ub_terms(int dim, int metric, double c_bf, double c_err, double c_ab
 bool pq32_supported(int dim, int M, int ksub, int k);
 int pq32_qmax(int dim, int M);      // queries per item
 int pq32_sample_values();           // sample values per (query, probe)
-int pq32_code_words(int M);         // 16-byte code words per row
-// codes (row-major, source rows) -> the tile layout cpack [tile][word][32 rows][16 B] of the list-major
-// positions (src: position -> source row or -1) and |x^|^2 per position (fp32 codebooks [M][ksub][dsub])
+int pq32_lane_words(int dim, int M);  // 16-byte code words per lane per 32-row tile (cpack: 64 lanes of them)
+// codes (row-major, source rows) -> the tile layout cpack [tile][64 lanes][lane words][16 B] of the list-major
+// positions (src: position -> source row or -1; pq32.hip pq_pack_kernel) and |x^|^2 per position (fp32
+// codebooks [M][ksub][dsub])
 void launch_pq32_pack(const uint8_t *codes_rm, const int64_t *src, int64_t tot, int M, int dsub, const float *cb,
                       int ksub, uint8_t *cpack, float *nrm, hipStream_t st);
 void launch_pq32_cb16(const float *cb, int M, int ksub, int dsub, float sc, _Float16 *cb16, hipStream_t st);
@@ -394,7 +395,7 @@ struct PqRefineArgs {
   const int32_t *mk;        // their positions (-2 floor, -1 none)
   const int32_t *qsel, *nsel;  // refine only these queries (null: all nq)
   int64_t nq;
-  int32_t ld, k1, k, dim, M, ksub, mw, dsub, nlist;
+  int32_t ld, k1, k, dim, M, ksub, lw, dsub, nlist;
   float *out_s;
   int64_t *out_l;
   int32_t *out_c;

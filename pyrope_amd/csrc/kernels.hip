@@ -746,6 +746,8 @@ __global__ __launch_bounds__(1024) void ivf_scan_kernel(const int32_t *cnt, int 
     *n_items = si[1023];
     if (chk.xcd)  // the end bound, and the bounds of queues with no list (nlist < 8)
       for (int x = min(nlist, 8); x <= 8; ++x) n_items[1 + x] = si[1023];
+    else  // one queue holding every item (a queue-taking kernel steals it from the others' empty ones)
+      for (int x = 0; x <= 8; ++x) n_items[1 + x] = x == 0 ? 0 : si[1023];
   }
 }
 

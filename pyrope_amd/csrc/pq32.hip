@@ -65,7 +65,7 @@ __device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf
 struct PqGeo {
   int ks;    // k-steps (D / 16)
   int dsub;  // dims per subspace
-  int mw;    // 16-byte code words per row (16 subspaces each)
+  int lw;    // 16-byte code words per lane per tile (the lane's code stream, k-step order)
   int res;   // 1: A-resident tile loop (KS <= 8)
   int kp;    // A-resident: padded k-steps (8); k-outer: query groups per item
   int qmax;  // queries per item
@@ -74,7 +74,7 @@ PqGeo pq_geo(int dim, int M) {
   PqGeo g{};
   g.ks = dim / 16;
   g.dsub = M > 0 ? dim / M : 0;
-  g.mw = (M + 15) / 16;
+  g.lw = (g.ks * (g.dsub == 4 ? 2 : 1) + 15) / 16;
   g.res = g.ks <= 8;  // (16 resident k-steps spill: 64 VGPRs of A besides the accumulator and the row terms)
   if (g.res) {
     g.kp = 8;
@@ -87,28 +87,39 @@ PqGeo pq_geo(int dim, int M) {
 }
 
 // ---- build: the tile layout of the codes, |x^|^2 per row, the fp16 codebook ----
-// tile t (positions 32t .. 32t + 31 of the list-major rows), row r: code word w (codes 16w .. 16w + 15,
-// zero past M) at byte ((t * mw + w) * 32 + r) * 16 -- a wave's 32 rows read one word in 512 contiguous bytes
-__global__ void pq_pack_kernel(const uint8_t *codes_rm, const int64_t *src, int64_t tot, int M, int mw, int dsub,
-                               const float *cb, int ksub, uint8_t *cpack, float *nrm) {
+// Lane (r, h) of a 32-row tile reads, k-step by k-step, the code(s) its A fragment (dims 16 s + 8 h .. +7
+// of row r) decodes from: dsub 8 -> code[2s + h]; 16 -> code[s]; 32 -> code[s / 2]; 4 -> code[4s + 2h],
+// code[4s + 2h + 1].  These bytes, in k-step order, are the lane's code stream: tile t, lane l at
+// ((t * 64 + l) * lw * 16), lw 16-byte words (as many bytes as the row has codes at dsub 8 and 4; the
+// codes repeat across the two halves at dsub 16 and also across a subspace's two k-steps at 32).
+__device__ __forceinline__ int pq_stream_code(int dsub, int h, int b) {  // the subspace of stream byte b
+  return dsub == 8 ? 2 * b + h : dsub == 16 ? b : dsub == 32 ? b / 2 : 4 * (b >> 1) + 2 * h + (b & 1);
+}
+__global__ void pq_pack_kernel(const uint8_t *codes_rm, const int64_t *src, int64_t tot, int M, int ks, int lw,
+                               int dsub, const float *cb, int ksub, uint8_t *cpack, float *nrm) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= tot) return;
   const int64_t sr = src[p];
   const int64_t t = p >> 5;
   const int r = (int)(p & 31);
+  const int nb = ks * (dsub == 4 ? 2 : 1);  // stream bytes per lane
+  for (int h = 0; h < 2; ++h)
+    for (int w = 0; w < lw; ++w) {
+      uint32_t cw[4] = {0u, 0u, 0u, 0u};
+      for (int j = 0; j < 16; ++j) {
+        const int bi = 16 * w + j;
+        if (bi >= nb || sr < 0) continue;
+        const int m = pq_stream_code(dsub, h, bi);
+        cw[j >> 2] |= (uint32_t)codes_rm[(size_t)sr * M + m] << (8 * (j & 3));
+      }
+      *reinterpret_cast<u4v *>(cpack + (((size_t)t * 64 + 32 * h + r) * lw + w) * 16) = (u4v){cw[0], cw[1], cw[2], cw[3]};
+    }
   float n = 0.0f;
-  for (int w = 0; w < mw; ++w) {
-    uint32_t cw[4] = {0u, 0u, 0u, 0u};
-    for (int j = 0; j < 16; ++j) {
-      const int m = 16 * w + j;
-      if (m >= M || sr < 0) continue;
-      const int c = codes_rm[(size_t)sr * M + m];
-      cw[j >> 2] |= (uint32_t)c << (8 * (j & 3));
-      const float *v = cb + ((size_t)m * ksub + c) * dsub;
+  if (sr >= 0)
+    for (int m = 0; m < M; ++m) {
+      const float *v = cb + ((size_t)m * ksub + codes_rm[(size_t)sr * M + m]) * dsub;
       for (int u = 0; u < dsub; ++u) n += v[u] * v[u];
     }
-    *reinterpret_cast<u4v *>(cpack + (((size_t)t * mw + w) * 32 + r) * 16) = (u4v){cw[0], cw[1], cw[2], cw[3]};
-  }
   nrm[p] = n;
 }
 
@@ -157,26 +168,24 @@ __global__ __launch_bounds__(256) void pq_prep_kernel(StreamArgs a, int64_t npos
   if (lane == 0) a.qsc[pos] = make_float2(2.0f / (sq * a.sx), -cq + ep);
 }
 
-// ---- decode: k-step u of code word w (16 subspaces = dsub k-steps), lane half h ----
+// ---- decode: the A fragment of k-step s for lane half h; u = its position in the lane's current code
+// word (the word's byte u, or bytes 2u, 2u + 1 at dsub 4) ----
 template <int DSUB>
-__device__ __forceinline__ h8v pq_decode(const uint32_t (&cw)[4], const _Float16 *cb16, int w, int u, int h) {
-  if constexpr (DSUB == 4) {  // dims 8h .. 8h+7 of the k-step: subspaces 4u + 2h, 4u + 2h + 1 of the word
-    const uint32_t sh = 16u * (uint32_t)h;
-    const uint32_t c0 = (cw[u] >> sh) & 0xFFu, c1 = (cw[u] >> (sh + 8u)) & 0xFFu;
-    const int m0 = 16 * w + 4 * u + 2 * h;
+constexpr int pq_steps_per_word() { return DSUB == 4 ? 8 : 16; }
+template <int DSUB>
+__device__ __forceinline__ h8v pq_decode(const uint32_t (&cw)[4], const _Float16 *cb16, int s, int u, int h) {
+  auto byte = [&](int b) { return (cw[b >> 2] >> (8 * (b & 3))) & 0xFFu; };
+  if constexpr (DSUB == 4) {  // dims 8h .. 8h+7 of the k-step: subspaces 4s + 2h, 4s + 2h + 1
+    const uint32_t c0 = byte(2 * u), c1 = byte(2 * u + 1);
+    const int m0 = 4 * s + 2 * h;
     const u2v lo = *reinterpret_cast<const u2v *>(cb16 + ((size_t)m0 * 256 + c0) * 4);
     const u2v hi = *reinterpret_cast<const u2v *>(cb16 + ((size_t)(m0 + 1) * 256 + c1) * 4);
     return __builtin_bit_cast(h8v, ((u4v){lo.x, lo.y, hi.x, hi.y}));
-  } else if constexpr (DSUB == 8) {  // subspace 2u + h
-    const uint32_t c = (cw[u >> 1] >> (8u * (uint32_t)((2 * u) & 3) + 8u * (uint32_t)h)) & 0xFFu;
-    const int m = 16 * w + 2 * u + h;
-    return *reinterpret_cast<const h8v *>(cb16 + ((size_t)m * 256 + c) * 8);
-  } else {  // 16, 32: subspace u / (DSUB / 16), both halves; dims (16 u + 8 h) mod DSUB of its sub-centroid
-    constexpr int SPK = DSUB / 16;  // k-steps per subspace
-    const int j = u / SPK;
-    const uint32_t c = (cw[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-    const int m = 16 * w + j;
-    return *reinterpret_cast<const h8v *>(cb16 + ((size_t)m * 256 + c) * DSUB + 16 * (u % SPK) + 8 * h);
+  } else if constexpr (DSUB == 8) {  // subspace 2s + h
+    return *reinterpret_cast<const h8v *>(cb16 + ((size_t)(2 * s + h) * 256 + byte(u)) * 8);
+  } else {  // 16, 32: subspace s / (DSUB / 16); dims (16 s + 8 h) mod DSUB of its sub-centroid
+    constexpr int SPK = DSUB / 16;
+    return *reinterpret_cast<const h8v *>(cb16 + ((size_t)(s / SPK) * 256 + byte(u)) * DSUB + 16 * (s % SPK) + 8 * h);
   }
 }
 
@@ -299,10 +308,11 @@ __device__ __forceinline__ float pq_tile_max(const f16v &acc, float f, const flo
 
 // ---- tile loop 1 (KS <= 16): decoded A resident, every group against it ----
 template <int KSP, int DSUB, bool SAMPLE>
-__global__ __launch_bounds__(64 * PNW, 1) void pq_scan_res_kernel(StreamArgs a, const _Float16 *cb16, int mw) {
+__global__ __launch_bounds__(64 * PNW, 1) void pq_scan_res_kernel(StreamArgs a, const _Float16 *cb16, int lw) {
   constexpr int QG = KSP <= 8 ? 16 : 8;
   constexpr int QMAX = 32 * QG;
-  constexpr int NW = (KSP + DSUB - 1) / DSUB;  // code words covering KSP k-steps
+  constexpr int SPW = pq_steps_per_word<DSUB>();
+  constexpr int NW = (KSP + SPW - 1) / SPW;  // code words covering KSP k-steps
   __shared__ __attribute__((aligned(16))) char bl[QG * KSP * 1024];
   __shared__ PqItemLds<QMAX> L;
   const uint32_t bl_base = (uint32_t)(size_t)(lds_void *)bl;
@@ -334,16 +344,16 @@ __global__ __launch_bounds__(64 * PNW, 1) void pq_scan_res_kernel(StreamArgs a, 
       const int rt = r0 + 32 * t;
       h8v A[KSP];
       {
-        const u4v *cp = reinterpret_cast<const u4v *>(cpk + ((size_t)(rt >> 5) * mw * 32 + r) * 16);
+        const u4v *cp = reinterpret_cast<const u4v *>(cpk + ((size_t)(rt >> 5) * 64 + lane) * lw * 16);
 #pragma unroll
         for (int wi = 0; wi < NW; ++wi) {
           uint32_t cw[4] = {0u, 0u, 0u, 0u};
-          if (wi < mw) split_word(cp[wi * 32], cw);
+          if (wi < lw) split_word(cp[wi], cw);
 #pragma unroll
-          for (int u = 0; u < DSUB; ++u) {
-            const int s = wi * DSUB + u;
+          for (int u = 0; u < SPW; ++u) {
+            const int s = wi * SPW + u;
             if (s >= KSP) break;
-            A[s] = s < KS ? pq_decode<DSUB>(cw, cb16, wi, u, h) : (h8v){};
+            A[s] = s < KS ? pq_decode<DSUB>(cw, cb16, s, u, h) : (h8v){};
           }
         }
       }
@@ -387,9 +397,9 @@ __global__ __launch_bounds__(64 * PNW, 1) void pq_scan_res_kernel(StreamArgs a, 
 
 // ---- tile loop 2 (KS > 16): k-outer, each decoded k-step against PQG groups ----
 template <int PQG, int DSUB, bool SAMPLE>
-__global__ __launch_bounds__(64 * PNW, 1) void pq_scan_kout_kernel(StreamArgs a, const _Float16 *cb16, int mw) {
+__global__ __launch_bounds__(64 * PNW, 1) void pq_scan_kout_kernel(StreamArgs a, const _Float16 *cb16, int lw) {
   constexpr int QMAX = 32 * PQG;
-  constexpr int WPI = DSUB >= 16 ? 1 : 16 / DSUB;  // code words per iteration (16 k-steps at dsub <= 16)
+  constexpr int SPW = pq_steps_per_word<DSUB>();  // k-steps per code word
   __shared__ __attribute__((aligned(16))) char bl[144 * 1024];
   __shared__ PqItemLds<QMAX> L;
   const uint32_t bl_base = (uint32_t)(size_t)(lds_void *)bl;
@@ -419,35 +429,26 @@ __global__ __launch_bounds__(64 * PNW, 1) void pq_scan_kout_kernel(StreamArgs a,
 #pragma unroll 1
     for (int t = w; t < nt; t += PNW) {
       const int rt = r0 + 32 * t;
-      const u4v *cp = reinterpret_cast<const u4v *>(cpk + ((size_t)(rt >> 5) * mw * 32 + r) * 16);
+      const u4v *cp = reinterpret_cast<const u4v *>(cpk + ((size_t)(rt >> 5) * 64 + lane) * lw * 16);
       f16v acc[PQG];
 #pragma unroll
       for (int g = 0; g < PQG; ++g) acc[g] = (f16v){};
-      u4v nxt[WPI];  // the next iteration's code words, loaded one iteration ahead
-#pragma unroll
-      for (int wi = 0; wi < WPI; ++wi) nxt[wi] = wi < mw ? cp[wi * 32] : (u4v){0u, 0u, 0u, 0u};
+      u4v nxt = cp[0];  // the next word of the lane's code stream, loaded one word ahead
 #pragma unroll 1
-      for (int w0 = 0; w0 < mw; w0 += WPI) {
-        uint32_t cw[WPI][4];
+      for (int wi = 0; wi < lw; ++wi) {
+        uint32_t cw[4];
+        split_word(nxt, cw);
+        if (wi + 1 < lw) nxt = cp[wi + 1];
 #pragma unroll
-        for (int wi = 0; wi < WPI; ++wi) {
-          split_word(nxt[wi], cw[wi]);
-          const int wn = w0 + WPI + wi;
-          nxt[wi] = wn < mw ? cp[wn * 32] : (u4v){0u, 0u, 0u, 0u};
-        }
+        for (int u = 0; u < SPW; ++u) {
+          const int s = wi * SPW + u;
+          if (s >= KS) break;
+          const h8v A = pq_decode<DSUB>(cw, cb16, s, u, h);
 #pragma unroll
-        for (int wi = 0; wi < WPI; ++wi) {
-#pragma unroll
-          for (int u = 0; u < DSUB; ++u) {
-            const int s = (w0 + wi) * DSUB + u;
-            if (s >= KS) break;
-            const h8v A = pq_decode<DSUB>(cw[wi], cb16, w0 + wi, u, h);
-#pragma unroll
-            for (int g = 0; g < PQG; ++g) {
-              if (g >= ng) break;  // (wave-uniform) a short item skips the empty groups' MFMAs
-              const h8v B = *reinterpret_cast<const h8v *>(bl + (g * KS + s) * 1024 + lane * 16);
-              acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, B, acc[g], 0, 0, 0);
-            }
+          for (int g = 0; g < PQG; ++g) {
+            if (g >= ng) break;  // (wave-uniform) a short item skips the empty groups' MFMAs
+            const h8v B = *reinterpret_cast<const h8v *>(bl + (g * KS + s) * 1024 + lane * 16);
+            acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, B, acc[g], 0, 0, 0);
           }
         }
       }
@@ -501,11 +502,14 @@ __global__ __launch_bounds__(256) void pq_refine_kernel(PqRefineArgs a) {
     }
     const float *qv = a.queries + (size_t)q * a.dim;
     const float *cv = a.cents + (size_t)lo * a.dim;
-    const uint8_t *cp = a.cpack + ((size_t)(key >> 5) * a.mw * 32 + (key & 31)) * 16;
-    const int ds = a.dsub;
+    const uint8_t *tp = a.cpack + (size_t)(key >> 5) * 64 * a.lw * 16;  // the row's tile
+    const int ds = a.dsub, r = key & 31;
     float dist = 0.0f;
     for (int m = 0; m < a.M; ++m) {
-      const int c = cp[(size_t)(m >> 4) * 512 + (m & 15)];
+      // code m in the code stream of lane (r, h) (pq_pack_kernel): its k-step's byte
+      const int h = ds == 8 ? (m & 1) : ds == 4 ? ((m >> 1) & 1) : 0;
+      const int b = ds == 8 ? m >> 1 : ds == 16 ? m : ds == 32 ? 2 * m : 2 * (m >> 2) + (m & 1);
+      const int c = tp[(size_t)(32 * h + r) * a.lw * 16 + b];
       dist = dist + em_l2sq_unsafe(Res{qv + m * ds, cv + m * ds}, Off{a.codebooks + ((size_t)m * a.ksub + c) * ds}, ds);
     }
     sc = -dist;
@@ -548,23 +552,23 @@ __global__ __launch_bounds__(256) void pq_refine_kernel(PqRefineArgs a) {
 }
 
 template <class K>
-void pq_launch(K kern, int grid, const StreamArgs &a, const _Float16 *cb16, int mw, hipStream_t st) {
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * PNW), 0, st, a, cb16, mw);
+void pq_launch(K kern, int grid, const StreamArgs &a, const _Float16 *cb16, int lw, hipStream_t st) {
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * PNW), 0, st, a, cb16, lw);
 }
 template <int DSUB>
 void launch_scan_dsub(const StreamArgs &a, const _Float16 *cb16, const PqGeo &g, int grid, bool sample, hipStream_t st) {
   if (g.res) {
-    if (sample) pq_launch(pq_scan_res_kernel<8, DSUB, true>, grid, a, cb16, g.mw, st);
-    else pq_launch(pq_scan_res_kernel<8, DSUB, false>, grid, a, cb16, g.mw, st);
+    if (sample) pq_launch(pq_scan_res_kernel<8, DSUB, true>, grid, a, cb16, g.lw, st);
+    else pq_launch(pq_scan_res_kernel<8, DSUB, false>, grid, a, cb16, g.lw, st);
   } else if (g.kp == 4) {
-    if (sample) pq_launch(pq_scan_kout_kernel<4, DSUB, true>, grid, a, cb16, g.mw, st);
-    else pq_launch(pq_scan_kout_kernel<4, DSUB, false>, grid, a, cb16, g.mw, st);
+    if (sample) pq_launch(pq_scan_kout_kernel<4, DSUB, true>, grid, a, cb16, g.lw, st);
+    else pq_launch(pq_scan_kout_kernel<4, DSUB, false>, grid, a, cb16, g.lw, st);
   } else if (g.kp == 3) {
-    if (sample) pq_launch(pq_scan_kout_kernel<3, DSUB, true>, grid, a, cb16, g.mw, st);
-    else pq_launch(pq_scan_kout_kernel<3, DSUB, false>, grid, a, cb16, g.mw, st);
+    if (sample) pq_launch(pq_scan_kout_kernel<3, DSUB, true>, grid, a, cb16, g.lw, st);
+    else pq_launch(pq_scan_kout_kernel<3, DSUB, false>, grid, a, cb16, g.lw, st);
   } else {
-    if (sample) pq_launch(pq_scan_kout_kernel<2, DSUB, true>, grid, a, cb16, g.mw, st);
-    else pq_launch(pq_scan_kout_kernel<2, DSUB, false>, grid, a, cb16, g.mw, st);
+    if (sample) pq_launch(pq_scan_kout_kernel<2, DSUB, true>, grid, a, cb16, g.lw, st);
+    else pq_launch(pq_scan_kout_kernel<2, DSUB, false>, grid, a, cb16, g.lw, st);
   }
 }
 
@@ -578,13 +582,14 @@ bool pq32_supported(int dim, int M, int ksub, int k) {
 }
 int pq32_qmax(int dim, int M) { return pq_geo(dim, M).qmax; }
 int pq32_sample_values() { return PSV; }
-int pq32_code_words(int M) { return (M + 15) / 16; }
+int pq32_lane_words(int dim, int M) { return pq_geo(dim, M).lw; }
 
 void launch_pq32_pack(const uint8_t *codes_rm, const int64_t *src, int64_t tot, int M, int dsub, const float *cb,
                       int ksub, uint8_t *cpack, float *nrm, hipStream_t st) {
   if (tot <= 0) return;
+  const PqGeo g = pq_geo(M * dsub, M);
   hipLaunchKernelGGL(pq_pack_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, codes_rm, src, tot, M,
-                     pq32_code_words(M), dsub, cb, ksub, cpack, nrm);
+                     g.ks, g.lw, dsub, cb, ksub, cpack, nrm);
 }
 void launch_pq32_cb16(const float *cb, int M, int ksub, int dsub, float sc, _Float16 *cb16, hipStream_t st) {
   const int64_t n = (int64_t)M * 256 * dsub;

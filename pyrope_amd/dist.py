@@ -194,6 +194,13 @@ def rank_memory_plan(dim: int, nrows: int, nlist: int, max_list_len: int, nq: in
     return ib.value, wb.value
 
 
+def rank_build_peak_bytes(dim: int, nrows: int, nlist: int, max_list_len: int) -> int:
+    """Peak HBM while a rank builds its shard: commit_lists builds the new list store beside the
+    old one (2 x the steady-state index bytes) and holds a row-major and a blocked fp32 copy of the rows."""
+    ib, _ = rank_memory_plan(dim, nrows, nlist, max_list_len, 1, 1, 1)
+    return 2 * ib + 2 * 4 * dim * nrows
+
+
 # =============================================================================================
 # List-sharded IVF_FLAT (SURVEY.md 8(e)(i); C ABI: include/pyrope_ann.h "List-sharded multi-GPU")
 # =============================================================================================

@@ -338,7 +338,7 @@ class HipVectorIndex(IVectorIndex):
                 ids = json.load(f)
         except FileNotFoundError:
             pass
-        if ids is not None and ids.get("image_nonce") != self._image_nonce(path):
+        if ids is not None and not self._map_matches(path, ids):
             warnings.warn(f"{path}.ids belongs to another image (nonce mismatch); ids fall back to "
                           "str(label)", RuntimeWarning, stacklevel=2)
             ids = None
@@ -351,6 +351,21 @@ class HipVectorIndex(IVectorIndex):
             self._label_of[i] = lab
             self._id_of[lab] = i
         self._next_label = int(ids.get("next", 0))
+
+    def _map_matches(self, path, ids) -> bool:
+        """An id map pairs with the image whose nonce it recorded.  A map written before images carried a
+        nonce (no 'image_nonce'; round 3's 'image': [size, mtime_ns]) pairs only with a nonce-less image
+        (its nonce reads as zeros) whose size and mtime it recorded."""
+        nonce = self._image_nonce(path)
+        if "image_nonce" in ids:
+            return ids["image_nonce"] == nonce
+        if nonce != "00" * 16:
+            return False
+        img = ids.get("image")
+        if img is None:
+            return True
+        st = os.stat(str(path))
+        return [int(st.st_size), int(st.st_mtime_ns)] == [int(v) for v in img]
 
     def loaded_labels(self) -> np.ndarray:
         """Labels of every row the index holds (pyr_index_labels)."""

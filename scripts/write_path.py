@@ -54,7 +54,7 @@ def main():
         head.add_labels(lab[a:a + 65536], x[a:a + 65536], track_ids=False)
     print(f"[write] bulk-loaded {args.base} rows in {time.time() - t:.1f}s", flush=True)
     qs = generate_synthetic(4096, D, 1337)
-    h = C.c_void_p(head._h)
+    h = head._h
     pf, pl = x.ctypes.data, lab.ctypes.data
     checks, add_s = [], 0.0
     t_loop = time.perf_counter()
@@ -117,7 +117,7 @@ def main():
             ub = np.empty((len(q), cap), np.float32)
             lb = np.empty((len(q), cap), np.int64)
             cnt = np.empty(len(q), np.int32)
-            rc = L.pyr_index_debug_candidates(C.c_void_p(ix._h), len(q), cap, ub.ctypes.data_as(C.c_void_p),
+            rc = L.pyr_index_debug_candidates(ix._h, len(q), cap, ub.ctypes.data_as(C.c_void_p),
                                               lb.ctypes.data_as(C.c_void_p), cnt.ctypes.data_as(C.c_void_p))
             emitted = float(cnt.mean()) if rc == 0 else None
             same = None

@@ -309,6 +309,10 @@ def test_rank_memory_plan_list_sharded_m8(hiplib):
     ib0, _ = rank_memory_plan(128, 10_000_000, 8192, 40_000, 80_000, 32, 10)
     assert ib0 < ib < ib0 + 8192 * 512 * 1.5e3   # + the sample store (<= 1.5 kB per sampled row)
     assert ib + wb < 0.25 * hbm, (ib, wb)
+    # and the build peak of that shard (old + new list store, row temporaries) fits as well
+    from pyrope_amd.dist import rank_build_peak_bytes
+    bp = rank_build_peak_bytes(128, 10_000_000, 8192, 40_000)
+    assert 2 * ib0 < bp < 0.25 * hbm
     # the step's buffers grow with the batch; I1 at 8 ranks (nlist 1024) is far smaller
     ib1, wb1 = rank_memory_plan_lists(128, 1_250_000, 1024, 20_000, 10_000, 8, 32, 10)
     assert ib1 + wb1 < ib + wb

@@ -67,7 +67,7 @@ def emitted(hiplib, idx, q, k, opts, nq_cap):
     ub = np.empty((nq, nq_cap), np.float32)
     lab = np.empty((nq, nq_cap), np.int64)
     cnt = np.empty(nq, np.int32)
-    rc = hiplib.pyr_index_debug_candidates(C.c_void_p(idx._h), nq, nq_cap, ub.ctypes.data_as(C.c_void_p),
+    rc = hiplib.pyr_index_debug_candidates(idx._h, nq, nq_cap, ub.ctypes.data_as(C.c_void_p),
                                            lab.ctypes.data_as(C.c_void_p), cnt.ctypes.data_as(C.c_void_p))
     assert rc == 0, hiplib.pyr_last_error()
     assert (cnt <= nq_cap).all()

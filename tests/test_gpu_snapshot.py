@@ -237,6 +237,37 @@ def test_stale_id_map_is_ignored(hiplib, tmp_path):
     assert d.search([0, 0, 1, 0], 1)[0].id == "0"
 
 
+def test_pre_nonce_snapshot_keeps_its_ids(hiplib, tmp_path):
+    """a snapshot written before images carried a nonce (round 3: no T_NONCE section, an .ids map
+    with 'image': [size, mtime_ns] and no 'image_nonce') still loads with its string ids; the same legacy
+    map next to a newer image (which has a nonce) or a changed image is rejected."""
+    import json
+    from pyrope_amd import BruteForceVectorIndex, VectorMetric
+    a = BruteForceVectorIndex(4, VectorMetric.L2)
+    a.add("alpha", [1, 0, 0, 0])
+    a.add("beta", [0, 1, 0, 0])
+    path = str(tmp_path / "old")
+    os.environ["PYR_IMAGE_NO_NONCE"] = "1"
+    try:
+        a.snapshot(path)
+    finally:
+        os.environ.pop("PYR_IMAGE_NO_NONCE", None)
+    m = json.load(open(path + ".ids"))
+    st = os.stat(path)
+    legacy = {"next": m["next"], "image": [st.st_size, st.st_mtime_ns], "ids": m["ids"]}
+    json.dump(legacy, open(path + ".ids", "w"))
+    c = BruteForceVectorIndex(4, VectorMetric.L2)
+    c.load(path)
+    assert c.search([0, 1, 0, 0], 1)[0].id == "beta"
+    # the legacy map beside an image with a nonce: rejected
+    a.snapshot(path)
+    json.dump(legacy, open(path + ".ids", "w"))
+    d = BruteForceVectorIndex(4, VectorMetric.L2)
+    with pytest.warns(RuntimeWarning, match="nonce"):
+        d.load(path)
+    assert d.search([0, 1, 0, 0], 1)[0].id == "1"
+
+
 def test_corrupt_images_raise_format_errors(hiplib, tmp_path):
     """centroids that are not whole rows, and section sizes running past the end of the
     file (including sizes that would wrap the offset), are rejected as malformed images."""
