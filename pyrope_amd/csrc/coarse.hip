@@ -368,6 +368,46 @@ __device__ __forceinline__ float exact_cs_l8(const float *qp, const float *cp, i
   return MET == L2 ? -sum : sum;
 }
 
+// the same for two centroids at once (two independent accumulation chains per lane: twice the work per
+// dependent step); each result is bit for bit exact_cs_l8's
+template <int MET, int DT = 0>
+__device__ __forceinline__ void exact_cs_l8x2(const float *qp, const float *ca, const float *cb, int Dr, int j,
+                                              float &ra, float &rb) {
+  const int D = DT > 0 ? DT : Dr;
+  constexpr int U = DT > 0 ? DT / 8 : 4;
+  float acc = 0.0f, bcc = 0.0f;
+#pragma unroll U
+  for (int d = j; d < (D & ~7); d += 8) {
+    const float x = qp[d];
+    if (MET == L2) {
+      const float t = x - ca[d], v = x - cb[d];
+      acc = acc + t * t;
+      bcc = bcc + v * v;
+    } else {
+      acc = acc + x * ca[d];
+      bcc = bcc + x * cb[d];
+    }
+  }
+  acc = acc + __shfl_xor(acc, 1);
+  bcc = bcc + __shfl_xor(bcc, 1);
+  acc = acc + __shfl_xor(acc, 2);
+  bcc = bcc + __shfl_xor(bcc, 2);
+  float sa = (D & ~7) > 0 ? 0.0f + (acc + __shfl_xor(acc, 4)) : 0.0f;
+  float sb = (D & ~7) > 0 ? 0.0f + (bcc + __shfl_xor(bcc, 4)) : 0.0f;
+  for (int d = D & ~7; d < D; ++d) {
+    if (MET == L2) {
+      const float t = qp[d] - ca[d], v = qp[d] - cb[d];
+      sa = sa + t * t;
+      sb = sb + v * v;
+    } else {
+      sa = sa + qp[d] * ca[d];
+      sb = sb + qp[d] * cb[d];
+    }
+  }
+  ra = MET == L2 ? -sa : sa;
+  rb = MET == L2 ? -sb : sb;
+}
+
 __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
   const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src);
   return ((uint64_t)hi << 32) | lo;
@@ -403,18 +443,17 @@ __device__ __forceinline__ uint64_t sort64_desc(uint64_t v, int lane) {
 
 // One wave per query: aP = the nprobe-th largest approximate score (wselect.h radix select over score
 // keys), the candidates = every centroid whose approximate
-// score reaches aP - 2E (at most PICK_MAX = 256, in index order), their exact ComputeScore and the first
+// score reaches aP - 2E (at most PICK_MAX = 1024, in index order), their exact ComputeScore and the first
 // nprobe of them by (score desc, index asc).  Every centroid left out scores exactly below the nprobe
-// centroids whose approximate score reached aP.  More than 256 candidates (d = 768 widens 2E: P1 at
-// nprobe = 64 keeps ~100), or a non-finite query: the exact scores of every centroid go to the row and
-// the query to the fail list (coarse_select_list_kernel).
+// centroids whose approximate score reached aP.  More than 1024 candidates, or a non-finite query: the
+// exact scores of every centroid go to the row and the query to the fail list (coarse_select_list_kernel).
 template <int MET, int DT>
 __global__ __launch_bounds__(256) void coarse_pick_kernel(const float *q, const float *c, float *scores, int64_t nq,
                                                           int nc, int Dr, int P, double cnmax, double c_err,
                                                           int32_t *probes, int32_t *fail, int32_t *nfail) {
   const int D = DT > 0 ? DT : Dr;
   __shared__ int hist[4][256];
-  constexpr int PICK_MAX = 256;
+  constexpr int PICK_MAX = 1024;  // (d = 768 widens 2E: P1 keeps a few hundred)
   __shared__ int cl[4][PICK_MAX];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t qi = (int64_t)blockIdx.x * 4 + w;
@@ -467,12 +506,13 @@ __global__ __launch_bounds__(256) void coarse_pick_kernel(const float *q, const 
       const int m = min(64, n - b0);
       const int cid = lane < m ? cl[w][b0 + lane] : -1;
       float sc = -INFINITY;
-      for (int p = 0; 8 * p < m; ++p) {
-        const int cc = 8 * p + (lane >> 3);
-        const int id = __shfl(cid, cc);
-        const float v = exact_cs_l8<MET, DT>(qp, c + (size_t)max(id, 0) * D, D, lane & 7);
-        const float t = __shfl(v, 8 * (lane & 7));
-        if ((lane >> 3) == p) sc = t;  // lane 8p + g took candidate 8p + g's score from group g
+      for (int p = 0; 8 * p < m; p += 2) {  // passes p and p + 1 together (two chains per lane)
+        const int ia = __shfl(cid, 8 * p + (lane >> 3)), ib = __shfl(cid, min(63, 8 * (p + 1) + (lane >> 3)));
+        float va, vb;
+        exact_cs_l8x2<MET, DT>(qp, c + (size_t)max(ia, 0) * D, c + (size_t)max(ib, 0) * D, D, lane & 7, va, vb);
+        const float ta = __shfl(va, 8 * (lane & 7)), tb = __shfl(vb, 8 * (lane & 7));
+        if ((lane >> 3) == p) sc = ta;  // lane 8p + g took candidate 8p + g's score from group g
+        if ((lane >> 3) == p + 1) sc = tb;
       }
       uint64_t key = cid >= 0 ? rank_key(sc, cid) : 0ull;
       key = sort64_desc(key, lane);

@@ -253,12 +253,12 @@ void RowStore::recenter(hipStream_t st) {
 }
 
 bool RowStore::write(const float *x, const int64_t *slots, const int64_t *labs, int64_t cnt, hipStream_t st,
-                     DevMem &stage_x, DevMem &stage_i, bool x_dev, uint8_t *q8ok) {
+                     DevMem &stage_x, DevMem &stage_i, bool x_dev, uint8_t *q8ok, bool need_slots) {
   if (cnt <= 0) return true;
   ++gen;
   // small-batch path: the rows' largest |x_i| (of x - center) is taken on the host, so the scale decision
   // needs no device read-back; one pinned copy, one fused kernel, no synchronization
-  if (!x_dev && cnt <= small_write_rows() && (!f16 || (sx > 0.0f && (center16 ? resid : !resid)))) {
+  if (!x_dev && !need_slots && cnt <= small_write_rows() && (!f16 || (sx > 0.0f && (center16 ? resid : !resid)))) {
     float am = 0.0f;
     if (f16)
       for (int64_t i = 0; i < cnt; i++)
@@ -1113,7 +1113,7 @@ struct FlatIndex : Index {
     const bool small = !quant && !unit && st.write(x, slots.data(), labels, n, wst, stage_x, stage_i, false,
                                                    q8ok.as<uint8_t>());
     if (!small) {
-      if (quant || unit) st.write(x, slots.data(), labels, n, wst, stage_x, stage_i);
+      if (quant || unit) st.write(x, slots.data(), labels, n, wst, stage_x, stage_i, false, nullptr, true);
       // (stage_i holds the device copy of the slots)
       if (quant)
         launch_sq8_quantize(st.rows.as<float>(), stage_i.as<int64_t>(), 1, n, dim, dp, 1, q8.as<uint8_t>(),

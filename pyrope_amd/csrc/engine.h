@@ -124,8 +124,9 @@ struct RowStore {
   // Returns true when the small-batch path took the write (host rows, <= SMALL_WRITE rows, the fp16 scale
   // unchanged): one pinned staging copy + one fused kernel, no host synchronization and no use of stage_i;
   // otherwise the bulk path ran (stage_i then holds the device slots) and st is synchronized.
+  // (need_slots: the caller reads stage_i afterwards -- the bulk path always)
   bool write(const float *x, const int64_t *slots, const int64_t *labs, int64_t cnt, hipStream_t st,
-             DevMem &stage_x, DevMem &stage_i, bool x_dev = false, uint8_t *q8ok = nullptr);
+             DevMem &stage_x, DevMem &stage_i, bool x_dev = false, uint8_t *q8ok = nullptr, bool need_slots = false);
   void set_live(const std::vector<int64_t> &slots, uint8_t v, hipStream_t st, DevMem &stage);
   // fp16 copy of slots (device list, or [0, cap) when null) with the current scale; raises the
   // scale (and re-encodes every slot) when a row exceeds it.  Synchronizes st.

@@ -51,11 +51,13 @@ def main():
     head.reserve(total)
     t = time.time()
     for a in range(0, args.base, 65536):
-        head.add_labels(lab[a:a + 65536], x[a:a + 65536], track_ids=False)
+        e = min(args.base, a + 65536)
+        head.add_labels(lab[a:e], x[a:e], track_ids=False)
     print(f"[write] bulk-loaded {args.base} rows in {time.time() - t:.1f}s", flush=True)
     qs = generate_synthetic(4096, D, 1337)
     h = head._h
     pf, pl = x.ctypes.data, lab.ctypes.data
+    FP, LP = C.POINTER(C.c_float), C.POINTER(C.c_int64)
     checks, add_s = [], 0.0
     t_loop = time.perf_counter()
     qi = 0
@@ -63,7 +65,7 @@ def main():
         e = min(total, a + args.every)
         t0 = time.perf_counter()
         for i in range(a, e):  # one row per call, as VEC.ADD issues them
-            rc = L.pyr_index_add(h, C.c_void_p(pf + i * D * 4), 1, C.c_void_p(pl + i * 8))
+            rc = L.pyr_index_add(h, C.cast(pf + i * D * 4, FP), 1, C.cast(pl + i * 8, LP))
             if rc:
                 raise RuntimeError(L.pyr_last_error())
         add_s += time.perf_counter() - t0
