@@ -138,9 +138,21 @@ static pyr_status write_op(pyr_index *index, const float *x, int64_t n, const in
   return guard([&] {
     HIPCHK(hipSetDevice(index->impl->device));
     std::unique_lock<std::shared_mutex> g(index->impl->mu);
+    const bool prof = pyr::wprof_on();
+    auto t0 = std::chrono::steady_clock::now();
+    auto lap = [&](int sec) {
+      if (!prof) return;
+      const auto t1 = std::chrono::steady_clock::now();
+      pyr::wprof_add(sec, std::chrono::duration<double>(t1 - t0).count());
+      t0 = t1;
+    };
     if (n > 0) index->impl->add(x, n, labels, upsert);
+    lap(5);
     index->impl->after_write();
+    lap(6);
     index->impl->note_write();
+    lap(7);
+    pyr::note_write_call();
   });
 }
 

@@ -190,35 +190,71 @@ void RowStore::encode16(const int64_t *d_slots, int64_t cnt, hipStream_t st) {
   HIPCHK(hipStreamSynchronize(st));
 }
 
+// Slots are mapped host memory the write kernel reads in place (no copy call).  An event closes every group
+// of G slots; a group is reused only once its event (K writes ago) has completed.
 char *PinnedRing::take(size_t need, int *slot) {
-  if (need > bytes) {  // (re)allocate every slot: wait for their copies first
+  constexpr int G = 8;
+  if (need > bytes) {  // (re)allocate every slot: wait for their readers first
+    for (int g = 0; g < K / G; ++g)
+      if (ev[g]) HIPCHK(hipEventSynchronize(ev[g]));
     for (int i = 0; i < K; ++i) {
-      if (ev[i]) HIPCHK(hipEventSynchronize(ev[i]));
       if (host[i]) HIPCHK(hipHostFree(host[i]));
       host[i] = nullptr;
     }
     bytes = std::max<size_t>(need, 4096);
     for (int i = 0; i < K; ++i) {
-      HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&host[i]), bytes, hipHostMallocDefault));
-      if (!ev[i]) HIPCHK(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+      HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&host[i]), bytes, hipHostMallocMapped));
+      HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&dev[i]), host[i], 0));
     }
+    for (int g = 0; g < K / G; ++g)
+      if (!ev[g]) HIPCHK(hipEventCreateWithFlags(&ev[g], hipEventDisableTiming));
     next = 0;
   }
   const int i = next;
   next = (next + 1) % K;
-  HIPCHK(hipEventSynchronize(ev[i]));  // its previous copy has run (normally long ago)
+  if (i % G == 0) HIPCHK(hipEventSynchronize(ev[i / G]));  // the group's readers have run (normally long ago)
   *slot = i;
   return host[i];
 }
-void PinnedRing::done(int slot, hipStream_t st) { HIPCHK(hipEventRecord(ev[slot], st)); }
+void PinnedRing::done(int slot, hipStream_t st) {
+  if (slot % 8 == 7) HIPCHK(hipEventRecord(ev[slot / 8], st));
+}
 PinnedRing::~PinnedRing() {
-  for (int i = 0; i < K; ++i) {
-    if (ev[i]) {
-      (void)hipEventSynchronize(ev[i]);
-      (void)hipEventDestroy(ev[i]);
-    }
-    if (host[i]) (void)hipHostFree(host[i]);
+  for (int i = 0; i < K; ++i)
+    if (host[i]) (void)hipHostFree(host[i]);  // (hipHostFree waits for the device)
+  for (int g = 0; g < K; ++g)
+    if (ev[g]) (void)hipEventDestroy(ev[g]);
+}
+
+// measurement only (PYR_WRITE_PROF=1): host time of the write path's sections, printed at exit
+struct WriteProf {
+  bool on = getenv("PYR_WRITE_PROF") != nullptr;
+  double t[8] = {};
+  int64_t n = 0;
+  ~WriteProf() {
+    if (on && n)
+      fprintf(stderr, "[write prof] %lld calls, us per call: prep %.2f amax %.2f stage %.2f launch %.2f done %.2f add-host %.2f after %.2f note %.2f\n",
+              (long long)n, 1e6 * t[0] / n, 1e6 * t[1] / n, 1e6 * t[2] / n, 1e6 * t[3] / n, 1e6 * t[4] / n,
+              1e6 * t[5] / n, 1e6 * t[6] / n, 1e6 * t[7] / n);
   }
+};
+static WriteProf &wprof() {
+  static WriteProf p;
+  return p;
+}
+struct WSec {
+  int i;
+  std::chrono::steady_clock::time_point t0;
+  explicit WSec(int s) : i(s), t0(wprof().on ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point()) {}
+  ~WSec() {
+    if (wprof().on) wprof().t[i] += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+};
+
+bool wprof_on() { return wprof().on; }
+void wprof_add(int i, double sec) { wprof().t[i] += sec; }
+void note_write_call() {
+  if (wprof().on) ++wprof().n;
 }
 
 // rows a write may take through the small-batch path (RowStore::write)
@@ -255,11 +291,13 @@ void RowStore::recenter(hipStream_t st) {
 bool RowStore::write(const float *x, const int64_t *slots, const int64_t *labs, int64_t cnt, hipStream_t st,
                      DevMem &stage_x, DevMem &stage_i, bool x_dev, uint8_t *q8ok, bool need_slots) {
   if (cnt <= 0) return true;
+  const uint64_t g0 = gen;
   ++gen;
   // small-batch path: the rows' largest |x_i| (of x - center) is taken on the host, so the scale decision
   // needs no device read-back; one pinned copy, one fused kernel, no synchronization
   if (!x_dev && !need_slots && cnt <= small_write_rows() && (!f16 || (sx > 0.0f && (center16 ? resid : !resid)))) {
     float am = 0.0f;
+    WSec sec_am(1);
     if (f16)
       for (int64_t i = 0; i < cnt; i++)
         for (int d = 0; d < dim; d++) {
@@ -268,18 +306,25 @@ bool RowStore::write(const float *x, const int64_t *slots, const int64_t *labs, 
         }
     if (!f16 || std::max(am, amax) * sx < 16384.0f) {
       const size_t xb = sizeof(float) * cnt * dim, ib = sizeof(int64_t) * cnt;
-      int slot;
-      char *h = ring.take(xb + 2 * ib, &slot);
-      std::memcpy(h, x, xb);
-      std::memcpy(h + xb, slots, ib);
-      std::memcpy(h + xb + ib, labs, ib);
-      stage_x.ensure(xb + 2 * ib);
-      HIPCHK(hipMemcpyAsync(stage_x.p, h, xb + 2 * ib, hipMemcpyHostToDevice, st));
-      ring.done(slot, st);
+      int slot = -1;
+      WSec sec_st(2);
       SmallWriteArgs a{};
-      a.x = stage_x.as<float>();
-      a.slots = reinterpret_cast<const int64_t *>(stage_x.as<char>() + xb);
-      a.labs = a.slots + cnt;
+      SmallWriteRows inl;
+      const bool inline_rows = cnt <= SMALL_INLINE_ROWS && cnt * dim <= SMALL_INLINE_FLOATS;
+      if (inline_rows) {  // the rows travel as kernel arguments
+        std::memcpy(inl.x, x, xb);
+        std::memcpy(inl.slot, slots, ib);
+        std::memcpy(inl.lab, labs, ib);
+      } else {  // the kernel reads a mapped host slot in place
+        char *h = ring.take(xb + 2 * ib, &slot);
+        std::memcpy(h, x, xb);
+        std::memcpy(h + xb, slots, ib);
+        std::memcpy(h + xb + ib, labs, ib);
+        const char *dh = ring.dev[slot];
+        a.x = reinterpret_cast<const float *>(dh);
+        a.slots = reinterpret_cast<const int64_t *>(dh + xb);
+        a.labs = a.slots + cnt;
+      }
       a.cnt = (int32_t)cnt;
       a.dim = dim;
       a.dp = tdim();
@@ -301,8 +346,22 @@ bool RowStore::write(const float *x, const int64_t *slots, const int64_t *labs, 
         amax = std::max(am, amax);
       }
       a.q8ok = q8ok;
-      launch_write_small(a, st);
-      HIPCHK(hipGetLastError());
+      // the cached per-row terms stay current: the kernel writes these rows' terms too
+      const bool mub_ok = f16 && mub_gen == g0 && mub.n >= sizeof(float) * cap;
+      if (mub_ok) {
+        a.mub = mub.as<float>();
+        a.mkr = mub_kr;
+        a.mkx = mub_kx;
+        a.mmet = mub_met;
+      }
+      {
+        WSec sec_l(3);
+        launch_write_small(a, st, inline_rows ? &inl : nullptr);
+        HIPCHK(hipGetLastError());
+      }
+      WSec sec_d(4);
+      if (slot >= 0) ring.done(slot, st);
+      if (mub_ok) mub_gen = gen;
       return true;
     }
   }
@@ -1052,7 +1111,7 @@ struct FlatIndex : Index {
   // hipGraph capture of one -- right after a write then finds them current; FlatIndex::stream_slice's
   // constants)
   void after_write() override {
-    if (st.f16 && st.cap > 0 && st.sx > 0.0f) {
+    if (st.f16 && st.cap > 0 && st.sx > 0.0f && st.mub_gen != st.gen) {  // (small writes keep them current)
       StreamArgs sa{};
       const int dt = st.tdim();
       stream_ub_terms(dt, metric, filter_f16_cerr(dt, metric, FILTER_F16X1), filter_cerr(dt),
@@ -1084,21 +1143,28 @@ struct FlatIndex : Index {
 
   void add(const float *x, int64_t n, const int64_t *labels, bool upsert) override {
     std::vector<int64_t> slots(n);
-    if (!upsert) {  // :141-144 duplicate id -> InvalidOperationException
-      std::unordered_map<int64_t, int> seen;
-      for (int64_t i = 0; i < n; i++)
-        if (slot_of.count(labels[i]) || seen[labels[i]]++)
-          throw Error(PYR_E_DUPLICATE, "Vector with id '" + std::to_string(labels[i]) + "' already exists.");
-    }
     int64_t next = st.n;
-    std::unordered_map<int64_t, int64_t> batch;
-    for (int64_t i = 0; i < n; i++) {
-      auto f = slot_of.find(labels[i]);
-      if (f != slot_of.end()) slots[i] = f->second;        // :193-210 update in place
-      else {
-        auto b = batch.find(labels[i]);
-        slots[i] = b != batch.end() ? b->second : next++;  // :151-179 append slot
-        batch[labels[i]] = slots[i];
+    if (n == 1) {  // VEC.ADD's granularity: no per-call maps
+      auto f = slot_of.find(labels[0]);
+      if (f != slot_of.end() && !upsert)
+        throw Error(PYR_E_DUPLICATE, "Vector with id '" + std::to_string(labels[0]) + "' already exists.");
+      slots[0] = f != slot_of.end() ? f->second : next++;
+    } else {
+      if (!upsert) {  // :141-144 duplicate id -> InvalidOperationException
+        std::unordered_map<int64_t, int> seen;
+        for (int64_t i = 0; i < n; i++)
+          if (slot_of.count(labels[i]) || seen[labels[i]]++)
+            throw Error(PYR_E_DUPLICATE, "Vector with id '" + std::to_string(labels[i]) + "' already exists.");
+      }
+      std::unordered_map<int64_t, int64_t> batch;
+      for (int64_t i = 0; i < n; i++) {
+        auto f = slot_of.find(labels[i]);
+        if (f != slot_of.end()) slots[i] = f->second;        // :193-210 update in place
+        else {
+          auto b = batch.find(labels[i]);
+          slots[i] = b != batch.end() ? b->second : next++;  // :151-179 append slot
+          batch[labels[i]] = slots[i];
+        }
       }
     }
     std::vector<float> xs;

@@ -50,12 +50,14 @@ struct DevMem {
   }
 };
 
-// Pinned host staging for small writes: K slots, each reusable once the copy that read it has run (an
-// event per slot), so a write never waits for the device (RowStore::write's small-batch path).
+// Pinned (mapped) host staging for small writes: K slots the write kernel reads in place, reused in groups of
+// 8 once the group's event has completed, so a write never waits for the device (RowStore::write's
+// small-batch path).
 struct PinnedRing {
   static constexpr int K = 64;
   char *host[K] = {};
-  hipEvent_t ev[K] = {};
+  char *dev[K] = {};      // the slots' device addresses (hipHostGetDevicePointer)
+  hipEvent_t ev[K] = {};  // (the first K / 8: one per group)
   size_t bytes = 0;
   int next = 0;
   // a slot of at least `need` bytes whose previous copy has completed; *slot = its index
@@ -148,6 +150,11 @@ struct RowStore {
 // (engine.cpp; pyr_ivf_memory_plan)
 void ivf_memory_plan(int dim, int64_t nrows, int nlist, int64_t max_len, int64_t nq, int nprobe, int k,
                      int64_t *index_bytes, int64_t *workspace_bytes);
+
+// measurement only (PYR_WRITE_PROF=1): the write path's host time by section (engine.cpp WriteProf)
+bool wprof_on();
+void wprof_add(int section, double seconds);
+void note_write_call();
 
 struct Workspace {
   hipStream_t st = nullptr;

@@ -408,7 +408,20 @@ __global__ __launch_bounds__(256) void merge_refine_kernel(CandMergeArgs m, Refi
   const int lane = threadIdx.x & 63;
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= a.nq) return;
-  const uint64_t cur = cand_merge_wave<STREAM_KO>(m, q, lane);
+  // fewer emitted rows than K1 and none dropped (a list-sharded rank holds a few of most queries' rows):
+  // they all sit within depth K1 whatever their order, the rest of the list is the floor -- no sort
+  uint64_t cur;
+  const int tot0 = m.cand_n[q];
+  if (tot0 < a.k1 && m.cand_f[q] == 0u) {
+    const float F = m.thr ? m.thr[q] : -INFINITY;
+    cur = F > -INFINITY ? pack_cand(F, KEY_FLOOR) : 0ull;
+    if (lane < tot0) {
+      const uint2 e = m.cand[(size_t)q * m.cap + lane];
+      cur = pack_cand(__uint_as_float(e.x), e.y);
+    }
+  } else {
+    cur = cand_merge_wave<STREAM_KO>(m, q, lane);
+  }
   const uint32_t kk = ~(uint32_t)cur;
   const float msl = cur != 0ull ? key_score((uint32_t)(cur >> 32)) : -INFINITY;   // lane j: ms[j]
   const int32_t mkl = cur == 0ull ? -1 : (kk == KEY_FLOOR ? -2 : (int32_t)kk);    // lane j: mk[j]

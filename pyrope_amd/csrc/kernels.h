@@ -658,8 +658,18 @@ struct SmallWriteArgs {
   float *meta;
   int32_t met16;
   uint8_t *q8ok;         // FLAT: the slot's 8-bit codes are invalid now (null: untouched)
+  float *mub;            // the stream scan's cached per-row terms (RowStore::row_terms), kept current for these
+  float mkr, mkx;        // rows with its constants (null: the cache is stale anyway)
+  int32_t mmet;
 };
-void launch_write_small(const SmallWriteArgs &a, hipStream_t st);
+// the rows themselves as kernel arguments (a.x == null): a host write never stages through pinned memory
+// (CPU stores into it measured ~22 us per 528 B row)
+constexpr int SMALL_INLINE_FLOATS = 832, SMALL_INLINE_ROWS = 8;
+struct SmallWriteRows {
+  float x[SMALL_INLINE_FLOATS];
+  int64_t slot[SMALL_INLINE_ROWS], lab[SMALL_INLINE_ROWS];
+};
+void launch_write_small(const SmallWriteArgs &a, hipStream_t st, const SmallWriteRows *rows = nullptr);
 // per-dimension sums (fp64) of the live rows among [0, n) of a blocked store and their count -> sums[dim],
 // *count (both zeroed by the caller): the FLAT L2 tiles' re-centring (RowStore::recenter)
 void launch_live_sums(const float *rows, const uint8_t *live, int64_t n, int32_t dim, double *sums,

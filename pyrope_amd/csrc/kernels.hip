@@ -1827,10 +1827,10 @@ void launch_scatter_u8(uint8_t *dst, const int64_t *idx, uint8_t v, int64_t n, h
   hipLaunchKernelGGL(scatter_u8_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, dst, idx, v, n);
 }
 namespace {
-__global__ __launch_bounds__(64) void write_small_kernel(SmallWriteArgs a) {
+__global__ __launch_bounds__(64) void write_small_kernel(SmallWriteArgs a, SmallWriteRows inl) {
   const int i = blockIdx.x, lane = threadIdx.x, D = a.dim;
-  const int64_t r = a.slots[i];
-  const float *xs = a.x + (size_t)i * D;
+  const int64_t r = a.x ? a.slots[i] : inl.slot[i];
+  const float *xs = a.x ? a.x + (size_t)i * D : inl.x + (size_t)i * D;
   for (int d = lane; d < D; d += 64) {
     const float v = xs[d];
     a.rows[blk_off(r, d, D)] = v;
@@ -1851,7 +1851,7 @@ __global__ __launch_bounds__(64) void write_small_kernel(SmallWriteArgs a) {
       a.rsq16[r] = s16;
       if (isfinite(s16)) atomicMax(a.rmax_r, score_key(s16));
     }
-    a.labels[r] = a.labs[i];
+    a.labels[r] = a.x ? a.labs[i] : inl.lab[i];
     a.live[r] = 1;
     if (a.q8ok) a.q8ok[r] = 0;
   }
@@ -1872,7 +1872,15 @@ __global__ __launch_bounds__(64) void write_small_kernel(SmallWriteArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = v[j];
   }
-  if (lane == 0) a.meta[r] = isnan(rn) ? -INFINITY : isinf(rn) ? INFINITY : (a.met16 == L2 ? -rn : 0.0f);
+  if (lane == 0) {
+    const float mt = isnan(rn) ? -INFINITY : isinf(rn) ? INFINITY : (a.met16 == L2 ? -rn : 0.0f);
+    a.meta[r] = mt;
+    if (a.mub) {  // row_terms_kernel (sample16.hip) for this row
+      float v = fmaf(a.mkr, rn, mt);
+      if (a.mmet == IP) v = fmaf(a.mkx, s, v);
+      a.mub[r] = v;
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void live_sums_kernel(const float *rows, const uint8_t *live, int64_t n, int D,
@@ -1897,9 +1905,10 @@ __global__ __launch_bounds__(256) void live_sums_kernel(const float *rows, const
 }
 }  // namespace
 
-void launch_write_small(const SmallWriteArgs &a, hipStream_t st) {
+void launch_write_small(const SmallWriteArgs &a, hipStream_t st, const SmallWriteRows *rows) {
   if (a.cnt <= 0) return;
-  hipLaunchKernelGGL(write_small_kernel, dim3((unsigned)a.cnt), dim3(64), 0, st, a);
+  static const SmallWriteRows none{};
+  hipLaunchKernelGGL(write_small_kernel, dim3((unsigned)a.cnt), dim3(64), 0, st, a, rows ? *rows : none);
 }
 void launch_live_sums(const float *rows, const uint8_t *live, int64_t n, int32_t dim, double *sums,
                       unsigned long long *count, hipStream_t st) {
