@@ -295,7 +295,8 @@ bool RowStore::write(const float *x, const int64_t *slots, const int64_t *labs, 
   ++gen;
   // small-batch path: the rows' largest |x_i| (of x - center) is taken on the host, so the scale decision
   // needs no device read-back; one pinned copy, one fused kernel, no synchronization
-  if (!x_dev && !need_slots && cnt <= small_write_rows() && (!f16 || (sx > 0.0f && (center16 ? resid : !resid)))) {
+  if (!x_dev && !need_slots && cnt <= small_write_rows() && dim <= SMALL_WRITE_MAX_DIM &&
+      (!f16 || (sx > 0.0f && (center16 ? resid : !resid)))) {
     float am = 0.0f;
     WSec sec_am(1);
     if (f16)

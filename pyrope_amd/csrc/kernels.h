@@ -664,7 +664,7 @@ struct SmallWriteArgs {
 };
 // the rows themselves as kernel arguments (a.x == null): a host write never stages through pinned memory
 // (CPU stores into it measured ~22 us per 528 B row)
-constexpr int SMALL_INLINE_FLOATS = 832, SMALL_INLINE_ROWS = 8;
+constexpr int SMALL_INLINE_FLOATS = 832, SMALL_INLINE_ROWS = 8, SMALL_WRITE_MAX_DIM = 4096;
 struct SmallWriteRows {
   float x[SMALL_INLINE_FLOATS];
   int64_t slot[SMALL_INLINE_ROWS], lab[SMALL_INLINE_ROWS];

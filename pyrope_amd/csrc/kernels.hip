@@ -1828,14 +1828,20 @@ void launch_scatter_u8(uint8_t *dst, const int64_t *idx, uint8_t v, int64_t n, h
 }
 namespace {
 __global__ __launch_bounds__(64) void write_small_kernel(SmallWriteArgs a, SmallWriteRows inl) {
+  // the row comes from host-coherent memory (kernel arguments or a mapped host slot): one coalesced read of
+  // it into LDS, every later pass reads LDS (a lane's sequential loop over host memory took ~20 us)
+  __shared__ float xsh[SMALL_WRITE_MAX_DIM];
   const int i = blockIdx.x, lane = threadIdx.x, D = a.dim;
   const int64_t r = a.x ? a.slots[i] : inl.slot[i];
-  const float *xs = a.x ? a.x + (size_t)i * D : inl.x + (size_t)i * D;
+  const float *xg = a.x ? a.x + (size_t)i * D : inl.x + (size_t)i * D;
   for (int d = lane; d < D; d += 64) {
-    const float v = xs[d];
+    const float v = xg[d];
+    xsh[d] = v;
     a.rows[blk_off(r, d, D)] = v;
     if (a.rrm) a.rrm[(size_t)r * D + d] = v;
   }
+  __syncthreads();
+  const float *xs = xsh;
   float s = 0.0f, s16 = 0.0f;
   if (lane == 0) {
     for (int d = 0; d < D; ++d) s = s + xs[d] * xs[d];  // sqnorms_kernel's order (filter.hip)
