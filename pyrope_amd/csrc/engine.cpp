@@ -1400,6 +1400,9 @@ struct FlatIndex : Index {
     sa.items = ws.items.as<ScanItem>();
     sa.n_items = ws.nitems.as<int32_t>();
     sa.qlist = ws.qlist.as<int32_t>();
+    sa.qpos = ws.qpos.as<int32_t>();  // (build_ivf_items: every probe of every query)
+    sa.probes = ws.probes.as<int32_t>();
+    sa.nq = nq;
     sa.nparts = nparts;
     sa.nprobe = probes;
     sa.cmax = 1;
@@ -1864,10 +1867,12 @@ static int build_ivf_items(Workspace &ws, int64_t nq, int nprobe, int nparts, in
   ws.ivf_qoff.ensure(sizeof(int32_t) * (nlist + 1));
   ws.ivf_ioff.ensure(sizeof(int32_t) * (nlist + 1));
   ws.qlist.ensure(sizeof(int32_t) * std::max<int64_t>(nq * nprobe, 1));
+  ws.qpos.ensure(sizeof(int32_t) * std::max<int64_t>(nq * nprobe, 1));
   items.ensure(sizeof(ScanItem) * std::max(maxi, 1));
   nitems.ensure(sizeof(int32_t) * 16);  // the count, then (IvfChunking::xcd) the 9 queue bounds
   IvfItemWs iw{ws.ivf_cnt.as<int32_t>(), ws.ivf_fill.as<int32_t>(), ws.ivf_qoff.as<int32_t>(),
-               ws.ivf_ioff.as<int32_t>(), ws.qlist.as<int32_t>(), items.as<ScanItem>(), nitems.as<int32_t>()};
+               ws.ivf_ioff.as<int32_t>(), ws.qlist.as<int32_t>(), items.as<ScanItem>(), nitems.as<int32_t>(),
+               ws.qpos.as<int32_t>()};
   launch_ivf_items(ws.probes.as<int32_t>(), nq, nprobe, nparts, nlist, lbeg.as<int32_t>(), lend.as<int32_t>(), qchunk,
                    ch, phase, iw, ws.st, 0, -1, balance, zeroed);
   return maxi;
@@ -2396,6 +2401,9 @@ struct IvfFlatIndex : Index {
     sa.items = ws.items.as<ScanItem>();
     sa.n_items = ws.nitems.as<int32_t>();
     sa.qlist = ws.qlist.as<int32_t>();
+    sa.qpos = ws.qpos.as<int32_t>();  // (build_ivf_items: every probe of every query)
+    sa.probes = ws.probes.as<int32_t>();
+    sa.nq = nq;
     sa.nparts = nparts;
     sa.nprobe = probes;
     sa.cmax = ch.cmax;

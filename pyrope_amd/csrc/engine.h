@@ -165,7 +165,7 @@ struct Workspace {
   DevMem q, qn, qt, items, nitems, items2, nitems2, items3, nitems3, qlist, part_s, part_k, probes, cpart_s, cpart_k,
       limits;
   DevMem ivf_cnt, ivf_fill, ivf_qoff, ivf_ioff, gthr;
-  DevMem ivf_cnt2, ivf_fill2, ivf_qoff2, ivf_ioff2, qlist2;  // second item set (nearest-list seeding)
+  DevMem ivf_cnt2, ivf_fill2, ivf_qoff2, ivf_ioff2, qlist2, qpos;  // second item set (nearest-list seeding)
   DevMem out_s, out_l, out_c;
   DevMem ms, mk, fail, fail_cnt, fq, fs, fl, fc;  // MFMA filter: merged candidates, certificate failures
   DevMem fprobes;                                 // probe lists of the failing queries (IVF_PQ LUT re-run)

@@ -202,6 +202,7 @@ struct IvfItemWs {
   int32_t *qlist;     // nq * nprobe
   ScanItem *items;    // max_items
   int32_t *n_items;   // 1
+  int32_t *qpos = nullptr;  // or [nq][nprobe]: the qlist position of (query, probe) (all probes only)
 };
 // Item list of one launch phase: phase 0 = chunk 0 of every list (all chunks when
 // ch.warm == 0), phase 1 = chunks >= 1 (only with ch.warm > 0).  Phase 0 also builds
@@ -357,6 +358,10 @@ struct StreamArgs {
   float kr, kx, kq, kqa, kqc;
   const float *mub;           // per row meta + E_row (RowStore::row_terms)
   unsigned long long *tdbg;   // measurement only (PYR_STREAM_TIMING=1): per-wave cycle buckets, or null
+  // [q][nprobe] the qlist position of (query, probe), every probe of every query (IvfItemWs::qpos), or null:
+  // then sprep builds the operands query-major (sample16.hip); nq its query count
+  const int32_t *qpos;
+  int64_t nq;
 };
 // per row the stream scan's additive term: meta + kr |x - c|^2 (+ kx |x|^2, IP): fmaf(kr, rsq16, meta),
 // then fmaf(kx, rsq, .)

@@ -644,7 +644,8 @@ __global__ __launch_bounds__(256) void ivf_count_lds_kernel(const int32_t *probe
 
 __global__ __launch_bounds__(256) void ivf_fill_lds_kernel(const int32_t *probes, int64_t nq, int nprobe, int pb,
                                                            int pe, int nparts, int cmax, int nlist,
-                                                           const int32_t *qoff, int32_t *fill, int32_t *qlist) {
+                                                           const int32_t *qoff, int32_t *fill, int32_t *qlist,
+                                                           int32_t *qpos) {
   extern __shared__ int hist[];
   const int np = pe - pb;
   const int64_t n = nq * np, e0 = (int64_t)blockIdx.x * IVF_EPB;
@@ -668,6 +669,7 @@ __global__ __launch_bounds__(256) void ivf_fill_lds_kernel(const int32_t *probes
     const int64_t q = i / np;
     const int p = pb + (int)(i % np);
     qlist[hist[lst[j]] + rank[j]] = (int32_t)(q * nparts + p * cmax);  // chunk c adds c (ScanItem.part)
+    if (qpos) qpos[q * nprobe + p] = hist[lst[j]] + rank[j];
   }
 }
 
@@ -752,7 +754,7 @@ __global__ __launch_bounds__(1024) void ivf_scan_kernel(const int32_t *cnt, int 
 }
 
 __global__ void ivf_fill_kernel(const int32_t *probes, int64_t nq, int nprobe, int pb, int pe, int nparts, int cmax,
-                                const int32_t *qoff, int32_t *fill, int32_t *qlist) {
+                                const int32_t *qoff, int32_t *fill, int32_t *qlist, int32_t *qpos) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int np = pe - pb;
   if (i >= nq * np) return;
@@ -761,6 +763,7 @@ __global__ void ivf_fill_kernel(const int32_t *probes, int64_t nq, int nprobe, i
   const int lst = probes[q * nprobe + p];
   const int pos = atomicAdd(&fill[lst], 1);
   qlist[qoff[lst] + pos] = (int32_t)(q * nparts + p * cmax);  // chunk c adds c (ScanItem.part)
+  if (qpos) qpos[q * nprobe + p] = qoff[lst] + pos;
 }
 
 // items of list l in launch phase `phase`: for each of its row chunks, for each block of
@@ -1672,10 +1675,10 @@ void launch_ivf_items(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t
                      phase, ws.qoff, ws.ioff, ws.n_items);
   if (phase == 0 && n > 0 && lds)
     hipLaunchKernelGGL(ivf_fill_lds_kernel, dim3(nblk(n, IVF_EPB)), dim3(256), hb, st, probes, nq, nprobe, pb, pe,
-                       nparts, ch.cmax, nlist, ws.qoff, ws.fill, ws.qlist);
+                       nparts, ch.cmax, nlist, ws.qoff, ws.fill, ws.qlist, pb == 0 && pe == nprobe ? ws.qpos : nullptr);
   else if (phase == 0 && n > 0)
     hipLaunchKernelGGL(ivf_fill_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, probes, nq, nprobe, pb, pe, nparts,
-                       ch.cmax, ws.qoff, ws.fill, ws.qlist);
+                       ch.cmax, ws.qoff, ws.fill, ws.qlist, pb == 0 && pe == nprobe ? ws.qpos : nullptr);
   hipLaunchKernelGGL(ivf_items_kernel, dim3(nblk(nlist, 256)), dim3(256), 0, st, ws.cnt, ws.qoff, ws.ioff, nlist,
                      list_begin, list_end, qchunk, ch, phase, balance ? 1 : 0, ws.items);
 }

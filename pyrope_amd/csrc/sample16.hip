@@ -45,11 +45,13 @@ __device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf
 
 // ---- 1. query operands per (list, query) pair ----
 // A lane group of D / 8 lanes per query (8 dims a lane, the centroid's 8 dims held in registers for
-// the whole list), 64 / (D / 8) queries per wave at a time.  An item's queries are split over
-// SPREP_SPLIT(D) blocks (block s takes every SPLIT-th run of 4 x QW queries): each wave's loop is a chain
-// of dependent loads (position -> query row), so more waves with fewer turns each hide its latency.
+// the whole list), 64 / (D / 8) queries per wave per pass.  A block's loads are a chain (item -> position
+// -> query row), so each wave issues the loads of SPREP_U passes before it computes any of them, and an
+// item's queries are split over SPREP_SPLIT(D) blocks: more chains in flight, fewer turns each.
+// (Round 4: one pass per turn and D / 16 blocks per item, 34-43 us at I1: latency-bound.)
 template <int D>
-constexpr int SPREP_SPLIT = D / 16;
+constexpr int SPREP_SPLIT = D >= 128 ? 2 : 1;
+constexpr int SPREP_U = 4;
 template <int D, int MET>
 __device__ void sprep_unit(const StreamArgs &a, int item, int part);
 
@@ -64,62 +66,151 @@ __global__ __launch_bounds__(256) void sprep_kernel(StreamArgs a) {
 
 template <int D, int MET>
 __device__ void sprep_unit(const StreamArgs &a, int item, int part) {
-  constexpr int SPLIT = SPREP_SPLIT<D>;
+  constexpr int SPLIT = SPREP_SPLIT<D>, U = SPREP_U;
   const ScanItem it = a.items[item];
   if (it.part != 0) return;  // chunk-0 items cover every qlist position of their list once
-  // (a bounded grid walking 64-item windows of chunk-0 items measured slower: 0.165 vs 0.146 ms, r4g)
-  constexpr int LQ = D / 8, QW = 64 / LQ;
+  constexpr int LQ = D / 8, QW = 64 / LQ, STEP = 4 * QW * SPLIT;  // STEP: queries between a wave's passes
   if (4 * QW * part >= it.qcnt) return;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, sub = lane % LQ, qsl = lane / LQ;
   const float4 *cp = reinterpret_cast<const float4 *>(a.cents + (size_t)it.list * D + 8 * sub);
   const float4 c0 = cp[0], c1 = cp[1];
   const float cv[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-  for (int qi0 = QW * w + 4 * QW * part; qi0 < it.qcnt; qi0 += 4 * QW * SPLIT) {
-    const int qi = qi0 + qsl;
-    const bool act = qi < it.qcnt;
-    const int pos = it.qbeg + (act ? qi : 0);
-    const int q = a.qlist[pos] / a.nparts;
-    const float4 *qp = reinterpret_cast<const float4 *>(a.queries + (size_t)q * D + 8 * sub);
-    const float4 q0 = qp[0], q1 = qp[1];
-    const float qv[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
-    float r[8], cq = 0.0f, amax = 0.0f, q2 = 0.0f, c2 = 0.0f;
+  for (int qb = QW * w + 4 * QW * part; qb < it.qcnt; qb += STEP * U) {
+    int pos[U], q[U];
+    float4 q0[U], q1[U];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < U; ++u) {
+      const int qi = qb + u * STEP + qsl;
+      pos[u] = it.qbeg + (qi < it.qcnt ? qi : 0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) q[u] = a.qlist[pos[u]] / a.nparts;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float4 *qp = reinterpret_cast<const float4 *>(a.queries + (size_t)q[u] * D + 8 * sub);
+      q0[u] = qp[0];
+      q1[u] = qp[1];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool act = qb + u * STEP + qsl < it.qcnt;
+      const float qv[8] = {q0[u].x, q0[u].y, q0[u].z, q0[u].w, q1[u].x, q1[u].y, q1[u].z, q1[u].w};
+      float r[8], cq = 0.0f, amax = 0.0f, q2 = 0.0f, c2 = 0.0f;
+#pragma unroll
+      for (int d = 0; d < 8; ++d) {
+        if (MET == L2) {
+          r[d] = qv[d] - cv[d];
+          cq += r[d] * r[d];
+        } else {
+          r[d] = qv[d];
+          cq += qv[d] * cv[d];
+          q2 += qv[d] * qv[d];
+          c2 += cv[d] * cv[d];
+        }
+        amax = fmaxf(amax, fabsf(r[d]));
+      }
+#pragma unroll
+      for (int off = 1; off < LQ; off <<= 1) {
+        cq += __shfl_xor(cq, off);
+        amax = fmaxf(amax, __shfl_xor(amax, off));
+        if (MET == IP) {
+          q2 += __shfl_xor(q2, off);
+          c2 += __shfl_xor(c2, off);
+        }
+      }
+      // the pair's share of the error bound (stream_ub_terms), rounded up by the 1e-3 in its constants
+      float ep = 0.0f;
       if (MET == L2) {
-        r[u] = qv[u] - cv[u];
-        cq += r[u] * r[u];
+        ep = a.kq * cq + a.kqa * sqrtf(cq);
       } else {
-        r[u] = qv[u];
-        cq += qv[u] * cv[u];
-        q2 += qv[u] * qv[u];
-        c2 += cv[u] * cv[u];
+        const float qn = sqrtf(q2);
+        ep = a.kq * q2 + a.kqa * qn + a.kqc * qn * sqrtf(c2);
       }
-      amax = fmaxf(amax, fabsf(r[u]));
-    }
+      const float sq = pow2_scale(amax);
+      if (act) {
+        h8v hv;
 #pragma unroll
-    for (int off = 1; off < LQ; off <<= 1) {
-      cq += __shfl_xor(cq, off);
-      amax = fmaxf(amax, __shfl_xor(amax, off));
-      if (MET == IP) {
-        q2 += __shfl_xor(q2, off);
-        c2 += __shfl_xor(c2, off);
+        for (int d = 0; d < 8; ++d) hv[d] = (_Float16)(r[d] * sq);  // the scaling is exact (a power of two)
+        *reinterpret_cast<h8v *>(a.bq + (size_t)pos[u] * D + 8 * sub) = hv;
+        if (sub == 0)
+          a.qsc[pos[u]] = make_float2((MET == L2 ? 2.0f : 1.0f) / (sq * a.sx), (MET == L2 ? -cq : cq) + ep);
       }
     }
-    // the pair's share of the error bound (stream_ub_terms), rounded up by the 1e-3 in its constants
-    float ep = 0.0f;
-    if (MET == L2) {
-      ep = a.kq * cq + a.kqa * sqrtf(cq);
-    } else {
-      const float qn = sqrtf(q2);
-      ep = a.kq * q2 + a.kqa * qn + a.kqc * qn * sqrtf(c2);
-    }
-    const float sq = pow2_scale(amax);
-    if (act) {
-      h8v hv;
+  }
+}
+
+// The same operands query-major, when the work lists recorded each (query, probe)'s position (StreamArgs::qpos):
+// one wave per query, lane group g of D / 8 lanes takes probes g, g + QW, ...  The query's dims are read
+// once and stay in registers across its probes, and the centroids (nlist x D x 4 B) stay L2-resident; the
+// list-major pass above re-reads a query row per (list, query) pair: at I1, 10,000 x 32 rows of 512 B
+// against L2s of 4 MiB per XCD.  Same arithmetic, same bq / qsc.
+template <int D, int MET>
+__global__ __launch_bounds__(256) void sprep_q_kernel(StreamArgs a) {
+  constexpr int LQ = D / 8, QW = 64 / LQ, PU = 32 / QW > 0 ? 32 / QW : 1;  // probes per lane group per turn
+  const int lane = threadIdx.x & 63, sub = lane % LQ, g = lane / LQ;
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= a.nq) return;
+  const float4 *qp = reinterpret_cast<const float4 *>(a.queries + (size_t)q * D + 8 * sub);
+  const float4 q0 = qp[0], q1 = qp[1];
+  const float qv[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+  for (int p0 = 0; p0 < a.nprobe; p0 += QW * PU) {
+    int pos[PU], lst[PU];
+    float4 c0[PU], c1[PU];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) hv[u] = (_Float16)(r[u] * sq);  // the scaling is exact (a power of two)
-      *reinterpret_cast<h8v *>(a.bq + (size_t)pos * D + 8 * sub) = hv;
-      if (sub == 0) a.qsc[pos] = make_float2((MET == L2 ? 2.0f : 1.0f) / (sq * a.sx), (MET == L2 ? -cq : cq) + ep);
+    for (int u = 0; u < PU; ++u) {
+      const int p = p0 + u * QW + g;
+      const bool ok = p < a.nprobe;
+      lst[u] = ok ? a.probes[(size_t)q * a.nprobe + p] : -1;
+      pos[u] = ok ? a.qpos[(size_t)q * a.nprobe + p] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < PU; ++u) {
+      const float4 *cp = reinterpret_cast<const float4 *>(a.cents + (size_t)max(lst[u], 0) * D + 8 * sub);
+      c0[u] = cp[0];
+      c1[u] = cp[1];
+    }
+#pragma unroll
+    for (int u = 0; u < PU; ++u) {
+      const float cv[8] = {c0[u].x, c0[u].y, c0[u].z, c0[u].w, c1[u].x, c1[u].y, c1[u].z, c1[u].w};
+      float r[8], cq = 0.0f, amax = 0.0f, q2 = 0.0f, c2 = 0.0f;
+#pragma unroll
+      for (int d = 0; d < 8; ++d) {
+        if (MET == L2) {
+          r[d] = qv[d] - cv[d];
+          cq += r[d] * r[d];
+        } else {
+          r[d] = qv[d];
+          cq += qv[d] * cv[d];
+          q2 += qv[d] * qv[d];
+          c2 += cv[d] * cv[d];
+        }
+        amax = fmaxf(amax, fabsf(r[d]));
+      }
+#pragma unroll
+      for (int off = 1; off < LQ; off <<= 1) {
+        cq += __shfl_xor(cq, off);
+        amax = fmaxf(amax, __shfl_xor(amax, off));
+        if (MET == IP) {
+          q2 += __shfl_xor(q2, off);
+          c2 += __shfl_xor(c2, off);
+        }
+      }
+      float ep = 0.0f;  // (as sprep_unit)
+      if (MET == L2) {
+        ep = a.kq * cq + a.kqa * sqrtf(cq);
+      } else {
+        const float qn = sqrtf(q2);
+        ep = a.kq * q2 + a.kqa * qn + a.kqc * qn * sqrtf(c2);
+      }
+      const float sq = pow2_scale(amax);
+      if (lst[u] >= 0 && pos[u] >= 0) {
+        h8v hv;
+#pragma unroll
+        for (int d = 0; d < 8; ++d) hv[d] = (_Float16)(r[d] * sq);
+        *reinterpret_cast<h8v *>(a.bq + (size_t)pos[u] * D + 8 * sub) = hv;
+        if (sub == 0)
+          a.qsc[pos[u]] = make_float2((MET == L2 ? 2.0f : 1.0f) / (sq * a.sx), (MET == L2 ? -cq : cq) + ep);
+      }
     }
   }
 }
@@ -330,6 +421,29 @@ void launch_sample16(const StreamArgs &a, int metric, int max_items, hipStream_t
   // holds far fewer)
   const int64_t pg = std::min<int64_t>((int64_t)max_items * split, 8 * (int64_t)device_cus());
   auto prep = [&](auto kern) { hipLaunchKernelGGL(kern, dim3((unsigned)pg), dim3(256), 0, st, a); };
+  // query-major when the work lists recorded the positions (PYR_SPREP_Q=0: the list-major pass; A/B only)
+  static const bool qmaj = !(getenv("PYR_SPREP_Q") && atoi(getenv("PYR_SPREP_Q")) == 0);
+  if (a.qpos && qmaj && a.nq > 0) {
+    const dim3 qg((unsigned)((a.nq + 3) / 4));
+    auto prepq = [&](auto kern) { hipLaunchKernelGGL(kern, qg, dim3(256), 0, st, a); };
+    auto samp2 = [&](auto kern) {
+      if (!prep_only) hipLaunchKernelGGL(kern, dim3(std::max(1, std::min(max_items, device_cus()))), dim3(64 * SNW), 0, st, a);
+    };
+    switch (a.dim) {
+      case 32:
+        metric == L2 ? prepq(sprep_q_kernel<32, L2>) : prepq(sprep_q_kernel<32, IP>);
+        metric == L2 ? samp2(sample16_kernel<32, L2>) : samp2(sample16_kernel<32, IP>);
+        return;
+      case 64:
+        metric == L2 ? prepq(sprep_q_kernel<64, L2>) : prepq(sprep_q_kernel<64, IP>);
+        metric == L2 ? samp2(sample16_kernel<64, L2>) : samp2(sample16_kernel<64, IP>);
+        return;
+      default:
+        metric == L2 ? prepq(sprep_q_kernel<128, L2>) : prepq(sprep_q_kernel<128, IP>);
+        metric == L2 ? samp2(sample16_kernel<128, L2>) : samp2(sample16_kernel<128, IP>);
+        return;
+    }
+  }
   const dim3 grid(std::max(1, std::min(max_items, device_cus())));
   auto samp = [&](auto kern) {
     if (!prep_only) hipLaunchKernelGGL(kern, grid, dim3(64 * SNW), 0, st, a);

@@ -435,9 +435,22 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
 #pragma unroll
         for (int s = 1; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[s], bj[s], acc, 0, 0, 0);
         const bool e = epi_test(acc, mr, q);
-        // all of the group's operand reads before its chain (one LDS wait, not one per MFMA)
-        __builtin_amdgcn_sched_group_barrier(0x100, KS + 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, KS, 0);
+        if constexpr (AB == 4) {  // round 4 (A/B only, PYR_FILTER_ABLATE=1024): every B read before the chain
+          __builtin_amdgcn_sched_group_barrier(0x100, KS + 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, KS, 0);
+        } else {
+          // staged: 4 B reads (+ the group's scalars), then 2 MFMAs per 2 further reads -- at most 4 B
+          // operands live (16 VGPRs, not 32): with all 8 live the kernel spilled 11 VGPRs, reloaded
+          // (serially) on every emitting (tile, group)
+          constexpr int P0 = KS < 4 ? KS : 4, NS = (KS - P0 + 1) / 2;
+          __builtin_amdgcn_sched_group_barrier(0x100, P0 + 1, 0);
+#pragma unroll
+          for (int i = 0; i < NS; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, KS - 2 * NS, 0);
+        }
         if (j == 0 && tpf >= 0 && (a.ablate & 512)) {  // the tile's own loads were waited for: warm L2
 #pragma unroll
           for (int o = 0; o < TB; o += 64 * 128)
@@ -485,6 +498,10 @@ void launch_scan_dm(const StreamArgs &a, int max_items, hipStream_t st) {
     }
     if (a.ablate & 256) {
       hipLaunchKernelGGL((scan_kernel<D, MET, 3>), dim3(grid), b, 0, st, a);
+      return;
+    }
+    if (a.ablate & 1024) {
+      hipLaunchKernelGGL((scan_kernel<D, MET, 4>), dim3(grid), b, 0, st, a);
       return;
     }
   }
