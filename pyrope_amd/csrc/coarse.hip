@@ -226,10 +226,24 @@ __global__ __launch_bounds__(256) void coarse_select_reg_kernel(const float *sco
 // 2. coarse_pick_kernel: the nprobe-th largest approximate score aP, the exact ComputeScore of every
 //    centroid within 2E of it (E bounds |approx - (score + |q|^2)|) and the first nprobe of those.
 // 3. coarse_select_list_kernel: the dense exact ranking of the queries the pick could not settle.
+// the search's counters zeroed by the approximate-score launch (its 2D grid, one word per thread at most):
+// the stream scan's WordFill without a fill_words launch of its own (engine.cpp stream_counters_fill)
+__device__ __forceinline__ void grid_word_fill(const WordFill &f) {
+  const int64_t nt = (int64_t)gridDim.x * gridDim.y * blockDim.x;
+  const int64_t t = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
+  int64_t base = 0;
+  for (int r = 0; r < f.cnt; ++r) {
+    for (int64_t e = t - base; e < f.n[r]; e += nt)
+      if (e >= 0) f.p[r][e] = f.v[r];
+    base += f.n[r];
+  }
+}
+
 template <int MET, int DT>
 __global__ __launch_bounds__(64) void coarse_approx_kernel(const float *q, const float *c, const float *c2, int64_t nq,
-                                                           int nc, int Dr, float *out, int32_t *zero) {
+                                                           int nc, int Dr, float *out, int32_t *zero, WordFill zf) {
   if (zero && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *zero = 0;  // the pick's failure count
+  grid_word_fill(zf);
   const int D = DT > 0 ? DT : Dr;  // a compile-time D unrolls the loop: every operand load is issued up front
   constexpr int UNS = DT > 0 ? DT / 16 : 1;
   const int64_t q0 = (int64_t)blockIdx.y * 32;
@@ -283,9 +297,11 @@ __global__ __launch_bounds__(64) void coarse_approx_kernel(const float *q, const
 constexpr int AKT = 64, AKS = AKT + 4;
 template <int MET>
 __global__ __launch_bounds__(256) void coarse_approx_lds_kernel(const float *q, const float *c, const float *c2,
-                                                                int64_t nq, int nc, int D, float *out, int32_t *zero) {
+                                                                int64_t nq, int nc, int D, float *out, int32_t *zero,
+                                                                WordFill zf) {
   __shared__ __attribute__((aligned(16))) float qs[64 * AKS], cs[64 * AKS];
   if (zero && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *zero = 0;  // the pick's failure count
+  grid_word_fill(zf);
   const int64_t q0 = (int64_t)blockIdx.y * 64;
   const int c0 = blockIdx.x * 64;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, r = l & 15, h = l >> 4;
@@ -605,8 +621,12 @@ bool coarse_mfma_supported(int nlist, int dim, int metric, int nprobe) {
 
 void launch_coarse_mfma(const float *q, const float *cents_rm, const float *c2, int64_t nq, int32_t nlist,
                         int32_t dim, int32_t metric, int32_t nprobe, double cnmax, double c_err, float *scores,
-                        int32_t *fail, int32_t *nfail, int32_t *probes, hipStream_t st) {
-  if (nq <= 0 || nlist <= 0 || nprobe <= 0) return;
+                        int32_t *fail, int32_t *nfail, int32_t *probes, hipStream_t st, const WordFill *zero) {
+  if (nq <= 0 || nlist <= 0 || nprobe <= 0) {
+    if (zero) launch_fill_words(*zero, st);
+    return;
+  }
+  const WordFill zf = zero ? *zero : WordFill{};
   const int P = std::min(nprobe, nlist);
   const dim3 ga((unsigned)((nlist + 31) / 32), (unsigned)((nq + 31) / 32));
   const dim3 g4((unsigned)((nq + 3) / 4));
@@ -621,10 +641,10 @@ void launch_coarse_mfma(const float *q, const float *cents_rm, const float *c2, 
     // scripts/diag/graph_memset.py)
     if (lds)
       hipLaunchKernelGGL((coarse_approx_lds_kernel<M>), gl, dim3(256), 0, st, q, cents_rm, c2, nq, nlist, dim, scores,
-                         nfail);
+                         nfail, zf);
     else
       hipLaunchKernelGGL((coarse_approx_kernel<M, DT>), ga, dim3(64), 0, st, q, cents_rm, c2, nq, nlist, dim, scores,
-                         nfail);
+                         nfail, zf);
     hipLaunchKernelGGL((coarse_pick_kernel<M, DT>), g4, dim3(256), 0, st, q, cents_rm, scores, nq, nlist, dim, P, cnmax,
                        c_err, probes, fail, nfail);
   };

@@ -660,7 +660,7 @@ static uint32_t *shared_bounds(Workspace &ws, int64_t nq) {
 // search must stay capturable into a hipGraph and replayable: hipMemsetAsync nodes of a captured graph
 // write stale values from its second replay on in the HIP runtime PyTorch ships, which is what faulted the
 // second replay of a captured FLAT search (scripts/diag/graph_memset.py; DESIGN.md §4 "hipGraph replays").
-static void reset_stream_counters(Workspace &ws, int64_t nq, int nlist) {
+static WordFill stream_counters_fill(Workspace &ws, int64_t nq, int nlist) {
   ws.ivf_cnt.ensure(sizeof(int32_t) * std::max(nlist, 1));
   ws.ivf_fill.ensure(sizeof(int32_t) * std::max(nlist, 1));
   ws.scn.ensure(sizeof(int32_t) * std::max<int64_t>(nq, 1));
@@ -676,8 +676,37 @@ static void reset_stream_counters(Workspace &ws, int64_t nq, int nlist) {
   z.add(ws.swork.p, 16, 0);  // two item counters, or two sets of 8 per-XCD queue counters (pq32)
   z.add(ws.fail_cnt.p, 1, 0);
   z.add(ws.fail_cnt2.p, 1, 0);
-  launch_fill_words(z, ws.st);
+  return z;
 }
+static void reset_stream_counters(Workspace &ws, int64_t nq, int nlist) {
+  launch_fill_words(stream_counters_fill(ws, nq, nlist), ws.st);
+}
+// the same words zeroed by the next coarse ranking's first launch (CoarseIndex::probe), or by a fill of their own
+// right after it (flush_stream_counters): one launch less on the IVF search
+static void defer_stream_counters(Workspace &ws, int64_t nq, int nlist) {
+  ws.pz = stream_counters_fill(ws, nq, nlist);
+  ws.pz_set = true;
+}
+static void flush_stream_counters(Workspace &ws) {
+  if (ws.pz_set) launch_fill_words(ws.pz, ws.st);
+  ws.pz_set = false;
+}
+// the device re-run's per-query unit counters (IvfRerunArgs::done): zeroed once when allocated, then left
+// zero by every launch (each merge resets its query's)
+static int32_t *rerun_done(Workspace &ws, int64_t max_fail) {
+  const size_t need = sizeof(int32_t) * (size_t)std::max<int64_t>(max_fail, 1);
+  if (ws.rrdone.n < need) {
+    ws.rrdone.ensure(need);
+    WordFill z;
+    z.add(ws.rrdone.p, (int64_t)(ws.rrdone.n / sizeof(int32_t)), 0);
+    launch_fill_words(z, ws.st);
+  }
+  return ws.rrdone.as<int32_t>();
+}
+struct DeferredCounters {  // a deferred fill never outlives the search that set it (an exception included)
+  Workspace &ws;
+  ~DeferredCounters() { ws.pz_set = false; }
+};
 
 // IVF-PQ LUT list scan kernel: 2 = pq_adc4 (default), 0 = the first-cut pq_scan (PYR_PQ_ADC=0; A/B
 // only, same results; also what k > 64 or an unsupported shape takes)
@@ -1562,6 +1591,7 @@ struct FlatIndex : Index {
     if (!filter_ablate() && !getenv("PYR_STREAM_THR_BIAS")) {
       PhaseTimer t(PH_FALLBACK, ws.st, nf);
       ra.nchunk = (int32_t)std::max<int64_t>(1, std::min<int64_t>(64, (flat_chunk_rows(cutoff) + 1023) / 1024));
+      ra.done = rerun_done(ws, nq);
       ws.rrpart.ensure(sizeof(uint64_t) * ivf_rerun_part_keys(nq, probes, k));
       launch_ivf_exact_rerun(ra, cr ? COS : metric, nq, ws.rrpart.as<uint64_t>(), ws.st);
     }
@@ -1803,7 +1833,9 @@ struct Coarse {
         const int64_t n = std::min<int64_t>(qb, nq - a);
         launch_coarse_mfma(d_q + a * cs.dim, rm.as<float>(), c2.as<float>(), n, nlist, cs.dim, met, nprobe, cnmax,
                            coarse_cerr(cs.dim), ws.cpart_s.as<float>(), ws.cfail.as<int32_t>(),
-                           ws.cnfail.as<int32_t>(), ws.probes.as<int32_t>() + a * nprobe, ws.st);
+                           ws.cnfail.as<int32_t>(), ws.probes.as<int32_t>() + a * nprobe, ws.st,
+                           ws.pz_set ? &ws.pz : nullptr);
+        ws.pz_set = false;
       }
       return;
     }
@@ -2360,7 +2392,8 @@ struct IvfFlatIndex : Index {
                     float *d_s, int64_t *d_l, int32_t *d_c, Workspace &ws, const ShardCtx *sh = nullptr) {
     const bool cosine = metric == COS;
     const int met = cosine ? L2 : metric;  // Cosine: L2 over the unit vectors (commit_lists)
-    reset_stream_counters(ws, nq, coarse.nlist);
+    defer_stream_counters(ws, nq, coarse.nlist);
+    DeferredCounters dc{ws};
     if (cosine) {
       ws.qn.ensure(sizeof(float) * std::max<int64_t>(nq, 1));
       launch_norms(d_q, nq, dim, 0, ws.qn.as<float>(), ws.st);  // VectorMath.ComputeNorm (:167)
@@ -2369,6 +2402,7 @@ struct IvfFlatIndex : Index {
       PhaseTimer t(PH_COARSE, ws.st, nq * coarse.nlist);
       // exact coarse ranking (ComputeScore, :186-198)
       coarse.probe(d_q, cosine ? ws.qn.as<float>() : nullptr, nq, probes, metric, ws);
+      flush_stream_counters(ws);
     }
     const float *d_qs = d_q;  // the queries the scan scores: the unit queries for Cosine
     if (cosine) {
@@ -2600,6 +2634,7 @@ struct IvfFlatIndex : Index {
     if (!filter_ablate() && !getenv("PYR_STREAM_THR_BIAS")) {
       PhaseTimer t(PH_FALLBACK, ws.st, nf);
       ra.nchunk = (int32_t)std::max<int64_t>(1, std::min<int64_t>(64, (max_len + 1023) / 1024));
+      ra.done = rerun_done(ws, nq);
       ws.rrpart.ensure(sizeof(uint64_t) * ivf_rerun_part_keys(nq, probes, k));
       launch_ivf_exact_rerun(ra, metric, nq, ws.rrpart.as<uint64_t>(), ws.st);
     }
@@ -2822,6 +2857,7 @@ struct IvfFlatIndex : Index {
     ra.rec_lb = dlb.as<int32_t>();
     ra.rec_nlist = coarse.nlist;
     PhaseTimer t(PH_FALLBACK, ws.st);
+    ra.done = rerun_done(ws, mf);
     ws.rrpart.ensure(sizeof(uint64_t) * ivf_rerun_part_keys(mf, P, k));
     launch_ivf_exact_rerun(ra, metric, mf, ws.rrpart.as<uint64_t>(), ws.st);
     HIPCHK(hipGetLastError());
@@ -3295,12 +3331,46 @@ struct IvfPqIndex : Index {
     const int probes = (built && coarse.nlist > 0) ? std::max(0, std::min(nprobe, coarse.nlist)) : 0;
     // the matrix-core scan: built lists only (no buffer rows), the P1 geometry (pq32_supported)
     const char *pm = getenv("PYR_PQ_MFMA");  // 0: the LUT scan below (A/B and the re-run path)
-    if (!(pm && atoi(pm) == 0) && pq32_ready && probes > 0 && buf.live_count() == 0 && filter_enabled() &&
-        pq32_supported(dim, M, ksub, k)) {
-      search_pq32(d_q, nq, k, probes, d_s, d_l, d_c, ws);
+    if (!(pm && atoi(pm) == 0) && pq32_ready && probes > 0 && filter_enabled() && pq32_supported(dim, M, ksub, k)) {
+      if (buf.live_count() == 0) {
+        search_pq32(d_q, nq, k, probes, d_s, d_l, d_c, ws);
+        return;
+      }
+      // a non-empty buffer (:130-136): the lists on the matrix cores, the buffer exactly beside them, the two
+      // answers merged (a list entry first on equal scores, as the LUT path's keys order them)
+      ws.bx_s.ensure(sizeof(float) * nq * k);
+      ws.bx_l.ensure(sizeof(int64_t) * nq * k);
+      ws.bx_c.ensure(sizeof(int32_t) * nq);
+      ws.lx_s.ensure(sizeof(float) * nq * k);
+      ws.lx_l.ensure(sizeof(int64_t) * nq * k);
+      ws.lx_c.ensure(sizeof(int32_t) * nq);
+      search_pq32(d_q, nq, k, probes, ws.lx_s.as<float>(), ws.lx_l.as<int64_t>(), ws.lx_c.as<int32_t>(), ws);
+      buffer_topk(d_q, nq, k, ws.bx_s.as<float>(), ws.bx_l.as<int64_t>(), ws.bx_c.as<int32_t>(), ws);
+      PhaseTimer tm(PH_MERGE, ws.st);
+      launch_merge_two(ws.lx_s.as<float>(), ws.lx_l.as<int64_t>(), ws.lx_c.as<int32_t>(), ws.bx_s.as<float>(),
+                       ws.bx_l.as<int64_t>(), ws.bx_c.as<int32_t>(), nq, k, d_s, d_l, d_c, ws.st);
+      HIPCHK(hipGetLastError());
       return;
     }
     search_lut(d_q, nq, k, probes, d_s, d_l, d_c, ws);
+  }
+
+  // the buffer's exact top k (:130-136, ComputeScore) in (score desc, slot asc) order
+  void buffer_topk(const float *d_q, int64_t nq, int k, float *d_s, int64_t *d_l, int32_t *d_c, Workspace &ws) {
+    const int64_t bcut = buf.st.n;
+    const ScanPlan bp = plan_flat(bcut, nq, dim, k, MAX_PARTS);
+    prep_queries(d_q, nq, dim, metric, ws);
+    const float *qn = metric == COS ? ws.qn.as<float>() : nullptr;
+    const size_t np = (size_t)nq * bp.nchunks * k;
+    ws.part_s.ensure(sizeof(float) * np);
+    ws.part_k.ensure(sizeof(uint32_t) * np);
+    {
+      PhaseTimer t(PH_BUF_SCAN, ws.st, nq * bcut);
+      flat_scan(buf.st, bcut, bp, d_q, qn, nq, k, 1, metric, bp.nchunks, 0, KEY_BUF, ws, ws.part_s.as<float>(),
+                ws.part_k.as<uint32_t>(), true);
+    }
+    launch_merge_keys(ws.part_s.as<float>(), ws.part_k.as<uint32_t>(), nq, bp.nchunks, k, clabels.as<int64_t>(),
+                      buf.st.labels.as<int64_t>(), d_s, d_l, nullptr, d_c, ws.st, nullptr);
   }
 
   // the per-position row terms of the fp16 filter: -|x^|^2 (or -inf when not visible) + kr |x^|^2
@@ -3506,13 +3576,16 @@ struct IvfPqIndex : Index {
                       Workspace &nw = ws.nested();
                       nw.ext_probes = ws.fprobes.as<int32_t>();
                       nw.ext_nprobe = probes;
+                      nw.skip_buffer = true;  // the lists only: a non-empty buffer is merged by search()
                       try {
                         search_lut(q2, n2, k, probes, s2, l2, c2, nw);
                       } catch (...) {
                         nw.ext_probes = nullptr;
+                        nw.skip_buffer = false;
                         throw;
                       }
                       nw.ext_probes = nullptr;
+                      nw.skip_buffer = false;
                     });
   }
 
@@ -3535,7 +3608,7 @@ struct IvfPqIndex : Index {
     }
     const int lparts = probes * ch.cmax;
     ScanPlan bp;
-    if (buf.live_count() > 0) bp = plan_flat(bcut, nq, dim, k, MAX_PARTS - lparts);
+    if (buf.live_count() > 0 && !ws.skip_buffer) bp = plan_flat(bcut, nq, dim, k, MAX_PARTS - lparts);
     const int nparts = lparts + bp.nchunks;
     if (nparts > MAX_PARTS) throw Error(PYR_E_ARG, "nprobe too large");
     if (nparts == 0) {

@@ -165,7 +165,11 @@ struct Workspace {
   DevMem q, qn, qt, items, nitems, items2, nitems2, items3, nitems3, qlist, part_s, part_k, probes, cpart_s, cpart_k,
       limits;
   DevMem ivf_cnt, ivf_fill, ivf_qoff, ivf_ioff, gthr;
-  DevMem ivf_cnt2, ivf_fill2, ivf_qoff2, ivf_ioff2, qlist2, qpos;  // second item set (nearest-list seeding)
+  DevMem ivf_cnt2, ivf_fill2, ivf_qoff2, ivf_ioff2, qlist2, qpos;
+  DevMem bx_s, bx_l, bx_c, lx_s, lx_l, lx_c;  // IVF_PQ with a buffer: its and the lists' answers
+  DevMem rrdone;       // the device re-run's per-query unit counters (rerun_done, engine.cpp)
+  WordFill pz;         // counters the next coarse ranking zeroes (defer_stream_counters, engine.cpp)
+  bool pz_set = false;  // second item set (nearest-list seeding)
   DevMem out_s, out_l, out_c;
   DevMem ms, mk, fail, fail_cnt, fq, fs, fl, fc;  // MFMA filter: merged candidates, certificate failures
   DevMem fprobes;                                 // probe lists of the failing queries (IVF_PQ LUT re-run)
@@ -179,6 +183,7 @@ struct Workspace {
   DevMem shp, shthr, rpos;  // list-sharded search: unpacked plan (probes, T_q), re-run record slots
   uint64_t wgen_seen = 0;                         // the index's write generation this stream is ordered after
   const int32_t *ext_probes = nullptr;            // caller-ranked probe lists [nq][ext_nprobe] (multi-GPU)
+  bool skip_buffer = false;                       // IVF_PQ LUT scan: the lists only (the buffer merged by the caller)
   int32_t ext_nprobe = 0;
   // the re-run of certificate failures searches with its own buffers on the same stream
   std::unique_ptr<Workspace> sub;

@@ -180,6 +180,9 @@ struct IvfRerunArgs {
   const int32_t *rec_pos;
   const int32_t *rec_lb;
   int32_t rec_nlist;
+  // or null: per failing query the units done (zero before the launch; every merge resets its own); the block
+  // that finishes a query's last unit merges it, and the separate merge launch is skipped
+  int32_t *done;
 };
 // part: ivf_rerun_part_keys() rank keys of scratch (one block per (failing query, probe, chunk), then
 // a merge per query)
@@ -189,6 +192,11 @@ void launch_ivf_exact_rerun(const IvfRerunArgs &a, int metric, int64_t max_fail,
 void launch_merge_keys(const float *ps, const uint32_t *pk, int64_t nq, int32_t nparts, int32_t k,
                        const int64_t *row_labels, const int64_t *buf_labels, float *out_s, int64_t *out_l,
                        int32_t *out_keys, int32_t *out_cnt, hipStream_t st, const MergeIvf *ivf = nullptr);
+// Two per-query result sets (each sorted, ca / cb real entries) into the top k, a before b on equal scores
+// (IVF_PQ: the lists' certified answer and the buffer's exact one; k <= 64).
+void launch_merge_two(const float *as, const int64_t *al, const int32_t *ca, const float *bs, const int64_t *bl,
+                      const int32_t *cb, int64_t nq, int k, float *out_s, int64_t *out_l, int32_t *out_c,
+                      hipStream_t st);
 // Merge partial lists that carry int64 labels (multi-GPU), ties by label asc.
 void launch_merge_labels(const float *ps, const int64_t *pl, int64_t nq, int32_t nparts, int32_t k, float *out_s,
                          int64_t *out_l, hipStream_t st, bool part_major = false);
@@ -271,9 +279,12 @@ void launch_coarse_dense(const float *q, const float *cents_rm, const float *qn,
 // max |c|; c_err: the error-bound constant.  scores: nq x nlist scratch, fail: nq, nfail: 1 (device
 // scratch).  Nothing synchronizes.
 bool coarse_mfma_supported(int nlist, int dim, int metric, int nprobe);
+// zero: words to fill by the approximate-score launch (the search's counters; no launch of their own)
+struct WordFill;
 void launch_coarse_mfma(const float *q, const float *cents_rm, const float *c2, int64_t nq, int32_t nlist,
                         int32_t dim, int32_t metric, int32_t nprobe, double cnmax, double c_err, float *scores,
-                        int32_t *fail, int32_t *nfail, int32_t *probes, hipStream_t st);
+                        int32_t *fail, int32_t *nfail, int32_t *probes, hipStream_t st,
+                        const WordFill *zero = nullptr);
 
 // ---- 8-bit search mode of the FLAT index (sq8.hip; BruteForceVectorIndex EnableQuantization) ----
 struct Sq8Args {

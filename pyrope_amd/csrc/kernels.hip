@@ -608,6 +608,35 @@ __global__ __launch_bounds__(256) void merge_labels_kernel(const float *ps, cons
     }
 }
 
+// Two sorted result sets of one query merged into its top k: a (the lists') before b (the buffer's) on equal
+// score keys -- the order launch_merge_keys gives list keys (< KEY_BUF) against KEY_BUF | slot -- each set
+// already in its own (score desc, storage slot asc) order; ca / cb their real entries.  One thread per query.
+__global__ void merge_two_kernel(const float *as, const int64_t *al, const int32_t *ca, const float *bs,
+                                 const int64_t *bl, const int32_t *cb, int64_t nq, int k, float *out_s,
+                                 int64_t *out_l, int32_t *out_c) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  const float *a = as + q * k, *b = bs + q * k;
+  const int64_t *la = al + q * k, *lb = bl + q * k;
+  const int na = min(ca[q], k), nb = min(cb[q], k);
+  int i = 0, j = 0, o = 0;
+  float rs[64];
+  int64_t rl[64];
+  for (; o < k && (i < na || j < nb); ++o) {
+    const bool ta = i < na && (j >= nb || score_key(a[i]) >= score_key(b[j]));
+    rs[o] = ta ? a[i] : b[j];
+    rl[o] = ta ? la[i] : lb[j];
+    if (ta) ++i;
+    else ++j;
+  }
+  const int n = o;
+  for (o = 0; o < k; ++o) {
+    out_s[q * k + o] = o < n ? rs[o] : -INFINITY;
+    out_l[q * k + o] = o < n ? rl[o] : -1;
+  }
+  if (out_c) out_c[q] = n;
+}
+
 // ---------------------------------------------------------------------------
 // IVF list-major work lists
 // ---------------------------------------------------------------------------
@@ -696,11 +725,40 @@ __device__ __forceinline__ int xcd_order_list(int i, int nlist, int *x, bool *fi
   return *x + 8 * j;
 }
 
+// the items of list `lst` in launch phase `phase` (c probing queries from qoff_l, items from o): for each of
+// its row chunks, for each block of <= qchunk probing queries
+__device__ __forceinline__ void ivf_list_items(int lst, int c, int qoff_l, int o, const int32_t *lb, const int32_t *le,
+                                               int qchunk, IvfChunking chk, int phase, int balance, ScanItem *items) {
+  const int len = le[lst] - lb[lst];
+  const int c0 = (chk.warm > 0 && phase == 1) ? 1 : 0;
+  const int c1 = c0 + phase_chunks(lb, le, lst, chk, phase);
+  // balance: the list's ceil(c / qchunk) groups get equal shares rounded up to 16 queries (whole
+  // 16-query MFMA groups) instead of full groups plus a remainder
+  const int ng = (c + qchunk - 1) / qchunk;
+  const int sz = balance && ng > 0 ? ((c + ng - 1) / ng + 15) / 16 * 16 : qchunk;
+  for (int ch = c0; ch < c1; ++ch) {
+    int rb, re;
+    ivf_chunk_rows(len, ch, chk, &rb, &re);
+    for (int gi = 0; gi < ng; ++gi, ++o) {
+      const int b = gi * sz;
+      ScanItem it;
+      it.row_begin = lb[lst] + rb;
+      it.row_end = lb[lst] + re;
+      it.qbeg = qoff_l + min(b, c);
+      it.qcnt = max(0, min(sz, c - b));
+      it.part = ch;
+      it.list = lst;
+      items[o] = it;
+    }
+  }
+}
+
 // single workgroup: qoff = exclusive scan of cnt, ioff = exclusive scan of ceil(cnt/qchunk) * chunks
-// (over the lists in XCD queue order when chk.xcd; n_items[1 + x] = the first item of queue x)
+// (over the lists in XCD queue order when chk.xcd; n_items[1 + x] = the first item of queue x), and each
+// list's items (ivf_list_items; round 4 wrote them in a launch of their own)
 __global__ __launch_bounds__(1024) void ivf_scan_kernel(const int32_t *cnt, int nlist, int qchunk, const int32_t *lb,
                                                         const int32_t *le, IvfChunking chk, int phase, int32_t *qoff,
-                                                        int32_t *ioff, int32_t *n_items) {
+                                                        int32_t *ioff, int32_t *n_items, int balance, ScanItem *items) {
   __shared__ int sq[1024], si[1024];
   const int tid = threadIdx.x;
   const int per = (nlist + 1023) / 1024;
@@ -739,6 +797,7 @@ __global__ __launch_bounds__(1024) void ivf_scan_kernel(const int32_t *cnt, int 
     }
     qoff[l] = rq;
     ioff[l] = ri;
+    ivf_list_items(l, cnt[l], rq, ri, lb, le, qchunk, chk, phase, balance, items);
     rq += cnt[l];
     ri += (cnt[l] + qchunk - 1) / qchunk * phase_chunks(lb, le, l, chk, phase);
   }
@@ -764,39 +823,6 @@ __global__ void ivf_fill_kernel(const int32_t *probes, int64_t nq, int nprobe, i
   const int pos = atomicAdd(&fill[lst], 1);
   qlist[qoff[lst] + pos] = (int32_t)(q * nparts + p * cmax);  // chunk c adds c (ScanItem.part)
   if (qpos) qpos[q * nprobe + p] = qoff[lst] + pos;
-}
-
-// items of list l in launch phase `phase`: for each of its row chunks, for each block of
-// <= qchunk probing queries
-__global__ void ivf_items_kernel(const int32_t *cnt, const int32_t *qoff, const int32_t *ioff, int nlist,
-                                 const int32_t *lb, const int32_t *le, int qchunk, IvfChunking chk, int phase,
-                                 int balance, ScanItem *items) {
-  const int lst = blockIdx.x * blockDim.x + threadIdx.x;
-  if (lst >= nlist) return;
-  const int c = cnt[lst];
-  const int len = le[lst] - lb[lst];
-  const int c0 = (chk.warm > 0 && phase == 1) ? 1 : 0;
-  const int c1 = c0 + phase_chunks(lb, le, lst, chk, phase);
-  int o = ioff[lst];
-  // balance: the list's ceil(c / qchunk) groups get equal shares rounded up to 16 queries (whole
-  // 16-query MFMA groups) instead of full groups plus a remainder
-  const int ng = (c + qchunk - 1) / qchunk;
-  const int sz = balance && ng > 0 ? ((c + ng - 1) / ng + 15) / 16 * 16 : qchunk;
-  for (int ch = c0; ch < c1; ++ch) {
-    int rb, re;
-    ivf_chunk_rows(len, ch, chk, &rb, &re);
-    for (int gi = 0; gi < ng; ++gi, ++o) {
-      const int b = gi * sz;
-      ScanItem it;
-      it.row_begin = lb[lst] + rb;
-      it.row_end = lb[lst] + re;
-      it.qbeg = qoff[lst] + min(b, c);
-      it.qcnt = max(0, min(sz, c - b));
-      it.part = ch;
-      it.list = lst;
-      items[o] = it;
-    }
-  }
 }
 
 __global__ void ivf_limits_kernel(const int32_t *probes, int64_t nq, int nprobe, int nparts, int cmax,
@@ -1439,6 +1465,7 @@ __device__ __forceinline__ float rr_score(const float *qs, const float *rows, in
   return MET == L2 ? -sum : sum;
 }
 
+__device__ void rerun_merge_one(IvfRerunArgs a, const uint64_t *part, int64_t i, int lane);
 template <int MET, int DT, int V = 1>
 __global__ __launch_bounds__(256) void ivf_rerun_scan_kernel(IvfRerunArgs a, uint64_t *part) {
   __shared__ uint64_t wl[4][64];
@@ -1501,13 +1528,22 @@ __global__ __launch_bounds__(256) void ivf_rerun_scan_kernel(IvfRerunArgs a, uin
         cur = rr_merge64_desc(cur > rv ? cur : rv, lane);
       }
       if (lane < k) part[u * k + lane] = cur;
+      if (a.done) {  // the query's last unit merges it (its units' parts are visible after the fences)
+        __threadfence();
+        int last = 0;
+        if (lane == 0) last = atomicAdd(a.done + i, 1) == a.nprobe * nc - 1;
+        if (__shfl(last, 0)) {
+          __threadfence();
+          rerun_merge_one(a, part, i, lane);
+          if (lane == 0) a.done[i] = 0;
+        }
+      }
     }
     __syncthreads();
   }
 }
 
 // one wave per failing query: its nprobe x nc partial lists merged, the top k written at the query's row
-__device__ void rerun_merge_one(IvfRerunArgs a, const uint64_t *part, int64_t i, int lane);
 __global__ __launch_bounds__(256) void ivf_rerun_merge_kernel(IvfRerunArgs a, const uint64_t *part) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t nfail = *a.nfail;
@@ -1672,15 +1708,13 @@ void launch_ivf_items(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t
       hipLaunchKernelGGL(ivf_count_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, probes, nq, nprobe, pb, pe, ws.cnt);
   }
   hipLaunchKernelGGL(ivf_scan_kernel, dim3(1), dim3(1024), 0, st, ws.cnt, nlist, qchunk, list_begin, list_end, ch,
-                     phase, ws.qoff, ws.ioff, ws.n_items);
+                     phase, ws.qoff, ws.ioff, ws.n_items, balance ? 1 : 0, ws.items);
   if (phase == 0 && n > 0 && lds)
     hipLaunchKernelGGL(ivf_fill_lds_kernel, dim3(nblk(n, IVF_EPB)), dim3(256), hb, st, probes, nq, nprobe, pb, pe,
                        nparts, ch.cmax, nlist, ws.qoff, ws.fill, ws.qlist, pb == 0 && pe == nprobe ? ws.qpos : nullptr);
   else if (phase == 0 && n > 0)
     hipLaunchKernelGGL(ivf_fill_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, probes, nq, nprobe, pb, pe, nparts,
                        ch.cmax, ws.qoff, ws.fill, ws.qlist, pb == 0 && pe == nprobe ? ws.qpos : nullptr);
-  hipLaunchKernelGGL(ivf_items_kernel, dim3(nblk(nlist, 256)), dim3(256), 0, st, ws.cnt, ws.qoff, ws.ioff, nlist,
-                     list_begin, list_end, qchunk, ch, phase, balance ? 1 : 0, ws.items);
 }
 
 void launch_ivf_limits(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t nparts, int64_t remaining,
@@ -1952,6 +1986,15 @@ void launch_fill_words(const WordFill &f, hipStream_t st) {
                      f);
 }
 
+void launch_merge_two(const float *as, const int64_t *al, const int32_t *ca, const float *bs, const int64_t *bl,
+                      const int32_t *cb, int64_t nq, int k, float *out_s, int64_t *out_l, int32_t *out_c,
+                      hipStream_t st) {
+  if (nq <= 0 || k <= 0) return;
+  if (k > 64) throw std::invalid_argument("merge_two: k > 64");
+  hipLaunchKernelGGL(merge_two_kernel, dim3(nblk(nq, 128)), dim3(128), 0, st, as, al, ca, bs, bl, cb, nq, k, out_s,
+                     out_l, out_c);
+}
+
 void launch_copy_words(void *dst, const void *src, int64_t words, hipStream_t st) {
   if (words <= 0) return;
   hipLaunchKernelGGL(copy_words_kernel, dim3((unsigned)std::min<int64_t>((words + 255) / 256, 4096)), dim3(256), 0, st,
@@ -1994,8 +2037,9 @@ void launch_ivf_exact_rerun(const IvfRerunArgs &a, int metric, int64_t max_fail,
   else
     by_dim(ivf_rerun_scan_kernel<COS, 32>, ivf_rerun_scan_kernel<COS, 64>, ivf_rerun_scan_kernel<COS, 128>,
            ivf_rerun_scan_kernel<COS, 0>);
-  hipLaunchKernelGGL(ivf_rerun_merge_kernel, dim3((unsigned)std::min<int64_t>((max_fail + 3) / 4, 256)), dim3(256), 0,
-                     st, a, part);
+  if (!a.done)
+    hipLaunchKernelGGL(ivf_rerun_merge_kernel, dim3((unsigned)std::min<int64_t>((max_fail + 3) / 4, 256)), dim3(256),
+                       0, st, a, part);
 }
 
 }  // namespace pyr

@@ -6,7 +6,10 @@ Then it runs the step phase by phase for every rank -- the collectives become te
   * times rank `--rank`'s device work: prepare (its home slice), search (all world x nq queries against
     its lists), merge (the world records of its home queries + certificate), rerun (the gathered failures);
   * checks every home's answers against the unsharded index on the same data (ids and score bits);
-  * prints the per-rank failure counts and the collectives' byte counts (no collective runs on one GPU).
+  * prints the per-rank failure counts and the collectives' byte counts (no collective runs on one GPU);
+  * --oracle N: the first N queries of every home against the CPU oracle (IvfFlatVectorIndex.Search restated,
+    oracle/oracle.c) over the whole data set -- the check for shapes too large for the unsharded index beside
+    the shards (M8: --n 80000000 --nlist 8192 --parity 0 --oracle 25).
 
     python scripts/rank_shape.py --world 8 [--n 10000000 --nlist 1024 --nprobe 32 --nq 10000 --steps 20]
 """
@@ -36,6 +39,7 @@ def main():
     ap.add_argument("--fcap", type=int, default=256)
     ap.add_argument("--train-rows", type=int, default=10_000_000)
     ap.add_argument("--parity", type=int, default=1, help="compare every home's answers with the unsharded index")
+    ap.add_argument("--oracle", type=int, default=0, help="queries per home compared with the CPU oracle")
     args = ap.parse_args()
 
     import torch
@@ -77,6 +81,18 @@ def main():
         full = index_of(np.arange(args.n, dtype=np.int64))
         ref = full.search_batch(qh, k, opts)
         full.close()
+    orc = None
+    if args.oracle:  # the oracle's list-major rows (stable by label, the index's storage order) and its answers
+        import oracle  # checker only
+        xs = data[order]
+        sel = np.concatenate([np.arange(h * nq, h * nq + min(args.oracle, nq)) for h in range(W)])
+        orc = {}
+        t0 = time.time()
+        for i in sel:
+            os_, ok = oracle.ivf_search(qh[i], k, cents, xs, off, metric=0, nprobe=args.nprobe)
+            orc[int(i)] = (os_, order[ok])
+        del xs
+        print(f"[rank_shape] oracle answers for {len(sel)} queries in {time.time() - t0:.1f}s", flush=True)
     del data, srows
     rows = np.bincount(owner, weights=glen, minlength=W)
     print(f"[rank_shape] world {W}: rank rows max/min {rows.max():.0f}/{rows.min():.0f}, built in "
@@ -140,6 +156,11 @@ def main():
         s_, l_ = out_s.cpu().numpy(), out_l.cpu().numpy()
         res["parity"] = {"queries": Q, "ids_equal": bool(np.array_equal(l_, ref[1])),
                          "scores_bit_identical": bool(np.array_equal(s_.view(np.uint32), ref[0].view(np.uint32)))}
+    if orc is not None:
+        s_, l_ = out_s.cpu().numpy(), out_l.cpu().numpy()
+        ok = [bool(np.array_equal(l_[i][:len(kk)], kk) and np.array_equal(s_[i][:len(ss)].view(np.uint32), ss.view(np.uint32)))
+              for i, (ss, kk) in orc.items()]
+        res["oracle_sample"] = {"queries": len(ok), "ids_and_bits_equal": all(ok), "equal": int(sum(ok))}
     # rank R's device phases, each timed over --steps repetitions (the other ranks' records stay as computed)
     phases = {"prepare": lambda: prepare(R), "search": lambda: search(R), "merge": lambda: merge(R),
               "rerun": lambda: (rerun(R), finish(R))}

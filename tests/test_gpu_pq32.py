@@ -154,3 +154,37 @@ def test_pq32_small_chunks_and_forced_failures(hiplib, dim, m):
         got, ph = _profiled(hiplib, lambda: idx.search_batch(q, 10, opts))
     assert ph[PH_FALLBACK][1] == len(q)
     _same(got, ref)
+
+
+@pytest.mark.parametrize("dim,m", [(128, 4), (768, 96)])
+def test_pq32_with_buffer_rows(hiplib, oracle, dim, m):
+    """A non-empty buffer (rows added after Build, IvfPqVectorIndex.cs:130-136): the lists run on pq32 and the
+    buffer exactly beside them, merged (a list entry first on equal scores).  New ids, ids that shadow their
+    list entries (:134, :170) and a deleted buffer row; as the certificates fall and with all forced to fail
+    (the LUT re-run then takes the lists only).  Equal to the LUT path and to the oracle."""
+    from pyrope_amd import SearchOptions, generate_synthetic
+    n = 4000
+    idx, x = _build(dim, m, n, 12)
+    extra = generate_synthetic(60, dim, 5)
+    extra[:5] = x[100:105]  # copies of listed rows under new ids (the queries below include three of them)
+    new = np.concatenate([np.arange(n, n + 40), np.arange(0, 20)]).astype(np.int64)  # the last 20 shadow ids 0..19
+    idx.add_labels(new, extra)
+    assert idx.delete(str(n + 7))
+    q = np.concatenate([generate_synthetic(200, dim, 7), x[100:103]])
+    opts = SearchOptions(nprobe=4)
+    with _env(PYR_PQ_MFMA=0):
+        ref = idx.search_batch(q, 10, opts)
+    for env in ({}, {"PYR_FILTER_CERR": "1e15"}):
+        with _env(**env):
+            got, ph = _profiled(hiplib, lambda: idx.search_batch(q, 10, opts))
+        assert ph[PH_SAMPLE][0] > 0, "the pq32 path did not run"
+        np.testing.assert_array_equal(got[2], ref[2])
+        _same(got, ref)
+    gcb, gcodes, off, labels, live = idx.pq_state()
+    cents = idx.centroids_array()
+    bl = np.array([lab != n + 7 for lab in new.tolist()], np.uint8)
+    for i in list(range(0, 200, 37)) + [200, 201, 202]:
+        os_, ok = oracle.ivfpq_search(q[i], 10, cents, gcodes, off, gcb, live, buf=extra, buf_live=bl, nprobe=4)
+        exp = [new[k - oracle.BUFKEY] if k >= oracle.BUFKEY else labels[k] for k in ok]
+        np.testing.assert_array_equal(got[1][i][: len(exp)], exp)
+        assert np.array_equal(got[0][i][: len(os_)].view(np.uint32), os_.view(np.uint32))
