@@ -694,6 +694,8 @@ static void flush_stream_counters(Workspace &ws) {
 // the device re-run's per-query unit counters (IvfRerunArgs::done): zeroed once when allocated, then left
 // zero by every launch (each merge resets its query's)
 static int32_t *rerun_done(Workspace &ws, int64_t max_fail) {
+  static const bool off = getenv("PYR_RERUN_FUSED") && atoi(getenv("PYR_RERUN_FUSED")) == 0;  // A/B: separate merge
+  if (off) return nullptr;
   const size_t need = sizeof(int32_t) * (size_t)std::max<int64_t>(max_fail, 1);
   if (ws.rrdone.n < need) {
     ws.rrdone.ensure(need);
@@ -2435,7 +2437,9 @@ struct IvfFlatIndex : Index {
     sa.items = ws.items.as<ScanItem>();
     sa.n_items = ws.nitems.as<int32_t>();
     sa.qlist = ws.qlist.as<int32_t>();
-    sa.qpos = ws.qpos.as<int32_t>();  // (build_ivf_items: every probe of every query)
+    // query-major operands (build_ivf_items: every probe of every query) -- not on a list-sharded rank, whose
+    // batch probes mostly lists it does not hold (their pairs get no item: the list-major pass skips them)
+    sa.qpos = sh ? nullptr : ws.qpos.as<int32_t>();
     sa.probes = ws.probes.as<int32_t>();
     sa.nq = nq;
     sa.nparts = nparts;
@@ -2743,10 +2747,12 @@ struct IvfFlatIndex : Index {
     for (int64_t a0 = 0; a0 < nq; a0 += qs) {
       const int64_t n = std::min(qs, nq - a0);
       const float *q = d_q + a0 * dim;
-      reset_stream_counters(ws, n, coarse.nlist);
+      defer_stream_counters(ws, n, coarse.nlist);
+      DeferredCounters dc{ws};
       {
         PhaseTimer t(PH_COARSE, ws.st, n * coarse.nlist);
         coarse.probe(q, nullptr, n, P, metric, ws);
+        flush_stream_counters(ws);
       }
       const IvfChunking ch{512, 1, 0};  // a sample list is one chunk (an empty one too: its sample is empty)
       const int maxi = build_ivf_items(ws, n, P, P, coarse.nlist, sslb, ssle, scan_qmax(dt), ch, 0, true, true);
@@ -2764,6 +2770,9 @@ struct IvfFlatIndex : Index {
       sa.items = ws.items.as<ScanItem>();
       sa.n_items = ws.nitems.as<int32_t>();
       sa.qlist = ws.qlist.as<int32_t>();
+      sa.qpos = ws.qpos.as<int32_t>();  // query-major operands (build_ivf_items: every probe of every query)
+      sa.probes = ws.probes.as<int32_t>();
+      sa.nq = n;
       sa.nparts = P;
       sa.nprobe = P;
       sa.cmax = 1;
@@ -2857,7 +2866,9 @@ struct IvfFlatIndex : Index {
     ra.rec_lb = dlb.as<int32_t>();
     ra.rec_nlist = coarse.nlist;
     PhaseTimer t(PH_FALLBACK, ws.st);
-    ra.done = rerun_done(ws, mf);
+    // (no fused merge here: a rank's re-run list is rarely empty, and the fused merge's agent-scope fences --
+    // L2 write-back / invalidate across the XCDs -- cost more than the launch they save: 0.085 vs 0.077 ms at
+    // the N = 8 rank shape, profiles/r5_i1/rank8_rerun_fused_ab.log)
     ws.rrpart.ensure(sizeof(uint64_t) * ivf_rerun_part_keys(mf, P, k));
     launch_ivf_exact_rerun(ra, metric, mf, ws.rrpart.as<uint64_t>(), ws.st);
     HIPCHK(hipGetLastError());

@@ -641,10 +641,17 @@ __global__ void merge_two_kernel(const float *as, const int64_t *al, const int32
 // IVF list-major work lists
 // ---------------------------------------------------------------------------
 // probes [nq][nprobe]; only probe ranks [pb, pe) of every query take part
-__global__ void ivf_count_kernel(const int32_t *probes, int64_t nq, int nprobe, int pb, int pe, int32_t *cnt) {
+// skip: the lists a rank does not hold (IvfChunking::skip_empty; list_taken) take no (query, probe) entry
+__device__ __forceinline__ bool list_taken(const int32_t *lb, const int32_t *le, int l) {
+  return !lb || le[l] > lb[l];
+}
+__global__ void ivf_count_kernel(const int32_t *probes, int64_t nq, int nprobe, int pb, int pe, int32_t *cnt,
+                                 const int32_t *lb, const int32_t *le) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int np = pe - pb;
-  if (i < nq * np) atomicAdd(&cnt[probes[(i / np) * nprobe + pb + i % np]], 1);
+  if (i >= nq * np) return;
+  const int l = probes[(i / np) * nprobe + pb + i % np];
+  if (list_taken(lb, le, l)) atomicAdd(&cnt[l], 1);
 }
 
 // The same two passes with block-local LDS histograms (nlist <= IVF_LDS_BINS): a block takes
@@ -656,7 +663,8 @@ __global__ void ivf_count_kernel(const int32_t *probes, int64_t nq, int nprobe, 
 constexpr int IVF_LDS_BINS = 16384, IVF_EPT = 16, IVF_EPB = 256 * IVF_EPT;
 
 __global__ __launch_bounds__(256) void ivf_count_lds_kernel(const int32_t *probes, int64_t nq, int nprobe, int pb,
-                                                            int pe, int nlist, int32_t *cnt) {
+                                                            int pe, int nlist, int32_t *cnt, const int32_t *lb,
+                                                            const int32_t *le) {
   extern __shared__ int hist[];
   const int np = pe - pb;
   const int64_t n = nq * np, e0 = (int64_t)blockIdx.x * IVF_EPB;
@@ -664,7 +672,10 @@ __global__ __launch_bounds__(256) void ivf_count_lds_kernel(const int32_t *probe
   __syncthreads();
   for (int j = 0; j < IVF_EPT; ++j) {
     const int64_t i = e0 + j * 256 + threadIdx.x;
-    if (i < n) atomicAdd(&hist[probes[(i / np) * nprobe + pb + i % np]], 1);
+    if (i < n) {
+      const int l = probes[(i / np) * nprobe + pb + i % np];
+      if (list_taken(lb, le, l)) atomicAdd(&hist[l], 1);
+    }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < nlist; i += 256)
@@ -674,7 +685,7 @@ __global__ __launch_bounds__(256) void ivf_count_lds_kernel(const int32_t *probe
 __global__ __launch_bounds__(256) void ivf_fill_lds_kernel(const int32_t *probes, int64_t nq, int nprobe, int pb,
                                                            int pe, int nparts, int cmax, int nlist,
                                                            const int32_t *qoff, int32_t *fill, int32_t *qlist,
-                                                           int32_t *qpos) {
+                                                           int32_t *qpos, const int32_t *lb, const int32_t *le) {
   extern __shared__ int hist[];
   const int np = pe - pb;
   const int64_t n = nq * np, e0 = (int64_t)blockIdx.x * IVF_EPB;
@@ -685,6 +696,7 @@ __global__ __launch_bounds__(256) void ivf_fill_lds_kernel(const int32_t *probes
   for (int j = 0; j < IVF_EPT; ++j) {
     const int64_t i = e0 + j * 256 + threadIdx.x;
     lst[j] = i < n ? probes[(i / np) * nprobe + pb + i % np] : -1;
+    if (lst[j] >= 0 && !list_taken(lb, le, lst[j])) lst[j] = -1;
     rank[j] = lst[j] >= 0 ? atomicAdd(&hist[lst[j]], 1) : 0;
   }
   __syncthreads();
@@ -813,13 +825,15 @@ __global__ __launch_bounds__(1024) void ivf_scan_kernel(const int32_t *cnt, int 
 }
 
 __global__ void ivf_fill_kernel(const int32_t *probes, int64_t nq, int nprobe, int pb, int pe, int nparts, int cmax,
-                                const int32_t *qoff, int32_t *fill, int32_t *qlist, int32_t *qpos) {
+                                const int32_t *qoff, int32_t *fill, int32_t *qlist, int32_t *qpos, const int32_t *lb,
+                                const int32_t *le) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int np = pe - pb;
   if (i >= nq * np) return;
   const int64_t q = i / np;
   const int p = pb + (int)(i % np);
   const int lst = probes[q * nprobe + p];
+  if (!list_taken(lb, le, lst)) return;
   const int pos = atomicAdd(&fill[lst], 1);
   qlist[qoff[lst] + pos] = (int32_t)(q * nparts + p * cmax);  // chunk c adds c (ScanItem.part)
   if (qpos) qpos[q * nprobe + p] = qoff[lst] + pos;
@@ -1694,6 +1708,8 @@ void launch_ivf_items(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t
   const int64_t n = nq * (pe - pb);
   const bool lds = nlist <= IVF_LDS_BINS && !getenv("PYR_IVF_GLOBAL_HIST");  // (knob: measurement only)
   const size_t hb = sizeof(int) * (size_t)nlist;
+  // skip_empty (a list-sharded rank): the (query, probe) entries of the lists it does not hold take no slot
+  const int32_t *skb = ch.skip_empty ? list_begin : nullptr, *ske = ch.skip_empty ? list_end : nullptr;
   if (phase == 0) {
     if (!zeroed) {
       WordFill z;
@@ -1703,18 +1719,20 @@ void launch_ivf_items(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t
     }
     if (n > 0 && lds)
       hipLaunchKernelGGL(ivf_count_lds_kernel, dim3(nblk(n, IVF_EPB)), dim3(256), hb, st, probes, nq, nprobe, pb, pe,
-                         nlist, ws.cnt);
+                         nlist, ws.cnt, skb, ske);
     else if (n > 0)
-      hipLaunchKernelGGL(ivf_count_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, probes, nq, nprobe, pb, pe, ws.cnt);
+      hipLaunchKernelGGL(ivf_count_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, probes, nq, nprobe, pb, pe, ws.cnt, skb,
+                         ske);
   }
   hipLaunchKernelGGL(ivf_scan_kernel, dim3(1), dim3(1024), 0, st, ws.cnt, nlist, qchunk, list_begin, list_end, ch,
                      phase, ws.qoff, ws.ioff, ws.n_items, balance ? 1 : 0, ws.items);
   if (phase == 0 && n > 0 && lds)
     hipLaunchKernelGGL(ivf_fill_lds_kernel, dim3(nblk(n, IVF_EPB)), dim3(256), hb, st, probes, nq, nprobe, pb, pe,
-                       nparts, ch.cmax, nlist, ws.qoff, ws.fill, ws.qlist, pb == 0 && pe == nprobe ? ws.qpos : nullptr);
+                       nparts, ch.cmax, nlist, ws.qoff, ws.fill, ws.qlist, pb == 0 && pe == nprobe ? ws.qpos : nullptr,
+                       skb, ske);
   else if (phase == 0 && n > 0)
     hipLaunchKernelGGL(ivf_fill_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, probes, nq, nprobe, pb, pe, nparts,
-                       ch.cmax, ws.qoff, ws.fill, ws.qlist, pb == 0 && pe == nprobe ? ws.qpos : nullptr);
+                       ch.cmax, ws.qoff, ws.fill, ws.qlist, pb == 0 && pe == nprobe ? ws.qpos : nullptr, skb, ske);
 }
 
 void launch_ivf_limits(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t nparts, int64_t remaining,
