@@ -2437,8 +2437,9 @@ struct IvfFlatIndex : Index {
     sa.items = ws.items.as<ScanItem>();
     sa.n_items = ws.nitems.as<int32_t>();
     sa.qlist = ws.qlist.as<int32_t>();
-    // query-major operands (build_ivf_items: every probe of every query) -- not on a list-sharded rank, whose
-    // batch probes mostly lists it does not hold (their pairs get no item: the list-major pass skips them)
+    // query-major operands (build_ivf_items: every probe of every query) -- not on a list-sharded rank: its batch
+    // is N x the queries, most of whose pairs fall on lists it does not hold (-1 positions); the list-major pass
+    // visits only its items' pairs (80,000 queries at the N = 8 shape: 46 us vs ~100 us query-major)
     sa.qpos = sh ? nullptr : ws.qpos.as<int32_t>();
     sa.probes = ws.probes.as<int32_t>();
     sa.nq = nq;

@@ -696,7 +696,10 @@ __global__ __launch_bounds__(256) void ivf_fill_lds_kernel(const int32_t *probes
   for (int j = 0; j < IVF_EPT; ++j) {
     const int64_t i = e0 + j * 256 + threadIdx.x;
     lst[j] = i < n ? probes[(i / np) * nprobe + pb + i % np] : -1;
-    if (lst[j] >= 0 && !list_taken(lb, le, lst[j])) lst[j] = -1;
+    if (lst[j] >= 0 && !list_taken(lb, le, lst[j])) {
+      lst[j] = -1;
+      if (qpos) qpos[(i / np) * nprobe + pb + i % np] = -1;  // (a dropped entry has no position)
+    }
     rank[j] = lst[j] >= 0 ? atomicAdd(&hist[lst[j]], 1) : 0;
   }
   __syncthreads();
@@ -833,7 +836,10 @@ __global__ void ivf_fill_kernel(const int32_t *probes, int64_t nq, int nprobe, i
   const int64_t q = i / np;
   const int p = pb + (int)(i % np);
   const int lst = probes[q * nprobe + p];
-  if (!list_taken(lb, le, lst)) return;
+  if (!list_taken(lb, le, lst)) {
+    if (qpos) qpos[q * nprobe + p] = -1;  // (a dropped entry has no position)
+    return;
+  }
   const int pos = atomicAdd(&fill[lst], 1);
   qlist[qoff[lst] + pos] = (int32_t)(q * nparts + p * cmax);  // chunk c adds c (ScanItem.part)
   if (qpos) qpos[q * nprobe + p] = qoff[lst] + pos;
@@ -1572,13 +1578,20 @@ __device__ void rerun_merge_one(IvfRerunArgs a, const uint64_t *part, int64_t i,
   const uint64_t *pp = part + (size_t)i * a.nprobe * nc * k;
   const int n = a.nprobe * nc * k;
   uint64_t cur = 0ull;
-  for (int b = 0; b < n; b += 64) {
-    uint64_t v = b + lane < n ? pp[b + lane] : 0ull;
-    const uint64_t kth = rr_shfl64(cur, k - 1);
-    if (!__builtin_amdgcn_ballot_w64(v > kth)) continue;
-    v = rr_sort64_desc(v, lane);
-    const uint64_t rv = rr_shfl64(v, 63 - lane);
-    cur = rr_merge64_desc(cur > rv ? cur : rv, lane);
+  // 8 rows of 64 keys loaded at once (independent loads: one L2 round trip per 512 keys, not per 64)
+  for (int b0 = 0; b0 < n; b0 += 512) {
+    uint64_t vv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) vv[j] = b0 + 64 * j + lane < n ? pp[b0 + 64 * j + lane] : 0ull;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      uint64_t v = vv[j];
+      const uint64_t kth = rr_shfl64(cur, k - 1);
+      if (!__builtin_amdgcn_ballot_w64(v > kth)) continue;
+      v = rr_sort64_desc(v, lane);
+      const uint64_t rv = rr_shfl64(v, 63 - lane);
+      cur = rr_merge64_desc(cur > rv ? cur : rv, lane);
+    }
   }
   const uint64_t real = __builtin_amdgcn_ballot_w64(lane < k && cur != 0ull);
   if (a.rec) {  // list-sharded re-run (shard.hip): the exact local top-k as record rec_pos[i], bound -inf

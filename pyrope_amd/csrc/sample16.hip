@@ -160,14 +160,16 @@ __global__ __launch_bounds__(256) void sprep_q_kernel(StreamArgs a) {
     for (int u = 0; u < PU; ++u) {
       const int p = p0 + u * QW + g;
       const bool ok = p < a.nprobe;
-      lst[u] = ok ? a.probes[(size_t)q * a.nprobe + p] : -1;
       pos[u] = ok ? a.qpos[(size_t)q * a.nprobe + p] : -1;
+      lst[u] = ok ? a.probes[(size_t)q * a.nprobe + p] : -1;
     }
 #pragma unroll
     for (int u = 0; u < PU; ++u) {
+      // (a position a list-sharded rank dropped, -1, loads nothing: most of its batch's pairs)
       const float4 *cp = reinterpret_cast<const float4 *>(a.cents + (size_t)max(lst[u], 0) * D + 8 * sub);
-      c0[u] = cp[0];
-      c1[u] = cp[1];
+      const bool use = pos[u] >= 0 && lst[u] >= 0;
+      c0[u] = use ? cp[0] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      c1[u] = use ? cp[1] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
 #pragma unroll
     for (int u = 0; u < PU; ++u) {

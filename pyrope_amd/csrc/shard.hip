@@ -51,8 +51,11 @@ __global__ void unpack_plan_kernel(const int32_t *plan, int64_t nq, int P, int32
 }
 
 // One wave per record index i: a k-step merge of the nparts sorted entry lists (lane s holds the head of
-// part s), then the certificate.
+// part s), then the certificate.  Up to SM_LDS entries (N = 8, k = 10: 80) are first copied into the wave's
+// LDS with independent loads, so the k steps read LDS instead of a chain of k dependent global loads.
+constexpr int SM_LDS = 256;
 __global__ __launch_bounds__(256) void shard_merge_kernel(ShardMergeArgs a) {
+  __shared__ ShardEntry sent[4][SM_LDS];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * 4 + w;
   int64_t n = a.nrec;
@@ -64,6 +67,15 @@ __global__ __launch_bounds__(256) void shard_merge_kernel(ShardMergeArgs a) {
   const bool mine = lane < a.nparts;
   const uint8_t *rec = a.rec + ((size_t)(mine ? lane : 0) * a.nrec + i) * rb;
   const ShardEntry *ent = reinterpret_cast<const ShardEntry *>(rec);
+  const bool lds = a.nparts * k <= SM_LDS;
+  if (lds) {
+    for (int e = lane; e < a.nparts * k; e += 64) {
+      const int s = e / k, j = e - s * k;
+      sent[w][e] = reinterpret_cast<const ShardEntry *>(a.rec + ((size_t)s * a.nrec + i) * rb)[j];
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
   const ShardTrailer tr = *reinterpret_cast<const ShardTrailer *>(rec + 16 * (size_t)k);
   float bound = mine ? tr.bound : -INFINITY;
   const int cnt = mine ? min(tr.n, k) : 0;
@@ -73,7 +85,7 @@ __global__ __launch_bounds__(256) void shard_merge_kernel(ShardMergeArgs a) {
   for (int r = 0; r < k; ++r) {
     const bool has = head < cnt;
     ShardEntry e;
-    if (has) e = ent[head];
+    if (has) e = lds ? sent[w][lane * k + head] : ent[head];
     float s = has ? e.score : -INFINITY;
     int32_t l = has ? e.list : 0x7FFFFFFF;
     int64_t b = has ? e.label : INT64_MAX;
