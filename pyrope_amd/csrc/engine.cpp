@@ -2026,7 +2026,23 @@ struct IvfFlatIndex : Index {
     nprobe_default = d.default_nprobe > 0 ? d.default_nprobe : 3;  // CombineNProbe (:14)
   }
 
+  // per row slot its list (shard records), rebuilt when the list bounds change
+  DevMem row_list;
+  uint64_t lmeta_gen = 1, rl_gen = 0;
+  std::mutex rl_mu;
+  const int32_t *row_lists(hipStream_t st) {
+    std::lock_guard<std::mutex> lk(rl_mu);
+    if (rl_gen != lmeta_gen) {
+      if (capturing(st)) return nullptr;  // (the records then search the bounds)
+      row_list.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(lists.n, 1));
+      launch_list_ids(dlb.as<int32_t>(), dle.as<int32_t>(), coarse.nlist, row_list.as<int32_t>(), st);
+      rl_gen = lmeta_gen;
+    }
+    return row_list.as<int32_t>();
+  }
+
   void upload_list_meta() {
+    ++lmeta_gen;
     const int nl = coarse.nlist;
     dlb.ensure(sizeof(int32_t) * std::max(nl, 1));
     dle.ensure(sizeof(int32_t) * std::max(nl, 1));
@@ -2574,6 +2590,7 @@ struct IvfFlatIndex : Index {
       r.rec = sh->rec;
       r.rec_lb = dlb.as<int32_t>();
       r.rec_nlist = coarse.nlist;
+      r.rec_row_list = row_lists(ws.st);
       if (fused) launch_merge_refine(m, r, met, 1, ws.st);
       else launch_refine(r, met, 1, ws.st);
       HIPCHK(hipGetLastError());

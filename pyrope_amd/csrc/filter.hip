@@ -205,7 +205,7 @@ __global__ __launch_bounds__(256) void refine_kernel(RefineArgs a) {
       ShardEntry e;
       e.label = a.row_labels ? a.row_labels[key] : (int64_t)key;
       e.score = s;
-      e.list = shard_list_of(a.rec_lb, a.rec_nlist, key);
+      e.list = a.rec_row_list ? a.rec_row_list[key] : shard_list_of(a.rec_lb, a.rec_nlist, key);
       ent[rank] = e;
     }
     if (lane >= nout && lane < k) {
@@ -430,7 +430,28 @@ __global__ __launch_bounds__(256) void merge_refine_kernel(CandMergeArgs m, Refi
   const uint32_t key = mkl >= 0 ? (uint32_t)mkl : KEY_NONE;
   const uint64_t real = __builtin_amdgcn_ballot_w64(key != KEY_NONE);
   float s = -INFINITY;  // lane j: the exact score of candidate j (a row)
+  auto score_one = [&](int32_t kc) -> float {
+    const int64_t rk = kc >= 0 ? (int64_t)kc : 0;
+    if (MET == L2 && a.cosine) {  // VectorMath.Cosine (:102-109) with the cached norms
+      const float dot = a.rows_rm ? exact_score_l8<V, IP, DT, true>(qp, a.rows_rm, rk, D, lane & 7)
+                                  : exact_score_l8<V, IP, DT, false>(qp, a.rows, rk, D, lane & 7);
+      const float qn = a.qnorm[q], xn = a.rnorm[rk];
+      return (qn < 1e-6f || xn < 1e-6f) ? 0.0f : dot / (qn * xn);
+    }
+    return a.rows_rm ? exact_score_l8<V, MET, DT, true>(qp, a.rows_rm, rk, D, lane & 7)
+                     : exact_score_l8<V, MET, DT, false>(qp, a.rows, rk, D, lane & 7);
+  };
   auto score_passes = [&](int p0, int p1) {
+    if (p1 - p0 == 2 && ((real >> (8 * p0)) & 0xFFFFull) != 0ull) {
+      // the depth-16 passes together: both rows' loads in flight before either sum (one round trip, not two)
+      const int c = 8 * p0 + (lane >> 3);
+      const int32_t k0 = __shfl((int)key, c), k1 = __shfl((int)key, c + 8);
+      const float s0 = score_one(k0), s1 = score_one(k1);
+      const float t0 = __shfl(s0, 8 * (lane & 7)), t1 = __shfl(s1, 8 * (lane & 7));
+      if ((lane >> 3) == p0 && key != KEY_NONE) s = t0;
+      if ((lane >> 3) == p0 + 1 && key != KEY_NONE) s = t1;
+      return;
+    }
     for (int p = p0; p < p1; ++p) {
       if (((real >> (8 * p)) & 0xFFull) == 0ull) continue;  // 8 placeholders / empties: nothing to score
       const int c = 8 * p + (lane >> 3);

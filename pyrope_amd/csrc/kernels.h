@@ -556,7 +556,10 @@ struct RefineArgs {
   void *rec;
   const int32_t *rec_lb;
   int32_t rec_nlist;
+  const int32_t *rec_row_list;  // or null: per row slot its list (launch_list_ids), one load instead of a search
 };
+// per list l, out[r] = l for its rows r in [lb[l], le[l]) (the slots' lists, for shard records)
+void launch_list_ids(const int32_t *lb, const int32_t *le, int nlist, int32_t *out, hipStream_t st);
 // unit rows (x / n, 0 when n < 1e-6 or not finite): blocked rows at slots (norms by slot), or row-major
 // x (norms[i]) when slots is null; out row-major n x dim; zflag (may be null) set to 1 by a zero row that
 // is live (live: per row index, null = every row)

@@ -1328,6 +1328,11 @@ __global__ void fill_words_kernel(WordFill f) {
   }
 }
 
+__global__ void list_ids_kernel(const int32_t *lb, const int32_t *le, int32_t *out) {
+  const int l = blockIdx.x;
+  for (int r = lb[l] + threadIdx.x; r < le[l]; r += blockDim.x) out[r] = l;
+}
+
 __global__ void copy_words_kernel(uint32_t *dst, const uint32_t *src, int64_t n) {
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x)
     dst[e] = src[e];
@@ -2024,6 +2029,11 @@ void launch_merge_two(const float *as, const int64_t *al, const int32_t *ca, con
   if (k > 64) throw std::invalid_argument("merge_two: k > 64");
   hipLaunchKernelGGL(merge_two_kernel, dim3(nblk(nq, 128)), dim3(128), 0, st, as, al, ca, bs, bl, cb, nq, k, out_s,
                      out_l, out_c);
+}
+
+void launch_list_ids(const int32_t *lb, const int32_t *le, int nlist, int32_t *out, hipStream_t st) {
+  if (nlist <= 0) return;
+  hipLaunchKernelGGL(list_ids_kernel, dim3((unsigned)nlist), dim3(256), 0, st, lb, le, out);
 }
 
 void launch_copy_words(void *dst, const void *src, int64_t words, hipStream_t st) {
