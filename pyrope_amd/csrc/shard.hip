@@ -81,6 +81,8 @@ __global__ __launch_bounds__(256) void shard_merge_kernel(ShardMergeArgs a) {
   const int cnt = mine ? min(tr.n, k) : 0;
   int head = 0;
   int produced = 0;
+  int lvl = 1;  // the largest butterfly offset that covers lanes 0 .. nparts - 1
+  while (2 * lvl < a.nparts) lvl <<= 1;
   float kth = -INFINITY;
   for (int r = 0; r < k; ++r) {
     const bool has = head < cnt;
@@ -90,9 +92,9 @@ __global__ __launch_bounds__(256) void shard_merge_kernel(ShardMergeArgs a) {
     int32_t l = has ? e.list : 0x7FFFFFFF;
     int64_t b = has ? e.label : INT64_MAX;
     int src = has ? lane : 64;
-    // wave argmax under entry_better (ties between parts cannot happen: a row lives on one rank)
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
+    // wave argmax under entry_better (ties between parts cannot happen: a row lives on one rank) over the
+    // lanes that hold a part: log2(nparts) butterfly levels (N = 8: 3, not 6), then lane 0's winner to all
+    for (int off = lvl; off >= 1; off >>= 1) {
       const float s2 = __shfl_xor(s, off);
       const int32_t l2 = __shfl_xor(l, off);
       const int64_t b2 = __shfl_xor(b, off);
@@ -106,6 +108,10 @@ __global__ __launch_bounds__(256) void shard_merge_kernel(ShardMergeArgs a) {
         src = src2;
       }
     }
+    s = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s)));  // (lane 0 is active: a uniform loop)
+    b = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)((uint64_t)b >> 32)) << 32) |
+                  (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uint64_t)b));
+    src = __builtin_amdgcn_readfirstlane(src);
     if (src == 64) break;  // every part is exhausted
     if (lane == src) ++head;
     if (lane == 0) {
