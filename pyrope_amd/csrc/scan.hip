@@ -345,16 +345,26 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
       // from hoisting 16 per-position words out of the group loop (they spilled)
       uint32_t base = ((uint32_t)qi << 23) | (uint32_t)(rt - r0 + 4 * h);
       asm volatile("" : "+v"(base));
+      // 4-row blocks first (a block's max, one ballot): an emitting (tile, group) usually holds one row
+      // above the threshold, so 4 block tests + 4 row tests instead of 16 row tests
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const bool p = y[e] >= thr;
-        if (__builtin_amdgcn_ballot_w64(p) == 0ull) continue;
-        if (p) {
-          const float sc = y[e] + cq;
-          const uint32_t word = base + (uint32_t)(8 * (e >> 2) + (e & 3));
-          const int at = stage ? atomicAdd(&eb_n, 1) : EB;
-          if (at < EB) eb[at] = make_uint2(__float_as_uint(sc), word);
-          else put(qi, sc, r0 + (int)(word & 0x7FFFFFu));
+      for (int b = 0; b < 4; ++b) {
+        if constexpr (AB != 7) {  // (AB 7: every row tested, round 4's loop; A/B only)
+          const float bm = fmaxf(max3f(y[4 * b], y[4 * b + 1], y[4 * b + 2]), y[4 * b + 3]);
+          if (__builtin_amdgcn_ballot_w64(bm >= thr) == 0ull) continue;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int e = 4 * b + i;
+          const bool p = y[e] >= thr;
+          if (__builtin_amdgcn_ballot_w64(p) == 0ull) continue;
+          if (p) {
+            const float sc = y[e] + cq;
+            const uint32_t word = base + (uint32_t)(8 * (e >> 2) + (e & 3));
+            const int at = stage ? atomicAdd(&eb_n, 1) : EB;
+            if (at < EB) eb[at] = make_uint2(__float_as_uint(sc), word);
+            else put(qi, sc, r0 + (int)(word & 0x7FFFFFu));
+          }
         }
       }
     };
@@ -502,6 +512,10 @@ void launch_scan_dm(const StreamArgs &a, int max_items, hipStream_t st) {
     }
     if (a.ablate & 1024) {
       hipLaunchKernelGGL((scan_kernel<D, MET, 4>), dim3(grid), b, 0, st, a);
+      return;
+    }
+    if (a.ablate & 2048) {  // A/B: the emit loop tests every row (no 4-row block test)
+      hipLaunchKernelGGL((scan_kernel<D, MET, 7>), dim3(grid), b, 0, st, a);
       return;
     }
   }
