@@ -282,16 +282,23 @@ __device__ __forceinline__ void pq_emit(const StreamArgs &a, f16v acc, int g, in
   const float cq = L.qz[qi].x;
   uint32_t base = ((uint32_t)qi << 23) | (uint32_t)(rt - r0 + 4 * h);
   asm volatile("" : "+v"(base));
+  // 4-row blocks first (one ballot each), then the rows of a block that can emit (as scan.hip's emit_y)
 #pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    const bool p = acc[e] >= q.y;
-    if (__builtin_amdgcn_ballot_w64(p) == 0ull) continue;
-    if (p) {
-      const float sc = acc[e] + cq;
-      const uint32_t word = base + (uint32_t)(8 * (e >> 2) + (e & 3));
-      const int at = stage ? atomicAdd(&L.eb_n, 1) : PEB;
-      if (at < PEB) L.eb[at] = make_uint2(__float_as_uint(sc), word);
-      else cand_put(a, __float_as_int(L.qz[qi].y), sc, a.key_base | (uint32_t)(r0 + (int)(word & 0x7FFFFFu)));
+  for (int b = 0; b < 4; ++b) {
+    const float bm = fmaxf(max3f(acc[4 * b], acc[4 * b + 1], acc[4 * b + 2]), acc[4 * b + 3]);
+    if (__builtin_amdgcn_ballot_w64(bm >= q.y) == 0ull) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = 4 * b + i;
+      const bool p = acc[e] >= q.y;
+      if (__builtin_amdgcn_ballot_w64(p) == 0ull) continue;
+      if (p) {
+        const float sc = acc[e] + cq;
+        const uint32_t word = base + (uint32_t)(8 * (e >> 2) + (e & 3));
+        const int at = stage ? atomicAdd(&L.eb_n, 1) : PEB;
+        if (at < PEB) L.eb[at] = make_uint2(__float_as_uint(sc), word);
+        else cand_put(a, __float_as_int(L.qz[qi].y), sc, a.key_base | (uint32_t)(r0 + (int)(word & 0x7FFFFFu)));
+      }
     }
   }
 }
