@@ -2878,7 +2878,9 @@ struct IvfFlatIndex : Index {
     ra.nfail = ws.fail_cnt.as<int32_t>();
     ra.dim = dim;
     ra.k = k;
-    ra.nchunk = (int32_t)std::max<int64_t>(1, std::min<int64_t>(64, (max_len + 1023) / 1024));
+    // a rank re-runs a handful of queries over the few of their lists it holds: 4,096-row chunks (1,024 would
+    // cut each probed list 10-18 ways and leave one wave ~6k partial keys to merge per query)
+    ra.nchunk = (int32_t)std::max<int64_t>(1, std::min<int64_t>(64, (max_len + 4095) / 4096));
     ra.rec = d_rec;
     ra.rec_pos = ws.rpos.as<int32_t>();
     ra.rec_lb = dlb.as<int32_t>();
