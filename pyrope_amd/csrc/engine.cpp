@@ -737,11 +737,23 @@ static int store16_dt(int dim) { return scan_tile_dim(dim); }
 // sample at every dim (measurement only).
 // prep_only: the operands without the sample where the native-dim pass allows it (the one-wave pass writes
 // both; its sample values are then simply not read)
+// Round 5: at those dims the sample itself runs on the main scan kernel (scan.hip SMP: 16 waves, one sampled
+// tile each, 32x32x16 MFMAs, every query group of the item) after sprep's operands; PYR_SAMPLE16=1 keeps
+// sample16_kernel (A/B: both write the same samp layout; T_q may differ in its last bits, the answers do not).
 static void stream_sample(const StreamArgs &sa, int met, int maxi, hipStream_t st, bool prep_only = false) {
   const char *e = getenv("PYR_SCAN_SAMPLE");
   const int dt = sa.dt > 0 ? sa.dt : sa.dim;
-  if (!(e && atoi(e) == 1) && dt == sa.dim && sample16_supported(sa.dim, met)) launch_sample16(sa, met, maxi, st, prep_only);
-  else launch_scan_sample(sa, met, maxi, st);
+  static const bool s16 = getenv("PYR_SAMPLE16") && atoi(getenv("PYR_SAMPLE16")) == 1;
+  if (!(e && atoi(e) == 1) && dt == sa.dim && sample16_supported(sa.dim, met)) {
+    if (s16 || !scan_sample_mode_supported(dt)) {
+      launch_sample16(sa, met, maxi, st, prep_only);
+    } else {
+      launch_sample16(sa, met, maxi, st, true);  // the operands only
+      if (!prep_only) launch_scan_sample_mode(sa, met, maxi, st);
+    }
+  } else {
+    launch_scan_sample(sa, met, maxi, st);
+  }
 }
 // T_q = the R-th largest sample value.  Any R is correct (rows below T_q are represented by floor
 // placeholders at T_q and the certificate decides); R trades emitted rows against queries with fewer

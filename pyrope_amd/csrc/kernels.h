@@ -493,6 +493,10 @@ void launch_chunk_lists(int32_t *lb, int32_t *le, int nch, int64_t crow, int64_t
 void launch_iota_rows(int32_t *out, int64_t rows, int cols, hipStream_t st);
 void launch_scan_sample(const StreamArgs &a, int metric, int max_items, hipStream_t st);
 void launch_scan_main(const StreamArgs &a, int metric, int max_items, hipStream_t st);
+// the sample pass on the main scan kernel (scan.hip, SMP): same samp layout and count as sample16 (bq / qsc
+// prepared beforehand); tile dims whose blocks have SAMPLE_TILES waves
+bool scan_sample_mode_supported(int dt);
+void launch_scan_sample_mode(const StreamArgs &a, int metric, int max_items, hipStream_t st);
 bool sample16_supported(int dim, int metric);  // dim == tile dim in {32, 64, 128}, L2 / IP
 // prep_only: the query operands (bq, qsc) without the sample (a list-sharded scan takes T_q from its plan)
 void launch_sample16(const StreamArgs &a, int metric, int max_items, hipStream_t st, bool prep_only = false);

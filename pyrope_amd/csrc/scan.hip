@@ -219,7 +219,11 @@ __global__ __launch_bounds__(256) void sample_kernel(StreamArgs a) {
 // 3 (256) = no emission and every tile read from the item's first one (compute without HBM); the bit 512
 // (any variant) adds an L2 prefetch of the wave's next tile (4-byte LDS-DMA per line; measured slower:
 // 0.94 vs 0.90 ms and FETCH 1.83x vs 1.09x the stored bytes at I1, profiles/r4_scan)
-template <int D, int MET, int AB = 0>
+// SMP: the sample pass on the same kernel (round 5): chunk-0 items only, wave w scores tile w of the list
+// (SAMPLE_TILES = 16 = the waves of a block at D <= 128) against every query group, and writes per (query,
+// probe) the 2 x 16 values max(f acc + row term) + cq over its lane half's rows -- each the bound of distinct
+// rows, as sample16_kernel's -- into samp; no emission.
+template <int D, int MET, int AB = 0, bool SMP = false>
 __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
   constexpr int NW = nw_of(D);       // waves per block
   constexpr int KS = D / 16;         // 32x32x16 k-steps
@@ -268,6 +272,7 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
       return;
     }
     const ScanItem it = a.items[item];
+    if (SMP && it.part != 0) continue;  // (block-uniform) chunk-0 items cover every (list, query) pair once
     stamp(-1);
     tb[4] += 1;
     const int qcnt = it.qcnt, ng = (qcnt + 31) >> 5;
@@ -289,10 +294,10 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
           const int pos = it.qbeg + i;
           const int slot = a.qlist[pos];
           const float2 fc = a.qsc[pos];
-          const float T = a.thr ? a.thr[slot / a.nparts] + a.thr_bias : -INFINITY;
+          const float T = (!SMP && a.thr) ? a.thr[slot / a.nparts] + a.thr_bias : -INFINITY;
           v = make_float2(fc.x, lower_thr(T, fc.y));
           cqv = fc.y;
-          o = slot / a.nparts;
+          o = SMP ? (slot / a.nparts) * a.nprobe + (slot % a.nparts) / a.cmax : slot / a.nparts;
         }
         qf[i] = v;
         qz[i] = make_float2(cqv, __int_as_float(o));
@@ -308,7 +313,7 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
     }
 
     const int r0 = it.row_begin;  // multiple of 32
-    const int nt = (it.row_end - r0 + 31) >> 5;
+    const int nt = SMP ? min((it.row_end - r0 + 31) >> 5, SAMPLE_TILES) : (it.row_end - r0 + 31) >> 5;
     const int rlim = (int)min((int64_t)it.row_end, (int64_t)a.row_limit);
     const bool stage = it.row_end - r0 < (1 << 23);  // row offsets fit the staged word
 
@@ -471,6 +476,41 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
       }
     };
 
+    if constexpr (SMP) {
+      static_assert(NW == SAMPLE_TILES && NC == 1, "the sample mode: one tile per wave, tiles in registers");
+      float smx[NG];
+#pragma unroll
+      for (int g = 0; g < NG; ++g) smx[g] = -INFINITY;
+      if (w < nt) {  // tile w of the list (nt: the item's tiles; the first SAMPLE_TILES of them)
+        h8v A[KC];
+        f4v M[4];
+        float mr[16];
+        load(w, A, M);
+        row_terms(M, w, mr);
+#pragma unroll
+        for (int j = 0; j < NG; ++j) {
+          if (j >= ng) break;  // (wave-uniform)
+          const float2 q = qf[32 * j + r];
+          h8v bj[KS];
+          read_b(j, bj);
+          f16v acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[0], bj[0], (f16v){}, 0, 0, 0);
+#pragma unroll
+          for (int s = 1; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[s], bj[s], acc, 0, 0, 0);
+          float mx = fmaf(q.x, acc[0], mr[0]);
+#pragma unroll
+          for (int v = 1; v < 16; ++v) mx = fmaxf(mx, fmaf(q.x, acc[v], mr[v]));
+          smx[j] = mx;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NG; ++j) {
+        if (j >= ng) break;
+        const int qi = 32 * j + r;
+        if (qi < qcnt) a.samp[(size_t)__float_as_int(qz[qi].y) * SV + 2 * w + h] = smx[j] + qz[qi].x;
+      }
+      __syncthreads();  // every wave is done with the item's LDS before the next prologue
+      continue;
+    }
     int t = w;
     while (t < nt) {
       h8v A[KC];
@@ -520,6 +560,14 @@ void launch_scan_dm(const StreamArgs &a, int max_items, hipStream_t st) {
     }
   }
   hipLaunchKernelGGL((scan_kernel<D, MET>), dim3(grid), b, 0, st, a);
+}
+
+template <int D, int MET>
+void launch_scan_sample_dm(const StreamArgs &a, int max_items, hipStream_t st) {
+  if constexpr (nw_of(D) == SAMPLE_TILES && D / 16 <= 16) {
+    const int grid = std::max(1, std::min(max_items, device_cus()));
+    hipLaunchKernelGGL((scan_kernel<D, MET, 0, true>), dim3(grid), dim3(64 * nw_of(D)), 0, st, a);
+  }
 }
 
 template <int D, int MET>
@@ -587,6 +635,13 @@ void launch_scan_sample(const StreamArgs &a, int metric, int max_items, hipStrea
   if (max_items <= 0) return;
   const int dt = a.dt > 0 ? a.dt : a.dim;
   PYR_SCAN_BY_DIM(launch_sample_dm)
+}
+
+bool scan_sample_mode_supported(int dt) { return nw_of(dt) == SAMPLE_TILES && dt / 16 <= 16; }
+void launch_scan_sample_mode(const StreamArgs &a, int metric, int max_items, hipStream_t st) {
+  if (max_items <= 0) return;
+  const int dt = a.dt > 0 ? a.dt : a.dim;
+  PYR_SCAN_BY_DIM(launch_scan_sample_dm)
 }
 
 void launch_scan_main(const StreamArgs &a, int metric, int max_items, hipStream_t st) {
