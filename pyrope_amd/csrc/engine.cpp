@@ -694,7 +694,7 @@ static void flush_stream_counters(Workspace &ws) {
 // the device re-run's per-query unit counters (IvfRerunArgs::done): zeroed once when allocated, then left
 // zero by every launch (each merge resets its query's)
 static int32_t *rerun_done(Workspace &ws, int64_t max_fail) {
-  static const bool off = getenv("PYR_RERUN_FUSED") && atoi(getenv("PYR_RERUN_FUSED")) == 0;  // A/B: separate merge
+  const bool off = getenv("PYR_RERUN_FUSED") && atoi(getenv("PYR_RERUN_FUSED")) == 0;  // A/B: separate merge
   if (off) return nullptr;
   const size_t need = sizeof(int32_t) * (size_t)std::max<int64_t>(max_fail, 1);
   if (ws.rrdone.n < need) {
@@ -743,7 +743,7 @@ static int store16_dt(int dim) { return scan_tile_dim(dim); }
 static void stream_sample(const StreamArgs &sa, int met, int maxi, hipStream_t st, bool prep_only = false) {
   const char *e = getenv("PYR_SCAN_SAMPLE");
   const int dt = sa.dt > 0 ? sa.dt : sa.dim;
-  static const bool s16 = getenv("PYR_SAMPLE16") && atoi(getenv("PYR_SAMPLE16")) == 1;
+  const bool s16 = getenv("PYR_SAMPLE16") && atoi(getenv("PYR_SAMPLE16")) == 1;
   if (!(e && atoi(e) == 1) && dt == sa.dim && sample16_supported(sa.dim, met)) {
     if (s16 || !scan_sample_mode_supported(dt)) {
       launch_sample16(sa, met, maxi, st, prep_only);
