@@ -740,13 +740,13 @@ __device__ __forceinline__ int xcd_order_list(int i, int nlist, int *x, bool *fi
   return *x + 8 * j;
 }
 
-// the items of list `lst` in launch phase `phase` (c probing queries from qoff_l, items from o): for each of
-// its row chunks, for each block of <= qchunk probing queries
-__device__ __forceinline__ void ivf_list_items(int lst, int c, int qoff_l, int o, const int32_t *lb, const int32_t *le,
-                                               int qchunk, IvfChunking chk, int phase, int balance, ScanItem *items) {
-  const int len = le[lst] - lb[lst];
+// the items of list `lst` (rows [lb0, lb0 + len)) in launch phase `phase` (c probing queries from qoff_l,
+// items from o): for each of its row chunks, for each block of <= qchunk probing queries
+__device__ __forceinline__ void ivf_list_items(int lst, int c, int qoff_l, int o, int lb0, int len, int qchunk,
+                                               IvfChunking chk, int phase, int balance, ScanItem *items) {
   const int c0 = (chk.warm > 0 && phase == 1) ? 1 : 0;
-  const int c1 = c0 + phase_chunks(lb, le, lst, chk, phase);
+  const int nch = ivf_list_chunks(len, chk);
+  const int c1 = c0 + (chk.warm <= 0 ? nch : (phase == 0 ? 1 : nch - 1));
   // balance: the list's ceil(c / qchunk) groups get equal shares rounded up to 16 queries (whole
   // 16-query MFMA groups) instead of full groups plus a remainder
   const int ng = (c + qchunk - 1) / qchunk;
@@ -757,8 +757,8 @@ __device__ __forceinline__ void ivf_list_items(int lst, int c, int qoff_l, int o
     for (int gi = 0; gi < ng; ++gi, ++o) {
       const int b = gi * sz;
       ScanItem it;
-      it.row_begin = lb[lst] + rb;
-      it.row_end = lb[lst] + re;
+      it.row_begin = lb0 + rb;
+      it.row_end = lb0 + re;
       it.qbeg = qoff_l + min(b, c);
       it.qcnt = max(0, min(sz, c - b));
       it.part = ch;
@@ -784,11 +784,22 @@ __global__ __launch_bounds__(1024) void ivf_scan_kernel(const int32_t *cnt, int 
     bool f;
     return xcd_order_list(i, nlist, &x, &f);
   };
+  // (4 lists at a time with their loads issued together: at nlist = 8,192 a thread owns 8 lists, and one
+  // dependent load chain per list made this single block a 50 us launch)
   int lq = 0, li = 0;
-  for (int i = b; i < e; ++i) {
-    const int l = at(i);
-    lq += cnt[l];
-    li += (cnt[l] + qchunk - 1) / qchunk * phase_chunks(lb, le, l, chk, phase);
+  for (int i0 = b; i0 < e; i0 += 4) {
+    int c4[4], n4[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int l = i0 + u < e ? at(i0 + u) : 0;
+      c4[u] = i0 + u < e ? cnt[l] : 0;
+      n4[u] = i0 + u < e ? phase_chunks(lb, le, l, chk, phase) : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      lq += c4[u];
+      li += (c4[u] + qchunk - 1) / qchunk * n4[u];
+    }
   }
   sq[tid] = lq;
   si[tid] = li;
@@ -802,19 +813,32 @@ __global__ __launch_bounds__(1024) void ivf_scan_kernel(const int32_t *cnt, int 
     __syncthreads();
   }
   int rq = sq[tid] - lq, ri = si[tid] - li;
-  for (int i = b; i < e; ++i) {
-    int l = i;
-    if (chk.xcd) {
-      int x;
-      bool first;
-      l = xcd_order_list(i, nlist, &x, &first);
-      if (first) n_items[1 + x] = ri;
+  for (int i0 = b; i0 < e; i0 += 4) {
+    int l4[4], c4[4], b4[4], n4[4], x4[4];
+    bool f4[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u;
+      x4[u] = 0;
+      f4[u] = false;
+      l4[u] = i < e ? (chk.xcd ? xcd_order_list(i, nlist, &x4[u], &f4[u]) : i) : -1;
+      const int l = max(l4[u], 0);
+      c4[u] = l4[u] >= 0 ? cnt[l] : 0;
+      b4[u] = l4[u] >= 0 ? lb[l] : 0;
+      n4[u] = l4[u] >= 0 ? le[l] - b4[u] : 0;
     }
-    qoff[l] = rq;
-    ioff[l] = ri;
-    ivf_list_items(l, cnt[l], rq, ri, lb, le, qchunk, chk, phase, balance, items);
-    rq += cnt[l];
-    ri += (cnt[l] + qchunk - 1) / qchunk * phase_chunks(lb, le, l, chk, phase);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (l4[u] < 0) continue;
+      const int l = l4[u];
+      if (chk.xcd && f4[u]) n_items[1 + x4[u]] = ri;
+      qoff[l] = rq;
+      ioff[l] = ri;
+      ivf_list_items(l, c4[u], rq, ri, b4[u], n4[u], qchunk, chk, phase, balance, items);
+      const int nch = ivf_list_chunks(n4[u], chk);
+      rq += c4[u];
+      ri += (c4[u] + qchunk - 1) / qchunk * (chk.warm <= 0 ? nch : (phase == 0 ? 1 : nch - 1));
+    }
   }
   if (tid == 1023) {
     qoff[nlist] = sq[1023];

@@ -3,10 +3,12 @@
 // The stream-and-emit scan (scan.hip) emits every row whose approximate score can reach its query's
 // threshold T_q.  This file holds the steps around it:
 //
-//  1. sprep_kernel: per (list, query) pair (the work lists' qlist order) the query's residual q - c
+//  1. sprep_q_kernel (round 5; query-major over the positions the work lists recorded) / sprep_kernel (list-major;
+//     list-sharded ranks): per (list, query) pair the query's residual q - c
 //     (L2) or q (IP), scaled by a power of two and rounded to fp16, plus the score factor f and the
 //     per-(query, list) constant cq -- once, instead of in every block that scans the list.
-//  2. sample16_kernel: persistent blocks (one per CU, 8 waves) take the chunk-0 work items (list,
+//  2. sample16_kernel (since round 5 the A/B path, PYR_SAMPLE16=1: the sample runs on scan.hip's scan_kernel in
+//     its SMP mode after sprep; both write the same samp layout): persistent blocks (one per CU, 8 waves) take the chunk-0 work items (list,
 //     <= 512 queries) from a counter.  The item's query operands go to LDS (LDS-DMA, 128 KiB at
 //     D = 128); each wave holds two of the list's first 16 tiles in registers and scores them against
 //     every query group of the item on v_mfma_f32_16x16x32_f16 with the ROWS as the A operand (lane
