@@ -660,7 +660,7 @@ __global__ void ivf_count_kernel(const int32_t *probes, int64_t nq, int nprobe, 
 // atomic and places entries by their LDS rank.  320k entries into 1,024 lists: ~80k global atomics
 // instead of 320k on 1,024 addresses.  (Entry order inside a list differs from the one-atomic-per-
 // entry pass; it is arbitrary in both, and results do not depend on it.)
-constexpr int IVF_LDS_BINS = 16384, IVF_EPT = 16, IVF_EPB = 256 * IVF_EPT;
+constexpr int IVF_LDS_BINS = 16384, IVF_EPT = 4, IVF_EPB = 256 * IVF_EPT;  // (EPT 16 left 79 blocks at I1)
 
 __global__ __launch_bounds__(256) void ivf_count_lds_kernel(const int32_t *probes, int64_t nq, int nprobe, int pb,
                                                             int pe, int nlist, int32_t *cnt, const int32_t *lb,
