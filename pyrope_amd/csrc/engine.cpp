@@ -905,6 +905,12 @@ struct CosRefine {
 // the stream scans' candidate merge and certified refine fused into one kernel (filter.hip
 // merge_refine_kernel); PYR_MERGE_REFINE=0 (A/B) and PYR_STREAM_DEBUG (it reads the merged candidates back)
 // take cand_merge + the two refine launches
+// PYR_MAXSCANS_STREAM=0: an IVF search with a MaxScans budget takes the exact scan (A/B; read per search)
+static bool max_scans_stream() {
+  const char *e = getenv("PYR_MAXSCANS_STREAM");
+  return !(e && atoi(e) == 0);
+}
+
 static bool merge_refine_fused() {
   const char *e = getenv("PYR_MERGE_REFINE");
   return !(e && atoi(e) == 0) && !getenv("PYR_STREAM_DEBUG");
@@ -2311,15 +2317,24 @@ struct IvfFlatIndex : Index {
       fill_empty_results(d_s, d_l, d_c, nq, std::max(k, 0), ws.st);
       return;
     }
-    // MFMA filter path: built lists only (empty pre-build buffer), no MaxScans, L2 / IP
+    // MFMA filter path: built lists only (empty pre-build buffer), L2 / IP / Cosine; a MaxScans budget bounds
+    // each (query, list) pair's rows (stream_slice), MaxScans 0 scans nothing (the exact path's empty answer)
     const int nprobe = prm.nprobe < 0 ? nprobe_default : prm.nprobe;
     const int probes = (built && coarse.nlist > 0) ? std::max(0, std::min(nprobe, coarse.nlist)) : 0;
     const int k1 = filter_k1(k);
-    const bool fast = filter_enabled() && probes > 0 && buf.live_count() == 0 && prm.max_scans < 0 &&
-                      k <= KMAX_FAST && probes < MAX_PARTS && k1 > 0;
+    const bool budget_ok = prm.max_scans < 0 || (prm.max_scans > 0 && !ws.ext_probes && max_scans_stream());
+    const bool fast = filter_enabled() && probes > 0 && buf.live_count() == 0 && budget_ok && k <= KMAX_FAST &&
+                      probes < MAX_PARTS && k1 > 0;
     // the stream scan (L2 / IP, and Cosine over the unit residual tiles with the exact Cosine in the refine)
     if (fast && stream_ok(k1)) {
-      search_stream(d_q, nq, k, k1, probes, d_s, d_l, d_c, ws);
+      ws.max_scans = prm.max_scans;
+      try {
+        search_stream(d_q, nq, k, k1, probes, d_s, d_l, d_c, ws);
+      } catch (...) {
+        ws.max_scans = -1;
+        throw;
+      }
+      ws.max_scans = -1;
       return;
     }
     search_exact(d_q, nq, k, prm, d_s, d_l, d_c, ws);
@@ -2447,6 +2462,18 @@ struct IvfFlatIndex : Index {
       maxi = build_ivf_items(ws, nq, probes, nparts, coarse.nlist, dlb, dle, qmax, ch, 0, true, true);
     }
     const int64_t npos = nq * probes;
+    // MaxScans (:202-212; the buffer is empty here): every pair's exclusive row bound, in probe order over the
+    // live rows (ivf_limits_kernel, one chunk per probe), then at its qlist position for the scan kernel
+    const bool budget = ws.max_scans > 0 && !sh;
+    if (budget) {
+      ws.limits.ensure(sizeof(uint32_t) * std::max<int64_t>(npos, 1));
+      ws.plim.ensure(sizeof(uint32_t) * std::max<int64_t>(npos, 1));
+      IvfChunking c1{1, 1, 0};
+      launch_ivf_limits(ws.probes.as<int32_t>(), nq, probes, probes, ws.max_scans, dlb.as<int32_t>(),
+                        dle.as<int32_t>(), dllive.as<int32_t>(), lists.live.as<uint8_t>(), c1,
+                        ws.limits.as<uint32_t>(), ws.st);
+      launch_pos_limits(ws.qpos.as<int32_t>(), ws.limits.as<uint32_t>(), npos, ws.plim.as<uint32_t>(), ws.st);
+    }
     const int sv = scan_sample_values();
     ws.sbq.ensure(sizeof(uint16_t) * std::max<int64_t>(npos, 1) * lists.tdim());
     ws.sqsc.ensure(sizeof(float2) * std::max<int64_t>(npos, 1));
@@ -2469,6 +2496,7 @@ struct IvfFlatIndex : Index {
     // is N x the queries, most of whose pairs fall on lists it does not hold (-1 positions); the list-major pass
     // visits only its items' pairs (80,000 queries at the N = 8 shape: 46 us vs ~100 us query-major)
     sa.qpos = sh ? nullptr : ws.qpos.as<int32_t>();
+    sa.plim = budget ? ws.plim.as<uint32_t>() : nullptr;
     sa.probes = ws.probes.as<int32_t>();
     sa.nq = nq;
     sa.nparts = nparts;
@@ -2663,6 +2691,7 @@ struct IvfFlatIndex : Index {
     ra.out_s = d_s;
     ra.out_l = d_l;
     ra.out_c = d_c;
+    ra.qlim = budget ? ws.limits.as<uint32_t>() : nullptr;
     // (measurement-only knobs that change the candidates skip the re-run: PYR_FILTER_ABLATE,
     // PYR_STREAM_THR_BIAS)
     if (!filter_ablate() && !getenv("PYR_STREAM_THR_BIAS")) {

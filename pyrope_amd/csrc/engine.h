@@ -181,6 +181,8 @@ struct Workspace {
   DevMem vlb, vle, vcents;  // FLAT on the stream scan: its chunks as lists (FlatIndex::search_stream)
   DevMem cq, ccs, ccl, ccc;  // Cosine on the filter path: unit queries, inner-product candidates
   DevMem shp, shthr, rpos;  // list-sharded search: unpacked plan (probes, T_q), re-run record slots
+  DevMem plim;              // IVF stream search with MaxScans: the pairs' row bounds at their qlist positions
+  int64_t max_scans = -1;   // the MaxScans of the IVF stream search in progress (-1: none)
   uint64_t wgen_seen = 0;                         // the index's write generation this stream is ordered after
   const int32_t *ext_probes = nullptr;            // caller-ranked probe lists [nq][ext_nprobe] (multi-GPU)
   bool skip_buffer = false;                       // IVF_PQ LUT scan: the lists only (the buffer merged by the caller)

@@ -183,6 +183,9 @@ struct IvfRerunArgs {
   // or null: per failing query the units done (zero before the launch; every merge resets its own); the block
   // that finishes a query's last unit merges it, and the separate merge launch is skipped
   int32_t *done;
+  // MaxScans, or null: [q][nprobe] the exclusive absolute row bound of each probed list (ivf_limits_kernel with
+  // one chunk per probe)
+  const uint32_t *qlim;
 };
 // part: ivf_rerun_part_keys() rank keys of scratch (one block per (failing query, probe, chunk), then
 // a merge per query)
@@ -226,6 +229,9 @@ void launch_ivf_items(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t
 void launch_ivf_limits(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t nparts, int64_t remaining,
                        const int32_t *list_begin, const int32_t *list_end, const int32_t *list_live,
                        const uint8_t *live, IvfChunking ch, uint32_t *limits, hipStream_t st);
+
+// the per-(query, probe) bounds (cmax 1) at the pairs' qlist positions: plim[qpos[i]] = limits[i]
+void launch_pos_limits(const int32_t *qpos, const uint32_t *limits, int64_t n, uint32_t *plim, hipStream_t st);
 
 // IVF-PQ ADC scan (IvfPqVectorIndex.cs:152-198).
 struct PqArgs {
@@ -373,6 +379,10 @@ struct StreamArgs {
   // then sprep builds the operands query-major (sample16.hip); nq its query count
   const int32_t *qpos;
   int64_t nq;
+  // MaxScans (IvfFlatVectorIndex.cs:202-212), or null: per qlist position the exclusive absolute row bound of
+  // that (query, list) pair's scanned rows (launch_pos_limits); a row at or past it is neither sampled nor
+  // emitted
+  const uint32_t *plim;
 };
 // per row the stream scan's additive term: meta + kr |x - c|^2 (+ kx |x|^2, IP): fmaf(kr, rsq16, meta),
 // then fmaf(kx, rsq, .)

@@ -869,33 +869,57 @@ __global__ void ivf_fill_kernel(const int32_t *probes, int64_t nq, int nprobe, i
   if (qpos) qpos[q * nprobe + p] = qoff[lst] + pos;
 }
 
-__global__ void ivf_limits_kernel(const int32_t *probes, int64_t nq, int nprobe, int nparts, int cmax,
-                                  int64_t remaining, const int32_t *lb, const int32_t *le, const int32_t *llive,
-                                  const uint8_t *live, uint32_t *limits) {
-  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// One wave per query: the probed lists in probe order, each taking min(its live rows, what is left); the list
+// where the budget runs out is bounded at its (rem + 1)-th live row (rows before it hold exactly rem live
+// ones), found 64 rows at a time (ballot + prefix popcount) -- a tombstone-free list directly at lb + rem.
+// (Round 4 walked that list row by row in one thread: 2.5 ms at I1 with MaxScans 5,000.)
+__global__ __launch_bounds__(256) void ivf_limits_kernel(const int32_t *probes, int64_t nq, int nprobe, int nparts,
+                                                         int cmax, int64_t remaining, const int32_t *lb,
+                                                         const int32_t *le, const int32_t *llive, const uint8_t *live,
+                                                         uint32_t *limits) {
+  const int lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= nq) return;
   int64_t rem = remaining;
   for (int p = 0; p < nprobe; ++p) {
     const int lst = probes[q * nprobe + p];
+    const int b = lb[lst], e = le[lst], n = llive[lst];
     uint32_t lim;
     if (rem <= 0) {
-      lim = (uint32_t)lb[lst];
-    } else if (rem >= llive[lst]) {
-      lim = (uint32_t)le[lst];
-      rem -= llive[lst];
+      lim = (uint32_t)b;
+    } else if (rem >= n) {
+      lim = (uint32_t)e;
+      rem -= n;
+    } else if (n == e - b) {
+      lim = (uint32_t)(b + rem);
+      rem = 0;
     } else {
-      int64_t c = 0;
-      int r = lb[lst];
-      for (; r < le[lst]; ++r)
-        if (live[r]) {
-          if (c == rem) break;
-          ++c;
+      int64_t c = 0;  // live rows before r0
+      lim = (uint32_t)e;
+      for (int r0 = b; r0 < e; r0 += 64) {
+        const int r = r0 + lane;
+        const bool lv = r < e && live[r] != 0;
+        const uint64_t m = __builtin_amdgcn_ballot_w64(lv);
+        const int cnt = (int)__builtin_popcountll(m);
+        if (c + cnt > rem) {  // the (rem - c)-th live row of this block (0-based) is the bound
+          const int pre = (int)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+          const uint64_t hit = __builtin_amdgcn_ballot_w64(lv && pre == (int)(rem - c));
+          lim = (uint32_t)(r0 + (int)__builtin_ctzll(hit));
+          break;
         }
-      lim = (uint32_t)r;
+        c += cnt;
+      }
       rem = 0;
     }
-    for (int c = 0; c < cmax; ++c) limits[(size_t)q * nparts + p * cmax + c] = lim;  // bound is absolute
+    for (int c = lane; c < cmax; c += 64) limits[(size_t)q * nparts + p * cmax + c] = lim;  // bound is absolute
   }
+}
+
+__global__ void pos_limits_kernel(const int32_t *qpos, const uint32_t *limits, int64_t n, uint32_t *plim) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t pos = qpos[i];
+  if (pos >= 0) plim[pos] = limits[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -1538,7 +1562,9 @@ __global__ __launch_bounds__(256) void ivf_rerun_scan_kernel(IvfRerunArgs a, uin
     const int lst = a.probes[(size_t)q * (a.pstride > 0 ? a.pstride : a.nprobe) + p];
     uint64_t cur = 0ull;  // lane j: the wave's j-th best so far
     if (lst >= 0) {
-      const int b = a.lb[lst], e = a.le[lst];
+      const int b = a.lb[lst];
+      const int e = a.qlim ? (int)min((uint32_t)a.le[lst], max((uint32_t)b, a.qlim[(size_t)q * a.nprobe + p]))
+                           : a.le[lst];  // MaxScans: the rows before the bound (:202-212)
       const int cl = (((e - b) + nc - 1) / nc + 63) & ~63;
       const int cb = b + c * cl, ce = min(e, cb + cl);
       for (int r0 = cb + 64 * w; r0 < ce; r0 += 256) {
@@ -1781,8 +1807,13 @@ void launch_ivf_limits(const int32_t *probes, int64_t nq, int32_t nprobe, int32_
                        const int32_t *list_begin, const int32_t *list_end, const int32_t *list_live,
                        const uint8_t *live, IvfChunking ch, uint32_t *limits, hipStream_t st) {
   if (nq <= 0) return;
-  hipLaunchKernelGGL(ivf_limits_kernel, dim3(nblk(nq, 64)), dim3(64), 0, st, probes, nq, nprobe, nparts, ch.cmax,
+  hipLaunchKernelGGL(ivf_limits_kernel, dim3(nblk(nq, 4)), dim3(256), 0, st, probes, nq, nprobe, nparts, ch.cmax,
                      remaining, list_begin, list_end, list_live, live, limits);
+}
+
+void launch_pos_limits(const int32_t *qpos, const uint32_t *limits, int64_t n, uint32_t *plim, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(pos_limits_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, qpos, limits, n, plim);
 }
 
 size_t pq_scan_lds_bytes(int dim, int M, int ksub, int k) {

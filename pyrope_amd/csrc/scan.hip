@@ -223,7 +223,10 @@ __global__ __launch_bounds__(256) void sample_kernel(StreamArgs a) {
 // (SAMPLE_TILES = 16 = the waves of a block at D <= 128) against every query group, and writes per (query,
 // probe) the 2 x 16 values max(f acc + row term) + cq over its lane half's rows -- each the bound of distinct
 // rows, as sample16_kernel's -- into samp; no emission.
-template <int D, int MET, int AB = 0, bool SMP = false>
+// LIM: a MaxScans search (a.plim): a row at or past its (query, list) pair's bound is neither sampled nor
+// emitted (its own instantiation: the check in the default kernel's emission path cost 4 % of the I1 step,
+// 1.175 vs 1.125 ms, profiles/r5_late/maxscans_ab.log)
+template <int D, int MET, int AB = 0, bool SMP = false, bool LIM = false>
 __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
   constexpr int NW = nw_of(D);       // waves per block
   constexpr int KS = D / 16;         // 32x32x16 k-steps
@@ -296,6 +299,11 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
           const float2 fc = a.qsc[pos];
           const float T = (!SMP && a.thr) ? a.thr[slot / a.nparts] + a.thr_bias : -INFINITY;
           v = make_float2(fc.x, lower_thr(T, fc.y));
+          // MaxScans: a pair whose bound is at or before the item's rows has none of them scanned -- its rows never
+          // reach the emission test (a low T_q from a small budget would otherwise send most of every other
+          // list's tiles down the emission path, to be dropped there)
+          if constexpr (LIM && !SMP)
+            if (a.plim[pos] <= (uint32_t)it.row_begin) v.y = __builtin_nanf("");
           cqv = fc.y;
           o = SMP ? (slot / a.nparts) * a.nprobe + (slot % a.nparts) / a.cmax : slot / a.nparts;
         }
@@ -364,6 +372,8 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
           const bool p = y[e] >= thr;
           if (__builtin_amdgcn_ballot_w64(p) == 0ull) continue;
           if (p) {
+            // MaxScans: a row at or past the pair's bound is not scanned (the bound read only here, per row)
+            if (LIM && (uint32_t)(rt + 4 * h + 8 * (e >> 2) + (e & 3)) >= a.plim[it.qbeg + qi]) continue;
             const float sc = y[e] + cq;
             const uint32_t word = base + (uint32_t)(8 * (e >> 2) + (e & 3));
             const int at = stage ? atomicAdd(&eb_n, 1) : EB;
@@ -444,6 +454,8 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
       }
       for (int j = 0; j < ng; ++j) {
         const float2 q = qf[32 * j + r];
+        if constexpr (LIM)  // MaxScans: a group none of whose pairs reaches these rows is not scored
+          if (__builtin_amdgcn_ballot_w64(!__builtin_isnan(q.y)) == 0ull) continue;
         h8v bj[KS];
         read_b(j, bj);
         f16v acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[0], bj[0], (f16v){}, 0, 0, 0);
@@ -499,6 +511,14 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
           float mx = fmaf(q.x, acc[0], mr[0]);
 #pragma unroll
           for (int v = 1; v < 16; ++v) mx = fmaxf(mx, fmaf(q.x, acc[v], mr[v]));
+          if constexpr (LIM) {  // MaxScans: only the rows before the pair's bound are sampled
+            const uint32_t lim = a.plim[it.qbeg + min(32 * j + r, qcnt - 1)];
+            const int rt = r0 + 32 * w + 4 * h;
+            mx = -INFINITY;
+#pragma unroll
+            for (int v = 0; v < 16; ++v)
+              if ((uint32_t)(rt + 8 * (v >> 2) + (v & 3)) < lim) mx = fmaxf(mx, fmaf(q.x, acc[v], mr[v]));
+          }
           smx[j] = mx;
         }
       }
@@ -559,14 +579,16 @@ void launch_scan_dm(const StreamArgs &a, int max_items, hipStream_t st) {
       return;
     }
   }
-  hipLaunchKernelGGL((scan_kernel<D, MET>), dim3(grid), b, 0, st, a);
+  if (a.plim) hipLaunchKernelGGL((scan_kernel<D, MET, 0, false, true>), dim3(grid), b, 0, st, a);  // MaxScans
+  else hipLaunchKernelGGL((scan_kernel<D, MET>), dim3(grid), b, 0, st, a);
 }
 
 template <int D, int MET>
 void launch_scan_sample_dm(const StreamArgs &a, int max_items, hipStream_t st) {
   if constexpr (nw_of(D) == SAMPLE_TILES && D / 16 <= 16) {
     const int grid = std::max(1, std::min(max_items, device_cus()));
-    hipLaunchKernelGGL((scan_kernel<D, MET, 0, true>), dim3(grid), dim3(64 * nw_of(D)), 0, st, a);
+    if (a.plim) hipLaunchKernelGGL((scan_kernel<D, MET, 0, true, true>), dim3(grid), dim3(64 * nw_of(D)), 0, st, a);
+    else hipLaunchKernelGGL((scan_kernel<D, MET, 0, true>), dim3(grid), dim3(64 * nw_of(D)), 0, st, a);
   }
 }
 
