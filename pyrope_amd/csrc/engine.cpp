@@ -911,6 +911,12 @@ static bool max_scans_stream() {
   return !(e && atoi(e) == 0);
 }
 
+// PYR_IVF_BUFFER_STREAM=0: an IVF_FLAT search with a non-empty buffer takes the exact scan (A/B; read per search)
+static bool buffer_stream() {
+  const char *e = getenv("PYR_IVF_BUFFER_STREAM");
+  return !(e && atoi(e) == 0);
+}
+
 static bool merge_refine_fused() {
   const char *e = getenv("PYR_MERGE_REFINE");
   return !(e && atoi(e) == 0) && !getenv("PYR_STREAM_DEBUG");
@@ -2323,21 +2329,72 @@ struct IvfFlatIndex : Index {
     const int probes = (built && coarse.nlist > 0) ? std::max(0, std::min(nprobe, coarse.nlist)) : 0;
     const int k1 = filter_k1(k);
     const bool budget_ok = prm.max_scans < 0 || (prm.max_scans > 0 && !ws.ext_probes && max_scans_stream());
-    const bool fast = filter_enabled() && probes > 0 && buf.live_count() == 0 && budget_ok && k <= KMAX_FAST &&
+    const bool nbuf = buf.live_count() > 0;
+    const bool fast = filter_enabled() && probes > 0 && (!nbuf || buffer_stream()) && budget_ok && k <= KMAX_FAST &&
                       probes < MAX_PARTS && k1 > 0;
     // the stream scan (L2 / IP, and Cosine over the unit residual tiles with the exact Cosine in the refine)
     if (fast && stream_ok(k1)) {
-      ws.max_scans = prm.max_scans;
-      try {
-        search_stream(d_q, nq, k, k1, probes, d_s, d_l, d_c, ws);
-      } catch (...) {
+      auto lists_stream = [&](int64_t budget, float *s, int64_t *l, int32_t *c) {
+        ws.max_scans = budget;
+        try {
+          search_stream(d_q, nq, k, k1, probes, s, l, c, ws);
+        } catch (...) {
+          ws.max_scans = -1;
+          throw;
+        }
         ws.max_scans = -1;
-        throw;
+      };
+      if (!nbuf) {
+        lists_stream(prm.max_scans, d_s, d_l, d_c);
+        return;
       }
-      ws.max_scans = -1;
+      // a non-empty buffer (:169-180): its exact top k over the slots the budget reaches, the lists on the
+      // stream scan with what is left of it (their buffer-shadowed rows are not live, :210), the two answers
+      // merged with a list entry first on equal scores (the exact path's key order)
+      const int64_t maxs = prm.max_scans < 0 ? INT64_MAX : prm.max_scans;
+      const int64_t bscanned = std::min<int64_t>(maxs, buf.live_count());
+      ws.bx_s.ensure(sizeof(float) * nq * k);
+      ws.bx_l.ensure(sizeof(int64_t) * nq * k);
+      ws.bx_c.ensure(sizeof(int32_t) * nq);
+      ws.lx_s.ensure(sizeof(float) * nq * k);
+      ws.lx_l.ensure(sizeof(int64_t) * nq * k);
+      ws.lx_c.ensure(sizeof(int32_t) * nq);
+      buffer_topk(d_q, nq, k, buf.cutoff(bscanned), ws.bx_s.as<float>(), ws.bx_l.as<int64_t>(),
+                  ws.bx_c.as<int32_t>(), ws);
+      if (bscanned < maxs)  // :183
+        lists_stream(prm.max_scans < 0 ? -1 : maxs - bscanned, ws.lx_s.as<float>(), ws.lx_l.as<int64_t>(),
+                     ws.lx_c.as<int32_t>());
+      else
+        fill_empty_results(ws.lx_s.as<float>(), ws.lx_l.as<int64_t>(), ws.lx_c.as<int32_t>(), nq, k, ws.st);
+      PhaseTimer tm(PH_MERGE, ws.st);
+      launch_merge_two(ws.lx_s.as<float>(), ws.lx_l.as<int64_t>(), ws.lx_c.as<int32_t>(), ws.bx_s.as<float>(),
+                       ws.bx_l.as<int64_t>(), ws.bx_c.as<int32_t>(), nq, k, d_s, d_l, d_c, ws.st);
+      HIPCHK(hipGetLastError());
       return;
     }
     search_exact(d_q, nq, k, prm, d_s, d_l, d_c, ws);
+  }
+
+  // the buffer's exact top k over its first bcut slots (:169-180, ComputeScore) in (score desc, slot asc) order
+  void buffer_topk(const float *d_q, int64_t nq, int k, int64_t bcut, float *d_s, int64_t *d_l, int32_t *d_c,
+                   Workspace &ws) {
+    if (bcut <= 0) {
+      fill_empty_results(d_s, d_l, d_c, nq, k, ws.st);
+      return;
+    }
+    const ScanPlan bp = plan_flat(bcut, nq, dim, k, MAX_PARTS);
+    prep_queries(d_q, nq, dim, metric, ws);
+    const float *qn = metric == COS ? ws.qn.as<float>() : nullptr;
+    const size_t np = (size_t)nq * bp.nchunks * k;
+    ws.part_s.ensure(sizeof(float) * np);
+    ws.part_k.ensure(sizeof(uint32_t) * np);
+    {
+      PhaseTimer t(PH_BUF_SCAN, ws.st, nq * bcut);
+      flat_scan(buf.st, bcut, bp, d_q, qn, nq, k, 1, metric, bp.nchunks, 0, KEY_BUF, ws, ws.part_s.as<float>(),
+                ws.part_k.as<uint32_t>(), true);
+    }
+    launch_merge_keys(ws.part_s.as<float>(), ws.part_k.as<uint32_t>(), nq, bp.nchunks, k, lists.labels.as<int64_t>(),
+                      buf.st.labels.as<int64_t>(), d_s, d_l, nullptr, d_c, ws.st, nullptr);
   }
 
   // the lists' fp16 residual tiles serve this search's stream scan (scan.hip) at every tile dimension;

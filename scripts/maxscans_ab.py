@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--budgets", default="5000,50000,200000")
+    ap.add_argument("--buffer", type=int, default=0, help="then add this many rows after Build (the buffer; half "
+                    "of them new ids, half shadowing list rows) and time the search with it, stream vs exact")
     args = ap.parse_args()
     import torch
     torch.cuda.init()
@@ -100,6 +102,24 @@ def main():
         if not same:
             bad = np.nonzero((out_s[1] != out_e[1]).any(1))[0]
             print(f"[maxscans]   {len(bad)} queries differ, first {bad[:5].tolist()}", flush=True)
+    if args.buffer > 0:  # IvfFlatVectorIndex.cs:169-180: the buffer scanned exactly beside the lists
+        nb = args.buffer
+        lab = np.concatenate([np.arange(N, N + nb - nb // 2), np.arange(0, N, max(1, N // (nb // 2 + 1)))[: nb // 2]])
+        idx.add_labels(lab.astype(np.int64), generate_synthetic(len(lab), D, 99))
+        for b in [None, 5000]:
+            opts = SearchOptions(nprobe=P, max_scans=b)
+            ms_s, mn_s, out_s = timed(opts)
+            os.environ["PYR_IVF_BUFFER_STREAM"] = "0"
+            try:
+                ms_e, mn_e, out_e = timed(opts)
+            finally:
+                os.environ.pop("PYR_IVF_BUFFER_STREAM", None)
+            same = (np.array_equal(out_s[1], out_e[1]) and np.array_equal(out_s[2], out_e[2]) and
+                    np.array_equal(out_s[0].view(np.uint32), out_e[0].view(np.uint32)))
+            res.setdefault("buffer", {})[str(b)] = {"buffer_rows": len(lab), "stream_ms": ms_s, "exact_ms": ms_e,
+                                                     "speedup": ms_e / ms_s, "bit_identical": bool(same)}
+            print(f"[maxscans] buffer {len(lab)} rows, budget {b}: stream {ms_s:.3f} ms, exact {ms_e:.3f} ms, "
+                  f"x{ms_e / ms_s:.1f}, identical {same}", flush=True)
     print(json.dumps(res), flush=True)
     idx.close()
 
