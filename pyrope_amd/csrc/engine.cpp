@@ -905,6 +905,21 @@ struct CosRefine {
 // the stream scans' candidate merge and certified refine fused into one kernel (filter.hip
 // merge_refine_kernel); PYR_MERGE_REFINE=0 (A/B) and PYR_STREAM_DEBUG (it reads the merged candidates back)
 // take cand_merge + the two refine launches
+// PYR_DEEP_REFINE=0: an IVF search with k > 60 takes the exact scan (A/B; read per search)
+static bool deep_refine_on() {
+  const char *e = getenv("PYR_DEEP_REFINE");
+  return !(e && atoi(e) == 0);
+}
+// the refine depth for k > 60 (deep_refine_kernel): 128 / 256 >= k + the margin, 0 past that or when the
+// candidate buffer's sort would not fit 60 KiB of LDS
+static int deep_k1(int k) {
+  int m = 4;
+  if (const char *e = getenv("PYR_FILTER_MARGIN")) m = std::max(0, atoi(e));
+  for (int c : {128, 256})
+    if (k + m <= c) return deep_refine_lds_bytes(stream_cap(), c) <= 60 * 1024 ? c : 0;
+  return 0;
+}
+
 // PYR_MAXSCANS_STREAM=0: an IVF search with a MaxScans budget takes the exact scan (A/B; read per search)
 static bool max_scans_stream() {
   const char *e = getenv("PYR_MAXSCANS_STREAM");
@@ -2327,11 +2342,14 @@ struct IvfFlatIndex : Index {
     // each (query, list) pair's rows (stream_slice), MaxScans 0 scans nothing (the exact path's empty answer)
     const int nprobe = prm.nprobe < 0 ? nprobe_default : prm.nprobe;
     const int probes = (built && coarse.nlist > 0) ? std::max(0, std::min(nprobe, coarse.nlist)) : 0;
-    const int k1 = filter_k1(k);
+    int k1 = filter_k1(k);
     const bool budget_ok = prm.max_scans < 0 || (prm.max_scans > 0 && !ws.ext_probes && max_scans_stream());
     const bool nbuf = buf.live_count() > 0;
-    const bool fast = filter_enabled() && probes > 0 && (!nbuf || buffer_stream()) && budget_ok && k <= KMAX_FAST &&
-                      probes < MAX_PARTS && k1 > 0;
+    // k > 60: depth 128 / 256 (deep_refine_kernel) on built lists with no buffer and no budget
+    const bool deep = k1 == 0 && !nbuf && prm.max_scans < 0 && !ws.ext_probes && deep_refine_on();
+    if (deep) k1 = deep_k1(k);
+    const bool fast = filter_enabled() && probes > 0 && (!nbuf || buffer_stream()) && budget_ok &&
+                      (k <= KMAX_FAST || deep) && probes < MAX_PARTS && k1 > 0;
     // the stream scan (L2 / IP, and Cosine over the unit residual tiles with the exact Cosine in the refine)
     if (fast && stream_ok(k1)) {
       auto lists_stream = [&](int64_t budget, float *s, int64_t *l, int32_t *c) {
@@ -2681,6 +2699,41 @@ struct IvfFlatIndex : Index {
     r.out_l = d_l;
     r.out_c = d_c;
     int32_t nf = 0;
+    if (k1 > STREAM_KO) {  // k > 60: depth K1 = 128 / 256 in one block per query, what fails on the exact scan
+      {
+        PhaseTimer t(PH_REFINE, ws.st, nq * k1);
+        r.k1 = k1;
+        r.fail_list = ws.fail.as<int32_t>();
+        r.fail_cnt = ws.fail_cnt.as<int32_t>();
+        launch_deep_refine(m, r, met, ws.st);
+        HIPCHK(hipGetLastError());
+      }
+      HIPCHK(hipMemcpyAsync(&nf, ws.fail_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, ws.st));
+      HIPCHK(hipStreamSynchronize(ws.st));
+      if (getenv("PYR_STREAM_DEBUG"))
+        fprintf(stderr, "[stream deep] nq %lld k %d: depth %d certificate failures %d\n", (long long)nq, k, k1, nf);
+      // the failures' own probe lists (gathered by the fail list) on the exact VALU scan, same arithmetic
+      filter_fallback(ws, nf, d_q, dim, k, d_s, d_l, d_c,
+                      [&](const float *q2, int64_t n2, float *s2, int64_t *l2, int32_t *c2) {
+                        ws.fprobes.ensure(sizeof(int32_t) * n2 * probes);
+                        launch_gather_words(ws.probes.as<uint32_t>(), ws.fail.as<int32_t>(), n2, probes,
+                                            ws.fprobes.as<uint32_t>(), ws.st);
+                        Workspace &nw = ws.nested();
+                        nw.ext_probes = ws.fprobes.as<int32_t>();
+                        nw.ext_nprobe = probes;
+                        pyr_search_params p2{};
+                        p2.nprobe = probes;
+                        p2.max_scans = -1;
+                        try {
+                          search_exact(q2, n2, k, p2, s2, l2, c2, nw);
+                        } catch (...) {
+                          nw.ext_probes = nullptr;
+                          throw;
+                        }
+                        nw.ext_probes = nullptr;
+                      });
+      return;
+    }
     if (sh) {  // list-sharded: the records (exact local top-k + bound); the home rank's merge certifies
       PhaseTimer t(PH_REFINE, ws.st, nq * k1);
       r.k1 = k1;

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
 #include <cmath>
 #include <stdexcept>
@@ -558,6 +559,125 @@ __global__ __launch_bounds__(256) void merge_refine_kernel(CandMergeArgs m, Refi
   }
 }
 
+// k > 60 (round 5): the stream scans' merge and certified refine at depth K1 = 128 / 256, one 256-thread block
+// per query.  The emitted rows and K1 copies of the floor placeholder max(T_q, floor) are sorted in LDS by rank
+// key (bitonic, descending); the first K1 are the candidates (every row left out scores at most the K1-th);
+// their exact scores come from 8-lane groups in the reference's order (as merge_refine_kernel's); the ranks by
+// better() (score desc, key asc), the top k written, and the certificate of refine_kernel's upper-bound branch.
+// A NaN score fails the query (the exact scan decides).  What fails is listed for the caller's exact scan.
+template <int MET, int DT>
+__global__ __launch_bounds__(256) void deep_refine_kernel(CandMergeArgs m, RefineArgs a) {
+  extern __shared__ uint64_t dk[];  // the sort: P = pow2 >= emitted rows + K1 entries
+  __shared__ float ex[256];
+  __shared__ uint32_t ky[256];
+  __shared__ float skth_s;
+  __shared__ int nan_s;
+  const int tid = threadIdx.x;
+  const int64_t q = blockIdx.x;
+  const int d = a.k1, k = a.k, D = DT > 0 ? DT : a.dim;
+  const int tot = min(m.cand_n[q], m.cap);
+  const uint32_t fk = m.cand_f[q];
+  float F = m.thr ? m.thr[q] : -INFINITY;
+  if (fk != 0u) F = fmaxf(F, key_score(fk));
+  int P = 256;
+  while (P < tot + d) P <<= 1;
+  const uint2 *cq = m.cand + (size_t)q * m.cap;
+  for (int i = tid; i < P; i += 256) {
+    uint64_t v = 0ull;
+    if (i < tot) {
+      const uint2 e = cq[i];
+      v = pack_cand(__uint_as_float(e.x), e.y);
+    } else if (i < tot + d && F > -INFINITY) {
+      v = pack_cand(F, KEY_FLOOR);
+    }
+    dk[i] = v;
+  }
+  if (tid == 0) {
+    skth_s = -INFINITY;
+    nan_s = 0;
+  }
+  __syncthreads();
+  for (int sz = 2; sz <= P; sz <<= 1)
+    for (int j = sz >> 1; j >= 1; j >>= 1) {
+      for (int i = tid; i < P; i += 256) {
+        const int o = i ^ j;
+        if (o > i) {
+          const uint64_t x = dk[i], y = dk[o];
+          if ((i & sz) == 0 ? x < y : x > y) {
+            dk[i] = y;
+            dk[o] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  const uint64_t v = tid < d ? dk[tid] : 0ull;
+  const uint32_t key = v == 0ull ? KEY_NONE : ~(uint32_t)v;
+  const bool real = key != KEY_NONE && key != KEY_FLOOR;
+  ky[tid] = real ? key : KEY_NONE;
+  ex[tid] = -INFINITY;
+  const uint64_t vl = dk[d - 1];
+  const bool excluded = vl != 0ull;  // the K1-th entry exists: rows (or the floor) were left out
+  const float bound = excluded ? key_score((uint32_t)(vl >> 32)) : -INFINITY;
+  __syncthreads();
+  // exact scores: group g of the block's 32 takes candidates g, g + 32, ... (every lane of a group ends with it)
+  const float *qp = a.queries + (size_t)q * D;
+  const int g = tid >> 3, l = tid & 7;
+  for (int c = g; c < d; c += 32) {
+    const uint32_t kc = ky[c];
+    if (kc == KEY_NONE) continue;  // (group-uniform)
+    float sc;
+    if (MET == L2 && a.cosine) {  // VectorMath.Cosine (:102-109) with the cached norms
+      const float dot = a.rows_rm ? exact_score_l8<1, IP, DT, true>(qp, a.rows_rm, kc, D, l)
+                                  : exact_score_l8<1, IP, DT, false>(qp, a.rows, kc, D, l);
+      const float qn = a.qnorm[q], xn = a.rnorm[kc];
+      sc = (qn < 1e-6f || xn < 1e-6f) ? 0.0f : dot / (qn * xn);
+    } else {
+      sc = a.rows_rm ? exact_score_l8<1, MET, DT, true>(qp, a.rows_rm, kc, D, l)
+                     : exact_score_l8<1, MET, DT, false>(qp, a.rows, kc, D, l);
+    }
+    if (l == 0) {
+      ex[c] = sc;
+      if (isnan(sc)) nan_s = 1;
+    }
+  }
+  __syncthreads();
+  const float s = ex[tid];
+  int rank = 0;
+  if (real)
+    for (int c = 0; c < d; ++c)
+      if (ky[c] != KEY_NONE && better(ex[c], ky[c], s, key)) ++rank;
+  const int nreal = __syncthreads_count(real);
+  const int nout = min(nreal, k);
+  if (real && rank == k - 1) skth_s = s;
+  __syncthreads();
+  const float skth = skth_s;
+  bool ok;
+  if (!excluded) {
+    ok = true;
+  } else if (MET == L2 && a.cosine) {
+    const double u = 5.9604644775390625e-8;  // 2^-24
+    const float qn = a.qnorm[q];
+    ok = nout == k && (double)skth > 1.0 + 0.5 * (double)bound + (2.0 * D + 256.0) * u && qn >= 1e-6f &&
+         isfinite(qn) && !(a.max_rsq && a.max_rsq[1] != 0u) && !(a.zflag && *a.zflag != 0u && !(skth > 0.0f));
+  } else {
+    ok = nout == k && skth > bound;
+  }
+  ok = ok && nan_s == 0;
+  if (real && rank < k) {
+    a.out_s[(size_t)q * k + rank] = s;
+    a.out_l[(size_t)q * k + rank] = a.row_labels ? a.row_labels[key] : (int64_t)key;
+  }
+  if (tid >= nout && tid < k) {
+    a.out_s[(size_t)q * k + tid] = -INFINITY;
+    a.out_l[(size_t)q * k + tid] = -1;
+  }
+  if (tid == 0) {
+    if (a.out_c) a.out_c[q] = nout;
+    if (!ok) a.fail_list[atomicAdd(a.fail_cnt, 1)] = (int32_t)q;
+  }
+}
+
 __global__ void unit_rows_kernel(const float *x, const int64_t *slots, const float *norms, int64_t n, int D,
                                  float *out, uint32_t *zflag, const uint8_t *live) {
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * D;
@@ -696,6 +816,29 @@ void launch_merge_refine(const CandMergeArgs &m, const RefineArgs &a, int metric
     else
       by_dim(merge_refine_kernel<1, IP, 0>, merge_refine_kernel<1, IP, 32>, merge_refine_kernel<1, IP, 64>,
              merge_refine_kernel<1, IP, 128>);
+  }
+}
+
+size_t deep_refine_lds_bytes(int cap, int k1) {
+  size_t P = 256;
+  while (P < (size_t)cap + (size_t)k1) P <<= 1;
+  return P * sizeof(uint64_t);
+}
+
+void launch_deep_refine(const CandMergeArgs &m, const RefineArgs &a, int metric, hipStream_t st) {
+  if (a.nq <= 0) return;
+  if (a.k1 > 256 || a.k1 < a.k || a.k > 256) throw std::invalid_argument("deep_refine: depth");
+  const size_t lds = deep_refine_lds_bytes(m.cap, a.k1);
+  // within the default 64 KiB per block with the 2 KiB of static LDS (no attribute call: raising the dynamic
+  // limit to 160 KiB fails for a kernel with static LDS and leaves hipGetLastError set)
+  if (lds > 60 * 1024) throw std::invalid_argument("deep_refine: candidate buffer too large");
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3((unsigned)a.nq), dim3(256), lds, st, m, a); };
+  if (metric == L2) {
+    if (a.dim == 128) go(deep_refine_kernel<L2, 128>);
+    else go(deep_refine_kernel<L2, 0>);
+  } else {
+    if (a.dim == 128) go(deep_refine_kernel<IP, 128>);
+    else go(deep_refine_kernel<IP, 0>);
   }
 }
 

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--budgets", default="5000,50000,200000")
+    ap.add_argument("--topk", default="", help="comma list of k > 60: the deep refine vs the exact scan "
+                    "(PYR_DEEP_REFINE=0)")
     ap.add_argument("--buffer", type=int, default=0, help="then add this many rows after Build (the buffer; half "
                     "of them new ids, half shadowing list rows) and time the search with it, stream vs exact")
     args = ap.parse_args()
@@ -78,7 +80,7 @@ def main():
     ms_none, _, _ = timed(SearchOptions(nprobe=P))
     res["no_budget_ms"] = ms_none
     print(f"[maxscans] no budget: {ms_none:.3f} ms", flush=True)
-    for b in [int(v) for v in args.budgets.split(",")]:
+    for b in [int(v) for v in args.budgets.split(",") if v]:
         opts = SearchOptions(nprobe=P, max_scans=b)
         ms_s, mn_s, out_s = timed(opts)
         os.environ["PYR_MAXSCANS_STREAM"] = "0"
@@ -102,6 +104,31 @@ def main():
         if not same:
             bad = np.nonzero((out_s[1] != out_e[1]).any(1))[0]
             print(f"[maxscans]   {len(bad)} queries differ, first {bad[:5].tolist()}", flush=True)
+    for kk in [int(v) for v in args.topk.split(",") if v]:  # k > 60: depth 128 / 256 (deep_refine_kernel)
+        opts = SearchOptions(nprobe=P)
+        sv = K
+        K = kk
+        try:
+            ms_s, mn_s, out_s = timed(opts)
+            os.environ["PYR_DEEP_REFINE"] = "0"
+            try:
+                ms_e, mn_e, out_e = timed(opts)
+            finally:
+                os.environ.pop("PYR_DEEP_REFINE", None)
+            os.environ["PYR_STREAM_DEBUG"] = "1"
+            try:
+                run(opts)
+                torch.cuda.synchronize()
+            finally:
+                os.environ.pop("PYR_STREAM_DEBUG", None)
+        finally:
+            K = sv
+        same = (np.array_equal(out_s[1], out_e[1]) and np.array_equal(out_s[2], out_e[2]) and
+                np.array_equal(out_s[0].view(np.uint32), out_e[0].view(np.uint32)))
+        res.setdefault("topk", {})[str(kk)] = {"stream_ms": ms_s, "exact_ms": ms_e, "speedup": ms_e / ms_s,
+                                               "bit_identical": bool(same)}
+        print(f"[maxscans] k {kk}: stream {ms_s:.3f} ms, exact {ms_e:.3f} ms, x{ms_e / ms_s:.1f}, identical {same}",
+              flush=True)
     if args.buffer > 0:  # IvfFlatVectorIndex.cs:169-180: the buffer scanned exactly beside the lists
         nb = args.buffer
         lab = np.concatenate([np.arange(N, N + nb - nb // 2), np.arange(0, N, max(1, N // (nb // 2 + 1)))[: nb // 2]])
