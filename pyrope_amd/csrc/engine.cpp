@@ -905,6 +905,9 @@ struct CosRefine {
 // the stream scans' candidate merge and certified refine fused into one kernel (filter.hip
 // merge_refine_kernel); PYR_MERGE_REFINE=0 (A/B) and PYR_STREAM_DEBUG (it reads the merged candidates back)
 // take cand_merge + the two refine launches
+// the candidate buffer per query of a deep (K1 > 64) search: a query emits ~7.5 K1 rows at I1 (T_q's floor
+// rank 3 K1 / 8 over a ~5 % sample), so 16 K1 keeps a full buffer rare (its floor would fail the certificate)
+static int deep_cap(int k1) { return std::max(stream_cap(), 16 * k1); }
 // PYR_DEEP_REFINE=0: an IVF search with k > 60 takes the exact scan (A/B; read per search)
 static bool deep_refine_on() {
   const char *e = getenv("PYR_DEEP_REFINE");
@@ -915,8 +918,10 @@ static bool deep_refine_on() {
 static int deep_k1(int k) {
   int m = 4;
   if (const char *e = getenv("PYR_FILTER_MARGIN")) m = std::max(0, atoi(e));
-  for (int c : {128, 256})
-    if (k + m <= c) return deep_refine_lds_bytes(stream_cap(), c) <= 60 * 1024 ? c : 0;
+  // k within 0.8 K1: k = 200 at depth 256 failed 2,453 of 10,000 I1 queries, k = 252 at 256 nearly all
+  // (profiles/r5_late/deepk_ab.log)
+  for (int c : {128, 256, 512})
+    if (k + m <= c && 5 * k <= 4 * c) return deep_refine_lds_bytes(deep_cap(c), c) <= 144 * 1024 ? c : 0;
   return 0;
 }
 
@@ -2431,7 +2436,7 @@ struct IvfFlatIndex : Index {
   // sliced so that the candidate regions stay within 16 GiB.
   void search_stream(const float *d_q, int64_t nq, int k, int k1, int probes, float *d_s, int64_t *d_l, int32_t *d_c,
                      Workspace &ws, const ShardCtx *sh = nullptr) {
-    const int cap = stream_cap();
+    const int cap = k1 > STREAM_KO ? deep_cap(k1) : stream_cap();
     int64_t chunk = stream_chunk();
     // a list-sharded rank's lists it does not own are empty: their (query, list) pairs get no item.  Not
     // otherwise: the sample pass writes the (empty) sample of an empty list's pairs through its item

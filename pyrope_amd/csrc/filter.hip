@@ -21,6 +21,7 @@
 #include <cfloat>
 #include <cmath>
 #include <stdexcept>
+#include <string>
 
 #include "kernels.h"
 
@@ -559,19 +560,20 @@ __global__ __launch_bounds__(256) void merge_refine_kernel(CandMergeArgs m, Refi
   }
 }
 
-// k > 60 (round 5): the stream scans' merge and certified refine at depth K1 = 128 / 256, one 256-thread block
-// per query.  The emitted rows and K1 copies of the floor placeholder max(T_q, floor) are sorted in LDS by rank
-// key (bitonic, descending); the first K1 are the candidates (every row left out scores at most the K1-th);
+// k > 60 (round 5): the stream scans' merge and certified refine at depth K1 = 128 / 256 / 512, one 256-thread
+// block per query.  The emitted rows and K1 copies of the floor placeholder max(T_q, floor) are sorted in LDS by
+// rank key (bitonic, descending); the first K1 are the candidates (every row left out scores at most the K1-th);
 // their exact scores come from 8-lane groups in the reference's order (as merge_refine_kernel's); the ranks by
 // better() (score desc, key asc), the top k written, and the certificate of refine_kernel's upper-bound branch.
 // A NaN score fails the query (the exact scan decides).  What fails is listed for the caller's exact scan.
+constexpr int DEEP_MAX = 512;
 template <int MET, int DT>
 __global__ __launch_bounds__(256) void deep_refine_kernel(CandMergeArgs m, RefineArgs a) {
   extern __shared__ uint64_t dk[];  // the sort: P = pow2 >= emitted rows + K1 entries
-  __shared__ float ex[256];
-  __shared__ uint32_t ky[256];
+  __shared__ float ex[DEEP_MAX];
+  __shared__ uint32_t ky[DEEP_MAX];
   __shared__ float skth_s;
-  __shared__ int nan_s;
+  __shared__ int nan_s, nreal_s;
   const int tid = threadIdx.x;
   const int64_t q = blockIdx.x;
   const int d = a.k1, k = a.k, D = DT > 0 ? DT : a.dim;
@@ -595,6 +597,7 @@ __global__ __launch_bounds__(256) void deep_refine_kernel(CandMergeArgs m, Refin
   if (tid == 0) {
     skth_s = -INFINITY;
     nan_s = 0;
+    nreal_s = 0;
   }
   __syncthreads();
   for (int sz = 2; sz <= P; sz <<= 1)
@@ -611,11 +614,23 @@ __global__ __launch_bounds__(256) void deep_refine_kernel(CandMergeArgs m, Refin
       }
       __syncthreads();
     }
-  const uint64_t v = tid < d ? dk[tid] : 0ull;
-  const uint32_t key = v == 0ull ? KEY_NONE : ~(uint32_t)v;
-  const bool real = key != KEY_NONE && key != KEY_FLOOR;
-  ky[tid] = real ? key : KEY_NONE;
-  ex[tid] = -INFINITY;
+  // candidates c = tid + 256 h (h < d / 256, at least one)
+  constexpr int H = DEEP_MAX / 256;
+  uint32_t key[H];
+  bool real[H];
+  int nr = 0;
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    const int c = tid + 256 * h;
+    const uint64_t v = c < d ? dk[c] : 0ull;
+    key[h] = v == 0ull ? KEY_NONE : ~(uint32_t)v;
+    real[h] = key[h] != KEY_NONE && key[h] != KEY_FLOOR;
+    nr += real[h] ? 1 : 0;
+    if (c < DEEP_MAX) {
+      ky[c] = real[h] ? key[h] : KEY_NONE;
+      ex[c] = -INFINITY;
+    }
+  }
   const uint64_t vl = dk[d - 1];
   const bool excluded = vl != 0ull;  // the K1-th entry exists: rows (or the floor) were left out
   const float bound = excluded ? key_score((uint32_t)(vl >> 32)) : -INFINITY;
@@ -642,15 +657,23 @@ __global__ __launch_bounds__(256) void deep_refine_kernel(CandMergeArgs m, Refin
     }
   }
   __syncthreads();
-  const float s = ex[tid];
-  int rank = 0;
-  if (real)
-    for (int c = 0; c < d; ++c)
-      if (ky[c] != KEY_NONE && better(ex[c], ky[c], s, key)) ++rank;
-  const int nreal = __syncthreads_count(real);
-  const int nout = min(nreal, k);
-  if (real && rank == k - 1) skth_s = s;
+  float s[H];
+  int rank[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    const int c = tid + 256 * h;
+    s[h] = c < d ? ex[c] : -INFINITY;
+    rank[h] = 0;
+    if (real[h])
+      for (int c2 = 0; c2 < d; ++c2)
+        if (ky[c2] != KEY_NONE && better(ex[c2], ky[c2], s[h], key[h])) ++rank[h];
+  }
+  if (nr) atomicAdd(&nreal_s, nr);  // (zeroed before the sort's first barrier)
+#pragma unroll
+  for (int h = 0; h < H; ++h)
+    if (real[h] && rank[h] == k - 1) skth_s = s[h];
   __syncthreads();
+  const int nout = min(nreal_s, k);
   const float skth = skth_s;
   bool ok;
   if (!excluded) {
@@ -664,13 +687,15 @@ __global__ __launch_bounds__(256) void deep_refine_kernel(CandMergeArgs m, Refin
     ok = nout == k && skth > bound;
   }
   ok = ok && nan_s == 0;
-  if (real && rank < k) {
-    a.out_s[(size_t)q * k + rank] = s;
-    a.out_l[(size_t)q * k + rank] = a.row_labels ? a.row_labels[key] : (int64_t)key;
-  }
-  if (tid >= nout && tid < k) {
-    a.out_s[(size_t)q * k + tid] = -INFINITY;
-    a.out_l[(size_t)q * k + tid] = -1;
+#pragma unroll
+  for (int h = 0; h < H; ++h)
+    if (real[h] && rank[h] < k) {
+      a.out_s[(size_t)q * k + rank[h]] = s[h];
+      a.out_l[(size_t)q * k + rank[h]] = a.row_labels ? a.row_labels[key[h]] : (int64_t)key[h];
+    }
+  for (int c = nout + tid; c < k; c += 256) {
+    a.out_s[(size_t)q * k + c] = -INFINITY;
+    a.out_l[(size_t)q * k + c] = -1;
   }
   if (tid == 0) {
     if (a.out_c) a.out_c[q] = nout;
@@ -827,12 +852,20 @@ size_t deep_refine_lds_bytes(int cap, int k1) {
 
 void launch_deep_refine(const CandMergeArgs &m, const RefineArgs &a, int metric, hipStream_t st) {
   if (a.nq <= 0) return;
-  if (a.k1 > 256 || a.k1 < a.k || a.k > 256) throw std::invalid_argument("deep_refine: depth");
+  if (a.k1 > DEEP_MAX || a.k1 < a.k || a.k > 256) throw std::invalid_argument("deep_refine: depth");
   const size_t lds = deep_refine_lds_bytes(m.cap, a.k1);
-  // within the default 64 KiB per block with the 2 KiB of static LDS (no attribute call: raising the dynamic
-  // limit to 160 KiB fails for a kernel with static LDS and leaves hipGetLastError set)
-  if (lds > 60 * 1024) throw std::invalid_argument("deep_refine: candidate buffer too large");
-  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3((unsigned)a.nq), dim3(256), lds, st, m, a); };
+  // the dynamic limit raised to exactly what this launch takes (static LDS ~4 KiB beside it: asking for the
+  // whole 160 KiB fails for a kernel with static LDS)
+  if (lds > 144 * 1024) throw std::invalid_argument("deep_refine: candidate buffer too large");
+  auto go = [&](auto kern) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      throw std::runtime_error(std::string("deep_refine: LDS attribute: ") + hipGetErrorString(e));
+    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)a.nq), dim3(256), lds, st, m, a);
+  };
   if (metric == L2) {
     if (a.dim == 128) go(deep_refine_kernel<L2, 128>);
     else go(deep_refine_kernel<L2, 0>);

@@ -650,7 +650,7 @@ int scan_sample_values() { return SV; }
 int scan_tile_dim(int dim) { return tile_dim_of(dim); }
 int scan_qmax(int dt) { return qmax_of(dt); }
 bool scan_supported(int dim, int metric, int k1) {
-  return (metric == L2 || metric == IP) && tile_dim_of(dim) > 0 && k1 >= 1 && k1 <= 256;  // (> 64: deep refine)
+  return (metric == L2 || metric == IP) && tile_dim_of(dim) > 0 && k1 >= 1 && k1 <= 512;  // (> 64: deep refine)
 }
 
 void launch_scan_sample(const StreamArgs &a, int metric, int max_items, hipStream_t st) {

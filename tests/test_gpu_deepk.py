@@ -1,11 +1,11 @@
 """IVF_FLAT with k > 60 on the stream scan (VERDICT r4 missing #5).
 
-The reference takes any topK (IvfFlatVectorIndex.cs:147-231).  For 60 < k <= 252 the stream scan's emitted rows
-are merged and refined at depth K1 = 128 / 256 (deep_refine_kernel, one block per query: a bitonic sort of the
+The reference takes any topK (IvfFlatVectorIndex.cs:147-231).  For 60 < k <= 256 the stream scan's emitted rows
+are merged and refined at depth K1 = 128 / 256 / 512, k <= 0.8 K1 (deep_refine_kernel, one block per query: a bitonic sort of the
 rows and the floor placeholders in LDS, exact re-scores in the reference's order, the upper-bound certificate);
 what fails goes to the exact VALU scan over the query's own probe lists.  Each case checks that the stream path
 ran, that the ids and score bits equal the oracle's and equal the exact path's (PYR_DEEP_REFINE=0), also with
-every certificate forced to fail; k = 253 .. 256 (the boundary's largest topK) keeps the exact scan.
+every certificate forced to fail, up to k = 256 (the boundary's largest topK).
 """
 import ctypes as C
 import os
@@ -67,7 +67,7 @@ def test_ivf_large_k_matches_oracle(hiplib, oracle, metric):
     rows = x[np.where(labels >= 0, labels, 0)]
     cents = idx.centroids_array()
     q = generate_synthetic(40, 128, 82)
-    for k, P in [(61, 6), (100, 6), (124, 3), (200, 6), (252, 24)]:
+    for k, P in [(61, 6), (100, 6), (124, 3), (200, 6), (252, 24), (256, 2)]:
         opts = SearchOptions(nprobe=P)
         got, calls = _sampled(hiplib, lambda: idx.search_batch(q, k, opts))
         assert calls >= 1, "k > 60 must take the stream scan"
@@ -102,10 +102,13 @@ def test_ivf_large_k_other_dim_and_past_range(hiplib, oracle):
         os_, ok = oracle.ivf_search(q[i], 90, cents, rows, off, live, nprobe=4)
         np.testing.assert_array_equal(got[1][i][: len(ok)], labels[ok])
         assert np.array_equal(got[0][i][: len(os_)].view(np.uint32), os_.astype(np.float32).view(np.uint32))
-    # k = 256 > 252 (the boundary's largest topK): the exact scan (no sample phase), still the oracle's answer
-    got, calls = _sampled(hiplib, lambda: idx.search_batch(q[:8], 256, opts))
-    assert calls == 0
-    for i in range(8):
+    # k = 256, the boundary's largest topK: depth 512
+    got, calls = _sampled(hiplib, lambda: idx.search_batch(q[:64], 256, opts))
+    assert calls >= 1
+    with _env(PYR_DEEP_REFINE=0):
+        _bits(got, idx.search_batch(q[:64], 256, opts))
+    for i in range(0, 64, 9):
         os_, ok = oracle.ivf_search(q[i], 256, cents, rows, off, live, nprobe=4)
         np.testing.assert_array_equal(got[1][i][: len(ok)], labels[ok])
+        assert np.array_equal(got[0][i][: len(os_)].view(np.uint32), os_.astype(np.float32).view(np.uint32))
     idx.close()
