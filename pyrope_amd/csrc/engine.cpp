@@ -1360,7 +1360,9 @@ struct FlatIndex : Index {
       search_sq8(d_q, nq, k, cutoff, d_s, d_l, d_c, ws);
       return;
     }
-    const int k1 = filter_k1(k);
+    int k1 = filter_k1(k);
+    // k > 60 (L2 / IP): depth 128 / 256 / 512 (deep_refine_kernel); Cosine keeps the exact scan
+    if (k1 == 0 && metric != COS && deep_refine_on()) k1 = deep_k1(k);
     if (flat_stream_ok(k, k1, cutoff)) {
       search_stream(d_q, nq, k, k1, cutoff, d_s, d_l, d_c, ws);
       return;
@@ -1380,7 +1382,7 @@ struct FlatIndex : Index {
   bool flat_stream_ok(int k, int k1, int64_t cutoff) const {
     if (!filter_enabled()) return false;
     if (metric != L2 && metric != IP) return false;
-    if (!st.f16 || k > KMAX_FAST || k1 <= 0 || !scan_supported(dim, metric, k1)) return false;
+    if (!st.f16 || (k > KMAX_FAST && k1 <= STREAM_KO) || k1 <= 0 || !scan_supported(dim, metric, k1)) return false;
     if (metric == L2 && !(st.resid && st.center16)) return false;
     return cutoff > 0 && cutoff < (int64_t)KEY_BUF;
   }
@@ -1418,7 +1420,7 @@ struct FlatIndex : Index {
                      int32_t *d_c, Workspace &ws, const CosRefine *cr = nullptr) {
     const int64_t crow = flat_chunk_rows(cutoff);
     const int nch = (int)((cutoff + crow - 1) / crow);
-    const int cap = stream_cap();
+    const int cap = k1 > STREAM_KO ? deep_cap(k1) : stream_cap();
     const int nparts = nch;  // one chunk per "list"
     const int64_t qs = stream_slice_queries(nq, nch, st.tdim(), cap, scan_sample_values());
     // the chunks as lists, on the device (no host work per search): bounds, the centroid copies (mu for
@@ -1576,6 +1578,27 @@ struct FlatIndex : Index {
     r.out_s = d_s;
     r.out_l = d_l;
     r.out_c = d_c;
+    if (k1 > STREAM_KO) {  // k > 60 (L2 / IP): depth K1 in one block per query, what fails on the exact scan
+      {
+        PhaseTimer t(PH_REFINE, ws.st, nq * k1);
+        r.k1 = k1;
+        r.fail_list = ws.fail.as<int32_t>();
+        r.fail_cnt = ws.fail_cnt.as<int32_t>();
+        launch_deep_refine(m, r, metric, exact_v, ws.st);
+        HIPCHK(hipGetLastError());
+      }
+      int32_t nf = 0;
+      HIPCHK(hipMemcpyAsync(&nf, ws.fail_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, ws.st));
+      HIPCHK(hipStreamSynchronize(ws.st));
+      if (getenv("PYR_STREAM_DEBUG"))
+        fprintf(stderr, "[flat stream deep] nq %lld k %d: depth %d certificate failures %d\n", (long long)nq, k, k1,
+                nf);
+      filter_fallback(ws, nf, d_q, dim, k, d_s, d_l, d_c,
+                      [&](const float *q2, int64_t n2, float *s2, int64_t *l2, int32_t *c2) {
+                        search_exact(q2, n2, k, cutoff, s2, l2, c2, ws.nested());
+                      });
+      return;
+    }
     if (fused) {  // merge, depth K1, depth 64 for the failures: one kernel
       PhaseTimer t(PH_REFINE, ws.st, nq * k1);
       r.k1 = k1;
@@ -2710,7 +2733,7 @@ struct IvfFlatIndex : Index {
         r.k1 = k1;
         r.fail_list = ws.fail.as<int32_t>();
         r.fail_cnt = ws.fail_cnt.as<int32_t>();
-        launch_deep_refine(m, r, met, ws.st);
+        launch_deep_refine(m, r, met, 1, ws.st);
         HIPCHK(hipGetLastError());
       }
       HIPCHK(hipMemcpyAsync(&nf, ws.fail_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, ws.st));

@@ -567,7 +567,7 @@ __global__ __launch_bounds__(256) void merge_refine_kernel(CandMergeArgs m, Refi
 // better() (score desc, key asc), the top k written, and the certificate of refine_kernel's upper-bound branch.
 // A NaN score fails the query (the exact scan decides).  What fails is listed for the caller's exact scan.
 constexpr int DEEP_MAX = 512;
-template <int MET, int DT>
+template <int V, int MET, int DT>
 __global__ __launch_bounds__(256) void deep_refine_kernel(CandMergeArgs m, RefineArgs a) {
   extern __shared__ uint64_t dk[];  // the sort: P = pow2 >= emitted rows + K1 entries
   __shared__ float ex[DEEP_MAX];
@@ -643,13 +643,13 @@ __global__ __launch_bounds__(256) void deep_refine_kernel(CandMergeArgs m, Refin
     if (kc == KEY_NONE) continue;  // (group-uniform)
     float sc;
     if (MET == L2 && a.cosine) {  // VectorMath.Cosine (:102-109) with the cached norms
-      const float dot = a.rows_rm ? exact_score_l8<1, IP, DT, true>(qp, a.rows_rm, kc, D, l)
-                                  : exact_score_l8<1, IP, DT, false>(qp, a.rows, kc, D, l);
+      const float dot = a.rows_rm ? exact_score_l8<V, IP, DT, true>(qp, a.rows_rm, kc, D, l)
+                                  : exact_score_l8<V, IP, DT, false>(qp, a.rows, kc, D, l);
       const float qn = a.qnorm[q], xn = a.rnorm[kc];
       sc = (qn < 1e-6f || xn < 1e-6f) ? 0.0f : dot / (qn * xn);
     } else {
-      sc = a.rows_rm ? exact_score_l8<1, MET, DT, true>(qp, a.rows_rm, kc, D, l)
-                     : exact_score_l8<1, MET, DT, false>(qp, a.rows, kc, D, l);
+      sc = a.rows_rm ? exact_score_l8<V, MET, DT, true>(qp, a.rows_rm, kc, D, l)
+                     : exact_score_l8<V, MET, DT, false>(qp, a.rows, kc, D, l);
     }
     if (l == 0) {
       ex[c] = sc;
@@ -850,7 +850,7 @@ size_t deep_refine_lds_bytes(int cap, int k1) {
   return P * sizeof(uint64_t);
 }
 
-void launch_deep_refine(const CandMergeArgs &m, const RefineArgs &a, int metric, hipStream_t st) {
+void launch_deep_refine(const CandMergeArgs &m, const RefineArgs &a, int metric, int V, hipStream_t st) {
   if (a.nq <= 0) return;
   if (a.k1 > DEEP_MAX || a.k1 < a.k || a.k > 256) throw std::invalid_argument("deep_refine: depth");
   const size_t lds = deep_refine_lds_bytes(m.cap, a.k1);
@@ -866,12 +866,21 @@ void launch_deep_refine(const CandMergeArgs &m, const RefineArgs &a, int metric,
     }
     hipLaunchKernelGGL(kern, dim3((unsigned)a.nq), dim3(256), lds, st, m, a);
   };
-  if (metric == L2) {
-    if (a.dim == 128) go(deep_refine_kernel<L2, 128>);
-    else go(deep_refine_kernel<L2, 0>);
+  // V = 1: the safe VectorMath forms (IVF); V = 4: the *Unsafe forms (FLAT, BruteForceVectorIndex.cs:350-356)
+  if (V == 4) {
+    if (metric == L2) {
+      if (a.dim == 128) go(deep_refine_kernel<4, L2, 128>);
+      else go(deep_refine_kernel<4, L2, 0>);
+    } else {
+      if (a.dim == 128) go(deep_refine_kernel<4, IP, 128>);
+      else go(deep_refine_kernel<4, IP, 0>);
+    }
+  } else if (metric == L2) {
+    if (a.dim == 128) go(deep_refine_kernel<1, L2, 128>);
+    else go(deep_refine_kernel<1, L2, 0>);
   } else {
-    if (a.dim == 128) go(deep_refine_kernel<IP, 128>);
-    else go(deep_refine_kernel<IP, 0>);
+    if (a.dim == 128) go(deep_refine_kernel<1, IP, 128>);
+    else go(deep_refine_kernel<1, IP, 0>);
   }
 }
 

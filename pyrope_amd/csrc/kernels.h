@@ -602,10 +602,10 @@ void launch_refine(const RefineArgs &a, int metric, int V, hipStream_t st);
 // what fails there into a.fail_list / a.fail_cnt; a.rec: shard records instead.  Upper-bound (resid, ub)
 // candidates only.
 void launch_merge_refine(const CandMergeArgs &m, const RefineArgs &a, int metric, int V, hipStream_t st);
-// k > 60: the same at depth K1 = 128 / 256 (K1 >= k + 4), one block per query (IVF, V = 1); LDS per block
+// k > 60: the same at depth K1 = 128 / 256 / 512 (k <= 0.8 K1), one block per query (IVF V = 1, FLAT V = 4); LDS per block
 // deep_refine_lds_bytes (the candidate buffer must keep it within 60 KiB)
 size_t deep_refine_lds_bytes(int cap, int k1);
-void launch_deep_refine(const CandMergeArgs &m, const RefineArgs &a, int metric, hipStream_t st);
+void launch_deep_refine(const CandMergeArgs &m, const RefineArgs &a, int metric, int V, hipStream_t st);
 void launch_gather_queries(const float *q, const int32_t *qidx, int64_t n, int32_t dim, float *out, hipStream_t st);
 // rows idx[i] of a [*][width] array of 32-bit words (probe lists of the failing queries)
 void launch_gather_words(const uint32_t *src, const int32_t *idx, int64_t n, int32_t width, uint32_t *out,

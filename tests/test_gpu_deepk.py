@@ -112,3 +112,30 @@ def test_ivf_large_k_other_dim_and_past_range(hiplib, oracle):
         np.testing.assert_array_equal(got[1][i][: len(ok)], labels[ok])
         assert np.array_equal(got[0][i][: len(os_)].view(np.uint32), os_.astype(np.float32).view(np.uint32))
     idx.close()
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_flat_large_k_matches_oracle(hiplib, oracle, metric):
+    """FLAT L2 / IP (BruteForceVectorIndex.cs:275-379, the *Unsafe forms) with k > 60 on the stream scan: the deep
+    refine at V = 4, failures on the exact scan; equal to the oracle and to PYR_DEEP_REFINE=0 (Cosine keeps the
+    exact scan)"""
+    from pyrope_amd import BruteForceVectorIndex, generate_synthetic
+    n, d = 30000, 128
+    x = generate_synthetic(n, d, 91)
+    idx = BruteForceVectorIndex(d, metric)
+    idx.add_labels(np.arange(n, dtype=np.int64), x)
+    q = generate_synthetic(48, d, 92)
+    for k in [61, 150, 256]:
+        got, calls = _sampled(hiplib, lambda: idx.search_batch(q, k))
+        assert calls >= 1, "FLAT k > 60 must take the stream scan"
+        with _env(PYR_DEEP_REFINE=0):
+            _bits(got, idx.search_batch(q, k))
+        for i in range(0, len(q), 7):
+            os_, ok = oracle.bf_search(x, None, metric, q[i], k)
+            np.testing.assert_array_equal(got[1][i], ok)
+            assert np.array_equal(got[0][i].view(np.uint32), os_.astype(np.float32).view(np.uint32))
+    with _env(PYR_FILTER_CERR="1e15"):
+        ref = idx.search_batch(q, 100)
+    with _env(PYR_DEEP_REFINE=0):
+        _bits(idx.search_batch(q, 100), ref)
+    idx.close()
