@@ -561,19 +561,20 @@ __global__ __launch_bounds__(256) void merge_refine_kernel(CandMergeArgs m, Refi
 }
 
 // k > 60 (round 5): the stream scans' merge and certified refine at depth K1 = 128 / 256 / 512, one 256-thread
-// block per query.  The emitted rows and K1 copies of the floor placeholder max(T_q, floor) are sorted in LDS by
-// rank key (bitonic, descending); the first K1 are the candidates (every row left out scores at most the K1-th);
+// block per query.  The emitted rows are sorted in LDS by rank key (bitonic, descending); the candidates are the
+// first K1 of them merged with K1 copies of the floor placeholder max(T_q, floor) -- the rows above the floor,
+// then floors (every row left out scores at most the K1-th);
 // their exact scores come from 8-lane groups in the reference's order (as merge_refine_kernel's); the ranks by
 // better() (score desc, key asc), the top k written, and the certificate of refine_kernel's upper-bound branch.
 // A NaN score fails the query (the exact scan decides).  What fails is listed for the caller's exact scan.
 constexpr int DEEP_MAX = 512;
 template <int V, int MET, int DT>
 __global__ __launch_bounds__(256) void deep_refine_kernel(CandMergeArgs m, RefineArgs a) {
-  extern __shared__ uint64_t dk[];  // the sort: P = pow2 >= emitted rows + K1 entries
+  extern __shared__ uint64_t dk[];  // the sort: P = pow2 >= max(emitted rows, K1, 256) entries
   __shared__ float ex[DEEP_MAX];
   __shared__ uint32_t ky[DEEP_MAX];
   __shared__ float skth_s;
-  __shared__ int nan_s, nreal_s;
+  __shared__ int nan_s, nreal_s, above_s;
   const int tid = threadIdx.x;
   const int64_t q = blockIdx.x;
   const int d = a.k1, k = a.k, D = DT > 0 ? DT : a.dim;
@@ -582,22 +583,22 @@ __global__ __launch_bounds__(256) void deep_refine_kernel(CandMergeArgs m, Refin
   float F = m.thr ? m.thr[q] : -INFINITY;
   if (fk != 0u) F = fmaxf(F, key_score(fk));
   int P = 256;
-  while (P < tot + d) P <<= 1;
+  while (P < tot || P < d) P <<= 1;
   const uint2 *cq = m.cand + (size_t)q * m.cap;
   for (int i = tid; i < P; i += 256) {
     uint64_t v = 0ull;
     if (i < tot) {
       const uint2 e = cq[i];
       v = pack_cand(__uint_as_float(e.x), e.y);
-    } else if (i < tot + d && F > -INFINITY) {
-      v = pack_cand(F, KEY_FLOOR);
     }
     dk[i] = v;
   }
+  const uint64_t fkey = F > -INFINITY ? pack_cand(F, KEY_FLOOR) : 0ull;
   if (tid == 0) {
     skth_s = -INFINITY;
     nan_s = 0;
     nreal_s = 0;
+    above_s = 0;
   }
   __syncthreads();
   for (int sz = 2; sz <= P; sz <<= 1)
@@ -614,6 +615,17 @@ __global__ __launch_bounds__(256) void deep_refine_kernel(CandMergeArgs m, Refin
       }
       __syncthreads();
     }
+  // the rows above the floor among the first K1 (sorted: a prefix), then floor copies
+  int above = 0;
+#pragma unroll
+  for (int h = 0; h < DEEP_MAX / 256; ++h) {
+    const int c = tid + 256 * h;
+    above += (c < d && c < tot && dk[c] > fkey) ? 1 : 0;
+  }
+  if (above) atomicAdd(&above_s, above);
+  __syncthreads();
+  const int j = above_s;
+  auto cand = [&](int c) -> uint64_t { return c < j ? dk[c] : (c < d ? fkey : 0ull); };
   // candidates c = tid + 256 h (h < d / 256, at least one)
   constexpr int H = DEEP_MAX / 256;
   uint32_t key[H];
@@ -622,7 +634,7 @@ __global__ __launch_bounds__(256) void deep_refine_kernel(CandMergeArgs m, Refin
 #pragma unroll
   for (int h = 0; h < H; ++h) {
     const int c = tid + 256 * h;
-    const uint64_t v = c < d ? dk[c] : 0ull;
+    const uint64_t v = cand(c);
     key[h] = v == 0ull ? KEY_NONE : ~(uint32_t)v;
     real[h] = key[h] != KEY_NONE && key[h] != KEY_FLOOR;
     nr += real[h] ? 1 : 0;
@@ -631,7 +643,7 @@ __global__ __launch_bounds__(256) void deep_refine_kernel(CandMergeArgs m, Refin
       ex[c] = -INFINITY;
     }
   }
-  const uint64_t vl = dk[d - 1];
+  const uint64_t vl = cand(d - 1);
   const bool excluded = vl != 0ull;  // the K1-th entry exists: rows (or the floor) were left out
   const float bound = excluded ? key_score((uint32_t)(vl >> 32)) : -INFINITY;
   __syncthreads();
@@ -846,7 +858,7 @@ void launch_merge_refine(const CandMergeArgs &m, const RefineArgs &a, int metric
 
 size_t deep_refine_lds_bytes(int cap, int k1) {
   size_t P = 256;
-  while (P < (size_t)cap + (size_t)k1) P <<= 1;
+  while (P < (size_t)cap || P < (size_t)k1) P <<= 1;
   return P * sizeof(uint64_t);
 }
 
