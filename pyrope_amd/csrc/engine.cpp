@@ -2373,8 +2373,8 @@ struct IvfFlatIndex : Index {
     int k1 = filter_k1(k);
     const bool budget_ok = prm.max_scans < 0 || (prm.max_scans > 0 && !ws.ext_probes && max_scans_stream());
     const bool nbuf = buf.live_count() > 0;
-    // k > 60: depth 128 / 256 (deep_refine_kernel) on built lists with no buffer and no budget
-    const bool deep = k1 == 0 && !nbuf && prm.max_scans < 0 && !ws.ext_probes && deep_refine_on();
+    // k > 60: depth 128 / 256 / 512 (deep_refine_kernel) with no budget (a buffer: merged beside, below)
+    const bool deep = k1 == 0 && prm.max_scans < 0 && !ws.ext_probes && deep_refine_on();
     if (deep) k1 = deep_k1(k);
     const bool fast = filter_enabled() && probes > 0 && (!nbuf || buffer_stream()) && budget_ok &&
                       (k <= KMAX_FAST || deep) && probes < MAX_PARTS && k1 > 0;

@@ -196,7 +196,8 @@ void launch_merge_keys(const float *ps, const uint32_t *pk, int64_t nq, int32_t 
                        const int64_t *row_labels, const int64_t *buf_labels, float *out_s, int64_t *out_l,
                        int32_t *out_keys, int32_t *out_cnt, hipStream_t st, const MergeIvf *ivf = nullptr);
 // Two per-query result sets (each sorted, ca / cb real entries) into the top k, a before b on equal scores
-// (IVF_PQ: the lists' certified answer and the buffer's exact one; k <= 64).
+// (IVF_PQ / IVF_FLAT: the lists' certified answer and the buffer's exact one; k <= 256; the outputs distinct
+// from both inputs).
 void launch_merge_two(const float *as, const int64_t *al, const int32_t *ca, const float *bs, const int64_t *bl,
                       const int32_t *cb, int64_t nq, int k, float *out_s, int64_t *out_l, int32_t *out_c,
                       hipStream_t st);

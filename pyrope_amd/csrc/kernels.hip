@@ -620,19 +620,18 @@ __global__ void merge_two_kernel(const float *as, const int64_t *al, const int32
   const int64_t *la = al + q * k, *lb = bl + q * k;
   const int na = min(ca[q], k), nb = min(cb[q], k);
   int i = 0, j = 0, o = 0;
-  float rs[64];
-  int64_t rl[64];
+  // (the outputs are neither input: written in place, any k)
   for (; o < k && (i < na || j < nb); ++o) {
     const bool ta = i < na && (j >= nb || score_key(a[i]) >= score_key(b[j]));
-    rs[o] = ta ? a[i] : b[j];
-    rl[o] = ta ? la[i] : lb[j];
+    out_s[q * k + o] = ta ? a[i] : b[j];
+    out_l[q * k + o] = ta ? la[i] : lb[j];
     if (ta) ++i;
     else ++j;
   }
   const int n = o;
-  for (o = 0; o < k; ++o) {
-    out_s[q * k + o] = o < n ? rs[o] : -INFINITY;
-    out_l[q * k + o] = o < n ? rl[o] : -1;
+  for (; o < k; ++o) {
+    out_s[q * k + o] = -INFINITY;
+    out_l[q * k + o] = -1;
   }
   if (out_c) out_c[q] = n;
 }
@@ -2081,7 +2080,7 @@ void launch_merge_two(const float *as, const int64_t *al, const int32_t *ca, con
                       const int32_t *cb, int64_t nq, int k, float *out_s, int64_t *out_l, int32_t *out_c,
                       hipStream_t st) {
   if (nq <= 0 || k <= 0) return;
-  if (k > 64) throw std::invalid_argument("merge_two: k > 64");
+  if (k > 256) throw std::invalid_argument("merge_two: k > 256");
   hipLaunchKernelGGL(merge_two_kernel, dim3(nblk(nq, 128)), dim3(128), 0, st, as, al, ca, bs, bl, cb, nq, k, out_s,
                      out_l, out_c);
 }

@@ -139,3 +139,36 @@ def test_flat_large_k_matches_oracle(hiplib, oracle, metric):
     with _env(PYR_DEEP_REFINE=0):
         _bits(idx.search_batch(q, 100), ref)
     idx.close()
+
+
+@pytest.mark.parametrize("metric", [0, 2])
+def test_ivf_large_k_with_buffer(hiplib, oracle, metric):
+    """k > 60 with rows added after Build: the lists through the deep refine, the buffer's exact top k beside them,
+    merged (merge_two_kernel, any k <= 256); equal to the oracle and to PYR_DEEP_REFINE=0"""
+    from pyrope_amd import IvfFlatVectorIndex, SearchOptions, generate_synthetic
+    d, n, nl, P = 128, 12000, 24, 6
+    x = generate_synthetic(n, d, 95)
+    idx = IvfFlatVectorIndex(d, metric, n_list=nl)
+    idx.add_labels(np.arange(n, dtype=np.int64), x)
+    idx.build()
+    extra = generate_synthetic(300, d, 96)
+    new_labels = np.concatenate([np.arange(n, n + 200), np.arange(0, 100)])
+    idx.add_labels(new_labels, extra)
+    off, labels, live = idx.ivf_layout()
+    rows = x[np.where(labels >= 0, labels, 0)]
+    cents = idx.centroids_array()
+    slot_labels = new_labels.tolist()
+    q = generate_synthetic(32, d, 97)
+    for k in [80, 200]:
+        opts = SearchOptions(nprobe=P)
+        got, calls = _sampled(hiplib, lambda: idx.search_batch(q, k, opts))
+        assert calls >= 1
+        with _env(PYR_DEEP_REFINE=0):
+            _bits(got, idx.search_batch(q, k, opts))
+        for i in range(0, len(q), 5):
+            os_, ok = oracle.ivf_search(q[i], k, cents, rows, off, live, buf=extra, metric=metric, nprobe=P)
+            exp = np.array([slot_labels[kk - oracle.BUFKEY] if kk >= oracle.BUFKEY else labels[kk] for kk in ok],
+                           np.int64)
+            np.testing.assert_array_equal(got[1][i][: len(exp)], exp)
+            assert np.array_equal(got[0][i][: len(os_)].view(np.uint32), os_.astype(np.float32).view(np.uint32))
+    idx.close()
