@@ -546,6 +546,20 @@ def run(args):
         pair_balance = {"pairs_per_rank": per, "max_over_mean": max(per) / (sum(per) / world),
                         "rows_per_rank": rank_rows,
                         "note": "(query, probed list) pairs of the whole batch by the rank owning the list"}
+    # list-sharded: the bytes each collective moves per rank per step (what a rank sends; an all_gather's
+    # output is world x its input), and the certificate failures of the home ranks (every one is re-run:
+    # rounds of fcap per home, ListShardedIvf)
+    shard_messages = shard_cert = None
+    if lists_sharded:
+        rb = 16 * (k + 1)
+        S = sharded.plan_home.shape[1]
+        shard_messages = {"plan_allgather_in": args.nq * S * 4, "record_alltoall_send": Q * rb,
+                          "fail_allgather_in": (1 + sharded.fcap) * 4, "rerun_alltoall_send": world * sharded.fcap * rb,
+                          "unit": "bytes per rank per step"}
+        shard_cert = {"fcap": sharded.fcap, "max_failures_per_home": sharded.max_fail,
+                      "extra_rounds_last_step": sharded.stats["extra_rounds"],
+                      "note": "certificate failures at one home rank over every step run (all ranks see every "
+                              "home's count); failures past fcap are re-run in further rounds"}
     if rank == 0:
         bytes_per_query = args.nprobe / args.nlist * N * D * 4 + args.nlist * D * 4
         out = {
@@ -612,6 +626,8 @@ def run(args):
             "collective_ms": {k_: round(v, 4) for k_, v in coll.items()} if world > 1 else None,
             "rank_rows": rank_rows,
             "pair_balance": pair_balance,
+            "shard_messages": shard_messages,
+            "shard_certificate": shard_cert,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -233,13 +233,21 @@ pyr_status pyr_merge_topk_parts_device(const float *d_scores, const int64_t *d_l
  * the probed-list loop of IvfFlatVectorIndex.Search (IvfFlatVectorIndex.cs:198-218): every rank holds
  * WHOLE lists (the rows FindNearestCentroid sends to a list it owns, in label order) plus the shared
  * quantizer, so a (query, list) pair is scanned by exactly one rank.  A step:
- *   home rank (its slice of the batch)  pyr_index_shard_prepare_device -> plan [nq][P + 1]
+ *   home rank (its slice of the batch)  pyr_index_shard_prepare_device -> plan [nq][P + 1 (+ P)]
  *   all ranks, all_gather(plans)        pyr_index_shard_search_device  -> one record per query
  *   all_to_all(records) to the homes    pyr_shard_merge_device         -> results + failed certificates
  *   all_gather(fail lists)              pyr_index_shard_rerun_device   -> exact records of the failures
  *   all_to_all(records) to the homes    pyr_shard_merge_device(qsel)   -> their exact results
  * Results equal the unsharded index's, ties included ((score desc, list asc, label asc) is the unsharded
- * storage order).  Device buffers, enqueued on `stream`; no host synchronisation. */
+ * storage order).  Device buffers, enqueued on `stream`; no host synchronisation.
+ * A home may have more failing certificates than one re-run round carries (fcap per home): its fail list
+ * (d_fail, sized to its batch) keeps every one, and the caller runs further rounds over the later entries
+ * (pyrope_amd/dist.py ListShardedIvf: a round takes entries [off, off + fcap) of every home's list).
+ * MaxScans (SearchOptions.MaxScans, IvfFlatVectorIndex.cs:202-212): the home runs the budget down its
+ * queries' probe order over every rank's lists (their lengths from pyr_index_set_list_samples) and the plan
+ * carries, per probe, what is left of it when that list is reached; the owning rank scans the list up to
+ * that many live rows.  A rank refuses a budgeted search (PYR_E_STATE) once one of its lists lost rows since
+ * its samples were set. */
 
 /* KMeansUtils.FindNearestCentroid (KMeansUtils.cs:70-93; the assignment of IvfFlatVectorIndex.Build,
  * :128-132) of n host rows against nlist host centroids: assign[i] = the list row i belongs to (ties ->
@@ -257,15 +265,21 @@ int64_t pyr_shard_record_bytes(int32_t k);
 pyr_status pyr_index_set_list_samples(pyr_index *index, const float *rows, const int64_t *counts,
                                       const int64_t *list_len, int32_t nlist);
 /* Home rank: the coarse ranking (IvfFlatVectorIndex.cs:186-198) and the threshold T_q of nq queries:
- * d_plan [nq][P + 1] int32 = P probe ids in rank order, then T_q's float bits; *width = P = min(nprobe, nlist). */
+ * d_plan [nq][P + 1] int32 = P probe ids in rank order, then T_q's float bits; *width = P = min(nprobe, nlist).
+ * With params->max_scans >= 0 the rows are [nq][2P + 1]: then, per probe, the MaxScans budget left when its
+ * list is reached (plan_budgets = 1 in the calls below).  Row stride: pyr_shard_plan_stride. */
 pyr_status pyr_index_shard_prepare_device(pyr_index *index, const float *d_q, int64_t nq, int32_t k,
                                           const pyr_search_params *params, int32_t *d_plan, int32_t *width,
                                           void *stream);
+/* The int32 row stride of a plan: P + 1, or 2P + 1 with a MaxScans budget (max_scans >= 0). */
+int32_t pyr_shard_plan_stride(int32_t width, int64_t max_scans);
 /* Every rank: the stream scan of the (query, list) pairs of the gathered plans whose list this rank owns
  * (the others are empty here) against T_q, the exact refine of each query's best candidates, and one
- * record per query (d_records: nq x pyr_shard_record_bytes(k)).  k <= 60. */
+ * record per query (d_records: nq x pyr_shard_record_bytes(k)).  k <= 60.  plan_budgets: the plans carry
+ * MaxScans budgets (prepared with max_scans >= 0); each owned list is then scanned up to its pair's budget. */
 pyr_status pyr_index_shard_search_device(pyr_index *index, const float *d_q, int64_t nq, int32_t k,
-                                         const int32_t *d_plan, int32_t width, void *d_records, void *stream);
+                                         const int32_t *d_plan, int32_t width, int32_t plan_budgets, void *d_records,
+                                         void *stream);
 /* Merge nparts (<= 64) records per query and certify.  d_records: [nparts][nrec] (an all_to_all's
  * output).  d_qsel = NULL: record i answers query i (i < nrec), results to row i, and with d_fail the
  * certificate (the k-th merged score beats every bound) lists failing queries: d_fail[0] = their count
@@ -276,11 +290,13 @@ pyr_status pyr_shard_merge_device(const void *d_records, int32_t nparts, int64_t
                                   int32_t *d_counts, int32_t *d_fail, int32_t fcap, void *stream);
 /* Every rank: the exact search (the *safe* VectorMath forms, IvfFlatVectorIndex.cs:200-218) of the
  * gathered failures d_fails [nranks][1 + fcap] (home-local query ids; home s's queries are rows
- * s * nq_home .. of d_q / d_plan) over this rank's lists: the answer to home s's j-th failure is record
- * s * fcap + j of d_records ([nranks * fcap] records, bound -inf). */
+ * s * nq_home .. of d_q / d_plan; nq = all of them) over this rank's lists: the answer to home s's j-th
+ * failure is record s * fcap + j of d_records ([nranks * fcap] records, bound -inf).  plan_budgets: as
+ * pyr_index_shard_search_device (the re-run stops where the scan did). */
 pyr_status pyr_index_shard_rerun_device(pyr_index *index, const float *d_q, int64_t nq, int32_t k,
-                                        const int32_t *d_plan, int32_t width, const int32_t *d_fails, int32_t nranks,
-                                        int32_t fcap, int64_t nq_home, void *d_records, void *stream);
+                                        const int32_t *d_plan, int32_t width, int32_t plan_budgets,
+                                        const int32_t *d_fails, int32_t nranks, int32_t fcap, int64_t nq_home,
+                                        void *d_records, void *stream);
 
 /* HBM plan (host arithmetic, no device needed): the bytes an IVF_FLAT index of nrows rows in nlist
  * lists (longest max_list_len rows) holds on one GPU, and the workspace one batched search of nq queries

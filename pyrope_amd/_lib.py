@@ -123,9 +123,11 @@ SIGNATURES = {
     "pyr_index_set_list_samples": (C.c_int, [_vp, _f, _i64, _i64, C.c_int32]),
     "pyr_index_shard_prepare_device": (C.c_int, [_vp, _vp, C.c_int64, C.c_int32, C.POINTER(SearchParams), _vp,
                                                  C.POINTER(C.c_int32), _vp]),
-    "pyr_index_shard_search_device": (C.c_int, [_vp, _vp, C.c_int64, C.c_int32, _vp, C.c_int32, _vp, _vp]),
-    "pyr_index_shard_rerun_device": (C.c_int, [_vp, _vp, C.c_int64, C.c_int32, _vp, C.c_int32, _vp, C.c_int32,
-                                               C.c_int32, C.c_int64, _vp, _vp]),
+    "pyr_shard_plan_stride": (C.c_int32, [C.c_int32, C.c_int64]),
+    "pyr_index_shard_search_device": (C.c_int, [_vp, _vp, C.c_int64, C.c_int32, _vp, C.c_int32, C.c_int32, _vp,
+                                                _vp]),
+    "pyr_index_shard_rerun_device": (C.c_int, [_vp, _vp, C.c_int64, C.c_int32, _vp, C.c_int32, C.c_int32, _vp,
+                                               C.c_int32, C.c_int32, C.c_int64, _vp, _vp]),
     "pyr_shard_merge_device": (C.c_int, [_vp, C.c_int32, C.c_int64, C.c_int32, _vp, C.c_int32, _vp, _vp, _vp, _vp,
                                          C.c_int32, _vp]),
     "pyr_profile_enable": (None, [C.c_int32]),

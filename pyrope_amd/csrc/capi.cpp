@@ -664,6 +664,9 @@ pyr_status pyr_merge_topk_parts_device(const float *d_scores, const int64_t *d_l
 }
 
 int64_t pyr_shard_record_bytes(int32_t k) { return k > 0 ? pyr::shard_record_bytes(k) : 0; }
+int32_t pyr_shard_plan_stride(int32_t width, int64_t max_scans) {
+  return width > 0 ? pyr::shard_plan_stride(width, max_scans >= 0) : 0;
+}
 
 pyr_status pyr_index_set_list_samples(pyr_index *index, const float *rows, const int64_t *counts,
                                       const int64_t *list_len, int32_t nlist) {
@@ -695,7 +698,8 @@ pyr_status pyr_index_shard_prepare_device(pyr_index *index, const float *d_q, in
 }
 
 pyr_status pyr_index_shard_search_device(pyr_index *index, const float *d_q, int64_t nq, int32_t k,
-                                         const int32_t *d_plan, int32_t width, void *d_records, void *stream) {
+                                         const int32_t *d_plan, int32_t width, int32_t plan_budgets, void *d_records,
+                                         void *stream) {
   if (!index || nq < 0 || (nq > 0 && (!d_q || !d_plan || !d_records))) return fail(PYR_E_ARG, "null argument");
   return guard([&] {
     pyr::Index &ix = *index->impl;
@@ -703,14 +707,15 @@ pyr_status pyr_index_shard_search_device(pyr_index *index, const float *d_q, int
     std::shared_lock<std::shared_mutex> g(ix.mu);
     pyr::Workspace &ws = ix.ws_for_stream(reinterpret_cast<hipStream_t>(stream));
     std::lock_guard<std::mutex> wg(ws.m);
-    ix.shard_search(d_q, nq, k, d_plan, width, d_records, ws);
+    ix.shard_search(d_q, nq, k, d_plan, width, plan_budgets != 0, d_records, ws);
     HIPCHK(hipGetLastError());
   });
 }
 
 pyr_status pyr_index_shard_rerun_device(pyr_index *index, const float *d_q, int64_t nq, int32_t k,
-                                        const int32_t *d_plan, int32_t width, const int32_t *d_fails, int32_t nranks,
-                                        int32_t fcap, int64_t nq_home, void *d_records, void *stream) {
+                                        const int32_t *d_plan, int32_t width, int32_t plan_budgets,
+                                        const int32_t *d_fails, int32_t nranks, int32_t fcap, int64_t nq_home,
+                                        void *d_records, void *stream) {
   if (!index || nq < 0 || !d_plan || !d_fails || !d_records || nranks <= 0 || nranks > 64 || fcap <= 0)
     return fail(PYR_E_ARG, "bad argument");
   return guard([&] {
@@ -719,7 +724,7 @@ pyr_status pyr_index_shard_rerun_device(pyr_index *index, const float *d_q, int6
     std::shared_lock<std::shared_mutex> g(ix.mu);
     pyr::Workspace &ws = ix.ws_for_stream(reinterpret_cast<hipStream_t>(stream));
     std::lock_guard<std::mutex> wg(ws.m);
-    ix.shard_rerun(d_q, nq, k, d_plan, width, d_fails, nranks, fcap, nq_home, d_records, ws);
+    ix.shard_rerun(d_q, nq, k, d_plan, width, plan_budgets != 0, d_fails, nranks, fcap, nq_home, d_records, ws);
     HIPCHK(hipGetLastError());
   });
 }

@@ -947,6 +947,8 @@ static bool merge_refine_fused() {
 struct ShardCtx {
   const float *thr;
   uint8_t *rec;
+  const int32_t *rem = nullptr;  // MaxScans: the plans' remaining budgets per (query, probe), row stride rstride
+  int rstride = 0;
 };
 
 // re-run the listed queries through the exact scan and put their rows in place
@@ -2479,7 +2481,9 @@ struct IvfFlatIndex : Index {
       const int32_t *ext = ws.ext_probes;
       if (ext) ws.ext_probes = ext + a0 * ws.ext_nprobe;
       ShardCtx s2{};
-      if (sh) s2 = ShardCtx{sh->thr + a0, sh->rec + a0 * shard_record_bytes(k)};
+      if (sh)
+        s2 = ShardCtx{sh->thr + a0, sh->rec + a0 * shard_record_bytes(k), sh->rem ? sh->rem + a0 * sh->rstride : nullptr,
+                      sh->rstride};
       try {
         stream_slice(d_q + a0 * dim, n, k, k1, probes, ch, nparts, cap, d_s ? d_s + a0 * k : nullptr,
                      d_l ? d_l + a0 * k : nullptr, d_c ? d_c + a0 : nullptr, ws, sh ? &s2 : nullptr);
@@ -2566,15 +2570,16 @@ struct IvfFlatIndex : Index {
     }
     const int64_t npos = nq * probes;
     // MaxScans (:202-212; the buffer is empty here): every pair's exclusive row bound, in probe order over the
-    // live rows (ivf_limits_kernel, one chunk per probe), then at its qlist position for the scan kernel
-    const bool budget = ws.max_scans > 0 && !sh;
+    // live rows (ivf_limits_kernel, one chunk per probe), then at its qlist position for the scan kernel; a
+    // list-sharded rank takes each pair's remaining budget from the home rank's plan
+    const bool budget = sh ? sh->rem != nullptr : ws.max_scans > 0;
     if (budget) {
       ws.limits.ensure(sizeof(uint32_t) * std::max<int64_t>(npos, 1));
       ws.plim.ensure(sizeof(uint32_t) * std::max<int64_t>(npos, 1));
       IvfChunking c1{1, 1, 0};
-      launch_ivf_limits(ws.probes.as<int32_t>(), nq, probes, probes, ws.max_scans, dlb.as<int32_t>(),
+      launch_ivf_limits(ws.probes.as<int32_t>(), nq, probes, probes, sh ? 0 : ws.max_scans, dlb.as<int32_t>(),
                         dle.as<int32_t>(), dllive.as<int32_t>(), lists.live.as<uint8_t>(), c1,
-                        ws.limits.as<uint32_t>(), ws.st);
+                        ws.limits.as<uint32_t>(), ws.st, sh ? sh->rem : nullptr, sh ? sh->rstride : 0);
       launch_pos_limits(ws.qpos.as<int32_t>(), ws.limits.as<uint32_t>(), npos, ws.plim.as<uint32_t>(), ws.st);
     }
     const int sv = scan_sample_values();
@@ -2858,6 +2863,7 @@ struct IvfFlatIndex : Index {
   // unsharded index's sample pass scores), so that a query's home rank computes the unsharded T_q.
   std::unique_ptr<RowStore> ssamp;
   DevMem sslb, ssle, sglb, sgle;
+  std::vector<int64_t> sglen;  // host copy of every list's length given with the samples (MaxScans accounting)
 
   void set_list_samples(const float *rows, const int64_t *counts, const int64_t *glen, int nl) override {
     if (!built || coarse.nlist <= 0) throw Error(PYR_E_STATE, "index is not built");
@@ -2925,6 +2931,17 @@ struct IvfFlatIndex : Index {
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(wst));
     ssamp = std::move(ss);
+    sglen.assign(glen, glen + nl);
+  }
+
+  // MaxScans on a list-sharded rank: the home ran the budget down every rank's lists with the lengths given to
+  // set_list_samples, so the lists this rank owns must still hold exactly that many live rows (a Delete since
+  // would shift every later pair's budget on the other ranks)
+  void check_shard_budget_lengths() const {
+    for (size_t l = 0; l < llen.size() && l < sglen.size(); ++l)
+      if (llen[l] > 0 && (int64_t)llive[l] != sglen[l])
+        throw Error(PYR_E_STATE, "list-sharded MaxScans: a list's live rows changed since set_list_samples (call it "
+                                 "again with the new lengths)");
   }
 
   int shard_prepare(const float *d_q, int64_t nq, int k, const pyr_search_params &prm, int32_t *d_plan,
@@ -2936,6 +2953,8 @@ struct IvfFlatIndex : Index {
     const int P = std::max(0, std::min(nprobe, coarse.nlist));
     if (P == 0 || nq == 0) return P;
     if (P >= MAX_PARTS) throw Error(PYR_E_ARG, "nprobe too large");
+    const bool budget = prm.max_scans >= 0;  // plan rows carry the remaining budget per probe (S = 2P + 1)
+    const int S = shard_plan_stride(P, budget);
     RowStore &s = *ssamp;
     const int dt = s.tdim(), sv = scan_sample_values();
     // slices of <= 1 GiB of operands and samples
@@ -2985,6 +3004,15 @@ struct IvfFlatIndex : Index {
       stream_ub_terms(dt, metric, filter_f16_cerr(dt, metric, FILTER_F16X1), filter_cerr(dt),
                       filter_f16_abs(dt, metric, s.sx, FILTER_F16X1), sa);
       sa.mub = s.row_terms(metric, sa.kr, sa.kx, ws.st);
+      if (budget) {  // the pairs' budgets, and the sample pass bounded as the unsharded LIM sample is
+        ws.shp.ensure(sizeof(int32_t) * npos);
+        ws.limits.ensure(sizeof(uint32_t) * npos);
+        ws.plim.ensure(sizeof(uint32_t) * npos);
+        launch_shard_budget(ws.probes.as<int32_t>(), n, P, prm.max_scans, sgle.as<int32_t>(), sslb.as<int32_t>(),
+                            ssle.as<int32_t>(), ws.shp.as<int32_t>(), ws.limits.as<uint32_t>(), ws.st);
+        launch_pos_limits(ws.qpos.as<int32_t>(), ws.limits.as<uint32_t>(), npos, ws.plim.as<uint32_t>(), ws.st);
+        sa.plim = ws.plim.as<uint32_t>();
+      }
       {
         PhaseTimer t(PH_SAMPLE, ws.st);
         stream_sample(sa, metric, maxi, ws.st);
@@ -3000,13 +3028,14 @@ struct IvfFlatIndex : Index {
         sel.thr = ws.sthr.as<float>();
         launch_stream_select(sel, ws.st);
       }
-      launch_pack_plan(ws.probes.as<int32_t>(), ws.sthr.as<float>(), n, P, d_plan + a0 * (P + 1), ws.st);
+      launch_pack_plan(ws.probes.as<int32_t>(), ws.sthr.as<float>(), budget ? ws.shp.as<int32_t>() : nullptr, n, P,
+                       d_plan + a0 * S, ws.st);
       HIPCHK(hipGetLastError());
     }
     return P;
   }
 
-  void shard_search(const float *d_q, int64_t nq, int k, const int32_t *d_plan, int P, void *d_rec,
+  void shard_search(const float *d_q, int64_t nq, int k, const int32_t *d_plan, int P, bool budget, void *d_rec,
                     Workspace &ws) override {
     if (!built || coarse.nlist <= 0) throw Error(PYR_E_STATE, "index is not built");
     if (metric == COS) throw Error(PYR_E_STATE, "list-sharded search serves L2 / IP");
@@ -3016,10 +3045,13 @@ struct IvfFlatIndex : Index {
       throw Error(PYR_E_ARG, "topK out of the list-sharded search's range");
     if (P <= 0 || P > coarse.nlist || P >= MAX_PARTS) throw Error(PYR_E_ARG, "plan width does not fit the index");
     if (nq == 0) return;
+    if (budget) check_shard_budget_lengths();
+    const int S = shard_plan_stride(P, budget);
     ws.shp.ensure(sizeof(int32_t) * nq * P);
     ws.shthr.ensure(sizeof(float) * nq);
-    launch_unpack_plan(d_plan, nq, P, ws.shp.as<int32_t>(), ws.shthr.as<float>(), ws.st);
-    const ShardCtx sh{ws.shthr.as<float>(), static_cast<uint8_t *>(d_rec)};
+    launch_unpack_plan(d_plan, nq, P, S, ws.shp.as<int32_t>(), ws.shthr.as<float>(), ws.st);
+    const ShardCtx sh{ws.shthr.as<float>(), static_cast<uint8_t *>(d_rec), budget ? d_plan + P + 1 : nullptr,
+                      budget ? S : 0};
     ws.ext_probes = ws.shp.as<int32_t>();
     ws.ext_nprobe = P;
     try {
@@ -3031,12 +3063,22 @@ struct IvfFlatIndex : Index {
     ws.ext_probes = nullptr;
   }
 
-  void shard_rerun(const float *d_q, int64_t nq, int k, const int32_t *d_plan, int P, const int32_t *d_fails,
-                   int nranks, int fcap, int64_t nq_home, void *d_rec, Workspace &ws) override {
-    (void)nq;
+  void shard_rerun(const float *d_q, int64_t nq, int k, const int32_t *d_plan, int P, bool budget,
+                   const int32_t *d_fails, int nranks, int fcap, int64_t nq_home, void *d_rec, Workspace &ws) override {
     if (!built || coarse.nlist <= 0) throw Error(PYR_E_STATE, "index is not built");
     if (k <= 0 || k > 64) throw Error(PYR_E_ARG, "topK out of the list-sharded search's range");
     if (fcap <= 0 || nranks <= 0) return;
+    const int S = shard_plan_stride(P, budget);
+    if (budget) {  // every pair's row bound on this rank's lists, as shard_search bounds the scan
+      check_shard_budget_lengths();
+      ws.shp.ensure(sizeof(int32_t) * std::max<int64_t>(nq, 1) * P);
+      ws.shthr.ensure(sizeof(float) * std::max<int64_t>(nq, 1));
+      ws.limits.ensure(sizeof(uint32_t) * std::max<int64_t>(nq, 1) * P);
+      launch_unpack_plan(d_plan, nq, P, S, ws.shp.as<int32_t>(), ws.shthr.as<float>(), ws.st);
+      IvfChunking c1{1, 1, 0};
+      launch_ivf_limits(ws.shp.as<int32_t>(), nq, P, P, 0, dlb.as<int32_t>(), dle.as<int32_t>(), dllive.as<int32_t>(),
+                        lists.live.as<uint8_t>(), c1, ws.limits.as<uint32_t>(), ws.st, d_plan + P + 1, S);
+    }
     const int64_t mf = (int64_t)nranks * fcap;
     ws.fail.ensure(sizeof(int32_t) * mf);
     ws.rpos.ensure(sizeof(int32_t) * mf);
@@ -3050,7 +3092,8 @@ struct IvfFlatIndex : Index {
     ra.queries = d_q;
     ra.probes = d_plan;
     ra.nprobe = P;
-    ra.pstride = P + 1;
+    ra.pstride = S;
+    ra.qlim = budget ? ws.limits.as<uint32_t>() : nullptr;
     ra.lb = dlb.as<int32_t>();
     ra.le = dle.as<int32_t>();
     ra.fail = ws.fail.as<int32_t>();

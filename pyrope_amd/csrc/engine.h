@@ -299,22 +299,23 @@ struct Index {
     (void)nlist;
     throw Error(PYR_E_STATE, "index kind has no list-sharded search (IVF_FLAT only)");
   }
-  // home side: coarse ranking + T_q of nq queries -> plan [nq][P + 1]; returns P
+  // home side: coarse ranking + T_q of nq queries -> plan [nq][shard_plan_stride(P, max_scans >= 0)]; returns P
   virtual int shard_prepare(const float *d_q, int64_t nq, int k, const pyr_search_params &p, int32_t *d_plan,
                             Workspace &ws) {
     (void)d_q, (void)nq, (void)k, (void)p, (void)d_plan, (void)ws;
     throw Error(PYR_E_STATE, "index kind has no list-sharded search (IVF_FLAT only)");
   }
   // every rank: its owned lists against the plans -> one record per query
-  virtual void shard_search(const float *d_q, int64_t nq, int k, const int32_t *d_plan, int P, void *d_rec,
-                            Workspace &ws) {
-    (void)d_q, (void)nq, (void)k, (void)d_plan, (void)P, (void)d_rec, (void)ws;
+  virtual void shard_search(const float *d_q, int64_t nq, int k, const int32_t *d_plan, int P, bool budget,
+                            void *d_rec, Workspace &ws) {
+    (void)d_q, (void)nq, (void)k, (void)d_plan, (void)P, (void)budget, (void)d_rec, (void)ws;
     throw Error(PYR_E_STATE, "index kind has no list-sharded search (IVF_FLAT only)");
   }
   // every rank: the exact re-run of the gathered failures [nranks][1 + fcap] -> records [nranks * fcap]
-  virtual void shard_rerun(const float *d_q, int64_t nq, int k, const int32_t *d_plan, int P, const int32_t *d_fails,
-                           int nranks, int fcap, int64_t nq_home, void *d_rec, Workspace &ws) {
-    (void)d_q, (void)nq, (void)k, (void)d_plan, (void)P, (void)d_fails, (void)nranks, (void)fcap, (void)nq_home;
+  virtual void shard_rerun(const float *d_q, int64_t nq, int k, const int32_t *d_plan, int P, bool budget,
+                           const int32_t *d_fails, int nranks, int fcap, int64_t nq_home, void *d_rec, Workspace &ws) {
+    (void)d_q, (void)nq, (void)k, (void)d_plan, (void)P, (void)budget, (void)d_fails, (void)nranks, (void)fcap;
+    (void)nq_home;
     (void)d_rec, (void)ws;
     throw Error(PYR_E_STATE, "index kind has no list-sharded search (IVF_FLAT only)");
   }

@@ -229,7 +229,8 @@ void launch_ivf_items(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t
 // IVF max_scans limits per (query, probe, chunk) slot (IvfFlatVectorIndex.cs:200-212)
 void launch_ivf_limits(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t nparts, int64_t remaining,
                        const int32_t *list_begin, const int32_t *list_end, const int32_t *list_live,
-                       const uint8_t *live, IvfChunking ch, uint32_t *limits, hipStream_t st);
+                       const uint8_t *live, IvfChunking ch, uint32_t *limits, hipStream_t st,
+                       const int32_t *prem = nullptr, int rstride = 0);
 
 // the per-(query, probe) bounds (cmax 1) at the pairs' qlist positions: plim[qpos[i]] = limits[i]
 void launch_pos_limits(const int32_t *qpos, const uint32_t *limits, int64_t n, uint32_t *plim, hipStream_t st);
@@ -470,8 +471,17 @@ struct ShardMergeArgs {
 };
 void launch_shard_merge(const ShardMergeArgs &a, int64_t max_rec, hipStream_t st);
 // plan [nq][P + 1] <-> probes [nq][P] + T_q [nq]
-void launch_pack_plan(const int32_t *probes, const float *thr, int64_t nq, int P, int32_t *plan, hipStream_t st);
-void launch_unpack_plan(const int32_t *plan, int64_t nq, int P, int32_t *probes, float *thr, hipStream_t st);
+// plan rows [P probes][T_q bits][P remaining budgets, with a MaxScans budget only]: shard_plan_stride(P, budget)
+inline int shard_plan_stride(int P, bool budget) { return P + 1 + (budget ? P : 0); }
+void launch_pack_plan(const int32_t *probes, const float *thr, const int32_t *rem, int64_t nq, int P, int32_t *plan,
+                      hipStream_t st);
+void launch_unpack_plan(const int32_t *plan, int64_t nq, int P, int stride, int32_t *probes, float *thr, hipStream_t st);
+// the home rank's MaxScans accounting (IvfFlatVectorIndex.cs:202-212) over every rank's lists: per (query, probe)
+// the budget left when the probe's list is reached, rem[q][p] = max(0, max_scans - sum of the live lengths of
+// the lists probed before it) (glive: every list's live rows, replicated), and the absolute row bound of the pair
+// in the replicated sample store (slb / sle: its lists' sample rows; a sample holds no tombstones)
+void launch_shard_budget(const int32_t *probes, int64_t nq, int P, int64_t max_scans, const int32_t *glive,
+                         const int32_t *slb, const int32_t *sle, int32_t *rem, uint32_t *slimits, hipStream_t st);
 // gathered fail lists [nranks][1 + fcap] -> global failing queries fail[], their record slots pos[], *nfail
 void launch_shard_fail_compact(const int32_t *fails, int nranks, int fcap, int64_t nq_home, int32_t *fail, int32_t *pos,
                                int32_t *nfail, hipStream_t st);

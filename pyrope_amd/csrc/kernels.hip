@@ -872,15 +872,18 @@ __global__ void ivf_fill_kernel(const int32_t *probes, int64_t nq, int nprobe, i
 // where the budget runs out is bounded at its (rem + 1)-th live row (rows before it hold exactly rem live
 // ones), found 64 rows at a time (ballot + prefix popcount) -- a tombstone-free list directly at lb + rem.
 // (Round 4 walked that list row by row in one thread: 2.5 ms at I1 with MaxScans 5,000.)
+// prem != null (a list-sharded rank): the home rank already ran the budget down the probe order over every
+// rank's lists (shard_budget_kernel); prem[q * rstride + p] is what was left when pair p's list was reached.
 __global__ __launch_bounds__(256) void ivf_limits_kernel(const int32_t *probes, int64_t nq, int nprobe, int nparts,
                                                          int cmax, int64_t remaining, const int32_t *lb,
                                                          const int32_t *le, const int32_t *llive, const uint8_t *live,
-                                                         uint32_t *limits) {
+                                                         uint32_t *limits, const int32_t *prem, int rstride) {
   const int lane = threadIdx.x & 63;
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= nq) return;
   int64_t rem = remaining;
   for (int p = 0; p < nprobe; ++p) {
+    if (prem) rem = prem[(size_t)q * rstride + p];
     const int lst = probes[q * nprobe + p];
     const int b = lb[lst], e = le[lst], n = llive[lst];
     uint32_t lim;
@@ -1804,10 +1807,11 @@ void launch_ivf_items(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t
 
 void launch_ivf_limits(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t nparts, int64_t remaining,
                        const int32_t *list_begin, const int32_t *list_end, const int32_t *list_live,
-                       const uint8_t *live, IvfChunking ch, uint32_t *limits, hipStream_t st) {
+                       const uint8_t *live, IvfChunking ch, uint32_t *limits, hipStream_t st, const int32_t *prem,
+                       int rstride) {
   if (nq <= 0) return;
   hipLaunchKernelGGL(ivf_limits_kernel, dim3(nblk(nq, 4)), dim3(256), 0, st, probes, nq, nprobe, nparts, ch.cmax,
-                     remaining, list_begin, list_end, list_live, live, limits);
+                     remaining, list_begin, list_end, list_live, live, limits, prem, rstride);
 }
 
 void launch_pos_limits(const int32_t *qpos, const uint32_t *limits, int64_t n, uint32_t *plim, hipStream_t st) {

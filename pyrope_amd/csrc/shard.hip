@@ -33,21 +33,40 @@ __device__ __forceinline__ bool entry_better(float s1, int32_t l1, int64_t b1, f
   return s1 > s2 || (s1 == s2 && (l1 < l2 || (l1 == l2 && b1 < b2)));
 }
 
-// plan [nq][P + 1] = P probe ids, then T_q's float bits
-__global__ void pack_plan_kernel(const int32_t *probes, const float *thr, int64_t nq, int P, int32_t *plan) {
+// plan [nq][S] = P probe ids, T_q's float bits, then (a MaxScans budget: S = 2P + 1) the P remaining budgets
+__global__ void pack_plan_kernel(const int32_t *probes, const float *thr, const int32_t *rem, int64_t nq, int P,
+                                 int32_t *plan) {
+  const int S = P + 1 + (rem ? P : 0);
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= nq * (P + 1)) return;
-  const int64_t q = e / (P + 1);
-  const int c = (int)(e - q * (P + 1));
-  plan[e] = c < P ? probes[q * P + c] : __float_as_int(thr[q]);
+  if (e >= nq * S) return;
+  const int64_t q = e / S;
+  const int c = (int)(e - q * S);
+  plan[e] = c < P ? probes[q * P + c] : c == P ? __float_as_int(thr[q]) : rem[q * P + c - P - 1];
 }
-__global__ void unpack_plan_kernel(const int32_t *plan, int64_t nq, int P, int32_t *probes, float *thr) {
+__global__ void unpack_plan_kernel(const int32_t *plan, int64_t nq, int P, int S, int32_t *probes, float *thr) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= nq * (P + 1)) return;
   const int64_t q = e / (P + 1);
   const int c = (int)(e - q * (P + 1));
-  if (c < P) probes[q * P + c] = plan[e];
-  else thr[q] = __int_as_float(plan[e]);
+  if (c < P) probes[q * P + c] = plan[q * S + c];
+  else thr[q] = __int_as_float(plan[q * S + P]);
+}
+
+// MaxScans on the home rank (IvfFlatVectorIndex.cs:202-212: the lists in probe order, each scanned until
+// `scanned` reaches maxScans; the list-sharded index has no buffer).  One thread per query.
+__global__ void shard_budget_kernel(const int32_t *probes, int64_t nq, int P, int64_t max_scans, const int32_t *glive,
+                                    const int32_t *slb, const int32_t *sle, int32_t *rem, uint32_t *slimits) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  int64_t r = max_scans;
+  for (int p = 0; p < P; ++p) {
+    const int lst = probes[q * P + p];
+    const int64_t left = r > 0 ? r : 0;
+    rem[q * P + p] = (int32_t)min(left, (int64_t)INT32_MAX);
+    const int64_t ns = sle[lst] - slb[lst];
+    slimits[q * P + p] = (uint32_t)(slb[lst] + min(left, ns));
+    r = left - glive[lst];
+  }
 }
 
 // One wave per record index i: a k-step merge of the nparts sorted entry lists (lane s holds the head of
@@ -170,13 +189,23 @@ __global__ __launch_bounds__(256) void shard_fail_compact_kernel(const int32_t *
 
 }  // namespace
 
-void launch_pack_plan(const int32_t *probes, const float *thr, int64_t nq, int P, int32_t *plan, hipStream_t st) {
+void launch_pack_plan(const int32_t *probes, const float *thr, const int32_t *rem, int64_t nq, int P, int32_t *plan,
+                      hipStream_t st) {
   if (nq <= 0) return;
-  hipLaunchKernelGGL(pack_plan_kernel, dim3(nblk(nq * (P + 1), 256)), dim3(256), 0, st, probes, thr, nq, P, plan);
+  const int S = shard_plan_stride(P, rem != nullptr);
+  hipLaunchKernelGGL(pack_plan_kernel, dim3(nblk(nq * S, 256)), dim3(256), 0, st, probes, thr, rem, nq, P, plan);
 }
-void launch_unpack_plan(const int32_t *plan, int64_t nq, int P, int32_t *probes, float *thr, hipStream_t st) {
+void launch_unpack_plan(const int32_t *plan, int64_t nq, int P, int stride, int32_t *probes, float *thr,
+                        hipStream_t st) {
   if (nq <= 0) return;
-  hipLaunchKernelGGL(unpack_plan_kernel, dim3(nblk(nq * (P + 1), 256)), dim3(256), 0, st, plan, nq, P, probes, thr);
+  hipLaunchKernelGGL(unpack_plan_kernel, dim3(nblk(nq * (P + 1), 256)), dim3(256), 0, st, plan, nq, P, stride, probes,
+                     thr);
+}
+void launch_shard_budget(const int32_t *probes, int64_t nq, int P, int64_t max_scans, const int32_t *glive,
+                         const int32_t *slb, const int32_t *sle, int32_t *rem, uint32_t *slimits, hipStream_t st) {
+  if (nq <= 0 || P <= 0) return;
+  hipLaunchKernelGGL(shard_budget_kernel, dim3(nblk(nq, 256)), dim3(256), 0, st, probes, nq, P, max_scans, glive, slb,
+                     sle, rem, slimits);
 }
 void launch_shard_merge(const ShardMergeArgs &a, int64_t max_rec, hipStream_t st) {
   if (max_rec <= 0 || a.k <= 0) return;

@@ -220,7 +220,8 @@ def rank_memory_plan_lists(dim: int, rank_rows: int, nlist: int, max_list_len: i
     ib, wb = rank_memory_plan(dim, rank_rows, nlist, max_list_len, Q, P, k)
     sb, swb = rank_memory_plan(dim, nlist * SAMPLE_ROWS, nlist, SAMPLE_ROWS, nq_home, P, k)
     rb = 16 * (k + 1)
-    step = 4 * (P + 1) * (nq_home + Q) + 2 * rb * Q + 4 * world * (1 + fcap) * 2 + 2 * rb * world * fcap
+    step = (4 * (2 * P + 1) * (nq_home + Q) + 2 * rb * Q + 4 * world * (1 + fcap) * 2 + 2 * rb * world * fcap
+            + 4 * (1 + world) * (1 + nq_home))
     return ib + sb, max(wb, swb) + step
 
 
@@ -308,12 +309,23 @@ class Comm:
         return int(self.all_reduce_sum(t).max())
 
 
+def shard_plan_stride(width: int, budget: bool) -> int:
+    """int32 row stride of a list-sharded plan (pyr_shard_plan_stride): P probes + T_q, and with a MaxScans
+    budget the P remaining budgets."""
+    return width + 1 + (width if budget else 0)
+
+
 class DeviceShardEngine:
     """The list-sharded step's per-rank operations on libpyrope_hip (IVF_FLAT shard index, device buffers
     as torch tensors, one stream)."""
 
     def __init__(self, index, k: int, options=None, stream=None):
         self.index, self.k, self.options, self._stream = index, k, options, stream
+
+    @property
+    def budget(self) -> bool:
+        """A MaxScans search: the plans carry the budget left at every probe (IvfFlatVectorIndex.cs:202-212)."""
+        return self.options is not None and getattr(self.options, "max_scans", None) is not None
 
     @property
     def stream(self) -> int:
@@ -330,7 +342,7 @@ class DeviceShardEngine:
 
     def search(self, q_all, plan_all, width, rec):
         self.index.shard_search_device(q_all.data_ptr(), q_all.shape[0], self.k, plan_all.data_ptr(), width,
-                                       rec.data_ptr(), self.stream)
+                                       rec.data_ptr(), self.stream, budgets=self.budget)
 
     def merge(self, rec_parts, out_s, out_l, fail):
         from . import _lib
@@ -342,7 +354,8 @@ class DeviceShardEngine:
     def rerun(self, q_all, plan_all, width, fails_all, nq_home, rec):
         world, f1 = fails_all.shape
         self.index.shard_rerun_device(q_all.data_ptr(), q_all.shape[0], self.k, plan_all.data_ptr(), width,
-                                      fails_all.data_ptr(), world, f1 - 1, nq_home, rec.data_ptr(), self.stream)
+                                      fails_all.data_ptr(), world, f1 - 1, nq_home, rec.data_ptr(), self.stream,
+                                      budgets=self.budget)
 
     def merge_rerun(self, rec_parts, fail_home, out_s, out_l):
         from . import _lib
@@ -356,20 +369,26 @@ class ListShardedIvf:
     """One list-sharded multi-GPU IVF_FLAT search step (include/pyrope_ann.h "List-sharded multi-GPU"):
 
       1. plan: the home rank ranks the quantizer for its nq_local queries and takes T_q from its replicated
-         sample of every list (engine.prepare);
+         sample of every list (engine.prepare); with a MaxScans budget the plan also carries, per probe, the
+         budget left when that list is reached (IvfFlatVectorIndex.cs:202-212);
       2. all_gather(plans): every rank gets every query's probe lists and threshold;
       3. every rank scans the (query, list) pairs of the lists it owns -> one record per query (exact local
          top-k + the bound of the rows it left out; engine.search);
       4. all_to_all(records): each home receives its queries' records from every rank;
-      5. the home merges and certifies (k-th merged score > every rank's bound; engine.merge);
-      6. all_gather(fail lists) [world][1 + fcap];
-      7. every rank runs the exact scan of the failures over its lists (engine.rerun);
+      5. the home merges and certifies (k-th merged score > every rank's bound; engine.merge); its fail list
+         keeps EVERY failing query (it is sized to the home's batch);
+      6. all_gather(the first fcap entries of every fail list) [world][1 + fcap];
+      7. every rank runs the exact scan of those failures over its lists (engine.rerun);
       8. all_to_all(re-run records) and the home merges them into its results (engine.merge_rerun).
 
-    Steps 6-8 always run (their buffers are small and fixed: fcap failures per home), so the step needs no
-    host synchronisation.  A home with more than fcap failures sets `overflow` (the device count exceeds
-    fcap); check_overflow() reads it (host sync) and step(..., validate=True) re-runs the excess.
-    All buffers are allocated once (torch tensors on `device`).
+    Steps 6-8 always run with fixed buffers, so a step with at most fcap failures per home needs no host
+    decision.  The failure counts of every home arrive with step 6 on every rank; the host reads them (an
+    event on that copy, while steps 7-8 run) and, when a home has more than fcap, every rank runs the same
+    further rounds: one all_gather of the whole fail lists, then per round of fcap entries steps 7-8 again.
+    So every failing query is re-run exactly, whatever the data.  `stats` holds the last
+    step's largest failure count and its extra rounds.  All buffers are allocated once (torch tensors on
+    `device`); the step is a generator of collectives (_ops), which __call__ runs over `comm` and
+    LocalShardGroup runs for W ranks in one process.
     """
 
     def __init__(self, engine, comm, nq_local: int, k: int, width: int, rank: int, world: int, device=None,
@@ -377,20 +396,30 @@ class ListShardedIvf:
         import torch
 
         self.engine, self.comm = engine, comm
-        self.nq, self.k, self.width, self.rank, self.world, self.fcap = nq_local, k, width, rank, world, fcap
+        self.nq, self.k, self.width, self.rank, self.world = nq_local, k, width, rank, world
+        self.fcap = max(1, min(int(fcap), nq_local)) if nq_local > 0 else max(1, int(fcap))
+        fcap = self.fcap
+        self.budget = bool(getattr(engine, "budget", False))
+        S = shard_plan_stride(width, self.budget)
         rb = 16 * (k + 1)
         Q = nq_local * world
-        self.plan_home = torch.empty((nq_local, width + 1), dtype=torch.int32, device=device)
-        self.plan_all = torch.empty((Q, width + 1), dtype=torch.int32, device=device)
+        self.plan_home = torch.empty((nq_local, S), dtype=torch.int32, device=device)
+        self.plan_all = torch.empty((Q, S), dtype=torch.int32, device=device)
         self.rec = torch.empty((Q, rb), dtype=torch.uint8, device=device)
         self.rec_home = torch.empty((world, nq_local, rb), dtype=torch.uint8, device=device)
-        self.fail_home = torch.zeros((1 + fcap,), dtype=torch.int32, device=device)
+        self.fail_home = torch.zeros((1 + nq_local,), dtype=torch.int32, device=device)
         self.fail_all = torch.zeros((world, 1 + fcap), dtype=torch.int32, device=device)
+        self.fail_full = None  # [world][1 + nq_local], allocated by the first step that needs a second round
+        self.fail_round = torch.zeros((world, 1 + fcap), dtype=torch.int32, device=device)
         self.rrec = torch.zeros((world * fcap, rb), dtype=torch.uint8, device=device)
         self.rrec_home = torch.zeros((world, fcap, rb), dtype=torch.uint8, device=device)
         self.out_s = torch.empty((nq_local, k), dtype=torch.float32, device=device)
         self.out_l = torch.empty((nq_local, k), dtype=torch.int64, device=device)
-        self.max_fail = torch.zeros((1,), dtype=torch.int32, device=device)  # the most failures of one step
+        cuda = self.fail_all.is_cuda
+        self._counts = torch.zeros((world,), dtype=torch.int32, pin_memory=cuda)
+        self._counts_ev = torch.cuda.Event() if cuda else None
+        self.stats = {"max_failures": 0, "extra_rounds": 0}
+        self.max_fail = 0        # the most failures of one home in any step so far
         self.timing = False
         self.collective_ms = {}
 
@@ -403,7 +432,6 @@ class ListShardedIvf:
 
     # the device work between two collectives (each may be replayed from a hipGraph: capture())
     def _phase(self, name, q_all):
-        import torch
         g = getattr(self, "graphs", {}).get(name)
         if g is not None:
             g.replay()
@@ -421,14 +449,13 @@ class ListShardedIvf:
             e.rerun(q_all, self.plan_all, P, self.fail_all, nq, self.rrec)
         else:  # "finish"
             e.merge_rerun(self.rrec_home, self.fail_home, self.out_s, self.out_l)
-            torch.maximum(self.max_fail, self.fail_home[:1], out=self.max_fail)
 
     PHASES = ("prepare", "search", "merge", "rerun", "finish")
 
     def capture(self, q_all):
         """Capture the five device phases into hipGraphs (the collectives stay outside them), replayed by
         every later call on the same q_all buffer.  One plain step on the capture stream sizes its
-        workspaces first (no allocation inside a capture)."""
+        workspaces first (no allocation inside a capture).  Overflow rounds run uncaptured."""
         import torch
         gst = torch.cuda.Stream()
         gst.wait_stream(torch.cuda.current_stream())
@@ -444,26 +471,93 @@ class ListShardedIvf:
         torch.cuda.synchronize()
         self.graphs = graphs
 
-    def __call__(self, q_all, validate: bool = False):
-        nq, w = self.nq, self.world
-        c = self.comm
+    def _read_counts(self):
+        """Every home's failure count (fail_all[:, 0], the same on every rank) -> numpy; the device copy was
+        enqueued after the fail-list gather (_note_counts), so this waits for that point of the step only."""
+        if self._counts_ev is not None:
+            self._counts_ev.synchronize()
+        return self._counts.numpy().copy()
+
+    def _note_counts(self):
+        if self._counts_ev is not None:
+            self._counts.copy_(self.fail_all[:, 0], non_blocking=True)
+            self._counts_ev.record()
+        else:
+            self._counts.copy_(self.fail_all[:, 0])
+
+    def _ops(self, q_all):
+        """The step as a generator: device phases run inline; each collective is yielded as
+        (kind, out, in, name) with kind "gather" (all_gather_into) or "a2a" (equal-split all_to_all) for the
+        caller to perform before resuming."""
+        nq, w, fcap = self.nq, self.world, self.fcap
         self._phase("prepare", q_all)
-        self._timed("plan_allgather", lambda: c.all_gather_into(self.plan_all, self.plan_home))
+        yield ("gather", self.plan_all, self.plan_home, "plan_allgather")
         self._phase("search", q_all)
-        self._timed("record_alltoall", lambda: c.all_to_all_single(self.rec_home.view(w * nq, -1), self.rec))
+        yield ("a2a", self.rec_home.view(w * nq, -1), self.rec, "record_alltoall")
         self._phase("merge", q_all)
-        self._timed("fail_allgather", lambda: c.all_gather_into(self.fail_all, self.fail_home))
+        yield ("gather", self.fail_all, self.fail_home[:1 + fcap], "fail_allgather")
+        self._note_counts()
         self._phase("rerun", q_all)
-        self._timed("rerun_alltoall", lambda: c.all_to_all_single(self.rrec_home.view(w * self.fcap, -1), self.rrec))
+        yield ("a2a", self.rrec_home.view(w * fcap, -1), self.rrec, "rerun_alltoall")
         self._phase("finish", q_all)
-        if validate and self.check_overflow():
-            raise RuntimeError(f"more than {self.fcap} certificate failures at one home rank in a step: rerun with a "
-                               f"larger fcap")
+        counts = self._read_counts()
+        mx = int(counts.max()) if len(counts) else 0
+        extra = max(0, (mx - 1) // fcap) if mx > fcap else 0
+        self.stats = {"max_failures": mx, "extra_rounds": extra}
+        self.max_fail = max(self.max_fail, mx)
+        if extra == 0:
+            return
+        import torch
+        if self.fail_full is None:
+            self.fail_full = torch.zeros((w, 1 + nq), dtype=torch.int32, device=self.fail_home.device)
+        yield ("gather", self.fail_full, self.fail_home, "fail_full_allgather")
+        ct = torch.as_tensor(counts, dtype=torch.int32, device=self.fail_home.device)
+        for j in range(1, extra + 1):
+            off = j * fcap
+            # round j: entries [off, off + fcap) of every home's fail list, in the [1 + fcap] form
+            self.fail_round.zero_()
+            self.fail_round[:, 0] = torch.clamp(ct - off, 0, fcap)
+            m = min(fcap, nq - off)
+            if m > 0:
+                self.fail_round[:, 1:1 + m] = self.fail_full[:, 1 + off:1 + off + m]
+            self.engine.rerun(q_all, self.plan_all, self.width, self.fail_round, nq, self.rrec)
+            yield ("a2a", self.rrec_home.view(w * fcap, -1), self.rrec, "rerun_alltoall")
+            self.engine.merge_rerun(self.rrec_home, self.fail_round[self.rank], self.out_s, self.out_l)
+
+    def __call__(self, q_all):
+        c = self.comm
+        for kind, out, inp, name in self._ops(q_all):
+            if kind == "gather":
+                self._timed(name, lambda: c.all_gather_into(out, inp))
+            else:
+                self._timed(name, lambda: c.all_to_all_single(out, inp))
         return self.out_s, self.out_l
 
-    def check_overflow(self) -> bool:
-        """True if any step so far had more certificate failures at this home than fcap (host sync)."""
-        return int(self.max_fail.max().item()) > self.fcap
+
+class LocalShardGroup:
+    """W ranks of the list-sharded step driven from one process (tests, scripts/rank_shape.py): the steps'
+    generators (ListShardedIvf._ops) advance in lockstep and each collective is done as device copies
+    between the ranks' buffers -- the same orchestration bench.py runs over RCCL, collectives aside."""
+
+    def __init__(self, steps):
+        self.steps = list(steps)
+
+    def __call__(self, q_all):
+        W = len(self.steps)
+        gens = [s._ops(q_all) for s in self.steps]
+        while True:
+            ops = [next(g, None) for g in gens]
+            if all(o is None for o in ops):
+                break
+            if any(o is None for o in ops) or len({(o[0], o[3]) for o in ops}) != 1:
+                raise RuntimeError("list-sharded ranks diverged: " + repr([o and o[3] for o in ops]))
+            kind = ops[0][0]
+            for r, (_, out, _, _) in enumerate(ops):
+                ov = out.view(W, -1)
+                for s in range(W):
+                    src = ops[s][2]
+                    ov[s].copy_(src.reshape(-1) if kind == "gather" else src.reshape(W, -1)[r])
+        return [(s.out_s, s.out_l) for s in self.steps]
 
 
 def exchange_rows(comm, rank: int, world: int, chunks, centroids, metric, owner_of=None, device: int = 0,

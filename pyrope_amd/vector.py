@@ -268,7 +268,8 @@ class HipVectorIndex(IVectorIndex):
 
     def shard_prepare_device(self, d_q: int, nq: int, top_k: int, d_plan: int, stream: int = 0,
                              options: Optional[SearchOptions] = None) -> int:
-        """Home rank: coarse ranking + T_q -> plan [nq][P + 1] at d_plan; returns P."""
+        """Home rank: coarse ranking + T_q -> plan [nq][P + 1] at d_plan (with options.max_scans: [nq][2P + 1],
+        the MaxScans budget left at each probe after T_q; shard_plan_stride); returns P."""
         p = self._params(options)
         out = C.c_int32()
         check(self._L.pyr_index_shard_prepare_device(self._h, C.c_void_p(d_q), nq, int(top_k), C.byref(p),
@@ -276,17 +277,20 @@ class HipVectorIndex(IVectorIndex):
         return out.value
 
     def shard_search_device(self, d_q: int, nq: int, top_k: int, d_plan: int, width: int, d_records: int,
-                            stream: int = 0) -> None:
-        """Every rank: its owned lists against the gathered plans -> one record per query."""
+                            stream: int = 0, budgets: bool = False) -> None:
+        """Every rank: its owned lists against the gathered plans -> one record per query (budgets: the plans
+        carry MaxScans budgets)."""
         check(self._L.pyr_index_shard_search_device(self._h, C.c_void_p(d_q), nq, int(top_k), C.c_void_p(d_plan),
-                                                    int(width), C.c_void_p(d_records), C.c_void_p(stream or None)))
+                                                    int(width), int(bool(budgets)), C.c_void_p(d_records),
+                                                    C.c_void_p(stream or None)))
 
     def shard_rerun_device(self, d_q: int, nq: int, top_k: int, d_plan: int, width: int, d_fails: int, nranks: int,
-                           fcap: int, nq_home: int, d_records: int, stream: int = 0) -> None:
+                           fcap: int, nq_home: int, d_records: int, stream: int = 0, budgets: bool = False) -> None:
         """Every rank: exact answers to the gathered failures [nranks][1 + fcap] -> records [nranks * fcap]."""
         check(self._L.pyr_index_shard_rerun_device(self._h, C.c_void_p(d_q), nq, int(top_k), C.c_void_p(d_plan),
-                                                   int(width), C.c_void_p(d_fails), int(nranks), int(fcap),
-                                                   int(nq_home), C.c_void_p(d_records), C.c_void_p(stream or None)))
+                                                   int(width), int(bool(budgets)), C.c_void_p(d_fails), int(nranks),
+                                                   int(fcap), int(nq_home), C.c_void_p(d_records),
+                                                   C.c_void_p(stream or None)))
 
     def set_centroids(self, centroids: np.ndarray) -> None:
         """Supply the coarse quantizer used by the next build() (pyr_index_set_centroids)."""

@@ -106,7 +106,7 @@ class CpuEngine:
         world, n = ent.shape[0], ent.shape[1]
         fcap = fail.shape[0] - 1 if fail is not None else 0
         nfail = 0
-        for i in range(n if qsel is None else min(int(qsel[0]), qsel.shape[0] - 1)):
+        for i in range(n if qsel is None else min(int(qsel[0]), n)):  # (the device merge's cap = its records)
             q = i if qsel is None else int(qsel[1 + i])
             allc = [(float(e["score"]), int(e["list"]), int(e["label"])) for s in range(world)
                     for e in ent[s, i][:int(tr[s, i]["n"])]]
@@ -196,8 +196,12 @@ def _worker(rank, world, port, data, cents, queries, thr, out, fcap):
         np.save(os.path.join(out, f"glen{rank}.npy"), glen)
         np.save(os.path.join(out, f"srows{rank}.npy"), srows)
         np.save(os.path.join(out, f"scounts{rank}.npy"), scounts)
-        np.save(os.path.join(out, f"meta{rank}.npy"), np.array([eng.reruns, int(step.check_overflow())]))
-        assert set(step.collective_ms) == {"plan_allgather", "record_alltoall", "fail_allgather", "rerun_alltoall"}
+        np.save(os.path.join(out, f"meta{rank}.npy"), np.array([eng.reruns, step.stats["extra_rounds"],
+                                                                step.max_fail]))
+        names = {"plan_allgather", "record_alltoall", "fail_allgather", "rerun_alltoall"}
+        if step.stats["extra_rounds"]:
+            names.add("fail_full_allgather")
+        assert set(step.collective_ms) == names
     finally:
         dist.destroy_process_group()
 
@@ -219,8 +223,10 @@ def _unsharded(oracle, data, cents, queries):
     return S, L, assign, order, off
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_list_sharded_step_equals_unsharded(oracle, tmp_path, world):
+@pytest.mark.parametrize("world,fcap", [(2, 8), (3, 8), (2, 1), (3, 2)])
+def test_list_sharded_step_equals_unsharded(oracle, tmp_path, world, fcap):
+    """fcap 8 holds every home's failures in the fixed re-run round; fcap 1 / 2 is smaller than a home's
+    failure count (NQ / 3 = 4), so the step runs further rounds -- every failure must still come back exact."""
     import torch.multiprocessing as mp
 
     from pyrope_amd.dist import SAMPLE_ROWS, list_owners
@@ -234,7 +240,7 @@ def test_list_sharded_step_equals_unsharded(oracle, tmp_path, world):
         s40, _ = oracle.ivf_search(q, 40, cents, lrows, off, metric=oracle.L2, nprobe=NPROBE)
         thr[i] = [s40[29], s40[3], -np.inf][i % 3]
     port = _free_port()
-    mp.start_processes(_worker, args=(world, port, data, cents, queries, thr, str(tmp_path), 8), nprocs=world,
+    mp.start_processes(_worker, args=(world, port, data, cents, queries, thr, str(tmp_path), fcap), nprocs=world,
                        join=True, start_method="spawn")
     glen = np.bincount(assign, minlength=len(cents))
     owner = list_owners(glen, world)
@@ -257,7 +263,9 @@ def test_list_sharded_step_equals_unsharded(oracle, tmp_path, world):
         assert np.array_equal(s.view(np.uint32), ref_s[r * NQ:(r + 1) * NQ].view(np.uint32))
         meta = np.load(tmp_path / f"meta{r}.npy")
         reruns += int(meta[0])
-        assert meta[1] == 0  # no home exceeded fcap
+        nf = NQ // 3  # the forced failures per home
+        assert meta[2] == nf
+        assert meta[1] == (nf - 1) // fcap  # rounds past the fixed one
     # every forced failure (a third of the queries) was re-run exactly, on every rank, in both steps
     assert reruns == 2 * world * (NQ * world // 3)
 
