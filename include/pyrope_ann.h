@@ -62,8 +62,21 @@ typedef struct {
   int32_t nlist;          /* IVF: NList (registry default 100, VectorIndexRegistry.cs:100,106) */
   int32_t pq_m;           /* IVF_PQ: M, dim % M == 0 (ProductQuantizer.cs:18) */
   int32_t pq_k;           /* IVF_PQ: K <= 256 (ProductQuantizer.cs:19) */
-  int32_t device;         /* HIP device ordinal (one process per GPU) */
+  int32_t device;         /* HIP device ordinal when device_mask is 0 */
   int32_t default_nprobe; /* <= 0 -> reference default: 3 IVF_FLAT (IvfFlatVectorIndex.cs:14), 1 IVF_PQ (IvfPqVectorIndex.cs:125) */
+  /* Multi-GPU (SURVEY.md 8(b) device_mask; 8(e)(i) lists sharded whole; DESIGN.md §5 "One process, several
+   * GPUs").  device_mask: bit d = HIP device d (0 -> `device` alone).  One bit and shards = 0: an ordinary
+   * single-GPU index on that device.  More bits, or shards >= 1 (IVF_FLAT only): ONE index whose lists are
+   * dealt whole to `shards` shard indexes (0 -> one per device of the mask; shard r on the (r mod n)-th device
+   * of the mask), searched by the list-sharded step inside the library with RCCL collectives between the
+   * devices (device copies when two shards share a device).  Every IVectorIndex call works on it: writes and
+   * Build go to a single-GPU index on the first device that holds every row (the reference Build, bit for
+   * bit), which then deals its lists to the shards; pyr_index_search* answers by the list-sharded step
+   * (L2 / IP, k <= 60, empty buffer) or else on that first-device index.  Results equal the single-GPU
+   * index's, ids and score bits. */
+  uint64_t device_mask;
+  int32_t shards;
+  int32_t reserved;
 } pyr_index_desc;
 
 /* SearchOptions (SearchOptions.cs:3) */
@@ -248,6 +261,13 @@ pyr_status pyr_merge_topk_parts_device(const float *d_scores, const int64_t *d_l
  * carries, per probe, what is left of it when that list is reached; the owning rank scans the list up to
  * that many live rows.  A rank refuses a budgeted search (PYR_E_STATE) once one of its lists lost rows since
  * its samples were set. */
+
+/* The multi-GPU index (pyr_index_desc.device_mask / shards): its shard count (1 for a single-GPU index), the
+ * transport of its list-sharded step (0 none yet, 1 device copies, 2 RCCL), the searches the step answered and
+ * those the first-device index answered alone (Cosine, k > 60, a non-empty buffer), and the last step's largest
+ * certificate-failure count at one home with its re-run rounds past the first.  Any output may be NULL. */
+pyr_status pyr_index_shard_info(const pyr_index *index, int32_t *shards, int32_t *xport, int64_t *sharded_searches,
+                                int64_t *staged_searches, int64_t *last_max_failures, int64_t *last_extra_rounds);
 
 /* KMeansUtils.FindNearestCentroid (KMeansUtils.cs:70-93; the assignment of IvfFlatVectorIndex.Build,
  * :128-132) of n host rows against nlist host centroids: assign[i] = the list row i belongs to (ties ->

@@ -63,7 +63,8 @@ class IOException(OSError):
 
 class IndexDesc(C.Structure):
     _fields_ = [("kind", C.c_int32), ("dim", C.c_int32), ("metric", C.c_int32), ("nlist", C.c_int32),
-                ("pq_m", C.c_int32), ("pq_k", C.c_int32), ("device", C.c_int32), ("default_nprobe", C.c_int32)]
+                ("pq_m", C.c_int32), ("pq_k", C.c_int32), ("device", C.c_int32), ("default_nprobe", C.c_int32),
+                ("device_mask", C.c_uint64), ("shards", C.c_int32), ("reserved", C.c_int32)]
 
 
 class SearchParams(C.Structure):
@@ -124,6 +125,7 @@ SIGNATURES = {
     "pyr_index_shard_prepare_device": (C.c_int, [_vp, _vp, C.c_int64, C.c_int32, C.POINTER(SearchParams), _vp,
                                                  C.POINTER(C.c_int32), _vp]),
     "pyr_shard_plan_stride": (C.c_int32, [C.c_int32, C.c_int64]),
+    "pyr_index_shard_info": (C.c_int, [_vp, _i32, _i32, _i64, _i64, _i64, _i64]),
     "pyr_index_shard_search_device": (C.c_int, [_vp, _vp, C.c_int64, C.c_int32, _vp, C.c_int32, C.c_int32, _vp,
                                                 _vp]),
     "pyr_index_shard_rerun_device": (C.c_int, [_vp, _vp, C.c_int64, C.c_int32, _vp, C.c_int32, C.c_int32, _vp,

@@ -11,7 +11,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libpyrope_hip.so")
-SOURCES = ["kernels.hip", "sort.hip", "filter.hip", "tiles16.hip", "sample16.hip", "scan.hip", "pq32.hip", "sq8.hip", "coarse.hip", "shard.hip", "engine.cpp", "persist.cpp", "capi.cpp"]
+SOURCES = ["kernels.hip", "sort.hip", "filter.hip", "tiles16.hip", "sample16.hip", "scan.hip", "pq32.hip", "sq8.hip", "coarse.hip", "shard.hip", "engine.cpp", "multi.cpp", "persist.cpp", "capi.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 # -ffp-contract=off: the parity contract (bit-identical scores) forbids FMA contraction.
@@ -89,7 +89,7 @@ def _build_locked(verbose: bool) -> str:
     if failed:
         raise RuntimeError("libpyrope_hip build failed")
     tmp = OUT + f".{os.getpid()}.tmp"
-    link = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp] + objs
+    link = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp] + objs + ["-ldl"]
     try:
         subprocess.run(link, check=True)
         os.replace(tmp, OUT)  # atomic: a concurrent loader sees the old or the new library

@@ -109,10 +109,21 @@ pyr_status pyr_index_create(const pyr_index_desc *desc, pyr_index **out) {
   if (!desc || !out) return fail(PYR_E_ARG, "null argument");
   *out = nullptr;
   return guard([&] {
-    check_device(desc->device);
+    pyr_index_desc d = *desc;
+    if (d.shards < 0) throw pyr::Error(PYR_E_ARG, "shards must be >= 0");
+    if (d.device_mask != 0) {
+      for (int b = 0; b < 64; ++b)
+        if (d.device_mask >> b & 1) check_device(b);
+      d.device = __builtin_ctzll(d.device_mask);  // the first device: the multi-GPU index's stage
+      if (__builtin_popcountll(d.device_mask) == 1 && d.shards == 0) d.device_mask = 0;  // one GPU: the plain index
+    } else {
+      check_device(d.device);
+      if (d.shards > 0) d.device_mask = 1ull << d.device;
+    }
+    if (d.device_mask == 0) d.shards = 0;
     auto *h = new pyr_index;
     try {
-      h->impl.reset(pyr::create_index(*desc));
+      h->impl.reset(pyr::create_index(d));
     } catch (...) {
       delete h;
       throw;
@@ -660,6 +671,22 @@ pyr_status pyr_merge_topk_parts_device(const float *d_scores, const int64_t *d_l
     pyr::launch_merge_labels(d_scores, d_labels, nq, nparts, k, d_out_scores, d_out_labels,
                              reinterpret_cast<hipStream_t>(stream), part_major != 0);
     HIPCHK(hipGetLastError());
+  });
+}
+
+pyr_status pyr_index_shard_info(const pyr_index *index, int32_t *shards, int32_t *xport, int64_t *sharded_searches,
+                                int64_t *staged_searches, int64_t *last_max_failures, int64_t *last_extra_rounds) {
+  if (!index) return fail(PYR_E_ARG, "null argument");
+  return guard([&] {
+    int32_t a = 0, b = 0;
+    int64_t c = 0, d = 0, e = 0, f = 0;
+    index->impl->shard_info(&a, &b, &c, &d, &e, &f);
+    if (shards) *shards = a;
+    if (xport) *xport = b;
+    if (sharded_searches) *sharded_searches = c;
+    if (staged_searches) *staged_searches = d;
+    if (last_max_failures) *last_max_failures = e;
+    if (last_extra_rounds) *last_extra_rounds = f;
   });
 }
 

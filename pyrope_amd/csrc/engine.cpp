@@ -2944,6 +2944,55 @@ struct IvfFlatIndex : Index {
                                  "again with the new lengths)");
   }
 
+  // ---- the multi-device index's hooks (multi.cpp; engine.h "the multi-device index") ----
+  bool ms_lists(MsLists &out) const override {
+    if (!built || coarse.nlist <= 0) return false;
+    out.nlist = coarse.nlist;
+    out.nprobe_default = nprobe_default;
+    out.lb = lb;
+    out.llen = llen;
+    out.llive = llive;
+    out.state = lstate;
+    out.cents.resize((size_t)coarse.nlist * dim);
+    int32_t nl = 0;
+    centroids(out.cents.data(), &nl);
+    return true;
+  }
+  void ms_gather_rows(const int64_t *d_pos, int64_t n, float *d_out, hipStream_t st) const override {
+    if (n > 0) launch_gather_blocked(lists.rows.as<float>(), d_pos, n, dim, d_out, st);
+  }
+  void ms_commit(const float *d_x, int64_t n, const std::vector<int32_t> &asg, const std::vector<int64_t> &labs,
+                 const float *c, int k) override {
+    DevMem C;
+    C.ensure(sizeof(float) * (size_t)k * dim);
+    HIPCHK(hipMemcpyAsync(C.p, c, sizeof(float) * (size_t)k * dim, hipMemcpyHostToDevice, wst));
+    commit_lists(d_x, n, asg, labs, C.as<float>(), k);
+    buf.clear(wst);
+    built = true;
+    HIPCHK(hipStreamSynchronize(wst));
+  }
+  void ms_set_list_lengths(const int64_t *glen, int nl) override {
+    if (!ssamp || nl != coarse.nlist) throw Error(PYR_E_STATE, "no list samples (pyr_index_set_list_samples)");
+    std::vector<int32_t> g(nl);
+    for (int l = 0; l < nl; ++l) g[l] = (int32_t)glen[l];
+    HIPCHK(hipMemcpyAsync(sgle.p, g.data(), sizeof(int32_t) * nl, hipMemcpyHostToDevice, wst));
+    HIPCHK(hipStreamSynchronize(wst));
+    sglen.assign(glen, glen + nl);
+  }
+  int64_t ms_position(int64_t label) const override {
+    auto f = pos_of.find(label);
+    return f == pos_of.end() ? -1 : f->second;
+  }
+  bool ms_shardable(int k, const pyr_search_params &prm, int *P) const override {
+    if (!built || coarse.nlist <= 0 || metric == COS || buf.live_count() > 0 || !filter_enabled()) return false;
+    const int k1 = filter_k1(k);
+    if (k <= 0 || k > KMAX_FAST || k1 <= 0 || !stream_ok(k1)) return false;
+    const int nprobe = prm.nprobe < 0 ? nprobe_default : prm.nprobe;
+    *P = std::max(0, std::min(nprobe, coarse.nlist));
+    return *P > 0 && *P < MAX_PARTS;
+  }
+  const int64_t *ms_position_labels() const override { return lists.labels.as<int64_t>(); }
+
   int shard_prepare(const float *d_q, int64_t nq, int k, const pyr_search_params &prm, int32_t *d_plan,
                     Workspace &ws) override {
     if (!ssamp) throw Error(PYR_E_STATE, "no list samples (pyr_index_set_list_samples)");
@@ -4040,6 +4089,7 @@ struct IvfPqIndex : Index {
 Index *create_index(const pyr_index_desc &d) {
   if (d.dim <= 0) throw Error(PYR_E_ARG, "Dimension must be positive.");  // BruteForceVectorIndex.cs:43-46
   if (d.metric < 0 || d.metric > 2) throw Error(PYR_E_ARG, "unknown metric");
+  if (d.device_mask != 0) return create_multi_index(d);  // (pyr_index_create clears a one-GPU mask)
   switch (d.kind) {
     case PYR_FLAT: return new FlatIndex(d);
     case PYR_IVF_FLAT: return new IvfFlatIndex(d);

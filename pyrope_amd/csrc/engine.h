@@ -319,6 +319,57 @@ struct Index {
     (void)d_rec, (void)ws;
     throw Error(PYR_E_STATE, "index kind has no list-sharded search (IVF_FLAT only)");
   }
+  // ---- the multi-device index (multi.cpp; pyr_index_desc.device_mask / shards): a single-device IVF_FLAT index
+  // (the "stage", on the first device) holds every row and builds exactly as the unsharded index does; its lists
+  // are then dealt whole to the shard indexes, whose row labels are the stage's storage positions ----
+  struct MsLists {
+    int nlist = 0, nprobe_default = 0;
+    std::vector<int32_t> lb, llen, llive;  // per list: first storage position, rows (incl. tombstones), live rows
+    std::vector<uint8_t> state;            // per storage position: 1 visible, 0 removed / padding, 2 shadowed
+    std::vector<float> cents;              // nlist x dim
+  };
+  virtual bool ms_lists(MsLists &out) const {  // false: not a built IVF_FLAT index
+    (void)out;
+    return false;
+  }
+  // row-major fp32 rows at the given list storage positions (device, this index's device), on st
+  virtual void ms_gather_rows(const int64_t *d_pos, int64_t n, float *d_out, hipStream_t st) const {
+    (void)d_pos, (void)n, (void)d_out, (void)st;
+    throw Error(PYR_E_STATE, "index kind has no lists");
+  }
+  // a shard: lists of exactly these rows (device, row-major; row i in list asg[i], label labs[i]) in this order,
+  // quantizer c (host, k x dim), replacing whatever the index held
+  virtual void ms_commit(const float *d_x, int64_t n, const std::vector<int32_t> &asg, const std::vector<int64_t> &labs,
+                         const float *c, int k) {
+    (void)d_x, (void)n, (void)asg, (void)labs, (void)c, (void)k;
+    throw Error(PYR_E_STATE, "index kind has no lists");
+  }
+  // every list's live rows over all shards (the MaxScans accounting of the list-sharded step), after a Delete
+  virtual void ms_set_list_lengths(const int64_t *glen, int nl) {
+    (void)glen, (void)nl;
+    throw Error(PYR_E_STATE, "index kind has no list-sharded search");
+  }
+  virtual int64_t ms_position(int64_t label) const {  // the list storage position of a label (-1: none)
+    (void)label;
+    return -1;
+  }
+  // the list-sharded step answers this search (built, empty buffer, L2 / IP, k within the stream scan's refine);
+  // else the stage searches alone; *P = the probe width
+  virtual bool ms_shardable(int k, const pyr_search_params &p, int *P) const {
+    (void)k, (void)p, (void)P;
+    return false;
+  }
+  virtual const int64_t *ms_position_labels() const { return nullptr; }  // device: storage position -> label
+  // pyr_index_shard_info: shards (1: a single-GPU index), transport (0 none, 1 device copies, 2 RCCL; set by the
+  // first list-sharded search), searches answered by the list-sharded step / by the stage alone, and the last
+  // step's largest failure count per home and its re-run rounds past the first
+  virtual void shard_info(int32_t *shards, int32_t *xport, int64_t *sharded, int64_t *staged, int64_t *max_fail,
+                          int64_t *rounds) const {
+    *shards = 1;
+    *xport = 0;
+    *sharded = *staged = *max_fail = *rounds = 0;
+  }
+
   // capacity hint: room for `rows` more rows without re-allocation (bulk loads of 10^7-10^8 rows,
   // where a grow-by-copy would need the old and the new store at once)
   virtual void reserve(int64_t rows) { (void)rows; }
@@ -362,6 +413,9 @@ struct NetRandom {  // System.Random legacy (Net5CompatSeedImpl); SURVEY.md Appe
 };
 
 Index *create_index(const pyr_index_desc &d);
+// a device mask left by pyr_index_create (several devices, or shards >= 1): the list-sharded index (multi.cpp)
+Index *create_multi_index(const pyr_index_desc &d);
+bool filter_k1_ok(int k);  // the stream scan's refine takes this k (k <= 60)
 
 // kernel-phase profiler (pyr_profile_*): HIP events around each phase on the search stream
 enum Phase { PH_COARSE = 0, PH_ITEMS = 1, PH_LIST_SCAN = 2, PH_BUF_SCAN = 3, PH_MERGE = 4, PH_FLAT_SCAN = 5,

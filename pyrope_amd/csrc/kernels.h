@@ -482,6 +482,10 @@ void launch_unpack_plan(const int32_t *plan, int64_t nq, int P, int stride, int3
 // in the replicated sample store (slb / sle: its lists' sample rows; a sample holds no tombstones)
 void launch_shard_budget(const int32_t *probes, int64_t nq, int P, int64_t max_scans, const int32_t *glive,
                          const int32_t *slb, const int32_t *sle, int32_t *rem, uint32_t *slimits, hipStream_t st);
+// l[i] = table[l[i]] where l[i] >= 0 (the multi-device index: shard labels are stage storage positions)
+void launch_map_positions(int64_t *l, int64_t n, const int64_t *table, hipStream_t st);
+// out [W][1 + fcap] = entries [off, off + fcap) of every home's whole fail list full [W][stride] (the count first)
+void launch_fail_round(const int32_t *full, int W, int64_t stride, int off, int fcap, int32_t *out, hipStream_t st);
 // gathered fail lists [nranks][1 + fcap] -> global failing queries fail[], their record slots pos[], *nfail
 void launch_shard_fail_compact(const int32_t *fails, int nranks, int fcap, int64_t nq_home, int32_t *fail, int32_t *pos,
                                int32_t *nfail, hipStream_t st);

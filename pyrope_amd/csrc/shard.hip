@@ -187,7 +187,34 @@ __global__ __launch_bounds__(256) void shard_fail_compact_kernel(const int32_t *
   }
 }
 
+// the multi-device index's shards label their rows by the stage's storage positions: back to the caller's
+// labels (table: the stage's per-position labels; -1 stays -1)
+__global__ void map_positions_kernel(int64_t *l, int64_t n, const int64_t *table) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && l[i] >= 0) l[i] = table[l[i]];
+}
+
+// round j of the failures past fcap: entries [off, off + fcap) of every home's whole fail list
+// (full [W][stride], stride = 1 + the home's batch) in the re-run's [W][1 + fcap] form
+__global__ void fail_round_kernel(const int32_t *full, int W, int64_t stride, int off, int fcap, int32_t *out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)W * (1 + fcap)) return;
+  const int s = (int)(e / (1 + fcap)), j = (int)(e - (int64_t)s * (1 + fcap));
+  const int c = min(max(full[(size_t)s * stride] - off, 0), fcap);
+  out[e] = j == 0 ? c : (j <= c ? full[(size_t)s * stride + off + j] : 0);
+}
+
 }  // namespace
+
+void launch_map_positions(int64_t *l, int64_t n, const int64_t *table, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(map_positions_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, l, n, table);
+}
+void launch_fail_round(const int32_t *full, int W, int64_t stride, int off, int fcap, int32_t *out, hipStream_t st) {
+  const int64_t n = (int64_t)W * (1 + fcap);
+  if (n <= 0) return;
+  hipLaunchKernelGGL(fail_round_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, full, W, stride, off, fcap, out);
+}
 
 void launch_pack_plan(const int32_t *probes, const float *thr, const int32_t *rem, int64_t nq, int P, int32_t *plan,
                       hipStream_t st) {

@@ -101,13 +101,15 @@ class HipVectorIndex(IVectorIndex):
     KIND = _lib.PYR_FLAT
 
     def __init__(self, dimension: int, metric: VectorMetric, *, nlist: int = 100, m: int = 4, k: int = 256,
-                 device: int = 0, default_nprobe: int = 0):
+                 device: int = 0, default_nprobe: int = 0, device_mask: int = 0, shards: int = 0):
+        """device_mask / shards: the multi-GPU index (IVF_FLAT; pyr_index_desc in include/pyrope_ann.h)."""
         if dimension <= 0:
             raise ArgumentOutOfRangeException("Dimension must be positive.")
         self.dimension = int(dimension)
         self.metric = VectorMetric(metric)
         self._L = _lib.load()
-        desc = _lib.IndexDesc(self.KIND, self.dimension, int(self.metric), nlist, m, k, device, default_nprobe)
+        desc = _lib.IndexDesc(self.KIND, self.dimension, int(self.metric), nlist, m, k, device, default_nprobe,
+                              int(device_mask), int(shards), 0)
         h = C.c_void_p()
         check(self._L.pyr_index_create(C.byref(desc), C.byref(h)))
         self._h = h
@@ -291,6 +293,15 @@ class HipVectorIndex(IVectorIndex):
                                                    int(width), int(bool(budgets)), C.c_void_p(d_fails), int(nranks),
                                                    int(fcap), int(nq_home), C.c_void_p(d_records),
                                                    C.c_void_p(stream or None)))
+
+    def shard_info(self) -> dict:
+        """The multi-GPU index's shards and its list-sharded step's counters (pyr_index_shard_info)."""
+        a, b = C.c_int32(), C.c_int32()
+        c, d, e, f = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64()
+        check(self._L.pyr_index_shard_info(self._h, C.byref(a), C.byref(b), C.byref(c), C.byref(d), C.byref(e),
+                                           C.byref(f)))
+        return {"shards": a.value, "xport": {0: None, 1: "copy", 2: "rccl"}[b.value], "sharded_searches": c.value,
+                "staged_searches": d.value, "last_max_failures": e.value, "last_extra_rounds": f.value}
 
     def set_centroids(self, centroids: np.ndarray) -> None:
         """Supply the coarse quantizer used by the next build() (pyr_index_set_centroids)."""

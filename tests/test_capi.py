@@ -121,3 +121,28 @@ def test_image_nonce_reads_the_nonce_section(hiplib, tmp_path):
     assert hiplib.pyr_image_nonce(str(tmp_path / "missing").encode(), out) == _lib.PYR_E_NOT_FOUND
     open(p, "wb").write(b"not an image")
     assert hiplib.pyr_image_nonce(p.encode(), out) == _lib.PYR_E_FORMAT
+
+
+def test_struct_layouts_match_the_header(tmp_path):
+    """pyr_index_desc / pyr_search_params as a C compiler lays them out (the C# shim's StructLayout.Sequential
+    mirrors them) equal the ctypes binding's: size and every field offset."""
+    import subprocess
+
+    from pyrope_amd import _lib
+    fields = {"pyr_index_desc": _lib.IndexDesc, "pyr_search_params": _lib.SearchParams}
+    body = []
+    for cname, ct in fields.items():
+        body.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
+        for f, _ in ct._fields_:
+            body.append(f'printf("{cname}.{f} %zu\\n", offsetof({cname}, {f}));')
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "pyrope_ann.h"\nint main(void) {\n' +
+                   "\n".join(body) + "\nreturn 0;\n}\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c99", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(line.split() for line in subprocess.run([str(exe)], check=True, capture_output=True,
+                                                       text=True).stdout.splitlines())
+    for cname, ct in fields.items():
+        assert int(got[cname]) == C.sizeof(ct), cname
+        for f, _ in ct._fields_:
+            assert int(got[f"{cname}.{f}"]) == getattr(ct, f).offset, (cname, f)
