@@ -417,7 +417,8 @@ def run(args):
         if ph == 8:
             fallback_queries = work.value
     scan = phases.get("list_scan", {"ms": float("nan"), "pairs": 0})
-    filt = os.environ.get("PYR_FILTER", "1") != "0"
+    # (the library honours PYR_FILTER only with PYR_DEV_KNOBS=1, kernels.h knob())
+    filt = not (os.environ.get("PYR_DEV_KNOBS") == "1" and os.environ.get("PYR_FILTER", "1") == "0")
     # MFMA filter (default): the (query, row) GEMM, 2*D flops per pair; exact VALU scan
     # (PYR_FILTER=0): sub, mul, add per element, 3*D
     flops = scan["pairs"] * (2 if filt else 3) * D

@@ -581,7 +581,7 @@ void launch_coarse_dense(const float *q, const float *cents_rm, const float *qn,
     hipLaunchKernelGGL(coarse_scores_kernel<COS>, grid, dim3(256), 0, st, q, cents_rm, qn, cn, nq, nlist, dim,
                        scores);
   // register lists for nprobe <= 64 (PYR_COARSE_SELECT=0: the LDS argmax rounds, measurement knob)
-  const bool reg = !getenv("PYR_COARSE_SELECT") || atoi(getenv("PYR_COARSE_SELECT")) != 0;
+  const bool reg = !knob("PYR_COARSE_SELECT") || atoi(knob("PYR_COARSE_SELECT")) != 0;
   const dim3 g4((unsigned)((nq + 3) / 4));
   // a lane sees every 64th centroid, so its list never needs more than ceil(nlist / 64) entries: the
   // wave's P pops then still find every key (nlist = 1,024: 16-entry lists for nprobe = 32)
@@ -631,7 +631,7 @@ void launch_coarse_mfma(const float *q, const float *cents_rm, const float *c2, 
   const dim3 ga((unsigned)((nlist + 31) / 32), (unsigned)((nq + 31) / 32));
   const dim3 g4((unsigned)((nq + 3) / 4));
   // PYR_COARSE_APPROX=0: the one-wave-per-tile kernel (A/B; the same approximate scores)
-  const char *ae = getenv("PYR_COARSE_APPROX");
+  const char *ae = knob("PYR_COARSE_APPROX");
   const bool lds = !(ae && atoi(ae) == 0);
   const dim3 gl((unsigned)((nlist + 63) / 64), (unsigned)((nq + 63) / 64));
   auto go = [&](auto met, auto dt) {

@@ -23,7 +23,7 @@ namespace pyr {
 // diagnostics only (PYR_DEBUG_ALLOC=<file>): every device allocation and free of the library appended to
 // the file, so that the address of a GPU memory fault can be matched to the buffer it falls in
 static void alloc_log(const char *what, const void *p, size_t n) {
-  static const char *path = getenv("PYR_DEBUG_ALLOC");
+  static const char *path = knob("PYR_DEBUG_ALLOC");
   if (!path || !*path) return;
   static std::mutex mu;
   std::lock_guard<std::mutex> g(mu);
@@ -228,7 +228,7 @@ PinnedRing::~PinnedRing() {
 
 // measurement only (PYR_WRITE_PROF=1): host time of the write path's sections, printed at exit
 struct WriteProf {
-  bool on = getenv("PYR_WRITE_PROF") != nullptr;
+  bool on = knob("PYR_WRITE_PROF") != nullptr;
   double t[8] = {};
   int64_t n = 0;
   ~WriteProf() {
@@ -259,7 +259,7 @@ void note_write_call() {
 
 // rows a write may take through the small-batch path (RowStore::write)
 static int64_t small_write_rows() {
-  const char *e = getenv("PYR_SMALL_WRITE");  // 0: the bulk path always (A/B)
+  const char *e = knob("PYR_SMALL_WRITE");  // 0: the bulk path always (A/B)
   return e ? atoll(e) : 64;
 }
 
@@ -643,7 +643,7 @@ static void flat_scan(const RowStore &rs, int64_t nrows, const ScanPlan &p, cons
 // Per-query shared top-k bound of one search (ScanArgs::gthr), reset to -inf.
 // PYR_GTHR=0 disables it (A/B measurement); results are identical either way.
 static bool bounds_enabled() {
-  const char *e = getenv("PYR_GTHR");
+  const char *e = knob("PYR_GTHR");
   return !(e && atoi(e) == 0);
 }
 static uint32_t *shared_bounds(Workspace &ws, int64_t nq) {
@@ -694,7 +694,7 @@ static void flush_stream_counters(Workspace &ws) {
 // the device re-run's per-query unit counters (IvfRerunArgs::done): zeroed once when allocated, then left
 // zero by every launch (each merge resets its query's)
 static int32_t *rerun_done(Workspace &ws, int64_t max_fail) {
-  const bool off = getenv("PYR_RERUN_FUSED") && atoi(getenv("PYR_RERUN_FUSED")) == 0;  // A/B: separate merge
+  const bool off = knob("PYR_RERUN_FUSED") && atoi(knob("PYR_RERUN_FUSED")) == 0;  // A/B: separate merge
   if (off) return nullptr;
   const size_t need = sizeof(int32_t) * (size_t)std::max<int64_t>(max_fail, 1);
   if (ws.rrdone.n < need) {
@@ -713,7 +713,7 @@ struct DeferredCounters {  // a deferred fill never outlives the search that set
 // IVF-PQ LUT list scan kernel: 2 = pq_adc4 (default), 0 = the first-cut pq_scan (PYR_PQ_ADC=0; A/B
 // only, same results; also what k > 64 or an unsupported shape takes)
 static int pq_adc_mode() {
-  const char *e = getenv("PYR_PQ_ADC");
+  const char *e = knob("PYR_PQ_ADC");
   return e ? atoi(e) : 2;
 }
 
@@ -723,7 +723,7 @@ static int pq_adc_mode() {
 // exact scans, PYR_FILTER_MARGIN sets the minimum K1 - k (default 4, see filter_k1).
 // ---------------------------------------------------------------------------
 static bool filter_enabled() {
-  const char *e = getenv("PYR_FILTER");
+  const char *e = knob("PYR_FILTER");
   return !(e && atoi(e) == 0);
 }
 // fp16 tiles are kept where the stream scan can use them (L2 / IP, tile dims up to 768)
@@ -741,9 +741,9 @@ static int store16_dt(int dim) { return scan_tile_dim(dim); }
 // tile each, 32x32x16 MFMAs, every query group of the item) after sprep's operands; PYR_SAMPLE16=1 keeps
 // sample16_kernel (A/B: both write the same samp layout; T_q may differ in its last bits, the answers do not).
 static void stream_sample(const StreamArgs &sa, int met, int maxi, hipStream_t st, bool prep_only = false) {
-  const char *e = getenv("PYR_SCAN_SAMPLE");
+  const char *e = knob("PYR_SCAN_SAMPLE");
   const int dt = sa.dt > 0 ? sa.dt : sa.dim;
-  const bool s16 = getenv("PYR_SAMPLE16") && atoi(getenv("PYR_SAMPLE16")) == 1;
+  const bool s16 = knob("PYR_SAMPLE16") && atoi(knob("PYR_SAMPLE16")) == 1;
   if (!(e && atoi(e) == 1) && dt == sa.dim && sample16_supported(sa.dim, met)) {
     if (s16 || !scan_sample_mode_supported(dt)) {
       launch_sample16(sa, met, maxi, st, prep_only);
@@ -767,13 +767,13 @@ static void stream_sample(const StreamArgs &sa, int met, int maxi, hipStream_t s
 // queries (+0.16 ms), R = 4 51 (+0.55 ms) (profiles/r4_scan/sweep_sample_rank*.log).  PYR_STREAM_RANK
 // fixes R.
 static void stream_rank(int k1, int32_t &rmin, int32_t &rmax, double &et) {
-  if (const char *e = getenv("PYR_STREAM_RANK")) {
+  if (const char *e = knob("PYR_STREAM_RANK")) {
     rmin = rmax = std::max(1, atoi(e));
     et = 0.0;
     return;
   }
   // PYR_STREAM_RMIN / PYR_STREAM_ET (measurement only): the floor of R and the emitted-row target per K1
-  const char *rm = getenv("PYR_STREAM_RMIN"), *ev = getenv("PYR_STREAM_ET");
+  const char *rm = knob("PYR_STREAM_RMIN"), *ev = knob("PYR_STREAM_ET");
   rmin = std::max(1, rm ? atoi(rm) : (3 * k1 + 7) / 8);
   rmax = std::max(rmin, k1);
   et = (ev ? atof(ev) : 6.0) * k1;
@@ -781,11 +781,11 @@ static void stream_rank(int k1, int32_t &rmin, int32_t &rmax, double &et) {
 // candidate buffer per query (PYR_STREAM_CAP; a query emits ~6 K1 rows, 96 at I1: a full buffer only
 // raises its floor, and the certificate decides) and rows per list chunk (PYR_STREAM_CHUNK)
 static int stream_cap() {
-  const char *e = getenv("PYR_STREAM_CAP");
+  const char *e = knob("PYR_STREAM_CAP");
   return e ? std::max(8, atoi(e)) : 2048;
 }
 static int64_t stream_chunk() {
-  const char *e = getenv("PYR_STREAM_CHUNK");
+  const char *e = knob("PYR_STREAM_CHUNK");
   return round_up(e ? std::max<int64_t>(32, atoll(e)) : 5120, 32);
 }
 
@@ -796,7 +796,7 @@ static int64_t stream_chunk() {
 static int64_t stream_slice_queries(int64_t nq, int probes, int dt, int cap, int sv) {
   const int64_t per_q = (int64_t)cap * 8 + 8 + 8 * STREAM_KO + 16 + (int64_t)probes * (2 * dt + 8 + 4 * sv + 8);
   int64_t qs = (int64_t(16) << 30) / per_q;
-  if (const char *e = getenv("PYR_SLICE_QUERIES")) qs = std::min<int64_t>(qs, atoll(e));  // tests: force slicing
+  if (const char *e = knob("PYR_SLICE_QUERIES")) qs = std::min<int64_t>(qs, atoll(e));  // tests: force slicing
   return std::max<int64_t>(1, std::min<int64_t>(nq, qs));
 }
 
@@ -846,7 +846,7 @@ void ivf_memory_plan(int dim, int64_t nrows, int nlist, int64_t max_len, int64_t
 // sampled thresholds, so every visible row of the scanned lists is emitted with its upper bound (with a
 // PYR_STREAM_CAP large enough, pyr_index_debug_candidates then returns every row's bound)
 static bool emit_all() {
-  const char *e = getenv("PYR_STREAM_EMIT_ALL");
+  const char *e = knob("PYR_STREAM_EMIT_ALL");
   return e && atoi(e) != 0;
 }
 static StreamArgs main_scan_args(const StreamArgs &sa) {
@@ -854,15 +854,22 @@ static StreamArgs main_scan_args(const StreamArgs &sa) {
   if (emit_all()) m.thr = nullptr;
   return m;
 }
+// (concurrent searches hold the index shared: the three fields are written and read together under ws_mu)
 void Index::note_stream_slice(Workspace &ws, int64_t nq, int cap) {
+  std::lock_guard<std::mutex> g(ws_mu);
   dbg_ws = &ws;
   dbg_nq = nq;
   dbg_cap = cap;
 }
 void Index::debug_candidates(int64_t nq, int32_t cap, float *h_ub, int64_t *h_label, int32_t *h_cnt) {
-  if (!dbg_ws) throw Error(PYR_E_STATE, "no stream-scan search ran on this index");
-  if (nq != dbg_nq || cap != dbg_cap) throw Error(PYR_E_ARG, "nq / cap differ from the last stream-scan slice");
-  Workspace &ws = *dbg_ws;
+  Workspace *w;
+  {
+    std::lock_guard<std::mutex> g(ws_mu);
+    if (!dbg_ws) throw Error(PYR_E_STATE, "no stream-scan search ran on this index");
+    if (nq != dbg_nq || cap != dbg_cap) throw Error(PYR_E_ARG, "nq / cap differ from the last stream-scan slice");
+    w = dbg_ws;
+  }
+  Workspace &ws = *w;
   HIPCHK(hipStreamSynchronize(ws.st));
   std::vector<uint2> c((size_t)nq * cap);
   HIPCHK(hipMemcpy(c.data(), ws.scand.p, sizeof(uint2) * c.size(), hipMemcpyDeviceToHost));
@@ -874,14 +881,14 @@ void Index::debug_candidates(int64_t nq, int32_t cap, float *h_ub, int64_t *h_la
   }
 }
 static int filter_ablate() {  // measurement only (StreamArgs::ablate)
-  const char *e = getenv("PYR_FILTER_ABLATE");
+  const char *e = knob("PYR_FILTER_ABLATE");
   return e ? atoi(e) : 0;
 }
 // K1 = candidates per query: the smallest register-list capacity (16, 32, 64) leaving at
 // least 4 candidates beyond k (PYR_FILTER_MARGIN overrides the 4); 0 = filter unavailable
 static int filter_k1(int k) {
   int m = 4;
-  if (const char *e = getenv("PYR_FILTER_MARGIN")) m = std::max(0, atoi(e));
+  if (const char *e = knob("PYR_FILTER_MARGIN")) m = std::max(0, atoi(e));
   for (int c : {16, 32, 64})
     if (k + m <= c) return c;
   return 0;
@@ -889,7 +896,7 @@ static int filter_k1(int k) {
 // error-bound constant of the refine certificate (filter.hip refine_kernel); PYR_FILTER_CERR
 // overrides it for tests (a huge value fails every certificate -> every query re-runs exactly)
 static double filter_cerr(int dim) {
-  if (const char *e = getenv("PYR_FILTER_CERR")) return atof(e);
+  if (const char *e = knob("PYR_FILTER_CERR")) return atof(e);
   return 4.0 * dim + 64.0;
 }
 
@@ -910,14 +917,14 @@ struct CosRefine {
 static int deep_cap(int k1) { return std::max(stream_cap(), 16 * k1); }
 // PYR_DEEP_REFINE=0: an IVF search with k > 60 takes the exact scan (A/B; read per search)
 static bool deep_refine_on() {
-  const char *e = getenv("PYR_DEEP_REFINE");
+  const char *e = knob("PYR_DEEP_REFINE");
   return !(e && atoi(e) == 0);
 }
 // the refine depth for k > 60 (deep_refine_kernel): 128 / 256 >= k + the margin, 0 past that or when the
 // candidate buffer's sort would not fit 60 KiB of LDS
 static int deep_k1(int k) {
   int m = 4;
-  if (const char *e = getenv("PYR_FILTER_MARGIN")) m = std::max(0, atoi(e));
+  if (const char *e = knob("PYR_FILTER_MARGIN")) m = std::max(0, atoi(e));
   // k within 0.8 K1: k = 200 at depth 256 failed 2,453 of 10,000 I1 queries, k = 252 at 256 nearly all
   // (profiles/r5_late/deepk_ab.log)
   for (int c : {128, 256, 512})
@@ -927,19 +934,19 @@ static int deep_k1(int k) {
 
 // PYR_MAXSCANS_STREAM=0: an IVF search with a MaxScans budget takes the exact scan (A/B; read per search)
 static bool max_scans_stream() {
-  const char *e = getenv("PYR_MAXSCANS_STREAM");
+  const char *e = knob("PYR_MAXSCANS_STREAM");
   return !(e && atoi(e) == 0);
 }
 
 // PYR_IVF_BUFFER_STREAM=0: an IVF_FLAT search with a non-empty buffer takes the exact scan (A/B; read per search)
 static bool buffer_stream() {
-  const char *e = getenv("PYR_IVF_BUFFER_STREAM");
+  const char *e = knob("PYR_IVF_BUFFER_STREAM");
   return !(e && atoi(e) == 0);
 }
 
 static bool merge_refine_fused() {
-  const char *e = getenv("PYR_MERGE_REFINE");
-  return !(e && atoi(e) == 0) && !getenv("PYR_STREAM_DEBUG");
+  const char *e = knob("PYR_MERGE_REFINE");
+  return !(e && atoi(e) == 0) && !knob("PYR_STREAM_DEBUG");
 }
 
 // list-sharded search (IvfFlatIndex::shard_search, shard.hip): a slice's thresholds T_q (from the home
@@ -1201,7 +1208,7 @@ struct FlatIndex : Index {
   // BruteForceVectorIndex.Build is a no-op for the results; here the FLAT L2 tiles are re-centred on the
   // live rows (a Delta head is built after its compaction, DeltaVectorIndex.cs:124-158)
   void build() override {
-    if (st.center16 && st.resid && !getenv("PYR_FROZEN_CENTER")) st.recenter(wst);
+    if (st.center16 && st.resid && !knob("PYR_FROZEN_CENTER")) st.recenter(wst);
   }
   void reserve(int64_t rows) override {
     st.reserve(st.n + rows, wst);
@@ -1275,7 +1282,7 @@ struct FlatIndex : Index {
     }
     st.n = next;
     // the FLAT L2 tiles' center follows the rows: re-centred each time the store has doubled since
-    if (st.center16 && st.resid && st.n >= 2 * st.center_rows && !getenv("PYR_FROZEN_CENTER")) st.recenter(wst);
+    if (st.center16 && st.resid && st.n >= 2 * st.center_rows && !knob("PYR_FROZEN_CENTER")) st.recenter(wst);
   }
 
   // BruteForceVectorIndex.Search with EnableQuantization (:296-336): quantize the queries,
@@ -1592,7 +1599,7 @@ struct FlatIndex : Index {
       int32_t nf = 0;
       HIPCHK(hipMemcpyAsync(&nf, ws.fail_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, ws.st));
       HIPCHK(hipStreamSynchronize(ws.st));
-      if (getenv("PYR_STREAM_DEBUG"))
+      if (knob("PYR_STREAM_DEBUG"))
         fprintf(stderr, "[flat stream deep] nq %lld k %d: depth %d certificate failures %d\n", (long long)nq, k, k1,
                 nf);
       filter_fallback(ws, nf, d_q, dim, k, d_s, d_l, d_c,
@@ -1624,12 +1631,12 @@ struct FlatIndex : Index {
     }
     // measurement only (the profiler's re-run count, PYR_STREAM_DEBUG): read the failure counts back
     int32_t nf = 0;
-    if (prof().on || getenv("PYR_STREAM_DEBUG")) {
+    if (prof().on || knob("PYR_STREAM_DEBUG")) {
       int32_t n1 = 0;
       HIPCHK(hipMemcpyAsync(&n1, ws.fail_cnt2.p, sizeof(int32_t), hipMemcpyDeviceToHost, ws.st));
       HIPCHK(hipMemcpyAsync(&nf, ws.fail_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, ws.st));
       HIPCHK(hipStreamSynchronize(ws.st));
-      if (getenv("PYR_STREAM_DEBUG"))
+      if (knob("PYR_STREAM_DEBUG"))
         fprintf(stderr, "[flat stream] nq %lld chunks %d: certificate failures depth %d %d, depth 64 %d\n",
                 (long long)nq, nch, k1, n1, nf);
     }
@@ -1659,7 +1666,7 @@ struct FlatIndex : Index {
     ra.out_s = d_s;
     ra.out_l = d_l;
     ra.out_c = d_c;
-    if (!filter_ablate() && !getenv("PYR_STREAM_THR_BIAS")) {
+    if (!filter_ablate() && !knob("PYR_STREAM_THR_BIAS")) {
       PhaseTimer t(PH_FALLBACK, ws.st, nf);
       ra.nchunk = (int32_t)std::max<int64_t>(1, std::min<int64_t>(64, (flat_chunk_rows(cutoff) + 1023) / 1024));
       ra.done = rerun_done(ws, nq);
@@ -1829,7 +1836,7 @@ struct DictBuffer {
 // covers (2.2 D + 8) u (|q| + |c|)^2; PYR_COARSE_CERR overrides it for tests (huge: every query takes
 // the dense exact fallback)
 static double coarse_cerr(int dim) {
-  if (const char *e = getenv("PYR_COARSE_CERR")) return atof(e);
+  if (const char *e = knob("PYR_COARSE_CERR")) return atof(e);
   return 4.0 * dim + 64.0;
 }
 
@@ -1891,7 +1898,7 @@ struct Coarse {
       return;
     }
     // the matrix-core ranking (PYR_COARSE_MFMA=0: the dense exact ranking below; same probes)
-    const char *cm = getenv("PYR_COARSE_MFMA");
+    const char *cm = knob("PYR_COARSE_MFMA");
     if (!(cm && atoi(cm) == 0) && cfinite && coarse_mfma_supported(nlist, cs.dim, met, nprobe) &&
         coarse_dense_supported(nlist)) {
       ws.probes.ensure(sizeof(int32_t) * nq * nprobe);
@@ -1910,7 +1917,7 @@ struct Coarse {
       }
       return;
     }
-    const char *ce = getenv("PYR_COARSE_DENSE");  // 0: the top-k scan below (A/B only, same ranking)
+    const char *ce = knob("PYR_COARSE_DENSE");  // 0: the top-k scan below (A/B only, same ranking)
     if (!(ce && atoi(ce) == 0) && coarse_dense_supported(nlist)) {
       ws.probes.ensure(sizeof(int32_t) * nq * nprobe);
       // <= 256 MB of scores and <= 2^21 queries (grid.y) per launch
@@ -1928,7 +1935,7 @@ struct Coarse {
     const int64_t nqc = (nq + qchunk - 1) / qchunk;
     int want = (int)std::max<int64_t>(1, std::min<int64_t>(16, (2048 + nqc - 1) / nqc));
     want = std::min(want, std::max(1, nlist / 32));
-    if (const char *e = getenv("PYR_COARSE_CHUNKS")) want = std::max(1, std::min(atoi(e), nlist));  // measurement
+    if (const char *e = knob("PYR_COARSE_CHUNKS")) want = std::max(1, std::min(atoi(e), nlist));  // measurement
     ScanPlan p;
     p.qchunk = qchunk;
     p.chunk_rows = (int)round_up((nlist + want - 1) / want, 8);
@@ -2014,7 +2021,7 @@ static int build_ivf_items_range(Workspace &ws, int set, int64_t nq, int nprobe,
 // Measured at the bench config: candidates 16.3 M -> 9.4 M, insertion iterations -7 %, but the
 // small first launch leaves the chip half idle: 9.84 -> 12.0 ms (profiles/r1_sweeps/sweep16-17).
 static bool ivf_seed_enabled() {
-  const char *e = getenv("PYR_IVF_SEED");
+  const char *e = knob("PYR_IVF_SEED");
   return e && atoi(e) != 0;
 }
 
@@ -2031,8 +2038,8 @@ static IvfChunking ivf_chunking(int64_t max_len, int probes, int other_parts, in
   // a small batch (e.g. the re-run of certificate failures) has few (list, query group) items:
   // shorter chunks give it more of the chip
   if (nq * probes < 8192) chunk = 1024;
-  if (const char *e = getenv("PYR_IVF_CHUNK")) chunk = std::max<int64_t>(8, atoll(e));
-  if (const char *e = getenv("PYR_IVF_WARM")) warm = std::max<int64_t>(0, atoll(e));
+  if (const char *e = knob("PYR_IVF_CHUNK")) chunk = std::max<int64_t>(8, atoll(e));
+  if (const char *e = knob("PYR_IVF_WARM")) warm = std::max<int64_t>(0, atoll(e));
   if (!bounds) warm = 0;  // the warm-up launch only pays with shared bounds
   chunk = round_up(chunk, 32);  // whole fp16 tiles (lists start on a 32-row boundary)
   warm = round_up(warm, 32);
@@ -2095,23 +2102,12 @@ struct IvfFlatIndex : Index {
     nprobe_default = d.default_nprobe > 0 ? d.default_nprobe : 3;  // CombineNProbe (:14)
   }
 
-  // per row slot its list (shard records), rebuilt when the list bounds change
+  // per row slot its list (shard records): built with the list bounds, on the write stream, under the write
+  // lock (no search can see it half built)
   DevMem row_list;
-  uint64_t lmeta_gen = 1, rl_gen = 0;
-  std::mutex rl_mu;
-  const int32_t *row_lists(hipStream_t st) {
-    std::lock_guard<std::mutex> lk(rl_mu);
-    if (rl_gen != lmeta_gen) {
-      if (capturing(st)) return nullptr;  // (the records then search the bounds)
-      row_list.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(lists.n, 1));
-      launch_list_ids(dlb.as<int32_t>(), dle.as<int32_t>(), coarse.nlist, row_list.as<int32_t>(), st);
-      rl_gen = lmeta_gen;
-    }
-    return row_list.as<int32_t>();
-  }
+  const int32_t *row_lists(hipStream_t) { return row_list.as<int32_t>(); }
 
   void upload_list_meta() {
-    ++lmeta_gen;
     const int nl = coarse.nlist;
     dlb.ensure(sizeof(int32_t) * std::max(nl, 1));
     dle.ensure(sizeof(int32_t) * std::max(nl, 1));
@@ -2119,6 +2115,9 @@ struct IvfFlatIndex : Index {
     HIPCHK(hipMemcpyAsync(dlb.p, lb.data(), sizeof(int32_t) * nl, hipMemcpyHostToDevice, wst));
     HIPCHK(hipMemcpyAsync(dle.p, le.data(), sizeof(int32_t) * nl, hipMemcpyHostToDevice, wst));
     HIPCHK(hipMemcpyAsync(dllive.p, llive.data(), sizeof(int32_t) * nl, hipMemcpyHostToDevice, wst));
+    if (row_list.n < sizeof(int32_t) * (size_t)std::max<int64_t>(lists.n, 1))
+      row_list.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(lists.n, 1));
+    launch_list_ids(dlb.as<int32_t>(), dle.as<int32_t>(), nl, row_list.as<int32_t>(), wst);
     HIPCHK(hipStreamSynchronize(wst));
   }
   int list_of_pos(int64_t pos) const {
@@ -2624,7 +2623,7 @@ struct IvfFlatIndex : Index {
     sa.key_base = 0;
     sa.row_limit = 0xFFFFFFFFu;
     sa.ablate = filter_ablate();
-    sa.thr_bias = getenv("PYR_STREAM_THR_BIAS") ? (float)atof(getenv("PYR_STREAM_THR_BIAS")) : 0.0f;
+    sa.thr_bias = knob("PYR_STREAM_THR_BIAS") ? (float)atof(knob("PYR_STREAM_THR_BIAS")) : 0.0f;
     const int prec = FILTER_F16X1;
     sa.rsq16 = lists.rsq16.as<float>();
     sa.rsq = lists.rsq.as<float>();
@@ -2632,7 +2631,7 @@ struct IvfFlatIndex : Index {
     stream_ub_terms(dt, met, filter_f16_cerr(dt, met, prec), filter_cerr(dt), filter_f16_abs(dt, met, lists.sx, prec),
                     sa);
     sa.mub = lists.row_terms(met, sa.kr, sa.kx, ws.st);
-    const bool timing = getenv("PYR_STREAM_TIMING") != nullptr;  // measurement only (syncs)
+    const bool timing = knob("PYR_STREAM_TIMING") != nullptr;  // measurement only (syncs)
     if (timing) {
       ws.tdbg.ensure(sizeof(unsigned long long) * 8);
       WordFill z;
@@ -2743,7 +2742,7 @@ struct IvfFlatIndex : Index {
       }
       HIPCHK(hipMemcpyAsync(&nf, ws.fail_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, ws.st));
       HIPCHK(hipStreamSynchronize(ws.st));
-      if (getenv("PYR_STREAM_DEBUG"))
+      if (knob("PYR_STREAM_DEBUG"))
         fprintf(stderr, "[stream deep] nq %lld k %d: depth %d certificate failures %d\n", (long long)nq, k, k1, nf);
       // the failures' own probe lists (gathered by the fail list) on the exact VALU scan, same arithmetic
       filter_fallback(ws, nf, d_q, dim, k, d_s, d_l, d_c,
@@ -2806,7 +2805,7 @@ struct IvfFlatIndex : Index {
       HIPCHK(hipGetLastError());
     }
     // measurement only (the profiler's re-run count, PYR_STREAM_DEBUG): read the failure count back
-    const bool dbg = getenv("PYR_STREAM_DEBUG") != nullptr;
+    const bool dbg = knob("PYR_STREAM_DEBUG") != nullptr;
     if (prof().on || dbg) {
       HIPCHK(hipMemcpyAsync(&nf, ws.fail_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, ws.st));
       HIPCHK(hipStreamSynchronize(ws.st));
@@ -2837,7 +2836,7 @@ struct IvfFlatIndex : Index {
     ra.qlim = budget ? ws.limits.as<uint32_t>() : nullptr;
     // (measurement-only knobs that change the candidates skip the re-run: PYR_FILTER_ABLATE,
     // PYR_STREAM_THR_BIAS)
-    if (!filter_ablate() && !getenv("PYR_STREAM_THR_BIAS")) {
+    if (!filter_ablate() && !knob("PYR_STREAM_THR_BIAS")) {
       PhaseTimer t(PH_FALLBACK, ws.st, nf);
       ra.nchunk = (int32_t)std::max<int64_t>(1, std::min<int64_t>(64, (max_len + 1023) / 1024));
       ra.done = rerun_done(ws, nq);
@@ -3516,7 +3515,7 @@ struct IvfPqIndex : Index {
     codes_rm.ensure((size_t)n * M);
     A.ensure(sizeof(int32_t) * n);
     int64_t chunk = std::max<int64_t>(1024, (int64_t(1) << 30) / ((int64_t)dim * 4));
-    if (const char *e = getenv("PYR_PQ_BUILD_CHUNK")) chunk = std::max<int64_t>(1, atoll(e));  // tests
+    if (const char *e = knob("PYR_PQ_BUILD_CHUNK")) chunk = std::max<int64_t>(1, atoll(e));  // tests
     X.ensure(sizeof(float) * std::min(chunk, n) * dim);
     ds.ensure(sizeof(int64_t) * std::min(chunk, n));
     const bool progress = getenv("PYR_PROGRESS") && atoi(getenv("PYR_PROGRESS")) != 0;  // long bulk builds
@@ -3632,7 +3631,7 @@ struct IvfPqIndex : Index {
     const int nprobe = prm.nprobe < 0 ? nprobe_default : prm.nprobe;
     const int probes = (built && coarse.nlist > 0) ? std::max(0, std::min(nprobe, coarse.nlist)) : 0;
     // the matrix-core scan: built lists only (no buffer rows), the P1 geometry (pq32_supported)
-    const char *pm = getenv("PYR_PQ_MFMA");  // 0: the LUT scan below (A/B and the re-run path)
+    const char *pm = knob("PYR_PQ_MFMA");  // 0: the LUT scan below (A/B and the re-run path)
     if (!(pm && atoi(pm) == 0) && pq32_ready && probes > 0 && filter_enabled() && pq32_supported(dim, M, ksub, k)) {
       if (buf.live_count() == 0) {
         search_pq32(d_q, nq, k, probes, d_s, d_l, d_c, ws);
@@ -3707,7 +3706,7 @@ struct IvfPqIndex : Index {
     const int cap = stream_cap();
     IvfChunking ch{(int32_t)stream_chunk(), 1, 0};
     // a list's items on one XCD (pq32.hip: its code chunks leave HBM once per L2); PYR_PQ_XCD=0: one queue (A/B)
-    ch.xcd = getenv("PYR_PQ_XCD") && atoi(getenv("PYR_PQ_XCD")) == 0 ? 0 : 1;
+    ch.xcd = knob("PYR_PQ_XCD") && atoi(knob("PYR_PQ_XCD")) == 0 ? 0 : 1;
     ch.cmax = std::max(1, ivf_list_chunks((int)pq_max_len, ch));
     if ((int64_t)probes * ch.cmax > MAX_PARTS) {
       const int64_t room = std::max<int64_t>(1, MAX_PARTS / std::max(probes, 1));
@@ -3863,7 +3862,7 @@ struct IvfPqIndex : Index {
       HIPCHK(hipMemcpyAsync(&nf, ws.fail_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, ws.st));
       HIPCHK(hipStreamSynchronize(ws.st));
     }
-    if (getenv("PYR_STREAM_DEBUG")) {
+    if (knob("PYR_STREAM_DEBUG")) {
       int32_t n1 = 0;
       HIPCHK(hipMemcpy(&n1, ws.fail_cnt2.p, sizeof(int32_t), hipMemcpyDeviceToHost));
       fprintf(stderr, "[pq32] nq %lld: certificate failures depth %d %d, depth 64 %d\n", (long long)nq, k1, n1, nf);
@@ -3950,7 +3949,7 @@ struct IvfPqIndex : Index {
       a.part_s = ws.part_s.as<float>();
       a.part_k = ws.part_k.as<uint32_t>();
       a.gthr = kern > 0 && bounds_enabled() ? shared_bounds(ws, nq) : nullptr;
-      if (const char *e = getenv("PYR_PQ_ABLATE")) a.ablate = atoi(e);  // measurement only
+      if (const char *e = knob("PYR_PQ_ABLATE")) a.ablate = atoi(e);  // measurement only
       if (kern == 0 && pq_scan_lds_bytes(dim, M, ksub, k) > 160 * 1024)
         throw Error(PYR_E_ARG, "PQ lookup table exceeds LDS");
       PhaseTimer t(PH_PQ_SCAN, ws.st, prof().on ? probed_rows(ws, nq, probes, le, lb) : 0);

@@ -862,37 +862,37 @@ size_t deep_refine_lds_bytes(int cap, int k1) {
   return P * sizeof(uint64_t);
 }
 
+// the dynamic-LDS limit of each instantiation is raised once per device to the largest launch deep_k1 allows
+// (144 KiB: the static LDS, ~4 KiB, sits beside it; asking for the whole 160 KiB fails), never lowered -- so
+// concurrent searches of different k on other streams cannot shrink it under one another
+constexpr int DEEP_LDS_MAX = 144 * 1024;
+template <int V, int MET, int D>
+static void go_deep(const CandMergeArgs &m, const RefineArgs &a, size_t lds, hipStream_t st) {
+  static std::atomic<uint64_t> done{0};
+  allow_max_lds(reinterpret_cast<const void *>(&deep_refine_kernel<V, MET, D>), done, DEEP_LDS_MAX);
+  hipLaunchKernelGGL((deep_refine_kernel<V, MET, D>), dim3((unsigned)a.nq), dim3(256), lds, st, m, a);
+}
+
 void launch_deep_refine(const CandMergeArgs &m, const RefineArgs &a, int metric, int V, hipStream_t st) {
   if (a.nq <= 0) return;
   if (a.k1 > DEEP_MAX || a.k1 < a.k || a.k > 256) throw std::invalid_argument("deep_refine: depth");
   const size_t lds = deep_refine_lds_bytes(m.cap, a.k1);
-  // the dynamic limit raised to exactly what this launch takes (static LDS ~4 KiB beside it: asking for the
-  // whole 160 KiB fails for a kernel with static LDS)
-  if (lds > 144 * 1024) throw std::invalid_argument("deep_refine: candidate buffer too large");
-  auto go = [&](auto kern) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) {
-      (void)hipGetLastError();
-      throw std::runtime_error(std::string("deep_refine: LDS attribute: ") + hipGetErrorString(e));
-    }
-    hipLaunchKernelGGL(kern, dim3((unsigned)a.nq), dim3(256), lds, st, m, a);
-  };
+  if (lds > (size_t)DEEP_LDS_MAX) throw std::invalid_argument("deep_refine: candidate buffer too large");
   // V = 1: the safe VectorMath forms (IVF); V = 4: the *Unsafe forms (FLAT, BruteForceVectorIndex.cs:350-356)
   if (V == 4) {
     if (metric == L2) {
-      if (a.dim == 128) go(deep_refine_kernel<4, L2, 128>);
-      else go(deep_refine_kernel<4, L2, 0>);
+      if (a.dim == 128) go_deep<4, L2, 128>(m, a, lds, st);
+      else go_deep<4, L2, 0>(m, a, lds, st);
     } else {
-      if (a.dim == 128) go(deep_refine_kernel<4, IP, 128>);
-      else go(deep_refine_kernel<4, IP, 0>);
+      if (a.dim == 128) go_deep<4, IP, 128>(m, a, lds, st);
+      else go_deep<4, IP, 0>(m, a, lds, st);
     }
   } else if (metric == L2) {
-    if (a.dim == 128) go(deep_refine_kernel<1, L2, 128>);
-    else go(deep_refine_kernel<1, L2, 0>);
+    if (a.dim == 128) go_deep<1, L2, 128>(m, a, lds, st);
+    else go_deep<1, L2, 0>(m, a, lds, st);
   } else {
-    if (a.dim == 128) go(deep_refine_kernel<1, IP, 128>);
-    else go(deep_refine_kernel<1, IP, 0>);
+    if (a.dim == 128) go_deep<1, IP, 128>(m, a, lds, st);
+    else go_deep<1, IP, 0>(m, a, lds, st);
   }
 }
 

@@ -2,6 +2,8 @@
 // Internal to libpyrope_hip.so (the public boundary is include/pyrope_ann.h).
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 #include <stdint.h>
 
 #include <atomic>
@@ -12,13 +14,24 @@ namespace pyr {
 // device, so it is set once per (kernel, device ordinal) -- `done` is the kernel's bit mask of
 // devices -- and the bit is published only after the call, so a thread that sees it set (any
 // thread, any index on any device) launches with the attribute in place.
-inline void allow_max_lds(const void *fn, std::atomic<uint64_t> &done) {
+inline void allow_max_lds(const void *fn, std::atomic<uint64_t> &done, int bytes = 160 * 1024) {
   int dev = 0;
   (void)hipGetDevice(&dev);
   const uint64_t bit = uint64_t(1) << (dev & 63);
   if (done.load(std::memory_order_acquire) & bit) return;
-  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
   done.fetch_or(bit, std::memory_order_acq_rel);
+}
+
+// Measurement and test switches (the PYR_* variables of DESIGN.md §7): honoured only when the process starts
+// with PYR_DEV_KNOBS=1 (read once, at the first switch read).  A production host's environment cannot steer
+// the search paths; tests/conftest.py and the A/B scripts set it.
+inline const char *knob(const char *name) {
+  static const bool on = [] {
+    const char *e = std::getenv("PYR_DEV_KNOBS");
+    return e && std::atoi(e) == 1;
+  }();
+  return on ? std::getenv(name) : nullptr;
 }
 
 enum Metric { L2 = 0, IP = 1, COS = 2 };

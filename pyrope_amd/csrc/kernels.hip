@@ -1776,7 +1776,7 @@ void launch_ivf_items(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t
                       int phase, IvfItemWs &ws, hipStream_t st, int32_t pb, int32_t pe, bool balance, bool zeroed) {
   if (pe < 0) pe = nprobe;
   const int64_t n = nq * (pe - pb);
-  const bool lds = nlist <= IVF_LDS_BINS && !getenv("PYR_IVF_GLOBAL_HIST");  // (knob: measurement only)
+  const bool lds = nlist <= IVF_LDS_BINS && !knob("PYR_IVF_GLOBAL_HIST");  // (knob: measurement only)
   const size_t hb = sizeof(int) * (size_t)nlist;
   // skip_empty (a list-sharded rank): the (query, probe) entries of the lists it does not hold take no slot
   const int32_t *skb = ch.skip_empty ? list_begin : nullptr, *ske = ch.skip_empty ? list_end : nullptr;

@@ -283,7 +283,7 @@ struct MultiIvfIndex : Index {
     HIPCHK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_cnt, hipEventDisableTiming));
     HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&h_counts), sizeof(int32_t) * 64, hipHostMallocDefault));
-    if (const char *e = getenv("PYR_SHARD_FCAP")) fcap = std::max(1, atoi(e));
+    if (const char *e = knob("PYR_SHARD_FCAP")) fcap = std::max(1, atoi(e));
   }
   ~MultiIvfIndex() override {
     for (int r = 0; r < W; ++r) {
@@ -521,7 +521,7 @@ struct MultiIvfIndex : Index {
   void sharded_search(const float *d_q, int64_t nq, int k, const pyr_search_params &prm, int P, float *d_s,
                       int64_t *d_l, int32_t *d_c, Workspace &ws) {
     if (!xp) {
-      const char *e = getenv("PYR_SHARD_XPORT");
+      const char *e = knob("PYR_SHARD_XPORT");
       const bool use_rccl = e ? std::strcmp(e, "rccl") == 0 : distinct;
       if (use_rccl && !distinct) throw Error(PYR_E_ARG, "RCCL needs one shard per device");
       if (use_rccl) xp = std::make_unique<RcclXport>(dev, st);

@@ -72,8 +72,7 @@ void ImageWriter::commit() {
   std::random_device rd;  // the image's identity (T_NONCE), fresh for every snapshot
   uint32_t nonce[NONCE_BYTES / 4];
   for (auto &w : nonce) w = rd();
-  // tests only (PYR_IMAGE_NO_NONCE): an image as round 3 wrote them, without the section
-  if (!std::getenv("PYR_IMAGE_NO_NONCE")) host(T_NONCE, nonce, NONCE_BYTES);
+  host(T_NONCE, nonce, NONCE_BYTES);
   if (std::fseek(f, 8 + 16, SEEK_SET) != 0) throw Error(PYR_E_IO, "seek in " + tmp + " failed");
   put(&nsec, 4);
   if (std::fflush(f) != 0 || fsync(fileno(f)) != 0) throw Error(PYR_E_IO, "flush of " + tmp + " failed");

@@ -426,7 +426,7 @@ void launch_sample16(const StreamArgs &a, int metric, int max_items, hipStream_t
   const int64_t pg = std::min<int64_t>((int64_t)max_items * split, 8 * (int64_t)device_cus());
   auto prep = [&](auto kern) { hipLaunchKernelGGL(kern, dim3((unsigned)pg), dim3(256), 0, st, a); };
   // query-major when the work lists recorded the positions (PYR_SPREP_Q=0: the list-major pass; A/B only)
-  const bool qmaj = !(getenv("PYR_SPREP_Q") && atoi(getenv("PYR_SPREP_Q")) == 0);
+  const bool qmaj = !(knob("PYR_SPREP_Q") && atoi(knob("PYR_SPREP_Q")) == 0);
   if (a.qpos && qmaj && a.nq > 0) {
     const dim3 qg((unsigned)((a.nq + 3) / 4));
     auto prepq = [&](auto kern) { hipLaunchKernelGGL(kern, qg, dim3(256), 0, st, a); };
@@ -471,7 +471,7 @@ void launch_sample16(const StreamArgs &a, int metric, int max_items, hipStream_t
 // measurement only (scripts/bound_slack.py): PYR_EB_<BF|ERR|ABS|G|T> scale one constant of the bound, to find
 // how far each could shrink before some row's bound falls below its exact score (results may then differ)
 static double eb_scale(const char *name) {
-  const char *e = getenv(name);
+  const char *e = knob(name);
   return e ? atof(e) : 1.0;
 }
 void stream_ub_terms(int dim, int metric, double c_bf, double c_err, double c_abs, StreamArgs &a) {

@@ -215,10 +215,12 @@ __global__ __launch_bounds__(256) void sample_kernel(StreamArgs a) {
 }
 
 // ---- 2. the list scan ----
-// AB (measurement only, PYR_FILTER_ABLATE): 1 (64) = no emission, 2 (128) = tile stream only (no MFMA),
-// 3 (256) = no emission and every tile read from the item's first one (compute without HBM); the bit 512
-// (any variant) adds an L2 prefetch of the wave's next tile (4-byte LDS-DMA per line; measured slower:
-// 0.94 vs 0.90 ms and FETCH 1.83x vs 1.09x the stored bytes at I1, profiles/r4_scan)
+// AB (measurement only, PYR_FILTER_ABLATE; separate instantiations at D = 128, none of them in the shipped
+// kernel): 1 (64) = no emission, 2 (128) = tile stream only (no MFMA), 3 (256) = no emission and every tile
+// read from the item's first one (compute without HBM), 4 (1024) = round 4's B schedule, 5 (512) = an L2
+// prefetch of the wave's next tile (4-byte LDS-DMA per line; measured slower: 0.94 vs 0.90 ms and FETCH 1.83x
+// vs 1.09x the stored bytes at I1, profiles/r4_scan), 7 (2048) = the emission without the 4-row block tests,
+// 8 (PYR_STREAM_TIMING) = per-wave cycle buckets into a.tdbg
 // SMP: the sample pass on the same kernel (round 5): chunk-0 items only, wave w scores tile w of the list
 // (SAMPLE_TILES = 16 = the waves of a block at D <= 128) against every query group, and writes per (query,
 // probe) the 2 x 16 values max(f acc + row term) + cq over its lane half's rows -- each the bound of distinct
@@ -252,12 +254,12 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const char *hsrc = reinterpret_cast<const char *>(a.h16);
 
-  // measurement only (a.tdbg): per wave, cycles in the prologue, its tiles, the end-of-item barrier and
+  // measurement only (AB 8, a.tdbg): per wave, cycles in the prologue, its tiles, the end-of-item barrier and
   // the flush; items taken
   uint64_t tb[5] = {0, 0, 0, 0, 0};
   uint64_t tq = 0;
   auto stamp = [&](int b) {
-    if (a.tdbg) {
+    if constexpr (AB == 8) {
       const uint64_t now = __builtin_amdgcn_s_memtime();
       if (b >= 0) tb[b] += now - tq;
       tq = now;
@@ -270,14 +272,15 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
     const int item = item_sh;
     __syncthreads();  // every thread has read item_sh before thread 0 may rewrite it
     if (item >= *a.n_items) {
-      if (a.tdbg && lane == 0)
-        for (int b = 0; b < 5; ++b) atomicAdd(a.tdbg + b, (unsigned long long)tb[b]);
+      if constexpr (AB == 8)
+        if (lane == 0)
+          for (int b = 0; b < 5; ++b) atomicAdd(a.tdbg + b, (unsigned long long)tb[b]);
       return;
     }
     const ScanItem it = a.items[item];
     if (SMP && it.part != 0) continue;  // (block-uniform) chunk-0 items cover every (list, query) pair once
     stamp(-1);
-    tb[4] += 1;
+    if constexpr (AB == 8) tb[4] += 1;
     const int qcnt = it.qcnt, ng = (qcnt + 31) >> 5;
 
     // prologue: piece (j, s) = dims 16s + 8h .. +7 of query 32j + r in lane (r, h) (the B layout);
@@ -431,7 +434,8 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
                                                               acc[j], 0, 0, 0);
           }
         }
-        if (c == 0 && tpf >= 0 && (a.ablate & 512)) prefetch(tpf);
+        if constexpr (AB == 5)
+          if (c == 0 && tpf >= 0) prefetch(tpf);
       }
 #pragma unroll
       for (int j = 0; j < NG; ++j) {
@@ -478,12 +482,8 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
           }
           __builtin_amdgcn_sched_group_barrier(0x008, KS - 2 * NS, 0);
         }
-        if (j == 0 && tpf >= 0 && (a.ablate & 512)) {  // the tile's own loads were waited for: warm L2
-#pragma unroll
-          for (int o = 0; o < TB; o += 64 * 128)
-            glds<4>(hsrc + (size_t)(r0 / 32 + tpf) * TB + min(o + lane * 128, TB - 128), sink);
-          glds<4>(a.mub + r0 + 32 * tpf + (lane & 31), sink);
-        }
+        if constexpr (AB == 5)
+          if (j == 0 && tpf >= 0) prefetch(tpf);  // the tile's own loads were waited for: warm L2
         if (__builtin_expect(e, 0)) emit_y(acc, q.y, 32 * j + r, rt);
       }
     };
@@ -576,6 +576,14 @@ void launch_scan_dm(const StreamArgs &a, int max_items, hipStream_t st) {
     }
     if (a.ablate & 2048) {  // A/B: the emit loop tests every row (no 4-row block test)
       hipLaunchKernelGGL((scan_kernel<D, MET, 7>), dim3(grid), b, 0, st, a);
+      return;
+    }
+    if (a.ablate & 512) {
+      hipLaunchKernelGGL((scan_kernel<D, MET, 5>), dim3(grid), b, 0, st, a);
+      return;
+    }
+    if (a.tdbg) {
+      hipLaunchKernelGGL((scan_kernel<D, MET, 8>), dim3(grid), b, 0, st, a);
       return;
     }
   }

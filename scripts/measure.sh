@@ -18,6 +18,7 @@
 # Example: bash scripts/measure.sh gpurun_out/r5a tests 300 && bash scripts/measure.sh gpurun_out/r5a bench i1 400
 set -o pipefail
 export TMPDIR=/tmp
+export PYR_DEV_KNOBS=1  # A/B and measurement switches (kernels.h knob()); the driver's bench runs without
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 O=$1; step=$2; shift 2
 mkdir -p "$O"

@@ -3,6 +3,10 @@ import sys
 
 import pytest
 
+# the library honours its measurement / test switches (PYR_FILTER_CERR, PYR_STREAM_*, ...) only with this set
+# before it is loaded (kernels.h knob())
+os.environ.setdefault("PYR_DEV_KNOBS", "1")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

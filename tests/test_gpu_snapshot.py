@@ -237,6 +237,19 @@ def test_stale_id_map_is_ignored(hiplib, tmp_path):
     assert d.search([0, 0, 1, 0], 1)[0].id == "0"
 
 
+def _strip_nonce(path):
+    """Drop the trailing T_NONCE section (tag 13, 16 bytes: persist.h) and fix the header's section count."""
+    b = bytearray(open(path, "rb").read())
+    tag, _, n = struct.unpack_from("<IIQ", b, len(b) - 32)
+    assert (tag, n) == (13, 16)
+    del b[len(b) - 32:]
+    nsec = struct.unpack_from("<I", b, 24)[0]
+    struct.pack_into("<I", b, 24, nsec - 1)
+    st = os.stat(path)
+    open(path, "wb").write(bytes(b))
+    os.utime(path, ns=(st.st_atime_ns, st.st_mtime_ns + 1))
+
+
 def test_pre_nonce_snapshot_keeps_its_ids(hiplib, tmp_path):
     """a snapshot written before images carried a nonce (round 3: no T_NONCE section, an .ids map
     with 'image': [size, mtime_ns] and no 'image_nonce') still loads with its string ids; the same legacy
@@ -247,11 +260,8 @@ def test_pre_nonce_snapshot_keeps_its_ids(hiplib, tmp_path):
     a.add("alpha", [1, 0, 0, 0])
     a.add("beta", [0, 1, 0, 0])
     path = str(tmp_path / "old")
-    os.environ["PYR_IMAGE_NO_NONCE"] = "1"
-    try:
-        a.snapshot(path)
-    finally:
-        os.environ.pop("PYR_IMAGE_NO_NONCE", None)
+    a.snapshot(path)
+    _strip_nonce(path)  # the image as round 3 wrote them: no T_NONCE section
     m = json.load(open(path + ".ids"))
     st = os.stat(path)
     legacy = {"next": m["next"], "image": [st.st_size, st.st_mtime_ns], "ids": m["ids"]}
