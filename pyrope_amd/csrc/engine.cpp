@@ -773,10 +773,14 @@ static void stream_rank(int k1, int32_t &rmin, int32_t &rmax, double &et) {
     return;
   }
   // PYR_STREAM_RMIN / PYR_STREAM_ET (measurement only): the floor of R and the emitted-row target per K1
+  // Deep K1 (128 / 256 / 512, k > 60): 3 K1 rows and R >= K1 / 8 -- a query's 1,024 sample values give a
+  // threshold that close to its K1-th row without short queries (round 5's 6 K1 and 3 K1 / 8 emitted ~3,700 rows
+  // per query at K1 = 512, and the emission set the scan's cost: 4.2 of a k = 256 search's 5.8 ms at I1)
+  const bool deep = k1 > STREAM_KO;
   const char *rm = knob("PYR_STREAM_RMIN"), *ev = knob("PYR_STREAM_ET");
-  rmin = std::max(1, rm ? atoi(rm) : (3 * k1 + 7) / 8);
+  rmin = std::max(1, rm ? atoi(rm) : deep ? k1 / 8 : (3 * k1 + 7) / 8);
   rmax = std::max(rmin, k1);
-  et = (ev ? atof(ev) : 6.0) * k1;
+  et = (ev ? atof(ev) : deep ? 3.0 : 6.0) * k1;
 }
 // candidate buffer per query (PYR_STREAM_CAP; a query emits ~6 K1 rows, 96 at I1: a full buffer only
 // raises its floor, and the certificate decides) and rows per list chunk (PYR_STREAM_CHUNK)
