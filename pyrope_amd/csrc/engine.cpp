@@ -11,6 +11,7 @@
 #include <cstdio>
 
 #include <algorithm>
+#include <functional>
 #include <chrono>
 #include <cstring>
 #include <numeric>
@@ -911,6 +912,8 @@ struct CosRefine {
   const float *queries;    // raw queries
   const float *qnorm;      // ComputeNorm per query
   const uint32_t *zflag;   // a zero-norm row was written
+  // k > 60: the Cosine index's exact scan of n raw queries (the deep refine's certificate failures)
+  std::function<void(const float *, int64_t, float *, int64_t *, int32_t *)> exact;
 };
 
 // the stream scans' candidate merge and certified refine fused into one kernel (filter.hip
@@ -1374,8 +1377,8 @@ struct FlatIndex : Index {
       return;
     }
     int k1 = filter_k1(k);
-    // k > 60 (L2 / IP): depth 128 / 256 / 512 (deep_refine_kernel); Cosine keeps the exact scan
-    if (k1 == 0 && metric != COS && deep_refine_on()) k1 = deep_k1(k);
+    // k > 60: depth 128 / 256 / 512 (deep_refine_kernel; Cosine on the unit store with the exact Cosine)
+    if (k1 == 0 && deep_refine_on()) k1 = deep_k1(k);
     if (flat_stream_ok(k, k1, cutoff)) {
       search_stream(d_q, nq, k, k1, cutoff, d_s, d_l, d_c, ws);
       return;
@@ -1422,7 +1425,10 @@ struct FlatIndex : Index {
     launch_norms(d_q, nq, dim, 0, ws.qn.as<float>(), ws.st);  // VectorMath.ComputeNorm (:339)
     ws.cq.ensure(sizeof(float) * std::max<int64_t>(nq, 1) * dim);
     launch_unit_rows(d_q, nullptr, ws.qn.as<float>(), nq, dim, ws.cq.as<float>(), ws.st);
-    const CosRefine cr{&st, d_q, ws.qn.as<float>(), zflag.as<uint32_t>()};
+    CosRefine cr{&st, d_q, ws.qn.as<float>(), zflag.as<uint32_t>(), nullptr};
+    cr.exact = [&](const float *q2, int64_t n2, float *s2, int64_t *l2, int32_t *c2) {
+      search_exact(q2, n2, k, cutoff, s2, l2, c2, ws.nested());  // BruteForceVectorIndex.cs:354 on the raw rows
+    };
     std::shared_lock<std::shared_mutex> g(unit->mu);
     unit->search_stream(ws.cq.as<float>(), nq, k, k1, cutoff, d_s, d_l, d_c, ws, &cr);
     // (measurement: the unit store's keys are this store's slots)
@@ -1606,9 +1612,11 @@ struct FlatIndex : Index {
       if (knob("PYR_STREAM_DEBUG"))
         fprintf(stderr, "[flat stream deep] nq %lld k %d: depth %d certificate failures %d\n", (long long)nq, k, k1,
                 nf);
-      filter_fallback(ws, nf, d_q, dim, k, d_s, d_l, d_c,
+      // Cosine: the raw queries through the Cosine index's own exact scan
+      filter_fallback(ws, nf, cr ? cr->queries : d_q, dim, k, d_s, d_l, d_c,
                       [&](const float *q2, int64_t n2, float *s2, int64_t *l2, int32_t *c2) {
-                        search_exact(q2, n2, k, cutoff, s2, l2, c2, ws.nested());
+                        if (cr) cr->exact(q2, n2, s2, l2, c2);
+                        else search_exact(q2, n2, k, cutoff, s2, l2, c2, ws.nested());
                       });
       return;
     }
@@ -2378,8 +2386,8 @@ struct IvfFlatIndex : Index {
     int k1 = filter_k1(k);
     const bool budget_ok = prm.max_scans < 0 || (prm.max_scans > 0 && !ws.ext_probes && max_scans_stream());
     const bool nbuf = buf.live_count() > 0;
-    // k > 60: depth 128 / 256 / 512 (deep_refine_kernel) with no budget (a buffer: merged beside, below)
-    const bool deep = k1 == 0 && prm.max_scans < 0 && !ws.ext_probes && deep_refine_on();
+    // k > 60: depth 128 / 256 / 512 (deep_refine_kernel), a MaxScans budget too (a buffer: merged beside, below)
+    const bool deep = k1 == 0 && !ws.ext_probes && deep_refine_on();
     if (deep) k1 = deep_k1(k);
     const bool fast = filter_enabled() && probes > 0 && (!nbuf || buffer_stream()) && budget_ok &&
                       (k <= KMAX_FAST || deep) && probes < MAX_PARTS && k1 > 0;
@@ -2757,16 +2765,20 @@ struct IvfFlatIndex : Index {
                         Workspace &nw = ws.nested();
                         nw.ext_probes = ws.fprobes.as<int32_t>();
                         nw.ext_nprobe = probes;
+                        // the lists only (a buffer is merged by search()), with what the buffer left of the budget
+                        nw.skip_buffer = true;
                         pyr_search_params p2{};
                         p2.nprobe = probes;
-                        p2.max_scans = -1;
+                        p2.max_scans = ws.max_scans;
                         try {
                           search_exact(q2, n2, k, p2, s2, l2, c2, nw);
                         } catch (...) {
                           nw.ext_probes = nullptr;
+                          nw.skip_buffer = false;
                           throw;
                         }
                         nw.ext_probes = nullptr;
+                        nw.skip_buffer = false;
                       });
       return;
     }
@@ -3173,8 +3185,10 @@ struct IvfFlatIndex : Index {
                     int32_t *d_c, Workspace &ws) {
     const int nprobe = prm.nprobe < 0 ? nprobe_default : prm.nprobe;                  // :151-158
     const int64_t maxs = prm.max_scans < 0 ? (int64_t)INT32_MAX : prm.max_scans;       // :152
-    const int64_t bcut = buf.cutoff(std::min<int64_t>(maxs, buf.live_count()));
-    const int64_t bscanned = std::min<int64_t>(maxs, buf.live_count());
+    // (ws.skip_buffer: the lists alone -- a stream search's re-run, whose buffer search() merges itself)
+    const int64_t blive = ws.skip_buffer ? 0 : buf.live_count();
+    const int64_t bcut = buf.cutoff(std::min<int64_t>(maxs, blive));
+    const int64_t bscanned = std::min<int64_t>(maxs, blive);
     const bool index_on = built && coarse.nlist > 0 && bscanned < maxs;                // :183
     const int probes = index_on ? std::max(0, std::min(nprobe, coarse.nlist)) : 0;    // :198
     if (probes >= MAX_PARTS) throw Error(PYR_E_ARG, "nprobe too large");

@@ -114,17 +114,23 @@ def test_ivf_large_k_other_dim_and_past_range(hiplib, oracle):
     idx.close()
 
 
-@pytest.mark.parametrize("metric", [0, 1])
+@pytest.mark.parametrize("metric", [0, 1, 2])
 def test_flat_large_k_matches_oracle(hiplib, oracle, metric):
-    """FLAT L2 / IP (BruteForceVectorIndex.cs:275-379, the *Unsafe forms) with k > 60 on the stream scan: the deep
-    refine at V = 4, failures on the exact scan; equal to the oracle and to PYR_DEEP_REFINE=0 (Cosine keeps the
-    exact scan)"""
+    """FLAT L2 / IP / Cosine (BruteForceVectorIndex.cs:275-379, the *Unsafe forms; Cosine :354 on the raw rows)
+    with k > 60 on the stream scan: the deep refine at V = 4 (Cosine: the unit store's scan, the exact Cosine in
+    the refine, round 6), failures on the exact scan; equal to the oracle and to PYR_DEEP_REFINE=0"""
     from pyrope_amd import BruteForceVectorIndex, generate_synthetic
     n, d = 30000, 128
     x = generate_synthetic(n, d, 91)
+    if metric == 2:  # signed rows with norms over a decade, and exact zero rows (cosine 0)
+        x = (x - 0.5) * np.exp(np.linspace(0, 2.3, n, dtype=np.float32))[:, None]
+        x[::997] = 0.0
+        x = x.astype(np.float32)
     idx = BruteForceVectorIndex(d, metric)
     idx.add_labels(np.arange(n, dtype=np.int64), x)
     q = generate_synthetic(48, d, 92)
+    if metric == 2:
+        q = (q - 0.5).astype(np.float32)
     for k in [61, 150, 256]:
         got, calls = _sampled(hiplib, lambda: idx.search_batch(q, k))
         assert calls >= 1, "FLAT k > 60 must take the stream scan"
@@ -171,4 +177,56 @@ def test_ivf_large_k_with_buffer(hiplib, oracle, metric):
                            np.int64)
             np.testing.assert_array_equal(got[1][i][: len(exp)], exp)
             assert np.array_equal(got[0][i][: len(os_)].view(np.uint32), os_.astype(np.float32).view(np.uint32))
+    idx.close()
+
+
+@pytest.mark.parametrize("metric", [0, 1, 2])
+@pytest.mark.parametrize("max_scans", [1, 800, 3000])
+def test_ivf_large_k_with_max_scans(hiplib, oracle, metric, max_scans):
+    """k > 60 under a MaxScans budget (IvfFlatVectorIndex.cs:152-156, :202-212; round 6: the deep refine on the
+    budgeted stream scan, its failures on the exact scan with the same budget over the lists alone); with and
+    without rows in the buffer (which the budget reaches first), certificates as they fall and all forced to
+    fail.  Equal to the oracle and to the exact path (PYR_DEEP_REFINE=0)."""
+    from pyrope_amd import IvfFlatVectorIndex, SearchOptions, generate_synthetic
+    d, n, nl, P = 128, 12000, 24, 6
+    x = generate_synthetic(n, d, 101)
+    idx = IvfFlatVectorIndex(d, metric, n_list=nl)
+    idx.add_labels(np.arange(n, dtype=np.int64), x)
+    idx.build()
+    q = generate_synthetic(36, d, 102)
+    off, labels, live = idx.ivf_layout()
+    rows = x[np.where(labels >= 0, labels, 0)]
+    cents = idx.centroids_array()
+    opts = SearchOptions(nprobe=P, max_scans=max_scans)
+    for k in [90, 200]:
+        got, calls = _sampled(hiplib, lambda: idx.search_batch(q, k, opts))
+        if max_scans > 1:
+            assert calls >= 1, "k > 60 with a budget must take the stream scan"
+        with _env(PYR_DEEP_REFINE=0):
+            _bits(got, idx.search_batch(q, k, opts))
+        with _env(PYR_FILTER_CERR="1e15"):
+            _bits(got, idx.search_batch(q, k, opts))
+        for i in range(0, len(q), 7):
+            os_, ok = oracle.ivf_search(q[i], k, cents, rows, off, live, metric=metric, nprobe=P,
+                                        max_scans=max_scans)
+            assert int(got[2][i]) == len(os_)
+            np.testing.assert_array_equal(got[1][i][: len(ok)], labels[ok])
+            assert np.array_equal(got[0][i][: len(os_)].view(np.uint32), os_.astype(np.float32).view(np.uint32))
+    # rows added after Build: the buffer takes its share of the budget first
+    extra = generate_synthetic(150, d, 103)
+    new_labels = np.concatenate([np.arange(n, n + 100), np.arange(0, 50)])
+    idx.add_labels(new_labels, extra)
+    off, labels, live = idx.ivf_layout()
+    slot_labels = new_labels.tolist()
+    got = idx.search_batch(q, 120, opts)
+    with _env(PYR_DEEP_REFINE=0):
+        _bits(got, idx.search_batch(q, 120, opts))
+    with _env(PYR_FILTER_CERR="1e15"):
+        _bits(got, idx.search_batch(q, 120, opts))
+    for i in range(0, len(q), 7):
+        os_, ok = oracle.ivf_search(q[i], 120, cents, rows, off, live, buf=extra, metric=metric, nprobe=P,
+                                    max_scans=max_scans)
+        exp = np.array([slot_labels[kk - oracle.BUFKEY] if kk >= oracle.BUFKEY else labels[kk] for kk in ok], np.int64)
+        np.testing.assert_array_equal(got[1][i][: len(exp)], exp)
+        assert np.array_equal(got[0][i][: len(os_)].view(np.uint32), os_.astype(np.float32).view(np.uint32))
     idx.close()
