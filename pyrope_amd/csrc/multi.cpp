@@ -591,7 +591,6 @@ struct MultiIvfIndex : Index {
         merge(r, R.rrec_home.p, fc, k, (R.*fails).as<int32_t>() + r * (1 + fc), fc, nullptr, 0);
       });
     };
-    rerun_round(&Rank::fail_all);  // 4. the exact re-run of the first fcap failures of every home
     HIPCHK(hipSetDevice(dev[0]));
     HIPCHK(hipEventSynchronize(ev_cnt));
     int64_t mx = 0;
@@ -599,6 +598,8 @@ struct MultiIvfIndex : Index {
     const int64_t rounds = mx > fc ? (mx - 1) / fc : 0;
     last_max_fail = mx;
     last_rounds = rounds;
+    // 4. no failure anywhere (the usual step): no re-run; else the first fcap failures of every home
+    if (mx > 0) rerun_round(&Rank::fail_all);
     if (rounds > 0) {  // 5. further rounds over the rest of every home's failures
       each([&](int r) { rk[r]->fail_full.ensure(sizeof(int32_t) * W * (1 + nqh)); });
       xp->all_gather(cptrs<int32_t>(&Rank::fail_home), ptrs(&Rank::fail_full), sizeof(int32_t) * (1 + nqh));

@@ -381,9 +381,9 @@ class ListShardedIvf:
       7. every rank runs the exact scan of those failures over its lists (engine.rerun);
       8. all_to_all(re-run records) and the home merges them into its results (engine.merge_rerun).
 
-    Steps 6-8 always run with fixed buffers, so a step with at most fcap failures per home needs no host
-    decision.  The failure counts of every home arrive with step 6 on every rank; the host reads them (an
-    event on that copy, while steps 7-8 run) and, when a home has more than fcap, every rank runs the same
+    The failure counts of every home arrive with step 6 on every rank; the host reads them (an event on that
+    copy) and every rank makes the same decision: no failure anywhere (the usual step) -- steps 7-8 are
+    skipped; else steps 7-8 for the first fcap failures of every home, and when a home has more than fcap,
     further rounds: one all_gather of the whole fail lists, then per round of fcap entries steps 7-8 again.
     So every failing query is re-run exactly, whatever the data.  `stats` holds the last
     step's largest failure count and its extra rounds.  All buffers are allocated once (torch tensors on
@@ -496,15 +496,19 @@ class ListShardedIvf:
         yield ("a2a", self.rec_home.view(w * nq, -1), self.rec, "record_alltoall")
         self._phase("merge", q_all)
         yield ("gather", self.fail_all, self.fail_home[:1 + fcap], "fail_allgather")
+        # every home's failure count, the same on every rank: with none anywhere (the usual step) the re-run's
+        # phases and its all_to_all are skipped; else rounds of fcap failures per home
         self._note_counts()
-        self._phase("rerun", q_all)
-        yield ("a2a", self.rrec_home.view(w * fcap, -1), self.rrec, "rerun_alltoall")
-        self._phase("finish", q_all)
         counts = self._read_counts()
         mx = int(counts.max()) if len(counts) else 0
         extra = max(0, (mx - 1) // fcap) if mx > fcap else 0
         self.stats = {"max_failures": mx, "extra_rounds": extra}
         self.max_fail = max(self.max_fail, mx)
+        if mx == 0:
+            return
+        self._phase("rerun", q_all)
+        yield ("a2a", self.rrec_home.view(w * fcap, -1), self.rrec, "rerun_alltoall")
+        self._phase("finish", q_all)
         if extra == 0:
             return
         import torch
