@@ -517,6 +517,9 @@ def run(args):
         ids_equal = bool(np.array_equal(np.where(ck >= 0, lab_l[np.maximum(ck, 0)], -1), l_fin[:S]))
         bits_equal = bool(np.array_equal(cs.view(np.uint32), s_fin[:S].view(np.uint32)))
         cpu = {"value": S / ct_, "unit": "queries/s", "cores": threads, "kind": "port",
+               # per thread: the figure that compares box to box (the whole-host rate moves with the quota and
+               # the other tenants of the box's cores)
+               "per_thread_qps": S / ct_ / max(threads, 1),
                "sample": f"{S} of the {Q} batch queries, same index (oracle/oracle.c IVF search, one query per "
                          f"thread, {threads} threads = every CPU this process may use, {ct_:.1f}s)",
                "host": host,
