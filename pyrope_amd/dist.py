@@ -461,6 +461,10 @@ class ListShardedIvf:
         gst.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(gst):
             self(q_all)
+            # (a step without failures skips the re-run: its phases size their workspaces here, on the last
+            # step's fail lists)
+            self._phase("rerun", q_all)
+            self._phase("finish", q_all)
         gst.synchronize()
         graphs = {}
         for name in self.PHASES:

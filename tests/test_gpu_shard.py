@@ -240,3 +240,32 @@ def test_list_sharded_exact_ties_across_lists(hiplib):
     idx, _, _ = _shards(data, cents, world)
     s, lab, _ = _run(idx, torch.from_numpy(qh).cuda(), nq, k, P, opts, fcap=nq)
     _same(s, lab, ref_s, ref_l)
+
+
+def test_list_sharded_phase_graphs_capture_and_replay(hiplib):
+    """ListShardedIvf.capture (bench.py's N > 1 step): the five device phases captured into hipGraphs after a step
+    that had no failures (so the re-run's workspaces are sized outside the capture), replayed twice, equal to the
+    unsharded index; a rank of one (dist.Comm(1): the collectives as copies)."""
+    import torch
+
+    from pyrope_amd import SearchOptions, generate_synthetic, kmeans_train
+    from pyrope_amd.dist import Comm, DeviceShardEngine, ListShardedIvf
+    n, d, nl, P, k, nq = 30_000, 128, 48, 6, 10, 200
+    data = generate_synthetic(n, d, 31)
+    cents = kmeans_train(data, nl, 0, 6, 42)
+    qh = generate_synthetic(nq, d, 32)
+    opts = SearchOptions(nprobe=P)
+    _, ref_s, ref_l = _unsharded(data, cents, 0, qh, k, opts)
+    idx, _, _ = _shards(data, cents, 1)
+    q = torch.from_numpy(qh).cuda()
+    step = ListShardedIvf(DeviceShardEngine(idx[0], k, opts), Comm(1), nq, k, P, 0, 1, device="cuda")
+    step(q)
+    torch.cuda.synchronize()
+    assert step.stats["max_failures"] == 0
+    step.capture(q)
+    for _ in range(2):
+        step.out_s.fill_(0)
+        step.out_l.fill_(-7)
+        s, lab = step(q)
+        torch.cuda.synchronize()
+        _same(s.cpu().numpy(), lab.cpu().numpy(), ref_s, ref_l)
