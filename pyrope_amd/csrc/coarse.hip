@@ -354,6 +354,103 @@ __global__ __launch_bounds__(256) void coarse_approx_lds_kernel(const float *q, 
   }
 }
 
+// The same approximate scores on the bf16 matrix cores (round 6): each fp32 operand x is split into
+// hi = bf16(x) and lo = bf16(x - hi) (x - hi is exact in fp32), and q.c ~ ch.qh + cl.qh + ch.ql, three
+// v_mfma_f32_32x32x16_bf16 per 16-dim k-step (2.5 PF dense against the fp32 MFMA's ~157 TF: the launch
+// is bound by its operand loads and score stores instead of the matrix pipe).  Per element,
+// q c - (qh ch + qh cl + ql ch) = qr cr - qh dc - dq ch with qr = q - qh, dq = ql - qr (and the same for
+// c): |qr| <= 2^-8 |q|, |dq| <= 2^-8 |qr| under round-to-nearest-even (the C++ float -> __bf16
+// conversion, an IEEE fptrunc, v_cvt_pk_bf16_f32 in the default rounding mode), so the split costs
+// <= 3.02 * 2^-16 |q_i c_i|, <= 773 u |q| |c|
+// summed (u = 2^-24, Cauchy-Schwarz); the 3D products accumulate in fp32 inside the matrix core, <= 6 D u
+// |q| |c| even at 2 u per addition.  launch_coarse_mfma widens c_err by both (L2: 2 q.c against
+// (|q| + |c|)^2 >= 4 |q| |c|, so 3 D + 400; IP: 6 D + 800) on top of the fp32 kernels' constant.
+// Wave: 32 queries x 64 centroids (two 32 x 32 accumulators, A = centroid tile, B = the queries: lane
+// (r, h) ends with query r's scores of centroids 8b + 4h + i); block: 32 queries x 256 centroids.
+// The centroids come pre-split in fragment order (coarse_split_kernel, once per quantizer): tile T,
+// k-step s, lane L -> 8 bf16 at ((T * KS + s) * 64 + L) * 8, hi and lo planes, tiles padded with zeros
+// to a multiple of 8.
+typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
+typedef float f16acc __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ void split_bf16x8(const float4 a, const float4 b, bf8v &hi, bf8v &lo) {
+  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    hi[i] = (__bf16)v[i];
+    lo[i] = (__bf16)(v[i] - (float)hi[i]);
+  }
+}
+
+__global__ void coarse_split_kernel(const float *c, int nc, int D, int ntiles, bf8v *hi, bf8v *lo) {
+  const int KS = D / 16;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (T, s, lane)
+  if (e >= (int64_t)ntiles * KS * 64) return;
+  const int L = (int)(e & 63), s = (int)((e >> 6) % KS), T = (int)((e >> 6) / KS);
+  const int row = 32 * T + (L & 31), d0 = 16 * s + 8 * (L >> 5);
+  float4 a = make_float4(0.0f, 0.0f, 0.0f, 0.0f), b = a;
+  if (row < nc) {
+    a = *reinterpret_cast<const float4 *>(c + (size_t)row * D + d0);
+    b = *reinterpret_cast<const float4 *>(c + (size_t)row * D + d0 + 4);
+  }
+  split_bf16x8(a, b, hi[e], lo[e]);
+}
+
+template <int MET, int DT>
+__global__ __launch_bounds__(256) void coarse_approx_bf3_kernel(const float *q, const bf8v *chi, const bf8v *clo,
+                                                                const float *c2, int64_t nq, int nc, int Dr,
+                                                                float *out, int32_t *zero, WordFill zf) {
+  if (zero && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *zero = 0;  // the pick's failure count
+  grid_word_fill(zf);
+  const int D = DT > 0 ? DT : Dr;
+  const int KS = D / 16;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int64_t q0 = (int64_t)blockIdx.y * 32;
+  const int T0 = blockIdx.x * 8 + 2 * w;  // the wave's two centroid tiles (zero-padded past nc)
+  if (32 * T0 >= nc) return;              // no barrier in this kernel
+  const float *qp = q + (size_t)min(q0 + r, nq - 1) * D + 8 * h;
+  const bf8v *h0 = chi + (size_t)T0 * KS * 64 + lane, *l0 = clo + (size_t)T0 * KS * 64 + lane;
+  const bf8v *h1 = h0 + (size_t)KS * 64, *l1 = l0 + (size_t)KS * 64;
+  f16acc a0 = {}, a1 = {};
+  constexpr int UNS = DT > 0 ? DT / 16 : 1;
+#pragma unroll UNS
+  for (int s = 0; s < KS; ++s) {
+    bf8v qh, ql;
+    split_bf16x8(*reinterpret_cast<const float4 *>(qp + 16 * s), *reinterpret_cast<const float4 *>(qp + 16 * s + 4),
+                 qh, ql);
+    const bf8v ch0 = h0[64 * s], cl0 = l0[64 * s], ch1 = h1[64 * s], cl1 = l1[64 * s];
+    a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch0, qh, a0, 0, 0, 0);
+    a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch1, qh, a1, 0, 0, 0);
+    a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cl0, qh, a0, 0, 0, 0);
+    a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cl1, qh, a1, 0, 0, 0);
+    a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch0, ql, a0, 0, 0, 0);
+    a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch1, ql, a1, 0, 0, 0);
+  }
+  const int64_t qi = q0 + r;
+  if (qi >= nq) return;
+  float *orow = out + qi * nc;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int cb = 32 * (T0 + t) + 8 * b + 4 * h;
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float acc = t == 0 ? a0[4 * b + i] : a1[4 * b + i];
+        v[i] = MET == L2 ? 2.0f * acc - (cb + i < nc ? c2[cb + i] : 0.0f) : acc;
+      }
+      if ((nc & 3) == 0 && cb + 3 < nc) {
+        *reinterpret_cast<float4 *>(orow + cb) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (cb + i < nc) orow[cb + i] = v[i];
+      }
+    }
+  }
+}
+
 // ComputeScore (safe VectorMath form, as coarse_scores_kernel) spread over an 8-lane group: lane j runs
 // accumulator j over dims j, j + 8, ...; the group sums as hsum8 does; every lane returns the score
 template <int MET, int DT = 0>
@@ -619,9 +716,24 @@ bool coarse_mfma_supported(int nlist, int dim, int metric, int nprobe) {
          nprobe <= 64;
 }
 
+size_t coarse_split_bytes(int nlist, int dim) {
+  const int ntiles = ((nlist + 31) / 32 + 7) / 8 * 8;
+  return (size_t)2 * ntiles * (dim / 16) * 64 * 16;
+}
+
+void launch_coarse_split(const float *cents_rm, int nlist, int dim, void *split, hipStream_t st) {
+  if (nlist <= 0 || dim % 16 != 0) return;
+  const int ntiles = ((nlist + 31) / 32 + 7) / 8 * 8;
+  const int64_t n = (int64_t)ntiles * (dim / 16) * 64;
+  bf8v *hi = reinterpret_cast<bf8v *>(split);
+  hipLaunchKernelGGL(coarse_split_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, cents_rm, nlist, dim,
+                     ntiles, hi, hi + n);
+}
+
 void launch_coarse_mfma(const float *q, const float *cents_rm, const float *c2, int64_t nq, int32_t nlist,
                         int32_t dim, int32_t metric, int32_t nprobe, double cnmax, double c_err, float *scores,
-                        int32_t *fail, int32_t *nfail, int32_t *probes, hipStream_t st, const WordFill *zero) {
+                        int32_t *fail, int32_t *nfail, int32_t *probes, hipStream_t st, const WordFill *zero,
+                        const void *split) {
   if (nq <= 0 || nlist <= 0 || nprobe <= 0) {
     if (zero) launch_fill_words(*zero, st);
     return;
@@ -630,16 +742,25 @@ void launch_coarse_mfma(const float *q, const float *cents_rm, const float *c2, 
   const int P = std::min(nprobe, nlist);
   const dim3 ga((unsigned)((nlist + 31) / 32), (unsigned)((nq + 31) / 32));
   const dim3 g4((unsigned)((nq + 3) / 4));
-  // PYR_COARSE_APPROX=0: the one-wave-per-tile kernel (A/B; the same approximate scores)
+  // the bf16 split kernel when the centroids come pre-split; PYR_COARSE_APPROX=0 / 1: the fp32 one-wave-per-
+  // tile / LDS kernels (A/B; approximate scores within their own, tighter bound)
   const char *ae = knob("PYR_COARSE_APPROX");
+  const bool bf3 = split != nullptr && !ae;
   const bool lds = !(ae && atoi(ae) == 0);
+  if (bf3) c_err += metric == L2 ? 3.0 * dim + 400.0 : 6.0 * dim + 800.0;
   const dim3 gl((unsigned)((nlist + 63) / 64), (unsigned)((nq + 63) / 64));
+  const dim3 gb((unsigned)((nlist + 255) / 256), (unsigned)((nq + 31) / 32));
+  const int64_t nsplit = (int64_t)(((nlist + 31) / 32 + 7) / 8 * 8) * (dim / 16) * 64;
   auto go = [&](auto met, auto dt) {
     constexpr int M = decltype(met)::value, DT = decltype(dt)::value;
     // the approximate-score kernel also zeroes the pick's failure count (no hipMemsetAsync on a search path:
     // the memset nodes of a captured graph write stale values from their second replay on,
     // scripts/diag/graph_memset.py)
-    if (lds)
+    if (bf3) {
+      const bf8v *hi = reinterpret_cast<const bf8v *>(split);
+      hipLaunchKernelGGL((coarse_approx_bf3_kernel<M, DT>), gb, dim3(256), 0, st, q, hi, hi + nsplit, c2, nq, nlist,
+                         dim, scores, nfail, zf);
+    } else if (lds)
       hipLaunchKernelGGL((coarse_approx_lds_kernel<M>), gl, dim3(256), 0, st, q, cents_rm, c2, nq, nlist, dim, scores,
                          nfail, zf);
     else

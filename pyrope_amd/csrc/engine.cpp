@@ -1860,6 +1860,7 @@ struct Coarse {
   // the matrix-core ranking (coarse.hip launch_coarse_mfma): |c|^2 per centroid, max |c|, and whether
   // every centroid value is finite (otherwise the dense exact ranking runs)
   DevMem c2;
+  DevMem split;  // bf16 hi / lo planes in MFMA fragment order (launch_coarse_split)
   double cnmax = 0.0;
   bool cfinite = false;
 
@@ -1898,6 +1899,13 @@ struct Coarse {
       HIPCHK(hipMemcpyAsync(c2.p, n2.data(), sizeof(float) * k, hipMemcpyHostToDevice, st));
       HIPCHK(hipStreamSynchronize(st));
     }
+    // the bf16 hi / lo split of the centroids for the matrix-core approximate scores (coarse.hip)
+    if (dim % 16 == 0 && dim <= 1024 && k >= 1) {
+      split.ensure(coarse_split_bytes(k, dim));
+      launch_coarse_split(rm.as<float>(), k, dim, split.p, st);
+    } else {
+      split.release();
+    }
   }
 
   // score all centroids (ComputeScore, safe VectorMath), rank desc (ties by index), keep nprobe
@@ -1924,7 +1932,7 @@ struct Coarse {
         launch_coarse_mfma(d_q + a * cs.dim, rm.as<float>(), c2.as<float>(), n, nlist, cs.dim, met, nprobe, cnmax,
                            coarse_cerr(cs.dim), ws.cpart_s.as<float>(), ws.cfail.as<int32_t>(),
                            ws.cnfail.as<int32_t>(), ws.probes.as<int32_t>() + a * nprobe, ws.st,
-                           ws.pz_set ? &ws.pz : nullptr);
+                           ws.pz_set ? &ws.pz : nullptr, split.p);
         ws.pz_set = false;
       }
       return;

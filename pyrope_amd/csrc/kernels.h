@@ -302,10 +302,15 @@ void launch_coarse_dense(const float *q, const float *cents_rm, const float *qn,
 bool coarse_mfma_supported(int nlist, int dim, int metric, int nprobe);
 // zero: words to fill by the approximate-score launch (the search's counters; no launch of their own)
 struct WordFill;
+// split: the centroids split into bf16 hi / lo planes in MFMA fragment order (launch_coarse_split, once per
+// quantizer; coarse_split_bytes of device memory): the approximate scores then run on the bf16 matrix cores
+// (three products per k-step; c_err widened by the split's bound inside); nullptr: the fp32 MFMA kernels
 void launch_coarse_mfma(const float *q, const float *cents_rm, const float *c2, int64_t nq, int32_t nlist,
                         int32_t dim, int32_t metric, int32_t nprobe, double cnmax, double c_err, float *scores,
                         int32_t *fail, int32_t *nfail, int32_t *probes, hipStream_t st,
-                        const WordFill *zero = nullptr);
+                        const WordFill *zero = nullptr, const void *split = nullptr);
+size_t coarse_split_bytes(int nlist, int dim);
+void launch_coarse_split(const float *cents_rm, int nlist, int dim, void *split, hipStream_t st);
 
 // ---- 8-bit search mode of the FLAT index (sq8.hip; BruteForceVectorIndex EnableQuantization) ----
 struct Sq8Args {

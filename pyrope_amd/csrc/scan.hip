@@ -220,7 +220,8 @@ __global__ __launch_bounds__(256) void sample_kernel(StreamArgs a) {
 // read from the item's first one (compute without HBM), 4 (1024) = round 4's B schedule, 5 (512) = an L2
 // prefetch of the wave's next tile (4-byte LDS-DMA per line; measured slower: 0.94 vs 0.90 ms and FETCH 1.83x
 // vs 1.09x the stored bytes at I1, profiles/r4_scan), 7 (2048) = the emission without the 4-row block tests,
-// 8 (PYR_STREAM_TIMING) = per-wave cycle buckets into a.tdbg
+// 8 (PYR_STREAM_TIMING) = per-wave cycle buckets into a.tdbg, 9 (4096) = issue priority 1 for half the waves, 10 (8192) =
+// wave-private emission staging
 // SMP: the sample pass on the same kernel (round 5): chunk-0 items only, wave w scores tile w of the list
 // (SAMPLE_TILES = 16 = the waves of a block at D <= 128) against every query group, and writes per (query,
 // probe) the 2 x 16 values max(f acc + row term) + cq over its lane half's rows -- each the bound of distinct
@@ -228,6 +229,31 @@ __global__ __launch_bounds__(256) void sample_kernel(StreamArgs a) {
 // LIM: a MaxScans search (a.plim): a row at or past its (query, list) pair's bound is neither sampled nor
 // emitted (its own instantiation: the check in the default kernel's emission path cost 4 % of the I1 step,
 // 1.175 vs 1.125 ms, profiles/r5_late/maxscans_ab.log)
+// cand_flush over per-wave staging regions: wave v's rows are eb[v R, v R + nw[v])
+template <int NT, int R, class QID>
+__device__ __forceinline__ void cand_flush_waves(const StreamArgs &a, const uint2 *eb, const int *nw, int waves,
+                                                 int qcnt, int r0, int *cnt, int *base, QID qid) {
+  const int tid = threadIdx.x, tot = waves * R;
+  for (int i = tid; i < tot; i += NT)
+    if (i % R < nw[i / R]) atomicAdd(&cnt[eb[i].y >> 23], 1);
+  __syncthreads();
+  for (int i = tid; i < qcnt; i += NT) {
+    const int c = cnt[i];
+    base[i] = c > 0 ? atomicAdd(a.cand_n + qid(i), c) : 0;
+    cnt[i] = 0;
+  }
+  __syncthreads();
+  for (int i = tid; i < tot; i += NT) {
+    if (i % R >= nw[i / R]) continue;
+    const uint2 e = eb[i];
+    const int qi = (int)(e.y >> 23);
+    const int slot = base[qi] + atomicAdd(&cnt[qi], 1);
+    const int q = qid(qi);
+    if (slot < a.cap) a.cand[(size_t)q * a.cap + slot] = make_uint2(e.x, a.key_base | (uint32_t)(r0 + (int)(e.y & 0x7FFFFFu)));
+    else atomicMax(a.cand_f + q, score_key(__uint_as_float(e.x)));
+  }
+}
+
 template <int D, int MET, int AB = 0, bool SMP = false, bool LIM = false>
 __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
   constexpr int NW = nw_of(D);       // waves per block
@@ -245,6 +271,7 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
   __shared__ int cnt_l[QMAX];        // the item's staged rows per query slot (cand_flush)
   __shared__ int base_l[QMAX];       // and their run in the query's buffer
   __shared__ int item_sh, eb_n, tnext;
+  __shared__ int ebw_n[NW];          // AB 10: each wave's staged rows
   __shared__ uint32_t pf_sink[64];   // the L2 prefetch's LDS-DMA target (never read)
   // the item's emitted rows, staged in the LDS left over: (score bits, query slot << 23 | row offset)
   constexpr int EB = (163840 - (int)sizeof(bl) - QMAX * 24 - 512) / 8;
@@ -266,6 +293,10 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
     }
   };
 
+  // AB 9 (measurement only): the second half of each SIMD's waves at issue priority 1 (MI355X_MICROARCH.md,
+  // two waves per SIMD, item 4)
+  if constexpr (AB == 9)
+    if (w >= NW / 2) __builtin_amdgcn_s_setprio(1);
   for (;;) {
     if (tid == 0) item_sh = atomicAdd(a.work, 1);
     __syncthreads();
@@ -327,6 +358,10 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
     const int nt = SMP ? min((it.row_end - r0 + 31) >> 5, SAMPLE_TILES) : (it.row_end - r0 + 31) >> 5;
     const int rlim = (int)min((int64_t)it.row_end, (int64_t)a.row_limit);
     const bool stage = it.row_end - r0 < (1 << 23);  // row offsets fit the staged word
+    // AB 10 (A/B): wave-private staging -- wave w writes rows [w EBW, (w + 1) EBW) of eb, counted in a
+    // wave-uniform register (no LDS atomic and its round trip per emitting row position)
+    constexpr int EBW = EB / NW;
+    int ebc = 0;
 
     // tile t for lane (r, h): the A fragments and the row terms of rows 8b + 4h .. +3
     auto load = [&](int t, h8v (&A)[KC], f4v (&M)[4]) {
@@ -372,6 +407,22 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int e = 4 * b + i;
+          if constexpr (AB == 10) {
+            const bool p = y[e] >= thr &&
+                           (!LIM || (uint32_t)(rt + 4 * h + 8 * (e >> 2) + (e & 3)) < a.plim[it.qbeg + qi]);
+            const uint64_t m = __builtin_amdgcn_ballot_w64(p);
+            if (m == 0ull) continue;
+            const int at = ebc + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            ebc += (int)__builtin_popcountll(m);
+            if (p) {
+              const float sc = y[e] + cq;
+              const uint32_t word = base + (uint32_t)(8 * (e >> 2) + (e & 3));
+              if (stage && at < EBW) eb[w * EBW + at] = make_uint2(__float_as_uint(sc), word);
+              else put(qi, sc, r0 + (int)(word & 0x7FFFFFu));
+            }
+            continue;
+          }
           const bool p = y[e] >= thr;
           if (__builtin_amdgcn_ballot_w64(p) == 0ull) continue;
           if (p) {
@@ -546,9 +597,16 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
       t = tn;
     }
     stamp(1);
+    if constexpr (AB == 10)
+      if (lane == 0) ebw_n[w] = stage ? min(ebc, EBW) : 0;
     __syncthreads();
     stamp(2);
-    cand_flush<64 * NW>(a, eb, min(eb_n, EB), qcnt, r0, cnt_l, base_l, [&](int i) { return __float_as_int(qz[i].y); });
+    if constexpr (AB == 10) {
+      cand_flush_waves<64 * NW, EBW>(a, eb, ebw_n, NW, qcnt, r0, cnt_l, base_l,
+                                     [&](int i) { return __float_as_int(qz[i].y); });
+    } else {
+      cand_flush<64 * NW>(a, eb, min(eb_n, EB), qcnt, r0, cnt_l, base_l, [&](int i) { return __float_as_int(qz[i].y); });
+    }
     stamp(3);
   }
 }
@@ -584,6 +642,14 @@ void launch_scan_dm(const StreamArgs &a, int max_items, hipStream_t st) {
     }
     if (a.tdbg) {
       hipLaunchKernelGGL((scan_kernel<D, MET, 8>), dim3(grid), b, 0, st, a);
+      return;
+    }
+    if (a.ablate & 8192) {  // A/B: wave-private emission staging
+      hipLaunchKernelGGL((scan_kernel<D, MET, 10>), dim3(grid), b, 0, st, a);
+      return;
+    }
+    if (a.ablate & 4096) {  // A/B: issue priority 1 for waves NW/2 .. NW-1
+      hipLaunchKernelGGL((scan_kernel<D, MET, 9>), dim3(grid), b, 0, st, a);
       return;
     }
   }

@@ -175,3 +175,27 @@ def test_mfma_coarse_ranking_ties_and_duplicate_centroids(hiplib):
     got = _probe_sets(idx, qh, 24)
     np.testing.assert_array_equal(got, ref)
     assert (np.diff(got[:, :4], axis=1) == 1).all()  # the four copies of the best centroid, in index order
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+@pytest.mark.parametrize("dim", [32, 64, 768])
+def test_bf16_split_coarse_ranking_wide_magnitudes(hiplib, metric, dim):
+    """The bf16 hi / lo split approximate scores (coarse.hip coarse_approx_bf3_kernel, the default when the
+    dimension is a multiple of 16) against the dense exact ranking and the fp32 MFMA kernel
+    (PYR_COARSE_APPROX=1): signed data whose dimensions span six decades of scale (the split's lo parts
+    span as many), centroids drawn near the queries (tightly packed scores), nlist not a multiple of 32."""
+    from pyrope_amd import IvfFlatVectorIndex
+    rng = np.random.default_rng(dim + metric)
+    scale = (10.0 ** rng.uniform(-3, 3, dim)).astype(np.float32)
+    nlist = 333
+    x = (rng.standard_normal((nlist * 8, dim)) * scale).astype(np.float32)
+    cents = x[rng.choice(len(x), nlist, replace=False)].copy()
+    idx = IvfFlatVectorIndex(dim, metric, n_list=nlist)
+    idx.set_centroids(cents)
+    idx.add_labels(np.arange(len(x), dtype=np.int64), x)
+    idx.build()
+    qh = np.concatenate([(rng.standard_normal((150, dim)) * scale).astype(np.float32),
+                         (cents[rng.choice(nlist, 150)] * (1 + 1e-4 * rng.standard_normal((150, dim)))).astype(np.float32)])
+    ref = _probe_sets(idx, qh, 16, PYR_COARSE_MFMA=0)
+    np.testing.assert_array_equal(_probe_sets(idx, qh, 16), ref)
+    np.testing.assert_array_equal(_probe_sets(idx, qh, 16, PYR_COARSE_APPROX=1), ref)
