@@ -220,8 +220,8 @@ __global__ __launch_bounds__(256) void sample_kernel(StreamArgs a) {
 // read from the item's first one (compute without HBM), 4 (1024) = round 4's B schedule, 5 (512) = an L2
 // prefetch of the wave's next tile (4-byte LDS-DMA per line; measured slower: 0.94 vs 0.90 ms and FETCH 1.83x
 // vs 1.09x the stored bytes at I1, profiles/r4_scan), 7 (2048) = the emission without the 4-row block tests,
-// 8 (PYR_STREAM_TIMING) = per-wave cycle buckets into a.tdbg, 9 (4096) = issue priority 1 for half the waves, 10 (8192) =
-// wave-private emission staging
+// 8 (PYR_STREAM_TIMING) = per-wave cycle buckets into a.tdbg, 9 (4096) = issue priority 1 for half the waves, 11 (8192) =
+// round 5's emission staging (one LDS atomic per emitting row position on a block-wide counter)
 // SMP: the sample pass on the same kernel (round 5): chunk-0 items only, wave w scores tile w of the list
 // (SAMPLE_TILES = 16 = the waves of a block at D <= 128) against every query group, and writes per (query,
 // probe) the 2 x 16 values max(f acc + row term) + cq over its lane half's rows -- each the bound of distinct
@@ -271,7 +271,7 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
   __shared__ int cnt_l[QMAX];        // the item's staged rows per query slot (cand_flush)
   __shared__ int base_l[QMAX];       // and their run in the query's buffer
   __shared__ int item_sh, eb_n, tnext;
-  __shared__ int ebw_n[NW];          // AB 10: each wave's staged rows
+  __shared__ int ebw_n[NW];          // each wave's staged rows (WP)
   __shared__ uint32_t pf_sink[64];   // the L2 prefetch's LDS-DMA target (never read)
   // the item's emitted rows, staged in the LDS left over: (score bits, query slot << 23 | row offset)
   constexpr int EB = (163840 - (int)sizeof(bl) - QMAX * 24 - 512) / 8;
@@ -280,6 +280,7 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
   const uint32_t sink = (uint32_t)(size_t)(lds_void *)pf_sink;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const char *hsrc = reinterpret_cast<const char *>(a.h16);
+  constexpr bool WP = AB != 11;  // wave-private emission staging (AB 11: the block-wide counter, A/B only)
 
   // measurement only (AB 8, a.tdbg): per wave, cycles in the prologue, its tiles, the end-of-item barrier and
   // the flush; items taken
@@ -358,8 +359,9 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
     const int nt = SMP ? min((it.row_end - r0 + 31) >> 5, SAMPLE_TILES) : (it.row_end - r0 + 31) >> 5;
     const int rlim = (int)min((int64_t)it.row_end, (int64_t)a.row_limit);
     const bool stage = it.row_end - r0 < (1 << 23);  // row offsets fit the staged word
-    // AB 10 (A/B): wave-private staging -- wave w writes rows [w EBW, (w + 1) EBW) of eb, counted in a
-    // wave-uniform register (no LDS atomic and its round trip per emitting row position)
+    // wave-private staging (round 6): wave w writes rows [w EBW, (w + 1) EBW) of eb, counted in a wave-uniform
+    // register -- no LDS atomic and its round trip per emitting row position (scan 0.775 vs 0.80 ms at I1,
+    // profiles/r6_scan_ab/scan_ab_2.log); a wave whose region is full writes straight to the query's buffer
     constexpr int EBW = EB / NW;
     int ebc = 0;
 
@@ -407,7 +409,7 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int e = 4 * b + i;
-          if constexpr (AB == 10) {
+          if constexpr (WP) {
             const bool p = y[e] >= thr &&
                            (!LIM || (uint32_t)(rt + 4 * h + 8 * (e >> 2) + (e & 3)) < a.plim[it.qbeg + qi]);
             const uint64_t m = __builtin_amdgcn_ballot_w64(p);
@@ -597,11 +599,11 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
       t = tn;
     }
     stamp(1);
-    if constexpr (AB == 10)
+    if constexpr (WP)
       if (lane == 0) ebw_n[w] = stage ? min(ebc, EBW) : 0;
     __syncthreads();
     stamp(2);
-    if constexpr (AB == 10) {
+    if constexpr (WP) {
       cand_flush_waves<64 * NW, EBW>(a, eb, ebw_n, NW, qcnt, r0, cnt_l, base_l,
                                      [&](int i) { return __float_as_int(qz[i].y); });
     } else {
@@ -644,8 +646,8 @@ void launch_scan_dm(const StreamArgs &a, int max_items, hipStream_t st) {
       hipLaunchKernelGGL((scan_kernel<D, MET, 8>), dim3(grid), b, 0, st, a);
       return;
     }
-    if (a.ablate & 8192) {  // A/B: wave-private emission staging
-      hipLaunchKernelGGL((scan_kernel<D, MET, 10>), dim3(grid), b, 0, st, a);
+    if (a.ablate & 8192) {  // A/B: round 5's block-wide emission counter
+      hipLaunchKernelGGL((scan_kernel<D, MET, 11>), dim3(grid), b, 0, st, a);
       return;
     }
     if (a.ablate & 4096) {  // A/B: issue priority 1 for waves NW/2 .. NW-1
