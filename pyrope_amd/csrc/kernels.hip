@@ -659,16 +659,23 @@ __global__ void ivf_count_kernel(const int32_t *probes, int64_t nq, int nprobe, 
 // atomic and places entries by their LDS rank.  320k entries into 1,024 lists: ~80k global atomics
 // instead of 320k on 1,024 addresses.  (Entry order inside a list differs from the one-atomic-per-
 // entry pass; it is arbitrary in both, and results do not depend on it.)
-constexpr int IVF_LDS_BINS = 16384, IVF_EPT = 4, IVF_EPB = 256 * IVF_EPT;  // (EPT 16 left 79 blocks at I1)
+// EPT entries per thread: 4 (EPT 16 left 79 blocks at I1), 16 from 2M entries on (a list-sharded rank's N x
+// batch: 2.56M entries at the N = 8 shape, most of them dropped, where 4 per thread spent the launch clearing
+// and scanning 2,500 blocks' histograms)
+constexpr int IVF_LDS_BINS = 16384;
+inline int ivf_ept(int64_t n) { return n >= (int64_t)2 << 20 ? 16 : 4; }
 
+template <int IVF_EPT>
 __global__ __launch_bounds__(256) void ivf_count_lds_kernel(const int32_t *probes, int64_t nq, int nprobe, int pb,
                                                             int pe, int nlist, int32_t *cnt, const int32_t *lb,
                                                             const int32_t *le) {
   extern __shared__ int hist[];
+  constexpr int IVF_EPB = 256 * IVF_EPT;
   const int np = pe - pb;
   const int64_t n = nq * np, e0 = (int64_t)blockIdx.x * IVF_EPB;
   for (int i = threadIdx.x; i < nlist; i += 256) hist[i] = 0;
   __syncthreads();
+#pragma unroll 4
   for (int j = 0; j < IVF_EPT; ++j) {
     const int64_t i = e0 + j * 256 + threadIdx.x;
     if (i < n) {
@@ -681,11 +688,13 @@ __global__ __launch_bounds__(256) void ivf_count_lds_kernel(const int32_t *probe
     if (hist[i]) atomicAdd(&cnt[i], hist[i]);
 }
 
+template <int IVF_EPT>
 __global__ __launch_bounds__(256) void ivf_fill_lds_kernel(const int32_t *probes, int64_t nq, int nprobe, int pb,
                                                            int pe, int nparts, int cmax, int nlist,
                                                            const int32_t *qoff, int32_t *fill, int32_t *qlist,
                                                            int32_t *qpos, const int32_t *lb, const int32_t *le) {
   extern __shared__ int hist[];
+  constexpr int IVF_EPB = 256 * IVF_EPT;
   const int np = pe - pb;
   const int64_t n = nq * np, e0 = (int64_t)blockIdx.x * IVF_EPB;
   for (int i = threadIdx.x; i < nlist; i += 256) hist[i] = 0;
@@ -1787,8 +1796,11 @@ void launch_ivf_items(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t
       z.add(ws.fill, nlist, 0);
       launch_fill_words(z, st);
     }
-    if (n > 0 && lds)
-      hipLaunchKernelGGL(ivf_count_lds_kernel, dim3(nblk(n, IVF_EPB)), dim3(256), hb, st, probes, nq, nprobe, pb, pe,
+    if (n > 0 && lds && ivf_ept(n) == 16)
+      hipLaunchKernelGGL(ivf_count_lds_kernel<16>, dim3(nblk(n, 256 * 16)), dim3(256), hb, st, probes, nq, nprobe, pb,
+                         pe, nlist, ws.cnt, skb, ske);
+    else if (n > 0 && lds)
+      hipLaunchKernelGGL(ivf_count_lds_kernel<4>, dim3(nblk(n, 256 * 4)), dim3(256), hb, st, probes, nq, nprobe, pb, pe,
                          nlist, ws.cnt, skb, ske);
     else if (n > 0)
       hipLaunchKernelGGL(ivf_count_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, probes, nq, nprobe, pb, pe, ws.cnt, skb,
@@ -1796,8 +1808,12 @@ void launch_ivf_items(const int32_t *probes, int64_t nq, int32_t nprobe, int32_t
   }
   hipLaunchKernelGGL(ivf_scan_kernel, dim3(1), dim3(1024), 0, st, ws.cnt, nlist, qchunk, list_begin, list_end, ch,
                      phase, ws.qoff, ws.ioff, ws.n_items, balance ? 1 : 0, ws.items);
-  if (phase == 0 && n > 0 && lds)
-    hipLaunchKernelGGL(ivf_fill_lds_kernel, dim3(nblk(n, IVF_EPB)), dim3(256), hb, st, probes, nq, nprobe, pb, pe,
+  if (phase == 0 && n > 0 && lds && ivf_ept(n) == 16)
+    hipLaunchKernelGGL(ivf_fill_lds_kernel<16>, dim3(nblk(n, 256 * 16)), dim3(256), hb, st, probes, nq, nprobe, pb, pe,
+                       nparts, ch.cmax, nlist, ws.qoff, ws.fill, ws.qlist, pb == 0 && pe == nprobe ? ws.qpos : nullptr,
+                       skb, ske);
+  else if (phase == 0 && n > 0 && lds)
+    hipLaunchKernelGGL(ivf_fill_lds_kernel<4>, dim3(nblk(n, 256 * 4)), dim3(256), hb, st, probes, nq, nprobe, pb, pe,
                        nparts, ch.cmax, nlist, ws.qoff, ws.fill, ws.qlist, pb == 0 && pe == nprobe ? ws.qpos : nullptr,
                        skb, ske);
   else if (phase == 0 && n > 0)
