@@ -366,9 +366,9 @@ __global__ __launch_bounds__(256) void coarse_approx_lds_kernel(const float *q, 
 // |q| |c| even at 2 u per addition.  launch_coarse_mfma widens c_err by both (L2: 2 q.c against
 // (|q| + |c|)^2 >= 4 |q| |c|, so 3 D + 400; IP: 6 D + 800) on top of the fp32 kernels' constant.
 // Wave: 32 queries x 64 centroids (two 32 x 32 accumulators, A = centroid tile, B = the queries: lane
-// (r, h) ends with query r's scores of centroids 8b + 4h + i); block: 128 queries x the same 64 centroids,
-// whose fragments are staged in LDS 8 k-steps at a time (each centroid fragment crosses L2 once per 128
-// queries, not per 32).
+// (r, h) ends with query r's scores of centroids 8b + 4h + i); block: 8 waves, 256 queries x the same 64
+// centroids, whose fragments are staged in LDS 8 k-steps at a time (each centroid fragment crosses L2 once per
+// 256 queries, not per 32; I1's 10,000 x 1,024 fit one round of resident blocks).
 // The centroids come pre-split in fragment order (coarse_split_kernel, once per quantizer): tile T,
 // k-step s, lane L -> 8 bf16 at ((T * KS + s) * 64 + L) * 8, hi and lo planes, tiles padded with zeros
 // to a multiple of 8.
@@ -399,7 +399,7 @@ __global__ void coarse_split_kernel(const float *c, int nc, int D, int ntiles, b
 }
 
 template <int MET, int DT>
-__global__ __launch_bounds__(256) void coarse_approx_bf3_kernel(const float *q, const bf8v *chi, const bf8v *clo,
+__global__ __launch_bounds__(512) void coarse_approx_bf3_kernel(const float *q, const bf8v *chi, const bf8v *clo,
                                                                 const float *c2, int64_t nq, int nc, int Dr,
                                                                 float *out, int32_t *zero, WordFill zf) {
   __shared__ bf8v cs[2][2][8][64];  // [hi / lo][tile][k-step of the chunk][lane]: 32 KB
@@ -408,14 +408,22 @@ __global__ __launch_bounds__(256) void coarse_approx_bf3_kernel(const float *q, 
   const int D = DT > 0 ? DT : Dr;
   const int KS = D / 16;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  const int64_t q0 = (int64_t)blockIdx.y * 128 + 32 * w;  // the wave's 32 queries
+  const int64_t q0 = (int64_t)blockIdx.y * 256 + 32 * w;  // the wave's 32 queries
   const int T0 = 2 * blockIdx.x;                          // the block's two centroid tiles (zero-padded past nc)
   const float *qp = q + (size_t)min(q0 + r, nq - 1) * D + 8 * h;
   f16acc a0 = {}, a1 = {};
   for (int s0 = 0; s0 < KS; s0 += 8) {
     const int kc = min(8, KS - s0);
+    // the chunk's query fragments first: their HBM latency overlaps the centroid staging below
+    float4 qv[8][2];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      if (s >= kc) break;  // (block-uniform)
+      qv[s][0] = *reinterpret_cast<const float4 *>(qp + 16 * (s0 + s));
+      qv[s][1] = *reinterpret_cast<const float4 *>(qp + 16 * (s0 + s) + 4);
+    }
     __syncthreads();  // the previous chunk is consumed
-    for (int i = threadIdx.x; i < 4 * kc * 64; i += 256) {  // the two tiles' fragments, both planes
+    for (int i = threadIdx.x; i < 4 * kc * 64; i += 512) {  // the two tiles' fragments, both planes
       const int L = i & 63, u = i >> 6, s = u % kc, t = (u / kc) & 1, pl = u / kc >> 1;
       cs[pl][t][s][L] = (pl ? clo : chi)[((size_t)(T0 + t) * KS + s0 + s) * 64 + L];
     }
@@ -423,9 +431,8 @@ __global__ __launch_bounds__(256) void coarse_approx_bf3_kernel(const float *q, 
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       if (s >= kc) break;  // (block-uniform)
-      const int d = 16 * (s0 + s);
       bf8v qh, ql;
-      split_bf16x8(*reinterpret_cast<const float4 *>(qp + d), *reinterpret_cast<const float4 *>(qp + d + 4), qh, ql);
+      split_bf16x8(qv[s][0], qv[s][1], qh, ql);
       const bf8v ch0 = cs[0][0][s][lane], ch1 = cs[0][1][s][lane], cl0 = cs[1][0][s][lane], cl1 = cs[1][1][s][lane];
       a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch0, qh, a0, 0, 0, 0);
       a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch1, qh, a1, 0, 0, 0);
@@ -758,7 +765,7 @@ void launch_coarse_mfma(const float *q, const float *cents_rm, const float *c2, 
   const bool lds = !(ae && atoi(ae) == 0);
   if (bf3) c_err += metric == L2 ? 3.0 * dim + 400.0 : 6.0 * dim + 800.0;
   const dim3 gl((unsigned)((nlist + 63) / 64), (unsigned)((nq + 63) / 64));
-  const dim3 gb((unsigned)((nlist + 63) / 64), (unsigned)((nq + 127) / 128));
+  const dim3 gb((unsigned)((nlist + 63) / 64), (unsigned)((nq + 255) / 256));
   const int64_t nsplit = (int64_t)(((nlist + 31) / 32 + 7) / 8 * 8) * (dim / 16) * 64;
   auto go = [&](auto met, auto dt) {
     constexpr int M = decltype(met)::value, DT = decltype(dt)::value;
@@ -767,7 +774,7 @@ void launch_coarse_mfma(const float *q, const float *cents_rm, const float *c2, 
     // scripts/diag/graph_memset.py)
     if (bf3) {
       const bf8v *hi = reinterpret_cast<const bf8v *>(split);
-      hipLaunchKernelGGL((coarse_approx_bf3_kernel<M, DT>), gb, dim3(256), 0, st, q, hi, hi + nsplit, c2, nq, nlist,
+      hipLaunchKernelGGL((coarse_approx_bf3_kernel<M, DT>), gb, dim3(512), 0, st, q, hi, hi + nsplit, c2, nq, nlist,
                          dim, scores, nfail, zf);
     } else if (lds)
       hipLaunchKernelGGL((coarse_approx_lds_kernel<M>), gl, dim3(256), 0, st, q, cents_rm, c2, nq, nlist, dim, scores,

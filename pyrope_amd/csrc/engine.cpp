@@ -2651,6 +2651,10 @@ struct IvfFlatIndex : Index {
     stream_ub_terms(dt, met, filter_f16_cerr(dt, met, prec), filter_cerr(dt), filter_f16_abs(dt, met, lists.sx, prec),
                     sa);
     sa.mub = lists.row_terms(met, sa.kr, sa.kx, ws.st);
+    sa.lioff = ws.ivf_ioff.as<int32_t>();  // the sample pass by list (scan.hip SMP)
+    sa.lcnt = ws.ivf_cnt.as<int32_t>();
+    sa.nlist = coarse.nlist;
+    sa.lqchunk = qmax;
     const bool timing = knob("PYR_STREAM_TIMING") != nullptr;  // measurement only (syncs)
     if (timing) {
       ws.tdbg.ensure(sizeof(unsigned long long) * 8);
@@ -3076,6 +3080,10 @@ struct IvfFlatIndex : Index {
       stream_ub_terms(dt, metric, filter_f16_cerr(dt, metric, FILTER_F16X1), filter_cerr(dt),
                       filter_f16_abs(dt, metric, s.sx, FILTER_F16X1), sa);
       sa.mub = s.row_terms(metric, sa.kr, sa.kx, ws.st);
+      sa.lioff = ws.ivf_ioff.as<int32_t>();  // the sample pass by list (scan.hip SMP)
+      sa.lcnt = ws.ivf_cnt.as<int32_t>();
+      sa.nlist = coarse.nlist;
+      sa.lqchunk = scan_qmax(dt);
       if (budget) {  // the pairs' budgets, and the sample pass bounded as the unsharded LIM sample is
         ws.shp.ensure(sizeof(int32_t) * npos);
         ws.limits.ensure(sizeof(uint32_t) * npos);

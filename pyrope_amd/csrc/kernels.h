@@ -403,6 +403,10 @@ struct StreamArgs {
   // that (query, list) pair's scanned rows (launch_pos_limits); a row at or past it is neither sampled nor
   // emitted
   const uint32_t *plim;
+  // the sample pass by list (scan.hip SMP), or null (then every item is drawn and non-chunk-0 ones skipped):
+  // list l's chunk-0 items are lioff[l] .. lioff[l] + ceil(lcnt[l] / lqchunk) - 1 (ivf_list_items' order)
+  const int32_t *lioff, *lcnt;
+  int32_t nlist, lqchunk;
 };
 // per row the stream scan's additive term: meta + kr |x - c|^2 (+ kx |x|^2, IP): fmaf(kr, rsq16, meta),
 // then fmaf(kx, rsq, .)

@@ -271,6 +271,7 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
   __shared__ int cnt_l[QMAX];        // the item's staged rows per query slot (cand_flush)
   __shared__ int base_l[QMAX];       // and their run in the query's buffer
   __shared__ int item_sh, eb_n, tnext;
+  __shared__ ScanItem it_sh;         // the block's next item, fetched by thread 0 ahead of the end barrier
   __shared__ int ebw_n[NW];          // each wave's staged rows (WP)
   __shared__ uint32_t pf_sink[64];   // the L2 prefetch's LDS-DMA target (never read)
   // the item's emitted rows, staged in the LDS left over: (score bits, query slot << 23 | row offset)
@@ -298,19 +299,55 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
   // two waves per SIMD, item 4)
   if constexpr (AB == 9)
     if (w >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  // Thread 0 takes the block's next item (the atomic and the item's load) while the other waves finish their
+  // tiles, so the round trips sit inside the end-of-item barrier instead of before each prologue (round 6).
+  // The sample pass (a.lioff) takes LISTS from its counter and walks each list's chunk-0 items
+  // (lioff[l] .. + ceil(lcnt[l] / lqchunk)), instead of drawing and skipping the other chunks' items.
+  const int nit = *a.n_items;
+  int sm_l = 0, sm_g = 0, sm_ng = 0;  // (thread 0: the sample pass's current list)
+  auto fetch = [&]() {
+    int nx;
+    if (SMP && a.lioff) {
+      if (sm_g < sm_ng) {
+        nx = a.lioff[sm_l] + sm_g++;
+      } else {
+        nx = nit;
+        for (;;) {
+          const int l = atomicAdd(a.work, 1);
+          if (l >= a.nlist) break;
+          const int c = a.lcnt[l];
+          if (c > 0) {
+            sm_l = l;
+            sm_ng = (c + a.lqchunk - 1) / a.lqchunk;
+            sm_g = 1;
+            nx = a.lioff[l];
+            break;
+          }
+        }
+      }
+    } else {
+      nx = atomicAdd(a.work, 1);
+    }
+    item_sh = nx;
+    if (nx < nit) it_sh = a.items[nx];
+  };
+  if (tid == 0) fetch();
+  __syncthreads();
   for (;;) {
-    if (tid == 0) item_sh = atomicAdd(a.work, 1);
-    __syncthreads();
-    const int item = item_sh;
-    __syncthreads();  // every thread has read item_sh before thread 0 may rewrite it
-    if (item >= *a.n_items) {
+    const int item = item_sh;  // (rewritten by thread 0 only after this item's prologue barrier)
+    if (item >= nit) {
       if constexpr (AB == 8)
         if (lane == 0)
           for (int b = 0; b < 5; ++b) atomicAdd(a.tdbg + b, (unsigned long long)tb[b]);
       return;
     }
-    const ScanItem it = a.items[item];
-    if (SMP && it.part != 0) continue;  // (block-uniform) chunk-0 items cover every (list, query) pair once
+    const ScanItem it = it_sh;
+    if (SMP && it.part != 0) {  // (block-uniform) chunk-0 items cover every (list, query) pair once
+      __syncthreads();  // every thread has read the item before thread 0 replaces it
+      if (tid == 0) fetch();
+      __syncthreads();
+      continue;
+    }
     stamp(-1);
     if constexpr (AB == 8) tb[4] += 1;
     const int qcnt = it.qcnt, ng = (qcnt + 31) >> 5;
@@ -581,6 +618,7 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
         const int qi = 32 * j + r;
         if (qi < qcnt) a.samp[(size_t)__float_as_int(qz[qi].y) * SV + 2 * w + h] = smx[j] + qz[qi].x;
       }
+      if (tid == 0) fetch();
       __syncthreads();  // every wave is done with the item's LDS before the next prologue
       continue;
     }
@@ -601,6 +639,7 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
     stamp(1);
     if constexpr (WP)
       if (lane == 0) ebw_n[w] = stage ? min(ebc, EBW) : 0;
+    if (tid == 0) fetch();  // the next item, inside the end barrier's wait
     __syncthreads();
     stamp(2);
     if constexpr (WP) {
