@@ -270,8 +270,11 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
   __shared__ float2 qz[QMAX];        // {cq (score = y + cq), the query as int bits}
   __shared__ int cnt_l[QMAX];        // the item's staged rows per query slot (cand_flush)
   __shared__ int base_l[QMAX];       // and their run in the query's buffer
-  __shared__ int item_sh, eb_n, tnext;
-  __shared__ ScanItem it_sh;         // the block's next item, fetched by thread 0 ahead of the end barrier
+  __shared__ int eb_n, tnext;
+  // the block's items, double-buffered: thread 0 writes the NEXT one (slot par ^ 1) while the block still works on
+  // slot par, so no thread can ever read a half-replaced item (or re-read the current one after the switch)
+  __shared__ int item_buf[2];
+  __shared__ ScanItem it_buf[2];
   __shared__ int ebw_n[NW];          // each wave's staged rows (WP)
   __shared__ uint32_t pf_sink[64];   // the L2 prefetch's LDS-DMA target (never read)
   // the item's emitted rows, staged in the LDS left over: (score bits, query slot << 23 | row offset)
@@ -305,7 +308,8 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
   // (lioff[l] .. + ceil(lcnt[l] / lqchunk)), instead of drawing and skipping the other chunks' items.
   const int nit = *a.n_items;
   int sm_l = 0, sm_g = 0, sm_ng = 0;  // (thread 0: the sample pass's current list)
-  auto fetch = [&]() {
+  int par = 0;  // (block-uniform) the current item's slot
+  auto fetch = [&](int slot) {
     int nx;
     if (SMP && a.lioff) {
       if (sm_g < sm_ng) {
@@ -328,23 +332,26 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
     } else {
       nx = atomicAdd(a.work, 1);
     }
-    item_sh = nx;
-    if (nx < nit) it_sh = a.items[nx];
+    item_buf[slot] = nx;
+    if (nx < nit) it_buf[slot] = a.items[nx];
   };
-  if (tid == 0) fetch();
+  if (tid == 0) fetch(0);
   __syncthreads();
   for (;;) {
-    const int item = item_sh;  // (rewritten by thread 0 only after this item's prologue barrier)
+    const int item = item_buf[par];
     if (item >= nit) {
       if constexpr (AB == 8)
         if (lane == 0)
           for (int b = 0; b < 5; ++b) atomicAdd(a.tdbg + b, (unsigned long long)tb[b]);
       return;
     }
-    const ScanItem it = it_sh;
+    // (the compiler may re-read these fields from it_buf[par] at any later point of the item, the flush included:
+    // slot par is not rewritten before the NEXT item's fetch -- with one buffer, rewritten by the fetch ahead of the
+    // end barrier, such re-reads picked up the next item's rows and misplaced the flushed candidates)
+    const ScanItem it = it_buf[par];
     if (SMP && it.part != 0) {  // (block-uniform) chunk-0 items cover every (list, query) pair once
-      __syncthreads();  // every thread has read the item before thread 0 replaces it
-      if (tid == 0) fetch();
+      if (tid == 0) fetch(par ^ 1);
+      par ^= 1;
       __syncthreads();
       continue;
     }
@@ -618,7 +625,8 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
         const int qi = 32 * j + r;
         if (qi < qcnt) a.samp[(size_t)__float_as_int(qz[qi].y) * SV + 2 * w + h] = smx[j] + qz[qi].x;
       }
-      if (tid == 0) fetch();
+      if (tid == 0) fetch(par ^ 1);
+      par ^= 1;
       __syncthreads();  // every wave is done with the item's LDS before the next prologue
       continue;
     }
@@ -639,7 +647,8 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
     stamp(1);
     if constexpr (WP)
       if (lane == 0) ebw_n[w] = stage ? min(ebc, EBW) : 0;
-    if (tid == 0) fetch();  // the next item, inside the end barrier's wait
+    if (tid == 0) fetch(par ^ 1);  // the next item, inside the end barrier's wait
+    par ^= 1;
     __syncthreads();
     stamp(2);
     if constexpr (WP) {
@@ -648,6 +657,10 @@ __global__ __launch_bounds__(64 * nw_of(D), 1) void scan_kernel(StreamArgs a) {
     } else {
       cand_flush<64 * NW>(a, eb, min(eb_n, EB), qcnt, r0, cnt_l, base_l, [&](int i) { return __float_as_int(qz[i].y); });
     }
+    // every wave has placed its rows (the flush reads qz / cnt_l / base_l of this item) before any wave's next
+    // prologue rewrites them: with the next item fetched ahead of the end barrier, the loop top no longer holds the
+    // barrier that used to separate the two (a wave that ran ahead misplaced a slower wave's rows)
+    __syncthreads();
     stamp(3);
   }
 }

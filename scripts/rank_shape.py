@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--train-rows", type=int, default=10_000_000)
     ap.add_argument("--parity", type=int, default=1, help="compare every home's answers with the unsharded index")
     ap.add_argument("--oracle", type=int, default=0, help="queries per home compared with the CPU oracle")
+    ap.add_argument("--determinism", type=int, default=0, help="repeat the unsharded search, the probe ranking and "
+                    "the sharded step, and compare (diagnostics)")
     args = ap.parse_args()
 
     import torch
@@ -77,9 +79,22 @@ def main():
     Q = W * nq
     qh = generate_synthetic(Q, D, 1337)
     ref = None
+    det = {}
     if args.parity:
         full = index_of(np.arange(args.n, dtype=np.int64))
         ref = full.search_batch(qh, k, opts)
+        if args.determinism:  # the unsharded answers and probe lists, twice (diagnostics)
+            ref2 = full.search_batch(qh, k, opts)
+            det["unsharded_repeat_equal"] = bool(np.array_equal(ref[1], ref2[1]) and
+                                                 np.array_equal(ref[0].view(np.uint32), ref2[0].view(np.uint32)))
+            pr = torch.empty((Q, min(args.nprobe, len(cents))), dtype=torch.int32, device="cuda")
+            qd = torch.from_numpy(qh).cuda()
+            full.probe_device(qd.data_ptr(), Q, pr.data_ptr(), 0, opts)
+            torch.cuda.synchronize()
+            full_probes = pr.cpu().numpy().copy()
+            full.probe_device(qd.data_ptr(), Q, pr.data_ptr(), 0, opts)
+            torch.cuda.synchronize()
+            det["probe_repeat_equal"] = bool(np.array_equal(full_probes, pr.cpu().numpy()))
         full.close()
     orc = None
     if args.oracle:  # the oracle's list-major rows (stable by label, the index's storage order) and its answers
@@ -147,8 +162,44 @@ def main():
 
     full_step()
     torch.cuda.synchronize()
+    if args.determinism and args.parity:
+        P0 = min(args.nprobe, len(cents))
+        hp = plans[:, :P0].cpu().numpy()
+        det["plan_probes_equal_unsharded"] = bool(np.array_equal(np.sort(hp, 1), np.sort(full_probes, 1)))
+        det["plan_probes_differing_queries"] = int((np.sort(hp, 1) != np.sort(full_probes, 1)).any(1).sum())
+        s1, l1 = out_s.cpu().numpy().copy(), out_l.cpu().numpy().copy()
+        plan1 = plans.cpu().numpy().copy()
+        recs1 = [r_.cpu().numpy().copy() for r_ in recs]
+        fails1 = fails.cpu().numpy().copy()
+        full_step()
+        torch.cuda.synchronize()
+        det["sharded_repeat_equal"] = bool(np.array_equal(l1, out_l.cpu().numpy()) and
+                                           np.array_equal(s1.view(np.uint32), out_s.cpu().numpy().view(np.uint32)))
+        hp2 = plans[:, :P0].cpu().numpy()
+        det["plan_repeat_equal"] = bool(np.array_equal(hp, hp2))
+        plan2 = plans.cpu().numpy()
+        det["plan_thr_repeat_equal"] = bool(np.array_equal(plan1.view(np.uint32), plan2.view(np.uint32)))
+        det["plan_thr_nan"] = int(np.isnan(plan1[:, P0].view(np.float32)).sum())
+        rdiff = [int((recs1[r_] != recs[r_].cpu().numpy()).any(1).sum()) for r_ in range(W)]
+        det["record_rows_differing_per_rank"] = rdiff
+        det["fails_repeat_equal"] = bool(np.array_equal(fails1, fails.cpu().numpy()))
+        bad = np.nonzero((l1 != out_l.cpu().numpy()).any(1))[0]
+        if len(bad):
+            b = int(bad[0])
+            dr = [r_ for r_ in range(W) if (recs1[r_][b] != recs[r_][b].cpu().numpy()).any()]
+
+            def dec(raw):  # k ShardEntry {int64 label, float score, int32 list} + trailer {float bound, int32 n}
+                ent = [(int(raw[16 * i:16 * i + 8].view(np.int64)[0]), float(raw[16 * i + 8:16 * i + 12].view(np.float32)[0]),
+                        int(raw[16 * i + 12:16 * i + 16].view(np.int32)[0])) for i in range(k)]
+                tr = (float(raw[16 * k:16 * k + 4].view(np.float32)[0]), int(raw[16 * k + 4:16 * k + 8].view(np.int32)[0]))
+                return {"ent": ent, "trailer": tr}
+            det["first_differing"] = {"q": b, "l1": l1[b].tolist(), "l2": out_l.cpu().numpy()[b].tolist(),
+                                      "recs_differ_on_ranks": dr,
+                                      "rec1": [dec(recs1[r_][b]) for r_ in dr], "rec2": [dec(recs[r_][b].cpu().numpy()) for r_ in dr]}
+        out_s.copy_(torch.from_numpy(s1))
+        out_l.copy_(torch.from_numpy(l1))
     per = np.bincount(owner[plans[:, :P].cpu().numpy().ravel()], minlength=W)
-    res = {"world": W, "rank": R, "rows": int(rows[R]), "lists": int((owner == R).sum()), "queries_all": Q,
+    res = {"determinism": det, "world": W, "rank": R, "rows": int(rows[R]), "lists": int((owner == R).sum()), "queries_all": Q,
            "queries_home": nq, "nprobe": P, "failures_per_home": fails[:, 0].cpu().tolist(),
            "pairs_per_rank": per.tolist(), "pairs_max_over_mean": round(float(per.max() / per.mean()), 4),
            "rows_per_rank": rows.astype(np.int64).tolist()}
@@ -156,6 +207,13 @@ def main():
         s_, l_ = out_s.cpu().numpy(), out_l.cpu().numpy()
         res["parity"] = {"queries": Q, "ids_equal": bool(np.array_equal(l_, ref[1])),
                          "scores_bit_identical": bool(np.array_equal(s_.view(np.uint32), ref[0].view(np.uint32)))}
+        bad = np.nonzero((l_ != ref[1]).any(1) | (s_.view(np.uint32) != ref[0].view(np.uint32)).any(1))[0]
+        if len(bad):  # which queries differ, and whether their home listed them as certificate failures
+            fl = fails.cpu().numpy()
+            failed = {h * nq + int(i) for h in range(W) for i in fl[h, 1:1 + min(int(fl[h, 0]), F)]}
+            res["parity"]["differing"] = [{"q": int(b), "home": int(b // nq), "failed": int(b) in failed,
+                                           "got": l_[b].tolist(), "ref": ref[1][b].tolist()} for b in bad[:4]]
+            res["parity"]["n_differing"] = int(len(bad))
     if orc is not None:
         s_, l_ = out_s.cpu().numpy(), out_l.cpu().numpy()
         ok = [bool(np.array_equal(l_[i][:len(kk)], kk) and np.array_equal(s_[i][:len(ss)].view(np.uint32), ss.view(np.uint32)))

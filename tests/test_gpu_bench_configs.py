@@ -199,3 +199,17 @@ def test_bf16_split_coarse_ranking_wide_magnitudes(hiplib, metric, dim):
     ref = _probe_sets(idx, qh, 16, PYR_COARSE_MFMA=0)
     np.testing.assert_array_equal(_probe_sets(idx, qh, 16), ref)
     np.testing.assert_array_equal(_probe_sets(idx, qh, 16, PYR_COARSE_APPROX=1), ref)
+
+
+def test_work_lists_sixteen_entries_per_thread(hiplib):
+    """A batch of >= 2M (query, probe) entries takes the 16-entries-per-thread work-list kernels
+    (kernels.hip ivf_ept; a list-sharded rank's N x batch): 65,536 queries x nprobe 32 on a small index, against
+    the exact VALU path."""
+    from pyrope_amd import SearchOptions, generate_synthetic
+    idx, _ = _ivf(256, 40, 0)
+    q = generate_synthetic(65_536, 128, 2024)
+    opts = SearchOptions(nprobe=32)
+    got = idx.search_batch(q, 10, opts)
+    with _env(PYR_FILTER=0):
+        ref = idx.search_batch(q, 10, opts)
+    _same(got, ref)
