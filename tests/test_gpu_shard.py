@@ -269,3 +269,24 @@ def test_list_sharded_phase_graphs_capture_and_replay(hiplib):
         s, lab = step(q)
         torch.cuda.synchronize()
         _same(s.cpu().numpy(), lab.cpu().numpy(), ref_s, ref_l)
+
+
+def test_list_sharded_repeatable_large_items(hiplib):
+    """Full 512-query items with many emitted rows per item on every rank (long lists, a low fixed sample rank):
+    three steps in a row, each equal to the unsharded index.  Round 6's flush / next-prologue race (fixed,
+    profiles/r6_race/) showed at this kind of shape as answers that changed from step to step."""
+    import torch
+
+    from pyrope_amd import SearchOptions, generate_synthetic, kmeans_train
+    n, d, nl, P, k, nq, world = 200_000, 64, 32, 8, 10, 2000, 4
+    data = generate_synthetic(n, d, 31)
+    cents = kmeans_train(data, nl, 0, 4, 42)
+    qh = generate_synthetic(nq * world, d, 32)
+    opts = SearchOptions(nprobe=P)
+    _, ref_s, ref_l = _unsharded(data, cents, 0, qh, k, opts)
+    idx, _, _ = _shards(data, cents, world)
+    q = torch.from_numpy(qh).cuda()
+    with _env(PYR_STREAM_RANK=48):
+        for _ in range(3):
+            s, lab, _ = _run(idx, q, nq, k, P, opts, fcap=256)
+            _same(s, lab, ref_s, ref_l)
