@@ -372,6 +372,7 @@ __global__ __launch_bounds__(256) void coarse_approx_lds_kernel(const float *q, 
 // The centroids come pre-split in fragment order (coarse_split_kernel, once per quantizer): tile T,
 // k-step s, lane L -> 8 bf16 at ((T * KS + s) * 64 + L) * 8, hi and lo planes, tiles padded with zeros
 // to a multiple of 8.
+constexpr int COARSE_BF3_MAX_DIM = 256;
 typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
 typedef float f16acc __attribute__((ext_vector_type(16)));
 
@@ -732,6 +733,11 @@ bool coarse_mfma_supported(int nlist, int dim, int metric, int nprobe) {
          nprobe <= 64;
 }
 
+// the bf16 split kernel up to this dimension: its wider bound (3 D + 400 on top of 4 D + 64) lets more centroids
+// into the pick's exact band, which P1 (d = 768, nlist 4,096) paid for: coarse 4.66 vs 2.90 ms with the fp32 kernel
+// (profiles/r6_p1/p1_bf3.log); at d = 128 the split kernel wins (I1 coarse 0.075 vs 0.086-0.092 ms)
+int coarse_bf3_max_dim() { return COARSE_BF3_MAX_DIM; }
+
 size_t coarse_split_bytes(int nlist, int dim) {
   const int ntiles = ((nlist + 31) / 32 + 7) / 8 * 8;
   return (size_t)2 * ntiles * (dim / 16) * 64 * 16;
@@ -761,7 +767,7 @@ void launch_coarse_mfma(const float *q, const float *cents_rm, const float *c2, 
   // the bf16 split kernel when the centroids come pre-split; PYR_COARSE_APPROX=0 / 1: the fp32 one-wave-per-
   // tile / LDS kernels (A/B; approximate scores within their own, tighter bound)
   const char *ae = knob("PYR_COARSE_APPROX");
-  const bool bf3 = split != nullptr && !ae;
+  const bool bf3 = split != nullptr && !ae && dim <= COARSE_BF3_MAX_DIM;
   const bool lds = !(ae && atoi(ae) == 0);
   if (bf3) c_err += metric == L2 ? 3.0 * dim + 400.0 : 6.0 * dim + 800.0;
   const dim3 gl((unsigned)((nlist + 63) / 64), (unsigned)((nq + 63) / 64));

@@ -1900,7 +1900,7 @@ struct Coarse {
       HIPCHK(hipStreamSynchronize(st));
     }
     // the bf16 hi / lo split of the centroids for the matrix-core approximate scores (coarse.hip)
-    if (dim % 16 == 0 && dim <= 1024 && k >= 1) {
+    if (dim % 16 == 0 && dim <= coarse_bf3_max_dim() && k >= 1) {
       split.ensure(coarse_split_bytes(k, dim));
       launch_coarse_split(rm.as<float>(), k, dim, split.p, st);
     } else {

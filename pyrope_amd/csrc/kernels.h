@@ -310,6 +310,7 @@ void launch_coarse_mfma(const float *q, const float *cents_rm, const float *c2, 
                         int32_t *fail, int32_t *nfail, int32_t *probes, hipStream_t st,
                         const WordFill *zero = nullptr, const void *split = nullptr);
 size_t coarse_split_bytes(int nlist, int dim);
+int coarse_bf3_max_dim();  // the split kernel's dimension limit (larger: the fp32 kernels)
 void launch_coarse_split(const float *cents_rm, int nlist, int dim, void *split, hipStream_t st);
 
 // ---- 8-bit search mode of the FLAT index (sq8.hip; BruteForceVectorIndex EnableQuantization) ----

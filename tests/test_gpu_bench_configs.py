@@ -178,7 +178,7 @@ def test_mfma_coarse_ranking_ties_and_duplicate_centroids(hiplib):
 
 
 @pytest.mark.parametrize("metric", [0, 1])
-@pytest.mark.parametrize("dim", [32, 64, 768])
+@pytest.mark.parametrize("dim", [32, 64, 256])
 def test_bf16_split_coarse_ranking_wide_magnitudes(hiplib, metric, dim):
     """The bf16 hi / lo split approximate scores (coarse.hip coarse_approx_bf3_kernel, the default when the
     dimension is a multiple of 16) against the dense exact ranking and the fp32 MFMA kernel
