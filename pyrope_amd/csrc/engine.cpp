@@ -3666,7 +3666,8 @@ struct IvfPqIndex : Index {
     const int probes = (built && coarse.nlist > 0) ? std::max(0, std::min(nprobe, coarse.nlist)) : 0;
     // the matrix-core scan: built lists only (no buffer rows), the P1 geometry (pq32_supported)
     const char *pm = knob("PYR_PQ_MFMA");  // 0: the LUT scan below (A/B and the re-run path)
-    if (!(pm && atoi(pm) == 0) && pq32_ready && probes > 0 && filter_enabled() && pq32_supported(dim, M, ksub, k)) {
+    if (!(pm && atoi(pm) == 0) && pq32_ready && probes > 0 && filter_enabled() && pq32_supported(dim, M, ksub, k) &&
+        pq32_depth(k, ws) > 0) {
       if (buf.live_count() == 0) {
         search_pq32(d_q, nq, k, probes, d_s, d_l, d_c, ws);
         return;
@@ -3734,10 +3735,19 @@ struct IvfPqIndex : Index {
   // IvfPqVectorIndex.Search (:118-212) on the matrix cores (pq32.hip): coarse ranking, per (list chunk,
   // <= 64 queries) item the decoded rows' approximate ADC bounds -> rows reaching the query's sampled
   // threshold -> the reference's ADC sum of the best 64, certified; what fails re-runs on the LUT scan.
+  // the refine depth K1 of the matrix-core scan: filter_k1 (k <= 60), else the deep refine's 128 / 256 / 512
+  // (deep_k1; not for caller-ranked probe lists, as the IVF_FLAT stream's); 0: the LUT scan
+  static int pq32_depth(int k, const Workspace &ws) {
+    const int k1 = filter_k1(k);
+    if (k1 > 0) return k1;
+    return !ws.ext_probes && deep_refine_on() ? deep_k1(k) : 0;
+  }
+
   void search_pq32(const float *d_q, int64_t nq, int k, int probes, float *d_s, int64_t *d_l, int32_t *d_c,
                    Workspace &ws) {
-    const int k1 = filter_k1(k);
-    const int cap = stream_cap();
+    const int k1 = pq32_depth(k, ws);
+    if (k1 <= 0) throw Error(PYR_E_STATE, "pq32: no refine depth for this k");
+    const int cap = k1 > STREAM_KO ? deep_cap(k1) : stream_cap();
     IvfChunking ch{(int32_t)stream_chunk(), 1, 0};
     // a list's items on one XCD (pq32.hip: its code chunks leave HBM once per L2); PYR_PQ_XCD=0: one queue (A/B)
     ch.xcd = knob("PYR_PQ_XCD") && atoi(knob("PYR_PQ_XCD")) == 0 ? 0 : 1;
@@ -3839,17 +3849,18 @@ struct IvfPqIndex : Index {
       launch_pq32_scan(main_scan_args(sa), cb16.as<_Float16>(), M, maxi, false, ws.st);
     }
     note_stream_slice(ws, nq, cap);
-    ws.ms.ensure(sizeof(float) * nq * STREAM_KO);
-    ws.mk.ensure(sizeof(int32_t) * nq * STREAM_KO);
-    {
+    const bool deep = k1 > STREAM_KO;
+    CandMergeArgs m{};
+    m.cand = ws.scand.as<uint2>();
+    m.cand_n = ws.scn.as<int32_t>();
+    m.cand_f = ws.scf.as<uint32_t>();
+    m.thr = ws.sthr.as<float>();
+    m.nq = nq;
+    m.cap = cap;
+    if (!deep) {
       PhaseTimer t(PH_MERGE, ws.st);
-      CandMergeArgs m{};
-      m.cand = ws.scand.as<uint2>();
-      m.cand_n = ws.scn.as<int32_t>();
-      m.cand_f = ws.scf.as<uint32_t>();
-      m.thr = ws.sthr.as<float>();
-      m.nq = nq;
-      m.cap = cap;
+      ws.ms.ensure(sizeof(float) * nq * STREAM_KO);
+      ws.mk.ensure(sizeof(int32_t) * nq * STREAM_KO);
       m.out_s = ws.ms.as<float>();
       m.out_k = ws.mk.as<int32_t>();
       launch_cand_merge(m, ws.st);
@@ -3880,7 +3891,17 @@ struct IvfPqIndex : Index {
     r.out_l = d_l;
     r.out_c = d_c;
     int32_t nf = 0;
-    {
+    if (deep) {  // one pass at depth K1 over the emitted rows; what fails re-runs on the LUT scan
+      PhaseTimer t(PH_REFINE, ws.st, nq * k1);
+      r.k1 = k1;
+      r.fail_list = ws.fail.as<int32_t>();
+      r.fail_cnt = ws.fail_cnt.as<int32_t>();
+      HIPCHK(hipMemsetAsync(ws.fail_cnt.p, 0, sizeof(int32_t), ws.st));
+      launch_pq32_deep_refine(m, r, ws.st);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemcpyAsync(&nf, ws.fail_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, ws.st));
+      HIPCHK(hipStreamSynchronize(ws.st));
+    } else {
       PhaseTimer t(PH_REFINE, ws.st, nq * k1);
       r.k1 = k1;
       r.fail_list = ws.fail2.as<int32_t>();

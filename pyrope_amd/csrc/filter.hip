@@ -29,6 +29,7 @@ namespace pyr {
 namespace {
 
 #include "candmerge.h"
+#include "deeprank.h"
 
 __device__ __forceinline__ bool better(float s1, uint32_t k1, float s2, uint32_t k2) {
   return s1 > s2 || (s1 == s2 && k1 < k2);
@@ -560,201 +561,40 @@ __global__ __launch_bounds__(256) void merge_refine_kernel(CandMergeArgs m, Refi
   }
 }
 
-// k > 60: the stream scans' merge and certified refine at depth K1 = 128 / 256 / 512, one 256-thread block per
-// query.  The candidates are the K1 best emitted rows by rank key merged with K1 copies of the floor placeholder
-// max(T_q, floor) -- the rows above the floor first, then floors (every row left out scores at most the K1-th);
-// their exact scores come from 8-lane groups in the reference's order (as merge_refine_kernel's); the ranks by
-// better() (score desc, key asc), the top k written, and the certificate of refine_kernel's upper-bound branch.
-// A NaN score fails the query (the exact scan decides).  What fails is listed for the caller's exact scan.
-// Round 6: the K1 best rows are SELECTED, not sorted out of the whole emitted set -- an MSB-first
-// radix select over the 64-bit rank keys (8-bit digits, stopping at the first digit whose bin is taken whole),
-// then one compaction; the K1 exact scores are ranked by a bitonic sort of K1 (score, key) words instead of K1^2
-// pairwise counts.  (Round 5 sorted up to 8,192 emitted keys and counted 512 x 512 pairs per query: 8.9 of the
-// 13.4 ms of a k = 256 search at I1, profiles/r6_deepk.)
-constexpr int DEEP_MAX = 512;
+// k > 60: the stream scans' merge and certified refine at depth K1 = 128 / 256 / 512 (deeprank.h: the select of
+// the K1 best emitted rows, their exact scores in the reference's order, as merge_refine_kernel's, and their
+// ranks); the top k written, and the certificate of refine_kernel's upper-bound branch.
 template <int V, int MET, int DT>
 __global__ __launch_bounds__(256) void deep_refine_kernel(CandMergeArgs m, RefineArgs a) {
-  extern __shared__ uint64_t dk[];   // the emitted rows' rank keys (pack_cand), in buffer order
-  __shared__ uint64_t sk[DEEP_MAX];  // the exact (score, key) words being ranked
-  __shared__ float ex[DEEP_MAX];     // candidate c's exact score (c < j), its key
-  __shared__ uint32_t ky[DEEP_MAX];
-  __shared__ int hist[256];
-  __shared__ uint64_t sel_s, kmin_s;  // the select's key prefix; the smallest candidate key
-  __shared__ int need_s, done_s, above_s, nsel_s, nan_s;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  extern __shared__ uint64_t dk[];  // the emitted rows' rank keys (pack_cand), in buffer order
   const int64_t q = blockIdx.x;
-  const int d = a.k1, k = a.k, D = DT > 0 ? DT : a.dim;
-  const int tot = min(m.cand_n[q], m.cap);
-  const uint32_t fk = m.cand_f[q];
-  float F = m.thr ? m.thr[q] : -INFINITY;
-  if (fk != 0u) F = fmaxf(F, key_score(fk));
-  const uint64_t fkey = F > -INFINITY ? pack_cand(F, KEY_FLOOR) : 0ull;
-  if (tid == 0) {
-    above_s = 0;
-    nsel_s = 0;
-    nan_s = 0;
-    sel_s = 0ull;
-    kmin_s = ~0ull;
-    need_s = d;
-    done_s = 0;
-  }
-  __syncthreads();
-  // 1. the rows' rank keys into LDS; how many lie above the floor
-  const uint2 *cq = m.cand + (size_t)q * m.cap;
-  int above = 0;
-  for (int i = tid; i < tot; i += 256) {
-    const uint2 e = cq[i];
-    const uint64_t v = pack_cand(__uint_as_float(e.x), e.y);
-    dk[i] = v;
-    above += v > fkey ? 1 : 0;
-  }
-  if (above) atomicAdd(&above_s, above);
-  __syncthreads();
-  const int na = above_s;
-  // 2. the threshold T: the candidates are the rows with key >= T.  na < d: every row above the floor (the rest
-  // of the K1 are floor copies); else the d-th largest key (keys are distinct: the low word is ~storage key)
-  uint64_t T = fkey + 1ull;
-  if (na >= d) {
-    uint64_t mask = 0ull;
-#pragma unroll 1
-    for (int shift = 56; shift >= 0; shift -= 8) {
-      hist[tid] = 0;
-      __syncthreads();
-      const uint64_t pre = sel_s;
-      for (int i = tid; i < tot; i += 256) {
-        const uint64_t v = dk[i];
-        if ((v & mask) == pre) atomicAdd(&hist[(int)(v >> shift) & 255], 1);
-      }
-      __syncthreads();
-      if (w == 0) {  // the digit b whose bin holds the need-th largest: a suffix sum over bins 255 .. 0
-        const int need = need_s;
-        int c4[4], sum = 0;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          c4[u] = hist[255 - 4 * lane - u];
-          sum += c4[u];
-        }
-        int incl = sum;  // inclusive prefix over lanes (lane 0 = the highest bins)
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-          const int t = __shfl_up(incl, off);
-          if (lane >= off) incl += t;
-        }
-        const int excl = incl - sum;
-        const uint64_t hit = __builtin_amdgcn_ballot_w64(excl < need && incl >= need);
-        const int L = (int)__builtin_ctzll(hit);  // (one lane: the counts reach need exactly once)
-        if (lane == L) {
-          int before = excl, b = 0, cb = 0;
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-            if (before + c4[u] >= need) {
-              b = 255 - 4 * lane - u;
-              cb = c4[u];
-              break;
-            } else {
-              before += c4[u];
-            }
-          sel_s = pre | ((uint64_t)b << shift);
-          need_s = need - before;
-          done_s = cb == need - before;  // the whole bin is taken: every key with this prefix is a candidate
-        }
-      }
-      __syncthreads();
-      mask |= 0xFFull << shift;
-      if (done_s) break;  // (block-uniform)
-    }
-    T = sel_s;  // keys >= the prefix (its lower digits zero) are exactly the d largest
-  }
-  // 3. the candidates, compacted (order free: they are ranked below), and the smallest of their keys
-  uint64_t kmin = ~0ull;
-  for (int i = tid; i < tot; i += 256) {
-    const uint64_t v = dk[i];
-    if (v >= T && v > fkey) {
-      const int c = atomicAdd(&nsel_s, 1);
-      if (c < DEEP_MAX) ky[c] = ~(uint32_t)v;
-      kmin = v < kmin ? v : kmin;
-    }
-  }
-  if (kmin != ~0ull) atomicMin(reinterpret_cast<unsigned long long *>(&kmin_s), (unsigned long long)kmin);
-  __syncthreads();
-  const int j = min(nsel_s, d);  // real candidates (rows); the other d - j are floor copies
-  // the K1-th entry exists: rows (or the floor) were left out; every one of them scores at most its bound --
-  // the K1-th row (na >= K1: the rows left out rank below it, the floor too) or the floor
-  const bool excluded = na >= d || fkey != 0ull;
-  const float bound = na >= d ? key_score((uint32_t)(kmin_s >> 32)) : (fkey != 0ull ? F : -INFINITY);
-  // 4. exact scores: group g of the block's 32 takes candidates g, g + 32, ... (every lane of a group ends with it)
+  const int k = a.k, D = DT > 0 ? DT : a.dim;
   const float *qp = a.queries + (size_t)q * D;
-  const int g = tid >> 3, l = tid & 7;
-  for (int c = g; c < j; c += 32) {
-    const uint32_t kc = ky[c];
-    float sc;
+  const DeepRank R = deep_select_rank(m, q, a.k1, dk, [&](uint32_t kc, int l) {
     if (MET == L2 && a.cosine) {  // VectorMath.Cosine (:102-109) with the cached norms
       const float dot = a.rows_rm ? exact_score_l8<V, IP, DT, true>(qp, a.rows_rm, kc, D, l)
                                   : exact_score_l8<V, IP, DT, false>(qp, a.rows, kc, D, l);
       const float qn = a.qnorm[q], xn = a.rnorm[kc];
-      sc = (qn < 1e-6f || xn < 1e-6f) ? 0.0f : dot / (qn * xn);
-    } else {
-      sc = a.rows_rm ? exact_score_l8<V, MET, DT, true>(qp, a.rows_rm, kc, D, l)
+      return (qn < 1e-6f || xn < 1e-6f) ? 0.0f : dot / (qn * xn);
+    }
+    return a.rows_rm ? exact_score_l8<V, MET, DT, true>(qp, a.rows_rm, kc, D, l)
                      : exact_score_l8<V, MET, DT, false>(qp, a.rows, kc, D, l);
-    }
-    if (l == 0) {
-      ex[c] = sc;
-      if (isnan(sc)) nan_s = 1;
-    }
-  }
-  __syncthreads();
-  // 5. rank by better(): a descending bitonic sort of the (score, key) words (-0 as +0: better() ties them)
-  int P = 128;
-  while (P < d) P <<= 1;
-  for (int c = tid; c < P; c += 256) sk[c] = c < j ? pack_cand(ex[c] == 0.0f ? 0.0f : ex[c], ky[c]) : 0ull;
-  __syncthreads();
-  for (int sz = 2; sz <= P; sz <<= 1)
-    for (int jj = sz >> 1; jj >= 1; jj >>= 1) {
-      for (int i = tid; i < P; i += 256) {
-        const int o = i ^ jj;
-        if (o > i) {
-          const uint64_t x = sk[i], y = sk[o];
-          if ((i & sz) == 0 ? x < y : x > y) {
-            sk[i] = y;
-            sk[o] = x;
-          }
-        }
-      }
-      __syncthreads();
-    }
-  const int nout = min(j, k);
-  const float skth = nout == k ? key_score((uint32_t)(sk[k - 1] >> 32)) : -INFINITY;
+  });
+  const int nout = min(R.j, k);
+  const float skth = deep_kth(R, k);
   bool ok;
-  if (!excluded) {
+  if (!R.excluded) {
     ok = true;
   } else if (MET == L2 && a.cosine) {
     const double u = 5.9604644775390625e-8;  // 2^-24
     const float qn = a.qnorm[q];
-    ok = nout == k && (double)skth > 1.0 + 0.5 * (double)bound + (2.0 * D + 256.0) * u && qn >= 1e-6f &&
+    ok = nout == k && (double)skth > 1.0 + 0.5 * (double)R.bound + (2.0 * D + 256.0) * u && qn >= 1e-6f &&
          isfinite(qn) && !(a.max_rsq && a.max_rsq[1] != 0u) && !(a.zflag && *a.zflag != 0u && !(skth > 0.0f));
   } else {
-    ok = nout == k && skth > bound;
+    ok = nout == k && skth > R.bound;
   }
-  ok = ok && nan_s == 0;
-  for (int r = tid; r < k; r += 256) {
-    if (r < nout) {
-      const uint64_t v = sk[r];
-      const uint32_t kr = ~(uint32_t)v;
-      float sc = key_score((uint32_t)(v >> 32));
-      if (sc == 0.0f)  // the exact zero's own sign (the word holds +0 for both)
-        for (int c = 0; c < j; ++c)
-          if (ky[c] == kr) sc = ex[c];
-      a.out_s[(size_t)q * k + r] = sc;
-      a.out_l[(size_t)q * k + r] = a.row_labels ? a.row_labels[kr] : (int64_t)kr;
-    } else {
-      a.out_s[(size_t)q * k + r] = -INFINITY;
-      a.out_l[(size_t)q * k + r] = -1;
-    }
-  }
-  if (tid == 0) {
-    if (a.out_c) a.out_c[q] = nout;
-    if (!ok) a.fail_list[atomicAdd(a.fail_cnt, 1)] = (int32_t)q;
-  }
+  ok = ok && !R.nan;
+  deep_write(R, q, k, ok, a.row_labels, a.out_s, a.out_l, a.out_c, a.fail_list, a.fail_cnt);
 }
 
 __global__ void unit_rows_kernel(const float *x, const int64_t *slots, const float *norms, int64_t n, int D,

@@ -523,6 +523,9 @@ struct CandMergeArgs {
   float *out_s;               // [nq][STREAM_KO] desc; floor placeholders key -2, none -1
   int32_t *out_k;
 };
+// pq32.hip, k > 60: the merge + certified refine of the emitted rows at depth a.k1 (128 / 256 / 512), one
+// block per query
+void launch_pq32_deep_refine(const CandMergeArgs &m, const PqRefineArgs &a, hipStream_t st);
 int device_cus();                   // compute units of the current device (persistent-grid launches)
 // scan.hip: the one-wave-per-32-queries sample (query operands + sample values, any tile dimension) and
 // the 32x32x16 list scan; sample16.hip: sprep + the 8-wave sample of tile dims 32 / 64 / 128 (same

@@ -49,6 +49,8 @@ __device__ __forceinline__ size_t blk_off(int64_t r, int d, int D) {
   return ((size_t)(r >> 3) * (size_t)D + (size_t)d) * 8 + (size_t)(r & 7);
 }
 #include "vmath.h"
+#include "candmerge.h"
+#include "deeprank.h"
 
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 typedef uint32_t u2v __attribute__((ext_vector_type(2)));
@@ -558,6 +560,45 @@ __global__ __launch_bounds__(256) void pq_refine_kernel(PqRefineArgs a) {
   }
 }
 
+// k > 60 (round 6): the merge + certified refine at depth K1 = 128 / 256 / 512 on the emitted
+// rows (deeprank.h), one block per query.  A candidate's exact score is pq_refine_kernel's ADC sum: its 8-lane
+// group computes the terms m = 8 i + l in parallel and every lane adds them in m order (distSq += table[m][code],
+// IvfPqVectorIndex.cs:182-194), so the sum is bit-identical to the serial loop's.  Certified as refine_kernel's
+// upper-bound branch (the K1 best rows, or every emitted row above the floor); what fails re-runs on the LUT scan.
+__global__ __launch_bounds__(256) void pq_deep_refine_kernel(CandMergeArgs m, PqRefineArgs a) {
+  extern __shared__ uint64_t dk[];
+  const int64_t q = blockIdx.x;
+  const float *qv = a.queries + (size_t)q * a.dim;
+  const int base = threadIdx.x & 56, ds = a.dsub;
+  const DeepRank R = deep_select_rank(m, q, a.k1, dk, [&](uint32_t key, int l) {
+    int lo = 0, hi = a.nlist;  // the row's list: lb[lo] <= key < lb[lo + 1]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (a.lb[mid] <= (int32_t)key) lo = mid;
+      else hi = mid;
+    }
+    const float *cv = a.cents + (size_t)lo * a.dim;
+    const uint8_t *tp = a.cpack + (size_t)(key >> 5) * 64 * a.lw * 16;  // the row's tile
+    const int r = key & 31;
+    float dist = 0.0f;
+    for (int m0 = 0; m0 < a.M; m0 += 8) {
+      const int mm = m0 + l;
+      float t = 0.0f;
+      if (mm < a.M) {  // code mm in the code stream of lane (r, h) (pq_pack_kernel): its k-step's byte
+        const int h = ds == 8 ? (mm & 1) : ds == 4 ? ((mm >> 1) & 1) : 0;
+        const int b = ds == 8 ? mm >> 1 : ds == 16 ? mm : ds == 32 ? 2 * mm : 2 * (mm >> 2) + (mm & 1);
+        const int c = tp[(size_t)(32 * h + r) * a.lw * 16 + b];
+        t = em_l2sq_unsafe(Res{qv + mm * ds, cv + mm * ds}, Off{a.codebooks + ((size_t)mm * a.ksub + c) * ds}, ds);
+      }
+      const int nm = min(8, a.M - m0);
+      for (int u = 0; u < nm; ++u) dist = dist + __shfl(t, base + u);
+    }
+    return -dist;
+  });
+  const bool ok = (!R.excluded || (min(R.j, a.k) == a.k && deep_kth(R, a.k) > R.bound)) && !R.nan;
+  deep_write(R, q, a.k, ok, a.labels, a.out_s, a.out_l, a.out_c, a.fail_list, a.fail_cnt);
+}
+
 template <class K>
 void pq_launch(K kern, int grid, const StreamArgs &a, const _Float16 *cb16, int lw, hipStream_t st) {
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * PNW), 0, st, a, cb16, lw);
@@ -585,7 +626,7 @@ bool pq32_supported(int dim, int M, int ksub, int k) {
   if (M <= 0 || dim <= 0 || dim % 16 != 0 || dim % M != 0) return false;
   const int dsub = dim / M;
   return (dsub == 4 || dsub == 8 || dsub == 16 || dsub == 32) && dim / 16 <= PQ_KS_MAX && ksub >= 1 && ksub <= 256 &&
-         k >= 1 && k + 4 <= STREAM_KO;
+         k >= 1 && k <= 256;  // k > 60: the deep refine (the engine checks its depth)
 }
 int pq32_qmax(int dim, int M) { return pq_geo(dim, M).qmax; }
 int pq32_sample_values() { return PSV; }
@@ -624,6 +665,16 @@ void launch_pq32_scan(const StreamArgs &a, const _Float16 *cb16, int M, int max_
     case 32: launch_scan_dsub<32>(a, cb16, g, grid, sample, st); break;
     default: throw std::runtime_error("pq32: unsupported subspace size");
   }
+}
+void launch_pq32_deep_refine(const CandMergeArgs &m, const PqRefineArgs &a, hipStream_t st) {
+  if (a.nq <= 0) return;
+  if (a.k1 > DEEP_MAX || a.k1 < a.k || a.k > 256) throw std::invalid_argument("pq32 deep refine: depth");
+  constexpr int LDS_MAX = 144 * 1024;  // as launch_deep_refine's (filter.hip)
+  const size_t lds = deep_refine_lds_bytes(m.cap, a.k1);
+  if (lds > (size_t)LDS_MAX) throw std::invalid_argument("pq32 deep refine: candidate buffer too large");
+  static std::atomic<uint64_t> done{0};
+  allow_max_lds(reinterpret_cast<const void *>(&pq_deep_refine_kernel), done, LDS_MAX);
+  hipLaunchKernelGGL(pq_deep_refine_kernel, dim3((unsigned)a.nq), dim3(256), lds, st, m, a);
 }
 void launch_pq32_refine(const PqRefineArgs &a, int64_t nq, hipStream_t st) {
   if (nq <= 0) return;

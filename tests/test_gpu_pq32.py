@@ -188,3 +188,58 @@ def test_pq32_with_buffer_rows(hiplib, oracle, dim, m):
         exp = [new[k - oracle.BUFKEY] if k >= oracle.BUFKEY else labels[k] for k in ok]
         np.testing.assert_array_equal(got[1][i][: len(exp)], exp)
         assert np.array_equal(got[0][i][: len(os_)].view(np.uint32), os_.view(np.uint32))
+
+
+@pytest.mark.parametrize("dim,m", [(128, 4), (128, 16), (768, 96)])
+def test_pq32_large_k_deep_refine(hiplib, oracle, dim, m):
+    """k > 60: the matrix-core scan emits at depth K1 = 128 / 256 / 512 and the deep refine
+    (pq_deep_refine_kernel) selects, scores by the reference's ADC sum and certifies; what fails re-runs on
+    the LUT scan.  Equal to the LUT scan bit for bit at k = 61 .. 256 (as the certificates fall and with all
+    forced to fail), and to the oracle."""
+    from pyrope_amd import SearchOptions, generate_synthetic
+    n = 6000 if dim <= 256 else 3000
+    idx, _ = _build(dim, m, n, 12)
+    q = generate_synthetic(700, dim, 99)
+    opts = SearchOptions(nprobe=5)
+    cb, codes, off, labels, live = idx.pq_state()
+    cents = idx.centroids_array()
+    for k in (61, 100, 200, 256):
+        with _env(PYR_PQ_MFMA=0):
+            ref = idx.search_batch(q, k, opts)
+        got, ph = _profiled(hiplib, lambda: idx.search_batch(q, k, opts))
+        assert ph[PH_SAMPLE][0] > 0, "the pq32 path did not run"
+        assert ph[PH_FALLBACK][1] < len(q), "no query certified by the deep refine"
+        np.testing.assert_array_equal(got[2], ref[2])
+        _same(got, ref)
+        with _env(PYR_FILTER_CERR="1e15"):
+            forced, ph = _profiled(hiplib, lambda: idx.search_batch(q, k, opts))
+        assert ph[PH_FALLBACK][1] == len(q)
+        _same(forced, ref)
+        for i in range(0, len(q), 233):
+            os_, ok = oracle.ivfpq_search(q[i], k, cents, codes, off, cb, live, metric=0, nprobe=5)
+            np.testing.assert_array_equal(got[1][i][: len(ok)], labels[ok])
+            assert np.array_equal(got[0][i][: len(os_)].view(np.uint32), os_.view(np.uint32))
+    with _env(PYR_DEEP_REFINE=0):  # the A/B knob: k > 60 back on the LUT scan
+        off_run, ph = _profiled(hiplib, lambda: idx.search_batch(q, 100, opts))
+    assert ph[PH_SAMPLE][0] == 0
+    with _env(PYR_PQ_MFMA=0):
+        _same(off_run, idx.search_batch(q, 100, opts))
+
+
+def test_pq32_large_k_with_buffer_rows(hiplib):
+    """k > 60 with rows added after Build: the deep pq32 answer merged with the buffer's exact top k."""
+    from pyrope_amd import SearchOptions, generate_synthetic
+    n, dim, m = 5000, 128, 16
+    idx, x = _build(dim, m, n, 12)
+    extra = generate_synthetic(80, dim, 5)
+    extra[:5] = x[100:105]
+    idx.add_labels(np.arange(n, n + 80, dtype=np.int64), extra)
+    q = np.concatenate([generate_synthetic(300, dim, 7), x[100:103]])
+    opts = SearchOptions(nprobe=4)
+    for k in (100, 200):
+        with _env(PYR_PQ_MFMA=0):
+            ref = idx.search_batch(q, k, opts)
+        got, ph = _profiled(hiplib, lambda: idx.search_batch(q, k, opts))
+        assert ph[PH_SAMPLE][0] > 0
+        np.testing.assert_array_equal(got[2], ref[2])
+        _same(got, ref)
