@@ -929,13 +929,16 @@ static bool deep_refine_on() {
 }
 // the refine depth for k > 60 (deep_refine_kernel): 128 / 256 >= k + the margin, 0 past that or when the
 // candidate buffer's sort would not fit 60 KiB of LDS
-static int deep_k1(int k) {
+// IVF_PQ (pq = true): k within K1 / 2 -- its fp16 decode filter bounds the ADC sum more loosely than the IVF_FLAT
+// tiles bound the exact score (k = 100 at depth 128 failed ~5 % of the queries, profiles/r6_pqdeep)
+static int deep_k1(int k, bool pq = false) {
   int m = 4;
   if (const char *e = knob("PYR_FILTER_MARGIN")) m = std::max(0, atoi(e));
   // k within 0.8 K1: k = 200 at depth 256 failed 2,453 of 10,000 I1 queries, k = 252 at 256 nearly all
   // (profiles/r5_late/deepk_ab.log)
   for (int c : {128, 256, 512})
-    if (k + m <= c && 5 * k <= 4 * c) return deep_refine_lds_bytes(deep_cap(c), c) <= 144 * 1024 ? c : 0;
+    if (k + m <= c && (pq ? 2 * k <= c || c == 512 : 5 * k <= 4 * c))
+      return deep_refine_lds_bytes(deep_cap(c), c) <= 144 * 1024 ? c : 0;
   return 0;
 }
 
@@ -3740,7 +3743,7 @@ struct IvfPqIndex : Index {
   static int pq32_depth(int k, const Workspace &ws) {
     const int k1 = filter_k1(k);
     if (k1 > 0) return k1;
-    return !ws.ext_probes && deep_refine_on() ? deep_k1(k) : 0;
+    return !ws.ext_probes && deep_refine_on() ? deep_k1(k, true) : 0;
   }
 
   void search_pq32(const float *d_q, int64_t nq, int k, int probes, float *d_s, int64_t *d_l, int32_t *d_c,
@@ -3891,13 +3894,21 @@ struct IvfPqIndex : Index {
     r.out_l = d_l;
     r.out_c = d_c;
     int32_t nf = 0;
-    if (deep) {  // one pass at depth K1 over the emitted rows; what fails re-runs on the LUT scan
+    if (deep) {  // depth K1 over the emitted rows, the failures again at 2 K1 (<= 512); what fails re-runs on the LUT scan
       PhaseTimer t(PH_REFINE, ws.st, nq * k1);
+      const int k2 = std::min(2 * k1, 512);
       r.k1 = k1;
-      r.fail_list = ws.fail.as<int32_t>();
-      r.fail_cnt = ws.fail_cnt.as<int32_t>();
-      HIPCHK(hipMemsetAsync(ws.fail_cnt.p, 0, sizeof(int32_t), ws.st));
+      r.fail_list = k2 > k1 ? ws.fail2.as<int32_t>() : ws.fail.as<int32_t>();
+      r.fail_cnt = k2 > k1 ? ws.fail_cnt2.as<int32_t>() : ws.fail_cnt.as<int32_t>();
       launch_pq32_deep_refine(m, r, ws.st);
+      if (k2 > k1) {
+        r.k1 = k2;
+        r.qsel = ws.fail2.as<int32_t>();
+        r.nsel = ws.fail_cnt2.as<int32_t>();
+        r.fail_list = ws.fail.as<int32_t>();
+        r.fail_cnt = ws.fail_cnt.as<int32_t>();
+        launch_pq32_deep_refine(m, r, ws.st);
+      }
       HIPCHK(hipGetLastError());
       HIPCHK(hipMemcpyAsync(&nf, ws.fail_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, ws.st));
       HIPCHK(hipStreamSynchronize(ws.st));
@@ -3920,7 +3931,8 @@ struct IvfPqIndex : Index {
     if (knob("PYR_STREAM_DEBUG")) {
       int32_t n1 = 0;
       HIPCHK(hipMemcpy(&n1, ws.fail_cnt2.p, sizeof(int32_t), hipMemcpyDeviceToHost));
-      fprintf(stderr, "[pq32] nq %lld: certificate failures depth %d %d, depth 64 %d\n", (long long)nq, k1, n1, nf);
+      fprintf(stderr, "[pq32] nq %lld: certificate failures depth %d %d, depth %d %d\n", (long long)nq, k1, n1,
+              deep ? std::min(2 * k1, 512) : STREAM_KO, nf);
     }
     // what neither depth certifies: the LUT scan of those queries over the same probe lists (the slice's
     // ranking or the caller's, gathered by the fail list), same arithmetic

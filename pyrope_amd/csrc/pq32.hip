@@ -564,10 +564,13 @@ __global__ __launch_bounds__(256) void pq_refine_kernel(PqRefineArgs a) {
 // rows (deeprank.h), one block per query.  A candidate's exact score is pq_refine_kernel's ADC sum: its 8-lane
 // group computes the terms m = 8 i + l in parallel and every lane adds them in m order (distSq += table[m][code],
 // IvfPqVectorIndex.cs:182-194), so the sum is bit-identical to the serial loop's.  Certified as refine_kernel's
-// upper-bound branch (the K1 best rows, or every emitted row above the floor); what fails re-runs on the LUT scan.
+// upper-bound branch (the K1 best rows, or every emitted row above the floor); a.qsel / a.nsel: only the queries a
+// shallower pass failed (the grid is sized for all nq).  What fails re-runs on the LUT scan.
 __global__ __launch_bounds__(256) void pq_deep_refine_kernel(CandMergeArgs m, PqRefineArgs a) {
   extern __shared__ uint64_t dk[];
-  const int64_t q = blockIdx.x;
+  const int64_t nsel = a.nsel ? *a.nsel : a.nq;  // (a.qsel: the queries a shallower pass failed)
+  if ((int64_t)blockIdx.x >= nsel) return;
+  const int64_t q = a.qsel ? a.qsel[blockIdx.x] : (int64_t)blockIdx.x;
   const float *qv = a.queries + (size_t)q * a.dim;
   const int base = threadIdx.x & 56, ds = a.dsub;
   const DeepRank R = deep_select_rank(m, q, a.k1, dk, [&](uint32_t key, int l) {
