@@ -190,7 +190,8 @@ def test_pq32_with_buffer_rows(hiplib, oracle, dim, m):
         assert np.array_equal(got[0][i][: len(os_)].view(np.uint32), os_.view(np.uint32))
 
 
-@pytest.mark.parametrize("dim,m", [(128, 4), (128, 16), (768, 96)])
+# dsub 32 / 8 / 4 / 16, M = 12 (the 8-lane ADC groups' short last round) and P1's geometry
+@pytest.mark.parametrize("dim,m", [(128, 4), (128, 16), (128, 32), (256, 16), (96, 12), (768, 96)])
 def test_pq32_large_k_deep_refine(hiplib, oracle, dim, m):
     """k > 60: the matrix-core scan emits at depth K1 = 128 / 256 / 512 and the deep refine
     (pq_deep_refine_kernel) selects, scores by the reference's ADC sum and certifies; what fails re-runs on
