@@ -711,8 +711,8 @@ struct DeferredCounters {  // a deferred fill never outlives the search that set
   ~DeferredCounters() { ws.pz_set = false; }
 };
 
-// IVF-PQ LUT list scan kernel: 2 = pq_adc4 (default), 0 = the first-cut pq_scan (PYR_PQ_ADC=0; A/B
-// only, same results; also what k > 64 or an unsupported shape takes)
+// IVF-PQ LUT list scan kernel: 2 = pq_adc4 (default, k <= 256), 0 = the first-cut pq_scan (PYR_PQ_ADC=0; A/B
+// only, same results; also what a shape past pq_adc4's LDS takes: D > 2048 at k > 64, D > 4096)
 static int pq_adc_mode() {
   const char *e = knob("PYR_PQ_ADC");
   return e ? atoi(e) : 2;

@@ -1051,6 +1051,64 @@ __device__ __forceinline__ void wave_list_insert(bool cand, float sc, uint32_t k
   }
 }
 
+// k > 64: the same list in R registers per lane (entry i = 64 r + lane, i < k <= 64 R); an insertion at pos
+// shifts the entries past it up by one, across the registers (lane 63 of register r - 1 -> lane 0 of r)
+template <int R>
+__device__ __forceinline__ void wave_list_insert_r(bool cand, float sc, uint32_t key, float (&ls)[R],
+                                                   uint32_t (&lk)[R], float &kth, uint32_t &kthk, int k, int lane) {
+  if constexpr (R == 1) {
+    wave_list_insert(cand, sc, key, ls[0], lk[0], kth, kthk, k, lane);
+  } else {
+    const int kr = (k - 1) >> 6, kl = (k - 1) & 63;
+    uint64_t m = __ballot(cand);
+    while (m) {
+      const int j = __ffsll((unsigned long long)m) - 1;
+      const float s = __shfl(sc, j);
+      const uint32_t kk = __shfl(key, j);
+      int pos = 0;
+#pragma unroll
+      for (int r = 0; r < R; ++r) pos += __popcll(__ballot(64 * r + lane < k && better(ls[r], lk[r], s, kk)));
+      float us[R];
+      uint32_t uk[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        us[r] = __shfl_up(ls[r], 1);
+        uk[r] = __shfl_up(lk[r], 1);
+        if (r > 0) {
+          const float cs = __shfl(ls[r - 1], 63);
+          const uint32_t ck = __shfl(lk[r - 1], 63);
+          if (lane == 0) {
+            us[r] = cs;
+            uk[r] = ck;
+          }
+        }
+      }
+      float ts = 0.0f;
+      uint32_t tk = 0u;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int i = 64 * r + lane;
+        if (i > pos && i < k) {
+          ls[r] = us[r];
+          lk[r] = uk[r];
+        }
+        if (i == pos) {
+          ls[r] = s;
+          lk[r] = kk;
+        }
+        if (r == kr) {  // (no dynamic register index)
+          ts = ls[r];
+          tk = lk[r];
+        }
+      }
+      kth = __shfl(ts, kl);
+      kthk = __shfl(tk, kl);
+      m &= m - 1;
+      m &= __ballot(cand && better(sc, key, kth, kthk));
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // pq_adc4: four queries per pass over the rows.  The LUT entries of the 4 queries for one
 // (subspace, code) form one float4, so a single ds_read_b128 serves a row's lookup for all
@@ -1072,7 +1130,7 @@ struct CbRow {  // one codebook centroid held in registers
   __device__ float operator()(int i) const { return v[i]; }
 };
 
-template <int SUB, bool K256, int NT>
+template <int SUB, bool K256, int NT, int R>
 __global__ __launch_bounds__(NT) void pq_adc4_kernel(PqArgs a) {
   constexpr int PQ4_NT = NT, PQ4_NW = NT / 64, PQ4_G = PQ4_ROWS / NT;  // row groups per wave
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -1166,8 +1224,13 @@ __global__ __launch_bounds__(NT) void pq_adc4_kernel(PqArgs a) {
       const int qi = a.qlist[it.qbeg + qb + t] / a.nparts;
       const float gs = a.gthr ? key_score(__hip_atomic_load(a.gthr + qi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                               : -INFINITY;
-      float ls = -INFINITY, kth = -INFINITY;
-      uint32_t lk = KEY_NONE, kthk = KEY_NONE;
+      float ls[R], kth = -INFINITY;
+      uint32_t lk[R], kthk = KEY_NONE;
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        ls[u] = -INFINITY;
+        lk[u] = KEY_NONE;
+      }
 #pragma unroll
       for (int gi = 0; gi < PQ4_G; ++gi) {
         const int g = w + gi * PQ4_NW;
@@ -1176,31 +1239,40 @@ __global__ __launch_bounds__(NT) void pq_adc4_kernel(PqArgs a) {
           const bool valid = r < re && a.live[r];
           const float score = -acc[gi][t];  // :194
           const bool cand = valid && score >= gs && better(score, (uint32_t)r, kth, kthk);
-          wave_list_insert(cand, score, (uint32_t)r, ls, lk, kth, kthk, k, lane);
+          wave_list_insert_r<R>(cand, score, (uint32_t)r, ls, lk, kth, kthk, k, lane);
         }
       }
-      if (lane < k) {
-        mrs[(t * PQ4_NW + w) * k + lane] = ls;
-        mrk[(t * PQ4_NW + w) * k + lane] = lk;
-      }
+#pragma unroll
+      for (int u = 0; u < R; ++u)
+        if (64 * u + lane < k) {
+          mrs[(t * PQ4_NW + w) * k + 64 * u + lane] = ls[u];
+          mrk[(t * PQ4_NW + w) * k + 64 * u + lane] = lk[u];
+        }
     }
     __syncthreads();
     if (w < 4 && qb + w < it.qcnt) {
       const int slot = a.qlist[it.qbeg + qb + w] + it.part;
       const int qi = slot / a.nparts;
-      float ls = -INFINITY, kth = -INFINITY;
-      uint32_t lk = KEY_NONE, kthk = KEY_NONE;
+      float ls[R], kth = -INFINITY;
+      uint32_t lk[R], kthk = KEY_NONE;
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        ls[u] = -INFINITY;
+        lk[u] = KEY_NONE;
+      }
       for (int e0 = 0; e0 < PQ4_NW * k; e0 += 64) {
         const int e = e0 + lane;
         const float s = e < PQ4_NW * k ? mrs[w * PQ4_NW * k + e] : -INFINITY;
         const uint32_t kk = e < PQ4_NW * k ? mrk[w * PQ4_NW * k + e] : KEY_NONE;
         const bool cand = kk != KEY_NONE && better(s, kk, kth, kthk);
-        wave_list_insert(cand, s, kk, ls, lk, kth, kthk, k, lane);
+        wave_list_insert_r<R>(cand, s, kk, ls, lk, kth, kthk, k, lane);
       }
-      if (lane < k) {
-        a.part_s[(size_t)slot * k + lane] = ls;
-        a.part_k[(size_t)slot * k + lane] = lk;
-      }
+#pragma unroll
+      for (int u = 0; u < R; ++u)
+        if (64 * u + lane < k) {
+          a.part_s[(size_t)slot * k + 64 * u + lane] = ls[u];
+          a.part_k[(size_t)slot * k + 64 * u + lane] = lk[u];
+        }
       if (lane == 0 && a.gthr && kthk != KEY_NONE) atomicMax(a.gthr + qi, score_key(kth));
     }
     // waves 0-3 finish reading mrs / mrk before the barrier after the next quad's residuals
@@ -1839,27 +1911,33 @@ size_t pq_scan_lds_bytes(int dim, int M, int ksub, int k) {
   return (size_t)(((dim + 3) & ~3) + M * ksub + 2 * k + 2 * 256 + 4) * 4;
 }
 
+// k <= 64: 1024-thread blocks (measured 1.5x faster than 512), one list register; k <= 256: 512 threads (the
+// 8 waves' lists of k entries per query fit the LDS beside the LUT), four list registers
+constexpr int PQ4_DEEP_NT = 512, PQ4_KMAX = 256;
 size_t pq_adc4_lds_bytes(int dim, int ksub, int k) {  // sized for the largest block
-  return (size_t)(2 * PQ4_SC * ksub * 4 + 4 * dim + 2 * 4 * PQ4_MAX_NW * k) * 4;
+  const int nw = k > 64 ? PQ4_DEEP_NT / 64 : PQ4_MAX_NW;
+  return (size_t)(2 * PQ4_SC * ksub * 4 + 4 * dim + 2 * 4 * nw * k) * 4;
 }
 int pq_adc4_rows() { return PQ4_ROWS; }
 bool pq_adc4_supported(int dim, int M, int ksub, int k) {
-  return k >= 1 && k <= 64 && ksub <= 256 && M >= 1 && pq_adc4_lds_bytes(dim, ksub, k) <= 160 * 1024;
+  return k >= 1 && k <= PQ4_KMAX && ksub <= 256 && M >= 1 && pq_adc4_lds_bytes(dim, ksub, k) <= 160 * 1024;
 }
-template <int SUB, bool K256, int NT>
+template <int SUB, bool K256, int NT, int R>
 static void launch_pq_adc4_nt(const PqArgs &a, int max_items, hipStream_t st) {
   static std::atomic<uint64_t> attr{0};
-  allow_max_lds(reinterpret_cast<const void *>(&pq_adc4_kernel<SUB, K256, NT>), attr);
+  allow_max_lds(reinterpret_cast<const void *>(&pq_adc4_kernel<SUB, K256, NT, R>), attr);
   const int grid = (max_items + 7) / 8 * 8;
-  hipLaunchKernelGGL((pq_adc4_kernel<SUB, K256, NT>), dim3(grid), dim3(NT), pq_adc4_lds_bytes(a.dim, a.ksub, a.k), st,
-                     a);
+  hipLaunchKernelGGL((pq_adc4_kernel<SUB, K256, NT, R>), dim3(grid), dim3(NT), pq_adc4_lds_bytes(a.dim, a.ksub, a.k),
+                     st, a);
 }
 template <int SUB, bool K256>
 static void launch_pq_adc4_t(const PqArgs &a, int max_items, hipStream_t st) {
-  launch_pq_adc4_nt<SUB, K256, 1024>(a, max_items, st);  // 1024 threads measured 1.5x faster than 512
+  if (a.k <= 64) launch_pq_adc4_nt<SUB, K256, 1024, 1>(a, max_items, st);
+  else launch_pq_adc4_nt<SUB, K256, PQ4_DEEP_NT, PQ4_KMAX / 64>(a, max_items, st);
 }
 void launch_pq_adc4(const PqArgs &a, int max_items, hipStream_t st) {
   if (max_items <= 0) return;
+  if (!pq_adc4_supported(a.dim, a.M, a.ksub, a.k)) throw std::invalid_argument("pq_adc4: unsupported shape");
   const int sub = a.dim / a.M;
   const bool k256 = a.ksub == 256;
   if (sub == 8) {

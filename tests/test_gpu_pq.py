@@ -124,7 +124,7 @@ def _same(a, b):
                                           (48, 48, 16, 64), (64, 16, 256, 65), (768, 96, 256, 10)])
 def test_pq_adc_equals_first_kernel_and_oracle(hiplib, oracle, dim, m, ksub, k):
     """pq_adc (default) vs the first-cut pq_scan (PYR_PQ_ADC=0) vs the oracle: M not a multiple
-    of 16, ksub < 256, k = 1 / 64 / 65 (65 takes the first-cut kernel)."""
+    of 16, ksub < 256, k = 1 / 64 / 65."""
     from pyrope_amd import SearchOptions, generate_synthetic
     n = 6000 if dim < 768 else 3000
     idx, x = _build(dim, 0, n, 12, m, k=ksub)
@@ -203,3 +203,31 @@ def test_pq_build_with_given_quantizers_streams_identically(hiplib, oracle, metr
     assert np.array_equal(s1.view(np.uint32), s2.view(np.uint32))
     with pytest.raises(Exception):
         idx.set_codebooks(cb[:4])  # wrong subspace count
+
+
+@pytest.mark.parametrize("dim,m,ksub,k", [(64, 16, 256, 65), (128, 16, 256, 100), (96, 12, 256, 256),
+                                          (48, 48, 16, 200), (100, 10, 256, 128), (768, 96, 256, 150)])
+def test_pq_adc_large_k_equals_first_kernel_and_oracle(hiplib, oracle, dim, m, ksub, k):
+    """The LUT scan at 64 < k <= 256 (pq_adc4 with four list registers per lane, 512-thread blocks): the
+    matrix-core scan off (PYR_PQ_MFMA=0), so the LUT kernels answer; vs the first-cut pq_scan and the oracle.
+    dsub 4 / 8 / 1 / 10 (the last not on pq32 at all), ksub 16, M not a multiple of 8."""
+    from pyrope_amd import SearchOptions, generate_synthetic
+    n = 6000 if dim < 768 else 3000
+    idx, x = _build(dim, 0, n, 12, m, k=ksub)
+    q = generate_synthetic(70, dim, 99)
+    opts = SearchOptions(nprobe=5)
+    with _env(PYR_PQ_MFMA=0):
+        got = idx.search_batch(q, k, opts)
+        with _env(PYR_PQ_ADC=0):
+            ref = idx.search_batch(q, k, opts)
+        with _env(PYR_GTHR=0):
+            _same(idx.search_batch(q, k, opts), ref)
+    _same(got, ref)
+    np.testing.assert_array_equal(got[2], ref[2])
+    _same(idx.search_batch(q, k, opts), ref)  # the default path (pq32 + deep refine where it applies)
+    cb, codes, off, labels, live = idx.pq_state()
+    cents = idx.centroids_array()
+    for i in range(0, len(q), 23):
+        os_, ok = oracle.ivfpq_search(q[i], k, cents, codes, off, cb, live, metric=0, nprobe=5)
+        np.testing.assert_array_equal(got[1][i][: len(ok)], labels[ok])
+        assert np.array_equal(got[0][i][: len(ok)].view(np.uint32), os_.view(np.uint32))
